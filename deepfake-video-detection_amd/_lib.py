@@ -1,0 +1,97 @@
+"""ctypes binding of ``libdfd_hip.so`` (the C ABI declared in ``include/dfd_hip.h``).
+
+The library is built in-tree (``csrc/Makefile`` / ``__graft_entry__.build()``) and loaded
+AFTER torch, so it shares torch's HIP runtime (same ``libamdhip64.so.7`` soname) and
+therefore its streams and device allocations.  There is no fallback: if the library or a
+HIP device is missing, the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must be loaded first: provides the HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdfd_hip.so")
+
+_lock = threading.Lock()
+_lib = None
+
+c_i = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_f = ctypes.c_float
+c_d = ctypes.c_double
+c_p = ctypes.c_void_p
+c_fpp = ctypes.POINTER(ctypes.c_void_p)
+
+_SIGS = {
+    "dfd_last_error": (ctypes.c_char_p, []),
+    "dfd_version": (c_i, []),
+    "dfd_b0_tensor_count": (c_i, []),
+    "dfd_b0_tensor_info": (c_i, [c_i, ctypes.c_char_p, c_i, ctypes.POINTER(c_i), ctypes.POINTER(c_i),
+                                 ctypes.POINTER(c_i64)]),
+    "dfd_b0_plan_create": (c_i, [c_i, c_i, c_i, c_i, ctypes.POINTER(c_p)]),
+    "dfd_b0_plan_destroy": (None, [c_p]),
+    "dfd_b0_workspace_bytes": (c_i64, [c_p]),
+    "dfd_b0_bind": (c_i, [c_p, ctypes.POINTER(c_i64), c_i]),
+    "dfd_b0_forward": (c_i, [c_p, c_p, c_p, ctypes.POINTER(c_i64), c_p, c_p, c_p, c_p, c_i, c_f]),
+    "dfd_b0_backward": (c_i, [c_p, c_p, c_p, ctypes.POINTER(c_i64), c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i]),
+    "dfd_b0_segment_count": (c_i, []),
+    "dfd_b0_saved_tensor": (c_i, [c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    "dfd_b0_segment_tensors": (c_i, [c_i, ctypes.POINTER(c_i), ctypes.POINTER(c_i)]),
+    "dfd_head_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
+    "dfd_head_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_fpp, c_p, c_p, c_u64, c_f, c_p, c_p]),
+    "dfd_head_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_fpp, c_p, c_p, c_u64, c_f, c_p, c_p, c_p,
+                                c_p, c_fpp]),
+    "dfd_ce_forward": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i64, c_p, c_p]),
+    "dfd_ce_backward": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i64, c_p, c_p, c_p]),
+    "dfd_grad_norm": (c_i, [c_p, c_p, c_i64, c_f, c_p, c_p]),
+    "dfd_adam_step": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_i, c_d, c_i, c_p]),
+}
+
+EXPORTED = tuple(_SIGS.keys())
+
+
+class DFDError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes library with typed signatures."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise DFDError(f"{p} not found: build it with `make -C deepfake-video-detection_amd/csrc` "
+                           f"or __graft_entry__.build()")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise DFDError(load().dfd_last_error().decode(errors="replace"))
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_hip(t: torch.Tensor, what: str = "input") -> None:
+    if not t.is_cuda:
+        raise DFDError(f"{what} must be on a HIP device (got {t.device}); the MI355X path has no CPU fallback")

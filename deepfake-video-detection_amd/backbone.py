@@ -1,0 +1,291 @@
+"""EfficientNet-B0 trunk on MI355X: module tree with timm's names + the HIP plan runtime.
+
+Drop-in for the reference's ``self.backbone`` (``src/pretrained_detector.py:43-46``):
+``nn.Sequential(*list(timm.create_model('efficientnet_b0').children())[:-1])``, called as
+``self.backbone(x_flat)`` with ``x_flat (B*T, 3, H, W)`` and returning ``(B*T, 1280)``
+(``:116``).  The parameter/buffer names, shapes and order come from the native plan's
+tensor table (``dfd_b0_tensor_info``), so ``state_dict()`` keys are exactly timm's
+(``backbone.0.weight``, ``backbone.2.3.1.conv_dw.weight``, ...).
+
+The submodules are parameter holders only: the whole trunk -- stem, 16 MBConv blocks,
+conv_head, BN+SiLU, global pool -- runs as ONE native launch sequence
+(``dfd_b0_forward`` / ``dfd_b0_backward``).  There is no per-layer PyTorch path and no CPU
+fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .flat import FlatModule, GradSink
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+FEATURE_DIM = 1280
+DTYPES = {"fp32": 0, "float32": 0, torch.float32: 0, "bf16": 1, "bfloat16": 1, torch.bfloat16: 1}
+
+
+class _Holder(nn.Module):
+    """Container mirroring a timm submodule; holds parameters, never runs on its own."""
+
+    def forward(self, *args, **kwargs):
+        raise RuntimeError("EfficientNet-B0 submodules do not run standalone: the trunk executes as one "
+                           "native HIP plan (call the trunk / detector instead)")
+
+
+def tensor_table():
+    """[(name, kind, shape)] of the native trunk, timm state_dict order."""
+    lib = _lib.load()
+    out = []
+    buf = ctypes.create_string_buffer(256)
+    kind, nd = ctypes.c_int(), ctypes.c_int()
+    shp = (ctypes.c_int64 * 4)()
+    for i in range(lib.dfd_b0_tensor_count()):
+        _lib.check(lib.dfd_b0_tensor_info(i, buf, 256, ctypes.byref(kind), ctypes.byref(nd), shp))
+        out.append((buf.value.decode(), kind.value, tuple(shp[j] for j in range(nd.value))))
+    return out
+
+
+def _timm_init_(name: str, t: torch.Tensor) -> None:
+    """timm ``_init_weight_goog``-style init: conv N(0, sqrt(2/fan_out)), BN 1/0, biases 0."""
+    leaf = name.rsplit(".", 1)[-1]
+    with torch.no_grad():
+        if leaf == "weight" and t.dim() == 4:
+            k = t.shape[2] * t.shape[3]
+            groups = t.shape[0] if t.shape[1] == 1 and k > 1 else 1
+            fan_out = k * t.shape[0] // groups
+            t.normal_(0.0, math.sqrt(2.0 / fan_out))
+        elif leaf == "weight":
+            t.fill_(1.0)
+        elif leaf in ("bias", "running_mean"):
+            t.zero_()
+        elif leaf == "running_var":
+            t.fill_(1.0)
+
+
+class EfficientNetB0Trunk(FlatModule):
+    """The 6-child trunk Sequential (conv_stem, bn1, blocks, conv_head, bn2, global_pool).
+
+    Args:
+        compute_dtype: activation storage / MFMA dtype of the trunk: ``"bf16"`` (default,
+            fp32 accumulation, fp32 master weights and BN statistics) or ``"fp32"`` (exact
+            fp32 MFMA; the parity mode).
+    """
+
+    def __init__(self, compute_dtype="bf16"):
+        super().__init__()
+        self.compute_dtype = compute_dtype
+        self._table = tensor_table()
+        for name, kind, shape in self._table:
+            *path, leaf = name.split(".")
+            m = self
+            for q in path:
+                if q not in m._modules:
+                    m.add_module(q, _Holder())
+                m = m._modules[q]
+            if kind == 0:
+                p = nn.Parameter(torch.empty(shape))
+                _timm_init_(name, p)
+                m.register_parameter(leaf, p)
+            elif kind == 1:
+                b = torch.empty(shape)
+                _timm_init_(name, b)
+                m.register_buffer(leaf, b)
+            else:
+                m.register_buffer(leaf, torch.tensor(0, dtype=torch.long))
+        self.add_module("5", _Holder())  # global_pool (no parameters)
+        self._runtime = None
+        self._owner_ref = None
+        self._prefix = ""
+
+    # -- Sequential-like access (reference code indexes / iterates the trunk)
+    def __getitem__(self, i):
+        return list(self._modules.values())[i]
+
+    def __len__(self):
+        return len(self._modules)
+
+    def __iter__(self):
+        return iter(self._modules.values())
+
+    def _owner(self) -> FlatModule:
+        o = self._owner_ref() if self._owner_ref is not None else None
+        return o if o is not None else self
+
+    def attach(self, owner: FlatModule, prefix: str) -> None:
+        """Called by an owning FlatModule after it flattened (this trunk's tensors live in its buffers)."""
+        import weakref
+
+        self._flat_p = None  # storage now belongs to the owner
+        self._owner_ref = weakref.ref(owner)
+        self._prefix = prefix
+        self._bind()
+
+    def _on_flatten(self) -> None:
+        self._owner_ref = None
+        self._prefix = ""
+        self._bind()
+
+    def _bind(self) -> None:
+        owner = self._owner()
+        po, bo = owner.param_offsets(), owner.bn_offsets()
+        offs = []
+        for name, kind, _ in self._table:
+            full = self._prefix + name
+            offs.append(po[full] if kind == 0 else (bo[full] if kind == 1 else 0))
+        self._offsets = offs
+        if self._runtime is not None:
+            self._runtime.rebind(offs)
+        # gradient segments -> flat ranges (tensor index range -> parameter offsets)
+        lib = _lib.load()
+        numel = {n: math.prod(shape) for n, _, shape in self._table}
+        self._seg_ranges = []
+        lo, hi = ctypes.c_int(), ctypes.c_int()
+        for s in range(lib.dfd_b0_segment_count()):
+            _lib.check(lib.dfd_b0_segment_tensors(s, ctypes.byref(lo), ctypes.byref(hi)))
+            names = [n for n, k, _ in self._table[lo.value:hi.value] if k == 0]
+            if names:
+                a = po[self._prefix + names[0]]
+                b = po[self._prefix + names[-1]] + numel[names[-1]]
+                self._seg_ranges.append((a, b))
+            else:
+                self._seg_ranges.append((0, 0))
+        self._param_names = [self._prefix + n for n, k, _ in self._table if k == 0]
+
+    def runtime(self):
+        if self._runtime is None:
+            self._runtime = B0Runtime(self._offsets)
+        return self._runtime
+
+    def forward(self, x: torch.Tensor, grad_sink: GradSink | None = None) -> torch.Tensor:
+        owner = self._owner()
+        owner.ensure_flat()
+        _lib.require_hip(x, "frames")
+        if x.dim() != 4 or x.shape[1] != 3:
+            raise ValueError(f"expected (N, 3, H, W) frames, got {tuple(x.shape)}")
+        if x.dtype != torch.float32:
+            x = x.float()
+        if owner._flat_p.device != x.device:
+            raise RuntimeError(f"frames on {x.device} but weights on {owner._flat_p.device}")
+        training = self.training
+        if training:
+            with torch.no_grad():
+                owner._flat_c.add_(1)  # BatchNorm2d num_batches_tracked (all layers at once)
+        params = [p for n, p in owner._flat_params if n in self._param_name_set()]
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        if need_grad and x.requires_grad:
+            raise NotImplementedError("gradient w.r.t. the input frames is not provided by the HIP trunk")
+        dt = DTYPES[self.compute_dtype]
+        if not need_grad:
+            feats, _ = self.runtime().forward(x, owner, dt, training)
+            return feats
+        sink = grad_sink if grad_sink is not None else GradSink(owner)
+        return _TrunkFn.apply(x, self, sink, dt, training, *params)
+
+    def _param_name_set(self):
+        s = getattr(self, "_pns", None)
+        if s is None or len(s) != len(self._param_names):
+            s = set(self._param_names)
+            self._pns = s
+        return s
+
+
+class B0Runtime:
+    """Per-model plan cache: one native plan per (frames, H, W, dtype, device)."""
+
+    def __init__(self, offsets):
+        self.lib = _lib.load()
+        self.offsets = list(offsets)
+        self.plans: dict = {}
+
+    def rebind(self, offsets):
+        self.offsets = list(offsets)
+        arr = (ctypes.c_int64 * len(self.offsets))(*self.offsets)
+        for h in self.plans.values():
+            _lib.check(self.lib.dfd_b0_bind(h, arr, len(self.offsets)))
+
+    def plan(self, frames, H, W, dtype, device):
+        key = (frames, H, W, dtype, device.index)
+        h = self.plans.get(key)
+        if h is None:
+            h = ctypes.c_void_p()
+            with torch.cuda.device(device):
+                _lib.check(self.lib.dfd_b0_plan_create(frames, H, W, dtype, ctypes.byref(h)))
+                arr = (ctypes.c_int64 * len(self.offsets))(*self.offsets)
+                _lib.check(self.lib.dfd_b0_bind(h, arr, len(self.offsets)))
+            self.plans[key] = h
+        return h
+
+    def workspace_bytes(self, h) -> int:
+        return int(self.lib.dfd_b0_workspace_bytes(h))
+
+    def forward(self, x, owner, dtype, training):
+        N, _, H, W = x.shape
+        h = self.plan(N, H, W, dtype, x.device)
+        ws = torch.empty(self.workspace_bytes(h), dtype=torch.uint8, device=x.device)
+        feats = torch.empty(N, FEATURE_DIM, dtype=torch.float32, device=x.device)
+        xs = (ctypes.c_int64 * 4)(*x.stride())
+        _lib.check(self.lib.dfd_b0_forward(h, _lib.stream_of(x.device), x.data_ptr(), xs, owner._flat_p.data_ptr(),
+                                           owner._flat_b.data_ptr(), ws.data_ptr(), feats.data_ptr(),
+                                           1 if training else 0, BN_MOMENTUM))
+        return feats, (h, ws)
+
+    def backward(self, h, ws, x, dfeat, owner, grads, training, seg_begin, seg_end, accumulate=False):
+        xs = (ctypes.c_int64 * 4)(*x.stride())
+        _lib.check(self.lib.dfd_b0_backward(h, _lib.stream_of(x.device), x.data_ptr(), xs, dfeat.data_ptr(),
+                                            owner._flat_p.data_ptr(), ws.data_ptr(), grads.data_ptr(),
+                                            1 if training else 0, seg_begin, seg_end, 1 if accumulate else 0))
+
+    def __del__(self):
+        try:
+            for h in self.plans.values():
+                self.lib.dfd_b0_plan_destroy(h)
+        except Exception:
+            pass
+
+
+class _TrunkFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, trunk, sink, dtype, training, *params):
+        owner = trunk._owner()
+        feats, (h, ws) = trunk.runtime().forward(x, owner, dtype, training)
+        ctx.trunk, ctx.sink, ctx.h, ctx.ws, ctx.training = trunk, sink, h, ws, training
+        ctx.save_for_backward(x)
+        return feats
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        (x,) = ctx.saved_tensors
+        trunk = ctx.trunk
+        owner = trunk._owner()
+        grads = ctx.sink.get()
+        dfeat = dfeat.contiguous().float()
+        rt = trunk.runtime()
+        nseg = len(trunk._seg_ranges)
+        for s in range(nseg):
+            rt.backward(ctx.h, ctx.ws, x, dfeat, owner, grads, ctx.training, s, s + 1)
+            lo, hi = trunk._seg_ranges[s]
+            if hi > lo:
+                ctx.sink.ready(lo, hi)
+        ctx.ws = None
+        views = ctx.sink.views(trunk._param_names)
+        return (None, None, None, None, None, *views)
+
+
+class B0FrameExtractor(nn.Module):
+    """Frame feature extractor for the detector seam (``src/detector.py:88-100``):
+    ``(N, 3, 224, 224) -> (N, 1280)`` = trunk + global average pool."""
+
+    def __init__(self, trunk: EfficientNetB0Trunk | None = None, compute_dtype="bf16"):
+        super().__init__()
+        if trunk is None:
+            trunk = EfficientNetB0Trunk(compute_dtype)
+            trunk._flatten()
+        self.trunk = trunk
+
+    def forward(self, x):
+        return self.trunk(x)

@@ -1,0 +1,243 @@
+// extern "C" surface of libdfd_hip.so (declared in include/dfd_hip.h).
+#include "../../include/dfd_hip.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "head.h"
+#include "plan.h"
+
+namespace dfd {
+static thread_local std::string g_err;
+void set_error(const char* msg, const char* file, int line) {
+  char buf[512];
+  const char* base = strrchr(file, '/');
+  snprintf(buf, sizeof(buf), "%s (%s:%d)", msg, base ? base + 1 : file, line);
+  g_err = buf;
+}
+}  // namespace dfd
+
+struct dfd_b0_plan {
+  dfd::Plan p;
+};
+
+#define DFD_GUARD_BEGIN try {
+#define DFD_GUARD_END                                        \
+  }                                                          \
+  catch (const std::exception& e) {                          \
+    dfd::set_error(e.what(), __FILE__, __LINE__);            \
+    return -1;                                               \
+  }                                                          \
+  catch (...) {                                              \
+    dfd::set_error("unknown C++ exception", __FILE__, __LINE__); \
+    return -1;                                               \
+  }
+
+extern "C" {
+
+const char* dfd_last_error(void) { return dfd::g_err.c_str(); }
+int dfd_version(void) { return 100; }
+
+int dfd_b0_tensor_count(void) { return (int)dfd::b0_tensor_table().size(); }
+
+int dfd_b0_tensor_info(int idx, char* name, int cap, int* kind, int* ndim, int64_t* shape4) {
+  const auto& t = dfd::b0_tensor_table();
+  if (idx < 0 || idx >= (int)t.size()) { dfd::set_error("tensor index out of range", __FILE__, __LINE__); return -1; }
+  const auto& s = t[idx];
+  if (name && cap > 0) {
+    strncpy(name, s.name.c_str(), cap - 1);
+    name[cap - 1] = 0;
+  }
+  if (kind) *kind = s.kind;
+  if (ndim) *ndim = (int)s.shape.size();
+  if (shape4)
+    for (int i = 0; i < 4; ++i) shape4[i] = i < (int)s.shape.size() ? s.shape[i] : 1;
+  return 0;
+}
+
+int dfd_b0_plan_create(int frames, int height, int width, int dtype, dfd_b0_plan** out) {
+  DFD_GUARD_BEGIN
+  if (!out) { dfd::set_error("null out", __FILE__, __LINE__); return -1; }
+  auto* h = new (std::nothrow) dfd_b0_plan();
+  if (!h) { dfd::set_error("out of host memory", __FILE__, __LINE__); return -1; }
+  if (dfd::plan_build(h->p, frames, height, width, dtype) != 0) { delete h; return -1; }
+  *out = h;
+  return 0;
+  DFD_GUARD_END
+}
+
+void dfd_b0_plan_destroy(dfd_b0_plan* plan) {
+  if (!plan) return;
+  dfd::plan_free(plan->p);
+  delete plan;
+}
+
+int64_t dfd_b0_workspace_bytes(const dfd_b0_plan* plan) { return plan ? plan->p.ws_bytes : -1; }
+
+int dfd_b0_bind(dfd_b0_plan* plan, const int64_t* offsets, int n) {
+  DFD_GUARD_BEGIN
+  if (!plan || !offsets) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::plan_bind(plan->p, offsets, n);
+  DFD_GUARD_END
+}
+
+int dfd_b0_forward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* xs, const float* params,
+                   float* bn_buffers, void* workspace, float* features, int training, float momentum) {
+  DFD_GUARD_BEGIN
+  if (!plan || !x || !xs || !params || !bn_buffers || !workspace || !features) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::plan_forward(plan->p, (hipStream_t)stream, x, xs, params, bn_buffers, (char*)workspace, features,
+                           training, momentum);
+  DFD_GUARD_END
+}
+
+int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* xs, const float* dfeatures,
+                    const float* params, void* workspace, float* grads, int training, int seg_begin, int seg_end,
+                    int accumulate) {
+  DFD_GUARD_BEGIN
+  if (!plan || !x || !xs || !dfeatures || !params || !workspace || !grads) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::plan_backward_x(plan->p, (hipStream_t)stream, x, xs, dfeatures, params, (char*)workspace, grads,
+                              training, seg_begin, seg_end, accumulate);
+  DFD_GUARD_END
+}
+
+int dfd_b0_segment_count(void) { return dfd::kNumSegments; }
+
+int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* off, int64_t* rows, int64_t* cols) {
+  if (!plan || !off || !rows || !cols) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  const dfd::Plan& p = plan->p;
+  const int64_t F = p.frames;
+  struct E { int64_t o, r, c; };
+  std::vector<E> v;
+  v.push_back({p.o_ystem, F * p.H1 * p.W1, 32});
+  for (const auto& b : p.blocks) {
+    const int64_t Min = F * b.hin * b.win, Mout = F * b.hout * b.wout;
+    if (!b.ds) v.push_back({b.o_y1, Min, b.mid});
+    v.push_back({b.o_y2, Mout, b.mid});
+    v.push_back({b.o_y3, Mout, b.cout});
+    v.push_back({b.o_x, Mout, b.cout});
+  }
+  v.push_back({p.o_yh, F * p.Hf * p.Wf, 1280});
+  if (idx < 0 || idx >= (int)v.size()) { dfd::set_error("saved tensor index out of range", __FILE__, __LINE__); return -1; }
+  *off = v[idx].o; *rows = v[idx].r; *cols = v[idx].c;
+  return 0;
+}
+
+int dfd_b0_segment_tensors(int seg, int* lo, int* hi) {
+  if (seg < 0 || seg >= dfd::kNumSegments || !lo || !hi) {
+    dfd::set_error("bad segment", __FILE__, __LINE__);
+    return -1;
+  }
+  dfd::Plan dummy;
+  dfd::plan_segment_range(dummy, seg, lo, hi);
+  return 0;
+}
+
+// ---------------------------------------------------------------- head
+static void head_layout(int B, int T, int D, int H, int F1, int64_t* offs, int64_t* total) {
+  int64_t cur = 0;
+  auto take = [&](int64_t n) { const int64_t o = cur; cur += (n + 63) & ~int64_t(63); return o; };
+  offs[0] = take((int64_t)B * T * H);  // hid
+  offs[1] = take((int64_t)B * T);      // e
+  offs[2] = take((int64_t)B * D);      // g
+  offs[3] = take((int64_t)B * F1);     // h1
+  offs[4] = take((int64_t)B * F1);     // dh1
+  offs[5] = take((int64_t)B * D);      // dg
+  offs[6] = take((int64_t)B * T);      // dpe
+  offs[7] = take((int64_t)B * T * H);  // dhid
+  *total = cur;
+}
+
+static dfd::HeadWork head_work(float* w, int B, int T, int D, int H, int F1) {
+  int64_t o[8], tot;
+  head_layout(B, T, D, H, F1, o, &tot);
+  return dfd::HeadWork{w + o[0], w + o[1], w + o[2], w + o[3], w + o[4], w + o[5], w + o[6], w + o[7]};
+}
+
+int64_t dfd_head_work_floats(int B, int T, int D, int H, int F1) {
+  int64_t o[8], tot;
+  head_layout(B, T, D, H, F1, o, &tot);
+  return tot;
+}
+
+int dfd_head_forward(void* stream, int B, int T, int D, int H, int F1, int NC, int use_attn,
+                     const float* const* p8, const float* features, float* work, uint64_t seed, float p,
+                     float* logits, float* scores) {
+  DFD_GUARD_BEGIN
+  if (!p8 || !features || !work || !logits || !scores) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  dfd::HeadDims d{B, T, D, H, F1, NC, use_attn};
+  dfd::HeadParams P{p8[0], p8[1], p8[2], p8[3], p8[4], p8[5], p8[6], p8[7]};
+  dfd::HeadWork w = head_work(work, B, T, D, H, F1);
+  return dfd::head_forward((hipStream_t)stream, d, P, features, w, seed, p, logits, scores);
+  DFD_GUARD_END
+}
+
+int dfd_head_backward(void* stream, int B, int T, int D, int H, int F1, int NC, int use_attn,
+                      const float* const* p8, const float* features, float* work, uint64_t seed, float p,
+                      const float* scores, const float* dlogits, const float* dscores, float* dfeatures,
+                      float* const* g8) {
+  DFD_GUARD_BEGIN
+  if (!p8 || !g8 || !features || !work || !dlogits || !dfeatures) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  dfd::HeadDims d{B, T, D, H, F1, NC, use_attn};
+  dfd::HeadParams P{p8[0], p8[1], p8[2], p8[3], p8[4], p8[5], p8[6], p8[7]};
+  dfd::HeadParams G{g8[0], g8[1], g8[2], g8[3], g8[4], g8[5], g8[6], g8[7]};
+  dfd::HeadWork w = head_work(work, B, T, D, H, F1);
+  return dfd::head_backward((hipStream_t)stream, d, P, features, w, seed, p, scores, dlogits, dscores, dfeatures, G);
+  DFD_GUARD_END
+}
+
+int dfd_ce_forward(void* stream, const float* logits, const int64_t* labels, const float* weight, int B, int NC,
+                   int64_t ignore_index, float* loss, float* wsum) {
+  DFD_GUARD_BEGIN
+  return dfd::ce_forward((hipStream_t)stream, logits, labels, weight, B, NC, ignore_index, loss, wsum);
+  DFD_GUARD_END
+}
+
+int dfd_ce_backward(void* stream, const float* logits, const int64_t* labels, const float* weight, int B, int NC,
+                    int64_t ignore_index, const float* wsum, const float* grad_out, float* dlogits) {
+  DFD_GUARD_BEGIN
+  return dfd::ce_backward((hipStream_t)stream, logits, labels, weight, B, NC, ignore_index, wsum, grad_out, dlogits);
+  DFD_GUARD_END
+}
+
+int dfd_grad_norm(void* stream, const float* grads, int64_t n, float max_norm, void* scratch, float* out2) {
+  DFD_GUARD_BEGIN
+  return dfd::grad_norm((hipStream_t)stream, grads, n, max_norm, (double*)scratch, 1024, out2);
+  DFD_GUARD_END
+}
+
+int dfd_adam_step(void* stream, float* params, float* grads, float* m, float* v, int64_t n, double lr, double beta1,
+                  double beta2, double eps, double weight_decay, int step, double grad_scale, int decoupled,
+                  const float* clip_out2) {
+  DFD_GUARD_BEGIN
+  // scalars rounded exactly as torch.optim.{Adam,AdamW} (_single_tensor path) rounds them
+  dfd::AdamHyper h{};
+  h.omb1 = (float)(1.0 - beta1);
+  h.beta2 = (float)beta2;
+  h.omb2 = (float)(1.0 - beta2);
+  h.eps = (float)eps;
+  h.weight_decay = (float)weight_decay;
+  h.decay = (float)(1.0 - lr * weight_decay);
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  h.step_size = (float)(lr / bc1);
+  h.bc2_sqrt = (float)std::sqrt(bc2);
+  h.grad_scale = (float)grad_scale;
+  h.decoupled = decoupled;
+  return dfd::adam_step((hipStream_t)stream, params, grads, m, v, n, h, clip_out2);
+  DFD_GUARD_END
+}
+
+}  // extern "C"

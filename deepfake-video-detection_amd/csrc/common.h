@@ -1,0 +1,136 @@
+// Shared device helpers for the gfx950 (MI355X) kernels of the EfficientNet-B0 hot path.
+//
+// Storage types: `float` (fp32 parity mode) and `bf16` (raw 16-bit brain-float, the
+// performance mode).  All arithmetic accumulates in fp32.  Activations are NHWC
+// ("[M][C]", M = frames*H*W rows, C contiguous), every channel count on the path is a
+// multiple of 8, so the unit of every global access is an 8-element vector
+// (16 B for bf16, 2 x 16 B for fp32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dfd {
+
+struct bf16 {
+  uint16_t x;
+};
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even; NaN stays NaN (quiet bit forced)
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T> struct Tr;
+template <> struct Tr<float> {
+  static constexpr int kDtype = 0;
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
+  __device__ __forceinline__ static float round(float v) { return v; }
+};
+template <> struct Tr<bf16> {
+  static constexpr int kDtype = 1;
+  __device__ __forceinline__ static float to_f(bf16 v) { return bf2f(v.x); }
+  __device__ __forceinline__ static bf16 from_f(float v) { return bf16{f2bf(v)}; }
+  __device__ __forceinline__ static float round(float v) { return bf2f(f2bf(v)); }
+};
+
+// ---- 8-element vector load/store (p must be 16-B aligned for bf16, 32-B for fp32) ----
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void ld8(const bf16* p, float (&v)[8]) {
+  const uint4 a = *reinterpret_cast<const uint4*>(p);
+  v[0] = __uint_as_float(a.x << 16); v[1] = __uint_as_float(a.x & 0xffff0000u);
+  v[2] = __uint_as_float(a.y << 16); v[3] = __uint_as_float(a.y & 0xffff0000u);
+  v[4] = __uint_as_float(a.z << 16); v[5] = __uint_as_float(a.z & 0xffff0000u);
+  v[6] = __uint_as_float(a.w << 16); v[7] = __uint_as_float(a.w & 0xffff0000u);
+}
+__device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+__device__ __forceinline__ void st8(bf16* p, const float (&v)[8]) {
+  uint4 a;
+  a.x = pack2bf(v[0], v[1]); a.y = pack2bf(v[2], v[3]);
+  a.z = pack2bf(v[4], v[5]); a.w = pack2bf(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = a;
+}
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) { ld8(p, v); }
+
+// ---- activations ----
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
+// d/dx silu(x) = s (1 + x (1 - s))
+__device__ __forceinline__ float dsiluf_(float x) {
+  const float s = sigmoidf_(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// ---- wave reductions (wave64) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ __forceinline__ int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Activation-prologue modes for kernels that consume a pre-BN tensor Y:
+//   PRO_NONE      a = y
+//   PRO_BN_SILU   a = silu(y*scale[c] + shift[c])
+//   PRO_BN_SILU_G a = silu(y*scale[c] + shift[c]) * gate[frame][c]
+enum ProMode { PRO_NONE = 0, PRO_BN_SILU = 1, PRO_BN_SILU_G = 2 };
+
+struct Pro {
+  const float* scale;  // [C]
+  const float* shift;  // [C]
+  const float* gate;   // [frames][C]
+  int rows_per_frame;  // H*W of the consumed tensor
+  int C;
+};
+
+template <int MODE>
+__device__ __forceinline__ void apply_pro8(const Pro& pr, int64_t row, int c0, float (&v)[8]) {
+  if constexpr (MODE == PRO_NONE) {
+    return;
+  } else {
+    float sc[8], sh[8];
+    ld8f(pr.scale + c0, sc);
+    ld8f(pr.shift + c0, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = siluf_(v[j] * sc[j] + sh[j]);
+    if constexpr (MODE == PRO_BN_SILU_G) {
+      const int64_t f = row / pr.rows_per_frame;
+      float g[8];
+      ld8f(pr.gate + f * pr.C + c0, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= g[j];
+    }
+  }
+}
+
+}  // namespace dfd
+
+#define DFD_HIP_CHECK(expr)                                                     \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      dfd::set_error(hipGetErrorString(_e), __FILE__, __LINE__);                \
+      return -1;                                                                \
+    }                                                                           \
+  } while (0)
+
+namespace dfd {
+void set_error(const char* msg, const char* file, int line);
+}

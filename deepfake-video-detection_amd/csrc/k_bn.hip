@@ -1,0 +1,546 @@
+// BatchNorm (training batch statistics / eval running statistics), SiLU, squeeze-excite and
+// global-average-pool kernels for the EfficientNet-B0 hot path on gfx950.
+//
+// Replaces aten batch_norm + silu (timm BatchNormAct2d), the SE module (mean(2,3), two
+// biased 1x1 convs, silu, sigmoid, mul) and adaptive_avg_pool2d+flatten reached from
+// src/pretrained_detector.py:116, forward and backward.  Every BN statistic is a
+// deterministic two-level reduction: producers write per-workgroup partial rows
+// [rows][2][C] and bn_finalize sums them in a fixed order (fp64) -- no float atomics in HBM.
+#include "kernels.h"
+
+namespace dfd {
+
+// ------------------------------------------------------------------ partial-row reduction
+// Sums rows of a [rows][2][C] slab for channels [blockIdx.x*64, +64) in fp64.
+__device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int C, double& s, double& q,
+                                 double* sh_s, double* sh_q) {
+  const int tid = threadIdx.x, cl = tid & 63, part = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int r = part; r < rows; r += 4) {
+      a += stats[((int64_t)r * 2 + 0) * C + c];
+      b += stats[((int64_t)r * 2 + 1) * C + c];
+    }
+  }
+  sh_s[tid] = a;
+  sh_q[tid] = b;
+  __syncthreads();
+  if (tid < 64) {
+    s = sh_s[tid] + sh_s[tid + 64] + sh_s[tid + 128] + sh_s[tid + 192];
+    q = sh_q[tid] + sh_q[tid + 64] + sh_q[tid + 128] + sh_q[tid + 192];
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
+                                                          int C, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* run_mean,
+                                                          float* run_var, float momentum, float eps, int training,
+                                                          float* mean, float* invstd, float* scale, float* shift) {
+  __shared__ double sh_s[256], sh_q[256];
+  double s = 0.0, q = 0.0;
+  if (training) reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x * 64 + tid;
+  if (tid < 64 && c < C) {
+    float mu, is;
+    if (training) {
+      const double m = s / (double)count;
+      double var = q / (double)count - m * m;
+      if (var < 0.0) var = 0.0;
+      mu = (float)m;
+      is = (float)(1.0 / sqrt(var + (double)eps));
+      if (run_mean) {
+        const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
+        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+      }
+    } else {
+      mu = run_mean[c];
+      is = 1.0f / sqrtf(run_var[c] + eps);
+    }
+    const float sc = gamma[c] * is;
+    mean[c] = mu;
+    invstd[c] = is;
+    scale[c] = sc;
+    shift[c] = beta[c] - mu * sc;
+  }
+}
+
+int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
+                       const float* beta, float* run_mean, float* run_var, float momentum, float eps, bool training,
+                       float* mean, float* invstd, float* scale, float* shift) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, stats, rows, count, C, gamma, beta,
+                     run_mean, run_var, momentum, eps, training ? 1 : 0, mean, invstd, scale, shift);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ BN apply (+ residual)
+template <typename T, bool RES>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ Y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const T* __restrict__ R,
+                                                       T* __restrict__ X, int64_t nvec, int cv) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % cv) * 8;
+    float y[8], sc[8], sh[8];
+    ld8(Y + i * 8, y);
+    ld8f(scale + c, sc);
+    ld8f(shift + c, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = y[j] * sc[j] + sh[j];
+    if constexpr (RES) {
+      float r[8];
+      ld8(R + i * 8, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] += r[j];
+    }
+    st8(X + i * 8, y);
+  }
+}
+
+static int ew_grid(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(nvec, 256), 4096)); }
+
+template <typename T>
+int launch_bn_apply(hipStream_t s, const T* Y, const float* scale, const float* shift, const T* R, T* X, int64_t M,
+                    int C) {
+  const int64_t nvec = M * C / 8;
+  if (R)
+    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(ew_grid(nvec)), dim3(256), 0, s, Y, scale, shift, R, X, nvec, C / 8);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(ew_grid(nvec)), dim3(256), 0, s, Y, scale, shift, R, X, nvec, C / 8);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ BN backward
+// g = dA * act'(z),  z = y*scale + shift,  dA = dZ*gate + bc*bc_scale
+template <typename T>
+__device__ __forceinline__ void bn_bwd_g8(const BnBwdIn& in, const T* __restrict__ Y, int64_t row, int c, int C,
+                                          float (&g)[8], float (&y)[8]) {
+  ld8(Y + row * C + c, y);
+  float da[8];
+  if (in.dZ) {
+    ld8(reinterpret_cast<const T*>(in.dZ) + row * C + c, da);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) da[j] = 0.f;
+  }
+  if (in.gate || in.bc) {
+    const int64_t f = row / in.rows_per_frame;
+    if (in.gate) {
+      float gt[8];
+      ld8f(in.gate + f * C + c, gt);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) da[j] *= gt[j];
+    }
+    if (in.bc) {
+      float b[8];
+      ld8f(in.bc + f * C + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) da[j] += b[j] * in.bc_scale;
+    }
+  }
+  if (in.silu) {
+    float sc[8], sh[8];
+    ld8f(in.scale + c, sc);
+    ld8f(in.shift + c, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = da[j] * dsiluf_(y[j] * sc[j] + sh[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = da[j];
+  }
+}
+
+// grid (gx, cdiv(C/8, VPG)); threads: vec = tid % vpg, rl = tid / vpg
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdIn in, const T* __restrict__ Y, int64_t M, int C,
+                                                            float* __restrict__ stats, int vpg) {
+  __shared__ float sh[2][256][8];
+  const int tid = threadIdx.x;
+  const int vec = tid % vpg, rl = tid / vpg, nrl = 256 / vpg;
+  const int c = (blockIdx.y * vpg + vec) * 8;
+  float as[8], aq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { as[j] = 0.f; aq[j] = 0.f; }
+  if (rl < nrl && c < C) {
+    float mu[8], is[8];
+    ld8f(in.mean + c, mu);
+    ld8f(in.invstd + c, is);
+    for (int64_t r = (int64_t)blockIdx.x * nrl + rl; r < M; r += (int64_t)gridDim.x * nrl) {
+      float g[8], y[8];
+      bn_bwd_g8<T>(in, Y, r, c, C, g, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        as[j] += g[j];
+        aq[j] += g[j] * (y[j] - mu[j]) * is[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sh[0][tid][j] = as[j]; sh[1][tid][j] = aq[j]; }
+  __syncthreads();
+  if (tid < vpg && c < C) {
+    for (int r = 1; r < nrl; ++r) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        as[j] += sh[0][r * vpg + tid][j];
+        aq[j] += sh[1][r * vpg + tid][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      stats[((int64_t)blockIdx.x * 2 + 0) * C + c + j] = as[j];
+      stats[((int64_t)blockIdx.x * 2 + 1) * C + c + j] = aq[j];
+    }
+  }
+}
+
+static void bn_vpg_groups(int C, int& vpg, int& groups) {
+  const int nv = C / 8;
+  vpg = nv < 16 ? nv : 16;
+  groups = cdiv(nv, vpg);
+}
+
+template <typename T>
+int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, float* stats, int* stat_rows) {
+  int vpg, groups;
+  bn_vpg_groups(C, vpg, groups);
+  const int nrl = 256 / vpg;
+  const int64_t rows_needed = cdiv64(M, nrl * 4);
+  const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(rows_needed, std::max(1, 1024 / groups)));
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3(gx, groups), dim3(256), 0, s, in, Y, M, C, stats, vpg);
+  DFD_HIP_CHECK(hipGetLastError());
+  *stat_rows = gx;
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
+                                                              int C, const float* __restrict__ gamma,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, int training,
+                                                              float* dgamma, float* dbeta, int accumulate,
+                                                              float* coef) {
+  __shared__ double sh_s[256], sh_q[256];
+  double s = 0.0, q = 0.0;
+  reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x * 64 + tid;
+  if (tid < 64 && c < C) {
+    const float db = (float)s, dg = (float)q;
+    if (accumulate) { dbeta[c] += db; dgamma[c] += dg; }
+    else { dbeta[c] = db; dgamma[c] = dg; }
+    const double gm = gamma[c], is = invstd[c];
+    const double k1 = gm * is;
+    double k2 = 0.0, k3 = 0.0;
+    if (training) {
+      const double n = (double)count;
+      k2 = -gm * is * is * q / n;
+      k3 = -gm * is * s / n + gm * is * is * (double)mean[c] * q / n;
+    }
+    coef[c] = (float)k1;
+    coef[C + c] = (float)k2;
+    coef[2 * C + c] = (float)k3;
+  }
+}
+
+int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
+                           const float* mean, const float* invstd, bool training, float* dgamma, float* dbeta,
+                           bool accumulate, float* coef) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, stats, rows, count, C, gamma, mean,
+                     invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdIn in, const T* __restrict__ Y,
+                                                           const float* __restrict__ coef, T* dY, int64_t nvec, int C) {
+  const int cv = C / 8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / cv;
+    const int c = (int)(i - row * cv) * 8;
+    float g[8], y[8], k1[8], k2[8], k3[8];
+    bn_bwd_g8<T>(in, Y, row, c, C, g, y);
+    ld8f(coef + c, k1);
+    ld8f(coef + C + c, k2);
+    ld8f(coef + 2 * C + c, k3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = k1[j] * g[j] + k2[j] * y[j] + k3[j];
+    st8(dY + i * 8, g);
+  }
+}
+
+template <typename T>
+int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const float* coef, T* dY, int64_t M, int C) {
+  const int64_t nvec = M * C / 8;
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, s, in, Y, coef, dY, nvec, C);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ per-frame channel sums
+// part[h][f][c] = sum over pixel chunk h of frame f of val(p, c), where
+//   SQUEEZE: val = silu(y*scale+shift);   SEBWD: val = dZ * silu(y*scale+shift)
+// grid (frames*hsplit, groups); threads: vec = tid % vpg, pl = tid / vpg
+template <typename T, bool SEBWD>
+__global__ __launch_bounds__(256) void frame_sum_kernel(const T* __restrict__ dZ, const T* __restrict__ Y, Pro pro,
+                                                        int frames, int HW, int C, int hsplit, int vpg,
+                                                        float* __restrict__ part) {
+  __shared__ float sh[256][8];
+  const int tid = threadIdx.x;
+  const int vec = tid % vpg, pl = tid / vpg, npl = 256 / vpg;
+  const int f = blockIdx.x / hsplit, h = blockIdx.x % hsplit;
+  const int c = (blockIdx.y * vpg + vec) * 8;
+  const int chunk = (HW + hsplit - 1) / hsplit;
+  const int p0 = h * chunk, p1 = min(HW, p0 + chunk);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (pl < npl && c < C) {
+    float sc[8], shf[8];
+    ld8f(pro.scale + c, sc);
+    ld8f(pro.shift + c, shf);
+    for (int p = p0 + pl; p < p1; p += npl) {
+      const int64_t row = (int64_t)f * HW + p;
+      float y[8];
+      ld8(Y + row * C + c, y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = siluf_(y[j] * sc[j] + shf[j]);
+      if constexpr (SEBWD) {
+        float d[8];
+        ld8(dZ + row * C + c, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] *= d[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += y[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sh[tid][j] = acc[j];
+  __syncthreads();
+  if (tid < vpg && c < C) {
+    for (int r = 1; r < npl; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += sh[r * vpg + tid][j];
+    float* o = part + ((int64_t)h * frames + f) * C + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = acc[j];
+  }
+}
+
+template <typename T, bool SEBWD>
+static int launch_frame_sum(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
+                            float* part, int64_t part_cap, int* hsplit_out) {
+  int vpg, groups;
+  bn_vpg_groups(C, vpg, groups);
+  const int npl = 256 / vpg;
+  int hsplit = 1;
+  while ((int64_t)frames * groups * hsplit < 1024 && HW / (hsplit * 2) >= npl * 2 &&
+         (int64_t)(hsplit * 2) * frames * C <= part_cap)
+    hsplit *= 2;
+  hipLaunchKernelGGL((frame_sum_kernel<T, SEBWD>), dim3(frames * hsplit, groups), dim3(256), 0, s, dZ, Y, pro, frames,
+                     HW, C, hsplit, vpg, part);
+  DFD_HIP_CHECK(hipGetLastError());
+  *hsplit_out = hsplit;
+  return 0;
+}
+
+// sum hsplit partials: out[f][c] = scale * sum_h part[h][f][c]
+__global__ void sum_parts_kernel(const float* __restrict__ part, int hsplit, int64_t n, float scale,
+                                 float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float a = 0.f;
+    for (int h = 0; h < hsplit; ++h) a += part[h * n + i];
+    out[i] = a * scale;
+  }
+}
+
+template <typename T>
+int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
+                      int64_t part_cap, float* sq) {
+  int hs;
+  if (launch_frame_sum<T, false>(s, nullptr, Y, pro, frames, HW, C, part, part_cap, &hs)) return -1;
+  const int64_t n = (int64_t)frames * C;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, part, hs, n, 1.0f / (float)HW, sq);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
+                         float* part, int64_t part_cap, float* dgate) {
+  int hs;
+  if (launch_frame_sum<T, true>(s, dZ, Y, pro, frames, HW, C, part, part_cap, &hs)) return -1;
+  const int64_t n = (int64_t)frames * C;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, part, hs, n, 1.0f, dgate);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat) {
+  // HW is tiny (7x7 at 224^2): one partial per frame, write means directly
+  int vpg, groups;
+  bn_vpg_groups(C, vpg, groups);
+  hipLaunchKernelGGL((frame_sum_kernel<T, false>), dim3(frames, groups), dim3(256), 0, s, (const T*)nullptr, Y, pro,
+                     frames, HW, C, 1, vpg, feat);
+  DFD_HIP_CHECK(hipGetLastError());
+  const int64_t n = (int64_t)frames * C;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, feat, 1, n, 1.0f / (float)HW, feat);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ SE excitation (per frame)
+// one workgroup per frame: rpre = Wr sq + br ; r = silu(rpre) ; gate = sigmoid(We r + be)
+__global__ __launch_bounds__(256) void se_fc_fwd_kernel(const float* __restrict__ sq, const float* __restrict__ wr,
+                                                        const float* __restrict__ br, const float* __restrict__ we,
+                                                        const float* __restrict__ be, int C, int rd,
+                                                        float* __restrict__ rpre, float* __restrict__ gate) {
+  extern __shared__ float sm[];
+  float* s_sq = sm;      // [C]
+  float* s_r = sm + C;   // [rd]
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int c = tid; c < C; c += 256) s_sq[c] = sq[(int64_t)f * C + c];
+  __syncthreads();
+  for (int j = wave; j < rd; j += 4) {
+    float a = 0.f;
+    for (int c = lane; c < C; c += 64) a += wr[(int64_t)j * C + c] * s_sq[c];
+    a = wave_sum(a);
+    if (lane == 0) {
+      a += br[j];
+      rpre[(int64_t)f * rd + j] = a;
+      s_r[j] = siluf_(a);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float a = be[c];
+    for (int j = 0; j < rd; ++j) a += we[(int64_t)c * rd + j] * s_r[j];
+    gate[(int64_t)f * C + c] = sigmoidf_(a);
+  }
+}
+
+int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
+                     const float* be, int frames, int C, int rd, float* rpre, float* gate) {
+  hipLaunchKernelGGL(se_fc_fwd_kernel, dim3(frames), dim3(256), (C + rd) * sizeof(float), s, sq, wr, br, we, be, C,
+                     rd, rpre, gate);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// per frame: de = dgate*g*(1-g) ; dz = (We^T de) * silu'(rpre) ; bc = (Wr^T dz) * inv_hw
+__global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* __restrict__ dgate, const float* __restrict__ gate,
+                                                        const float* __restrict__ rpre, const float* __restrict__ wr,
+                                                        const float* __restrict__ we, int C, int rd, float inv_hw,
+                                                        float* __restrict__ de_out, float* __restrict__ dz_out,
+                                                        float* __restrict__ bc_out) {
+  extern __shared__ float sm[];
+  float* s_de = sm;      // [C]
+  float* s_dz = sm + C;  // [rd]
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int c = tid; c < C; c += 256) {
+    const float g = gate[(int64_t)f * C + c];
+    const float d = dgate[(int64_t)f * C + c] * g * (1.f - g);
+    s_de[c] = d;
+    de_out[(int64_t)f * C + c] = d;
+  }
+  __syncthreads();
+  for (int j = wave; j < rd; j += 4) {
+    float a = 0.f;
+    for (int c = lane; c < C; c += 64) a += we[(int64_t)c * rd + j] * s_de[c];
+    a = wave_sum(a);
+    if (lane == 0) {
+      const float z = a * dsiluf_(rpre[(int64_t)f * rd + j]);
+      s_dz[j] = z;
+      dz_out[(int64_t)f * rd + j] = z;
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float a = 0.f;
+    for (int j = 0; j < rd; ++j) a += wr[(int64_t)j * C + c] * s_dz[j];
+    bc_out[(int64_t)f * C + c] = a * inv_hw;
+  }
+}
+
+// weight grads: gwe[c][j] = sum_f de[f][c] * silu(rpre[f][j]); gbe[c] = sum_f de[f][c]
+//               gwr[j][c] = sum_f dz[f][j] * sq[f][c];          gbr[j] = sum_f dz[f][j]
+__global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ de, const float* __restrict__ dz,
+                                                       const float* __restrict__ sq, const float* __restrict__ rpre,
+                                                       int frames, int C, int rd, float* gwr, float* gbr, float* gwe,
+                                                       float* gbe, int accumulate) {
+  const int64_t n = (int64_t)C * rd;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    {  // gwe[c][j], i = c*rd + j
+      const int c = (int)(i / rd), j = (int)(i % rd);
+      float a = 0.f;
+      for (int f = 0; f < frames; ++f) a += de[(int64_t)f * C + c] * siluf_(rpre[(int64_t)f * rd + j]);
+      gwe[i] = accumulate ? gwe[i] + a : a;
+    }
+    {  // gwr[j][c], i = j*C + c
+      const int j = (int)(i / C), c = (int)(i % C);
+      float a = 0.f;
+      for (int f = 0; f < frames; ++f) a += dz[(int64_t)f * rd + j] * sq[(int64_t)f * C + c];
+      gwr[i] = accumulate ? gwr[i] + a : a;
+    }
+  }
+  if (i < C) {
+    float a = 0.f;
+    for (int f = 0; f < frames; ++f) a += de[(int64_t)f * C + i];
+    gbe[i] = accumulate ? gbe[i] + a : a;
+  }
+  if (i < rd) {
+    float a = 0.f;
+    for (int f = 0; f < frames; ++f) a += dz[(int64_t)f * rd + i];
+    gbr[i] = accumulate ? gbr[i] + a : a;
+  }
+}
+
+int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
+                     const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
+                     float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
+  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(frames), dim3(256), (C + rd) * sizeof(float), s, dgate, gate, rpre, wr,
+                     we, C, rd, inv_hw, tmp_de, tmp_dr, bc_out);
+  DFD_HIP_CHECK(hipGetLastError());
+  const int64_t n = (int64_t)C * rd;
+  hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv64(std::max<int64_t>(n, C), 256)), dim3(256), 0, s, tmp_de,
+                     tmp_dr, sq, rpre, frames, C, rd, gwr, gbr, gwe, gbe, accumulate ? 1 : 0);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ slab reduce
+__global__ void reduce_slabs_kernel(const float* __restrict__ slab, int splits, int64_t n, float* out,
+                                    int accumulate) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float a = 0.f;
+    for (int sp = 0; sp < splits; ++sp) a += slab[(int64_t)sp * n + i];
+    out[i] = accumulate ? out[i] + a : a;
+  }
+}
+
+int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate) {
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(ew_grid(n)), dim3(256), 0, s, slab, splits, n, out,
+                     accumulate ? 1 : 0);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+#define DFD_BN_INST(T)                                                                                               \
+  template int launch_bn_apply<T>(hipStream_t, const T*, const float*, const float*, const T*, T*, int64_t, int);    \
+  template int launch_bn_bwd_reduce<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, float*, int*);          \
+  template int launch_bn_bwd_apply<T>(hipStream_t, const BnBwdIn&, const T*, const float*, T*, int64_t, int);       \
+  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, float*);     \
+  template int launch_se_bwd_reduce<T>(hipStream_t, const T*, const T*, const Pro&, int, int, int, float*, int64_t, \
+                                       float*);                                                                     \
+  template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);
+DFD_BN_INST(float)
+DFD_BN_INST(bf16)
+#undef DFD_BN_INST
+
+}  // namespace dfd

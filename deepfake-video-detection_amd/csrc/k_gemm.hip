@@ -1,0 +1,383 @@
+// Pointwise (1x1) convolutions of EfficientNet-B0 as MFMA GEMMs on gfx950.
+//
+// Replaces aten conv2d(kernel 1x1) for timm's conv_pw / conv_pwl / conv_head
+// (reached from src/pretrained_detector.py:116) in all three passes:
+//   forward  Y[M][N]  = pro(X)[M][K] . W[N][K]^T   + per-column BN-stat partials (epilogue)
+//   dgrad    dX[M][K] = dY[M][N] . (W^T)[K][N]^T   (+ residual gradient in the epilogue)
+//   wgrad    dW[N][K] = dY^T . pro(X)              (split over M, deterministic slab reduce)
+// where pro() is the consumer-side BatchNorm+SiLU (+SE channel gate) of the producing
+// layer, applied while staging A into LDS, so those activations are never materialised.
+//
+// Layout: NHWC rows, K/N contiguous.  MFMA: v_mfma_f32_16x16x32_bf16 (bf16 mode) or
+// v_mfma_f32_16x16x4_f32 (exact fp32 parity mode); C/D layout col=lane&15,
+// row=4*(lane>>4)+r for both.
+#include "kernels.h"
+
+namespace dfd {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+constexpr int GBM = 128;  // rows per tile
+constexpr int GBN = 128;  // output columns per tile
+constexpr int GBK = 32;   // contraction per step
+
+template <typename T> struct GemmCfg {
+  static constexpr int AS = sizeof(T) == 2 ? GBK + 8 : GBK + 4;   // LDS row stride (elements) of A/B tiles
+  static constexpr int CS = sizeof(T) == 2 ? GBN + 8 : GBN + 4;   // LDS row stride of the C tile
+  static constexpr int AB_BYTES = 2 * GBM * AS * (int)sizeof(T);
+  static constexpr int C_BYTES = GBM * CS * (int)sizeof(T);
+  static constexpr int SMEM = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
+};
+
+template <typename T>
+__device__ __forceinline__ void lds_st8(T* p, const float (&v)[8]) { st8(p, v); }
+template <typename T>
+__device__ __forceinline__ void lds_ld8(const T* p, float (&v)[8]) { ld8(p, v); }
+
+template <typename T, int MODE, bool STATS, bool RESID>
+__global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                      T* __restrict__ C, const T* __restrict__ R, int64_t M,
+                                                      int N, int K, Pro pro, float* __restrict__ stats,
+                                                      int64_t tiles_m) {
+  using G = GemmCfg<T>;
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  __shared__ float st_sum[GBN];
+  __shared__ float st_sq[GBN];
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = As + GBM * G::AS;
+  T* Cs = reinterpret_cast<T*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.y * GBN;
+  const int nvalid = min(GBN, N - n0);
+  const int nb = (nvalid + 15) >> 4;
+  if constexpr (STATS) {
+    for (int i = tid; i < GBN; i += 256) { st_sum[i] = 0.f; st_sq[i] = 0.f; }
+  }
+
+  for (int64_t mt = blockIdx.x; mt < tiles_m; mt += gridDim.x) {
+    const int64_t m0 = mt * GBM;
+    f32x4_t acc[2][8];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    for (int k0 = 0; k0 < K; k0 += GBK) {
+      // ---- stage A (with the consumer-side BN/SiLU/gate prologue) and B ----
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int v = tid + 256 * i;
+        const int row = v >> 2, kc = (v & 3) * 8;
+        const int64_t gm = m0 + row;
+        const int gk = k0 + kc;
+        float x[8];
+        if (gm < M && gk < K) {
+          ld8(A + gm * K + gk, x);
+          apply_pro8<MODE>(pro, gm, gk, x);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = 0.f;
+        }
+        lds_st8(As + row * G::AS + kc, x);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int v = tid + 256 * i;
+        const int row = v >> 2, kc = (v & 3) * 8;
+        const int gk = k0 + kc;
+        float x[8];
+        if (row < nvalid && gk < K) {
+          ld8(B + (int64_t)(n0 + row) * K + gk, x);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = 0.f;
+        }
+        lds_st8(Bs + row * G::AS + kc, x);
+      }
+      __syncthreads();
+      // ---- MFMA ----
+      if constexpr (sizeof(T) == 2) {
+        bf16x8_t af[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+          af[rb] = *reinterpret_cast<const bf16x8_t*>(As + (wave * 32 + rb * 16 + (lane & 15)) * G::AS +
+                                                      8 * (lane >> 4));
+#pragma unroll
+        for (int cb = 0; cb < 8; ++cb) {
+          if (cb < nb) {
+            const bf16x8_t bfr =
+                *reinterpret_cast<const bf16x8_t*>(Bs + (cb * 16 + (lane & 15)) * G::AS + 8 * (lane >> 4));
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+              acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rb], bfr, acc[rb][cb], 0, 0, 0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < GBK / 4; ++s) {
+          const int kk = 4 * s + (lane >> 4);
+          const float a0 = reinterpret_cast<const float*>(As)[(wave * 32 + (lane & 15)) * G::AS + kk];
+          const float a1 = reinterpret_cast<const float*>(As)[(wave * 32 + 16 + (lane & 15)) * G::AS + kk];
+#pragma unroll
+          for (int cb = 0; cb < 8; ++cb) {
+            if (cb < nb) {
+              const float b = reinterpret_cast<const float*>(Bs)[(cb * 16 + (lane & 15)) * G::AS + kk];
+              acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][cb], 0, 0, 0);
+              acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][cb], 0, 0, 0);
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+
+    // ---- epilogue: round, BN-stat partials, stage C tile in LDS ----
+#pragma unroll
+    for (int cb = 0; cb < 8; ++cb) {
+      if (cb < nb) {
+        const int col = cb * 16 + (lane & 15);
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wave * 32 + rb * 16 + 4 * (lane >> 4) + r;
+            const float v = Tr<T>::round(acc[rb][cb][r]);
+            Cs[row * G::CS + col] = Tr<T>::from_f(v);
+            if constexpr (STATS) {
+              if (m0 + row < M) { s += v; q += v * v; }
+            }
+          }
+        }
+        if constexpr (STATS) {
+          s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+          q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+          if (lane < 16 && col < nvalid) {
+            atomicAdd(&st_sum[col], s);
+            atomicAdd(&st_sq[col], q);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    const int vpr = nvalid >> 3;
+    for (int v = tid; v < GBM * vpr; v += 256) {
+      const int row = v / vpr, cv = (v - row * vpr) * 8;
+      const int64_t gm = m0 + row;
+      if (gm >= M) continue;
+      float x[8];
+      lds_ld8(Cs + row * G::CS + cv, x);
+      if constexpr (RESID) {
+        float r8[8];
+        ld8(R + gm * N + n0 + cv, r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] += r8[j];
+      }
+      st8(C + gm * N + n0 + cv, x);
+    }
+    __syncthreads();
+  }
+  if constexpr (STATS) {
+    for (int i = tid; i < nvalid; i += 256) {
+      stats[((int64_t)blockIdx.x * 2 + 0) * N + n0 + i] = st_sum[i];
+      stats[((int64_t)blockIdx.x * 2 + 1) * N + n0 + i] = st_sq[i];
+    }
+  }
+}
+
+template <typename T>
+int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K, int pro_mode,
+                   const Pro& pro, float* stats, int* stat_rows) {
+  if (M <= 0) return 0;
+  if ((N & 7) || (K & 7)) { set_error("pw_gemm: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
+  const int ntn = cdiv(N, GBN);
+  const int64_t tiles_m = cdiv64(M, GBM);
+  const int64_t cap = std::max<int64_t>(1, 1024 / ntn);
+  const int gx = (int)std::min<int64_t>(tiles_m, cap);
+  dim3 grid(gx, ntn), block(256);
+  const bool st = stats != nullptr, rs = R != nullptr;
+#define DFD_GEMM_LAUNCH(MODE, ST, RS) \
+  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, RS>), grid, block, 0, s, A, B, C, R, M, N, K, pro, stats, tiles_m)
+  if (rs) {
+    if (pro_mode != PRO_NONE || st) { set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__); return -1; }
+    DFD_GEMM_LAUNCH(PRO_NONE, false, true);
+  } else if (pro_mode == PRO_NONE) {
+    if (st) DFD_GEMM_LAUNCH(PRO_NONE, true, false); else DFD_GEMM_LAUNCH(PRO_NONE, false, false);
+  } else if (pro_mode == PRO_BN_SILU) {
+    if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU, true, false); else DFD_GEMM_LAUNCH(PRO_BN_SILU, false, false);
+  } else {
+    if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU_G, true, false); else DFD_GEMM_LAUNCH(PRO_BN_SILU_G, false, false);
+  }
+#undef DFD_GEMM_LAUNCH
+  if (stat_rows) *stat_rows = gx;
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// wgrad: dW[N][K] = sum_m dY[m][n] * pro(X)[m][k].  Output tile 64x64 per workgroup; each of the
+// 4 waves streams its own 32-row m-steps through a private LDS region (no block barrier in the
+// loop) and the MFMA operands are COLUMN reads of the row-major tiles: ds_read_b64_tr_b16 in
+// bf16 mode (two per 8-deep fragment), ds_read_b32 in fp32 mode.
+constexpr int WT = 64;
+constexpr int WMS = 32;
+
+template <typename T> struct WgCfg {
+  static constexpr int LS = sizeof(T) == 2 ? WT + 8 : WT + 4;
+  static constexpr int WAVE_BYTES = 2 * WMS * LS * (int)sizeof(T);
+  static constexpr int SMEM = 4 * WAVE_BYTES > WT * WT * 4 ? 4 * WAVE_BYTES : WT * WT * 4;
+};
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
+                                                       int N, int K, Pro pro, float* __restrict__ slab, int tnk,
+                                                       int64_t m_per_split) {
+  using G = WgCfg<T>;
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tn = blockIdx.x / tnk, tk = blockIdx.x - tn * tnk;
+  const int n0 = tn * WT, k0 = tk * WT;
+  const int nv = min(WT, N - n0), kv = min(WT, K - k0);
+  const int nbn = (nv + 15) >> 4, nbk = (kv + 15) >> 4;
+  const int64_t mbeg = (int64_t)blockIdx.y * m_per_split;
+  const int64_t mend = min(M, mbeg + m_per_split);
+  T* Ys = reinterpret_cast<T*>(smem + wave * G::WAVE_BYTES);
+  T* Xs = Ys + WMS * G::LS;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int64_t ms = mbeg + wave * WMS; ms < mend; ms += 4 * WMS) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int slot = lane + 64 * i;
+      const int row = slot >> 3, cv = (slot & 7) * 8;
+      const int64_t gm = ms + row;
+      float y[8], x[8];
+      if (gm < mend && cv < nv) {
+        ld8(dY + gm * N + n0 + cv, y);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = 0.f;
+      }
+      if (gm < mend && cv < kv) {
+        ld8(X + gm * K + k0 + cv, x);
+        apply_pro8<MODE>(pro, gm, k0 + cv, x);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = 0.f;
+      }
+      lds_st8(Ys + row * G::LS + cv, y);
+      lds_st8(Xs + row * G::LS + cv, x);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if constexpr (sizeof(T) == 2) {
+      const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+      bf16x8_t bfr[4];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        if (kb < nbk) {
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(Xs + (8 * g + q) * G::LS + kb * 16 + 4 * p));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(Xs + (8 * g + 4 + q) * G::LS + kb * 16 + 4 * p));
+          bfr[kb] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+#pragma unroll
+      for (int nb_ = 0; nb_ < 4; ++nb_) {
+        if (nb_ < nbn) {
+          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(Ys + (8 * g + q) * G::LS + nb_ * 16 + 4 * p));
+          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_s16x4_t*)(Ys + (8 * g + 4 + q) * G::LS + nb_ * 16 + 4 * p));
+          const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+            if (kb < nbk) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kb], acc[nb_][kb], 0, 0, 0);
+        }
+      }
+    } else {
+      const float* Yf = reinterpret_cast<const float*>(Ys);
+      const float* Xf = reinterpret_cast<const float*>(Xs);
+#pragma unroll
+      for (int s = 0; s < WMS / 4; ++s) {
+        const int mm = 4 * s + (lane >> 4);
+        float bv[4];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) bv[kb] = Xf[mm * G::LS + kb * 16 + (lane & 15)];
+#pragma unroll
+        for (int nb_ = 0; nb_ < 4; ++nb_) {
+          if (nb_ < nbn) {
+            const float av = Yf[mm * G::LS + nb_ * 16 + (lane & 15)];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+              if (kb < nbk) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kb], acc[nb_][kb], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // ---- cross-wave reduction of the 64x64 tile ----
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  for (int i = tid; i < WT * WT; i += 256) red[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int nb_ = 0; nb_ < 4; ++nb_)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nn = nb_ * 16 + 4 * (lane >> 4) + r, kk = kb * 16 + (lane & 15);
+        atomicAdd(&red[nn * WT + kk], acc[nb_][kb][r]);
+      }
+  __syncthreads();
+  float* out = slab + (int64_t)blockIdx.y * N * K;
+  for (int i = tid; i < WT * WT; i += 256) {
+    const int nn = i / WT, kk = i - nn * WT;
+    if (nn < nv && kk < kv) out[(int64_t)(n0 + nn) * K + k0 + kk] = red[i];
+  }
+}
+
+template <typename T>
+int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, int pro_mode, const Pro& pro,
+                    float* slab, int64_t slab_cap, float* dW, bool accumulate) {
+  if ((N & 7) || (K & 7)) { set_error("pw_wgrad: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
+  const int tnn = cdiv(N, WT), tnk = cdiv(K, WT);
+  const int tiles = tnn * tnk;
+  int64_t splits = std::max<int64_t>(1, 1024 / tiles);
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, cdiv64(M, 4 * WMS)));
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, slab_cap / ((int64_t)N * K)));
+  int64_t mps = cdiv64(cdiv64(std::max<int64_t>(M, 1), splits), 4 * WMS) * (4 * WMS);
+  splits = cdiv64(std::max<int64_t>(M, 1), mps);
+  dim3 grid(tiles, (unsigned)splits), block(256);
+  if (pro_mode == PRO_NONE)
+    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_NONE>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
+  else if (pro_mode == PRO_BN_SILU)
+    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
+  else
+    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU_G>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
+  DFD_HIP_CHECK(hipGetLastError());
+  return launch_reduce_slabs(s, slab, (int)splits, (int64_t)N * K, dW, accumulate);
+}
+
+template int launch_pw_gemm<float>(hipStream_t, const float*, const float*, float*, const float*, int64_t, int, int,
+                                   int, const Pro&, float*, int*);
+template int launch_pw_gemm<bf16>(hipStream_t, const bf16*, const bf16*, bf16*, const bf16*, int64_t, int, int, int,
+                                  const Pro&, float*, int*);
+template int launch_pw_wgrad<float>(hipStream_t, const float*, const float*, int64_t, int, int, int, const Pro&,
+                                    float*, int64_t, float*, bool);
+template int launch_pw_wgrad<bf16>(hipStream_t, const bf16*, const bf16*, int64_t, int, int, int, const Pro&, float*,
+                                   int64_t, float*, bool);
+
+}  // namespace dfd

@@ -1,0 +1,396 @@
+// Detector head, loss and optimizer kernels (K7, K8 of SURVEY §2.2) on gfx950.
+//
+//   head   : temporal attention MLP (Linear 1280->64, ReLU, Linear 64->1, Sigmoid),
+//            softmax over T, attention-weighted sum, Dropout, fc1 (->256) + ReLU, Dropout, fc2
+//            -- src/pretrained_detector.py:65-76, 123-141 -- forward and backward.
+//   loss   : weighted 2-class CrossEntropy (ensemble_trainer.py:358, train.py:337), fused fwd/bwd.
+//   optim  : global-L2 clip_grad_norm_(max_norm) (ensemble_trainer.py:199) fused into
+//            AdamW / Adam (ensemble_trainer.py:146, train.py:323) over the flat fp32 buffer.
+//   cast   : fp32 master weights -> compute dtype copies (+ transposed 1x1 weights for dgrad).
+#include "kernels.h"
+#include "head.h"
+
+namespace dfd {
+
+// ------------------------------------------------------------------ dropout hash (counter based)
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float drop_mul(uint64_t seed, uint32_t stream, int64_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  if (p >= 1.f) return 0.f;
+  const uint32_t h = mix32((uint32_t)idx ^ mix32((uint32_t)(idx >> 32) ^ mix32((uint32_t)seed ^ mix32(
+                          (uint32_t)(seed >> 32) + stream * 0x9E3779B9U))));
+  const float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.0f / (1.0f - p) : 0.f;
+}
+
+// ------------------------------------------------------------------ generic small linear ops
+// Y[r][o] = act( sum_i X[r][i]*xm(r,i) * W[o][i] + b[o] ),  xm = dropout multiplier (stream) or 1
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W,
+                                                         const float* __restrict__ b, float* __restrict__ Y, int R,
+                                                         int I, int O, int relu, uint64_t seed, uint32_t stream,
+                                                         float p) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)R * O) return;
+  const int r = (int)(idx / O), o = (int)(idx % O);
+  const float* x = X + (int64_t)r * I;
+  const float* w = W + (int64_t)o * I;
+  float a = 0.f;
+  if (p > 0.f) {
+    for (int i = 0; i < I; ++i) a += x[i] * drop_mul(seed, stream, (int64_t)r * I + i, p) * w[i];
+  } else {
+    for (int i = 0; i < I; ++i) a += x[i] * w[i];
+  }
+  if (b) a += b[o];
+  if (relu) a = fmaxf(a, 0.f);
+  Y[idx] = a;
+}
+
+// dX[r][i] = (acc? dX : 0) + sum_o dY[r][o] * W[o][i], then * xm(r,i) (dropout on the input)
+__global__ __launch_bounds__(256) void linear_dgrad_kernel(const float* __restrict__ dY, const float* __restrict__ W,
+                                                           float* __restrict__ dX, int R, int I, int O, int accumulate,
+                                                           uint64_t seed, uint32_t stream, float p) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)R * I) return;
+  const int r = (int)(idx / I), i = (int)(idx % I);
+  float a = 0.f;
+  for (int o = 0; o < O; ++o) a += dY[(int64_t)r * O + o] * W[(int64_t)o * I + i];
+  if (p > 0.f) a *= drop_mul(seed, stream, idx, p);
+  dX[idx] = accumulate ? dX[idx] + a : a;
+}
+
+// dW[o][i] = sum_r dY[r][o] * X[r][i]*xm(r,i);  db[o] = sum_r dY[r][o]
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restrict__ dY, const float* __restrict__ X,
+                                                           float* __restrict__ dW, float* __restrict__ db, int R,
+                                                           int I, int O, uint64_t seed, uint32_t stream, float p) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx < (int64_t)O * I) {
+    const int o = (int)(idx / I), i = (int)(idx % I);
+    float a = 0.f;
+    for (int r = 0; r < R; ++r) {
+      float x = X[(int64_t)r * I + i];
+      if (p > 0.f) x *= drop_mul(seed, stream, (int64_t)r * I + i, p);
+      a += dY[(int64_t)r * O + o] * x;
+    }
+    dW[idx] = a;
+  }
+  if (db && idx < O) {
+    float a = 0.f;
+    for (int r = 0; r < R; ++r) a += dY[(int64_t)r * O + idx];
+    db[idx] = a;
+  }
+}
+
+// Y[r] = post( dot(X[r], w) + b ) for a single output (the 64->1 attention scorer)
+// ------------------------------------------------------------------ temporal attention (per clip)
+// e[bt] = sigmoid(w2 . hid[bt] + b2) ; a[b] = softmax_t(e[b]) ; g[b] = sum_t a[b][t] f[bt]
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const float* __restrict__ F, const float* __restrict__ hid,
+                                                       const float* __restrict__ w2, const float* __restrict__ b2,
+                                                       int T, int D, int H, int use_attn, float* __restrict__ e,
+                                                       float* __restrict__ a, float* __restrict__ g) {
+  extern __shared__ float s_a[];  // [T]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (use_attn) {
+    for (int t = wave; t < T; t += 4) {
+      float v = 0.f;
+      for (int j = lane; j < H; j += 64) v += hid[((int64_t)b * T + t) * H + j] * w2[j];
+      v = wave_sum(v);
+      if (lane == 0) {
+        const float ev = sigmoidf_(v + b2[0]);
+        e[(int64_t)b * T + t] = ev;
+        s_a[t] = ev;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float mx = -INFINITY;
+      for (int t = 0; t < T; ++t) mx = fmaxf(mx, s_a[t]);
+      float sum = 0.f;
+      for (int t = 0; t < T; ++t) { s_a[t] = expf(s_a[t] - mx); sum += s_a[t]; }
+      for (int t = 0; t < T; ++t) s_a[t] /= sum;
+    }
+  } else {
+    for (int t = tid; t < T; t += 256) s_a[t] = 1.0f / (float)T;
+  }
+  __syncthreads();
+  for (int t = tid; t < T; t += 256) a[(int64_t)b * T + t] = s_a[t];
+  for (int i = tid; i < D; i += 256) {
+    float acc = 0.f;
+    if (use_attn) {
+      for (int t = 0; t < T; ++t) acc += F[((int64_t)b * T + t) * D + i] * s_a[t];
+    } else {
+      for (int t = 0; t < T; ++t) acc += F[((int64_t)b * T + t) * D + i];
+      acc /= (float)T;
+    }
+    g[(int64_t)b * D + i] = acc;
+  }
+}
+
+// backward of the attention pooling for clip b:
+//   da[t] = dg . f[bt] + dscores[b][t] ; de = a (da - sum a da) ; dpe = de e (1-e)
+//   dF[bt] = a[t] dg ;  dhid[bt][j] = dpe[bt] * w2[j] * (hid>0)
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const float* __restrict__ F, const float* __restrict__ hid,
+                                                       const float* __restrict__ w2, const float* __restrict__ e,
+                                                       const float* __restrict__ a, const float* __restrict__ dg,
+                                                       const float* __restrict__ dscores, int T, int D, int H,
+                                                       int use_attn, float* __restrict__ dF, float* __restrict__ dpe,
+                                                       float* __restrict__ dhid) {
+  extern __shared__ float sm[];  // [2T]
+  float* s_da = sm;
+  float* s_dpe = sm + T;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < D; i += 256) {
+    const float d = dg[(int64_t)b * D + i];
+    for (int t = 0; t < T; ++t) dF[((int64_t)b * T + t) * D + i] = a[(int64_t)b * T + t] * d;
+  }
+  if (!use_attn) return;
+  for (int t = wave; t < T; t += 4) {
+    float v = 0.f;
+    for (int i = lane; i < D; i += 64) v += dg[(int64_t)b * D + i] * F[((int64_t)b * T + t) * D + i];
+    v = wave_sum(v);
+    if (lane == 0) s_da[t] = v + (dscores ? dscores[(int64_t)b * T + t] : 0.f);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float dot = 0.f;
+    for (int t = 0; t < T; ++t) dot += a[(int64_t)b * T + t] * s_da[t];
+    for (int t = 0; t < T; ++t) {
+      const float at = a[(int64_t)b * T + t], ev = e[(int64_t)b * T + t];
+      const float de = at * (s_da[t] - dot);
+      const float d = de * ev * (1.f - ev);
+      s_dpe[t] = d;
+      dpe[(int64_t)b * T + t] = d;
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < T * H; idx += 256) {
+    const int t = idx / H, j = idx % H;
+    const float hv = hid[((int64_t)b * T + t) * H + j];
+    dhid[((int64_t)b * T + t) * H + j] = hv > 0.f ? s_dpe[t] * w2[j] : 0.f;
+  }
+}
+
+// relu'/dropout for fc1 output: d[r][j] *= (h>0) * xm2(r,j)   (in place)
+__global__ void relu_drop_bwd_kernel(float* __restrict__ d, const float* __restrict__ h, int64_t n, uint64_t seed,
+                                     uint32_t stream, float p) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  d[i] = h[i] > 0.f ? d[i] : 0.f;
+}
+
+// ------------------------------------------------------------------ weighted cross entropy
+// loss = sum_b w[y_b] * (-log softmax(z_b)[y_b]) / sum_b w[y_b]  (ignore_index rows excluded)
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ y,
+                                                     const float* __restrict__ w, int B, int NC, int64_t ignore,
+                                                     float* __restrict__ loss, float* __restrict__ wsum) {
+  __shared__ double sn[256], sd[256];
+  double num = 0.0, den = 0.0;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const int64_t lab = y[b];
+    if (lab == ignore) continue;
+    const float* zb = z + (int64_t)b * NC;
+    float mx = -INFINITY;
+    for (int k = 0; k < NC; ++k) mx = fmaxf(mx, zb[k]);
+    double se = 0.0;
+    for (int k = 0; k < NC; ++k) se += exp((double)zb[k] - mx);
+    const double lse = mx + log(se);
+    const double wb = w ? (double)w[lab] : 1.0;
+    num += wb * (lse - (double)zb[lab]);
+    den += wb;
+  }
+  sn[threadIdx.x] = num;
+  sd[threadIdx.x] = den;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, d = 0.0;
+    for (int i = 0; i < 256; ++i) { a += sn[i]; d += sd[i]; }
+    loss[0] = (float)(a / d);
+    wsum[0] = (float)d;
+  }
+}
+
+__global__ void ce_bwd_kernel(const float* __restrict__ z, const int64_t* __restrict__ y, const float* __restrict__ w,
+                              int B, int NC, int64_t ignore, const float* __restrict__ wsum,
+                              const float* __restrict__ gout, float* __restrict__ dz) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const int64_t lab = y[b];
+  const float* zb = z + (int64_t)b * NC;
+  float* db = dz + (int64_t)b * NC;
+  if (lab == ignore) {
+    for (int k = 0; k < NC; ++k) db[k] = 0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int k = 0; k < NC; ++k) mx = fmaxf(mx, zb[k]);
+  float se = 0.f;
+  for (int k = 0; k < NC; ++k) se += expf(zb[k] - mx);
+  const float scale = (w ? w[lab] : 1.f) / wsum[0] * gout[0];
+  for (int k = 0; k < NC; ++k) db[k] = (expf(zb[k] - mx) / se - (k == lab ? 1.f : 0.f)) * scale;
+}
+
+// ------------------------------------------------------------------ grad norm + Adam(W)
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part) {
+  __shared__ double sh[256];
+  double a = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = g[i];
+    a += v * v;
+  }
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
+}
+
+// out[0] = total norm, out[1] = clip coefficient min(1, max_norm/(norm+1e-6)) (1 if max_norm <= 0)
+__global__ void norm_finalize_kernel(const double* __restrict__ part, int nparts, float max_norm, float* out) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0;
+  for (int i = 0; i < nparts; ++i) a += part[i];
+  const float nrm = (float)sqrt(a);
+  out[0] = nrm;
+  float c = 1.f;
+  if (max_norm > 0.f) {
+    c = max_norm / (nrm + 1e-6f);
+    if (c > 1.f) c = 1.f;
+  }
+  out[1] = c;
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                                   float* __restrict__ v, int64_t n, AdamHyper h,
+                                                   const float* __restrict__ coef) {
+  const float cf = coef ? coef[1] : 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float gi = g[i] * h.grad_scale;
+    if (coef) { gi = gi * cf; g[i] = gi; }
+    float pi = p[i];
+    if (h.decoupled) {
+      pi = pi * h.decay;
+    } else if (h.weight_decay != 0.f) {
+      gi = gi + h.weight_decay * pi;
+    }
+    float mi = m[i];
+    mi = mi + h.omb1 * (gi - mi);
+    float vi = v[i] * h.beta2 + h.omb2 * gi * gi;
+    const float denom = sqrtf(vi) / h.bc2_sqrt + h.eps;
+    pi = pi + (-h.step_size * mi) / denom;
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+// ------------------------------------------------------------------ param cast (+ transpose)
+template <typename T>
+__global__ __launch_bounds__(256) void cast_params_kernel(const float* __restrict__ params, T* __restrict__ out,
+                                                          const CastSeg* __restrict__ segs) {
+  const CastSeg sg = segs[blockIdx.y];
+  const int64_t n = (int64_t)sg.rows * sg.cols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (sg.transpose) {
+      // out[c][r] = in[r][c]; i indexes the output
+      const int c = (int)(i / sg.rows), r = (int)(i % sg.rows);
+      out[sg.dst + i] = Tr<T>::from_f(params[sg.src + (int64_t)r * sg.cols + c]);
+    } else {
+      out[sg.dst + i] = Tr<T>::from_f(params[sg.src + i]);
+    }
+  }
+}
+
+template <typename T>
+int launch_cast_params(hipStream_t s, const float* params, T* out, const CastSeg* segs_dev, int nseg, int max_elems) {
+  if (nseg <= 0) return 0;
+  const int gx = std::max(1, std::min(64, cdiv(max_elems, 256)));
+  hipLaunchKernelGGL((cast_params_kernel<T>), dim3(gx, nseg), dim3(256), 0, s, params, out, segs_dev);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+template int launch_cast_params<float>(hipStream_t, const float*, float*, const CastSeg*, int, int);
+template int launch_cast_params<bf16>(hipStream_t, const float*, bf16*, const CastSeg*, int, int);
+
+// ------------------------------------------------------------------ host launchers (head.h)
+static unsigned nblk(int64_t n) { return (unsigned)std::max<int64_t>(1, cdiv64(n, 256)); }
+
+int head_forward(hipStream_t s, const HeadDims& d, const HeadParams& P, const float* F, HeadWork& w, uint64_t seed,
+                 float p, float* logits, float* scores) {
+  if (d.use_attn) {
+    hipLaunchKernelGGL(linear_fwd_kernel, dim3(nblk((int64_t)d.B * d.T * d.H)), dim3(256), 0, s, F, P.ta_w1,
+                       P.ta_b1, w.hid, d.B * d.T, d.D, d.H, 1, seed, 0u, 0.f);
+  }
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(d.B), dim3(256), d.T * sizeof(float), s, F, w.hid, P.ta_w2, P.ta_b2, d.T,
+                     d.D, d.H, d.use_attn, w.e, scores, w.g);
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3(nblk((int64_t)d.B * d.F1)), dim3(256), 0, s, w.g, P.fc1_w, P.fc1_b, w.h1,
+                     d.B, d.D, d.F1, 1, seed, 1u, p);
+  hipLaunchKernelGGL(linear_fwd_kernel, dim3(nblk((int64_t)d.B * d.NC)), dim3(256), 0, s, w.h1, P.fc2_w, P.fc2_b,
+                     logits, d.B, d.F1, d.NC, 0, seed, 2u, p);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int head_backward(hipStream_t s, const HeadDims& d, const HeadParams& P, const float* F, HeadWork& w, uint64_t seed,
+                  float p, const float* scores, const float* dlogits, const float* dscores, float* dF, HeadParams& G) {
+  // fc2: dW2 = dlogits^T . drop(h1) ; db2 ; dh1 = dlogits . W2 (then * drop2 * relu')
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.NC * d.F1)), dim3(256), 0, s, dlogits, w.h1,
+                     (float*)G.fc2_w, (float*)G.fc2_b, d.B, d.F1, d.NC, seed, 2u, p);
+  hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)d.B * d.F1)), dim3(256), 0, s, dlogits, P.fc2_w, w.dh1,
+                     d.B, d.F1, d.NC, 0, seed, 2u, p);
+  hipLaunchKernelGGL(relu_drop_bwd_kernel, dim3(nblk((int64_t)d.B * d.F1)), dim3(256), 0, s, w.dh1, w.h1,
+                     (int64_t)d.B * d.F1, seed, 0u, 0.f);
+  // fc1: dW1 = dh1^T . drop(g) ; db1 ; dg = dh1 . W1 * drop1
+  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.F1 * d.D)), dim3(256), 0, s, w.dh1, w.g,
+                     (float*)G.fc1_w, (float*)G.fc1_b, d.B, d.D, d.F1, seed, 1u, p);
+  hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)d.B * d.D)), dim3(256), 0, s, w.dh1, P.fc1_w, w.dg, d.B,
+                     d.D, d.F1, 0, seed, 1u, p);
+  // attention pooling
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(d.B), dim3(256), 2 * d.T * sizeof(float), s, F, w.hid, P.ta_w2, w.e,
+                     scores, w.dg, dscores, d.T, d.D, d.H, d.use_attn, dF, w.dpe, w.dhid);
+  if (d.use_attn) {
+    const int R = d.B * d.T;
+    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.H)), dim3(256), 0, s, w.dpe, w.hid,
+                       (float*)G.ta_w2, (float*)G.ta_b2, R, d.H, 1, seed, 0u, 0.f);
+    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.H * d.D)), dim3(256), 0, s, w.dhid, F,
+                       (float*)G.ta_w1, (float*)G.ta_b1, R, d.D, d.H, seed, 0u, 0.f);
+    hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)R * d.D)), dim3(256), 0, s, w.dhid, P.ta_w1, dF, R,
+                       d.D, d.H, 1, seed, 0u, 0.f);
+  }
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int ce_forward(hipStream_t s, const float* z, const int64_t* y, const float* w, int B, int NC, int64_t ignore,
+               float* loss, float* wsum) {
+  hipLaunchKernelGGL(ce_fwd_kernel, dim3(1), dim3(256), 0, s, z, y, w, B, NC, ignore, loss, wsum);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int ce_backward(hipStream_t s, const float* z, const int64_t* y, const float* w, int B, int NC, int64_t ignore,
+                const float* wsum, const float* gout, float* dz) {
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3(nblk(B)), dim3(256), 0, s, z, y, w, B, NC, ignore, wsum, gout, dz);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int grad_norm(hipStream_t s, const float* g, int64_t n, float max_norm, double* part, int nparts, float* out) {
+  const int gx = std::max(1, std::min<int>(nparts, (int)nblk(n)));
+  hipLaunchKernelGGL(sumsq_kernel, dim3(gx), dim3(256), 0, s, g, n, part);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(64), 0, s, part, gx, max_norm, out);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int adam_step(hipStream_t s, float* p, float* g, float* m, float* v, int64_t n, const AdamHyper& h, const float* coef) {
+  const int gx = (int)std::min<int64_t>(nblk(n), 4096);
+  hipLaunchKernelGGL(adam_kernel, dim3(gx), dim3(256), 0, s, p, g, m, v, n, h, coef);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace dfd

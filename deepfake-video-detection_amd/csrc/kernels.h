@@ -1,0 +1,113 @@
+// Internal launcher declarations (host side).  Every launcher enqueues on `stream`
+// and returns 0 on success / -1 with dfd::set_error() on failure.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace dfd {
+
+// ---------------- pointwise (1x1 conv) GEMMs: k_gemm.hip ----------------
+// C[M][N] = pro(A)[M][K] * B[N][K]^T (+ R[M][N]); optional BN-stat partials of C's columns
+// into stats[gridDim.x][2][N] (rows written = *stat_rows).
+template <typename T>
+int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K,
+                   int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+// dW[N][K] = sum_m dY[m][n] * pro(X)[m][k]  -> written (or added) into dW (fp32) via slabs
+template <typename T>
+int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, int pro_mode,
+                    const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
+
+// ---------------- depthwise convs: k_dw.hip ----------------
+struct DwGeom {
+  int frames, H, W, C, k, s, pad, Ho, Wo;
+};
+// Y[n,ho,wo,c] = sum_taps pro(X)[n, ho*s-pad+kh, wo*s-pad+kw, c] * w[c][kh][kw]
+template <typename T>
+int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro,
+                  int pro_mode, float* stats, int* stat_rows);
+template <typename T>
+int launch_dw_dgrad(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* dX);
+template <typename T>
+int launch_dw_wgrad(hipStream_t s, const DwGeom& g, const T* dY, const T* X, const Pro& pro,
+                    int pro_mode, float* slab, int64_t slab_cap, float* dW, bool accumulate);
+
+// ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------
+// finalize training stats: mean/invstd/scale/shift + running update (momentum); eval: from running
+int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
+                       const float* beta, float* run_mean, float* run_var, float momentum, float eps,
+                       bool training, float* mean, float* invstd, float* scale, float* shift);
+// X = Y*scale + shift (+ R)
+template <typename T>
+int launch_bn_apply(hipStream_t s, const T* Y, const float* scale, const float* shift, const T* R, T* X,
+                    int64_t M, int C);
+// BN backward, phase 1: per-channel partials of g and g*xhat, where
+//   dA = dZ * gate[f][c] (if gate) + bc[f][c]*bc_scale (if bc);  g = dA * act'(y)  (act = SiLU or identity)
+struct BnBwdIn {
+  const void* dZ;       // [M][C] T or null
+  const float* gate;    // [frames][C] or null
+  const float* bc;      // [frames][C] broadcast term or null
+  float bc_scale;
+  int rows_per_frame;
+  bool silu;
+  const float* mean;    // saved batch mean   (or running mean in eval)
+  const float* invstd;  // saved batch invstd (or running invstd in eval)
+  const float* scale;   // gamma*invstd
+  const float* shift;   // beta - mean*scale
+};
+template <typename T>
+int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, float* stats,
+                         int* stat_rows);
+// phase 2 (finalize): dgamma/dbeta into grads, coefficients k1,k2,k3 for dY = k1*g + k2*y + k3
+int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C,
+                           const float* gamma, const float* mean, const float* invstd, bool training,
+                           float* dgamma, float* dbeta, bool accumulate, float* coef /*[3][C]*/);
+// phase 3: dY = k1*g + k2*y + k3   (dY may alias dZ)
+template <typename T>
+int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const float* coef, T* dY, int64_t M,
+                        int C);
+// SE squeeze: sq[f][c] = mean_hw pro(Y)   (pro = BN+SiLU)
+template <typename T>
+int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
+                      int64_t part_cap, float* sq);
+// SE excitation: r = silu(Wr sq + br) ; gate = sigmoid(We r + be) ; saves rpre
+int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
+                     const float* be, int frames, int C, int rd, float* rpre, float* gate);
+// SE backward reduce: dgate[f][c] = sum_hw dZ * pro(Y)   (pro = BN+SiLU, no gate)
+template <typename T>
+int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
+                         float* part, int64_t part_cap, float* dgate);
+// SE FC backward: from dgate -> dsq (written, scaled by 1/HW into bc), grads of wr,br,we,be
+int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
+                     const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
+                     float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
+// head global average pool: feat[f][c] = mean_hw silu(Y*scale+shift)
+template <typename T>
+int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat);
+// sum `splits` slabs of n floats into out (= or +=)
+int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate);
+
+// ---------------- stem (3->32, k3 s2): k_stem.hip ----------------
+struct StemGeom {
+  int frames, H, W, Ho, Wo;
+  int64_t sf, sc, sh, sw;  // element strides of the fp32 input (frame, channel, row, col)
+};
+template <typename T>
+int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const float* w, T* Y, float* stats,
+                    int* stat_rows);
+template <typename T>
+int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const float* x, const T* dY, float* slab,
+                      int64_t slab_cap, float* dW, bool accumulate);
+
+// ---------------- misc: k_misc.hip ----------------
+struct CastSeg {
+  int64_t src, dst;  // element offsets
+  int rows, cols;    // transpose a [rows][cols] matrix into [cols][rows] if transpose
+  int transpose;
+};
+template <typename T>
+int launch_cast_params(hipStream_t s, const float* params, T* out, const CastSeg* segs_dev, int nseg,
+                       int max_elems);
+
+}  // namespace dfd

@@ -1,0 +1,417 @@
+// EfficientNet-B0 trunk runtime: topology, workspace layout and launch sequences.
+//
+// Native replacement for the trunk the reference obtains from
+// timm.create_model('efficientnet_b0') and runs as nn.Sequential(children()[:-1])
+// (src/pretrained_detector.py:43-46, called at :116).  The tensor table reproduces timm's
+// state_dict names/shapes/order, so checkpoints written by the reference load unchanged
+// (app.py:1413-1528 strips prefixes and shape-filters by these names).
+#include "plan.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace dfd {
+
+namespace {
+
+struct ArchRow {
+  int ds, repeats, k, s, e, cout;
+};
+// timm efficientnet_b0 arch_def: ds_r1_k3_s1_e1_c16, ir_r2_k3_s2_e6_c24, ir_r2_k5_s2_e6_c40,
+// ir_r3_k3_s2_e6_c80, ir_r3_k5_s1_e6_c112, ir_r4_k5_s2_e6_c192, ir_r1_k3_s1_e6_c320 (all se0.25)
+const ArchRow kArch[7] = {{1, 1, 3, 1, 1, 16},  {0, 2, 3, 2, 6, 24},  {0, 2, 5, 2, 6, 40},  {0, 3, 3, 2, 6, 80},
+                          {0, 3, 5, 1, 6, 112}, {0, 4, 5, 2, 6, 192}, {0, 1, 3, 1, 6, 320}};
+constexpr int kStem = 32, kHead = 1280;
+
+struct Topo {
+  std::vector<TensorSpec> t;
+  int t_stem;
+  BNL bn_stem, bn_head;
+  PWL head;
+  std::vector<Block> blocks;
+  int stage_first[8];  // first tensor index of stage s (stage_first[7] = conv_head)
+
+  int add(const std::string& n, int kind, std::vector<int64_t> shape) {
+    t.push_back(TensorSpec{n, kind, std::move(shape)});
+    return (int)t.size() - 1;
+  }
+  BNL bn(const std::string& pre, int C) {
+    BNL b{};
+    b.C = C;
+    b.t_w = add(pre + ".weight", TK_PARAM, {C});
+    b.t_b = add(pre + ".bias", TK_PARAM, {C});
+    b.t_rm = add(pre + ".running_mean", TK_BNBUF, {C});
+    b.t_rv = add(pre + ".running_var", TK_BNBUF, {C});
+    add(pre + ".num_batches_tracked", TK_COUNTER, {});
+    return b;
+  }
+  PWL pw(const std::string& n, int cin, int cout) {
+    PWL p{};
+    p.cin = cin;
+    p.cout = cout;
+    p.t_w = add(n, TK_PARAM, {cout, cin, 1, 1});
+    return p;
+  }
+  Topo() {
+    t_stem = add("0.weight", TK_PARAM, {kStem, 3, 3, 3});
+    bn_stem = bn("1", kStem);
+    int cin = kStem;
+    for (int si = 0; si < 7; ++si) {
+      stage_first[si] = (int)t.size();
+      const ArchRow& a = kArch[si];
+      for (int bi = 0; bi < a.repeats; ++bi) {
+        Block b{};
+        b.ds = a.ds;
+        b.stage = si;
+        b.idx = bi;
+        b.cin = cin;
+        b.cout = a.cout;
+        b.k = a.k;
+        b.s = bi == 0 ? a.s : 1;
+        b.mid = cin * a.e;
+        b.rd = (int)((double)cin * 0.25 + 0.5);  // round(0.25 * block_in_chs)
+        b.skip = (b.s == 1 && cin == a.cout);
+        const std::string pre = "2." + std::to_string(si) + "." + std::to_string(bi) + ".";
+        if (b.ds) {
+          b.t_dw = add(pre + "conv_dw.weight", TK_PARAM, {b.mid, 1, b.k, b.k});
+          b.bn1 = bn(pre + "bn1", b.mid);
+        } else {
+          b.pw = pw(pre + "conv_pw.weight", cin, b.mid);
+          b.bn1 = bn(pre + "bn1", b.mid);
+          b.t_dw = add(pre + "conv_dw.weight", TK_PARAM, {b.mid, 1, b.k, b.k});
+          b.bn2 = bn(pre + "bn2", b.mid);
+        }
+        b.t_se_wr = add(pre + "se.conv_reduce.weight", TK_PARAM, {b.rd, b.mid, 1, 1});
+        b.t_se_br = add(pre + "se.conv_reduce.bias", TK_PARAM, {b.rd});
+        b.t_se_we = add(pre + "se.conv_expand.weight", TK_PARAM, {b.mid, b.rd, 1, 1});
+        b.t_se_be = add(pre + "se.conv_expand.bias", TK_PARAM, {b.mid});
+        if (b.ds) {
+          b.pwl = pw(pre + "conv_pw.weight", b.mid, b.cout);
+          b.bn3 = bn(pre + "bn2", b.cout);
+        } else {
+          b.pwl = pw(pre + "conv_pwl.weight", b.mid, b.cout);
+          b.bn3 = bn(pre + "bn3", b.cout);
+        }
+        blocks.push_back(b);
+        cin = a.cout;
+      }
+    }
+    stage_first[7] = (int)t.size();
+    head = pw("3.weight", cin, kHead);
+    bn_head = bn("4", kHead);
+  }
+};
+
+const Topo& topo() {
+  static const Topo tp;
+  return tp;
+}
+
+int conv_out(int h, int k, int s) { return (h + 2 * (((s - 1) + (k - 1)) / 2) - k) / s + 1; }
+
+}  // namespace
+
+const std::vector<TensorSpec>& b0_tensor_table() { return topo().t; }
+
+void plan_segment_range(const Plan& p, int seg, int* lo, int* hi) {
+  const Topo& tp = topo();
+  const int n = (int)tp.t.size();
+  if (seg == 0) { *lo = tp.stage_first[7]; *hi = n; }
+  else if (seg >= 1 && seg <= 7) { const int st = 7 - seg; *lo = tp.stage_first[st]; *hi = tp.stage_first[st + 1]; }
+  else { *lo = 0; *hi = tp.stage_first[0]; }
+  (void)p;
+}
+
+int plan_build(Plan& p, int frames, int H, int W, int dtype) {
+  if (frames <= 0 || H < 8 || W < 8) { set_error("plan: bad shape", __FILE__, __LINE__); return -1; }
+  if (dtype != 0 && dtype != 1) { set_error("plan: dtype must be 0 (fp32) or 1 (bf16)", __FILE__, __LINE__); return -1; }
+  const Topo& tp = topo();
+  p.frames = frames; p.H = H; p.W = W; p.dtype = dtype;
+  p.tensors = tp.t;
+  p.t_stem = tp.t_stem;
+  p.bn_stem = tp.bn_stem;
+  p.bn_head = tp.bn_head;
+  p.head = tp.head;
+  p.blocks = tp.blocks;
+  p.H1 = conv_out(H, 3, 2);
+  p.W1 = conv_out(W, 3, 2);
+  const int64_t es = dtype ? 2 : 4;
+  int64_t cur = 0;
+  auto alloc = [&](int64_t bytes) { const int64_t o = cur; cur += (std::max<int64_t>(bytes, 1) + 255) & ~int64_t(255); return o; };
+  auto alloc_bn = [&](BNL& b) {
+    b.o_mean = alloc(b.C * 4); b.o_invstd = alloc(b.C * 4); b.o_scale = alloc(b.C * 4); b.o_shift = alloc(b.C * 4);
+  };
+  const int64_t F = frames;
+  p.o_ystem = alloc(F * p.H1 * p.W1 * kStem * es);
+  alloc_bn(p.bn_stem);
+  int h = p.H1, w = p.W1;
+  int64_t maxX = F * h * w * kStem, maxS = 0, maxE1 = F * h * w * kStem, maxE2 = 0, maxSE = 0, maxRD = 0;
+  for (Block& b : p.blocks) {
+    b.hin = h; b.win = w;
+    b.hout = conv_out(h, b.k, b.s); b.wout = conv_out(w, b.k, b.s);
+    const int64_t Min = F * b.hin * b.win, Mout = F * b.hout * b.wout;
+    if (!b.ds) { b.o_y1 = alloc(Min * b.mid * es); alloc_bn(b.bn1); alloc_bn(b.bn2); }
+    else { b.o_y1 = -1; alloc_bn(b.bn1); }
+    b.o_y2 = alloc(Mout * b.mid * es);
+    b.o_y3 = alloc(Mout * b.cout * es);
+    b.o_x = alloc(Mout * b.cout * es);
+    alloc_bn(b.bn3);
+    b.o_sq = alloc(F * b.mid * 4);
+    b.o_rpre = alloc(F * b.rd * 4);
+    b.o_gate = alloc(F * b.mid * 4);
+    maxX = std::max({maxX, Min * b.cin, Mout * b.cout});
+    maxS = std::max(maxS, Mout * b.cout);
+    if (!b.ds) maxE1 = std::max(maxE1, Min * b.mid);
+    maxE2 = std::max(maxE2, Mout * b.mid);
+    maxSE = std::max<int64_t>(maxSE, b.mid);
+    maxRD = std::max<int64_t>(maxRD, b.rd);
+    h = b.hout; w = b.wout;
+  }
+  p.Hf = h; p.Wf = w;
+  const int64_t Mf = F * h * w;
+  p.o_yh = alloc(Mf * kHead * es);
+  alloc_bn(p.bn_head);
+  maxS = std::max(maxS, Mf * kHead);
+  maxX = std::max(maxX, Mf * 320);
+  // compute-dtype 1x1 weights (+ transposes for dgrad)
+  p.cast_host.clear();
+  p.cast_max = 0;
+  auto alloc_pw = [&](PWL& q) {
+    q.o_w = alloc((int64_t)q.cout * q.cin * es);
+    q.o_wt = alloc((int64_t)q.cout * q.cin * es);
+    p.cast_max = std::max(p.cast_max, q.cout * q.cin);
+  };
+  for (Block& b : p.blocks) { if (!b.ds) alloc_pw(b.pw); alloc_pw(b.pwl); }
+  alloc_pw(p.head);
+  // scratch
+  p.stats_cap = (int64_t)2048 * 2 * kHead;
+  p.slab_cap = (int64_t)8 << 20;
+  p.part_cap = std::max<int64_t>((int64_t)4 << 20, F * kHead);
+  p.o_stats = alloc(p.stats_cap * 4);
+  p.o_slab = alloc(p.slab_cap * 4);
+  p.o_part = alloc(p.part_cap * 4);
+  p.o_coef = alloc(3 * kHead * 4);
+  p.o_dgate = alloc(F * maxSE * 4);
+  p.o_bc = alloc(F * maxSE * 4);
+  p.o_de = alloc(F * maxSE * 4);
+  p.o_dz = alloc(F * maxRD * 4);
+  p.o_gx[0] = alloc(maxX * es);
+  p.o_gx[1] = alloc(maxX * es);
+  p.o_gs = alloc(maxS * es);
+  p.o_ge1 = alloc(maxE1 * es);
+  p.o_ge2 = alloc(maxE2 * es);
+  p.ws_bytes = cur;
+  p.offs.assign(p.tensors.size(), -1);
+  p.bound = false;
+  DFD_HIP_CHECK(hipGetDevice(&p.device));
+  return 0;
+}
+
+int plan_bind(Plan& p, const int64_t* offs, int n) {
+  if (n != (int)p.tensors.size()) { set_error("bind: tensor count mismatch", __FILE__, __LINE__); return -1; }
+  p.offs.assign(offs, offs + n);
+  const int64_t es = p.dtype ? 2 : 4;
+  p.cast_host.clear();
+  auto seg = [&](const PWL& q) {
+    p.cast_host.push_back(CastSeg{p.offs[q.t_w], q.o_w / es, q.cout, q.cin, 0});
+    p.cast_host.push_back(CastSeg{p.offs[q.t_w], q.o_wt / es, q.cout, q.cin, 1});
+  };
+  for (const Block& b : p.blocks) { if (!b.ds) seg(b.pw); seg(b.pwl); }
+  seg(p.head);
+  if (!p.cast_dev) DFD_HIP_CHECK(hipMalloc(&p.cast_dev, p.cast_host.size() * sizeof(CastSeg)));
+  DFD_HIP_CHECK(hipMemcpy(p.cast_dev, p.cast_host.data(), p.cast_host.size() * sizeof(CastSeg), hipMemcpyHostToDevice));
+  p.bound = true;
+  return 0;
+}
+
+void plan_free(Plan& p) {
+  if (p.cast_dev) { (void)hipFree(p.cast_dev); p.cast_dev = nullptr; }
+}
+
+// ------------------------------------------------------------------ forward / backward
+namespace {
+
+#define DFD_TRY(x) do { if ((x) != 0) return -1; } while (0)
+
+template <typename T>
+struct Run {
+  Plan& p;
+  hipStream_t s;
+  char* ws;
+  const float* P;
+  int tr;
+  float* f(int64_t o) const { return reinterpret_cast<float*>(ws + o); }
+  T* a(int64_t o) const { return reinterpret_cast<T*>(ws + o); }
+  const float* prm(int t) const { return P + p.offs[t]; }
+  Pro pro_bn(const BNL& b, int rpf, const float* gate = nullptr) const {
+    Pro q{};
+    q.scale = f(b.o_scale); q.shift = f(b.o_shift); q.gate = gate; q.rows_per_frame = rpf; q.C = b.C;
+    return q;
+  }
+};
+
+template <typename T>
+int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* P, float* bnb, char* ws,
+                 float* feat, int tr, float mom) {
+  Run<T> r{p, s, ws, P, tr};
+  const float eps = 1e-5f;
+  float* stats = tr ? r.f(p.o_stats) : nullptr;
+  int rows = 0;
+  auto fin = [&](const BNL& b, int64_t count) {
+    return launch_bn_finalize(s, r.f(p.o_stats), rows, count, b.C, r.prm(b.t_w), r.prm(b.t_b), bnb + p.offs[b.t_rm],
+                              bnb + p.offs[b.t_rv], mom, eps, tr != 0, r.f(b.o_mean), r.f(b.o_invstd), r.f(b.o_scale),
+                              r.f(b.o_shift));
+  };
+  DFD_TRY(launch_cast_params<T>(s, P, reinterpret_cast<T*>(ws), p.cast_dev, (int)p.cast_host.size(), p.cast_max));
+  const int64_t F = p.frames;
+  StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3]};
+  DFD_TRY(launch_stem_fwd<T>(s, sg, x, r.prm(p.t_stem), r.a(p.o_ystem), stats, &rows));
+  DFD_TRY(fin(p.bn_stem, F * p.H1 * p.W1));
+  const T* xin = nullptr;
+  for (size_t i = 0; i < p.blocks.size(); ++i) {
+    Block& b = p.blocks[i];
+    const int64_t Min = F * b.hin * b.win, Mout = F * b.hout * b.wout;
+    const int hwo = b.hout * b.wout;
+    const BNL& bn_dw = b.ds ? b.bn1 : b.bn2;  // BN after the depthwise conv
+    DwGeom g{p.frames, b.hin, b.win, b.mid, b.k, b.s, b.k / 2, b.hout, b.wout};
+    if (b.ds) {
+      DFD_TRY(launch_dw_fwd<T>(s, g, r.a(p.o_ystem), r.prm(b.t_dw), r.a(b.o_y2), r.pro_bn(p.bn_stem, b.hin * b.win),
+                               PRO_BN_SILU, stats, &rows));
+    } else {
+      DFD_TRY(launch_pw_gemm<T>(s, xin, r.a(b.pw.o_w), r.a(b.o_y1), nullptr, Min, b.mid, b.cin, PRO_NONE, Pro{},
+                                stats, &rows));
+      DFD_TRY(fin(b.bn1, Min));
+      DFD_TRY(launch_dw_fwd<T>(s, g, r.a(b.o_y1), r.prm(b.t_dw), r.a(b.o_y2), r.pro_bn(b.bn1, b.hin * b.win),
+                               PRO_BN_SILU, stats, &rows));
+    }
+    DFD_TRY(fin(bn_dw, Mout));
+    DFD_TRY(launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid, r.f(p.o_part), p.part_cap,
+                                 r.f(b.o_sq)));
+    DFD_TRY(launch_se_fc_fwd(s, r.f(b.o_sq), r.prm(b.t_se_wr), r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be),
+                             p.frames, b.mid, b.rd, r.f(b.o_rpre), r.f(b.o_gate)));
+    DFD_TRY(launch_pw_gemm<T>(s, r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout, b.cout, b.mid, PRO_BN_SILU_G,
+                              r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats, &rows));
+    DFD_TRY(fin(b.bn3, Mout));
+    DFD_TRY(launch_bn_apply<T>(s, r.a(b.o_y3), r.f(b.bn3.o_scale), r.f(b.bn3.o_shift), b.skip ? xin : nullptr,
+                               r.a(b.o_x), Mout, b.cout));
+    xin = r.a(b.o_x);
+  }
+  const int64_t Mf = F * p.Hf * p.Wf;
+  DFD_TRY(launch_pw_gemm<T>(s, xin, r.a(p.head.o_w), r.a(p.o_yh), nullptr, Mf, kHead, p.head.cin, PRO_NONE, Pro{},
+                            stats, &rows));
+  DFD_TRY(fin(p.bn_head, Mf));
+  DFD_TRY(launch_gap<T>(s, r.a(p.o_yh), r.pro_bn(p.bn_head, p.Hf * p.Wf), p.frames, p.Hf * p.Wf, kHead, feat));
+  return 0;
+}
+
+template <typename T>
+int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat, const float* P,
+                  char* ws, float* G, int tr, int seg_begin, int seg_end, int acc) {
+  Run<T> r{p, s, ws, P, tr};
+  int rows = 0;
+  const int64_t F = p.frames;
+  auto grad = [&](int t) { return G + p.offs[t]; };
+  auto bwd_bn = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out) {
+    in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
+    DFD_TRY(launch_bn_bwd_reduce<T>(s, in, Y, M, b.C, r.f(p.o_stats), &rows));
+    DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), rows, M, b.C, r.prm(b.t_w), r.f(b.o_mean), r.f(b.o_invstd),
+                                   tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
+    DFD_TRY(launch_bn_bwd_apply<T>(s, in, Y, r.f(p.o_coef), out, M, b.C));
+    return 0;
+  };
+  const int nb = (int)p.blocks.size();
+  for (int seg = seg_begin; seg < seg_end; ++seg) {
+    if (seg == 0) {
+      const int64_t Mf = F * p.Hf * p.Wf;
+      const Block& last = p.blocks[nb - 1];
+      BnBwdIn in{};
+      in.bc = dfeat; in.bc_scale = 1.0f / (float)(p.Hf * p.Wf); in.rows_per_frame = p.Hf * p.Wf; in.silu = true;
+      DFD_TRY(bwd_bn(in, p.bn_head, r.a(p.o_yh), Mf, r.a(p.o_gs)));
+      DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(p.head.o_wt), r.a(p.o_gx[(nb - 1) & 1]), nullptr, Mf, p.head.cin,
+                                kHead, PRO_NONE, Pro{}, nullptr, nullptr));
+      DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(last.o_x), Mf, kHead, p.head.cin, PRO_NONE, Pro{},
+                                 r.f(p.o_slab), p.slab_cap, grad(p.head.t_w), acc != 0));
+    } else if (seg <= 7) {
+      const int st = 7 - seg;
+      for (int i = nb - 1; i >= 0; --i) {
+        const Block& b = p.blocks[i];
+        if (b.stage != st) continue;
+        const int64_t Min = F * b.hin * b.win, Mout = F * b.hout * b.wout;
+        const int hwo = b.hout * b.wout;
+        const BNL& bn_dw = b.ds ? b.bn1 : b.bn2;
+        T* gout = r.a(p.o_gx[i & 1]);
+        DwGeom g{p.frames, b.hin, b.win, b.mid, b.k, b.s, b.k / 2, b.hout, b.wout};
+        // BN after the 1x1 projection (no activation)
+        BnBwdIn i3{};
+        i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
+        DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
+        DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout, b.mid, b.cout,
+                                  PRO_NONE, Pro{}, nullptr, nullptr));
+        DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(b.o_y2), Mout, b.cout, b.mid, PRO_BN_SILU_G,
+                                   r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), r.f(p.o_slab), p.slab_cap, grad(b.pwl.t_w),
+                                   acc != 0));
+        // squeeze-excite
+        DFD_TRY(launch_se_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
+                                        r.f(p.o_part), p.part_cap, r.f(p.o_dgate)));
+        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_dgate), r.f(b.o_gate), r.f(b.o_sq), r.f(b.o_rpre), r.prm(b.t_se_wr),
+                                 r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo, r.f(p.o_de), r.f(p.o_dz),
+                                 r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we), grad(b.t_se_be),
+                                 acc != 0));
+        // BN+SiLU after the depthwise conv (input grad = gated path + squeeze path)
+        BnBwdIn i2{};
+        i2.dZ = r.a(p.o_ge2); i2.gate = r.f(b.o_gate); i2.bc = r.f(p.o_bc); i2.bc_scale = 1.f;
+        i2.rows_per_frame = hwo; i2.silu = true;
+        DFD_TRY(bwd_bn(i2, bn_dw, r.a(b.o_y2), Mout, r.a(p.o_ge2)));
+        // depthwise conv
+        DFD_TRY(launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1)));
+        if (b.ds) {
+          DFD_TRY(launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), r.a(p.o_ystem), r.pro_bn(p.bn_stem, b.hin * b.win),
+                                     PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0));
+          // grad of the stem activation stays in ge1 for the stem segment
+        } else {
+          DFD_TRY(launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), r.a(b.o_y1), r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU,
+                                     r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0));
+          BnBwdIn i1{};
+          i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = true;
+          DFD_TRY(bwd_bn(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1)));
+          const T* xin = r.a(p.blocks[i - 1].o_x);
+          DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(b.pw.o_wt), r.a(p.o_gx[(i - 1) & 1]), b.skip ? gout : nullptr,
+                                    Min, b.cin, b.mid, PRO_NONE, Pro{}, nullptr, nullptr));
+          DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{}, r.f(p.o_slab),
+                                     p.slab_cap, grad(b.pw.t_w), acc != 0));
+        }
+      }
+    } else {
+      const int64_t M = F * p.H1 * p.W1;
+      BnBwdIn in{};
+      in.dZ = r.a(p.o_ge1); in.rows_per_frame = p.H1 * p.W1; in.silu = true;
+      DFD_TRY(bwd_bn(in, p.bn_stem, r.a(p.o_ystem), M, r.a(p.o_ge1)));
+      StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3]};
+      DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), r.f(p.o_slab), p.slab_cap, grad(p.t_stem), acc != 0));
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+int plan_forward(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* params, float* bnbuf,
+                 char* ws, float* feat, int training, float momentum) {
+  if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
+  if (p.dtype == 1) return forward_impl<bf16>(p, s, x, xs, params, bnbuf, ws, feat, training, momentum);
+  return forward_impl<float>(p, s, x, xs, params, bnbuf, ws, feat, training, momentum);
+}
+
+int plan_backward_x(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat, const float* params,
+                    char* ws, float* grads, int training, int seg_begin, int seg_end, int accumulate) {
+  if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
+  if (seg_begin < 0 || seg_end > kNumSegments || seg_begin > seg_end) {
+    set_error("backward: bad segment range", __FILE__, __LINE__);
+    return -1;
+  }
+  if (p.dtype == 1)
+    return backward_impl<bf16>(p, s, x, xs, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
+  return backward_impl<float>(p, s, x, xs, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
+}
+
+}  // namespace dfd

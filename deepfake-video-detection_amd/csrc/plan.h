@@ -1,0 +1,82 @@
+// EfficientNet-B0 trunk plan: topology (timm efficientnet_b0), tensor table in
+// timm state_dict order, per-shape workspace layout and the forward/backward launch sequences.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+namespace dfd {
+
+enum TensorKind { TK_PARAM = 0, TK_BNBUF = 1, TK_COUNTER = 2 };
+
+struct TensorSpec {
+  std::string name;  // relative to the trunk Sequential, e.g. "2.1.0.conv_dw.weight"
+  int kind;
+  std::vector<int64_t> shape;
+};
+
+struct BNL {        // one BatchNorm(+act) layer
+  int C;
+  int t_w, t_b, t_rm, t_rv;  // tensor indices
+  int64_t o_mean, o_invstd, o_scale, o_shift;  // workspace byte offsets (fp32 [C] each)
+};
+
+struct PWL {        // one 1x1 conv
+  int cin, cout, t_w;
+  int64_t o_w, o_wt;  // workspace byte offsets of compute-dtype W [cout][cin] and W^T [cin][cout]
+};
+
+struct Block {
+  int ds;           // 1 = DepthwiseSeparable (stage 0), 0 = InvertedResidual
+  int stage, idx;
+  int cin, cout, mid, rd, k, s;
+  int hin, win, hout, wout;
+  bool skip;
+  PWL pw, pwl;      // ds: only pw (32->16) is used, stored in `pwl`
+  BNL bn1, bn2, bn3;  // ds: bn1 after dw, bn3 after pw (bn2 unused)
+  int t_dw, t_se_wr, t_se_br, t_se_we, t_se_be;
+  // workspace byte offsets of saved tensors
+  int64_t o_y1, o_y2, o_y3, o_x, o_sq, o_rpre, o_gate;
+};
+
+struct Plan {
+  int frames, H, W, dtype;
+  int H1, W1, Hf, Wf;  // stem output, final feature map
+  std::vector<TensorSpec> tensors;
+  std::vector<int64_t> offs;  // bound offsets (params: into param flat, bnbufs: into bn flat)
+  bool bound = false;
+  int t_stem;
+  BNL bn_stem, bn_head;
+  PWL head;
+  std::vector<Block> blocks;
+  // workspace
+  int64_t ws_bytes = 0;
+  int64_t o_ystem, o_yh, o_stats, o_slab, o_part, o_coef, o_dgate, o_bc, o_de, o_dz;
+  int64_t o_gx[2], o_gs, o_ge1, o_ge2;
+  int64_t stats_cap, slab_cap, part_cap;
+  // cast table (device copy)
+  std::vector<CastSeg> cast_host;
+  CastSeg* cast_dev = nullptr;
+  int cast_max = 0;
+  int device = 0;
+};
+
+int plan_build(Plan& p, int frames, int H, int W, int dtype);
+int plan_bind(Plan& p, const int64_t* offs, int n);
+void plan_free(Plan& p);
+int plan_forward(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* params, float* bnbuf,
+                 char* ws, float* feat, int training, float momentum);
+int plan_backward_x(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat,
+                    const float* params, char* ws, float* grads, int training, int seg_begin, int seg_end,
+                    int accumulate);
+// segments: 0 = conv_head+bn2, 1..7 = stage 6..0, 8 = stem.  Tensor index range [lo, hi) whose
+// gradients are final once the segment has run.
+void plan_segment_range(const Plan& p, int seg, int* lo, int* hi);
+constexpr int kNumSegments = 9;
+// static topology (shape-independent)
+const std::vector<TensorSpec>& b0_tensor_table();
+
+}  // namespace dfd

@@ -1,0 +1,121 @@
+/*
+ * dfd_hip.h -- C ABI of the MI355X-native EfficientNet-B0 frame-classifier hot path.
+ *
+ * libdfd_hip.so (built from deepfake-video-detection_amd/csrc for gfx950) exports exactly
+ * the functions below.  Every argument is a plain pointer / size; device pointers are HIP
+ * device memory owned by the caller (PyTorch's caching allocator in the Python binding);
+ * `stream` is a hipStream_t passed as void*.  No function allocates device memory on the
+ * launch path, synchronises, or aborts: every entry point returns 0 on success and -1 on
+ * failure, with a message from dfd_last_error() (the Python layer raises RuntimeError,
+ * which the reference's callers turn into error dicts, app.py:2320-2321, detector.py:134-141).
+ *
+ * The reference has no native code; each entry point names the reference
+ * Python call site whose computation it replaces.
+ */
+#ifndef DFD_HIP_H
+#define DFD_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFD_API __attribute__((visibility("default")))
+
+/* dtype codes for the activation storage of the trunk */
+#define DFD_DTYPE_F32 0
+#define DFD_DTYPE_BF16 1
+
+/* tensor kinds reported by dfd_b0_tensor_info */
+#define DFD_TENSOR_PARAM 0   /* trainable fp32 parameter (flat parameter buffer)      */
+#define DFD_TENSOR_BNBUF 1   /* BatchNorm running_mean / running_var (flat BN buffer) */
+#define DFD_TENSOR_COUNTER 2 /* BatchNorm num_batches_tracked (host-managed int64)   */
+
+typedef struct dfd_b0_plan dfd_b0_plan;
+
+/* Last error message of the calling thread ("" if none). */
+DFD_API const char* dfd_last_error(void);
+/* ABI version (major*100 + minor). */
+DFD_API int dfd_version(void);
+
+/* ---- EfficientNet-B0 trunk ------------------------------------------------------------
+ * Replaces timm.create_model('efficientnet_b0') wrapped as
+ * nn.Sequential(*list(backbone.children())[:-1])   (src/pretrained_detector.py:43-46)
+ * and its call self.backbone(x_flat) -> (B*T, 1280)  (src/pretrained_detector.py:116). */
+
+/* Number of trunk tensors, in timm state_dict order (names relative to the Sequential,
+ * e.g. "2.1.0.conv_dw.weight"; the detector prefixes "backbone."). */
+DFD_API int dfd_b0_tensor_count(void);
+/* Name (NUL-terminated, truncated to cap), kind, rank and shape (up to 4 dims) of tensor idx. */
+DFD_API int dfd_b0_tensor_info(int idx, char* name, int cap, int* kind, int* ndim, int64_t* shape4);
+
+/* Shape-specialised plan for `frames` frames of height x width (dtype DFD_DTYPE_*). */
+DFD_API int dfd_b0_plan_create(int frames, int height, int width, int dtype, dfd_b0_plan** out);
+DFD_API void dfd_b0_plan_destroy(dfd_b0_plan* plan);
+/* Bytes of device workspace one forward(+backward) needs (saved activations + scratch). */
+DFD_API int64_t dfd_b0_workspace_bytes(const dfd_b0_plan* plan);
+/* Bind element offsets of every tensor (params: into the fp32 parameter buffer; BN buffers:
+ * into the fp32 BN buffer; counters ignored).  n must equal dfd_b0_tensor_count(). */
+DFD_API int dfd_b0_bind(dfd_b0_plan* plan, const int64_t* offsets, int n);
+/* Forward.  x: fp32 frames, element strides x_strides4 = {frame, channel, row, col} (any
+ * layout; channels-last input is read in place).  training=1 uses batch statistics and
+ * updates running stats with `momentum` (BatchNorm2d train semantics); 0 = eval.
+ * features: fp32 [frames][1280].  The workspace keeps what backward needs. */
+DFD_API int dfd_b0_forward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* x_strides4,
+                           const float* params, float* bn_buffers, void* workspace, float* features,
+                           int training, float momentum);
+/* Backward of the same forward (same workspace).  Runs segments [seg_begin, seg_end) in
+ * reverse network order: 0 = conv_head+bn2, 1..7 = blocks stage 6..0, 8 = stem.  Gradients
+ * are written (accumulate=0) or added (accumulate=1) at the parameter offsets of `grads`. */
+DFD_API int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* x_strides4,
+                            const float* dfeatures, const float* params, void* workspace, float* grads,
+                            int training, int seg_begin, int seg_end, int accumulate);
+DFD_API int dfd_b0_segment_count(void);
+/* Introspection of the activations a forward saved in the workspace (pre-BN conv outputs and
+ * block outputs, NHWC [rows][cols] in the plan dtype): 0 = conv_stem, then per block
+ * (conv_pw (IR only), conv_dw, conv_pwl/conv_pw, block output), last = conv_head.
+ * Returns -1 past the end.  Used by the layer-by-layer parity tests. */
+DFD_API int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* byte_offset, int64_t* rows,
+                                int64_t* cols);
+/* Tensor index range [*lo, *hi) whose gradients are final after segment `seg`. */
+DFD_API int dfd_b0_segment_tensors(int seg, int* lo, int* hi);
+
+/* ---- detector head ---------------------------------------------------------------------
+ * Replaces PretrainedBackboneDetector's temporal attention + classifier
+ * (src/pretrained_detector.py:65-76 construction, :123-141 forward).
+ * params8 / grads8: ta.0.weight, ta.0.bias, ta.2.weight, ta.2.bias, fc1.weight, fc1.bias,
+ * fc2.weight, fc2.bias (fp32).  work: fp32 scratch of dfd_head_work_floats() elements that
+ * must be kept between forward and backward.  Dropout (p) uses a counter hash of `seed`. */
+DFD_API int64_t dfd_head_work_floats(int B, int T, int D, int H, int F1);
+DFD_API int dfd_head_forward(void* stream, int B, int T, int D, int H, int F1, int NC, int use_attn,
+                             const float* const* params8, const float* features, float* work, uint64_t seed,
+                             float p, float* logits, float* frame_scores);
+DFD_API int dfd_head_backward(void* stream, int B, int T, int D, int H, int F1, int NC, int use_attn,
+                              const float* const* params8, const float* features, float* work, uint64_t seed,
+                              float p, const float* frame_scores, const float* dlogits,
+                              const float* dframe_scores, float* dfeatures, float* const* grads8);
+
+/* ---- weighted cross entropy --------------------------------------------------------------
+ * Replaces nn.CrossEntropyLoss(weight=class_weights) (src/ensemble_trainer.py:358,
+ * src/train.py:337): mean of w[y]*nll over non-ignored rows, normalised by sum of w[y]. */
+DFD_API int dfd_ce_forward(void* stream, const float* logits, const int64_t* labels, const float* weight, int B,
+                           int NC, int64_t ignore_index, float* loss, float* wsum);
+DFD_API int dfd_ce_backward(void* stream, const float* logits, const int64_t* labels, const float* weight, int B,
+                            int NC, int64_t ignore_index, const float* wsum, const float* grad_out,
+                            float* dlogits);
+
+/* ---- optimizer ----------------------------------------------------------------------------
+ * Replaces torch.nn.utils.clip_grad_norm_(params, max_norm) (src/ensemble_trainer.py:199) and
+ * optim.AdamW / optim.Adam .step() (src/ensemble_trainer.py:146,200; src/train.py:323,126)
+ * over one flat fp32 buffer.  out2[0] = total norm, out2[1] = clip coefficient.
+ * scratch: >= 8192 bytes of device memory. */
+DFD_API int dfd_grad_norm(void* stream, const float* grads, int64_t n, float max_norm, void* scratch, float* out2);
+DFD_API int dfd_adam_step(void* stream, float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                          double lr, double beta1, double beta2, double eps, double weight_decay, int step,
+                          double grad_scale, int decoupled, const float* clip_out2);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFD_HIP_H */
