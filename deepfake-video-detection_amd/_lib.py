@@ -41,6 +41,9 @@ _SIGS = {
     "dfd_b0_backward": (c_i, [c_p, c_p, c_p, ctypes.POINTER(c_i64), c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i]),
     "dfd_b0_segment_count": (c_i, []),
     "dfd_b0_saved_tensor": (c_i, [c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
+    "dfd_b0_probe_arm": (c_i, [c_p, c_i, c_i, c_i, c_i]),
+    "dfd_b0_probe_read": (c_i, [c_p, ctypes.POINTER(c_f), c_i, ctypes.POINTER(c_i)]),
+    "dfd_b0_probe_disarm": (c_i, [c_p]),
     "dfd_b0_segment_tensors": (c_i, [c_i, ctypes.POINTER(c_i), ctypes.POINTER(c_i)]),
     "dfd_head_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_head_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_fpp, c_p, c_p, c_u64, c_f, c_p, c_p]),

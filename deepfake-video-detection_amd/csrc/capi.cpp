@@ -112,6 +112,20 @@ int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64
 
 int dfd_b0_segment_count(void) { return dfd::kNumSegments; }
 
+int dfd_b0_probe_arm(dfd_b0_plan* plan, int kind, int stage, int idx, int n) {
+  if (!plan || n <= 0) { dfd::set_error("bad probe arguments", __FILE__, __LINE__); return -1; }
+  return dfd::probe_arm(plan->p, kind, stage, idx, n);
+}
+int dfd_b0_probe_read(dfd_b0_plan* plan, float* ms, int cap, int* count) {
+  if (!plan || !ms || !count) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::probe_read(plan->p, ms, cap, count);
+}
+int dfd_b0_probe_disarm(dfd_b0_plan* plan) {
+  if (!plan) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  dfd::probe_disarm(plan->p);
+  return 0;
+}
+
 int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* off, int64_t* rows, int64_t* cols) {
   if (!plan || !off || !rows || !cols) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
   const dfd::Plan& p = plan->p;

@@ -15,14 +15,15 @@ struct bf16 {
   uint16_t x;
 };
 
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  // round-to-nearest-even; NaN stays NaN (quiet bit forced)
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+// hardware round-to-nearest-even (v_cvt_pk_bf16_f32; NaN stays NaN)
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{lo, hi}), bf16x2_t));
 }
+__device__ __forceinline__ uint16_t f2bf(float f) { return (uint16_t)(pack2bf(f, 0.f) & 0xffffu); }
 
 template <typename T> struct Tr;
 template <> struct Tr<float> {
@@ -56,9 +57,6 @@ __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
-__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-}
 __device__ __forceinline__ void st8(bf16* p, const float (&v)[8]) {
   uint4 a;
   a.x = pack2bf(v[0], v[1]); a.y = pack2bf(v[2], v[3]);
@@ -68,7 +66,8 @@ __device__ __forceinline__ void st8(bf16* p, const float (&v)[8]) {
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) { ld8(p, v); }
 
 // ---- activations ----
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp); an IEEE division here costs ~10 VALU ops per element
+__device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float siluf_(float x) { return x * sigmoidf_(x); }
 // d/dx silu(x) = s (1 + x (1 - s))
 __device__ __forceinline__ float dsiluf_(float x) {

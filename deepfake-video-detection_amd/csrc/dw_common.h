@@ -1,0 +1,122 @@
+// Shared pieces of the depthwise-conv kernels (k_dw_fwd.hip, k_dw_dgrad.hip, k_dw_wgrad.hip).
+//
+// Design (HBM-bound op, AI 3-10 flop/B; the first profile showed the kernels VALU-bound, so the
+// per-element instruction count is the second constraint):
+//   * compile-time 2D tiles (TH x TW outputs) x 32 channels per workgroup; tile shapes are
+//     chosen per layer from {16x16, 8x28, 14x14, 8x8, 7x7} to divide the feature map exactly
+//     (the EfficientNet-B0 maps are 112/56/28/14/7) and to fit LDS; all index math uses
+//     compile-time divisors;
+//   * the input tile (+halo) is staged ONCE into LDS as fp32, through the producer's
+//     BatchNorm+SiLU, with every load of the tile issued before the first is used;
+//   * the channel group is the fastest-varying workgroup index (gridDim.x % groups == 0), so
+//     the groups of one pixel run together and their 64-B slices merge into full L2 lines;
+//   * per-channel statistics accumulate in registers across all tiles of a workgroup and are
+//     reduced once (wave shuffles + LDS) into one deterministic partial row.
+#pragma once
+#include "kernels.h"
+
+namespace dfd {
+
+constexpr int DCG = 32;  // channels per workgroup (4 x 8-element vectors)
+
+template <int TH, int TW, int K, int S>
+struct DwT {
+  static constexpr int NPX = TH * TW;                 // output (fwd/wgrad) or input (dgrad) pixels
+  static constexpr int P = (NPX + 63) / 64;           // pixels per thread
+  static constexpr int IH = (TH - 1) * S + K;         // fwd/wgrad input tile
+  static constexpr int IW = (TW - 1) * S + K;
+  static constexpr int NIN = IH * IW;
+  static constexpr int GH = (TH - 1 + K - 1) / S + 2;  // dgrad dY tile (bound)
+  static constexpr int GW = (TW - 1 + K - 1) / S + 2;
+  static constexpr int NG = GH * GW;
+  static constexpr int LDS_FWD = NIN * DCG * 4 + K * K * DCG * 4;
+  static constexpr int LDS_DGRAD = NG * DCG * 4 + K * K * DCG * 4;
+  static constexpr int LDS_WGRAD = (NIN + NPX) * DCG * 4;
+  static constexpr int LDS_CAP = 60 * 1024;
+  static constexpr bool fwd_ok = LDS_FWD <= LDS_CAP && (NIN + 63) / 64 <= 8;
+  static constexpr bool dgrad_ok = LDS_DGRAD <= LDS_CAP && (NG + 63) / 64 <= 8;
+  static constexpr bool wgrad_ok = LDS_WGRAD <= LDS_CAP && (NIN + 63) / 64 <= 8;
+};
+
+__host__ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// Stage an NR x NC pixel window (origin y0, x0; zero outside the map) of channel vector c of
+// a [frames][H][W][C] tensor into fp32 LDS [NR*NC][32] (this thread's 8 channels), applying the
+// producer's BN+SiLU when MODE != PRO_NONE.  All loads are issued before any is consumed.
+template <typename T, int MODE, int NR, int NC>
+__device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src, int f, int y0, int x0, int H, int W,
+                                           int C, int c, bool cok, const float (&sc)[8], const float (&sh)[8]) {
+  constexpr int N = NR * NC;
+  constexpr int NLD = (N + 63) / 64;
+  const int tp = threadIdx.x >> 2, vec = threadIdx.x & 3;
+  float x[NLD][8];
+  bool in[NLD];
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) {
+    const int pix = tp + 64 * i;
+    const int ry = pix / NC, rx = pix - (pix / NC) * NC;
+    const int iy = y0 + ry, ix = x0 + rx;
+    in[i] = pix < N && cok && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    if (in[i]) {
+      ld8(src + (((int64_t)f * H + iy) * W + ix) * C + c, x[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[i][j] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) {
+    const int pix = tp + 64 * i;
+    if (pix < N) {
+      if (MODE != PRO_NONE && in[i]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[i][j] = siluf_(x[i][j] * sc[j] + sh[j]);
+      }
+      st8(dst + pix * DCG + vec * 8, x[i]);
+    }
+  }
+}
+
+// Reduce per-thread 8-channel partials a (sum) and b over all threads with the same vec
+// (wave shuffles, then 4 waves through LDS) and write out[0*C + c0 + ch], out[1*C + c0 + ch].
+__device__ __forceinline__ void reduce_write_stats(float (&a)[8], float (&b)[8], float* red, float* out, int C,
+                                                   int c0) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, vec = tid & 3;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {
+      a[j] += __shfl_xor(a[j], o, 64);
+      b[j] += __shfl_xor(b[j], o, 64);
+    }
+  }
+  __syncthreads();
+  if (lane < 4) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wave * 2 + 0) * DCG + vec * 8 + j] = a[j];
+      red[(wave * 2 + 1) * DCG + vec * 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int ch = tid & 31, which = tid >> 5;
+    const float s = red[(0 * 2 + which) * DCG + ch] + red[(1 * 2 + which) * DCG + ch] +
+                    red[(2 * 2 + which) * DCG + ch] + red[(3 * 2 + which) * DCG + ch];
+    if (c0 + ch < C) out[(int64_t)which * C + c0 + ch] = s;
+  }
+}
+
+// Host: candidate tiles in preference order; pick the first that divides (rows, cols) and
+// fits, else the first that fits (partial tiles are masked).
+struct TileChoice {
+  int th, tw;
+};
+constexpr TileChoice kDwTiles[5] = {{16, 16}, {8, 28}, {14, 14}, {8, 8}, {7, 7}};
+
+static inline int dw_grid(int64_t ntiles, int groups) {
+  const int64_t per_group = std::min<int64_t>(ntiles, std::max<int64_t>(1, 1024 / groups));
+  return (int)(per_group * groups);
+}
+
+}  // namespace dfd

@@ -11,14 +11,18 @@
 namespace dfd {
 
 // ------------------------------------------------------------------ partial-row reduction
-// Sums rows of a [rows][2][C] slab for channels [blockIdx.x*64, +64) in fp64.
+// Sums rows of a [rows][2][C] slab for channels [blockIdx.x*16, +16) in fp64:
+// 1024 threads = 16 channels x 64 row lanes, then a fixed-order LDS tree (deterministic).
+constexpr int FIN_CH = 16;
+constexpr int FIN_RL = 64;
+
 __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int C, double& s, double& q,
                                  double* sh_s, double* sh_q) {
-  const int tid = threadIdx.x, cl = tid & 63, part = tid >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int tid = threadIdx.x, cl = tid % FIN_CH, rl = tid / FIN_CH;
+  const int c = blockIdx.x * FIN_CH + cl;
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int r = part; r < rows; r += 4) {
+    for (int r = rl; r < rows; r += FIN_RL) {
       a += stats[((int64_t)r * 2 + 0) * C + c];
       b += stats[((int64_t)r * 2 + 1) * C + c];
     }
@@ -26,23 +30,28 @@ __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int 
   sh_s[tid] = a;
   sh_q[tid] = b;
   __syncthreads();
-  if (tid < 64) {
-    s = sh_s[tid] + sh_s[tid + 64] + sh_s[tid + 128] + sh_s[tid + 192];
-    q = sh_q[tid] + sh_q[tid + 64] + sh_q[tid + 128] + sh_q[tid + 192];
+  for (int o = FIN_RL / 2; o > 0; o >>= 1) {
+    if (rl < o) {
+      sh_s[tid] += sh_s[tid + o * FIN_CH];
+      sh_q[tid] += sh_q[tid + o * FIN_CH];
+    }
+    __syncthreads();
   }
+  s = sh_s[cl];
+  q = sh_q[cl];
 }
 
-__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
-                                                          int C, const float* __restrict__ gamma,
-                                                          const float* __restrict__ beta, float* run_mean,
-                                                          float* run_var, float momentum, float eps, int training,
-                                                          float* mean, float* invstd, float* scale, float* shift) {
-  __shared__ double sh_s[256], sh_q[256];
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
+                                                           int C, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float* run_mean,
+                                                           float* run_var, float momentum, float eps, int training,
+                                                           float* mean, float* invstd, float* scale, float* shift) {
+  __shared__ double sh_s[1024], sh_q[1024];
   double s = 0.0, q = 0.0;
   if (training) reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
-  const int c = blockIdx.x * 64 + tid;
-  if (tid < 64 && c < C) {
+  const int c = blockIdx.x * FIN_CH + tid;
+  if (tid < FIN_CH && c < C) {
     float mu, is;
     if (training) {
       const double m = s / (double)count;
@@ -70,7 +79,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps, bool training,
                        float* mean, float* invstd, float* scale, float* shift) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, stats, rows, count, C, gamma, beta,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, FIN_CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, beta,
                      run_mean, run_var, momentum, eps, training ? 1 : 0, mean, invstd, scale, shift);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
@@ -216,18 +225,18 @@ int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M
   return 0;
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
                                                               int C, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, int training,
                                                               float* dgamma, float* dbeta, int accumulate,
                                                               float* coef) {
-  __shared__ double sh_s[256], sh_q[256];
+  __shared__ double sh_s[1024], sh_q[1024];
   double s = 0.0, q = 0.0;
   reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
-  const int c = blockIdx.x * 64 + tid;
-  if (tid < 64 && c < C) {
+  const int c = blockIdx.x * FIN_CH + tid;
+  if (tid < FIN_CH && c < C) {
     const float db = (float)s, dg = (float)q;
     if (accumulate) { dbeta[c] += db; dgamma[c] += dg; }
     else { dbeta[c] = db; dgamma[c] = dg; }
@@ -248,7 +257,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
 int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                            const float* mean, const float* invstd, bool training, float* dgamma, float* dbeta,
                            bool accumulate, float* coef) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, 64)), dim3(256), 0, s, stats, rows, count, C, gamma, mean,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, FIN_CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, mean,
                      invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
@@ -469,35 +478,70 @@ __global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* __restrict_
 
 // weight grads: gwe[c][j] = sum_f de[f][c] * silu(rpre[f][j]); gbe[c] = sum_f de[f][c]
 //               gwr[j][c] = sum_f dz[f][j] * sq[f][c];          gbr[j] = sum_f dz[f][j]
+// block = 64 channels x 4 frame lanes; each thread keeps all rd (<= 48) outputs of both
+// products for its channel in registers, frames streamed through LDS in chunks of 64;
+// the 4 frame lanes are summed in a fixed order (deterministic).
+constexpr int SEW_FC = 64;
+constexpr int SEW_RD = 48;
 __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ de, const float* __restrict__ dz,
                                                        const float* __restrict__ sq, const float* __restrict__ rpre,
                                                        int frames, int C, int rd, float* gwr, float* gbr, float* gwe,
                                                        float* gbe, int accumulate) {
-  const int64_t n = (int64_t)C * rd;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    {  // gwe[c][j], i = c*rd + j
-      const int c = (int)(i / rd), j = (int)(i % rd);
-      float a = 0.f;
-      for (int f = 0; f < frames; ++f) a += de[(int64_t)f * C + c] * siluf_(rpre[(int64_t)f * rd + j]);
-      gwe[i] = accumulate ? gwe[i] + a : a;
+  __shared__ float s_r[SEW_FC][SEW_RD];
+  __shared__ float s_dz[SEW_FC][SEW_RD];
+  __shared__ float s_red[4][64][2 * SEW_RD + 1];
+  const int tid = threadIdx.x, cl = tid & 63, fl = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float ae[SEW_RD], ar[SEW_RD], be = 0.f;
+#pragma unroll
+  for (int k = 0; k < SEW_RD; ++k) { ae[k] = 0.f; ar[k] = 0.f; }
+  for (int f0 = 0; f0 < frames; f0 += SEW_FC) {
+    const int nf = min(SEW_FC, frames - f0);
+    __syncthreads();
+    for (int e = tid; e < nf * rd; e += 256) {
+      const int ff = e / rd, j = e - (e / rd) * rd;
+      s_r[ff][j] = siluf_(rpre[(int64_t)(f0 + ff) * rd + j]);
+      s_dz[ff][j] = dz[(int64_t)(f0 + ff) * rd + j];
     }
-    {  // gwr[j][c], i = j*C + c
-      const int j = (int)(i / C), c = (int)(i % C);
-      float a = 0.f;
-      for (int f = 0; f < frames; ++f) a += dz[(int64_t)f * rd + j] * sq[(int64_t)f * C + c];
-      gwr[i] = accumulate ? gwr[i] + a : a;
+    __syncthreads();
+    if (c < C) {
+      for (int ff = fl; ff < nf; ff += 4) {
+        const float d = de[(int64_t)(f0 + ff) * C + c];
+        const float sv = sq[(int64_t)(f0 + ff) * C + c];
+        be += d;
+#pragma unroll
+        for (int k = 0; k < SEW_RD; ++k) {
+          if (k < rd) {
+            ae[k] = fmaf(d, s_r[ff][k], ae[k]);
+            ar[k] = fmaf(s_dz[ff][k], sv, ar[k]);
+          }
+        }
+      }
     }
   }
-  if (i < C) {
-    float a = 0.f;
-    for (int f = 0; f < frames; ++f) a += de[(int64_t)f * C + i];
-    gbe[i] = accumulate ? gbe[i] + a : a;
+#pragma unroll
+  for (int k = 0; k < SEW_RD; ++k) {
+    if (k < rd) { s_red[fl][cl][k] = ae[k]; s_red[fl][cl][SEW_RD + k] = ar[k]; }
   }
-  if (i < rd) {
+  s_red[fl][cl][2 * SEW_RD] = be;
+  __syncthreads();
+  if (fl == 0 && c < C) {
+    for (int k = 0; k < rd; ++k) {
+      const float e = s_red[0][cl][k] + s_red[1][cl][k] + s_red[2][cl][k] + s_red[3][cl][k];
+      const float q = s_red[0][cl][SEW_RD + k] + s_red[1][cl][SEW_RD + k] + s_red[2][cl][SEW_RD + k] +
+                      s_red[3][cl][SEW_RD + k];
+      const int64_t ie = (int64_t)c * rd + k, ir = (int64_t)k * C + c;
+      gwe[ie] = accumulate ? gwe[ie] + e : e;
+      gwr[ir] = accumulate ? gwr[ir] + q : q;
+    }
+    const float b = s_red[0][cl][2 * SEW_RD] + s_red[1][cl][2 * SEW_RD] + s_red[2][cl][2 * SEW_RD] +
+                    s_red[3][cl][2 * SEW_RD];
+    gbe[c] = accumulate ? gbe[c] + b : b;
+  }
+  if (blockIdx.x == 0 && tid < rd) {
     float a = 0.f;
-    for (int f = 0; f < frames; ++f) a += dz[(int64_t)f * rd + i];
-    gbr[i] = accumulate ? gbr[i] + a : a;
+    for (int f = 0; f < frames; ++f) a += dz[(int64_t)f * rd + tid];
+    gbr[tid] = accumulate ? gbr[tid] + a : a;
   }
 }
 
@@ -507,25 +551,34 @@ int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const
   hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(frames), dim3(256), (C + rd) * sizeof(float), s, dgate, gate, rpre, wr,
                      we, C, rd, inv_hw, tmp_de, tmp_dr, bc_out);
   DFD_HIP_CHECK(hipGetLastError());
-  const int64_t n = (int64_t)C * rd;
-  hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv64(std::max<int64_t>(n, C), 256)), dim3(256), 0, s, tmp_de,
+  if (rd > 48) { set_error("se: reduce width > 48 unsupported", __FILE__, __LINE__); return -1; }
+  hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv(C, 64)), dim3(256), 0, s, tmp_de,
                      tmp_dr, sq, rpre, frames, C, rd, gwr, gbr, gwe, gbe, accumulate ? 1 : 0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
 // ------------------------------------------------------------------ slab reduce
-__global__ void reduce_slabs_kernel(const float* __restrict__ slab, int splits, int64_t n, float* out,
-                                    int accumulate) {
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    float a = 0.f;
-    for (int sp = 0; sp < splits; ++sp) a += slab[(int64_t)sp * n + i];
-    out[i] = accumulate ? out[i] + a : a;
+// out[i] (+)= sum_s slab[s][i]; block = 64 consecutive elements x 16 split lanes (fixed order)
+__global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ slab, int splits, int64_t n,
+                                                            float* out, int accumulate) {
+  __shared__ float sh[1024];
+  const int tid = threadIdx.x, il = tid & 63, sl = tid >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + il;
+  float a = 0.f;
+  if (i < n)
+    for (int sp = sl; sp < splits; sp += 16) a += slab[(int64_t)sp * n + i];
+  sh[tid] = a;
+  __syncthreads();
+  for (int o = 8; o > 0; o >>= 1) {
+    if (sl < o) sh[tid] += sh[tid + o * 64];
+    __syncthreads();
   }
+  if (sl == 0 && i < n) out[i] = accumulate ? out[i] + sh[il] : sh[il];
 }
 
 int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate) {
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(ew_grid(n)), dim3(256), 0, s, slab, splits, n, out,
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)cdiv64(n, 64)), dim3(1024), 0, s, slab, splits, n, out,
                      accumulate ? 1 : 0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;

@@ -1,0 +1,159 @@
+// Depthwise conv forward (timm conv_dw; src/pretrained_detector.py:116): NHWC, k = 3/5,
+// s = 1/2, pad k//2, producer BN+SiLU fused into staging, BN-stat partials in the epilogue.
+#include "dw_common.h"
+
+namespace dfd {
+
+template <typename T, int TH, int TW, int K, int S, bool STATS>
+__global__ __launch_bounds__(256) void dw_fwd_kernel(DwGeom g, const T* __restrict__ X, const float* __restrict__ w,
+                                                     T* __restrict__ Y, Pro pro, float* __restrict__ stats, int ntiles,
+                                                     int groups, int tiles_x, int tiles_y) {
+  using D = DwT<TH, TW, K, S>;
+  __shared__ __attribute__((aligned(16))) float tin[D::NIN * DCG];
+  __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];
+  const int tid = threadIdx.x, vec = tid & 3, tp = tid >> 2;
+  const int grp = blockIdx.x % groups;
+  const int c0 = grp * DCG, C = g.C;
+  const int c = c0 + vec * 8;
+  const bool cok = c < C;
+  for (int i = tid; i < K * K * DCG; i += 256) {
+    const int tap = i / DCG, cl = i - tap * DCG;
+    wts[i] = (c0 + cl < C) ? w[(int64_t)(c0 + cl) * K * K + tap] : 0.f;
+  }
+  float sc[8], sh[8];
+  if (cok) {
+    ld8f(pro.scale + c, sc);
+    ld8f(pro.shift + c, sh);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sc[j] = 1.f; sh[j] = 0.f; }
+  }
+  int lofs[D::P], ly[D::P], lx[D::P];
+#pragma unroll
+  for (int i = 0; i < D::P; ++i) {
+    const int p = tp + 64 * i;
+    ly[i] = p / TW;
+    lx[i] = p - (p / TW) * TW;
+    lofs[i] = ((ly[i] * S) * D::IW + lx[i] * S) * DCG + vec * 8;
+  }
+  float st_s[8], st_q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
+  const int tpf = tiles_x * tiles_y;
+  __syncthreads();
+  float wr[K == 3 ? 9 : 1][8];
+  if constexpr (K == 3) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) ld8(wts + t * DCG + vec * 8, wr[t]);
+  }
+  for (int t = blockIdx.x / groups; t < ntiles; t += gridDim.x / groups) {
+    const int f = t / tpf, r = t - (t / tpf) * tpf;
+    const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
+    const int oy0 = ty * TH, ox0 = tx * TW;
+    __syncthreads();
+    stage_tile<T, PRO_BN_SILU, D::IH, D::IW>(tin, X, f, oy0 * S - g.pad, ox0 * S - g.pad, g.H, g.W, C, c, cok, sc,
+                                             sh);
+    __syncthreads();
+    float acc[D::P][8];
+#pragma unroll
+    for (int i = 0; i < D::P; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh) {
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) {
+        float wv[8];
+        if constexpr (K == 3) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) wv[j] = wr[kh * 3 + kw][j];
+        } else {
+          ld8(wts + (kh * K + kw) * DCG + vec * 8, wv);
+        }
+#pragma unroll
+        for (int i = 0; i < D::P; ++i) {
+          if (i == D::P - 1 && tp + 64 * i >= D::NPX) continue;
+          float x[8];
+          ld8(tin + lofs[i] + (kh * D::IW + kw) * DCG, x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(x[j], wv[j], acc[i][j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < D::P; ++i) {
+      const int oy = oy0 + ly[i], ox = ox0 + lx[i];
+      if (tp + 64 * i < D::NPX && oy < g.Ho && ox < g.Wo && cok) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = Tr<T>::round(acc[i][j]);
+        st8(Y + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * C + c, acc[i]);
+        if constexpr (STATS) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { st_s[j] += acc[i][j]; st_q[j] += acc[i][j] * acc[i][j]; }
+        }
+      }
+    }
+  }
+  if constexpr (STATS) reduce_write_stats(st_s, st_q, tin, stats + (int64_t)(blockIdx.x / groups) * 2 * C, C, c0);
+}
+
+template <typename T, int TH, int TW, int K, int S>
+static int fwd_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
+                      int* stat_rows) {
+  if constexpr (!DwT<TH, TW, K, S>::fwd_ok) {
+    set_error("dw fwd: tile does not fit", __FILE__, __LINE__);
+    return -1;
+  } else {
+    const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
+    const int ntiles = g.frames * tiles_x * tiles_y;
+    const int groups = cdiv(g.C, DCG);
+    const int gx = dw_grid(ntiles, groups);
+    if (stats)
+      hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, true>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
+                         ntiles, groups, tiles_x, tiles_y);
+    else
+      hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, false>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
+                         ntiles, groups, tiles_x, tiles_y);
+    if (stat_rows) *stat_rows = gx / groups;
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
+}
+
+template <typename T, int K, int S>
+static int fwd_ks(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
+                  int* stat_rows) {
+  const bool ok[5] = {DwT<16, 16, K, S>::fwd_ok, DwT<8, 28, K, S>::fwd_ok, DwT<14, 14, K, S>::fwd_ok,
+                      DwT<8, 8, K, S>::fwd_ok, DwT<7, 7, K, S>::fwd_ok};
+  int pick = -1;
+  for (int i = 0; i < 5 && pick < 0; ++i)
+    if (ok[i] && g.Ho % kDwTiles[i].th == 0 && g.Wo % kDwTiles[i].tw == 0) pick = i;
+  if (pick < 0) pick = 3;  // 8x8 with masked partial tiles
+  switch (pick) {
+    case 0: return fwd_launch<T, 16, 16, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    case 1: return fwd_launch<T, 8, 28, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    case 2: return fwd_launch<T, 14, 14, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    case 3: return fwd_launch<T, 8, 8, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    default: return fwd_launch<T, 7, 7, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+  }
+}
+
+template <typename T>
+int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, int pro_mode,
+                  float* stats, int* stat_rows) {
+  if (g.C & 7) { set_error("dw: C must be a multiple of 8", __FILE__, __LINE__); return -1; }
+  if (pro_mode != PRO_BN_SILU) { set_error("dw fwd: input must be a BN+SiLU producer", __FILE__, __LINE__); return -1; }
+  if (g.k == 3 && g.s == 1) return fwd_ks<T, 3, 1>(s, g, X, w, Y, pro, stats, stat_rows);
+  if (g.k == 3 && g.s == 2) return fwd_ks<T, 3, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+  if (g.k == 5 && g.s == 1) return fwd_ks<T, 5, 1>(s, g, X, w, Y, pro, stats, stat_rows);
+  if (g.k == 5 && g.s == 2) return fwd_ks<T, 5, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+  set_error("dw: unsupported kernel/stride", __FILE__, __LINE__);
+  return -1;
+}
+
+template int launch_dw_fwd<float>(hipStream_t, const DwGeom&, const float*, const float*, float*, const Pro&, int,
+                                  float*, int*);
+template int launch_dw_fwd<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, int,
+                                 float*, int*);
+
+}  // namespace dfd

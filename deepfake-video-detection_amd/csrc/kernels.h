@@ -27,8 +27,12 @@ struct DwGeom {
 template <typename T>
 int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro,
                   int pro_mode, float* stats, int* stat_rows);
+struct BnBwdIn;
+// dA = dgrad(dY).  With bn != null (fused backward of the producer's BN+SiLU): writes
+// g = dA * silu'(Yp*scale+shift) and per-channel partials of g, g*xhat into stats rows.
 template <typename T>
-int launch_dw_dgrad(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* dX);
+int launch_dw_dgrad(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* out, const T* Yp,
+                    const BnBwdIn* bn, float* stats, int* stat_rows);
 template <typename T>
 int launch_dw_wgrad(hipStream_t s, const DwGeom& g, const T* dY, const T* X, const Pro& pro,
                     int pro_mode, float* slab, int64_t slab_cap, float* dW, bool accumulate);

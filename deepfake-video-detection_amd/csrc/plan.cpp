@@ -224,7 +224,36 @@ int plan_bind(Plan& p, const int64_t* offs, int n) {
   return 0;
 }
 
+void probe_disarm(Plan& p) {
+  for (auto ev : p.probe.b) (void)hipEventDestroy(ev);
+  for (auto ev : p.probe.e) (void)hipEventDestroy(ev);
+  p.probe = Probe{};
+}
+
+int probe_arm(Plan& p, int kind, int stage, int idx, int n) {
+  probe_disarm(p);
+  p.probe.b.resize(n);
+  p.probe.e.resize(n);
+  for (int i = 0; i < n; ++i) {
+    DFD_HIP_CHECK(hipEventCreate(&p.probe.b[i]));
+    DFD_HIP_CHECK(hipEventCreate(&p.probe.e[i]));
+  }
+  p.probe.kind = kind; p.probe.stage = stage; p.probe.idx = idx; p.probe.n = n; p.probe.count = 0;
+  return 0;
+}
+
+int probe_read(Plan& p, float* ms, int cap, int* count) {
+  const int c = std::min(p.probe.count, std::min(p.probe.n, cap));
+  for (int i = 0; i < c; ++i) {
+    DFD_HIP_CHECK(hipEventSynchronize(p.probe.e[i]));
+    DFD_HIP_CHECK(hipEventElapsedTime(&ms[i], p.probe.b[i], p.probe.e[i]));
+  }
+  *count = c;
+  return 0;
+}
+
 void plan_free(Plan& p) {
+  probe_disarm(p);
   if (p.cast_dev) { (void)hipFree(p.cast_dev); p.cast_dev = nullptr; }
 }
 
@@ -232,6 +261,19 @@ void plan_free(Plan& p) {
 namespace {
 
 #define DFD_TRY(x) do { if ((x) != 0) return -1; } while (0)
+
+inline bool probe_hit(const Plan& p, int kind, const Block* b) {
+  return p.probe.kind == kind && p.probe.count < p.probe.n && b && b->stage == p.probe.stage &&
+         b->idx == p.probe.idx;
+}
+// Wrap one launch: PROBED(kind, block, launch-expression)
+#define PROBED(KIND, BLK, EXPR)                                                    \
+  do {                                                                             \
+    const bool _hit = probe_hit(p, KIND, BLK);                                     \
+    if (_hit) (void)hipEventRecord(p.probe.b[p.probe.count], s);                   \
+    DFD_TRY(EXPR);                                                                 \
+    if (_hit) { (void)hipEventRecord(p.probe.e[p.probe.count], s); ++p.probe.count; } \
+  } while (0)
 
 template <typename T>
 struct Run {
@@ -278,19 +320,20 @@ int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, cons
       DFD_TRY(launch_dw_fwd<T>(s, g, r.a(p.o_ystem), r.prm(b.t_dw), r.a(b.o_y2), r.pro_bn(p.bn_stem, b.hin * b.win),
                                PRO_BN_SILU, stats, &rows));
     } else {
-      DFD_TRY(launch_pw_gemm<T>(s, xin, r.a(b.pw.o_w), r.a(b.o_y1), nullptr, Min, b.mid, b.cin, PRO_NONE, Pro{},
-                                stats, &rows));
+      PROBED(PK_PW_FWD, &b, (launch_pw_gemm<T>(s, xin, r.a(b.pw.o_w), r.a(b.o_y1), nullptr, Min, b.mid, b.cin,
+                                               PRO_NONE, Pro{}, stats, &rows)));
       DFD_TRY(fin(b.bn1, Min));
-      DFD_TRY(launch_dw_fwd<T>(s, g, r.a(b.o_y1), r.prm(b.t_dw), r.a(b.o_y2), r.pro_bn(b.bn1, b.hin * b.win),
-                               PRO_BN_SILU, stats, &rows));
+      PROBED(PK_DW_FWD, &b, (launch_dw_fwd<T>(s, g, r.a(b.o_y1), r.prm(b.t_dw), r.a(b.o_y2),
+                                              r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU, stats, &rows)));
     }
     DFD_TRY(fin(bn_dw, Mout));
-    DFD_TRY(launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid, r.f(p.o_part), p.part_cap,
-                                 r.f(b.o_sq)));
+    PROBED(PK_SE_SQUEEZE, &b, (launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
+                                                    r.f(p.o_part), p.part_cap, r.f(b.o_sq))));
     DFD_TRY(launch_se_fc_fwd(s, r.f(b.o_sq), r.prm(b.t_se_wr), r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be),
                              p.frames, b.mid, b.rd, r.f(b.o_rpre), r.f(b.o_gate)));
-    DFD_TRY(launch_pw_gemm<T>(s, r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout, b.cout, b.mid, PRO_BN_SILU_G,
-                              r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats, &rows));
+    PROBED(PK_PWL_FWD, &b, (launch_pw_gemm<T>(s, r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout, b.cout,
+                                              b.mid, PRO_BN_SILU_G, r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats,
+                                              &rows)));
     DFD_TRY(fin(b.bn3, Mout));
     DFD_TRY(launch_bn_apply<T>(s, r.a(b.o_y3), r.f(b.bn3.o_scale), r.f(b.bn3.o_shift), b.skip ? xin : nullptr,
                                r.a(b.o_x), Mout, b.cout));
@@ -315,6 +358,14 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
     in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
     DFD_TRY(launch_bn_bwd_reduce<T>(s, in, Y, M, b.C, r.f(p.o_stats), &rows));
     DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), rows, M, b.C, r.prm(b.t_w), r.f(b.o_mean), r.f(b.o_invstd),
+                                   tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
+    DFD_TRY(launch_bn_bwd_apply<T>(s, in, Y, r.f(p.o_coef), out, M, b.C));
+    return 0;
+  };
+  // BN backward when the partials of g, g*xhat are already in o_stats (written by a fused producer)
+  auto bwd_bn_from_stats = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out, int nrows) {
+    in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
+    DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), nrows, M, b.C, r.prm(b.t_w), r.f(b.o_mean), r.f(b.o_invstd),
                                    tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
     DFD_TRY(launch_bn_bwd_apply<T>(s, in, Y, r.f(p.o_coef), out, M, b.C));
     return 0;
@@ -345,11 +396,11 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         BnBwdIn i3{};
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
         DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
-        DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout, b.mid, b.cout,
-                                  PRO_NONE, Pro{}, nullptr, nullptr));
-        DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(b.o_y2), Mout, b.cout, b.mid, PRO_BN_SILU_G,
-                                   r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), r.f(p.o_slab), p.slab_cap, grad(b.pwl.t_w),
-                                   acc != 0));
+        PROBED(PK_PWL_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout,
+                                                    b.mid, b.cout, PRO_NONE, Pro{}, nullptr, nullptr)));
+        PROBED(PK_PWL_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(b.o_y2), Mout, b.cout, b.mid, PRO_BN_SILU_G,
+                                                     r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), r.f(p.o_slab), p.slab_cap,
+                                                     grad(b.pwl.t_w), acc != 0)));
         // squeeze-excite
         DFD_TRY(launch_se_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
                                         r.f(p.o_part), p.part_cap, r.f(p.o_dgate)));
@@ -363,29 +414,35 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         i2.rows_per_frame = hwo; i2.silu = true;
         DFD_TRY(bwd_bn(i2, bn_dw, r.a(b.o_y2), Mout, r.a(p.o_ge2)));
         // depthwise conv
-        DFD_TRY(launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1)));
-        if (b.ds) {
-          DFD_TRY(launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), r.a(p.o_ystem), r.pro_bn(p.bn_stem, b.hin * b.win),
-                                     PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0));
-          // grad of the stem activation stays in ge1 for the stem segment
-        } else {
-          DFD_TRY(launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), r.a(b.o_y1), r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU,
-                                     r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0));
+        // depthwise dgrad fused with the backward reduction of the producer's BN+SiLU
+        // (stem BN for the stage-0 block, bn1 otherwise): ge1 = g, stats = partials of g, g*xhat
+        const BNL& bn_in = b.ds ? p.bn_stem : b.bn1;
+        const T* y_in = b.ds ? r.a(p.o_ystem) : r.a(b.o_y1);
+        BnBwdIn fz{};
+        fz.mean = r.f(bn_in.o_mean); fz.invstd = r.f(bn_in.o_invstd);
+        fz.scale = r.f(bn_in.o_scale); fz.shift = r.f(bn_in.o_shift); fz.silu = true;
+        PROBED(PK_DW_DGRAD, &b, (launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in, &fz,
+                                                    r.f(p.o_stats), &rows)));
+        p.pending_rows = rows;
+        PROBED(PK_DW_WGRAD, &b, (launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), y_in, r.pro_bn(bn_in, b.hin * b.win),
+                                                    PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0)));
+        if (!b.ds) {
           BnBwdIn i1{};
-          i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = true;
-          DFD_TRY(bwd_bn(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1)));
+          i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = false;
+          DFD_TRY(bwd_bn_from_stats(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1), p.pending_rows));
           const T* xin = r.a(p.blocks[i - 1].o_x);
-          DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(b.pw.o_wt), r.a(p.o_gx[(i - 1) & 1]), b.skip ? gout : nullptr,
-                                    Min, b.cin, b.mid, PRO_NONE, Pro{}, nullptr, nullptr));
-          DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{}, r.f(p.o_slab),
-                                     p.slab_cap, grad(b.pw.t_w), acc != 0));
+          PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(b.pw.o_wt), r.a(p.o_gx[(i - 1) & 1]),
+                                                     b.skip ? gout : nullptr, Min, b.cin, b.mid, PRO_NONE, Pro{},
+                                                     nullptr, nullptr)));
+          PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
+                                                      r.f(p.o_slab), p.slab_cap, grad(b.pw.t_w), acc != 0)));
         }
       }
     } else {
       const int64_t M = F * p.H1 * p.W1;
       BnBwdIn in{};
-      in.dZ = r.a(p.o_ge1); in.rows_per_frame = p.H1 * p.W1; in.silu = true;
-      DFD_TRY(bwd_bn(in, p.bn_stem, r.a(p.o_ystem), M, r.a(p.o_ge1)));
+      in.dZ = r.a(p.o_ge1); in.rows_per_frame = p.H1 * p.W1; in.silu = false;  // ge1 holds g (fused in dw dgrad)
+      DFD_TRY(bwd_bn_from_stats(in, p.bn_stem, r.a(p.o_ystem), M, r.a(p.o_ge1), p.pending_rows));
       StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3]};
       DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), r.f(p.o_slab), p.slab_cap, grad(p.t_stem), acc != 0));
     }

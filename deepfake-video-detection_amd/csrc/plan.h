@@ -42,6 +42,15 @@ struct Block {
   int64_t o_y1, o_y2, o_y3, o_x, o_sq, o_rpre, o_gate;
 };
 
+// Live timing of one launch site inside the plan (HIP events; created when armed, never on the
+// launch path).  kind: see ProbeKind.
+enum ProbeKind { PK_PW_FWD = 0, PK_DW_FWD = 1, PK_PWL_FWD = 2, PK_DW_DGRAD = 3, PK_DW_WGRAD = 4, PK_PW_DGRAD = 5,
+                 PK_PW_WGRAD = 6, PK_PWL_DGRAD = 7, PK_PWL_WGRAD = 8, PK_SE_SQUEEZE = 9, PK_BN_APPLY = 10 };
+struct Probe {
+  int kind = -1, stage = -1, idx = -1, n = 0, count = 0;
+  std::vector<hipEvent_t> b, e;
+};
+
 struct Plan {
   int frames, H, W, dtype;
   int H1, W1, Hf, Wf;  // stem output, final feature map
@@ -62,7 +71,13 @@ struct Plan {
   CastSeg* cast_dev = nullptr;
   int cast_max = 0;
   int device = 0;
+  int pending_rows = 0;  // stat rows written by the stage-0 dw dgrad, consumed by the stem segment
+  Probe probe;
 };
+
+int probe_arm(Plan& p, int kind, int stage, int idx, int n);
+int probe_read(Plan& p, float* ms, int cap, int* count);
+void probe_disarm(Plan& p);
 
 int plan_build(Plan& p, int frames, int H, int W, int dtype);
 int plan_bind(Plan& p, const int64_t* offs, int n);

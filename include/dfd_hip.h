@@ -81,6 +81,14 @@ DFD_API int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* byte_
 /* Tensor index range [*lo, *hi) whose gradients are final after segment `seg`. */
 DFD_API int dfd_b0_segment_tensors(int seg, int* lo, int* hi);
 
+/* Live timing of one launch site (HIP events recorded around it on the launch stream, at most n
+ * times).  kind: 0 conv_pw fwd, 1 conv_dw fwd, 2 conv_pwl fwd, 3 conv_dw dgrad, 4 conv_dw wgrad,
+ * 5 conv_pw dgrad, 6 conv_pw wgrad, 7 conv_pwl dgrad, 8 conv_pwl wgrad, 9 SE squeeze; (stage, idx) =
+ * the MBConv block.  Events are created by arm (not on the launch path); read synchronises on them. */
+DFD_API int dfd_b0_probe_arm(dfd_b0_plan* plan, int kind, int stage, int idx, int n);
+DFD_API int dfd_b0_probe_read(dfd_b0_plan* plan, float* ms, int cap, int* count);
+DFD_API int dfd_b0_probe_disarm(dfd_b0_plan* plan);
+
 /* ---- detector head ---------------------------------------------------------------------
  * Replaces PretrainedBackboneDetector's temporal attention + classifier
  * (src/pretrained_detector.py:65-76 construction, :123-141 forward).
