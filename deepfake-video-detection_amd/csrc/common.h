@@ -65,6 +65,41 @@ __device__ __forceinline__ void st8(bf16* p, const float (&v)[8]) {
 }
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) { ld8(p, v); }
 
+// ---- raw (unconverted) 8-element vectors for register prefetch ----
+// Masked loads are branch-free: the load is always issued (from `safe` when !ok) and the
+// value zero-selected afterwards.  A guarded `if (ok) ld8(...)` compiles to a branch with an
+// s_waitcnt vmcnt(0) per load, which serialises every global round trip of a staging loop.
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16> { uint4 a; };
+template <> struct Raw8<float> { float4 a, b; };
+
+__device__ __forceinline__ void raw_ld(Raw8<bf16>& r, const bf16* p, const bf16* safe, bool ok) {
+  r.a = *reinterpret_cast<const uint4*>(ok ? p : safe);
+  if (!ok) r.a = make_uint4(0u, 0u, 0u, 0u);
+}
+__device__ __forceinline__ void raw_ld(Raw8<float>& r, const float* p, const float* safe, bool ok) {
+  const float* q = ok ? p : safe;
+  r.a = *reinterpret_cast<const float4*>(q);
+  r.b = *reinterpret_cast<const float4*>(q + 4);
+  if (!ok) { r.a = make_float4(0.f, 0.f, 0.f, 0.f); r.b = r.a; }
+}
+__device__ __forceinline__ void raw_to_f(const Raw8<bf16>& r, float (&v)[8]) {
+  v[0] = __uint_as_float(r.a.x << 16); v[1] = __uint_as_float(r.a.x & 0xffff0000u);
+  v[2] = __uint_as_float(r.a.y << 16); v[3] = __uint_as_float(r.a.y & 0xffff0000u);
+  v[4] = __uint_as_float(r.a.z << 16); v[5] = __uint_as_float(r.a.z & 0xffff0000u);
+  v[6] = __uint_as_float(r.a.w << 16); v[7] = __uint_as_float(r.a.w & 0xffff0000u);
+}
+__device__ __forceinline__ void raw_to_f(const Raw8<float>& r, float (&v)[8]) {
+  v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w;
+  v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+}
+__device__ __forceinline__ void raw_st(bf16* p, const Raw8<bf16>& r) { *reinterpret_cast<uint4*>(p) = r.a; }
+__device__ __forceinline__ void raw_st(float* p, const Raw8<float>& r) {
+  *reinterpret_cast<float4*>(p) = r.a;
+  *reinterpret_cast<float4*>(p + 4) = r.b;
+}
+
+
 // ---- activations ----
 // v_exp_f32 + v_rcp_f32 (1 ulp); an IEEE division here costs ~10 VALU ops per element
 __device__ __forceinline__ float sigmoidf_(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -113,6 +148,23 @@ __device__ __forceinline__ void apply_pro8(const Pro& pr, int64_t row, int c0, f
       const int64_t f = row / pr.rows_per_frame;
       float g[8];
       ld8f(pr.gate + f * pr.C + c0, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= g[j];
+    }
+  }
+}
+
+// producer BN+SiLU(+gate) on 8 channels with per-lane preloaded scale/shift; gate row given
+template <int MODE>
+__device__ __forceinline__ void pro8_pre(float (&v)[8], const float (&sc)[8], const float (&sh)[8], const float* gate) {
+  if constexpr (MODE != PRO_NONE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * sc[j] + sh[j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * sigmoidf_(v[j]);
+    if constexpr (MODE == PRO_BN_SILU_G) {
+      float g[8];
+      ld8f(gate, g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] *= g[j];
     }

@@ -3,7 +3,7 @@
 // Design (HBM-bound op, AI 3-10 flop/B; the first profile showed the kernels VALU-bound, so the
 // per-element instruction count is the second constraint):
 //   * compile-time 2D tiles (TH x TW outputs) x 32 channels per workgroup; tile shapes are
-//     chosen per layer from {16x16, 8x28, 14x14, 8x8, 7x7} to divide the feature map exactly
+//     chosen per layer from {16x16, 8x28, 14x14, 14x7, 8x8, 7x7} to divide the feature map exactly
 //     (the EfficientNet-B0 maps are 112/56/28/14/7) and to fit LDS; all index math uses
 //     compile-time divisors;
 //   * the input tile (+halo) is staged ONCE into LDS as fp32, through the producer's
@@ -33,8 +33,10 @@ struct DwT {
   static constexpr int LDS_DGRAD = NG * DCG * 4 + K * K * DCG * 4;
   static constexpr int LDS_WGRAD = (NIN + NPX) * DCG * 4;
   static constexpr int LDS_CAP = 60 * 1024;
-  static constexpr bool fwd_ok = LDS_FWD <= LDS_CAP && (NIN + 63) / 64 <= 8;
-  static constexpr bool dgrad_ok = LDS_DGRAD <= LDS_CAP && (NG + 63) / 64 <= 8;
+  // k5 tiles keep <= 2 pixels per thread (P x 25 taps otherwise exceeds the register budget)
+  static constexpr bool p_ok = K == 3 || P <= 2;
+  static constexpr bool fwd_ok = p_ok && LDS_FWD <= LDS_CAP && (NIN + 63) / 64 <= 8;
+  static constexpr bool dgrad_ok = p_ok && LDS_DGRAD <= LDS_CAP && (NG + 63) / 64 <= 8;
   static constexpr bool wgrad_ok = LDS_WGRAD <= LDS_CAP && (NIN + 63) / 64 <= 8;
 };
 
@@ -49,7 +51,7 @@ __device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src
   constexpr int N = NR * NC;
   constexpr int NLD = (N + 63) / 64;
   const int tp = threadIdx.x >> 2, vec = threadIdx.x & 3;
-  float x[NLD][8];
+  Raw8<T> raw[NLD];
   bool in[NLD];
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
@@ -57,22 +59,19 @@ __device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src
     const int ry = pix / NC, rx = pix - (pix / NC) * NC;
     const int iy = y0 + ry, ix = x0 + rx;
     in[i] = pix < N && cok && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    if (in[i]) {
-      ld8(src + (((int64_t)f * H + iy) * W + ix) * C + c, x[i]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[i][j] = 0.f;
-    }
+    raw_ld(raw[i], src + (((int64_t)f * H + iy) * W + ix) * C + c, src, in[i]);
   }
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
     const int pix = tp + 64 * i;
     if (pix < N) {
-      if (MODE != PRO_NONE && in[i]) {
+      float x[8];
+      raw_to_f(raw[i], x);
+      if (MODE != PRO_NONE) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[i][j] = siluf_(x[i][j] * sc[j] + sh[j]);
+        for (int j = 0; j < 8; ++j) x[j] = in[i] ? siluf_(x[j] * sc[j] + sh[j]) : 0.f;
       }
-      st8(dst + pix * DCG + vec * 8, x[i]);
+      st8(dst + pix * DCG + vec * 8, x);
     }
   }
 }
@@ -112,7 +111,9 @@ __device__ __forceinline__ void reduce_write_stats(float (&a)[8], float (&b)[8],
 struct TileChoice {
   int th, tw;
 };
-constexpr TileChoice kDwTiles[5] = {{16, 16}, {8, 28}, {14, 14}, {8, 8}, {7, 7}};
+constexpr int kNumDwTiles = 6;
+constexpr TileChoice kDwTiles[kNumDwTiles] = {{16, 16}, {8, 28}, {14, 14}, {14, 7}, {8, 8}, {7, 7}};
+constexpr int kDwFallback = 4;  // 8x8
 
 static inline int dw_grid(int64_t ntiles, int groups) {
   const int64_t per_group = std::min<int64_t>(ntiles, std::max<int64_t>(1, 1024 / groups));

@@ -85,85 +85,120 @@ int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t coun
   return 0;
 }
 
+// ------------------------------------------------------------------ elementwise grid
+// "Channel-stationary" grid-stride: the launch uses a block count whose thread total is a
+// multiple of the row width cv (in 8-vectors), so a thread's channel vector -- and every
+// per-channel coefficient it needs -- is loop-invariant and the loop has no division.
+static int ew_grid(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(nvec, 256), 4096)); }
+static int gcd_int(int a, int b) { while (b) { const int t = a % b; a = b; b = t; } return a; }
+static int cs_grid(int64_t nvec, int cv) {
+  const int unit = cv / gcd_int(cv, 256);
+  const int64_t want = std::max<int64_t>(1, std::min<int64_t>(cdiv64(nvec, 256), 4096));
+  return (int)std::max<int64_t>(unit, (want / unit) * unit);
+}
+
 // ------------------------------------------------------------------ BN apply (+ residual)
 template <typename T, bool RES>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ Y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const T* __restrict__ R,
                                                        T* __restrict__ X, int64_t nvec, int cv) {
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)(i % cv) * 8;
-    float y[8], sc[8], sh[8];
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nvec) return;
+  const int64_t step = (int64_t)gridDim.x * 256;  // multiple of cv (cs_grid)
+  const int c = (int)(i % cv) * 8;
+  float sc[8], sh[8];
+  ld8f(scale + c, sc);
+  ld8f(shift + c, sh);
+  for (; i < nvec; i += step) {
+    float y[8];
     ld8(Y + i * 8, y);
-    ld8f(scale + c, sc);
-    ld8f(shift + c, sh);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) y[j] = y[j] * sc[j] + sh[j];
     if constexpr (RES) {
       float r[8];
       ld8(R + i * 8, r);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] += r[j];
+      for (int j = 0; j < 8; ++j) y[j] = y[j] * sc[j] + sh[j] + r[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y[j] = y[j] * sc[j] + sh[j];
     }
     st8(X + i * 8, y);
   }
 }
 
-static int ew_grid(int64_t nvec) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(nvec, 256), 4096)); }
-
 template <typename T>
 int launch_bn_apply(hipStream_t s, const T* Y, const float* scale, const float* shift, const T* R, T* X, int64_t M,
                     int C) {
   const int64_t nvec = M * C / 8;
+  const int gx = cs_grid(nvec, C / 8);
   if (R)
-    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(ew_grid(nvec)), dim3(256), 0, s, Y, scale, shift, R, X, nvec, C / 8);
+    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(gx), dim3(256), 0, s, Y, scale, shift, R, X, nvec, C / 8);
   else
-    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(ew_grid(nvec)), dim3(256), 0, s, Y, scale, shift, R, X, nvec, C / 8);
+    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(gx), dim3(256), 0, s, Y, scale, shift, R, X, nvec, C / 8);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
 // ------------------------------------------------------------------ BN backward
 // g = dA * act'(z),  z = y*scale + shift,  dA = dZ*gate + bc*bc_scale
-template <typename T>
-__device__ __forceinline__ void bn_bwd_g8(const BnBwdIn& in, const T* __restrict__ Y, int64_t row, int c, int C,
-                                          float (&g)[8], float (&y)[8]) {
+// FL: compile-time presence flags of the optional inputs (one kernel instance per combination)
+enum { BF_DZ = 1, BF_GATE = 2, BF_BC = 4, BF_SILU = 8 };
+static int bn_flags(const BnBwdIn& in) {
+  return (in.dZ ? BF_DZ : 0) | (in.gate ? BF_GATE : 0) | (in.bc ? BF_BC : 0) | (in.silu ? BF_SILU : 0);
+}
+
+// per-thread channel constants of the backward
+struct BnBwdCh {
+  float sc[8], sh[8];
+};
+
+template <typename T, int FL>
+__device__ __forceinline__ void bn_bwd_g8(const BnBwdIn& in, const T* __restrict__ Y, int64_t row, uint32_t frame,
+                                          int c, int C, const BnBwdCh& ch, float (&g)[8], float (&y)[8]) {
   ld8(Y + row * C + c, y);
   float da[8];
-  if (in.dZ) {
+  if constexpr ((FL & BF_DZ) != 0) {
     ld8(reinterpret_cast<const T*>(in.dZ) + row * C + c, da);
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) da[j] = 0.f;
   }
-  if (in.gate || in.bc) {
-    const int64_t f = row / in.rows_per_frame;
-    if (in.gate) {
-      float gt[8];
-      ld8f(in.gate + f * C + c, gt);
+  if constexpr ((FL & BF_GATE) != 0) {
+    float gt[8];
+    ld8f(in.gate + (int64_t)frame * C + c, gt);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) da[j] *= gt[j];
-    }
-    if (in.bc) {
-      float b[8];
-      ld8f(in.bc + f * C + c, b);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) da[j] += b[j] * in.bc_scale;
-    }
+    for (int j = 0; j < 8; ++j) da[j] *= gt[j];
   }
-  if (in.silu) {
-    float sc[8], sh[8];
-    ld8f(in.scale + c, sc);
-    ld8f(in.shift + c, sh);
+  if constexpr ((FL & BF_BC) != 0) {
+    float b[8];
+    ld8f(in.bc + (int64_t)frame * C + c, b);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] = da[j] * dsiluf_(y[j] * sc[j] + sh[j]);
+    for (int j = 0; j < 8; ++j) da[j] += b[j] * in.bc_scale;
+  }
+  if constexpr ((FL & BF_SILU) != 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = da[j] * dsiluf_(y[j] * ch.sc[j] + ch.sh[j]);
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = da[j];
   }
 }
 
+template <int FL>
+__device__ __forceinline__ void bn_bwd_ch(const BnBwdIn& in, int c, BnBwdCh& ch) {
+  if constexpr ((FL & BF_SILU) != 0) {
+    ld8f(in.scale + c, ch.sc);
+    ld8f(in.shift + c, ch.sh);
+  }
+}
+
+template <int FL>
+__device__ __forceinline__ uint32_t bn_frame(const BnBwdIn& in, int64_t row) {
+  if constexpr ((FL & (BF_GATE | BF_BC)) != 0) return (uint32_t)row / (uint32_t)in.rows_per_frame;
+  return 0u;
+}
+
 // grid (gx, cdiv(C/8, VPG)); threads: vec = tid % vpg, rl = tid / vpg
-template <typename T>
+template <typename T, int FL>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdIn in, const T* __restrict__ Y, int64_t M, int C,
                                                             float* __restrict__ stats, int vpg) {
   __shared__ float sh[2][256][8];
@@ -175,11 +210,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdIn in, const T*
   for (int j = 0; j < 8; ++j) { as[j] = 0.f; aq[j] = 0.f; }
   if (rl < nrl && c < C) {
     float mu[8], is[8];
+    BnBwdCh ch;
+    bn_bwd_ch<FL>(in, c, ch);
     ld8f(in.mean + c, mu);
     ld8f(in.invstd + c, is);
     for (int64_t r = (int64_t)blockIdx.x * nrl + rl; r < M; r += (int64_t)gridDim.x * nrl) {
       float g[8], y[8];
-      bn_bwd_g8<T>(in, Y, r, c, C, g, y);
+      bn_bwd_g8<T, FL>(in, Y, r, bn_frame<FL>(in, r), c, C, ch, g, y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         as[j] += g[j];
@@ -214,12 +251,18 @@ static void bn_vpg_groups(int C, int& vpg, int& groups) {
 
 template <typename T>
 int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, float* stats, int* stat_rows) {
+  if (M > (int64_t)UINT32_MAX) { set_error("bn: more than 2^32 rows", __FILE__, __LINE__); return -1; }
   int vpg, groups;
   bn_vpg_groups(C, vpg, groups);
   const int nrl = 256 / vpg;
   const int64_t rows_needed = cdiv64(M, nrl * 4);
   const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(rows_needed, std::max(1, 1024 / groups)));
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3(gx, groups), dim3(256), 0, s, in, Y, M, C, stats, vpg);
+  switch (bn_flags(in)) {
+#define DFD_BNR(F) case F: hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, F>), dim3(gx, groups), dim3(256), 0, s, in, Y, M, C, stats, vpg); break;
+    DFD_BNR(0) DFD_BNR(1) DFD_BNR(2) DFD_BNR(3) DFD_BNR(4) DFD_BNR(5) DFD_BNR(6) DFD_BNR(7)
+    DFD_BNR(8) DFD_BNR(9) DFD_BNR(10) DFD_BNR(11) DFD_BNR(12) DFD_BNR(13) DFD_BNR(14) DFD_BNR(15)
+#undef DFD_BNR
+  }
   DFD_HIP_CHECK(hipGetLastError());
   *stat_rows = gx;
   return 0;
@@ -263,18 +306,25 @@ int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t 
   return 0;
 }
 
-template <typename T>
+template <typename T, int FL>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdIn in, const T* __restrict__ Y,
                                                            const float* __restrict__ coef, T* dY, int64_t nvec, int C) {
   const int cv = C / 8;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    const int64_t row = i / cv;
-    const int c = (int)(i - row * cv) * 8;
-    float g[8], y[8], k1[8], k2[8], k3[8];
-    bn_bwd_g8<T>(in, Y, row, c, C, g, y);
-    ld8f(coef + c, k1);
-    ld8f(coef + C + c, k2);
-    ld8f(coef + 2 * C + c, k3);
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nvec) return;
+  const int64_t step = (int64_t)gridDim.x * 256;  // multiple of cv (cs_grid)
+  const int64_t rstep = step / cv;
+  int64_t row = i / cv;
+  const int c = (int)(i - row * cv) * 8;
+  float k1[8], k2[8], k3[8];
+  BnBwdCh ch;
+  bn_bwd_ch<FL>(in, c, ch);
+  ld8f(coef + c, k1);
+  ld8f(coef + C + c, k2);
+  ld8f(coef + 2 * C + c, k3);
+  for (; i < nvec; i += step, row += rstep) {
+    float g[8], y[8];
+    bn_bwd_g8<T, FL>(in, Y, row, bn_frame<FL>(in, row), c, C, ch, g, y);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = k1[j] * g[j] + k2[j] * y[j] + k3[j];
     st8(dY + i * 8, g);
@@ -283,8 +333,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdIn in, const T* 
 
 template <typename T>
 int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const float* coef, T* dY, int64_t M, int C) {
+  if (M > (int64_t)UINT32_MAX) { set_error("bn: more than 2^32 rows", __FILE__, __LINE__); return -1; }
   const int64_t nvec = M * C / 8;
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), dim3(ew_grid(nvec)), dim3(256), 0, s, in, Y, coef, dY, nvec, C);
+  const int gx = cs_grid(nvec, C / 8);
+  switch (bn_flags(in)) {
+#define DFD_BNA(F) case F: hipLaunchKernelGGL((bn_bwd_apply_kernel<T, F>), dim3(gx), dim3(256), 0, s, in, Y, coef, dY, nvec, C); break;
+    DFD_BNA(0) DFD_BNA(1) DFD_BNA(2) DFD_BNA(3) DFD_BNA(4) DFD_BNA(5) DFD_BNA(6) DFD_BNA(7)
+    DFD_BNA(8) DFD_BNA(9) DFD_BNA(10) DFD_BNA(11) DFD_BNA(12) DFD_BNA(13) DFD_BNA(14) DFD_BNA(15)
+#undef DFD_BNA
+  }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -446,7 +503,7 @@ __global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* __restrict_
                                                         const float* __restrict__ rpre, const float* __restrict__ wr,
                                                         const float* __restrict__ we, int C, int rd, float inv_hw,
                                                         float* __restrict__ de_out, float* __restrict__ dz_out,
-                                                        float* __restrict__ bc_out) {
+                                                        float* __restrict__ r_out, float* __restrict__ bc_out) {
   extern __shared__ float sm[];
   float* s_de = sm;      // [C]
   float* s_dz = sm + C;  // [rd]
@@ -463,9 +520,11 @@ __global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* __restrict_
     for (int c = lane; c < C; c += 64) a += we[(int64_t)c * rd + j] * s_de[c];
     a = wave_sum(a);
     if (lane == 0) {
-      const float z = a * dsiluf_(rpre[(int64_t)f * rd + j]);
+      const float rp = rpre[(int64_t)f * rd + j];
+      const float z = a * dsiluf_(rp);
       s_dz[j] = z;
       dz_out[(int64_t)f * rd + j] = z;
+      r_out[(int64_t)f * rd + j] = siluf_(rp);
     }
   }
   __syncthreads();
@@ -476,84 +535,69 @@ __global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* __restrict_
   }
 }
 
-// weight grads: gwe[c][j] = sum_f de[f][c] * silu(rpre[f][j]); gbe[c] = sum_f de[f][c]
-//               gwr[j][c] = sum_f dz[f][j] * sq[f][c];          gbr[j] = sum_f dz[f][j]
-// block = 64 channels x 4 frame lanes; each thread keeps all rd (<= 48) outputs of both
-// products for its channel in registers, frames streamed through LDS in chunks of 64;
-// the 4 frame lanes are summed in a fixed order (deterministic).
-constexpr int SEW_FC = 64;
-constexpr int SEW_RD = 48;
+// weight grads: gwe[c][j] = sum_f de[f][c] * r[f][j]; gbe[c] = sum_f de[f][c]   (r = silu(rpre))
+//               gwr[j][c] = sum_f dz[f][j] * sq[f][c]; gbr[j] = sum_f dz[f][j]
+// One thread per output element, channel fastest: the [f][c] operand is read coalesced and the
+// [f][j] operand is a wave-uniform broadcast; frames are summed in order (deterministic).
 __global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ de, const float* __restrict__ dz,
-                                                       const float* __restrict__ sq, const float* __restrict__ rpre,
+                                                       const float* __restrict__ sq, const float* __restrict__ r,
                                                        int frames, int C, int rd, float* gwr, float* gbr, float* gwe,
                                                        float* gbe, int accumulate) {
-  __shared__ float s_r[SEW_FC][SEW_RD];
-  __shared__ float s_dz[SEW_FC][SEW_RD];
-  __shared__ float s_red[4][64][2 * SEW_RD + 1];
-  const int tid = threadIdx.x, cl = tid & 63, fl = tid >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float ae[SEW_RD], ar[SEW_RD], be = 0.f;
+  const int64_t n_w = (int64_t)C * rd;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const float* a;  // [f][C] operand (stride C)
+  const float* b;  // [f][rd] operand (stride rd), or nullptr for a bias
+  int64_t ai, bi = 0, stride_a, stride_b = rd;
+  float* out;
+  int64_t oi;
+  if (i < n_w) {                      // gwe
+    const int j = (int)(i / C), c = (int)(i - (int64_t)j * C);
+    a = de; ai = c; stride_a = C; b = r; bi = j; out = gwe; oi = (int64_t)c * rd + j;
+  } else if ((i -= n_w) < n_w) {      // gwr
+    const int j = (int)(i / C), c = (int)(i - (int64_t)j * C);
+    a = sq; ai = c; stride_a = C; b = dz; bi = j; out = gwr; oi = (int64_t)j * C + c;
+  } else if ((i -= n_w) < C) {        // gbe
+    a = de; ai = i; stride_a = C; b = nullptr; out = gbe; oi = i;
+  } else if ((i -= C) < rd) {         // gbr
+    a = dz; ai = i; stride_a = rd; b = nullptr; out = gbr; oi = i;
+  } else {
+    return;
+  }
+  float acc = 0.f;
+  if (b) {
+    int f = 0;
+    for (; f + 8 <= frames; f += 8) {
+      float va[8], vb[8];
 #pragma unroll
-  for (int k = 0; k < SEW_RD; ++k) { ae[k] = 0.f; ar[k] = 0.f; }
-  for (int f0 = 0; f0 < frames; f0 += SEW_FC) {
-    const int nf = min(SEW_FC, frames - f0);
-    __syncthreads();
-    for (int e = tid; e < nf * rd; e += 256) {
-      const int ff = e / rd, j = e - (e / rd) * rd;
-      s_r[ff][j] = siluf_(rpre[(int64_t)(f0 + ff) * rd + j]);
-      s_dz[ff][j] = dz[(int64_t)(f0 + ff) * rd + j];
-    }
-    __syncthreads();
-    if (c < C) {
-      for (int ff = fl; ff < nf; ff += 4) {
-        const float d = de[(int64_t)(f0 + ff) * C + c];
-        const float sv = sq[(int64_t)(f0 + ff) * C + c];
-        be += d;
+      for (int u = 0; u < 8; ++u) { va[u] = a[(f + u) * stride_a + ai]; vb[u] = b[(f + u) * stride_b + bi]; }
 #pragma unroll
-        for (int k = 0; k < SEW_RD; ++k) {
-          if (k < rd) {
-            ae[k] = fmaf(d, s_r[ff][k], ae[k]);
-            ar[k] = fmaf(s_dz[ff][k], sv, ar[k]);
-          }
-        }
-      }
+      for (int u = 0; u < 8; ++u) acc = fmaf(va[u], vb[u], acc);
     }
-  }
+    for (; f < frames; ++f) acc = fmaf(a[f * stride_a + ai], b[f * stride_b + bi], acc);
+  } else {
+    int f = 0;
+    for (; f + 8 <= frames; f += 8) {
+      float va[8];
 #pragma unroll
-  for (int k = 0; k < SEW_RD; ++k) {
-    if (k < rd) { s_red[fl][cl][k] = ae[k]; s_red[fl][cl][SEW_RD + k] = ar[k]; }
-  }
-  s_red[fl][cl][2 * SEW_RD] = be;
-  __syncthreads();
-  if (fl == 0 && c < C) {
-    for (int k = 0; k < rd; ++k) {
-      const float e = s_red[0][cl][k] + s_red[1][cl][k] + s_red[2][cl][k] + s_red[3][cl][k];
-      const float q = s_red[0][cl][SEW_RD + k] + s_red[1][cl][SEW_RD + k] + s_red[2][cl][SEW_RD + k] +
-                      s_red[3][cl][SEW_RD + k];
-      const int64_t ie = (int64_t)c * rd + k, ir = (int64_t)k * C + c;
-      gwe[ie] = accumulate ? gwe[ie] + e : e;
-      gwr[ir] = accumulate ? gwr[ir] + q : q;
+      for (int u = 0; u < 8; ++u) va[u] = a[(f + u) * stride_a + ai];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += va[u];
     }
-    const float b = s_red[0][cl][2 * SEW_RD] + s_red[1][cl][2 * SEW_RD] + s_red[2][cl][2 * SEW_RD] +
-                    s_red[3][cl][2 * SEW_RD];
-    gbe[c] = accumulate ? gbe[c] + b : b;
+    for (; f < frames; ++f) acc += a[f * stride_a + ai];
   }
-  if (blockIdx.x == 0 && tid < rd) {
-    float a = 0.f;
-    for (int f = 0; f < frames; ++f) a += dz[(int64_t)f * rd + tid];
-    gbr[tid] = accumulate ? gbr[tid] + a : a;
-  }
+  out[oi] = accumulate ? out[oi] + acc : acc;
 }
 
 int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
                      const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
                      float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
+  float* tmp_r = tmp_dr + (int64_t)frames * rd;  // tmp_dr holds 2 * frames * rd floats
   hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(frames), dim3(256), (C + rd) * sizeof(float), s, dgate, gate, rpre, wr,
-                     we, C, rd, inv_hw, tmp_de, tmp_dr, bc_out);
+                     we, C, rd, inv_hw, tmp_de, tmp_dr, tmp_r, bc_out);
   DFD_HIP_CHECK(hipGetLastError());
-  if (rd > 48) { set_error("se: reduce width > 48 unsupported", __FILE__, __LINE__); return -1; }
-  hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv(C, 64)), dim3(256), 0, s, tmp_de,
-                     tmp_dr, sq, rpre, frames, C, rd, gwr, gbr, gwe, gbe, accumulate ? 1 : 0);
+  const int64_t n = 2 * (int64_t)C * rd + C + rd;
+  hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, tmp_de, tmp_dr, sq, tmp_r,
+                     frames, C, rd, gwr, gbr, gwe, gbe, accumulate ? 1 : 0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

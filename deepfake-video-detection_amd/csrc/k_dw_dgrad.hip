@@ -8,7 +8,7 @@
 namespace dfd {
 
 template <typename T, int TH, int TW, int K, int S>
-__global__ __launch_bounds__(256) void dw_dgrad_kernel(DwGeom g, const T* __restrict__ dY, const float* __restrict__ w,
+__global__ __launch_bounds__(256, 2) void dw_dgrad_kernel(DwGeom g, const T* __restrict__ dY, const float* __restrict__ w,
                                                        T* __restrict__ out, const T* __restrict__ Yp, BnBwdIn bn,
                                                        float* __restrict__ stats, int ntiles, int groups, int tiles_x,
                                                        int tiles_y) {
@@ -51,6 +51,14 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(DwGeom g, const T* __rest
     const int gy0 = floordiv(iy0 + g.pad - (K - 1), S), gx0 = floordiv(ix0 + g.pad - (K - 1), S);
     __syncthreads();
     stage_tile<T, PRO_NONE, D::GH, D::GW>(tg, dY, f, gy0, gx0, g.Ho, g.Wo, C, c, cok, one, zero);
+    // producer pre-BN values of this thread's pixels (masked loads, in flight during the taps)
+    Raw8<T> ryp[D::P];
+#pragma unroll
+    for (int i = 0; i < D::P; ++i) {
+      const int iy = iy0 + ly[i], ix = ix0 + lx[i];
+      const bool ok = tp + 64 * i < D::NPX && iy < g.H && ix < g.W && cok;
+      raw_ld(ryp[i], Yp + (((int64_t)f * g.H + iy) * g.W + ix) * C + c, Yp, ok);
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < D::P; ++i) {
@@ -59,7 +67,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(DwGeom g, const T* __rest
       float acc[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-#pragma unroll
+#pragma unroll 1
       for (int kh = 0; kh < K; ++kh) {
         const int tyv = iy + g.pad - kh;
         if (S == 2 && (tyv & 1)) continue;
@@ -78,7 +86,7 @@ __global__ __launch_bounds__(256) void dw_dgrad_kernel(DwGeom g, const T* __rest
       }
       const int64_t o = (((int64_t)f * g.H + iy) * g.W + ix) * C + c;
       float y[8];
-      ld8(Yp + o, y);
+      raw_to_f(ryp[i], y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gg = Tr<T>::round(acc[j] * dsiluf_(y[j] * sc[j] + sh[j]));
@@ -114,17 +122,18 @@ static int dgrad_launch(hipStream_t s, const DwGeom& g, const T* dY, const float
 template <typename T, int K, int S>
 static int dgrad_ks(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* out, const T* Yp,
                     const BnBwdIn& bn, float* stats, int* stat_rows) {
-  const bool ok[5] = {DwT<16, 16, K, S>::dgrad_ok, DwT<8, 28, K, S>::dgrad_ok, DwT<14, 14, K, S>::dgrad_ok,
-                      DwT<8, 8, K, S>::dgrad_ok, DwT<7, 7, K, S>::dgrad_ok};
+  const bool ok[kNumDwTiles] = {DwT<16, 16, K, S>::dgrad_ok, DwT<8, 28, K, S>::dgrad_ok, DwT<14, 14, K, S>::dgrad_ok,
+                                DwT<14, 7, K, S>::dgrad_ok, DwT<8, 8, K, S>::dgrad_ok, DwT<7, 7, K, S>::dgrad_ok};
   int pick = -1;
-  for (int i = 0; i < 5 && pick < 0; ++i)
+  for (int i = 0; i < kNumDwTiles && pick < 0; ++i)
     if (ok[i] && g.H % kDwTiles[i].th == 0 && g.W % kDwTiles[i].tw == 0) pick = i;
-  if (pick < 0) pick = 3;
+  if (pick < 0) pick = kDwFallback;
   switch (pick) {
     case 0: return dgrad_launch<T, 16, 16, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
     case 1: return dgrad_launch<T, 8, 28, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
     case 2: return dgrad_launch<T, 14, 14, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
-    case 3: return dgrad_launch<T, 8, 8, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
+    case 3: return dgrad_launch<T, 14, 7, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
+    case 4: return dgrad_launch<T, 8, 8, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
     default: return dgrad_launch<T, 7, 7, K, S>(s, g, dY, w, out, Yp, bn, stats, stat_rows);
   }
 }

@@ -5,7 +5,7 @@
 namespace dfd {
 
 template <typename T, int TH, int TW, int K, int S, bool STATS>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(DwGeom g, const T* __restrict__ X, const float* __restrict__ w,
+__global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __restrict__ X, const float* __restrict__ w,
                                                      T* __restrict__ Y, Pro pro, float* __restrict__ stats, int ntiles,
                                                      int groups, int tiles_x, int tiles_y) {
   using D = DwT<TH, TW, K, S>;
@@ -40,12 +40,6 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwGeom g, const T* __restri
 #pragma unroll
   for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
   const int tpf = tiles_x * tiles_y;
-  __syncthreads();
-  float wr[K == 3 ? 9 : 1][8];
-  if constexpr (K == 3) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) ld8(wts + t * DCG + vec * 8, wr[t]);
-  }
   for (int t = blockIdx.x / groups; t < ntiles; t += gridDim.x / groups) {
     const int f = t / tpf, r = t - (t / tpf) * tpf;
     const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
@@ -59,17 +53,14 @@ __global__ __launch_bounds__(256) void dw_fwd_kernel(DwGeom g, const T* __restri
     for (int i = 0; i < D::P; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
-#pragma unroll
+    // taps: one kernel row per iteration (not unrolled) keeps the live registers to
+    // P x 8 accumulators + one row of inputs; every weight read is a 16-lane LDS broadcast
+#pragma unroll 1
     for (int kh = 0; kh < K; ++kh) {
 #pragma unroll
       for (int kw = 0; kw < K; ++kw) {
         float wv[8];
-        if constexpr (K == 3) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) wv[j] = wr[kh * 3 + kw][j];
-        } else {
-          ld8(wts + (kh * K + kw) * DCG + vec * 8, wv);
-        }
+        ld8(wts + (kh * K + kw) * DCG + vec * 8, wv);
 #pragma unroll
         for (int i = 0; i < D::P; ++i) {
           if (i == D::P - 1 && tp + 64 * i >= D::NPX) continue;
@@ -123,17 +114,18 @@ static int fwd_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w
 template <typename T, int K, int S>
 static int fwd_ks(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                   int* stat_rows) {
-  const bool ok[5] = {DwT<16, 16, K, S>::fwd_ok, DwT<8, 28, K, S>::fwd_ok, DwT<14, 14, K, S>::fwd_ok,
-                      DwT<8, 8, K, S>::fwd_ok, DwT<7, 7, K, S>::fwd_ok};
+  const bool ok[kNumDwTiles] = {DwT<16, 16, K, S>::fwd_ok, DwT<8, 28, K, S>::fwd_ok, DwT<14, 14, K, S>::fwd_ok,
+                                DwT<14, 7, K, S>::fwd_ok, DwT<8, 8, K, S>::fwd_ok, DwT<7, 7, K, S>::fwd_ok};
   int pick = -1;
-  for (int i = 0; i < 5 && pick < 0; ++i)
+  for (int i = 0; i < kNumDwTiles && pick < 0; ++i)
     if (ok[i] && g.Ho % kDwTiles[i].th == 0 && g.Wo % kDwTiles[i].tw == 0) pick = i;
-  if (pick < 0) pick = 3;  // 8x8 with masked partial tiles
+  if (pick < 0) pick = kDwFallback;  // 8x8 with masked partial tiles
   switch (pick) {
     case 0: return fwd_launch<T, 16, 16, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
     case 1: return fwd_launch<T, 8, 28, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
     case 2: return fwd_launch<T, 14, 14, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
-    case 3: return fwd_launch<T, 8, 8, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    case 3: return fwd_launch<T, 14, 7, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    case 4: return fwd_launch<T, 8, 8, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
     default: return fwd_launch<T, 7, 7, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
   }
 }

@@ -8,7 +8,7 @@
 namespace dfd {
 
 template <typename T, int TH, int TW, int K, int S>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(DwGeom g, const T* __restrict__ dY, const T* __restrict__ X,
+__global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwGeom g, const T* __restrict__ dY, const T* __restrict__ X,
                                                        Pro pro, float* __restrict__ slab, int ntiles, int groups,
                                                        int tiles_x, int tiles_y) {
   using D = DwT<TH, TW, K, S>;
@@ -101,17 +101,18 @@ static int wgrad_launch(hipStream_t s, const DwGeom& g, const T* dY, const T* X,
 template <typename T, int K, int S>
 static int wgrad_ks(hipStream_t s, const DwGeom& g, const T* dY, const T* X, const Pro& pro, float* slab,
                     int64_t slab_cap, float* dW, bool accumulate) {
-  const bool ok[5] = {DwT<16, 16, K, S>::wgrad_ok, DwT<8, 28, K, S>::wgrad_ok, DwT<14, 14, K, S>::wgrad_ok,
-                      DwT<8, 8, K, S>::wgrad_ok, DwT<7, 7, K, S>::wgrad_ok};
+  const bool ok[kNumDwTiles] = {DwT<16, 16, K, S>::wgrad_ok, DwT<8, 28, K, S>::wgrad_ok, DwT<14, 14, K, S>::wgrad_ok,
+                                DwT<14, 7, K, S>::wgrad_ok, DwT<8, 8, K, S>::wgrad_ok, DwT<7, 7, K, S>::wgrad_ok};
   int pick = -1;
-  for (int i = 0; i < 5 && pick < 0; ++i)
+  for (int i = 0; i < kNumDwTiles && pick < 0; ++i)
     if (ok[i] && g.Ho % kDwTiles[i].th == 0 && g.Wo % kDwTiles[i].tw == 0) pick = i;
-  if (pick < 0) pick = 3;
+  if (pick < 0) pick = kDwFallback;
   switch (pick) {
     case 0: return wgrad_launch<T, 16, 16, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
     case 1: return wgrad_launch<T, 8, 28, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
     case 2: return wgrad_launch<T, 14, 14, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
-    case 3: return wgrad_launch<T, 8, 8, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
+    case 3: return wgrad_launch<T, 14, 7, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
+    case 4: return wgrad_launch<T, 8, 8, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
     default: return wgrad_launch<T, 7, 7, K, S>(s, g, dY, X, pro, slab, slab_cap, dW, accumulate);
   }
 }

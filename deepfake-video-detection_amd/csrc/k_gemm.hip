@@ -58,6 +58,34 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
     for (int i = tid; i < GBN; i += 256) { st_sum[i] = 0.f; st_sq[i] = 0.f; }
   }
 
+  // staging: this thread owns rows srow, srow + 64 and k-vector skc of each 128 x 32 A/B step
+  const int srow = tid >> 2, skc = (tid & 3) * 8;
+  Raw8<T> ra[2], rb[2];
+  float psc[8], psh[8], pg[MODE == PRO_BN_SILU_G ? 2 : 1][8];
+  auto load = [&](int64_t m0, int k0) {
+    const int gk = k0 + skc;
+    const bool kok = gk < K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t gm = m0 + srow + 64 * i;
+      raw_ld(ra[i], A + gm * K + gk, A, gm < M && kok);
+      raw_ld(rb[i], B + (int64_t)(n0 + srow + 64 * i) * K + gk, B, srow + 64 * i < nvalid && kok);
+    }
+    if constexpr (MODE != PRO_NONE) {
+      const int kc = kok ? gk : 0;
+      ld8f(pro.scale + kc, psc);
+      ld8f(pro.shift + kc, psh);
+      if constexpr (MODE == PRO_BN_SILU_G) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int64_t gm = m0 + srow + 64 * i;
+          const uint32_t f = (uint32_t)(gm < M ? gm : m0) / (uint32_t)pro.rows_per_frame;
+          ld8f(pro.gate + (int64_t)f * pro.C + kc, pg[i]);
+        }
+      }
+    }
+  };
+
   for (int64_t mt = blockIdx.x; mt < tiles_m; mt += gridDim.x) {
     const int64_t m0 = mt * GBM;
     f32x4_t acc[2][8];
@@ -66,55 +94,47 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
 #pragma unroll
       for (int b = 0; b < 8; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+    load(m0, 0);
     for (int k0 = 0; k0 < K; k0 += GBK) {
-      // ---- stage A (with the consumer-side BN/SiLU/gate prologue) and B ----
+      // ---- registers -> LDS (A through the consumer-side BN/SiLU/gate prologue) ----
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int v = tid + 256 * i;
-        const int row = v >> 2, kc = (v & 3) * 8;
-        const int64_t gm = m0 + row;
-        const int gk = k0 + kc;
-        float x[8];
-        if (gm < M && gk < K) {
-          ld8(A + gm * K + gk, x);
-          apply_pro8<MODE>(pro, gm, gk, x);
+        const int row = srow + 64 * i;
+        if constexpr (MODE == PRO_NONE) {
+          raw_st(As + row * G::AS + skc, ra[i]);
         } else {
+          float x[8];
+          raw_to_f(ra[i], x);
+          if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = 0.f;
+            for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]) * pg[i][j];
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]);
+          }
+          const bool ok = m0 + row < M && k0 + skc < K;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = ok ? x[j] : 0.f;
+          lds_st8(As + row * G::AS + skc, x);
         }
-        lds_st8(As + row * G::AS + kc, x);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int v = tid + 256 * i;
-        const int row = v >> 2, kc = (v & 3) * 8;
-        const int gk = k0 + kc;
-        float x[8];
-        if (row < nvalid && gk < K) {
-          ld8(B + (int64_t)(n0 + row) * K + gk, x);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = 0.f;
-        }
-        lds_st8(Bs + row * G::AS + kc, x);
+        raw_st(Bs + row * G::AS + skc, rb[i]);
       }
       __syncthreads();
-      // ---- MFMA ----
+      if (k0 + GBK < K) load(m0, k0 + GBK);
+      // ---- MFMA (partial N tiles are zero padded: the sequence is unconditional) ----
       if constexpr (sizeof(T) == 2) {
         bf16x8_t af[2];
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-          af[rb] = *reinterpret_cast<const bf16x8_t*>(As + (wave * 32 + rb * 16 + (lane & 15)) * G::AS +
-                                                      8 * (lane >> 4));
+        for (int rb_ = 0; rb_ < 2; ++rb_)
+          af[rb_] = *reinterpret_cast<const bf16x8_t*>(As + (wave * 32 + rb_ * 16 + (lane & 15)) * G::AS +
+                                                       8 * (lane >> 4));
 #pragma unroll
         for (int cb = 0; cb < 8; ++cb) {
-          if (cb < nb) {
-            const bf16x8_t bfr =
-                *reinterpret_cast<const bf16x8_t*>(Bs + (cb * 16 + (lane & 15)) * G::AS + 8 * (lane >> 4));
+          const bf16x8_t bfr =
+              *reinterpret_cast<const bf16x8_t*>(Bs + (cb * 16 + (lane & 15)) * G::AS + 8 * (lane >> 4));
 #pragma unroll
-            for (int rb = 0; rb < 2; ++rb)
-              acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rb], bfr, acc[rb][cb], 0, 0, 0);
-          }
+          for (int rb_ = 0; rb_ < 2; ++rb_)
+            acc[rb_][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rb_], bfr, acc[rb_][cb], 0, 0, 0);
         }
       } else {
 #pragma unroll
@@ -124,11 +144,9 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
           const float a1 = reinterpret_cast<const float*>(As)[(wave * 32 + 16 + (lane & 15)) * G::AS + kk];
 #pragma unroll
           for (int cb = 0; cb < 8; ++cb) {
-            if (cb < nb) {
-              const float b = reinterpret_cast<const float*>(Bs)[(cb * 16 + (lane & 15)) * G::AS + kk];
-              acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][cb], 0, 0, 0);
-              acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][cb], 0, 0, 0);
-            }
+            const float b = reinterpret_cast<const float*>(Bs)[(cb * 16 + (lane & 15)) * G::AS + kk];
+            acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][cb], 0, 0, 0);
+            acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][cb], 0, 0, 0);
           }
         }
       }
@@ -194,6 +212,7 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
                    const Pro& pro, float* stats, int* stat_rows) {
   if (M <= 0) return 0;
   if ((N & 7) || (K & 7)) { set_error("pw_gemm: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
+  if (M > (int64_t)UINT32_MAX) { set_error("pw_gemm: M exceeds 2^32 rows", __FILE__, __LINE__); return -1; }
   const int ntn = cdiv(N, GBN);
   const int64_t tiles_m = cdiv64(M, GBM);
   const int64_t cap = std::max<int64_t>(1, 1024 / ntn);
@@ -222,7 +241,9 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
 // wgrad: dW[N][K] = sum_m dY[m][n] * pro(X)[m][k].  Output tile 64x64 per workgroup; each of the
 // 4 waves streams its own 32-row m-steps through a private LDS region (no block barrier in the
 // loop) and the MFMA operands are COLUMN reads of the row-major tiles: ds_read_b64_tr_b16 in
-// bf16 mode (two per 8-deep fragment), ds_read_b32 in fp32 mode.
+// bf16 mode (two per 8-deep fragment), ds_read_b32 in fp32 mode.  The global loads of m-step
+// i+1 are issued (branch-free, masked) before the MFMAs of step i; partial tiles are zero
+// padded so the MFMA sequence is unconditional.
 constexpr int WT = 64;
 constexpr int WMS = 32;
 
@@ -233,7 +254,7 @@ template <typename T> struct WgCfg {
 };
 
 template <typename T, int MODE>
-__global__ __launch_bounds__(256) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 : 2) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
                                                        int N, int K, Pro pro, float* __restrict__ slab, int tnk,
                                                        int64_t m_per_split) {
   using G = WgCfg<T>;
@@ -242,11 +263,35 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const T* __restrict__ dY,
   const int tn = blockIdx.x / tnk, tk = blockIdx.x - tn * tnk;
   const int n0 = tn * WT, k0 = tk * WT;
   const int nv = min(WT, N - n0), kv = min(WT, K - k0);
-  const int nbn = (nv + 15) >> 4, nbk = (kv + 15) >> 4;
   const int64_t mbeg = (int64_t)blockIdx.y * m_per_split;
   const int64_t mend = min(M, mbeg + m_per_split);
   T* Ys = reinterpret_cast<T*>(smem + wave * G::WAVE_BYTES);
   T* Xs = Ys + WMS * G::LS;
+
+  // this lane stages column vector cv of rows rl + 8 i (i < 4) of every m-step
+  const int cv = (lane & 7) * 8, rl = lane >> 3;
+  const bool yc = cv < nv, xc = cv < kv;
+  const int kc = k0 + (xc ? cv : 0);
+  float sc[8], sh[8];
+  if constexpr (MODE != PRO_NONE) {
+    ld8f(pro.scale + kc, sc);
+    ld8f(pro.shift + kc, sh);
+  }
+  Raw8<T> ry[4], rx[4];
+  float rg[MODE == PRO_BN_SILU_G ? 4 : 1][8];
+  auto load = [&](int64_t ms) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t gm = ms + rl + 8 * i;
+      const bool ok = gm < mend;
+      raw_ld(ry[i], dY + gm * N + n0 + cv, dY, ok && yc);
+      raw_ld(rx[i], X + gm * K + k0 + cv, X, ok && xc);
+      if constexpr (MODE == PRO_BN_SILU_G) {
+        const uint32_t f = (uint32_t)(ok ? gm : mbeg) / (uint32_t)pro.rows_per_frame;
+        ld8f(pro.gate + (int64_t)f * pro.C + kc, rg[i]);
+      }
+    }
+  };
 
   f32x4_t acc[4][4];
 #pragma unroll
@@ -254,56 +299,54 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const T* __restrict__ dY,
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  for (int64_t ms = mbeg + wave * WMS; ms < mend; ms += 4 * WMS) {
+  int64_t ms = mbeg + wave * WMS;
+  if (ms < mend) load(ms);
+  for (; ms < mend; ms += 4 * WMS) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int slot = lane + 64 * i;
-      const int row = slot >> 3, cv = (slot & 7) * 8;
-      const int64_t gm = ms + row;
-      float y[8], x[8];
-      if (gm < mend && cv < nv) {
-        ld8(dY + gm * N + n0 + cv, y);
+      const int row = rl + 8 * i;
+      raw_st(Ys + row * G::LS + cv, ry[i]);
+      if constexpr (MODE == PRO_NONE) {
+        raw_st(Xs + row * G::LS + cv, rx[i]);
       } else {
+        float x[8];
+        raw_to_f(rx[i], x);
+        if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] = 0.f;
-      }
-      if (gm < mend && cv < kv) {
-        ld8(X + gm * K + k0 + cv, x);
-        apply_pro8<MODE>(pro, gm, k0 + cv, x);
-      } else {
+          for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * rg[i][j];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = 0.f;
+          for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]);
+        }
+        const bool ok = ms + row < mend && xc;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = ok ? x[j] : 0.f;
+        lds_st8(Xs + row * G::LS + cv, x);
       }
-      lds_st8(Ys + row * G::LS + cv, y);
-      lds_st8(Xs + row * G::LS + cv, x);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    if (ms + 4 * WMS < mend) load(ms + 4 * WMS);
     if constexpr (sizeof(T) == 2) {
       const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
       bf16x8_t bfr[4];
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
-        if (kb < nbk) {
-          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(Xs + (8 * g + q) * G::LS + kb * 16 + 4 * p));
-          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(Xs + (8 * g + 4 + q) * G::LS + kb * 16 + 4 * p));
-          bfr[kb] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
+        const s16x4_t lo =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Xs + (8 * g + q) * G::LS + kb * 16 + 4 * p));
+        const s16x4_t hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Xs + (8 * g + 4 + q) * G::LS + kb * 16 + 4 * p));
+        bfr[kb] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int nb_ = 0; nb_ < 4; ++nb_) {
-        if (nb_ < nbn) {
-          const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(Ys + (8 * g + q) * G::LS + nb_ * 16 + 4 * p));
-          const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_s16x4_t*)(Ys + (8 * g + 4 + q) * G::LS + nb_ * 16 + 4 * p));
-          const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const s16x4_t lo =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Ys + (8 * g + q) * G::LS + nb_ * 16 + 4 * p));
+        const s16x4_t hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Ys + (8 * g + 4 + q) * G::LS + nb_ * 16 + 4 * p));
+        const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
-            if (kb < nbk) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kb], acc[nb_][kb], 0, 0, 0);
-        }
+        for (int kb = 0; kb < 4; ++kb) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kb], acc[nb_][kb], 0, 0, 0);
       }
     } else {
       const float* Yf = reinterpret_cast<const float*>(Ys);
@@ -316,31 +359,31 @@ __global__ __launch_bounds__(256) void pw_wgrad_kernel(const T* __restrict__ dY,
         for (int kb = 0; kb < 4; ++kb) bv[kb] = Xf[mm * G::LS + kb * 16 + (lane & 15)];
 #pragma unroll
         for (int nb_ = 0; nb_ < 4; ++nb_) {
-          if (nb_ < nbn) {
-            const float av = Yf[mm * G::LS + nb_ * 16 + (lane & 15)];
+          const float av = Yf[mm * G::LS + nb_ * 16 + (lane & 15)];
 #pragma unroll
-            for (int kb = 0; kb < 4; ++kb)
-              if (kb < nbk) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kb], acc[nb_][kb], 0, 0, 0);
-          }
+          for (int kb = 0; kb < 4; ++kb) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kb], acc[nb_][kb], 0, 0, 0);
         }
       }
     }
     __builtin_amdgcn_wave_barrier();
   }
-  // ---- cross-wave reduction of the 64x64 tile ----
-  __syncthreads();
+  // ---- cross-wave reduction of the 64x64 tile, waves added in a fixed order (deterministic) ----
   float* red = reinterpret_cast<float*>(smem);
-  for (int i = tid; i < WT * WT; i += 256) red[i] = 0.f;
-  __syncthreads();
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wave == w) {
 #pragma unroll
-  for (int nb_ = 0; nb_ < 4; ++nb_)
+      for (int nb_ = 0; nb_ < 4; ++nb_)
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int nn = nb_ * 16 + 4 * (lane >> 4) + r, kk = kb * 16 + (lane & 15);
-        atomicAdd(&red[nn * WT + kk], acc[nb_][kb][r]);
-      }
+          for (int r = 0; r < 4; ++r) {
+            const int idx = (nb_ * 16 + 4 * (lane >> 4) + r) * WT + kb * 16 + (lane & 15);
+            red[idx] = (w == 0 ? 0.f : red[idx]) + acc[nb_][kb][r];
+          }
+    }
+  }
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.y * N * K;
   for (int i = tid; i < WT * WT; i += 256) {
@@ -353,6 +396,7 @@ template <typename T>
 int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, int pro_mode, const Pro& pro,
                     float* slab, int64_t slab_cap, float* dW, bool accumulate) {
   if ((N & 7) || (K & 7)) { set_error("pw_wgrad: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
+  if (M > (int64_t)UINT32_MAX) { set_error("pw_wgrad: M exceeds 2^32 rows", __FILE__, __LINE__); return -1; }
   const int tnn = cdiv(N, WT), tnk = cdiv(K, WT);
   const int tiles = tnn * tnk;
   int64_t splits = std::max<int64_t>(1, 1024 / tiles);

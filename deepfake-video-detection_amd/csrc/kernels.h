@@ -82,7 +82,8 @@ int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const floa
 template <typename T>
 int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
                          float* part, int64_t part_cap, float* dgate);
-// SE FC backward: from dgate -> dsq (written, scaled by 1/HW into bc), grads of wr,br,we,be
+// SE FC backward: from dgate -> dsq (written, scaled by 1/HW into bc), grads of wr,br,we,be.
+// tmp_de: frames*C floats; tmp_dr: 2*frames*rd floats
 int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
                      const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
                      float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);

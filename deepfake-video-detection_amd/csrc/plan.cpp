@@ -194,7 +194,7 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.o_dgate = alloc(F * maxSE * 4);
   p.o_bc = alloc(F * maxSE * 4);
   p.o_de = alloc(F * maxSE * 4);
-  p.o_dz = alloc(F * maxRD * 4);
+  p.o_dz = alloc(F * maxRD * 2 * 4);  // dz and r = silu(rpre)
   p.o_gx[0] = alloc(maxX * es);
   p.o_gx[1] = alloc(maxX * es);
   p.o_gs = alloc(maxS * es);
