@@ -38,7 +38,7 @@ template <typename T>
 __device__ __forceinline__ void lds_ld8(const T* p, float (&v)[8]) { ld8(p, v); }
 
 template <typename T, int MODE, bool STATS, bool RESID>
-__global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
+__global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, const T* __restrict__ R, int64_t M,
                                                       int N, int K, Pro pro, float* __restrict__ stats,
                                                       int64_t tiles_m) {
@@ -61,7 +61,16 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
   // staging: this thread owns rows srow, srow + 64 and k-vector skc of each 128 x 32 A/B step
   const int srow = tid >> 2, skc = (tid & 3) * 8;
   Raw8<T> ra[2], rb[2];
-  float psc[8], psh[8], pg[MODE == PRO_BN_SILU_G ? 2 : 1][8];
+  float pg[MODE == PRO_BN_SILU_G ? 2 : 1][8];
+  // producer BN scale/shift of all K columns, staged once per workgroup (dynamic LDS, 2K floats)
+  extern __shared__ float pro_lds[];
+  if constexpr (MODE != PRO_NONE) {
+    for (int i = tid; i < K; i += 256) {
+      pro_lds[i] = pro.scale[i];
+      pro_lds[K + i] = pro.shift[i];
+    }
+    __syncthreads();
+  }
   auto load = [&](int64_t m0, int k0) {
     const int gk = k0 + skc;
     const bool kok = gk < K;
@@ -73,8 +82,6 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
     }
     if constexpr (MODE != PRO_NONE) {
       const int kc = kok ? gk : 0;
-      ld8f(pro.scale + kc, psc);
-      ld8f(pro.shift + kc, psh);
       if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -86,6 +93,9 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
     }
   };
 
+  // The first k-step of the NEXT tile is loaded before this tile's epilogue stores: vmcnt
+  // counts loads and stores together, so loads issued after the stores would wait for them.
+  if ((int64_t)blockIdx.x < tiles_m) load((int64_t)blockIdx.x * GBM, 0);
   for (int64_t mt = blockIdx.x; mt < tiles_m; mt += gridDim.x) {
     const int64_t m0 = mt * GBM;
     f32x4_t acc[2][8];
@@ -94,7 +104,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
 #pragma unroll
       for (int b = 0; b < 8; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    load(m0, 0);
+    if (MODE != PRO_NONE && mt != (int64_t)blockIdx.x) load(m0, 0);
     for (int k0 = 0; k0 < K; k0 += GBK) {
       // ---- registers -> LDS (A through the consumer-side BN/SiLU/gate prologue) ----
 #pragma unroll
@@ -103,8 +113,11 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
         if constexpr (MODE == PRO_NONE) {
           raw_st(As + row * G::AS + skc, ra[i]);
         } else {
-          float x[8];
+          float x[8], psc[8], psh[8];
           raw_to_f(ra[i], x);
+          const int kc = k0 + skc < K ? k0 + skc : 0;
+          ld8(pro_lds + kc, psc);
+          ld8(pro_lds + K + kc, psh);
           if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]) * pg[i][j];
@@ -121,6 +134,7 @@ __global__ __launch_bounds__(256) void pw_gemm_kernel(const T* __restrict__ A, c
       }
       __syncthreads();
       if (k0 + GBK < K) load(m0, k0 + GBK);
+      else if (MODE == PRO_NONE && mt + gridDim.x < tiles_m) load((mt + gridDim.x) * GBM, 0);
       // ---- MFMA (partial N tiles are zero padded: the sequence is unconditional) ----
       if constexpr (sizeof(T) == 2) {
         bf16x8_t af[2];
@@ -219,8 +233,9 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
   const int gx = (int)std::min<int64_t>(tiles_m, cap);
   dim3 grid(gx, ntn), block(256);
   const bool st = stats != nullptr, rs = R != nullptr;
+  const size_t dyn = pro_mode != PRO_NONE ? 2 * (size_t)K * sizeof(float) : 0;
 #define DFD_GEMM_LAUNCH(MODE, ST, RS) \
-  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, RS>), grid, block, 0, s, A, B, C, R, M, N, K, pro, stats, tiles_m)
+  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, RS>), grid, block, dyn, s, A, B, C, R, M, N, K, pro, stats, tiles_m)
   if (rs) {
     if (pro_mode != PRO_NONE || st) { set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__); return -1; }
     DFD_GEMM_LAUNCH(PRO_NONE, false, true);

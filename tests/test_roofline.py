@@ -1,0 +1,41 @@
+"""The algorithmic byte/flop model behind bench.py's ``roofline`` field reproduces SURVEY §8(d)."""
+import pytest
+
+from deepfake_amd import roofline as R
+
+
+def _totals(frames=256, H=224, es=2):
+    tot = {}
+    for (s, i), b in R.block_geometry(H, H).items():
+        groups = [("dw%d" % b["k"], ("dw_fwd", "dw_dgrad", "dw_wgrad")), ("proj", ("pwl_fwd", "pwl_dgrad", "pwl_wgrad"))]
+        if b["mid"] != b["cin"] or (s, i) != (0, 0):
+            groups.append(("exp", ("pw_fwd", "pw_dgrad", "pw_wgrad")))
+        for key, kinds in groups:
+            for kind in kinds:
+                by, fl = R.algorithmic(kind, s, i, frames, H, H, es)
+                a, f = tot.get(key, (0, 0))
+                tot[key] = (a + by, f + fl)
+    return tot
+
+
+def test_survey_totals():
+    t = _totals()
+    # dw3x3 20.0 GFLOP / 6.05 GB, dw5x5 33.1 / 3.32, expand 255.3 / 6.08, project 233.9 / 4.44
+    assert t["dw3"][0] / 1e9 == pytest.approx(6.05, abs=0.01) and t["dw3"][1] / 1e9 == pytest.approx(20.0, abs=0.05)
+    assert t["dw5"][0] / 1e9 == pytest.approx(3.32, abs=0.01) and t["dw5"][1] / 1e9 == pytest.approx(33.1, abs=0.05)
+    assert t["exp"][0] / 1e9 == pytest.approx(6.08, abs=0.01) and t["exp"][1] / 1e9 == pytest.approx(255.3, abs=0.1)
+    assert t["proj"][0] / 1e9 == pytest.approx(4.44, abs=0.01) and t["proj"][1] / 1e9 == pytest.approx(233.9, abs=0.1)
+
+
+def test_geometry_224():
+    g = R.block_geometry(224, 224)
+    assert len(g) == 16
+    assert g[(1, 0)] == dict(cin=16, cout=24, mid=96, k=3, s=2, hin=112, win=112, hout=56, wout=56)
+    assert g[(6, 0)]["hout"] == 7 and g[(6, 0)]["cout"] == 320
+
+
+def test_probe_kernel_bytes():
+    # bench.py probes dw_fwd of blocks.1.0: bf16 in 112x112x96 + out 56x56x96, weights fp32
+    by, fl = R.algorithmic("dw_fwd", 1, 0, 256, 224, 224, 2)
+    assert by == 2 * (256 * 112 * 112 * 96 + 256 * 56 * 56 * 96) + 4 * 9 * 96
+    assert fl == 2 * 256 * 56 * 56 * 96 * 9

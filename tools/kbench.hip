@@ -1,0 +1,172 @@
+// Kernel microbenchmark for the EfficientNet-B0 hot path (development tool, not shipped).
+//
+// Times each launcher of deepfake-video-detection_amd/csrc on the layer shapes of a
+// 256-frame 224x224 training step (bf16), with HIP events over `iters` back-to-back launches,
+// and prints the average duration next to the algorithmic HBM floor
+// (roofline.py / SURVEY.md §8(d) bytes ÷ 6.3 TB/s measured copy bandwidth).
+//
+// build: make -C tools kbench        run: tools/kbench [filter] [frames]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../deepfake-video-detection_amd/csrc/kernels.h"
+#include "../include/dfd_hip.h"
+
+using namespace dfd;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+static const double kBw = 6.3e12;  // measured HBM copy bandwidth (MI355X_MICROARCH.md)
+
+struct Blk {
+  int cin, cout, mid, k, s, hin, hout;
+  bool ds;  // depthwise-separable (no expansion)
+};
+
+static std::vector<Blk> b0_blocks(int H) {
+  const int arch[7][6] = {{1, 1, 3, 1, 1, 16},  {0, 2, 3, 2, 6, 24}, {0, 2, 5, 2, 6, 40}, {0, 3, 3, 2, 6, 80},
+                          {0, 3, 5, 1, 6, 112}, {0, 4, 5, 2, 6, 192}, {0, 1, 3, 1, 6, 320}};
+  auto out = [](int h, int k, int s) { return (h + 2 * (((s - 1) + (k - 1)) / 2) - k) / s + 1; };
+  int h = out(H, 3, 2), cin = 32;
+  std::vector<Blk> v;
+  for (int si = 0; si < 7; ++si)
+    for (int bi = 0; bi < arch[si][1]; ++bi) {
+      const int st = bi == 0 ? arch[si][3] : 1, k = arch[si][2];
+      const int ho = out(h, k, st);
+      v.push_back({cin, arch[si][5], cin * arch[si][4], k, st, h, ho, arch[si][0] == 1});
+      h = ho;
+      cin = arch[si][5];
+    }
+  return v;
+}
+
+struct Bench {
+  hipStream_t s;
+  hipEvent_t e0, e1;
+  int iters = 20;
+  std::string filter;
+  double total_us = 0, total_floor = 0;
+  template <class F>
+  void run(const char* kind, const char* name, double bytes, F&& f) {
+    if (!filter.empty() && std::string(kind).find(filter) == std::string::npos) return;
+    if (f() != 0) { fprintf(stderr, "%s %s: launch failed: %s\n", kind, name, dfd_last_error_str()); exit(1); }
+    CK(hipStreamSynchronize(s));
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) f();
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1e3 * ms / iters, fl = bytes / kBw * 1e6;
+    total_us += us;
+    total_floor += fl;
+    printf("%-10s %-28s %9.1f us  floor %7.1f us  %5.2f TB/s  (x%.1f)\n", kind, name, us, fl, bytes / us * 1e-6,
+           us / fl);
+  }
+  static const char* dfd_last_error_str() { return dfd_last_error(); }
+};
+
+int main(int argc, char** argv) {
+  Bench b;
+  b.filter = argc > 1 ? argv[1] : "";
+  const int F = argc > 2 ? atoi(argv[2]) : 256;
+  const int H = 224;
+  CK(hipStreamCreate(&b.s));
+  CK(hipEventCreate(&b.e0));
+  CK(hipEventCreate(&b.e1));
+  auto blocks = b0_blocks(H);
+  // buffers sized for the largest tensor (stage-1 expanded map) and operands
+  const int64_t big = (int64_t)F * 112 * 112 * 96;
+  bf16 *A, *B, *C, *D;
+  float *W, *stats, *slab, *dW, *sc, *sh, *gate, *coef, *mean, *invstd;
+  CK(hipMalloc(&A, big * 2));
+  CK(hipMalloc(&B, big * 2));
+  CK(hipMalloc(&C, big * 2));
+  CK(hipMalloc(&D, big * 2));
+  CK(hipMemset(A, 0x3c, big * 2));
+  CK(hipMemset(B, 0x3c, big * 2));
+  CK(hipMemset(C, 0x3c, big * 2));
+  CK(hipMemset(D, 0x3c, big * 2));
+  const int64_t slab_cap = 64ll << 20;
+  CK(hipMalloc(&W, 4 << 20));
+  CK(hipMalloc(&stats, 64 << 20));
+  CK(hipMalloc(&slab, slab_cap * 4));
+  CK(hipMalloc(&dW, 4 << 20));
+  CK(hipMalloc(&sc, 1 << 16));
+  CK(hipMalloc(&sh, 1 << 16));
+  CK(hipMalloc(&coef, 1 << 16));
+  CK(hipMalloc(&mean, 1 << 16));
+  CK(hipMalloc(&invstd, 1 << 16));
+  CK(hipMalloc(&gate, (int64_t)F * 2048 * 4));
+  CK(hipMemset(W, 0, 4 << 20));
+  CK(hipMemset(sc, 0, 1 << 16));
+  CK(hipMemset(sh, 0, 1 << 16));
+  CK(hipMemset(coef, 0, 1 << 16));
+  CK(hipMemset(mean, 0, 1 << 16));
+  CK(hipMemset(invstd, 0, 1 << 16));
+  CK(hipMemset(gate, 0, (int64_t)F * 2048 * 4));
+  int rows = 0;
+  char nm[64];
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    const Blk& k = blocks[i];
+    const int64_t Mi = (int64_t)F * k.hin * k.hin, Mo = (int64_t)F * k.hout * k.hout;
+    const int C1 = k.ds ? k.cin : k.mid;
+    Pro pn{}, pb{sc, sh, nullptr, k.hin * k.hin, C1}, pg{sc, sh, gate, k.hout * k.hout, C1};
+    if (!k.ds) {
+      snprintf(nm, sizeof nm, "b%zu exp %ldx%dx%d", i, (long)Mi, k.mid, k.cin);
+      b.run("pw_fwd", nm, 2.0 * (Mi * k.cin + Mi * k.mid), [&] {
+        return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mi, k.mid, k.cin, PRO_NONE, pn, stats, &rows);
+      });
+      b.run("pw_dgrad", nm, 2.0 * (Mi * k.cin + Mi * k.mid), [&] {
+        return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mi, k.cin, k.mid, PRO_NONE, pn, nullptr, nullptr);
+      });
+      b.run("pw_wgrad", nm, 2.0 * (Mi * k.cin + Mi * k.mid), [&] {
+        return launch_pw_wgrad<bf16>(b.s, A, B, Mi, k.mid, k.cin, PRO_NONE, pn, slab, slab_cap, dW, false);
+      });
+    }
+    DwGeom g{F, k.hin, k.hin, C1, k.k, k.s, k.k / 2, k.hout, k.hout};
+    g.pad = ((k.s - 1) + (k.k - 1)) / 2;
+    snprintf(nm, sizeof nm, "b%zu dw%d s%d %dx%d c%d", i, k.k, k.s, k.hin, k.hin, C1);
+    const double dwb = 2.0 * (Mi * C1 + Mo * C1);
+    b.run("dw_fwd", nm, dwb, [&] { return launch_dw_fwd<bf16>(b.s, g, A, W, C, pb, PRO_BN_SILU, stats, &rows); });
+    BnBwdIn bi{};
+    bi.mean = mean; bi.invstd = invstd; bi.scale = sc; bi.shift = sh; bi.silu = true;
+    b.run("dw_dgrad", nm, dwb + 2.0 * Mi * C1, [&] {
+      return launch_dw_dgrad<bf16>(b.s, g, A, W, C, B, &bi, stats, &rows);
+    });
+    b.run("dw_wgrad", nm, dwb, [&] {
+      return launch_dw_wgrad<bf16>(b.s, g, A, B, pb, PRO_BN_SILU, slab, slab_cap, dW, false);
+    });
+    snprintf(nm, sizeof nm, "b%zu proj %ldx%dx%d", i, (long)Mo, k.cout, C1);
+    b.run("pwl_fwd", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
+      return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_BN_SILU_G, pg, stats, &rows);
+    });
+    b.run("pwl_dgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
+      return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, C1, k.cout, PRO_NONE, pn, nullptr, nullptr);
+    });
+    b.run("pwl_wgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
+      return launch_pw_wgrad<bf16>(b.s, A, B, Mo, k.cout, C1, PRO_BN_SILU_G, pg, slab, slab_cap, dW, false);
+    });
+    BnBwdIn bo{};
+    bo.dZ = A; bo.mean = mean; bo.invstd = invstd; bo.scale = sc; bo.shift = sh;
+    snprintf(nm, sizeof nm, "b%zu bn3 %ldx%d", i, (long)Mo, k.cout);
+    b.run("bn_bwd_apply", nm, 2.0 * 3 * Mo * k.cout, [&] {
+      return launch_bn_bwd_apply<bf16>(b.s, bo, B, coef, C, Mo, k.cout);
+    });
+    b.run("bn_bwd_reduce", nm, 2.0 * 2 * Mo * k.cout, [&] {
+      return launch_bn_bwd_reduce<bf16>(b.s, bo, B, Mo, k.cout, stats, &rows);
+    });
+  }
+  printf("TOTAL %.1f us, floor %.1f us\n", b.total_us, b.total_floor);
+  return 0;
+}
