@@ -289,3 +289,9 @@ class B0FrameExtractor(nn.Module):
 
     def forward(self, x):
         return self.trunk(x)
+
+
+class B0FrameExtractor(EfficientNetB0Trunk):
+    """Frame feature extractor for the ``DeepfakeDetector(model_type='rnn')`` seam
+    (``src/detector.py:88-100``): ``(N, 3, H, W)`` face crops -> ``(N, 1280)`` pooled B0 features,
+    feeding a ``LogicRNNLSTM(input_size=1280)``.  A standalone trunk owning its flat buffers."""
