@@ -461,78 +461,132 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
 }
 
 // ------------------------------------------------------------------ SE excitation (per frame)
-// one workgroup per frame: rpre = Wr sq + br ; r = silu(rpre) ; gate = sigmoid(We r + be)
-__global__ __launch_bounds__(256) void se_fc_fwd_kernel(const float* __restrict__ sq, const float* __restrict__ wr,
-                                                        const float* __restrict__ br, const float* __restrict__ we,
-                                                        const float* __restrict__ be, int C, int rd,
-                                                        float* __restrict__ rpre, float* __restrict__ gate) {
-  extern __shared__ float sm[];
-  float* s_sq = sm;      // [C]
-  float* s_r = sm + C;   // [rd]
-  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int c = tid; c < C; c += 256) s_sq[c] = sq[(int64_t)f * C + c];
-  __syncthreads();
-  for (int j = wave; j < rd; j += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += wr[(int64_t)j * C + c] * s_sq[c];
-    a = wave_sum(a);
-    if (lane == 0) {
-      a += br[j];
-      rpre[(int64_t)f * rd + j] = a;
-      s_r[j] = siluf_(a);
-    }
+// SE excitation, forward:  rpre = Wr sq + br ; r = silu(rpre) ; gate = sigmoid(We r + be)
+// (timm SqueezeExcite conv_reduce / act / conv_expand / sigmoid).  Two kernels per direction,
+// templated on the reduce width RD (4..48 in B0) so every accumulator array is exact:
+//   se_rd_kernel   one workgroup per frame: each thread accumulates all RD products over its
+//                  channel subset (coalesced Wr rows), fixed-order block reduction;
+//   se_gate_kernel one thread per (frame, channel): RD-long dot product with an LDS copy of r.
+template <int RD>
+__device__ __forceinline__ void block_sum_rd(float (&acc)[RD], float* red, float* out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int j = 0; j < RD; ++j) {
+    const float v = wave_sum(acc[j]);
+    if (lane == 0) red[wave * RD + j] = v;
   }
   __syncthreads();
+  if (tid < RD) out[tid] = red[tid] + red[RD + tid] + red[2 * RD + tid] + red[3 * RD + tid];
+  __syncthreads();
+}
+
+template <int RD>
+__global__ __launch_bounds__(256) void se_rd_kernel(const float* __restrict__ sq, const float* __restrict__ wr,
+                                                    const float* __restrict__ br, int C, float* __restrict__ rpre) {
+  __shared__ float red[4 * RD];
+  __shared__ float s_o[RD];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  float acc[RD];
+#pragma unroll
+  for (int j = 0; j < RD; ++j) acc[j] = 0.f;
   for (int c = tid; c < C; c += 256) {
-    float a = be[c];
-    for (int j = 0; j < rd; ++j) a += we[(int64_t)c * rd + j] * s_r[j];
-    gate[(int64_t)f * C + c] = sigmoidf_(a);
+    const float v = sq[(int64_t)f * C + c];
+#pragma unroll
+    for (int j = 0; j < RD; ++j) acc[j] = fmaf(wr[(int64_t)j * C + c], v, acc[j]);
   }
+  block_sum_rd<RD>(acc, red, s_o);
+  if (tid < RD) rpre[(int64_t)f * RD + tid] = s_o[tid] + br[tid];
 }
 
-int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
-                     const float* be, int frames, int C, int rd, float* rpre, float* gate) {
-  hipLaunchKernelGGL(se_fc_fwd_kernel, dim3(frames), dim3(256), (C + rd) * sizeof(float), s, sq, wr, br, we, be, C,
-                     rd, rpre, gate);
-  DFD_HIP_CHECK(hipGetLastError());
-  return 0;
+template <int RD>
+__global__ __launch_bounds__(256) void se_gate_kernel(const float* __restrict__ rpre, const float* __restrict__ we,
+                                                      const float* __restrict__ be, int C, float* __restrict__ gate) {
+  __shared__ float s_r[RD];
+  const int f = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (threadIdx.x < RD) s_r[threadIdx.x] = siluf_(rpre[(int64_t)f * RD + threadIdx.x]);
+  __syncthreads();
+  if (c >= C) return;
+  const float* w = we + (int64_t)c * RD;
+  float a = be[c];
+#pragma unroll
+  for (int j = 0; j < RD; ++j) a = fmaf(w[j], s_r[j], a);
+  gate[(int64_t)f * C + c] = sigmoidf_(a);
 }
 
-// per frame: de = dgate*g*(1-g) ; dz = (We^T de) * silu'(rpre) ; bc = (Wr^T dz) * inv_hw
-__global__ __launch_bounds__(256) void se_fc_bwd_kernel(const float* __restrict__ dgate, const float* __restrict__ gate,
-                                                        const float* __restrict__ rpre, const float* __restrict__ wr,
-                                                        const float* __restrict__ we, int C, int rd, float inv_hw,
-                                                        float* __restrict__ de_out, float* __restrict__ dz_out,
-                                                        float* __restrict__ r_out, float* __restrict__ bc_out) {
-  extern __shared__ float sm[];
-  float* s_de = sm;      // [C]
-  float* s_dz = sm + C;  // [rd]
-  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// backward:  de = dgate*g*(1-g) ; dz = (We^T de) * silu'(rpre) ; bc = (Wr^T dz) * inv_hw
+template <int RD>
+__global__ __launch_bounds__(256) void se_dz_kernel(const float* __restrict__ dgate, const float* __restrict__ gate,
+                                                    const float* __restrict__ rpre, const float* __restrict__ we,
+                                                    int C, float* __restrict__ de_out, float* __restrict__ dz_out,
+                                                    float* __restrict__ r_out) {
+  __shared__ float red[4 * RD];
+  __shared__ float s_o[RD];
+  const int f = blockIdx.x, tid = threadIdx.x;
+  float acc[RD];
+#pragma unroll
+  for (int j = 0; j < RD; ++j) acc[j] = 0.f;
   for (int c = tid; c < C; c += 256) {
     const float g = gate[(int64_t)f * C + c];
     const float d = dgate[(int64_t)f * C + c] * g * (1.f - g);
-    s_de[c] = d;
     de_out[(int64_t)f * C + c] = d;
+    const float* w = we + (int64_t)c * RD;
+#pragma unroll
+    for (int j = 0; j < RD; ++j) acc[j] = fmaf(w[j], d, acc[j]);
   }
+  block_sum_rd<RD>(acc, red, s_o);
+  if (tid < RD) {
+    const float rp = rpre[(int64_t)f * RD + tid];
+    dz_out[(int64_t)f * RD + tid] = s_o[tid] * dsiluf_(rp);
+    r_out[(int64_t)f * RD + tid] = siluf_(rp);
+  }
+}
+
+template <int RD>
+__global__ __launch_bounds__(256) void se_bc_kernel(const float* __restrict__ dz, const float* __restrict__ wr, int C,
+                                                    float inv_hw, float* __restrict__ bc_out) {
+  __shared__ float s_dz[RD];
+  const int f = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (threadIdx.x < RD) s_dz[threadIdx.x] = dz[(int64_t)f * RD + threadIdx.x];
   __syncthreads();
-  for (int j = wave; j < rd; j += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += we[(int64_t)c * rd + j] * s_de[c];
-    a = wave_sum(a);
-    if (lane == 0) {
-      const float rp = rpre[(int64_t)f * rd + j];
-      const float z = a * dsiluf_(rp);
-      s_dz[j] = z;
-      dz_out[(int64_t)f * rd + j] = z;
-      r_out[(int64_t)f * rd + j] = siluf_(rp);
-    }
+  if (c >= C) return;
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < RD; ++j) a = fmaf(wr[(int64_t)j * C + c], s_dz[j], a);
+  bc_out[(int64_t)f * C + c] = a * inv_hw;
+}
+
+template <int RD>
+static void se_fwd_launch(hipStream_t s, dim3 g2, int frames, const float* sq, const float* wr, const float* br,
+                          const float* we, const float* be, int C, float* rpre, float* gate) {
+  hipLaunchKernelGGL(se_rd_kernel<RD>, dim3(frames), dim3(256), 0, s, sq, wr, br, C, rpre);
+  hipLaunchKernelGGL(se_gate_kernel<RD>, g2, dim3(256), 0, s, rpre, we, be, C, gate);
+}
+template <int RD>
+static void se_bwd_launch(hipStream_t s, dim3 g2, int frames, const float* dgate, const float* gate, const float* rpre,
+                          const float* wr, const float* we, int C, float inv_hw, float* de, float* dz, float* r,
+                          float* bc) {
+  hipLaunchKernelGGL(se_dz_kernel<RD>, dim3(frames), dim3(256), 0, s, dgate, gate, rpre, we, C, de, dz, r);
+  hipLaunchKernelGGL(se_bc_kernel<RD>, g2, dim3(256), 0, s, dz, wr, C, inv_hw, bc);
+}
+
+#define DFD_SE_RD_SWITCH(RDV, CALL)                                                        \
+  switch (RDV) {                                                                           \
+    case 4: { constexpr int RD = 4; CALL; } break;                                         \
+    case 6: { constexpr int RD = 6; CALL; } break;                                         \
+    case 8: { constexpr int RD = 8; CALL; } break;                                         \
+    case 10: { constexpr int RD = 10; CALL; } break;                                       \
+    case 20: { constexpr int RD = 20; CALL; } break;                                       \
+    case 28: { constexpr int RD = 28; CALL; } break;                                       \
+    case 48: { constexpr int RD = 48; CALL; } break;                                       \
+    default: set_error("se: reduce width not instantiated", __FILE__, __LINE__); return -1; \
   }
-  __syncthreads();
-  for (int c = tid; c < C; c += 256) {
-    float a = 0.f;
-    for (int j = 0; j < rd; ++j) a += wr[(int64_t)j * C + c] * s_dz[j];
-    bc_out[(int64_t)f * C + c] = a * inv_hw;
-  }
+
+int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
+                     const float* be, int frames, int C, int rd, float* rpre, float* gate) {
+  const dim3 g2((unsigned)cdiv(C, 256), (unsigned)frames);
+  DFD_SE_RD_SWITCH(rd, se_fwd_launch<RD>(s, g2, frames, sq, wr, br, we, be, C, rpre, gate));
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
 }
 
 // weight grads: gwe[c][j] = sum_f de[f][c] * r[f][j]; gbe[c] = sum_f de[f][c]   (r = silu(rpre))
@@ -592,8 +646,9 @@ int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const
                      const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
                      float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
   float* tmp_r = tmp_dr + (int64_t)frames * rd;  // tmp_dr holds 2 * frames * rd floats
-  hipLaunchKernelGGL(se_fc_bwd_kernel, dim3(frames), dim3(256), (C + rd) * sizeof(float), s, dgate, gate, rpre, wr,
-                     we, C, rd, inv_hw, tmp_de, tmp_dr, tmp_r, bc_out);
+  const dim3 g2((unsigned)cdiv(C, 256), (unsigned)frames);
+  DFD_SE_RD_SWITCH(rd, se_bwd_launch<RD>(s, g2, frames, dgate, gate, rpre, wr, we, C, inv_hw, tmp_de, tmp_dr, tmp_r,
+                                          bc_out));
   DFD_HIP_CHECK(hipGetLastError());
   const int64_t n = 2 * (int64_t)C * rd + C + rd;
   hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, tmp_de, tmp_dr, sq, tmp_r,

@@ -28,24 +28,66 @@ __device__ __forceinline__ float drop_mul(uint64_t seed, uint32_t stream, int64_
 
 // ------------------------------------------------------------------ generic small linear ops
 // Y[r][o] = act( sum_i X[r][i]*xm(r,i) * W[o][i] + b[o] ),  xm = dropout multiplier (stream) or 1
+// Y[r][o] = post(sum_i drop(X)[r][i] * W[o][i] + b[o]).  A 256-thread block owns 16 rows x 16
+// outputs; its 4 waves split K into quarters, each streaming 64-wide chunks through a private
+// LDS tile with the next chunk already in registers (X through its dropout mask); lane
+// (row = lane>>2, 4 outputs) accumulates in ascending i, the quarters are added in a fixed order.
+constexpr int LKC = 64;  // K chunk
 __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ X, const float* __restrict__ W,
                                                          const float* __restrict__ b, float* __restrict__ Y, int R,
                                                          int I, int O, int relu, uint64_t seed, uint32_t stream,
                                                          float p) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (int64_t)R * O) return;
-  const int r = (int)(idx / O), o = (int)(idx % O);
-  const float* x = X + (int64_t)r * I;
-  const float* w = W + (int64_t)o * I;
-  float a = 0.f;
-  if (p > 0.f) {
-    for (int i = 0; i < I; ++i) a += x[i] * drop_mul(seed, stream, (int64_t)r * I + i, p) * w[i];
-  } else {
-    for (int i = 0; i < I; ++i) a += x[i] * w[i];
+  __shared__ float xs[4][16][LKC + 1], ws[4][16][LKC + 1];
+  __shared__ float red[4][256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r0 = blockIdx.y * 16, o0 = blockIdx.x * 16;
+  const int quarter = (I + 3) / 4;
+  const int kb = wave * quarter, ke = min(I, kb + quarter);
+  const int row = lane >> 2, og = (lane & 3) * 4;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float nx[16], nw[16];  // 16 rows x 64 k per operand / 64 lanes
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i, rr = e >> 6, kk = e & 63, k = k0 + kk;
+      const int r = r0 + rr, o = o0 + rr;
+      const bool xok = r < R && k < ke, wok = o < O && k < ke;
+      float x = X[xok ? (int64_t)r * I + k : 0];
+      if (p > 0.f && xok) x *= drop_mul(seed, stream, (int64_t)r * I + k, p);
+      nx[i] = xok ? x : 0.f;
+      const float w = W[wok ? (int64_t)o * I + k : 0];
+      nw[i] = wok ? w : 0.f;
+    }
+  };
+  if (kb < ke) load(kb);
+  for (int k0 = kb; k0 < ke; k0 += LKC) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      xs[wave][e >> 6][e & 63] = nx[i];
+      ws[wave][e >> 6][e & 63] = nw[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (k0 + LKC < ke) load(k0 + LKC);
+    const int kn = min(LKC, ke - k0);
+    for (int kk = 0; kk < kn; ++kk) {
+      const float x = xs[wave][row][kk];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = fmaf(x, ws[wave][og + q][kk], acc[q]);
+    }
+    __builtin_amdgcn_wave_barrier();
   }
-  if (b) a += b[o];
-  if (relu) a = fmaxf(a, 0.f);
-  Y[idx] = a;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[wave][row * 16 + og + q] = acc[q];
+  __syncthreads();
+  const int r = r0 + (tid >> 4), o = o0 + (tid & 15);
+  if (r < R && o < O) {
+    float a = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    if (b) a += b[o];
+    if (relu) a = fmaxf(a, 0.f);
+    Y[(int64_t)r * O + o] = a;
+  }
 }
 
 // dX[r][i] = (acc? dX : 0) + sum_o dY[r][o] * W[o][i], then * xm(r,i) (dropout on the input)
@@ -318,17 +360,19 @@ template int launch_cast_params<bf16>(hipStream_t, const float*, bf16*, const Ca
 // ------------------------------------------------------------------ host launchers (head.h)
 static unsigned nblk(int64_t n) { return (unsigned)std::max<int64_t>(1, cdiv64(n, 256)); }
 
+static dim3 lin_grid(int R, int O) { return dim3((unsigned)cdiv(O, 16), (unsigned)cdiv(R, 16)); }
+
 int head_forward(hipStream_t s, const HeadDims& d, const HeadParams& P, const float* F, HeadWork& w, uint64_t seed,
                  float p, float* logits, float* scores) {
   if (d.use_attn) {
-    hipLaunchKernelGGL(linear_fwd_kernel, dim3(nblk((int64_t)d.B * d.T * d.H)), dim3(256), 0, s, F, P.ta_w1,
+    hipLaunchKernelGGL(linear_fwd_kernel, lin_grid(d.B * d.T, d.H), dim3(256), 0, s, F, P.ta_w1,
                        P.ta_b1, w.hid, d.B * d.T, d.D, d.H, 1, seed, 0u, 0.f);
   }
   hipLaunchKernelGGL(attn_fwd_kernel, dim3(d.B), dim3(256), d.T * sizeof(float), s, F, w.hid, P.ta_w2, P.ta_b2, d.T,
                      d.D, d.H, d.use_attn, w.e, scores, w.g);
-  hipLaunchKernelGGL(linear_fwd_kernel, dim3(nblk((int64_t)d.B * d.F1)), dim3(256), 0, s, w.g, P.fc1_w, P.fc1_b, w.h1,
+  hipLaunchKernelGGL(linear_fwd_kernel, lin_grid(d.B, d.F1), dim3(256), 0, s, w.g, P.fc1_w, P.fc1_b, w.h1,
                      d.B, d.D, d.F1, 1, seed, 1u, p);
-  hipLaunchKernelGGL(linear_fwd_kernel, dim3(nblk((int64_t)d.B * d.NC)), dim3(256), 0, s, w.h1, P.fc2_w, P.fc2_b,
+  hipLaunchKernelGGL(linear_fwd_kernel, lin_grid(d.B, d.NC), dim3(256), 0, s, w.h1, P.fc2_w, P.fc2_b,
                      logits, d.B, d.F1, d.NC, 0, seed, 2u, p);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;

@@ -6,84 +6,136 @@
 
 namespace dfd {
 
-constexpr int ST = 8;                 // output tile edge
-constexpr int SIE = (ST - 1) * 2 + 3; // 17: input tile edge
+constexpr int ST = 16;                // output tile edge
+constexpr int SIE = (ST - 1) * 2 + 3; // 33: input tile edge
+constexpr int SNIN = 3 * SIE * SIE;   // 3267 input floats per tile
+constexpr int SNLD = (SNIN + 255) / 256;
 constexpr int SCO = 32;               // output channels
+constexpr int SP = ST * ST / 64;      // output pixels per thread (fwd)
+
+struct StemTiles {
+  int tiles_x, tiles_y;
+  __device__ void coords(int64_t t, int& f, int& oy0, int& ox0) const {
+    const int64_t tpf = (int64_t)tiles_x * tiles_y;
+    f = (int)(t / tpf);
+    const int rem = (int)(t - (int64_t)f * tpf);
+    oy0 = (rem / tiles_x) * ST;
+    ox0 = (rem - (rem / tiles_x) * tiles_x) * ST;
+  }
+};
+
+// input tile [pix][ci] (pix = row*SIE + col) of frame f at origin (iy0, ix0): branch-free
+// masked loads through the caller's strides, all issued together (register prefetch).
+__device__ __forceinline__ void stem_load(const StemGeom& g, const float* __restrict__ x, int f, int iy0, int ix0,
+                                          float (&r)[SNLD]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < SNLD; ++i) {
+    const int e = tid + 256 * i;
+    const int pix = e / 3, ci = e - 3 * (e / 3);
+    const int iy = iy0 + pix / SIE, ix = ix0 + pix % SIE;
+    const bool ok = e < SNIN && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+    const int64_t off = ok ? (int64_t)f * g.sf + ci * g.sc + (int64_t)iy * g.sh + (int64_t)ix * g.sw : 0;
+    const float v = x[off];
+    r[i] = ok ? v : 0.f;
+  }
+}
+__device__ __forceinline__ void stem_store(float* tin, const float (&r)[SNLD]) {
+#pragma unroll
+  for (int i = 0; i < SNLD; ++i) {
+    const int e = threadIdx.x + 256 * i;
+    if (e < SNIN) tin[e] = r[i];
+  }
+}
 
 template <typename T, bool STATS>
-__global__ __launch_bounds__(256) void stem_fwd_kernel(StemGeom g, const float* __restrict__ x,
+__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const float* __restrict__ x,
                                                        const float* __restrict__ w, T* __restrict__ Y,
                                                        float* __restrict__ stats, int64_t ntiles) {
-  __shared__ float tin[3][SIE * SIE];
+  __shared__ float tin[SNIN];
   __shared__ __attribute__((aligned(16))) float wts[27][SCO];  // [ci*9+tap][co]
-  __shared__ float st_sum[SCO], st_sq[SCO];
+  __shared__ float red[2][4][SCO];
   const int tid = threadIdx.x, vec = tid & 3, pt = tid >> 2;
   for (int i = tid; i < 27 * SCO; i += 256) {
     const int co = i / 27, r = i % 27;  // w[co][ci][kh][kw], r = ci*9 + kh*3 + kw
     wts[r][co] = w[i];
   }
-  if (STATS && tid < SCO) { st_sum[tid] = 0.f; st_sq[tid] = 0.f; }
-  const int tiles_x = (g.Wo + ST - 1) / ST, tiles_y = (g.Ho + ST - 1) / ST;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int f = (int)(t / (tiles_x * tiles_y));
-    const int rem = (int)(t - (int64_t)f * tiles_x * tiles_y);
-    const int oy0 = (rem / tiles_x) * ST, ox0 = (rem % tiles_x) * ST;
-    const int iy0 = oy0 * 2 - 1, ix0 = ox0 * 2 - 1;
+  const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
+  float st_s[8], st_q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
+  float nxt[SNLD];
+  int64_t t = blockIdx.x;
+  if (t < ntiles) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
+    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nxt);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
     __syncthreads();
-    for (int e = tid; e < 3 * SIE * SIE; e += 256) {
-      const int pix = e / 3, ci = e % 3;
-      const int iy = iy0 + pix / SIE, ix = ix0 + pix % SIE;
-      float v = 0.f;
-      if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) v = x[f * g.sf + ci * g.sc + iy * g.sh + ix * g.sw];
-      tin[ci][pix] = v;
+    stem_store(tin, nxt);
+    __syncthreads();
+    if (t + gridDim.x < ntiles) {  // next tile in flight during this tile's math and stores
+      int f2, oy2, ox2;
+      tl.coords(t + gridDim.x, f2, oy2, ox2);
+      stem_load(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nxt);
     }
-    __syncthreads();
-    const int ly = pt >> 3, lx = pt & 7;
-    const int oy = oy0 + ly, ox = ox0 + lx;
-    float acc[8];
+    float acc[SP][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int i = 0; i < SP; ++i)
 #pragma unroll
-    for (int ci = 0; ci < 3; ++ci)
+      for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+#pragma unroll 3
+    for (int tap = 0; tap < 27; ++tap) {
+      const int ci = tap / 9, kh = (tap % 9) / 3, kw = tap % 3;
+      float wv[8];
+      ld8(&wts[tap][vec * 8], wv);
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh)
+      for (int i = 0; i < SP; ++i) {
+        const int p = pt + 64 * i, ly = p / ST, lx = p % ST;
+        const float xv = tin[((ly * 2 + kh) * SIE + lx * 2 + kw) * 3 + ci];
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const float xv = tin[ci][(ly * 2 + kh) * SIE + lx * 2 + kw];
-          float wv[8];
-          ld8(&wts[ci * 9 + kh * 3 + kw][vec * 8], wv);
+        for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(xv, wv[j], acc[i][j]);
+      }
+    }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] = fmaf(xv, wv[j], acc[j]);
-        }
-    const bool ovalid = oy < g.Ho && ox < g.Wo;
+    for (int i = 0; i < SP; ++i) {
+      const int p = pt + 64 * i, oy = oy0 + p / ST, ox = ox0 + p % ST;
+      const bool ok = oy < g.Ho && ox < g.Wo;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = Tr<T>::round(acc[j]);
-    if (ovalid) st8(Y + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + vec * 8, acc);
-    if constexpr (STATS) {
-      float s[8], q[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { s[j] = ovalid ? acc[j] : 0.f; q[j] = s[j] * s[j]; }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int o = 4; o < 64; o <<= 1) {
-          s[j] += __shfl_xor(s[j], o, 64);
-          q[j] += __shfl_xor(q[j], o, 64);
-        }
-      if ((tid & 63) < 4) {
+      for (int j = 0; j < 8; ++j) acc[i][j] = Tr<T>::round(acc[i][j]);
+      if (ok) st8(Y + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + vec * 8, acc[i]);
+      if constexpr (STATS) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          atomicAdd(&st_sum[vec * 8 + j], s[j]);
-          atomicAdd(&st_sq[vec * 8 + j], q[j]);
+          const float v = ok ? acc[i][j] : 0.f;
+          st_s[j] += v;
+          st_q[j] += v * v;
         }
       }
     }
   }
   if constexpr (STATS) {
+    // fixed-order reduction: lanes with the same vec (shuffles), then the 4 waves through LDS
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) {
+        st_s[j] += __shfl_xor(st_s[j], o, 64);
+        st_q[j] += __shfl_xor(st_q[j], o, 64);
+      }
+    if (lane < 4) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { red[0][wave][vec * 8 + j] = st_s[j]; red[1][wave][vec * 8 + j] = st_q[j]; }
+    }
     __syncthreads();
-    if (tid < SCO) {
-      stats[((int64_t)blockIdx.x * 2 + 0) * SCO + tid] = st_sum[tid];
-      stats[((int64_t)blockIdx.x * 2 + 1) * SCO + tid] = st_sq[tid];
+    if (tid < 2 * SCO) {
+      const int which = tid / SCO, c = tid % SCO;
+      stats[((int64_t)blockIdx.x * 2 + which) * SCO + c] =
+          red[which][0][c] + red[which][1][c] + red[which][2][c] + red[which][3][c];
     }
   }
 }
@@ -92,7 +144,7 @@ template <typename T>
 int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const float* w, T* Y, float* stats,
                     int* stat_rows) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
-  const int gx = (int)std::min<int64_t>(ntiles, 2048);
+  const int gx = (int)std::min<int64_t>(ntiles, 1024);
   if (stats)
     hipLaunchKernelGGL((stem_fwd_kernel<T, true>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
   else
@@ -103,66 +155,66 @@ int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const floa
 }
 
 // dW[co][ci][kh][kw] = sum dY[f,oy,ox,co] * x[f,ci,2oy-1+kh,2ox-1+kw]
-// thread (co = tid & 31, sub = tid >> 5) accumulates all 27 taps over pixels p = sub (mod 8)
+// thread (co = tid & 31, sub = tid >> 5) accumulates all 27 taps over pixels p = sub (mod 8);
+// the next tile's input and dY are loaded into registers while the current tile is reduced.
 template <typename T>
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float* __restrict__ x,
                                                          const T* __restrict__ dY, float* __restrict__ slab,
                                                          int64_t ntiles) {
-  __shared__ float tin[3][SIE * SIE];
-  __shared__ __attribute__((aligned(16))) float tg[ST * ST][SCO];
-  __shared__ float red[8][27][SCO];
+  __shared__ float tin[SNIN];
+  __shared__ __attribute__((aligned(16))) float tg[ST * ST * SCO];  // [pix][co]; reused as red[8][27][32]
   const int tid = threadIdx.x, co = tid & 31, sub = tid >> 5;
+  const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
   float acc[27];
 #pragma unroll
   for (int r = 0; r < 27; ++r) acc[r] = 0.f;
-  const int tiles_x = (g.Wo + ST - 1) / ST, tiles_y = (g.Ho + ST - 1) / ST;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int f = (int)(t / (tiles_x * tiles_y));
-    const int rem = (int)(t - (int64_t)f * tiles_x * tiles_y);
-    const int oy0 = (rem / tiles_x) * ST, ox0 = (rem % tiles_x) * ST;
-    const int iy0 = oy0 * 2 - 1, ix0 = ox0 * 2 - 1;
-    __syncthreads();
-    for (int e = tid; e < 3 * SIE * SIE; e += 256) {
-      const int pix = e / 3, ci = e % 3;
-      const int iy = iy0 + pix / SIE, ix = ix0 + pix % SIE;
-      float v = 0.f;
-      if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) v = x[f * g.sf + ci * g.sc + iy * g.sh + ix * g.sw];
-      tin[ci][pix] = v;
-    }
-    for (int e = tid; e < ST * ST * 4; e += 256) {
-      const int pix = e >> 2, v = e & 3;
+  float nx[SNLD];
+  Raw8<T> nd[4];  // 256 px x 4 vectors / 256 threads
+  auto load = [&](int64_t t) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
+    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nx);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
       const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
-      float d[8];
-      if (oy < g.Ho && ox < g.Wo) {
-        ld8(dY + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8, d);
-      } else {
+      raw_ld(nd[i], dY + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8, dY, oy < g.Ho && ox < g.Wo);
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+    __syncthreads();
+    stem_store(tin, nx);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = 0.f;
-      }
-      st8(&tg[pix][v * 8], d);
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
+      float d[8];
+      raw_to_f(nd[i], d);
+      st8(&tg[pix * SCO + v * 8], d);
     }
     __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);
     for (int p = sub; p < ST * ST; p += 8) {
-      const int ly = p >> 3, lx = p & 7;
-      const float d = tg[p][co];
+      const int ly = p / ST, lx = p % ST;
+      const float d = tg[p * SCO + co];
 #pragma unroll
-      for (int ci = 0; ci < 3; ++ci)
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 3; ++kw)
-            acc[ci * 9 + kh * 3 + kw] = fmaf(d, tin[ci][(ly * 2 + kh) * SIE + lx * 2 + kw], acc[ci * 9 + kh * 3 + kw]);
+      for (int tap = 0; tap < 27; ++tap) {
+        const int ci = tap / 9, kh = (tap % 9) / 3, kw = tap % 3;
+        acc[tap] = fmaf(d, tin[((ly * 2 + kh) * SIE + lx * 2 + kw) * 3 + ci], acc[tap]);
+      }
     }
   }
   __syncthreads();
+  float* red = tg;  // [8][27][32] = 6912 floats <= 8192
 #pragma unroll
-  for (int r = 0; r < 27; ++r) red[sub][r][co] = acc[r];
+  for (int r = 0; r < 27; ++r) red[(sub * 27 + r) * SCO + co] = acc[r];
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * 27 * SCO;
   for (int i = tid; i < 27 * SCO; i += 256) {
     const int c = i / 27, r = i % 27;
     float a = 0.f;
-    for (int sb = 0; sb < 8; ++sb) a += red[sb][r][c];
+    for (int sb = 0; sb < 8; ++sb) a += red[(sb * 27 + r) * SCO + c];
     out[i] = a;
   }
 }
