@@ -7,6 +7,7 @@ Drop-in counterparts of the reference's hot-path API (SaiPranav1506/DeepFake-Vid
 * ``WeightedCrossEntropyLoss``                           (nn.CrossEntropyLoss(weight), ensemble_trainer.py:358)
 * ``FusedAdamW`` / ``FusedAdam`` / ``clip_grad_norm_``     (ensemble_trainer.py:146,199-200; train.py:323)
 * ``train_step`` / ``DataParallelTrainer``                 (EnsembleTrainer.train_epoch step, ensemble_trainer.py:182-200)
+* ``LogicRNNLSTM`` / ``LogicCell`` / ``create_model``       (src/RNNModel.py)
 
 Compute runs in hand-written HIP kernels for gfx950 behind the C ABI of ``include/dfd_hip.h``
 (``libdfd_hip.so``); PyTorch supplies device memory, streams and torch.distributed (RCCL).
@@ -15,7 +16,8 @@ Submodules import lazily so ``import deepfake_amd`` works before the library is 
 
 __all__ = [
     "PretrainedBackboneDetector", "EnsembleDetector", "EfficientNetB0Trunk", "B0FrameExtractor",
-    "WeightedCrossEntropyLoss", "FusedAdamW", "FusedAdam", "clip_grad_norm_",
+    "WeightedCrossEntropyLoss", "FusedAdamW", "FusedAdam", "clip_grad_norm_", "LogicRNNLSTM", "LogicCell",
+    "create_model",
 ]
 
 
@@ -28,6 +30,8 @@ def __getattr__(name):
         from . import losses as m
     elif name in ("FusedAdamW", "FusedAdam", "clip_grad_norm_"):
         from . import optim as m
+    elif name in ("LogicRNNLSTM", "LogicCell", "create_model"):
+        from . import rnn as m
     else:
         raise AttributeError(name)
     return getattr(m, name)

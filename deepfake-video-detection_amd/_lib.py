@@ -53,6 +53,10 @@ _SIGS = {
     "dfd_ce_backward": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i64, c_p, c_p, c_p]),
     "dfd_grad_norm": (c_i, [c_p, c_p, c_i64, c_f, c_p, c_p]),
     "dfd_adam_step": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_i, c_d, c_i, c_p]),
+    "dfd_rnn_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
+    "dfd_rnn_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
+    "dfd_rnn_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_u64, c_f]),
+    "dfd_rnn_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_p, c_fpp, c_u64, c_f]),
 }
 
 EXPORTED = tuple(_SIGS.keys())

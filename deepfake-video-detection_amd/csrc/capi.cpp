@@ -10,6 +10,7 @@
 
 #include "head.h"
 #include "plan.h"
+#include "rnn.h"
 
 namespace dfd {
 static thread_local std::string g_err;
@@ -255,3 +256,50 @@ int dfd_adam_step(void* stream, float* params, float* grads, float* m, float* v,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- LogicRNNLSTM
+static bool rnn_dims_ok(int B, int T, int IN, int H, int L) {
+  if (B <= 0 || T <= 0 || IN <= 0 || H <= 0 || L < 1 || L > 8) {
+    dfd::set_error("rnn: bad dimensions", __FILE__, __LINE__);
+    return false;
+  }
+  return true;
+}
+
+int64_t dfd_rnn_work_floats(int B, int T, int IN, int H, int L) {
+  DFD_GUARD_BEGIN
+  if (!rnn_dims_ok(B, T, IN, H, L)) return -1;
+  return dfd::rnn_work_floats(dfd::RnnDims{B, T, IN, H, L});
+  DFD_GUARD_END
+}
+
+int64_t dfd_rnn_scratch_floats(int B, int T, int IN, int H, int L) {
+  DFD_GUARD_BEGIN
+  if (!rnn_dims_ok(B, T, IN, H, L)) return -1;
+  return dfd::rnn_scratch_floats(dfd::RnnDims{B, T, IN, H, L});
+  DFD_GUARD_END
+}
+
+int dfd_rnn_forward(void* stream, int B, int T, int IN, int H, int L, const float* x, const int64_t* order,
+                    const int64_t* lengths, float* const* params, float* work, float* y, uint64_t seed, float p) {
+  DFD_GUARD_BEGIN
+  if (!rnn_dims_ok(B, T, IN, H, L)) return -1;
+  if (!x || !params || !work || !y) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  dfd::RnnParams P{};
+  if (dfd::rnn_params_from_table(params, L, P)) return -1;
+  return dfd::rnn_forward((hipStream_t)stream, dfd::RnnDims{B, T, IN, H, L}, P, x, order, lengths, work, y, seed, p);
+  DFD_GUARD_END
+}
+
+int dfd_rnn_backward(void* stream, int B, int T, int IN, int H, int L, const float* x, const int64_t* order,
+                     const int64_t* lengths, float* const* params, float* work, float* scratch, const float* dy,
+                     float* const* grads, uint64_t seed, float p) {
+  DFD_GUARD_BEGIN
+  if (!rnn_dims_ok(B, T, IN, H, L)) return -1;
+  if (!x || !params || !work || !scratch || !dy || !grads) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  dfd::RnnParams P{}, G{};
+  if (dfd::rnn_params_from_table(params, L, P) || dfd::rnn_params_from_table(grads, L, G)) return -1;
+  return dfd::rnn_backward((hipStream_t)stream, dfd::RnnDims{B, T, IN, H, L}, P, x, order, lengths, work, scratch, dy,
+                           G, seed, p);
+  DFD_GUARD_END
+}

@@ -66,38 +66,55 @@ __device__ __forceinline__ void st8(bf16* p, const float (&v)[8]) {
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) { ld8(p, v); }
 
 // ---- raw (unconverted) 8-element vectors for register prefetch ----
-// Masked loads are branch-free: the load is always issued (from `safe` when !ok) and the
-// value zero-selected afterwards.  A guarded `if (ok) ld8(...)` compiles to a branch with an
-// s_waitcnt vmcnt(0) per load, which serialises every global round trip of a staging loop.
+// Masked loads are branch-free and wait-free: a masked-off lane loads from `safe` (a valid
+// address of the same tensor) and carries ok = false; the zero is selected when the value is
+// CONSUMED (raw_to_f / raw_st), after the wait the consumer needs anyway.  A guarded
+// `if (ok) ld8(...)`, or zeroing the destination right after the load, makes hipcc emit a
+// branch and an s_waitcnt vmcnt(0) per load, serialising every global round trip.
 template <typename T> struct Raw8;
-template <> struct Raw8<bf16> { uint4 a; };
-template <> struct Raw8<float> { float4 a, b; };
+template <> struct Raw8<bf16> { uint4 a; bool ok; };
+template <> struct Raw8<float> { float4 a, b; bool ok; };
 
 __device__ __forceinline__ void raw_ld(Raw8<bf16>& r, const bf16* p, const bf16* safe, bool ok) {
   r.a = *reinterpret_cast<const uint4*>(ok ? p : safe);
-  if (!ok) r.a = make_uint4(0u, 0u, 0u, 0u);
+  r.ok = ok;
 }
 __device__ __forceinline__ void raw_ld(Raw8<float>& r, const float* p, const float* safe, bool ok) {
   const float* q = ok ? p : safe;
   r.a = *reinterpret_cast<const float4*>(q);
   r.b = *reinterpret_cast<const float4*>(q + 4);
-  if (!ok) { r.a = make_float4(0.f, 0.f, 0.f, 0.f); r.b = r.a; }
+  r.ok = ok;
 }
 __device__ __forceinline__ void raw_to_f(const Raw8<bf16>& r, float (&v)[8]) {
-  v[0] = __uint_as_float(r.a.x << 16); v[1] = __uint_as_float(r.a.x & 0xffff0000u);
-  v[2] = __uint_as_float(r.a.y << 16); v[3] = __uint_as_float(r.a.y & 0xffff0000u);
-  v[4] = __uint_as_float(r.a.z << 16); v[5] = __uint_as_float(r.a.z & 0xffff0000u);
-  v[6] = __uint_as_float(r.a.w << 16); v[7] = __uint_as_float(r.a.w & 0xffff0000u);
+  const uint32_t m = r.ok ? 0xffffffffu : 0u;
+  const uint32_t x = r.a.x & m, y = r.a.y & m, z = r.a.z & m, w = r.a.w & m;
+  v[0] = __uint_as_float(x << 16); v[1] = __uint_as_float(x & 0xffff0000u);
+  v[2] = __uint_as_float(y << 16); v[3] = __uint_as_float(y & 0xffff0000u);
+  v[4] = __uint_as_float(z << 16); v[5] = __uint_as_float(z & 0xffff0000u);
+  v[6] = __uint_as_float(w << 16); v[7] = __uint_as_float(w & 0xffff0000u);
 }
 __device__ __forceinline__ void raw_to_f(const Raw8<float>& r, float (&v)[8]) {
   v[0] = r.a.x; v[1] = r.a.y; v[2] = r.a.z; v[3] = r.a.w;
   v[4] = r.b.x; v[5] = r.b.y; v[6] = r.b.z; v[7] = r.b.w;
+  if (!r.ok) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  }
 }
-__device__ __forceinline__ void raw_st(bf16* p, const Raw8<bf16>& r) { *reinterpret_cast<uint4*>(p) = r.a; }
+__device__ __forceinline__ void raw_st(bf16* p, const Raw8<bf16>& r) {
+  const uint32_t m = r.ok ? 0xffffffffu : 0u;
+  *reinterpret_cast<uint4*>(p) = make_uint4(r.a.x & m, r.a.y & m, r.a.z & m, r.a.w & m);
+}
 __device__ __forceinline__ void raw_st(float* p, const Raw8<float>& r) {
-  *reinterpret_cast<float4*>(p) = r.a;
-  *reinterpret_cast<float4*>(p + 4) = r.b;
+  float v[8];
+  raw_to_f(r, v);
+  st8(p, v);
 }
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global loads (prefetches stay in flight) or stores.  __syncthreads() carries a
+// workgroup-scope fence that drains vmcnt to 0 whenever a global store is pending.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 
 // ---- activations ----
@@ -172,6 +189,8 @@ __device__ __forceinline__ void pro8_pre(float (&v)[8], const float (&sc)[8], co
 }
 
 }  // namespace dfd
+
+#define DFD_TRY(x) do { if ((x) != 0) return -1; } while (0)
 
 #define DFD_HIP_CHECK(expr)                                                     \
   do {                                                                          \

@@ -89,7 +89,7 @@ __device__ __forceinline__ void reduce_write_stats(float (&a)[8], float (&b)[8],
       b[j] += __shfl_xor(b[j], o, 64);
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (lane < 4) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -97,7 +97,7 @@ __device__ __forceinline__ void reduce_write_stats(float (&a)[8], float (&b)[8],
       red[(wave * 2 + 1) * DCG + vec * 8 + j] = b[j];
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 64) {
     const int ch = tid & 31, which = tid >> 5;
     const float s = red[(0 * 2 + which) * DCG + ch] + red[(1 * 2 + which) * DCG + ch] +

@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256, 2) void dw_dgrad_kernel(DwGeom g, const T* __r
     const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
     const int iy0 = ty * TH, ix0 = tx * TW;
     const int gy0 = floordiv(iy0 + g.pad - (K - 1), S), gx0 = floordiv(ix0 + g.pad - (K - 1), S);
-    __syncthreads();
+    lds_barrier();
     stage_tile<T, PRO_NONE, D::GH, D::GW>(tg, dY, f, gy0, gx0, g.Ho, g.Wo, C, c, cok, one, zero);
     // producer pre-BN values of this thread's pixels (masked loads, in flight during the taps)
     Raw8<T> ryp[D::P];
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256, 2) void dw_dgrad_kernel(DwGeom g, const T* __r
       const bool ok = tp + 64 * i < D::NPX && iy < g.H && ix < g.W && cok;
       raw_ld(ryp[i], Yp + (((int64_t)f * g.H + iy) * g.W + ix) * C + c, Yp, ok);
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < D::P; ++i) {
       const int iy = iy0 + ly[i], ix = ix0 + lx[i];

@@ -44,10 +44,10 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
     const int f = t / tpf, r = t - (t / tpf) * tpf;
     const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
     const int oy0 = ty * TH, ox0 = tx * TW;
-    __syncthreads();
+    lds_barrier();
     stage_tile<T, PRO_BN_SILU, D::IH, D::IW>(tin, X, f, oy0 * S - g.pad, ox0 * S - g.pad, g.H, g.W, C, c, cok, sc,
                                              sh);
-    __syncthreads();
+    lds_barrier();
     float acc[D::P][8];
 #pragma unroll
     for (int i = 0; i < D::P; ++i)

@@ -42,11 +42,11 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwGeom g, const T* __r
     const int f = t / tpf, r = t - (t / tpf) * tpf;
     const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
     const int oy0 = ty * TH, ox0 = tx * TW;
-    __syncthreads();
+    lds_barrier();
     stage_tile<T, PRO_BN_SILU, D::IH, D::IW>(tin, X, f, oy0 * S - g.pad, ox0 * S - g.pad, g.H, g.W, C, c, cok, sc,
                                              sh);
     stage_tile<T, PRO_NONE, TH, TW>(tg, dY, f, oy0, ox0, g.Ho, g.Wo, C, c, cok, one, zero);
-    __syncthreads();
+    lds_barrier();
     if (active) {
 #pragma unroll 4
       for (int p = sub; p < D::NPX; p += NSUB) {
@@ -59,13 +59,13 @@ __global__ __launch_bounds__(256, 2) void dw_wgrad_kernel(DwGeom g, const T* __r
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   float* red = tin;  // [NSUB][KK][32] <= NIN*32
   if (active) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[(sub * KK + tap) * DCG + vec * 8 + j] = acc[j];
   }
-  __syncthreads();
+  lds_barrier();
   float* out = slab + (int64_t)(blockIdx.x / groups) * C * KK;
   for (int i = tid; i < KK * DCG; i += 256) {
     const int tp2 = i / DCG, cl = i - tp2 * DCG;

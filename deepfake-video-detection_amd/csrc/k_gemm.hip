@@ -41,7 +41,7 @@ template <typename T, int MODE, bool STATS, bool RESID>
 __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                       T* __restrict__ C, const T* __restrict__ R, int64_t M,
                                                       int N, int K, Pro pro, float* __restrict__ stats,
-                                                      int64_t tiles_m) {
+                                                      int64_t tiles_m, int ntn) {
   using G = GemmCfg<T>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   __shared__ float st_sum[GBN];
@@ -51,7 +51,11 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
   T* Cs = reinterpret_cast<T*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.y * GBN;
+  // 1-D grid, N tile fastest: the ntn workgroups that share an A row-tile are adjacent in
+  // dispatch order, so A is read from HBM once and from L2 by the others.
+  const int nt = (int)(blockIdx.x % ntn);
+  const int64_t mg = blockIdx.x / ntn, mstep = gridDim.x / ntn;
+  const int n0 = nt * GBN;
   const int nvalid = min(GBN, N - n0);
   const int nb = (nvalid + 15) >> 4;
   if constexpr (STATS) {
@@ -69,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
       pro_lds[i] = pro.scale[i];
       pro_lds[K + i] = pro.shift[i];
     }
-    __syncthreads();
+    lds_barrier();
   }
   auto load = [&](int64_t m0, int k0) {
     const int gk = k0 + skc;
@@ -95,8 +99,8 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
 
   // The first k-step of the NEXT tile is loaded before this tile's epilogue stores: vmcnt
   // counts loads and stores together, so loads issued after the stores would wait for them.
-  if ((int64_t)blockIdx.x < tiles_m) load((int64_t)blockIdx.x * GBM, 0);
-  for (int64_t mt = blockIdx.x; mt < tiles_m; mt += gridDim.x) {
+  if (mg < tiles_m) load(mg * GBM, 0);
+  for (int64_t mt = mg; mt < tiles_m; mt += mstep) {
     const int64_t m0 = mt * GBM;
     f32x4_t acc[2][8];
 #pragma unroll
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
 #pragma unroll
       for (int b = 0; b < 8; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    if (MODE != PRO_NONE && mt != (int64_t)blockIdx.x) load(m0, 0);
+    if (MODE != PRO_NONE && mt != mg) load(m0, 0);
     for (int k0 = 0; k0 < K; k0 += GBK) {
       // ---- registers -> LDS (A through the consumer-side BN/SiLU/gate prologue) ----
 #pragma unroll
@@ -132,9 +136,9 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
         }
         raw_st(Bs + row * G::AS + skc, rb[i]);
       }
-      __syncthreads();
+      lds_barrier();
       if (k0 + GBK < K) load(m0, k0 + GBK);
-      else if (MODE == PRO_NONE && mt + gridDim.x < tiles_m) load((mt + gridDim.x) * GBM, 0);
+      else if (MODE == PRO_NONE && mt + mstep < tiles_m) load((mt + mstep) * GBM, 0);
       // ---- MFMA (partial N tiles are zero padded: the sequence is unconditional) ----
       if constexpr (sizeof(T) == 2) {
         bf16x8_t af[2];
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
 
     // ---- epilogue: round, BN-stat partials, stage C tile in LDS ----
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     const int vpr = nvalid >> 3;
     for (int v = tid; v < GBM * vpr; v += 256) {
       const int row = v / vpr, cv = (v - row * vpr) * 8;
@@ -211,12 +215,12 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
       }
       st8(C + gm * N + n0 + cv, x);
     }
-    __syncthreads();
+    lds_barrier();
   }
   if constexpr (STATS) {
     for (int i = tid; i < nvalid; i += 256) {
-      stats[((int64_t)blockIdx.x * 2 + 0) * N + n0 + i] = st_sum[i];
-      stats[((int64_t)blockIdx.x * 2 + 1) * N + n0 + i] = st_sq[i];
+      stats[(mg * 2 + 0) * N + n0 + i] = st_sum[i];
+      stats[(mg * 2 + 1) * N + n0 + i] = st_sq[i];
     }
   }
 }
@@ -231,11 +235,12 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
   const int64_t tiles_m = cdiv64(M, GBM);
   const int64_t cap = std::max<int64_t>(1, 1024 / ntn);
   const int gx = (int)std::min<int64_t>(tiles_m, cap);
-  dim3 grid(gx, ntn), block(256);
+  dim3 grid((unsigned)(gx * ntn)), block(256);
   const bool st = stats != nullptr, rs = R != nullptr;
   const size_t dyn = pro_mode != PRO_NONE ? 2 * (size_t)K * sizeof(float) : 0;
 #define DFD_GEMM_LAUNCH(MODE, ST, RS) \
-  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, RS>), grid, block, dyn, s, A, B, C, R, M, N, K, pro, stats, tiles_m)
+  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, RS>), grid, block, dyn, s, A, B, C, R, M, N, K, pro, stats, tiles_m, \
+                     ntn)
   if (rs) {
     if (pro_mode != PRO_NONE || st) { set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__); return -1; }
     DFD_GEMM_LAUNCH(PRO_NONE, false, true);
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
   float* red = reinterpret_cast<float*>(smem);
 #pragma unroll 1
   for (int w = 0; w < 4; ++w) {
-    __syncthreads();
+    lds_barrier();
     if (wave == w) {
 #pragma unroll
       for (int nb_ = 0; nb_ < 4; ++nb_)
@@ -399,7 +404,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
           }
     }
   }
-  __syncthreads();
+  lds_barrier();
   float* out = slab + (int64_t)blockIdx.y * N * K;
   for (int i = tid; i < WT * WT; i += 256) {
     const int nn = i / WT, kk = i - nn * WT;

@@ -52,20 +52,20 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
       const int e = lane + 64 * i, rr = e >> 6, kk = e & 63, k = k0 + kk;
       const int r = r0 + rr, o = o0 + rr;
       const bool xok = r < R && k < ke, wok = o < O && k < ke;
-      float x = X[xok ? (int64_t)r * I + k : 0];
-      if (p > 0.f && xok) x *= drop_mul(seed, stream, (int64_t)r * I + k, p);
-      nx[i] = xok ? x : 0.f;
-      const float w = W[wok ? (int64_t)o * I + k : 0];
-      nw[i] = wok ? w : 0.f;
+      nx[i] = *(xok ? X + (int64_t)r * I + k : X);  // masked / dropout-scaled when staged
+      nw[i] = *(wok ? W + (int64_t)o * I + k : W);
     }
   };
   if (kb < ke) load(kb);
   for (int k0 = kb; k0 < ke; k0 += LKC) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int e = lane + 64 * i;
-      xs[wave][e >> 6][e & 63] = nx[i];
-      ws[wave][e >> 6][e & 63] = nw[i];
+      const int e = lane + 64 * i, rr = e >> 6, kk = e & 63;
+      const bool xok = r0 + rr < R && k0 + kk < ke, wok = o0 + rr < O && k0 + kk < ke;
+      float x = xok ? nx[i] : 0.f;
+      if (p > 0.f && xok) x *= drop_mul(seed, stream, (int64_t)(r0 + rr) * I + k0 + kk, p);
+      xs[wave][rr][kk] = x;
+      ws[wave][rr][kk] = wok ? nw[i] : 0.f;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -1,0 +1,672 @@
+// LogicRNNLSTM (src/RNNModel.py:5-147) on gfx950, fp32 throughout (the reference is fp32).
+//
+// Forward per timestep t, layer l (RNNModel.py:103-115; all layers share one (h, c) per step):
+//   u = [x_l, h_l];  a = sig(Wa u), o_ = sig(Wo u), n = tanh(Wn h_l), f = sig(Wf u), i = sig(Wi u),
+//   g = tanh(Wg u);  cn = f*c + i*g;  cl = a*cn + o_*n;  out = sig(Wout u);  h' = out * tanh(cl)
+// with x_0 = x_t, h_0 = h_{t-1}, c_0 = c_{t-1} (the LAST layer's state of step t-1), and for
+// l >= 1: x_l = h_l = dropout(h'_{l-1}) (the reference passes h_temp as both arguments), c_l = cl_{l-1}.
+// Hence layer 0 = precomputed x-projection (one GEMM over all B*T rows) + h @ P0^T with
+// P0 = [Wa..Wout h-columns ; Wn] (7H x H), and layer l >= 1 = h @ Pl^T with Pl = [(Wx + Wh) ; Wn].
+//
+// Kernels: sgemm_kernel<TA,TB> (fp32 v_mfma_f32_16x16x4f32, exact fp32 products, 64x64 tiles,
+// LDS-staged with coalesced loads along the contiguous dimension of either operand layout),
+// rnn_cell_fwd/bwd (fused gate nonlinearities + cell algebra + saved activations),
+// rnn_attn_* (attention pooling over T), weight pack/scatter, column sums.
+#include "kernels.h"
+#include "rnn.h"
+
+namespace dfd {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ fp32 MFMA GEMM
+// C[m][n] = beta*C[m][n] + sum_k A(m,k) B(n,k) (+ bias[n]),  A(m,k) = TA ? A[k*lda+m] : A[m*lda+k],
+// B(n,k) = TB ? B[k*ldb+n] : B[n*ldb+k].  64x64 tile per 256-thread block, BK = 16; wave w owns
+// rows 32*(w>>1).. and cols 32*(w&1).. (2x2 MFMA 16x16 blocks).
+constexpr int SG_T = 64, SG_K = 16;
+
+template <bool T_>
+__device__ __forceinline__ void sg_load(const float* __restrict__ P, int ld, int r0, int k0, int R, int K, float (&v)[4],
+                                        bool (&ok)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + 256 * i;
+    int r, k;
+    if (T_) { k = e / SG_T; r = e % SG_T; }   // contiguous along r
+    else { r = e / SG_K; k = e % SG_K; }      // contiguous along k
+    const int gr = r0 + r, gk = k0 + k;
+    ok[i] = gr < R && gk < K;
+    const float* q = T_ ? P + (int64_t)gk * ld + gr : P + (int64_t)gr * ld + gk;
+    v[i] = *(ok[i] ? q : P);
+  }
+}
+template <bool T_>
+__device__ __forceinline__ void sg_store(float (*S)[SG_K + 1], const float (&v)[4], const bool (&ok)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + 256 * i;
+    int r, k;
+    if (T_) { k = e / SG_T; r = e % SG_T; }
+    else { r = e / SG_K; k = e % SG_K; }
+    S[r][k] = ok[i] ? v[i] : 0.f;
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void sgemm_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                    int ldb, float* __restrict__ C, int ldc, int M, int N, int K,
+                                                    float beta, const float* __restrict__ bias) {
+  __shared__ float As[SG_T][SG_K + 1], Bs[SG_T][SG_K + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.y * SG_T, n0 = blockIdx.x * SG_T;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float va[4], vb[4];
+  bool oa[4], ob[4];
+  sg_load<TA>(A, lda, m0, 0, M, K, va, oa);
+  sg_load<TB>(B, ldb, n0, 0, N, K, vb, ob);
+  for (int k0 = 0; k0 < K; k0 += SG_K) {
+    lds_barrier();
+    sg_store<TA>(As, va, oa);
+    sg_store<TB>(Bs, vb, ob);
+    lds_barrier();
+    if (k0 + SG_K < K) {
+      sg_load<TA>(A, lda, m0, k0 + SG_K, M, K, va, oa);
+      sg_load<TB>(B, ldb, n0, k0 + SG_K, N, K, vb, ob);
+    }
+#pragma unroll
+    for (int s = 0; s < SG_K / 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+      const float a0 = As[wm + (lane & 15)][kk], a1 = As[wm + 16 + (lane & 15)][kk];
+      const float b0 = Bs[wn + (lane & 15)][kk], b1 = Bs[wn + 16 + (lane & 15)][kk];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + a * 16 + 4 * (lane >> 4) + r, n = n0 + wn + b * 16 + (lane & 15);
+        if (m < M && n < N) {
+          float v = acc[a][b][r];
+          if (bias) v += bias[n];
+          float* c = C + (int64_t)m * ldc + n;
+          *c = beta != 0.f ? beta * *c + v : v;
+        }
+      }
+}
+
+int launch_sgemm(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+                 int M, int N, int K, float beta, const float* bias) {
+  if (M <= 0 || N <= 0) return 0;
+  const dim3 grid((unsigned)cdiv(N, SG_T), (unsigned)cdiv(M, SG_T));
+  if (!ta && !tb) hipLaunchKernelGGL((sgemm_kernel<false, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
+  else if (!ta && tb) hipLaunchKernelGGL((sgemm_kernel<false, true>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
+  else if (ta && !tb) hipLaunchKernelGGL((sgemm_kernel<true, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
+  else hipLaunchKernelGGL((sgemm_kernel<true, true>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ float sig_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanh_(float x) { return tanhf(x); }
+
+// dropout keep-scale for element idx of stream `st` (same counter hash as the detector head)
+__device__ __forceinline__ float rnn_drop(uint64_t seed, uint32_t st, int64_t idx, float p) {
+  if (p <= 0.f) return 1.f;
+  uint64_t z = seed ^ ((uint64_t)st << 56) ^ (uint64_t)idx * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+// xs[b][t][:] = x[order[b]][t][:]   (the reference's x[sort_idx], RNNModel.py:92-95)
+__global__ void rnn_gather_kernel(const float* __restrict__ x, const int64_t* __restrict__ order, float* __restrict__ xs,
+                                  int B, int64_t row) {
+  const int64_t n = (int64_t)B * row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int b = (int)(i / row);
+    xs[i] = x[order[b] * row + (i - (int64_t)b * row)];
+  }
+}
+
+// pack the recurrent weights of layer l (rows: a, o_, f, i, g, out gates then not; cols H):
+//   l == 0 : h-columns [in, in+H) of the six u-gates, then Wn
+//   l >= 1 : x-columns + h-columns (x = h = dropout(h_{l-1})), then Wn
+// and (l == 0) the x-columns of the six u-gates into WX0 [6H][in]; biases into bias7 [7H].
+__global__ void rnn_pack_kernel(RnnLayerW w, int in, int H, int layer, float* __restrict__ P, float* __restrict__ WX0,
+                                float* __restrict__ bias7) {
+  const int ld = in + H;
+  const int64_t nP = (int64_t)7 * H * H;
+  const int64_t nX = layer == 0 ? (int64_t)6 * H * in : 0;
+  const int64_t n = nP + nX + 7 * H;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (i < nP) {
+      const int row = (int)(i / H), k = (int)(i - (int64_t)row * H);
+      const int g = row / H, r = row - g * H;
+      float v;
+      if (g == 6) v = w.wn[(int64_t)r * H + k];
+      else {
+        const float* W = w.wu[g] + (int64_t)r * ld;
+        v = layer == 0 ? W[in + k] : W[k] + W[in + k];
+      }
+      P[i] = v;
+    } else if (i < nP + nX) {
+      const int64_t j = i - nP;
+      const int row = (int)(j / in), k = (int)(j - (int64_t)row * in);
+      const int g = row / H, r = row - g * H;
+      WX0[j] = w.wu[g][(int64_t)r * ld + k];
+    } else {
+      const int j = (int)(i - nP - nX), g = j / H, r = j - g * H;
+      bias7[j] = g == 6 ? w.bn[r] : w.bu[g][r];
+    }
+  }
+}
+
+// forward cell of one (step, layer) for all B rows:
+//   z[b][:] = G[b][:] (recurrent, 7H) + X0[b*T+t][:6H] (layer 0) + bias7
+// saved (row = b*T + t): ACT[row][7H] activated gates, CN, CL; outputs h' (+dropout for the
+// next layer's input), c'.
+__global__ void rnn_cell_fwd_kernel(const float* __restrict__ G, const float* __restrict__ X0, const float* __restrict__ bias7,
+                                    const float* __restrict__ c_in, int c_in_ld, int B, int T, int t, int H,
+                                    float* __restrict__ ACT, float* __restrict__ CN, float* __restrict__ CL,
+                                    float* __restrict__ h_out, int h_out_ld, float* __restrict__ c_out,
+                                    float* __restrict__ hd_out, float p, uint64_t seed, uint32_t stream) {
+  const int n = B * H;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int b = i / H, j = i - b * H;
+    const int64_t row = (int64_t)b * T + t;
+    float z[7];
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+      float v = G[(int64_t)b * 7 * H + g * H + j] + bias7[g * H + j];
+      if (X0 && g < 6) v += X0[row * 6 * H + g * H + j];
+      z[g] = v;
+    }
+    const float a = sig_(z[0]), o_ = sig_(z[1]), f = sig_(z[2]), ii = sig_(z[3]), gg = tanh_(z[4]), ou = sig_(z[5]);
+    const float nn = tanh_(z[6]);
+    const float c = c_in[(int64_t)b * c_in_ld + j];
+    const float cn = f * c + ii * gg;
+    const float cl = a * cn + o_ * nn;
+    const float h = ou * tanh_(cl);
+    float* act = ACT + row * 7 * H;
+    act[0 * H + j] = a; act[1 * H + j] = o_; act[2 * H + j] = f; act[3 * H + j] = ii;
+    act[4 * H + j] = gg; act[5 * H + j] = ou; act[6 * H + j] = nn;
+    CN[row * H + j] = cn;
+    CL[row * H + j] = cl;
+    h_out[(int64_t)b * h_out_ld + j] = h;
+    c_out[(int64_t)b * H + j] = cl;
+    if (hd_out) hd_out[(int64_t)b * H + j] = h * rnn_drop(seed, stream, row * H + j, p);
+  }
+}
+
+// backward cell: from dh (gradient of h') and dc (gradient of c' = cl) -> dz (7H pre-activation
+// grads, row b*T+t) and dc_in.  dh = dh_a[b] (+ dh_b[b]) , dc = dc_a[b]
+__global__ void rnn_cell_bwd_kernel(const float* __restrict__ dh_a, int dh_a_ld, const float* __restrict__ dh_b,
+                                    const float* __restrict__ dc_a, const float* __restrict__ ACT,
+                                    const float* __restrict__ CN, const float* __restrict__ CL,
+                                    const float* __restrict__ c_in, int c_in_ld, int B, int T, int t, int H,
+                                    float* __restrict__ DZ, float* __restrict__ dc_in) {
+  const int n = B * H;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int b = i / H, j = i - b * H;
+    const int64_t row = (int64_t)b * T + t;
+    float dh = dh_a ? dh_a[(int64_t)b * dh_a_ld + j] : 0.f;
+    if (dh_b) dh += dh_b[(int64_t)b * H + j];
+    const float dcl0 = dc_a ? dc_a[(int64_t)b * H + j] : 0.f;
+    const float* act = ACT + row * 7 * H;
+    const float a = act[0 * H + j], o_ = act[1 * H + j], f = act[2 * H + j], ii = act[3 * H + j];
+    const float gg = act[4 * H + j], ou = act[5 * H + j], nn = act[6 * H + j];
+    const float cn = CN[row * H + j], cl = CL[row * H + j];
+    const float c = c_in[(int64_t)b * c_in_ld + j];
+    const float tc = tanh_(cl);
+    const float dou = dh * tc;
+    const float dcl = dh * ou * (1.f - tc * tc) + dcl0;
+    const float da = dcl * cn, dcn = dcl * a, do_ = dcl * nn, dnn = dcl * o_;
+    const float df = dcn * c, di = dcn * gg, dg = dcn * ii;
+    float* dz = DZ + row * 7 * H;
+    dz[0 * H + j] = da * a * (1.f - a);
+    dz[1 * H + j] = do_ * o_ * (1.f - o_);
+    dz[2 * H + j] = df * f * (1.f - f);
+    dz[3 * H + j] = di * ii * (1.f - ii);
+    dz[4 * H + j] = dg * (1.f - gg * gg);
+    dz[5 * H + j] = dou * ou * (1.f - ou);
+    dz[6 * H + j] = dnn * (1.f - nn * nn);
+    dc_in[(int64_t)b * H + j] = dcn * f;
+  }
+}
+
+// dh *= dropout scale (the inter-layer dropout of RNNModel.py:113-114)
+__global__ void rnn_drop_bwd_kernel(float* __restrict__ dh, int B, int T, int t, int H, float p, uint64_t seed,
+                                    uint32_t stream) {
+  const int n = B * H;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int b = i / H, j = i - b * H;
+    dh[i] *= rnn_drop(seed, stream, ((int64_t)b * T + t) * H + j, p);
+  }
+}
+
+// colsum[n] (+)= sum_m X[m][n]   (bias gradients), one thread per column, fixed row order
+__global__ void rnn_colsum_kernel(const float* __restrict__ X, int M, int N, int ld, float* __restrict__ out, int acc) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f;
+  for (int m = 0; m < M; ++m) a += X[(int64_t)m * ld + n];
+  out[n] = acc ? out[n] + a : a;
+}
+
+// scatter packed gradients back into the per-gate weight gradients of layer l (accumulating)
+__global__ void rnn_scatter_kernel(RnnLayerW gw, int in, int H, int layer, const float* __restrict__ dP,
+                                   const float* __restrict__ dWX0, const float* __restrict__ dbias7) {
+  const int ld = in + H;
+  const int64_t nU = (int64_t)6 * H * ld, nN = (int64_t)H * H;
+  const int64_t n = nU + nN + 7 * H;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (i < nU) {
+      const int grow = (int)(i / ld), k = (int)(i - (int64_t)grow * ld);
+      const int g = grow / H, r = grow - g * H;
+      float v;
+      if (layer == 0) v = k < in ? dWX0[(int64_t)(g * H + r) * in + k] : dP[(int64_t)(g * H + r) * H + (k - in)];
+      else v = dP[(int64_t)(g * H + r) * H + (k < in ? k : k - in)];
+      gw.wu[g][(int64_t)r * ld + k] = v;
+    } else if (i < nU + nN) {
+      const int64_t j = i - nU;
+      gw.wn[j] = dP[(int64_t)6 * H * H + j];
+    } else {
+      const int j = (int)(i - nU - nN), g = j / H, r = j - g * H;
+      if (g == 6) gw.bn[r] = dbias7[j];
+      else gw.bu[g][r] = dbias7[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ attention + classifier
+// Om[b][t][:] = O * (t < len[b]);  E = tanh(Om W1^T + b1) (GEMM + tanh in place);
+// s[b][t] = E . w2 + b2 ; a = softmax_t(s) ; ctx[b] = sum_t a * Om
+__global__ void rnn_mask_kernel(const float* __restrict__ O, const int64_t* __restrict__ len, float* __restrict__ Om,
+                                int B, int T, int H) {
+  const int64_t n = (int64_t)B * T * H;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / H;
+    const int b = (int)(row / T), t = (int)(row - (int64_t)b * T);
+    Om[i] = (len == nullptr || t < len[b]) ? O[i] : 0.f;
+  }
+}
+__global__ void rnn_tanh_kernel(float* __restrict__ X, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) X[i] = tanh_(X[i]);
+}
+// one block per clip: scores, softmax over T, context
+__global__ void rnn_attn_fwd_kernel(const float* __restrict__ Om, const float* __restrict__ E,
+                                    const float* __restrict__ w2, const float* __restrict__ b2, int T, int H,
+                                    float* __restrict__ att, float* __restrict__ ctx) {
+  extern __shared__ float sh[];  // [T]
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int t = wave; t < T; t += 4) {
+    const float* e = E + ((int64_t)b * T + t) * H;
+    float a = 0.f;
+    for (int j = lane; j < H; j += 64) a += e[j] * w2[j];
+    a = wave_sum(a);
+    if (lane == 0) sh[t] = a + b2[0];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float mx = -INFINITY;
+    for (int t = 0; t < T; ++t) mx = fmaxf(mx, sh[t]);
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) { sh[t] = __expf(sh[t] - mx); s += sh[t]; }
+    for (int t = 0; t < T; ++t) { sh[t] /= s; att[(int64_t)b * T + t] = sh[t]; }
+  }
+  __syncthreads();
+  for (int j = tid; j < H; j += 256) {
+    float a = 0.f;
+    for (int t = 0; t < T; ++t) a += sh[t] * Om[((int64_t)b * T + t) * H + j];
+    ctx[(int64_t)b * H + j] = a;
+  }
+}
+// classifier tail: h1 = relu(ctx W1^T + b1) (GEMM, then this kernel), dropout, z = h1d . w2 + b2, y = sigmoid(z)
+__global__ void rnn_cls_fwd_kernel(float* __restrict__ h1, const float* __restrict__ w2, const float* __restrict__ b2,
+                                   int H, float p, uint64_t seed, float* __restrict__ y) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ float red[4];
+  float a = 0.f;
+  for (int j = tid; j < H; j += 256) {
+    float v = fmaxf(h1[(int64_t)b * H + j], 0.f);
+    h1[(int64_t)b * H + j] = v;  // relu in place (saved for backward)
+    a += v * rnn_drop(seed, 9u, (int64_t)b * H + j, p) * w2[j];
+  }
+  a = wave_sum(a);
+  if (lane == 0) red[wave] = a;
+  __syncthreads();
+  if (tid == 0) {
+    const float z = red[0] + red[1] + red[2] + red[3] + b2[0];
+    y[b] = sig_(z);
+  }
+}
+
+// backward of the tail: dy -> dz = dy*y*(1-y) ; dw2 = sum_b dz*h1d ; db2 ; dh1 = dz*w2*drop*relu'
+__global__ void rnn_cls_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ h1,
+                                   const float* __restrict__ w2, int B, int H, float p, uint64_t seed,
+                                   float* __restrict__ dh1, float* __restrict__ gw2, float* __restrict__ gb2) {
+  // one thread per hidden unit j (and b loop) for gw2; dh1 per (b, j)
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < H) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float dz = dy[b] * y[b] * (1.f - y[b]);
+      const float d = rnn_drop(seed, 9u, (int64_t)b * H + j, p);
+      a += dz * h1[(int64_t)b * H + j] * d;
+      dh1[(int64_t)b * H + j] = h1[(int64_t)b * H + j] > 0.f ? dz * w2[j] * d : 0.f;
+    }
+    gw2[j] = a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += dy[b] * y[b] * (1.f - y[b]);
+    gb2[0] = a;
+  }
+}
+
+// attention backward, one block per clip:
+//   dctx[b] -> dOm += a_t * dctx ; da_t = dctx . Om_t ; ds = a*(da - sum a*da) ;
+//   dE[b][t][:] = ds_t * w2 * (1 - E^2)  ; gw2 += ds_t * E ; gb2 += ds_t
+__global__ void rnn_attn_bwd_kernel(const float* __restrict__ Om, const float* __restrict__ E,
+                                    const float* __restrict__ att, const float* __restrict__ dctx,
+                                    const float* __restrict__ w2, int T, int H, float* __restrict__ dOm,
+                                    float* __restrict__ dE, float* __restrict__ ds_out) {
+  extern __shared__ float sh[];  // [2T]
+  float* da = sh;
+  float* ds = sh + T;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int t = wave; t < T; t += 4) {
+    const float* o = Om + ((int64_t)b * T + t) * H;
+    float a = 0.f;
+    for (int j = lane; j < H; j += 64) a += dctx[(int64_t)b * H + j] * o[j];
+    a = wave_sum(a);
+    if (lane == 0) da[t] = a;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += att[(int64_t)b * T + t] * da[t];
+    for (int t = 0; t < T; ++t) {
+      const float a = att[(int64_t)b * T + t];
+      ds[t] = a * (da[t] - s);
+      ds_out[(int64_t)b * T + t] = ds[t];
+    }
+  }
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const float a = att[(int64_t)b * T + t];
+    for (int j = tid; j < H; j += 256) {
+      const int64_t idx = ((int64_t)b * T + t) * H + j;
+      dOm[idx] = a * dctx[(int64_t)b * H + j];
+      const float e = E[idx];
+      dE[idx] = ds[t] * w2[j] * (1.f - e * e);
+    }
+  }
+}
+// gw2[j] = sum_{b,t} ds[b][t] * E[b][t][j] ; gb2 = sum ds
+__global__ void rnn_attn_w2_kernel(const float* __restrict__ E, const float* __restrict__ ds, int BT, int H,
+                                   float* __restrict__ gw2, float* __restrict__ gb2) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < H) {
+    float a = 0.f;
+    for (int r = 0; r < BT; ++r) a += ds[r] * E[(int64_t)r * H + j];
+    gw2[j] = a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float a = 0.f;
+    for (int r = 0; r < BT; ++r) a += ds[r];
+    gb2[0] = a;
+  }
+}
+// dO = (dOm_ctx + dOm_att) * mask   (in place into dOm)
+__global__ void rnn_mask_bwd_kernel(float* __restrict__ dOm, const float* __restrict__ dOm2, const int64_t* __restrict__ len,
+                                    int B, int T, int H) {
+  const int64_t n = (int64_t)B * T * H;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i / H;
+    const int b = (int)(row / T), t = (int)(row - (int64_t)b * T);
+    const float v = dOm[i] + dOm2[i];
+    dOm[i] = (len == nullptr || t < len[b]) ? v : 0.f;
+  }
+}
+
+static int ew_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 2048)); }
+
+// ------------------------------------------------------------------ host orchestration
+int64_t rnn_work_floats(const RnnDims& d) {
+  const int64_t BT = (int64_t)d.B * d.T, H = d.H;
+  int64_t n = 0;
+  n += BT * d.IN;                          // xs (sorted input)
+  n += BT * 6 * H;                         // X0 (layer-0 x projection)
+  n += (int64_t)d.B * 7 * H;               // G (one step's recurrent gates)
+  n += (int64_t)d.L * (7 * H * H + 7 * H); // packed weights + biases per layer
+  n += 6 * H * d.IN;                       // WX0
+  n += (int64_t)d.L * BT * (7 * H + 4 * H); // per layer ACT, CN, CL, UH (hidden input), CI (c input)
+  n += BT * H * 3;                         // O (outputs), Om, E
+  n += BT * 2 + (int64_t)d.B * H * 3 + d.B; // att, (spare), ctx, h1, spare, y
+  n += (int64_t)d.B * H * 4;               // h/c state ping-pong
+  return n + 64;
+}
+
+struct RnnWs {
+  float *xs, *X0, *G, *P[8], *bias7[8], *WX0, *ACT[8], *CN[8], *CL[8], *UH[8], *CI[8], *O, *Om, *E, *att, *ctx, *h1,
+      *y, *st;
+};
+static RnnWs rnn_ws(const RnnDims& d, float* w) {
+  RnnWs s{};
+  const int64_t BT = (int64_t)d.B * d.T, H = d.H;
+  float* p = w;
+  auto take = [&](int64_t n) { float* r = p; p += (n + 63) & ~int64_t(63); return r; };
+  s.xs = take(BT * d.IN);
+  s.X0 = take(BT * 6 * H);
+  s.G = take((int64_t)d.B * 7 * H);
+  for (int l = 0; l < d.L; ++l) { s.P[l] = take(7 * H * H); s.bias7[l] = take(7 * H); }
+  s.WX0 = take(6 * H * d.IN);
+  for (int l = 0; l < d.L; ++l) {
+    s.ACT[l] = take(BT * 7 * H); s.CN[l] = take(BT * H); s.CL[l] = take(BT * H); s.UH[l] = take(BT * H);
+    s.CI[l] = take(BT * H);
+  }
+  s.O = take(BT * H); s.Om = take(BT * H); s.E = take(BT * H);
+  s.att = take(BT); take(BT);
+  s.ctx = take((int64_t)d.B * H); s.h1 = take((int64_t)d.B * H); take((int64_t)d.B * H);
+  s.y = take(d.B);
+  s.st = take((int64_t)d.B * H * 4);
+  return s;
+}
+
+int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,
+                const int64_t* lens, float* work, float* y, uint64_t seed, float p) {
+  if (d.L < 1 || d.L > 8) { set_error("rnn: 1..8 layers supported", __FILE__, __LINE__); return -1; }
+  const int B = d.B, T = d.T, H = d.H, IN = d.IN;
+  const int64_t BT = (int64_t)B * T;
+  RnnWs w = rnn_ws(d, work);
+  // (sorted) input
+  const float* xs = x;
+  if (order) {
+    hipLaunchKernelGGL(rnn_gather_kernel, dim3(ew_blocks(BT * IN)), dim3(256), 0, s, x, order, w.xs, B, (int64_t)T * IN);
+    xs = w.xs;
+  }
+  for (int l = 0; l < d.L; ++l)
+    hipLaunchKernelGGL(rnn_pack_kernel, dim3(ew_blocks((int64_t)7 * H * H + (l == 0 ? 6LL * H * IN : 0) + 7 * H)),
+                       dim3(256), 0, s, P.layer[l], l == 0 ? IN : H, H, l, w.P[l], w.WX0, w.bias7[l]);
+  DFD_HIP_CHECK(hipGetLastError());
+  // layer-0 x projection for all rows (b*T + t)
+  DFD_TRY(launch_sgemm(s, false, false, xs, IN, w.WX0, IN, w.X0, 6 * H, (int)BT, 6 * H, IN, 0.f, nullptr));
+  float* h = w.st;                       // [B][H] state of the last layer, previous step
+  float* c = w.st + (int64_t)B * H;
+  float* hd = w.st + 2LL * B * H;        // dropped-out inter-layer h
+  float* ctmp = w.st + 3LL * B * H;
+  DFD_HIP_CHECK(hipMemsetAsync(h, 0, sizeof(float) * 2 * B * H, s));
+  const int eb = ew_blocks((int64_t)B * H);
+  for (int t = 0; t < T; ++t) {
+    for (int l = 0; l < d.L; ++l) {
+      const float* hin = l == 0 ? h : hd;      // layer input hidden (== x for l >= 1)
+      const float* cin = l == 0 ? c : ctmp;
+      // save inputs for backward (row b*T+t)
+      DFD_HIP_CHECK(hipMemcpy2DAsync(w.UH[l] + (int64_t)t * H, (size_t)T * H * 4, hin, (size_t)H * 4, (size_t)H * 4, B,
+                                     hipMemcpyDeviceToDevice, s));
+      DFD_HIP_CHECK(hipMemcpy2DAsync(w.CI[l] + (int64_t)t * H, (size_t)T * H * 4, cin, (size_t)H * 4, (size_t)H * 4, B,
+                                     hipMemcpyDeviceToDevice, s));
+      DFD_TRY(launch_sgemm(s, false, false, hin, H, w.P[l], H, w.G, 7 * H, B, 7 * H, H, 0.f, nullptr));
+      const bool last = l == d.L - 1;
+      // outputs: last layer -> O[b][t] (ld T*H) and state h (copied below); others -> hd (dropout)
+      if (last) {
+        hipLaunchKernelGGL(rnn_cell_fwd_kernel, dim3(eb), dim3(256), 0, s, w.G, l == 0 ? w.X0 : nullptr, w.bias7[l], cin,
+                           H, B, T, t, H, w.ACT[l], w.CN[l], w.CL[l], w.O + (int64_t)t * H, T * H, ctmp, nullptr, p,
+                           seed, (uint32_t)l);
+      } else {
+        // raw h' of a non-last layer is only consumed through dropout (hd); c' -> ctmp
+        hipLaunchKernelGGL(rnn_cell_fwd_kernel, dim3(eb), dim3(256), 0, s, w.G, l == 0 ? w.X0 : nullptr, w.bias7[l], cin,
+                           H, B, T, t, H, w.ACT[l], w.CN[l], w.CL[l], w.h1, H, ctmp, hd, p, seed, (uint32_t)l);
+      }
+      DFD_HIP_CHECK(hipGetLastError());
+    }
+    // state for the next step = last layer's (h', c')
+    DFD_HIP_CHECK(hipMemcpy2DAsync(h, (size_t)H * 4, w.O + (int64_t)t * H, (size_t)T * H * 4, (size_t)H * 4, B,
+                                   hipMemcpyDeviceToDevice, s));
+    DFD_HIP_CHECK(hipMemcpyAsync(c, ctmp, sizeof(float) * B * H, hipMemcpyDeviceToDevice, s));
+  }
+  // mask, attention, classifier
+  hipLaunchKernelGGL(rnn_mask_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, w.O, lens, w.Om, B, T, H);
+  DFD_TRY(launch_sgemm(s, false, false, w.Om, H, P.att_w1, H, w.E, H, (int)BT, H, H, 0.f, P.att_b1));
+  hipLaunchKernelGGL(rnn_tanh_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, w.E, BT * H);
+  hipLaunchKernelGGL(rnn_attn_fwd_kernel, dim3(B), dim3(256), T * sizeof(float), s, w.Om, w.E, P.att_w2, P.att_b2, T, H,
+                     w.att, w.ctx);
+  DFD_TRY(launch_sgemm(s, false, false, w.ctx, H, P.cls_w1, H, w.h1, H, B, H, H, 0.f, P.cls_b1));
+  hipLaunchKernelGGL(rnn_cls_fwd_kernel, dim3(B), dim3(256), 0, s, w.h1, P.cls_w2, P.cls_b2, H, p, seed, w.y);
+  DFD_HIP_CHECK(hipGetLastError());
+  DFD_HIP_CHECK(hipMemcpyAsync(y, w.y, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,
+                 const int64_t* lens, float* work, float* scratch, const float* dy, RnnParams& Gr, uint64_t seed,
+                 float p) {
+  const int B = d.B, T = d.T, H = d.H, IN = d.IN;
+  const int64_t BT = (int64_t)B * T;
+  RnnWs w = rnn_ws(d, work);
+  // scratch layout: dh1 [B][H], dctx [B][H], dE [BT][H], dOm [BT][H], dOm2 [BT][H], ds [BT],
+  //                 DZ per layer [BT][7H], dP [7H][H], dWX0 [6H][IN], dbias [7H], dh/dc state
+  float* q = scratch;
+  auto take = [&](int64_t n) { float* r = q; q += (n + 63) & ~int64_t(63); return r; };
+  float* dh1 = take((int64_t)B * H);
+  float* dctx = take((int64_t)B * H);
+  float* dE = take(BT * H);
+  float* dOm = take(BT * H);
+  float* dOm2 = take(BT * H);
+  float* ds = take(BT);
+  float* DZ[8];
+  for (int l = 0; l < d.L; ++l) DZ[l] = take(BT * 7 * H);
+  float* dP = take((int64_t)7 * H * H);
+  float* dWX0 = take((int64_t)6 * H * IN);
+  float* dbias = take(7 * H);
+  float* dh = take((int64_t)B * H);      // gradient into the last layer's h' of the current step
+  float* dc = take((int64_t)B * H);      // gradient into the last layer's c'
+  float* dhl = take((int64_t)B * H);     // gradient into an inner layer's output (through dropout)
+  float* dcl = take((int64_t)B * H);
+  float* dcin = take((int64_t)B * H);
+  // classifier tail
+  const dim3 gH((unsigned)cdiv(H, 256));
+  hipLaunchKernelGGL(rnn_cls_bwd_kernel, gH, dim3(256), 0, s, dy, w.y, w.h1, P.cls_w2, B, H, p, seed, dh1, Gr.cls_w2,
+                     Gr.cls_b2);
+  DFD_TRY(launch_sgemm(s, true, true, dh1, H, w.ctx, H, Gr.cls_w1, H, H, H, B, 0.f, nullptr));   // dW1 = dh1^T ctx
+  hipLaunchKernelGGL(rnn_colsum_kernel, gH, dim3(256), 0, s, dh1, B, H, H, Gr.cls_b1, 0);
+  DFD_TRY(launch_sgemm(s, false, true, dh1, H, P.cls_w1, H, dctx, H, B, H, H, 0.f, nullptr));     // dctx = dh1 W1
+  // attention
+  hipLaunchKernelGGL(rnn_attn_bwd_kernel, dim3(B), dim3(256), 2 * T * sizeof(float), s, w.Om, w.E, w.att, dctx,
+                     P.att_w2, T, H, dOm, dE, ds);
+  hipLaunchKernelGGL(rnn_attn_w2_kernel, gH, dim3(256), 0, s, w.E, ds, (int)BT, H, Gr.att_w2, Gr.att_b2);
+  DFD_TRY(launch_sgemm(s, true, true, dE, H, w.Om, H, Gr.att_w1, H, H, H, (int)BT, 0.f, nullptr));  // dWa1 = dE^T Om
+  hipLaunchKernelGGL(rnn_colsum_kernel, gH, dim3(256), 0, s, dE, (int)BT, H, H, Gr.att_b1, 0);
+  DFD_TRY(launch_sgemm(s, false, true, dE, H, P.att_w1, H, dOm2, H, (int)BT, H, H, 0.f, nullptr));  // dOm2 = dE Wa1
+  hipLaunchKernelGGL(rnn_mask_bwd_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, dOm, dOm2, lens, B, T, H);
+  DFD_HIP_CHECK(hipGetLastError());
+  // BPTT
+  DFD_HIP_CHECK(hipMemsetAsync(dh, 0, sizeof(float) * B * H, s));
+  DFD_HIP_CHECK(hipMemsetAsync(dc, 0, sizeof(float) * B * H, s));
+  const int eb = ew_blocks((int64_t)B * H);
+  for (int t = T - 1; t >= 0; --t) {
+    for (int l = d.L - 1; l >= 0; --l) {
+      const bool last = l == d.L - 1;
+      // gradient of this layer's h' and c'
+      const float* gh_a = last ? dOm + (int64_t)t * H : dhl;
+      const int gh_ld = last ? T * H : H;
+      const float* gh_b = last ? dh : nullptr;
+      const float* gc = last ? dc : dcl;
+      hipLaunchKernelGGL(rnn_cell_bwd_kernel, dim3(eb), dim3(256), 0, s, gh_a, gh_ld, gh_b, gc, w.ACT[l], w.CN[l],
+                         w.CL[l], w.CI[l] + (int64_t)t * H, T * H, B, T, t, H, DZ[l], dcin);
+      DFD_HIP_CHECK(hipGetLastError());
+      // gradient into the layer's hidden input: dz (rows b*T+t) @ P_l
+      float* dst = l == 0 ? dh : dhl;
+      DFD_TRY(launch_sgemm(s, false, true, DZ[l] + (int64_t)t * 7 * H, T * 7 * H, w.P[l], H, dst, H, B, H, 7 * H, 0.f,
+                           nullptr));
+      if (l > 0) {
+        // into layer l-1's output through the inter-layer dropout; its c' gradient = dc_in
+        hipLaunchKernelGGL(rnn_drop_bwd_kernel, dim3(eb), dim3(256), 0, s, dhl, B, T, t, H, p, seed, (uint32_t)(l - 1));
+        DFD_HIP_CHECK(hipMemcpyAsync(dcl, dcin, sizeof(float) * B * H, hipMemcpyDeviceToDevice, s));
+      } else {
+        DFD_HIP_CHECK(hipMemcpyAsync(dc, dcin, sizeof(float) * B * H, hipMemcpyDeviceToDevice, s));
+      }
+    }
+  }
+  // weight gradients, one GEMM per layer over all B*T rows
+  for (int l = 0; l < d.L; ++l) {
+    // dP[7H][H] = DZ^T UH ; dWX0[6H][IN] = DZ[:, :6H]^T X   (sums over all B*T rows)
+    DFD_TRY(launch_sgemm(s, true, true, DZ[l], 7 * H, w.UH[l], H, dP, H, 7 * H, H, (int)BT, 0.f, nullptr));
+    if (l == 0)
+      DFD_TRY(launch_sgemm(s, true, true, DZ[0], 7 * H, order ? w.xs : x, IN, dWX0, IN, 6 * H, IN, (int)BT, 0.f,
+                           nullptr));
+    hipLaunchKernelGGL(rnn_colsum_kernel, dim3((unsigned)cdiv(7 * H, 256)), dim3(256), 0, s, DZ[l], (int)BT, 7 * H,
+                       7 * H, dbias, 0);
+    hipLaunchKernelGGL(rnn_scatter_kernel, dim3(ew_blocks((int64_t)6 * H * (IN + H) + (int64_t)H * H + 7 * H)),
+                       dim3(256), 0, s, Gr.layer[l], l == 0 ? IN : H, H, l, dP, dWX0, dbias);
+    DFD_HIP_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+int rnn_params_from_table(float* const* t, int L, RnnParams& P) {
+  if (L < 1 || L > 8) { set_error("rnn: 1..8 layers supported", __FILE__, __LINE__); return -1; }
+  // named_parameters() order of LogicCell: and, or, not, forget, input, cell, output (weight, bias)
+  for (int l = 0; l < L; ++l) {
+    float* const* q = t + 14 * l;
+    RnnLayerW& w = P.layer[l];
+    w.wu[0] = q[0]; w.bu[0] = q[1];    // and
+    w.wu[1] = q[2]; w.bu[1] = q[3];    // or
+    w.wn = q[4]; w.bn = q[5];          // not
+    w.wu[2] = q[6]; w.bu[2] = q[7];    // forget
+    w.wu[3] = q[8]; w.bu[3] = q[9];    // input
+    w.wu[4] = q[10]; w.bu[4] = q[11];  // cell
+    w.wu[5] = q[12]; w.bu[5] = q[13];  // output
+  }
+  float* const* q = t + 14 * L;
+  P.att_w1 = q[0]; P.att_b1 = q[1]; P.att_w2 = q[2]; P.att_b2 = q[3];
+  P.cls_w1 = q[4]; P.cls_b1 = q[5]; P.cls_w2 = q[6]; P.cls_b2 = q[7];
+  for (int i = 0; i < 14 * L + 8; ++i)
+    if (!t[i]) { set_error("rnn: null parameter pointer", __FILE__, __LINE__); return -1; }
+  return 0;
+}
+
+int64_t rnn_scratch_floats(const RnnDims& d) {
+  const int64_t BT = (int64_t)d.B * d.T, H = d.H;
+  return 64 * 20 + (int64_t)d.B * H * 7 + BT * H * 3 + BT + (int64_t)d.L * BT * 7 * H + 7 * H * H + 6 * H * d.IN +
+         7 * H;
+}
+
+}  // namespace dfd

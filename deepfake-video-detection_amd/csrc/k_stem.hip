@@ -27,7 +27,8 @@ struct StemTiles {
 // input tile [pix][ci] (pix = row*SIE + col) of frame f at origin (iy0, ix0): branch-free
 // masked loads through the caller's strides, all issued together (register prefetch).
 __device__ __forceinline__ void stem_load(const StemGeom& g, const float* __restrict__ x, int f, int iy0, int ix0,
-                                          float (&r)[SNLD]) {
+                                          float (&r)[SNLD], uint32_t& okm) {
+  okm = 0u;
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < SNLD; ++i) {
@@ -35,16 +36,15 @@ __device__ __forceinline__ void stem_load(const StemGeom& g, const float* __rest
     const int pix = e / 3, ci = e - 3 * (e / 3);
     const int iy = iy0 + pix / SIE, ix = ix0 + pix % SIE;
     const bool ok = e < SNIN && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-    const int64_t off = ok ? (int64_t)f * g.sf + ci * g.sc + (int64_t)iy * g.sh + (int64_t)ix * g.sw : 0;
-    const float v = x[off];
-    r[i] = ok ? v : 0.f;
+    r[i] = *(ok ? x + ((int64_t)f * g.sf + ci * g.sc + (int64_t)iy * g.sh + (int64_t)ix * g.sw) : x);
+    okm |= ok ? (1u << i) : 0u;
   }
 }
-__device__ __forceinline__ void stem_store(float* tin, const float (&r)[SNLD]) {
+__device__ __forceinline__ void stem_store(float* tin, const float (&r)[SNLD], uint32_t okm) {
 #pragma unroll
   for (int i = 0; i < SNLD; ++i) {
     const int e = threadIdx.x + 256 * i;
-    if (e < SNIN) tin[e] = r[i];
+    if (e < SNIN) tin[e] = ((okm >> i) & 1u) ? r[i] : 0.f;
   }
 }
 
@@ -65,22 +65,23 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const floa
 #pragma unroll
   for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
   float nxt[SNLD];
+  uint32_t nok = 0u;
   int64_t t = blockIdx.x;
   if (t < ntiles) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
-    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nxt);
+    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nxt, nok);
   }
   for (; t < ntiles; t += gridDim.x) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
-    __syncthreads();
-    stem_store(tin, nxt);
-    __syncthreads();
+    lds_barrier();
+    stem_store(tin, nxt, nok);
+    lds_barrier();
     if (t + gridDim.x < ntiles) {  // next tile in flight during this tile's math and stores
       int f2, oy2, ox2;
       tl.coords(t + gridDim.x, f2, oy2, ox2);
-      stem_load(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nxt);
+      stem_load(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nxt, nok);
     }
     float acc[SP][8];
 #pragma unroll
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const floa
 #pragma unroll
       for (int j = 0; j < 8; ++j) { red[0][wave][vec * 8 + j] = st_s[j]; red[1][wave][vec * 8 + j] = st_q[j]; }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 2 * SCO) {
       const int which = tid / SCO, c = tid % SCO;
       stats[((int64_t)blockIdx.x * 2 + which) * SCO + c] =
@@ -169,11 +170,12 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float
 #pragma unroll
   for (int r = 0; r < 27; ++r) acc[r] = 0.f;
   float nx[SNLD];
+  uint32_t nxok = 0u;
   Raw8<T> nd[4];  // 256 px x 4 vectors / 256 threads
   auto load = [&](int64_t t) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
-    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nx);
+    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nx, nxok);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
@@ -184,8 +186,8 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float
   int64_t t = blockIdx.x;
   if (t < ntiles) load(t);
   for (; t < ntiles; t += gridDim.x) {
-    __syncthreads();
-    stem_store(tin, nx);
+    lds_barrier();
+    stem_store(tin, nx, nxok);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float
       raw_to_f(nd[i], d);
       st8(&tg[pix * SCO + v * 8], d);
     }
-    __syncthreads();
+    lds_barrier();
     if (t + gridDim.x < ntiles) load(t + gridDim.x);
     for (int p = sub; p < ST * ST; p += 8) {
       const int ly = p / ST, lx = p % ST;
@@ -205,11 +207,11 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   float* red = tg;  // [8][27][32] = 6912 floats <= 8192
 #pragma unroll
   for (int r = 0; r < 27; ++r) red[(sub * 27 + r) * SCO + co] = acc[r];
-  __syncthreads();
+  lds_barrier();
   float* out = slab + (int64_t)blockIdx.x * 27 * SCO;
   for (int i = tid; i < 27 * SCO; i += 256) {
     const int c = i / 27, r = i % 27;

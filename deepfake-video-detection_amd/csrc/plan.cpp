@@ -260,7 +260,6 @@ void plan_free(Plan& p) {
 // ------------------------------------------------------------------ forward / backward
 namespace {
 
-#define DFD_TRY(x) do { if ((x) != 0) return -1; } while (0)
 
 inline bool probe_hit(const Plan& p, int kind, const Block* b) {
   return p.probe.kind == kind && p.probe.count < p.probe.n && b && b->stage == p.probe.stage &&

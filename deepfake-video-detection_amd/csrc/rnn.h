@@ -1,0 +1,37 @@
+// LogicRNNLSTM launchers (k_rnn.hip); see the header comment there for the algorithm.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dfd {
+
+// one LogicCell's parameters (src/RNNModel.py:9-19): the six gates on u = [x, h] in the order
+// and, or, forget, input, cell, output (each weight [H][in+H], bias [H]) and the not-gate on h.
+struct RnnLayerW {
+  float* wu[6];
+  float* bu[6];
+  float* wn;
+  float* bn;
+};
+struct RnnParams {
+  RnnLayerW layer[8];
+  float *att_w1, *att_b1, *att_w2, *att_b2;  // attention.0 (H->H), attention.2 (H->1)
+  float *cls_w1, *cls_b1, *cls_w2, *cls_b2;  // classifier.0 (H->H), classifier.3 (H->1)
+};
+struct RnnDims {
+  int B, T, IN, H, L;
+};
+
+int launch_sgemm(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+                 int M, int N, int K, float beta, const float* bias);
+int64_t rnn_work_floats(const RnnDims& d);
+int64_t rnn_scratch_floats(const RnnDims& d);
+int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,
+                const int64_t* lens, float* work, float* y, uint64_t seed, float p);
+int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,
+                 const int64_t* lens, float* work, float* scratch, const float* dy, RnnParams& Gr, uint64_t seed,
+                 float p);
+// table of 14*L + 8 pointers in the reference's named_parameters() order -> RnnParams
+int rnn_params_from_table(float* const* t, int L, RnnParams& P);
+
+}  // namespace dfd

@@ -123,6 +123,26 @@ DFD_API int dfd_adam_step(void* stream, float* params, float* grads, float* exp_
                           double lr, double beta1, double beta2, double eps, double weight_decay, int step,
                           double grad_scale, int decoupled, const float* clip_out2);
 
+/* ---- LogicRNNLSTM (src/RNNModel.py:43-147), fp32 ----
+ * Replaces LogicRNNLSTM.forward (RNNModel.py:81-133) and its autograd backward.
+ * x: (B, T, IN) fp32 contiguous.  order: the reference's sort_idx of lengths.sort(0, descending=True)
+ * (RNNModel.py:92-95; B int64) or NULL when lengths is None; lengths: the SORTED lengths (B int64)
+ * or NULL.  The output stays in sorted order, exactly like the reference (it never un-sorts).
+ * params / grads: 14*L + 8 fp32 pointers in named_parameters() order: per layer
+ * {and,or,not,forget,input,cell,output}_gate.{weight,bias}, then attention.{0,2}.{weight,bias},
+ * classifier.{0,3}.{weight,bias}.  y: (B) = sigmoid output.  p: dropout probability (0 in eval),
+ * seed: counter-hash dropout seed (must match between forward and backward).
+ * work: dfd_rnn_work_floats() floats kept from forward to backward; scratch: dfd_rnn_scratch_floats(). */
+DFD_API int64_t dfd_rnn_work_floats(int B, int T, int IN, int H, int L);
+DFD_API int64_t dfd_rnn_scratch_floats(int B, int T, int IN, int H, int L);
+DFD_API int dfd_rnn_forward(void* stream, int B, int T, int IN, int H, int L, const float* x, const int64_t* order,
+                            const int64_t* lengths, float* const* params, float* work, float* y, uint64_t seed,
+                            float p);
+/* dy: (B) gradient of y; writes (overwrites) every parameter gradient. */
+DFD_API int dfd_rnn_backward(void* stream, int B, int T, int IN, int H, int L, const float* x, const int64_t* order,
+                             const int64_t* lengths, float* const* params, float* work, float* scratch,
+                             const float* dy, float* const* grads, uint64_t seed, float p);
+
 #ifdef __cplusplus
 }
 #endif
