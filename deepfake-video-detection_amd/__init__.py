@@ -8,6 +8,7 @@ Drop-in counterparts of the reference's hot-path API (SaiPranav1506/DeepFake-Vid
 * ``FusedAdamW`` / ``FusedAdam`` / ``clip_grad_norm_``     (ensemble_trainer.py:146,199-200; train.py:323)
 * ``train_step`` / ``DataParallelTrainer``                 (EnsembleTrainer.train_epoch step, ensemble_trainer.py:182-200)
 * ``LogicRNNLSTM`` / ``LogicCell`` / ``create_model``       (src/RNNModel.py)
+* ``CNNLSTMHybrid``                                       (src/models.py:20-85)
 
 Compute runs in hand-written HIP kernels for gfx950 behind the C ABI of ``include/dfd_hip.h``
 (``libdfd_hip.so``); PyTorch supplies device memory, streams and torch.distributed (RCCL).
@@ -17,7 +18,7 @@ Submodules import lazily so ``import deepfake_amd`` works before the library is 
 __all__ = [
     "PretrainedBackboneDetector", "EnsembleDetector", "EfficientNetB0Trunk", "B0FrameExtractor",
     "WeightedCrossEntropyLoss", "FusedAdamW", "FusedAdam", "clip_grad_norm_", "LogicRNNLSTM", "LogicCell",
-    "create_model",
+    "create_model", "CNNLSTMHybrid",
 ]
 
 
@@ -32,6 +33,8 @@ def __getattr__(name):
         from . import optim as m
     elif name in ("LogicRNNLSTM", "LogicCell", "create_model"):
         from . import rnn as m
+    elif name == "CNNLSTMHybrid":
+        from . import cnn_lstm as m
     else:
         raise AttributeError(name)
     return getattr(m, name)

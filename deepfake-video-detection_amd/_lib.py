@@ -57,6 +57,12 @@ _SIGS = {
     "dfd_rnn_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_rnn_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_u64, c_f]),
     "dfd_rnn_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_p, c_fpp, c_u64, c_f]),
+    "dfd_cnnlstm_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i, c_i]),
+    "dfd_cnnlstm_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i, c_i]),
+    "dfd_cnnlstm_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, ctypes.POINTER(c_i64), c_fpp, c_fpp,
+                                  c_p, c_i, c_f, c_u64, c_f, c_p]),
+    "dfd_cnnlstm_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, ctypes.POINTER(c_i64), c_fpp, c_p,
+                                   c_p, c_i, c_u64, c_f, c_p, c_fpp]),
 }
 
 EXPORTED = tuple(_SIGS.keys())

@@ -1,0 +1,450 @@
+// Dense convolutions of CNNLSTMHybrid's frame CNN (src/models.py:26-45) on gfx950, fp32.
+//
+// All three passes are one implicit-GEMM kernel on v_mfma_f32_16x16x4f32 (exact fp32 products),
+// 64x64 output tile per 256-thread block, BK = 16, operands staged through LDS by "operand
+// policies" that gather on the fly (no im2col buffer):
+//   forward  Y[m][co]  = b[co] + sum_{ky,kx,ci} X[n, oy*s-p+ky, ox*s-p+kx, ci] * W[co][ky][kx][ci]
+//   dgrad    dX[m][ci] = sum_{ky,kx,co} dY[n, iy+p-ky, ix+p-kx, co] * W[co][ci][ky][kx]   (s = 1)
+//   wgrad    dW[co][(ky,kx,ci)] = sum_m dY[m][co] * X(m, ky, kx, ci)     (split over m, slabs)
+// NHWC activations (the input frames are read through their strides, channels-last per
+// SURVEY F10); the forward epilogue writes per-tile BatchNorm partial rows (sum, sum of squares).
+// BatchNorm+ReLU+MaxPool(3, 2, 1) is one fused kernel (argmax kept for backward, first maximum
+// in scan order like PyTorch's max_pool2d), BatchNorm+ReLU+global-average-pool another.
+#include "kernels.h"
+#include "cnnlstm.h"
+
+namespace dfd {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int CG_T = 64, CG_K = 16;
+
+// ------------------------------------------------------------------ operand policies
+// load(): the thread's 4 elements of the (64 rows x 16 k) tile at (r0, k0) into v / ok.
+// kR == false: element e = tid + 256 i -> (r = e / 16, k = e % 16)   (contiguous along k)
+// kR == true : element e -> (r = e % 64, k = e / 64)                  (contiguous along r)
+struct OpRows {  // a(r, k) = p[r * ld + k]
+  const float* p;
+  int ld, R, K;
+  static constexpr bool kR = false;
+  __device__ void prep(int) {}
+  __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, r = r0 + e / CG_K, k = k0 + e % CG_K;
+      ok[i] = r < R && k < K;
+      v[i] = *(ok[i] ? p + (int64_t)r * ld + k : p);
+    }
+  }
+};
+struct OpCols {  // a(r, k) = p[k * ld + r]
+  const float* p;
+  int ld, R, K;
+  static constexpr bool kR = true;
+  __device__ void prep(int) {}
+  __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, r = r0 + e % CG_T, k = k0 + e / CG_T;
+      ok[i] = r < R && k < K;
+      v[i] = *(ok[i] ? p + (int64_t)k * ld + r : p);
+    }
+  }
+};
+// forward gather: rows = output pixels m = (n, oy, ox); k = (ky, kx, ci), ci fastest
+struct OpConvA {
+  const float* x;
+  int64_t sn, sy, sx, sc;  // element strides of the source (n, y, x, c)
+  int H, W, C, KW, S, P, Ho, Wo, R, K;
+  int iy0[4], ix0[4];
+  int64_t base[4];
+  static constexpr bool kR = false;
+  __device__ void prep(int r0) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(r0 + (tid + 256 * i) / CG_K, R - 1);
+      const int hw = Ho * Wo, n = r / hw, q = r - n * hw, oy = q / Wo, ox = q - oy * Wo;
+      iy0[i] = oy * S - P;
+      ix0[i] = ox * S - P;
+      base[i] = (int64_t)n * sn;
+    }
+  }
+  __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
+    const int tid = threadIdx.x;
+    const int k = k0 + (tid & 15);
+    const int tap = k / C, ci = k - tap * C, ky = tap / KW, kx = tap - ky * KW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + (tid + 256 * i) / CG_K;
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      ok[i] = r < R && k < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      v[i] = *(ok[i] ? x + base[i] + iy * sy + ix * sx + ci * sc : x);
+    }
+  }
+};
+// dgrad gather (stride 1): rows = input pixels (n, iy, ix); k = (ky, kx, co), co fastest;
+// source dY [N][Ho][Wo][Co] at (iy + p - ky, ix + p - kx)
+struct OpConvDgradA {
+  const float* dy;
+  int Ho, Wo, Co, KW, P, H, W, R, K;
+  int iy[4], ix[4];
+  int64_t base[4];
+  static constexpr bool kR = false;
+  __device__ void prep(int r0) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(r0 + (tid + 256 * i) / CG_K, R - 1);
+      const int hw = H * W, n = r / hw, q = r - n * hw;
+      iy[i] = q / W + P;
+      ix[i] = q - (q / W) * W + P;
+      base[i] = (int64_t)n * Ho * Wo * Co;
+    }
+  }
+  __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
+    const int tid = threadIdx.x;
+    const int k = k0 + (tid & 15);
+    const int tap = k / Co, co = k - tap * Co, ky = tap / KW, kx = tap - ky * KW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + (tid + 256 * i) / CG_K;
+      const int oy = iy[i] - ky, ox = ix[i] - kx;
+      ok[i] = r < R && k < K && oy >= 0 && oy < Ho && ox >= 0 && ox < Wo;
+      v[i] = *(ok[i] ? dy + base[i] + ((int64_t)oy * Wo + ox) * Co + co : dy);
+    }
+  }
+};
+// wgrad B operand: b(j, m) = X(m, j) with j = (ky, kx, ci) (contiguous along j), m = output pixel
+struct OpConvBT {
+  const float* x;
+  int64_t sn, sy, sx, sc;
+  int H, W, C, KW, S, P, Ho, Wo, R /* = KH*KW*C */, K /* = M */;
+  int ky, kx, ci;
+  bool jok;
+  static constexpr bool kR = true;
+  __device__ void prep(int j0) {
+    const int j = j0 + (threadIdx.x & 63);
+    jok = j < R;
+    const int jj = jok ? j : 0;
+    const int tap = jj / C;
+    ci = jj - tap * C;
+    ky = tap / KW;
+    kx = tap - ky * KW;
+  }
+  __device__ void load(int j0, int m0, float (&v)[4], bool (&ok)[4]) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + (tid >> 6) + 4 * i;
+      const int hw = Ho * Wo, n = m / hw, q = m - n * hw, oy = q / Wo, ox = q - oy * Wo;
+      const int iy = oy * S - P + ky, ix = ox * S - P + kx;
+      ok[i] = jok && m < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      v[i] = *(ok[i] ? x + (int64_t)n * sn + iy * sy + ix * sx + ci * sc : x);
+    }
+  }
+};
+
+template <bool kR>
+__device__ __forceinline__ void cg_store(float (*S)[CG_K + 1], const float (&v)[4], const bool (&ok)[4]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid + 256 * i;
+    const int r = kR ? e % CG_T : e / CG_K, k = kR ? e / CG_T : e % CG_K;
+    S[r][k] = ok[i] ? v[i] : 0.f;
+  }
+}
+
+enum { CEPI_STORE = 0, CEPI_STATS = 1, CEPI_SLAB = 2 };
+
+// C[m][n] = sum_k A(m,k) B(n,k) (+ bias[n]); grid.x = n-tiles * m-tiles (n fastest), grid.y = k splits
+template <class PA, class PB, int EPI>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __restrict__ C, int ldc, int M, int N,
+                                                        int K, int ksplit, const float* __restrict__ bias,
+                                                        float* __restrict__ stats) {
+  __shared__ float As[CG_T][CG_K + 1], Bs[CG_T][CG_K + 1];
+  __shared__ float red[2][2][CG_T];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntn = (N + CG_T - 1) / CG_T;
+  const int nt = blockIdx.x % ntn, mt = blockIdx.x / ntn;
+  const int m0 = mt * CG_T, n0 = nt * CG_T;
+  const int kb = blockIdx.y * ksplit, ke = min(K, kb + ksplit);
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  pa.prep(m0);
+  pb.prep(n0);
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float va[4], vb[4];
+  bool oa[4], ob[4];
+  if (kb < ke) {
+    pa.load(m0, kb, va, oa);
+    pb.load(n0, kb, vb, ob);
+  }
+  for (int k0 = kb; k0 < ke; k0 += CG_K) {
+    lds_barrier();
+    // elements past ke belong to the next split: mask them
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i;
+      const int ka = k0 + (PA::kR ? e / CG_T : e % CG_K), kbb = k0 + (PB::kR ? e / CG_T : e % CG_K);
+      oa[i] = oa[i] && ka < ke;
+      ob[i] = ob[i] && kbb < ke;
+    }
+    cg_store<PA::kR>(As, va, oa);
+    cg_store<PB::kR>(Bs, vb, ob);
+    lds_barrier();
+    if (k0 + CG_K < ke) {
+      pa.load(m0, k0 + CG_K, va, oa);
+      pb.load(n0, k0 + CG_K, vb, ob);
+    }
+#pragma unroll
+    for (int s = 0; s < CG_K / 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+      const float a0 = As[wm + (lane & 15)][kk], a1 = As[wm + 16 + (lane & 15)][kk];
+      const float b0 = Bs[wn + (lane & 15)][kk], b1 = Bs[wn + 16 + (lane & 15)][kk];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+  float* Cz = EPI == CEPI_SLAB ? C + (int64_t)blockIdx.y * M * N : C;
+  float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + a * 16 + 4 * (lane >> 4) + r, n = n0 + wn + b * 16 + (lane & 15);
+        if (m < M && n < N) {
+          float v = acc[a][b][r];
+          if (bias) v += bias[n];
+          Cz[(int64_t)m * ldc + n] = v;
+          if (EPI == CEPI_STATS) { cs[b] += v; cq[b] += v * v; }
+        }
+      }
+  if constexpr (EPI == CEPI_STATS) {
+    // per column: lanes with equal (lane & 15) hold its 4-row groups -> xor 16, 32; then the
+    // two row-halves of the tile (waves 0/1 and 2/3) in a fixed order through LDS
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      cs[b] += __shfl_xor(cs[b], 16, 64); cs[b] += __shfl_xor(cs[b], 32, 64);
+      cq[b] += __shfl_xor(cq[b], 16, 64); cq[b] += __shfl_xor(cq[b], 32, 64);
+      if (lane < 16) {
+        red[wave >> 1][0][wn + b * 16 + lane] = cs[b];
+        red[wave >> 1][1][wn + b * 16 + lane] = cq[b];
+      }
+    }
+    lds_barrier();
+    if (tid < 2 * CG_T) {
+      const int which = tid / CG_T, c = tid % CG_T;
+      if (n0 + c < N) stats[((int64_t)mt * 2 + which) * N + n0 + c] = red[0][which][c] + red[1][which][c];
+    }
+  }
+}
+
+template <class PA, class PB, int EPI>
+static int conv_gemm(hipStream_t s, const PA& pa, const PB& pb, float* C, int ldc, int M, int N, int K, int splits,
+                     const float* bias, float* stats) {
+  const int64_t tiles = (int64_t)cdiv(N, CG_T) * cdiv(M, CG_T);
+  if (tiles > 0x7fffffff) { set_error("conv: too many tiles", __FILE__, __LINE__); return -1; }
+  const int ksplit = cdiv(cdiv(K, splits), CG_K) * CG_K;
+  splits = cdiv(K, ksplit);
+  hipLaunchKernelGGL((conv_gemm_kernel<PA, PB, EPI>), dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, s, pa, pb,
+                     C, ldc, M, N, K, ksplit, bias, stats);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ weight layouts
+// W [Co][Ci][KH][KW] -> Wf [Co][KH][KW][Ci] (forward) and Wd [Ci][KH][KW][Co] (dgrad)
+__global__ void conv_pack_kernel(const float* __restrict__ w, int Co, int Ci, int KK, float* __restrict__ wf,
+                                 float* __restrict__ wd) {
+  const int64_t n = (int64_t)Co * Ci * KK;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int co = (int)(i / ((int64_t)Ci * KK));
+    const int rem = (int)(i - (int64_t)co * Ci * KK), ci = rem / KK, t = rem - ci * KK;
+    const float v = w[i];
+    wf[((int64_t)co * KK + t) * Ci + ci] = v;
+    if (wd) wd[((int64_t)ci * KK + t) * Co + co] = v;
+  }
+}
+// gw [Co][Ci][KH][KW] = sum_s slab[s][co][(t, ci)]
+__global__ void conv_unpack_grad_kernel(const float* __restrict__ slab, int splits, int Co, int Ci, int KK,
+                                        float* __restrict__ gw) {
+  const int64_t n = (int64_t)Co * Ci * KK;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int co = (int)(i / ((int64_t)Ci * KK));
+    const int rem = (int)(i - (int64_t)co * Ci * KK), ci = rem / KK, t = rem - ci * KK;
+    const int64_t j = ((int64_t)co * KK + t) * Ci + ci;
+    float a = 0.f;
+    for (int sp = 0; sp < splits; ++sp) a += slab[(int64_t)sp * n + j];
+    gw[i] = a;
+  }
+}
+
+// ------------------------------------------------------------------ BN + ReLU + MaxPool(3,2,1)
+__global__ void bn_relu_pool_fwd_kernel(const float* __restrict__ Y, const float* __restrict__ sc,
+                                        const float* __restrict__ sh, int N, int H, int W, int C, int Ho, int Wo,
+                                        float* __restrict__ P, uint8_t* __restrict__ arg) {
+  const int64_t n = (int64_t)N * Ho * Wo * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int64_t pix = i / C;
+    const int ox = (int)(pix % Wo);
+    const int64_t t = pix / Wo;
+    const int oy = (int)(t % Ho);
+    const int f = (int)(t / Ho);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * 2 - 1 + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * 2 - 1 + kx;
+        if (ix < 0 || ix >= W) continue;
+        const float z = fmaxf(Y[(((int64_t)f * H + iy) * W + ix) * C + c] * sc[c] + sh[c], 0.f);
+        if (z > best) { best = z; bi = ky * 3 + kx; }
+      }
+    }
+    P[i] = best;
+    arg[i] = (uint8_t)bi;
+  }
+}
+// g[n][iy][ix][c] = relu'(z) * sum of dP over the windows whose argmax is (iy, ix)
+__global__ void bn_relu_pool_bwd_kernel(const float* __restrict__ dP, const uint8_t* __restrict__ arg,
+                                        const float* __restrict__ Y, const float* __restrict__ sc,
+                                        const float* __restrict__ sh, int N, int H, int W, int C, int Ho, int Wo,
+                                        float* __restrict__ g) {
+  const int64_t n = (int64_t)N * H * W * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int64_t pix = i / C;
+    const int ix = (int)(pix % W);
+    const int64_t t = pix / W;
+    const int iy = (int)(t % H);
+    const int f = (int)(t / H);
+    float a = 0.f;
+    const int oy_lo = max(0, (iy) / 2 - 0), oy_hi = min(Ho - 1, (iy + 1) / 2);
+    const int ox_lo = max(0, (ix) / 2 - 0), ox_hi = min(Wo - 1, (ix + 1) / 2);
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      const int ky = iy - (oy * 2 - 1);
+      if (ky < 0 || ky > 2) continue;
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        const int kx = ix - (ox * 2 - 1);
+        if (kx < 0 || kx > 2) continue;
+        const int64_t o = (((int64_t)f * Ho + oy) * Wo + ox) * C + c;
+        if (arg[o] == ky * 3 + kx) a += dP[o];
+      }
+    }
+    const float z = Y[i] * sc[c] + sh[c];
+    g[i] = z > 0.f ? a : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ BN + ReLU + global average pool
+// feat[f][c] = mean_hw relu(Y*sc+sh); one block per (frame, 64-channel group), fixed-order sums
+__global__ void bn_relu_gap_fwd_kernel(const float* __restrict__ Y, const float* __restrict__ sc,
+                                       const float* __restrict__ sh, int HW, int C, float* __restrict__ feat) {
+  __shared__ float red[4][64];
+  const int f = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), q = threadIdx.x >> 6;
+  float a = 0.f;
+  if (c < C)
+    for (int p = q; p < HW; p += 4) a += fmaxf(Y[((int64_t)f * HW + p) * C + c] * sc[c] + sh[c], 0.f);
+  red[q][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (q == 0 && c < C)
+    feat[(int64_t)f * C + c] = (((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) +
+                                red[3][threadIdx.x]) / (float)HW;
+}
+__global__ void bn_relu_gap_bwd_kernel(const float* __restrict__ dfeat, const float* __restrict__ Y,
+                                       const float* __restrict__ sc, const float* __restrict__ sh, int64_t M, int HW,
+                                       int C, float* __restrict__ g) {
+  const int64_t n = M * C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const int64_t row = i / C;
+    const float z = Y[i] * sc[c] + sh[c];
+    g[i] = z > 0.f ? dfeat[(row / HW) * C + c] / (float)HW : 0.f;
+  }
+}
+
+static int ew(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 4096)); }
+
+// ------------------------------------------------------------------ layer launchers
+int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* w,
+                 const float* bias, float* wf, float* Y, float* stats, int* stat_rows) {
+  const int KK = g.KH * g.KW;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
+                     (float*)nullptr);
+  const int M = g.N * g.Ho * g.Wo, K = KK * g.Ci;
+  OpConvA pa{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, M, K};
+  OpRows pb{wf, K, g.Co, K};
+  if (stat_rows) *stat_rows = cdiv(M, CG_T);
+  return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats);
+}
+
+int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX) {
+  if (g.S != 1) { set_error("conv dgrad: stride 1 only", __FILE__, __LINE__); return -1; }
+  const int KK = g.KH * g.KW;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
+                     wd);
+  const int M = g.N * g.H * g.W, K = KK * g.Co;
+  OpConvDgradA pa{dY, g.Ho, g.Wo, g.Co, g.KW, g.P, g.H, g.W, M, K};
+  OpRows pb{wd, K, g.Ci, K};
+  return conv_gemm<OpConvDgradA, OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr);
+}
+
+int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* dY, float* slab,
+               int64_t slab_cap, float* gw) {
+  const int KK = g.KH * g.KW;
+  const int M = g.N * g.Ho * g.Wo, Kp = KK * g.Ci;  // GEMM: C[Co][Kp] = sum_m dY[m][co] X(m, kp)
+  const int64_t per = (int64_t)g.Co * Kp;
+  const int tiles = cdiv(g.Co, CG_T) * cdiv(Kp, CG_T);
+  int splits = std::max(1, std::min(cdiv(M, 256), 2048 / std::max(tiles, 1)));
+  splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / per));
+  OpCols pa{dY, g.Co, g.Co, M};
+  OpConvBT pb{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, Kp, M};
+  const int ksplit = cdiv(cdiv(M, splits), CG_K) * CG_K;
+  const int used = cdiv(M, ksplit);
+  DFD_TRY((conv_gemm<OpCols, OpConvBT, CEPI_SLAB>(s, pa, pb, slab, Kp, g.Co, Kp, M, splits, nullptr, nullptr)));
+  hipLaunchKernelGGL(conv_unpack_grad_kernel, dim3(ew(per)), dim3(256), 0, s, slab, used, g.Co, g.Ci, KK, gw);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int bn_relu_pool_fwd(hipStream_t s, const float* Y, const float* sc, const float* sh, int N, int H, int W, int C,
+                     int Ho, int Wo, float* P, uint8_t* arg) {
+  hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(ew((int64_t)N * Ho * Wo * C)), dim3(256), 0, s, Y, sc, sh, N, H, W,
+                     C, Ho, Wo, P, arg);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+int bn_relu_pool_bwd(hipStream_t s, const float* dP, const uint8_t* arg, const float* Y, const float* sc,
+                     const float* sh, int N, int H, int W, int C, int Ho, int Wo, float* g) {
+  hipLaunchKernelGGL(bn_relu_pool_bwd_kernel, dim3(ew((int64_t)N * H * W * C)), dim3(256), 0, s, dP, arg, Y, sc, sh,
+                     N, H, W, C, Ho, Wo, g);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+int bn_relu_gap_fwd(hipStream_t s, const float* Y, const float* sc, const float* sh, int N, int HW, int C,
+                    float* feat) {
+  hipLaunchKernelGGL(bn_relu_gap_fwd_kernel, dim3(N, cdiv(C, 64)), dim3(256), 0, s, Y, sc, sh, HW, C, feat);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+int bn_relu_gap_bwd(hipStream_t s, const float* dfeat, const float* Y, const float* sc, const float* sh, int N,
+                    int HW, int C, float* g) {
+  hipLaunchKernelGGL(bn_relu_gap_bwd_kernel, dim3(ew((int64_t)N * HW * C)), dim3(256), 0, s, dfeat, Y, sc, sh,
+                     (int64_t)N * HW, HW, C, g);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace dfd

@@ -663,6 +663,43 @@ int rnn_params_from_table(float* const* t, int L, RnnParams& P) {
   return 0;
 }
 
+// attention pooling used by CNNLSTMHybrid too (models.py:60-64, no mask):
+//   E = tanh(O W1^T + b1) ; att = softmax_t(E w2 + b2) ; ctx = sum_t att * O
+int attn_forward(hipStream_t s, const float* O, int B, int T, int H, const float* w1, const float* b1, const float* w2,
+                 const float* b2, float* E, float* att, float* ctx) {
+  const int64_t BT = (int64_t)B * T;
+  DFD_TRY(launch_sgemm(s, false, false, O, H, w1, H, E, H, (int)BT, H, H, 0.f, b1));
+  hipLaunchKernelGGL(rnn_tanh_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, E, BT * H);
+  hipLaunchKernelGGL(rnn_attn_fwd_kernel, dim3(B), dim3(256), T * sizeof(float), s, O, E, w2, b2, T, H, att, ctx);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+// scratch: 2*BT*H + BT floats
+int attn_backward(hipStream_t s, const float* O, const float* E, const float* att, const float* dctx, const float* w1,
+                  const float* w2, int B, int T, int H, float* scratch, float* dO, float* gw1, float* gb1, float* gw2,
+                  float* gb2) {
+  const int64_t BT = (int64_t)B * T;
+  float* dE = scratch;
+  float* dO2 = dE + BT * H;
+  float* ds = dO2 + BT * H;
+  const dim3 gH((unsigned)cdiv(H, 256));
+  hipLaunchKernelGGL(rnn_attn_bwd_kernel, dim3(B), dim3(256), 2 * T * sizeof(float), s, O, E, att, dctx, w2, T, H, dO,
+                     dE, ds);
+  hipLaunchKernelGGL(rnn_attn_w2_kernel, gH, dim3(256), 0, s, E, ds, (int)BT, H, gw2, gb2);
+  DFD_TRY(launch_sgemm(s, true, true, dE, H, O, H, gw1, H, H, H, (int)BT, 0.f, nullptr));
+  hipLaunchKernelGGL(rnn_colsum_kernel, gH, dim3(256), 0, s, dE, (int)BT, H, H, gb1, 0);
+  DFD_TRY(launch_sgemm(s, false, true, dE, H, w1, H, dO2, H, (int)BT, H, H, 0.f, nullptr));
+  hipLaunchKernelGGL(rnn_mask_bwd_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, dO, dO2, (const int64_t*)nullptr,
+                     B, T, H);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+int colsum(hipStream_t s, const float* X, int M, int N, int ld, float* out) {
+  hipLaunchKernelGGL(rnn_colsum_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, s, X, M, N, ld, out, 0);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int64_t rnn_scratch_floats(const RnnDims& d) {
   const int64_t BT = (int64_t)d.B * d.T, H = d.H;
   return 64 * 20 + (int64_t)d.B * H * 7 + BT * H * 3 + BT + (int64_t)d.L * BT * 7 * H + 7 * H * H + 6 * H * d.IN +

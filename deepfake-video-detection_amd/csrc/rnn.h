@@ -31,6 +31,12 @@ int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float
 int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,
                  const int64_t* lens, float* work, float* scratch, const float* dy, RnnParams& Gr, uint64_t seed,
                  float p);
+int attn_forward(hipStream_t s, const float* O, int B, int T, int H, const float* w1, const float* b1, const float* w2,
+                 const float* b2, float* E, float* att, float* ctx);
+int attn_backward(hipStream_t s, const float* O, const float* E, const float* att, const float* dctx, const float* w1,
+                  const float* w2, int B, int T, int H, float* scratch, float* dO, float* gw1, float* gb1, float* gw2,
+                  float* gb2);
+int colsum(hipStream_t s, const float* X, int M, int N, int ld, float* out);
 // table of 14*L + 8 pointers in the reference's named_parameters() order -> RnnParams
 int rnn_params_from_table(float* const* t, int L, RnnParams& P);
 

@@ -143,6 +143,27 @@ DFD_API int dfd_rnn_backward(void* stream, int B, int T, int IN, int H, int L, c
                              const int64_t* lengths, float* const* params, float* work, float* scratch,
                              const float* dy, float* const* grads, uint64_t seed, float p);
 
+/* ---- CNNLSTMHybrid (src/models.py:20-85), fp32 ----
+ * Replaces CNNLSTMHybrid.forward (models.py:72-85) and its autograd backward: frame CNN
+ * (4 conv+BN+ReLU, 3 maxpools, GAP), nn.LSTM(512, hidden, layers, dropout, batch_first),
+ * attention pooling, classifier.  x: (B*T, 3, H, W) fp32 with element strides x_strides4
+ * (n, c, h, w) -- channels-last strides are fine.  params / grads: 16 + 4*layers + 8 pointers in
+ * named_parameters() order (cnn.{0,1,4,5,8,9,12,13}.{weight,bias}, lstm.{weight_ih,weight_hh,
+ * bias_ih,bias_hh}_l{k}, attention.{0,2}.*, classifier.{0,3}.*); bn_running: 8 pointers
+ * cnn.{1,5,9,13}.{running_mean,running_var} (updated in training, momentum as given, eps 1e-5).
+ * logits: (B, num_classes).  work: dfd_cnnlstm_work_floats() kept from forward to backward. */
+DFD_API int64_t dfd_cnnlstm_work_floats(int B, int T, int H, int W, int hidden, int layers, int num_classes);
+DFD_API int64_t dfd_cnnlstm_scratch_floats(int B, int T, int H, int W, int hidden, int layers, int num_classes);
+DFD_API int dfd_cnnlstm_forward(void* stream, int B, int T, int H, int W, int hidden, int layers, int num_classes,
+                                const float* x, const int64_t* x_strides4, float* const* params,
+                                float* const* bn_running, float* work, int training, float momentum, uint64_t seed,
+                                float p, float* logits);
+/* dlogits: (B, num_classes); writes (overwrites) every parameter gradient. */
+DFD_API int dfd_cnnlstm_backward(void* stream, int B, int T, int H, int W, int hidden, int layers, int num_classes,
+                                 const float* x, const int64_t* x_strides4, float* const* params, float* work,
+                                 float* scratch, int training, uint64_t seed, float p, const float* dlogits,
+                                 float* const* grads);
+
 #ifdef __cplusplus
 }
 #endif
