@@ -51,7 +51,7 @@ class CNNLSTMHybrid(FlatModule):
 
     def _on_flatten(self) -> None:
         self._names = [n for n, _ in self._flat_params]
-        bufs = dict(self._flat_bufs)
+        bufs = dict(self.named_buffers())  # after flattening: views into the flat BN buffer
         self._bn_run = [bufs[f"cnn.{i}.{k}"] for i in _BN_IDX for k in ("running_mean", "running_var")]
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
