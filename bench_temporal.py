@@ -1,0 +1,165 @@
+"""Throughput of the temporal-aggregation rows of the hot path on one GPU.
+
+Not the headline bench (that is ``bench.py``, EfficientNet-B0); this measures the two other
+reference models behind their drop-in modules, one JSON line each:
+
+* ``CNNLSTMHybrid`` (src/models.py:20-85) train step as ``train.py`` runs it
+  (``train.py:104-133``: forward, CE, backward, Adam lr 1e-4) on 16-frame clips, synthetic frames
+  (seeded uint8 -> /255, channels-last like ``collate_batch_cnn_lstm``), fp32;
+  unit: frames/s (clips x 16 per step).
+* ``LogicRNNLSTM`` (src/RNNModel.py) train step (forward with lengths, BCE, backward, Adam) on
+  (B, 16, 1024) features; unit: sequence-steps/s (B x T per step).
+
+Each line carries a ``cpu_baseline``: the oracle restatement timed on the host cores for a
+bounded sample (the reference itself does not travel to the GPU box).
+
+    python bench_temporal.py [--model cnnlstm|rnn|both] [--clips 64] [--image 224] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+import deepfake_amd  # noqa: E402,F401
+from deepfake_amd.cnn_lstm import CNNLSTMHybrid  # noqa: E402
+from deepfake_amd.optim import FusedAdam  # noqa: E402
+from deepfake_amd.rnn import LogicRNNLSTM  # noqa: E402
+from deepfake_amd.weights import deterministic_init_  # noqa: E402
+
+
+def _time(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def _cpu_time(step, seconds):
+    step()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            return (time.perf_counter() - t0) / n, n
+
+
+def bench_cnnlstm(args, dev):
+    B, T, S = args.clips, 16, args.image
+    m = CNNLSTMHybrid(3, 256, 2, 2, 0.3)
+    deterministic_init_(m, seed=0)
+    m = m.to(dev).train()
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    u8 = torch.randint(0, 256, (B, T, S, S, 3), generator=g, device=dev, dtype=torch.uint8)
+    x = (u8.float() / 255.0).permute(0, 1, 4, 2, 3)  # (B, T, 3, S, S) channels-last strides (train.py:59)
+    y = torch.randint(0, 2, (B,), generator=g, device=dev)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = crit(m(x), y)
+        loss.backward()
+        opt.step()
+
+    dt = _time(step, args.steps, args.warmup)
+    line = {"metric": "frames/sec training CNNLSTMHybrid 16-frame clips", "value": round(B * T / dt, 2),
+            "unit": "frames/s", "n_gpus": 1, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "f32", "data": "synthetic uint8 frames (seeded, on device) /255, random-init weights",
+            "config": {"workload": "CNNLSTMHybrid train step (forward, CE, backward, Adam lr 1e-4)",
+                       "clips": B, "frames_per_clip": T, "image": [S, S, 3]}}
+    if not args.no_cpu_baseline:
+        from oracle.detector_cpu import CNNLSTMHybridCPU
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
+        ref = CNNLSTMHybridCPU(3, 256, 2, 2, 0.3).train()
+        ropt = torch.optim.Adam(ref.parameters(), lr=1e-4)
+        xc = torch.rand(2, T, 3, S, S)
+        yc = torch.tensor([0, 1])
+
+        def cstep():
+            ropt.zero_grad()
+            crit(ref(xc), yc).backward()
+            ropt.step()
+
+        ct, n = _cpu_time(cstep, args.cpu_seconds)
+        line["cpu_baseline"] = {"value": round(2 * T / ct, 3), "unit": "frames/s", "cores": torch.get_num_threads(),
+                                "kind": "port", "sample": f"{n} steps x 2 clips x {T} frames {S}^2, fp32 oracle"}
+    return line
+
+
+def bench_rnn(args, dev):
+    B, T, F = args.clips, 16, 1024
+    m = LogicRNNLSTM(F, 512, 2, 0.5)
+    deterministic_init_(m, seed=0)
+    m = m.to(dev).train()
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    x = torch.randn(B, T, F, generator=g, device=dev)
+    lengths = torch.randint(1, T + 1, (B,), generator=g, device=dev)
+    tgt = torch.randint(0, 2, (B, 1), generator=g, device=dev).float()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = torch.nn.functional.binary_cross_entropy(m(x, lengths), tgt)
+        loss.backward()
+        opt.step()
+
+    dt = _time(step, args.steps, args.warmup)
+    line = {"metric": "sequence-steps/sec training LogicRNNLSTM", "value": round(B * T / dt, 2),
+            "unit": "sequence-steps/s", "n_gpus": 1, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "f32", "data": "synthetic N(0,1) features, random lengths, random-init weights",
+            "config": {"workload": "LogicRNNLSTM train step (forward with lengths, BCE, backward, Adam lr 1e-4)",
+                       "batch": B, "steps": T, "input_size": F, "hidden": 512, "layers": 2}}
+    if not args.no_cpu_baseline:
+        from oracle.detector_cpu import LogicRNNLSTMCPU
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
+        ref = LogicRNNLSTMCPU(F, 512, 2, 0.5).train()
+        ropt = torch.optim.Adam(ref.parameters(), lr=1e-4)
+        xc, lc, tc = x.cpu(), lengths.cpu(), tgt.cpu()
+
+        def cstep():
+            ropt.zero_grad()
+            torch.nn.functional.binary_cross_entropy(ref(xc, lc), tc).backward()
+            ropt.step()
+
+        ct, n = _cpu_time(cstep, args.cpu_seconds)
+        line["cpu_baseline"] = {"value": round(B * T / ct, 3), "unit": "sequence-steps/s",
+                                "cores": torch.get_num_threads(), "kind": "port",
+                                "sample": f"{n} steps of the same batch, fp32 oracle"}
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "both"])
+    ap.add_argument("--clips", type=int, default=64)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if args.model in ("rnn", "both"):
+        print(json.dumps(bench_rnn(args, dev)), flush=True)
+    if args.model in ("cnnlstm", "both"):
+        print(json.dumps(bench_cnnlstm(args, dev)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,8 @@
 #pragma once
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace dfd {
 
 constexpr int DCG = 32;  // channels per workgroup (4 x 8-element vectors)
@@ -118,6 +120,19 @@ constexpr int kDwFallback = 4;  // 8x8
 static inline int dw_grid(int64_t ntiles, int groups) {
   const int64_t per_group = std::min<int64_t>(ntiles, std::max<int64_t>(1, 1024 / groups));
   return (int)(per_group * groups);
+}
+
+// Register-blocked stride-1 forward (k_dw_strip.hip): 1 = launched, 0 = no config for this
+// layer (use the tile kernel), -1 = launch error.  DFD_DW_STRIP=0 disables it (A/B runs).
+template <typename T>
+int try_dw_fwd_strip(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
+                     int* stat_rows);
+static inline bool dw_strip_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DFD_DW_STRIP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 }  // namespace dfd

@@ -46,6 +46,7 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   __shared__ float st_sum[GBN];
   __shared__ float st_sq[GBN];
+  __shared__ float st_part[STATS ? 4 : 1][2][GBN];  // per-wave column partials (fixed-order sum)
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = As + GBM * G::AS;
   T* Cs = reinterpret_cast<T*>(smem);
@@ -192,14 +193,21 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
         if constexpr (STATS) {
           s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
           q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-          if (lane < 16 && col < nvalid) {
-            atomicAdd(&st_sum[col], s);
-            atomicAdd(&st_sq[col], q);
+          if (lane < 16) {
+            st_part[wave][0][col] = s;
+            st_part[wave][1][col] = q;
           }
         }
       }
     }
     lds_barrier();
+    if constexpr (STATS) {
+      // waves 0..3 in order: bit-reproducible BN statistics
+      if (tid < nvalid) {
+        st_sum[tid] += ((st_part[0][0][tid] + st_part[1][0][tid]) + st_part[2][0][tid]) + st_part[3][0][tid];
+        st_sq[tid] += ((st_part[0][1][tid] + st_part[1][1][tid]) + st_part[2][1][tid]) + st_part[3][1][tid];
+      }
+    }
     const int vpr = nvalid >> 3;
     for (int v = tid; v < GBM * vpr; v += 256) {
       const int row = v / vpr, cv = (v - row * vpr) * 8;

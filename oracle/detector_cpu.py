@@ -155,6 +155,27 @@ def collate_cnn_lstm(batch, max_frames=16, image_size=(224, 224)):
     return x, torch.tensor(labels, dtype=torch.long)
 
 
+def normalize_adjacency(a):
+    """``normalize_adjacency`` (src/utils.py:95-104): D^-1/2 (A + I) D^-1/2 in float32."""
+    a = a.astype(np.float32) + np.eye(a.shape[0], dtype=np.float32)
+    d = np.power(np.sum(a, axis=1), -0.5)
+    d[np.isinf(d)] = 0.0
+    dm = np.diag(d)
+    return dm @ a @ dm
+
+
+def collate_vit_gcn(batch, max_nodes=16, image_size=(224, 224)):
+    """``collate_batch`` (src/train.py:62-100): the same sampling as the CNN-LSTM collate, plus a
+    chain graph over the nodes, symmetric-normalised per clip."""
+    x, labels = collate_cnn_lstm(batch, max_frames=max_nodes, image_size=image_size)
+    b, n = x.shape[0], x.shape[1]
+    a = np.zeros((n, n), dtype=np.float32)
+    for i in range(n - 1):
+        a[i, i + 1] = a[i + 1, i] = 1.0
+    a_norm = torch.from_numpy(np.stack([normalize_adjacency(a) for _ in range(b)])).float()
+    return x, a_norm, labels
+
+
 def train_step(model, x, labels, opt, class_weights=None, max_norm=1.0):
     """One step of ``EnsembleTrainer.train_epoch`` (src/ensemble_trainer.py:182-203):
     zero_grad -> forward -> weighted CE -> backward -> clip_grad_norm_(1.0) -> step."""

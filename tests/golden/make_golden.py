@@ -8,14 +8,14 @@ portable hash generator (``deepfake_amd.weights``) on both sides.
 Shims: the reference imports ``torchvision`` and ``timm`` at
 ``src/pretrained_detector.py:9-10`` and ``cv2`` at ``src/detector.py:4``; none is
 installed.  ``torchvision`` and ``cv2`` are empty stand-ins (unused on the paths
-recorded here); ``timm.create_model('efficientnet_b0')`` returns the oracle's
-CPU restatement (``oracle/b0_cpu.py``).  The reference's own wrapping
+recorded here); ``timm.create_model('efficientnet_b0')`` / ``('vit_base_patch16_224')``
+return the oracle's CPU restatements (``oracle/b0_cpu.py``, ``oracle/vit_cpu.py``).  The reference's own wrapping
 (``children()[:-1]``), temporal attention, head, dropout/eval behaviour, loss,
 clip-norm + AdamW step, ``LogicRNNLSTM``, ``CNNLSTMHybrid`` and the collate
 rules are the reference's code; only the trunk arithmetic is the restatement
 ("parity unpinned" at the timm boundary).
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [b0 step rnn cnn_lstm vit_gcn]
 """
 from __future__ import annotations
 
@@ -34,7 +34,7 @@ import torch  # noqa: E402
 
 import deepfake_amd  # noqa: E402,F401
 from deepfake_amd.weights import deterministic_init_, hash_uniform  # noqa: E402
-from oracle import b0_cpu  # noqa: E402
+from oracle import b0_cpu, vit_cpu  # noqa: E402
 
 N_HEAD = 64  # number of leading elements of each flattened gradient stored
 
@@ -47,7 +47,11 @@ def _install_shims():
     sys.modules.setdefault("torchvision", tv)
     sys.modules.setdefault("torchvision.transforms", tvt)
     timm = types.ModuleType("timm")
-    timm.create_model = b0_cpu.create_model
+
+    def create_model(name, *a, **kw):
+        return (vit_cpu if name.startswith("vit_") else b0_cpu).create_model(name, *a, **kw)
+
+    timm.create_model = create_model
     sys.modules["timm"] = timm
     cv2 = types.ModuleType("cv2")
     sys.modules.setdefault("cv2", cv2)
@@ -226,13 +230,55 @@ def gen_cnn_lstm():
                         labels=labels_t.numpy(), counts=np.array([0, 5, 16, 23]))
 
 
+def gen_vit_gcn():
+    """DeepfakeModel (models.py:222-291, timm ViT branch) eval + train step, and the
+    vit_gcn collate rules (train.py:62-100, utils.normalize_adjacency)."""
+    import models as M
+    import train as TR
+
+    # collate: tiny 4x4 faces, M = 0, 5, 16, 23 -> (B, 16, 3, 4, 4), chain-graph A_norm
+    batch = []
+    for i, M_ in enumerate([0, 5, 16, 23]):
+        f = (np.arange(M_ * 4 * 4 * 3, dtype=np.int64) * 11 + i * 5) % 256
+        batch.append({"faces": f.astype(np.uint8).reshape(M_, 4, 4, 3), "label": i % 2})
+    nodes, a_norm, labels = TR.collate_batch(batch, max_nodes=16, image_size=(4, 4))
+    np.savez_compressed(os.path.join(HERE, "collate_vit_gcn.npz"), nodes=nodes.numpy(), a_norm=a_norm.numpy(),
+                        labels=labels.numpy(), counts=np.array([0, 5, 16, 23]))
+
+    torch.manual_seed(0)
+    m = M.DeepfakeModel()
+    deterministic_init_(m, seed=12)
+    B, N = 2, 3
+    x = frames(13, (B, N, 3, 224, 224))
+    from utils import normalize_adjacency
+    A = np.zeros((N, N), dtype=np.float32)
+    for i in range(N - 1):
+        A[i, i + 1] = A[i + 1, i] = 1.0
+    a_norm = torch.from_numpy(np.stack([normalize_adjacency(A)] * B)).float()
+    m.eval()
+    with torch.no_grad():
+        y_eval = m(x, a_norm)
+    m.train()
+    m.gcn.dropout.p = 0.0
+    m.classifier[2].p = 0.0
+    y = m(x, a_norm)
+    labels = torch.tensor([1, 0])
+    loss = torch.nn.functional.cross_entropy(y, labels)
+    loss.backward()
+    rec = dict(x_seed=13, shape=np.array([B, N, 3, 224, 224]), a_norm=a_norm.numpy(), y_eval=y_eval.numpy(),
+               y_train=y.detach().numpy(), labels=labels.numpy(), loss=np.array(float(loss)), seed=12)
+    rec.update(grad_fingerprint(m.named_parameters()))
+    np.savez_compressed(os.path.join(HERE, "vit_gcn_224.npz"), **rec)
+
+
 def main():
     _install_shims()
     torch.set_num_threads(8)
-    gen_b0_detector()
-    gen_train_step()
-    gen_logic_rnn()
-    gen_cnn_lstm()
+    only = sys.argv[1:]
+    for name, fn in [("b0", gen_b0_detector), ("step", gen_train_step), ("rnn", gen_logic_rnn),
+                     ("cnn_lstm", gen_cnn_lstm), ("vit_gcn", gen_vit_gcn)]:
+        if not only or name in only:
+            fn()
     print("golden fixtures written to", HERE)
 
 

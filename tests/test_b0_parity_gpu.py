@@ -27,7 +27,7 @@ def _det(seed, dtype="fp32", dropout=0.5, cuda=None):
     return det.to(cuda)
 
 
-@pytest.mark.parametrize("shape", [(2, 64, 64), (3, 96, 80)])
+@pytest.mark.parametrize("shape", [(2, 64, 64), (3, 96, 80), (1, 224, 224)])
 @pytest.mark.parametrize("training", [True, False])
 def test_trunk_layerwise_fp32(cuda, shape, training):
     n, h, w = shape
@@ -127,3 +127,20 @@ def test_detector_train_bf16_close(cuda, golden_dir):
         if ref_norm > 1e-6 and abs(float(gr.norm()) - ref_norm) <= 0.1 * ref_norm:
             norms_ok += 1
     assert norms_ok >= 0.9 * len(names), (norms_ok, len(names))
+
+
+def test_detector_train_bf16_deterministic(cuda, golden_dir):
+    """Two identical bf16 training steps give bit-identical logits, gradients and BN running
+    statistics: every reduction (BN statistics, weight gradients, SE squeezes) is fixed-order."""
+    g = np.load(os.path.join(golden_dir, "b0_train_64.npz"))
+    x = torch.from_numpy(g["x"]).to(cuda)
+    outs = []
+    for _ in range(2):
+        det = _det(int(g["seed"]), "bf16", dropout=0.0, cuda=cuda).train()
+        logits, _ = det(x)
+        logits.float().sum().backward()
+        grads = torch.cat([p.grad.flatten() for p in det.parameters()])
+        bufs = torch.cat([b.float().flatten() for b in det.buffers()])
+        outs.append((logits.detach().clone(), grads.clone(), bufs.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from deepfake_amd.weights import deterministic_init_, hash_uniform
 from oracle import b0_cpu
-from oracle.detector_cpu import (CNNLSTMHybridCPU, DetectorCPU, LogicRNNLSTMCPU, collate_cnn_lstm,
+from oracle.detector_cpu import (CNNLSTMHybridCPU, DetectorCPU, LogicRNNLSTMCPU, collate_cnn_lstm, collate_vit_gcn,
                                  train_step)
 from b0_helpers import frames
 
@@ -188,3 +188,38 @@ def test_frames_generator_matches_fixture(golden_dir):
     """The synthetic-frame generator used by the GPU tests reproduces the fixture inputs."""
     g = _load(golden_dir, "b0_eval_64.npz")
     torch.testing.assert_close(frames(1, (2, 4, 3, 64, 64)), torch.from_numpy(g["x"]), rtol=0, atol=0)
+
+
+def test_collate_vit_gcn_golden(golden_dir):
+    g = _load(golden_dir, "collate_vit_gcn.npz")
+    batch = []
+    for i, m in enumerate(g["counts"].tolist()):
+        f = (np.arange(m * 4 * 4 * 3, dtype=np.int64) * 11 + i * 5) % 256
+        batch.append({"faces": f.astype(np.uint8).reshape(m, 4, 4, 3), "label": i % 2})
+    x, a_norm, y = collate_vit_gcn(batch, max_nodes=16, image_size=(4, 4))
+    torch.testing.assert_close(x, torch.from_numpy(g["nodes"]), rtol=0, atol=0)
+    torch.testing.assert_close(a_norm, torch.from_numpy(g["a_norm"]), rtol=0, atol=0)
+    assert y.tolist() == g["labels"].tolist()
+
+
+def test_vit_gcn_golden(golden_dir):
+    """DeepfakeModel (models.py:222-291) with the ViT restatement: eval logits, train logits,
+    CE loss and every gradient against the reference run (timm stand-in = oracle/vit_cpu.py)."""
+    from oracle.vit_cpu import DeepfakeModelCPU
+    g = _load(golden_dir, "vit_gcn_224.npz")
+    m = DeepfakeModelCPU()
+    deterministic_init_(m, seed=int(g["seed"]))
+    x = frames(int(g["x_seed"]), tuple(int(v) for v in g["shape"]))
+    a = torch.from_numpy(g["a_norm"])
+    m.eval()
+    with torch.no_grad():
+        torch.testing.assert_close(m(x, a), torch.from_numpy(g["y_eval"]), rtol=1e-4, atol=1e-6)
+    m.train()
+    m.gcn.dropout.p = 0.0
+    m.classifier[2].p = 0.0
+    y = m(x, a)
+    torch.testing.assert_close(y.detach(), torch.from_numpy(g["y_train"]), rtol=1e-4, atol=1e-6)
+    loss = torch.nn.functional.cross_entropy(y, torch.from_numpy(g["labels"]))
+    loss.backward()
+    assert abs(float(loss) - float(g["loss"])) <= 1e-5 * abs(float(g["loss"])) + 1e-7
+    _check_fingerprint(_grads(m), g, "g", rtol=1e-3, atol=1e-7)
