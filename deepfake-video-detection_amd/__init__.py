@@ -9,6 +9,7 @@ Drop-in counterparts of the reference's hot-path API (SaiPranav1506/DeepFake-Vid
 * ``train_step`` / ``DataParallelTrainer``                 (EnsembleTrainer.train_epoch step, ensemble_trainer.py:182-200)
 * ``LogicRNNLSTM`` / ``LogicCell`` / ``create_model``       (src/RNNModel.py)
 * ``CNNLSTMHybrid``                                       (src/models.py:20-85)
+* ``DeepfakeModel`` / ``ViTFeatureExtractor`` / ``SimpleGCN`` (src/models.py:88-107, 199-291)
 
 Compute runs in hand-written HIP kernels for gfx950 behind the C ABI of ``include/dfd_hip.h``
 (``libdfd_hip.so``); PyTorch supplies device memory, streams and torch.distributed (RCCL).
@@ -18,7 +19,7 @@ Submodules import lazily so ``import deepfake_amd`` works before the library is 
 __all__ = [
     "PretrainedBackboneDetector", "EnsembleDetector", "EfficientNetB0Trunk", "B0FrameExtractor",
     "WeightedCrossEntropyLoss", "FusedAdamW", "FusedAdam", "clip_grad_norm_", "LogicRNNLSTM", "LogicCell",
-    "create_model", "CNNLSTMHybrid",
+    "create_model", "CNNLSTMHybrid", "DeepfakeModel", "ViTFeatureExtractor", "SimpleGCN",
 ]
 
 
@@ -35,6 +36,8 @@ def __getattr__(name):
         from . import rnn as m
     elif name == "CNNLSTMHybrid":
         from . import cnn_lstm as m
+    elif name in ("DeepfakeModel", "ViTFeatureExtractor", "SimpleGCN"):
+        from . import vit_gcn as m
     else:
         raise AttributeError(name)
     return getattr(m, name)

@@ -57,6 +57,16 @@ _SIGS = {
     "dfd_rnn_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_rnn_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_u64, c_f]),
     "dfd_rnn_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_p, c_fpp, c_u64, c_f]),
+    "dfd_vit_param_count": (c_i, [c_i]),
+    "dfd_vit_work_bytes": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
+    "dfd_vit_scratch_bytes": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
+    "dfd_vit_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, ctypes.POINTER(c_i64), c_fpp, c_p, c_p]),
+    "dfd_vit_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_fpp, c_p, c_p, c_p, c_fpp]),
+    "dfd_gcn_head_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i]),
+    "dfd_gcn_head_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i]),
+    "dfd_gcn_head_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_fpp, c_p, c_i, c_u64, c_f, c_p]),
+    "dfd_gcn_head_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_fpp, c_p, c_p, c_i, c_u64, c_f, c_p,
+                                    c_fpp, c_p]),
     "dfd_cnnlstm_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i, c_i]),
     "dfd_cnnlstm_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i, c_i]),
     "dfd_cnnlstm_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, ctypes.POINTER(c_i64), c_fpp, c_fpp,

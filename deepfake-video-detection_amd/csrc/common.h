@@ -141,7 +141,15 @@ __host__ __device__ __forceinline__ int64_t cdiv64(int64_t a, int64_t b) { retur
 //   PRO_NONE      a = y
 //   PRO_BN_SILU   a = silu(y*scale[c] + shift[c])
 //   PRO_BN_SILU_G a = silu(y*scale[c] + shift[c]) * gate[frame][c]
-enum ProMode { PRO_NONE = 0, PRO_BN_SILU = 1, PRO_BN_SILU_G = 2 };
+//   PRO_GELU      a = gelu(y)   (exact erf form; ViT MLP, no per-channel parameters)
+enum ProMode { PRO_NONE = 0, PRO_BN_SILU = 1, PRO_BN_SILU_G = 2, PRO_GELU = 3 };
+constexpr bool pro_is_bn(int mode) { return mode == PRO_BN_SILU || mode == PRO_BN_SILU_G; }
+
+// torch.nn.functional.gelu (approximate='none'): 0.5 x (1 + erf(x / sqrt 2)) and its derivative
+__device__ __forceinline__ float geluf_(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float dgeluf_(float x) {
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
 
 struct Pro {
   const float* scale;  // [C]

@@ -660,13 +660,13 @@ int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const
 // ------------------------------------------------------------------ slab reduce
 // out[i] (+)= sum_s slab[s][i]; block = 64 consecutive elements x 16 split lanes (fixed order)
 __global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ slab, int splits, int64_t n,
-                                                            float* out, int accumulate) {
+                                                            int64_t stride, float* out, int accumulate) {
   __shared__ float sh[1024];
   const int tid = threadIdx.x, il = tid & 63, sl = tid >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + il;
   float a = 0.f;
   if (i < n)
-    for (int sp = sl; sp < splits; sp += 16) a += slab[(int64_t)sp * n + i];
+    for (int sp = sl; sp < splits; sp += 16) a += slab[(int64_t)sp * stride + i];
   sh[tid] = a;
   __syncthreads();
   for (int o = 8; o > 0; o >>= 1) {
@@ -677,8 +677,13 @@ __global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restr
 }
 
 int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate) {
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)cdiv64(n, 64)), dim3(1024), 0, s, slab, splits, n, out,
-                     accumulate ? 1 : 0);
+  return launch_reduce_slabs_strided(s, slab, splits, n, n, out, accumulate);
+}
+
+int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, int64_t n, int64_t stride, float* out,
+                                bool accumulate) {
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)cdiv64(n, 64)), dim3(1024), 0, s, slab, splits, n, stride,
+                     out, accumulate ? 1 : 0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

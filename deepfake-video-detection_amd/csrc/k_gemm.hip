@@ -37,11 +37,13 @@ __device__ __forceinline__ void lds_st8(T* p, const float (&v)[8]) { st8(p, v); 
 template <typename T>
 __device__ __forceinline__ void lds_ld8(const T* p, float (&v)[8]) { ld8(p, v); }
 
-template <typename T, int MODE, bool STATS, bool RESID>
+template <typename T, int MODE, bool STATS, int EPI>
 __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                      T* __restrict__ C, const T* __restrict__ R, int64_t M,
-                                                      int N, int K, Pro pro, float* __restrict__ stats,
+                                                      T* __restrict__ C, const T* __restrict__ R,
+                                                      const float* __restrict__ bias, const T* __restrict__ Z,
+                                                      int64_t M, int N, int K, Pro pro, float* __restrict__ stats,
                                                       int64_t tiles_m, int ntn) {
+  constexpr bool RESID = (EPI & EPI_RESID) != 0, BIAS = (EPI & EPI_BIAS) != 0, DGELU = (EPI & EPI_DGELU) != 0;
   using G = GemmCfg<T>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   __shared__ float st_sum[GBN];
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
   float pg[MODE == PRO_BN_SILU_G ? 2 : 1][8];
   // producer BN scale/shift of all K columns, staged once per workgroup (dynamic LDS, 2K floats)
   extern __shared__ float pro_lds[];
-  if constexpr (MODE != PRO_NONE) {
+  if constexpr (pro_is_bn(MODE)) {
     for (int i = tid; i < K; i += 256) {
       pro_lds[i] = pro.scale[i];
       pro_lds[K + i] = pro.shift[i];
@@ -85,9 +87,9 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
       raw_ld(ra[i], A + gm * K + gk, A, gm < M && kok);
       raw_ld(rb[i], B + (int64_t)(n0 + srow + 64 * i) * K + gk, B, srow + 64 * i < nvalid && kok);
     }
-    if constexpr (MODE != PRO_NONE) {
+    if constexpr (MODE == PRO_BN_SILU_G) {
       const int kc = kok ? gk : 0;
-      if constexpr (MODE == PRO_BN_SILU_G) {
+      {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int64_t gm = m0 + srow + 64 * i;
@@ -117,6 +119,12 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
         const int row = srow + 64 * i;
         if constexpr (MODE == PRO_NONE) {
           raw_st(As + row * G::AS + skc, ra[i]);
+        } else if constexpr (MODE == PRO_GELU) {
+          float x[8];
+          raw_to_f(ra[i], x);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);  // masked lanes hold 0 and gelu(0) = 0
+          lds_st8(As + row * G::AS + skc, x);
         } else {
           float x[8], psc[8], psh[8];
           raw_to_f(ra[i], x);
@@ -177,13 +185,15 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
     for (int cb = 0; cb < 8; ++cb) {
       if (cb < nb) {
         const int col = cb * 16 + (lane & 15);
+        float bcol = 0.f;
+        if constexpr (BIAS) bcol = col < nvalid ? bias[n0 + col] : 0.f;
         float s = 0.f, q = 0.f;
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = wave * 32 + rb * 16 + 4 * (lane >> 4) + r;
-            const float v = Tr<T>::round(acc[rb][cb][r]);
+            const float v = Tr<T>::round(acc[rb][cb][r] + bcol);
             Cs[row * G::CS + col] = Tr<T>::from_f(v);
             if constexpr (STATS) {
               if (m0 + row < M) { s += v; q += v * v; }
@@ -221,6 +231,12 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] += r8[j];
       }
+      if constexpr (DGELU) {
+        float z8[8];
+        ld8(Z + gm * N + n0 + cv, z8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] *= dgeluf_(z8[j]);
+      }
       st8(C + gm * N + n0 + cv, x);
     }
     lds_barrier();
@@ -234,35 +250,64 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
 }
 
 template <typename T>
-int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K, int pro_mode,
-                   const Pro& pro, float* stats, int* stat_rows) {
+static int gemm_dispatch(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z,
+                         int64_t M, int N, int K, int pro_mode, int epi, const Pro& pro, float* stats, int* stat_rows) {
   if (M <= 0) return 0;
   if ((N & 7) || (K & 7)) { set_error("pw_gemm: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
   if (M > (int64_t)UINT32_MAX) { set_error("pw_gemm: M exceeds 2^32 rows", __FILE__, __LINE__); return -1; }
+  if (((epi & EPI_RESID) && !R) || ((epi & EPI_BIAS) && !bias) || ((epi & EPI_DGELU) && !Z)) {
+    set_error("pw_gemm: epilogue operand missing", __FILE__, __LINE__);
+    return -1;
+  }
   const int ntn = cdiv(N, GBN);
   const int64_t tiles_m = cdiv64(M, GBM);
   const int64_t cap = std::max<int64_t>(1, 1024 / ntn);
   const int gx = (int)std::min<int64_t>(tiles_m, cap);
   dim3 grid((unsigned)(gx * ntn)), block(256);
-  const bool st = stats != nullptr, rs = R != nullptr;
-  const size_t dyn = pro_mode != PRO_NONE ? 2 * (size_t)K * sizeof(float) : 0;
-#define DFD_GEMM_LAUNCH(MODE, ST, RS) \
-  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, RS>), grid, block, dyn, s, A, B, C, R, M, N, K, pro, stats, tiles_m, \
-                     ntn)
-  if (rs) {
-    if (pro_mode != PRO_NONE || st) { set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__); return -1; }
-    DFD_GEMM_LAUNCH(PRO_NONE, false, true);
-  } else if (pro_mode == PRO_NONE) {
-    if (st) DFD_GEMM_LAUNCH(PRO_NONE, true, false); else DFD_GEMM_LAUNCH(PRO_NONE, false, false);
-  } else if (pro_mode == PRO_BN_SILU) {
-    if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU, true, false); else DFD_GEMM_LAUNCH(PRO_BN_SILU, false, false);
-  } else {
-    if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU_G, true, false); else DFD_GEMM_LAUNCH(PRO_BN_SILU_G, false, false);
+  const bool st = stats != nullptr;
+  const size_t dyn = pro_is_bn(pro_mode) ? 2 * (size_t)K * sizeof(float) : 0;
+#define DFD_GEMM_LAUNCH(MODE, ST, EP) \
+  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, EP>), grid, block, dyn, s, A, B, C, R, bias, Z, M, N, K, pro, stats, \
+                     tiles_m, ntn)
+  // instantiated combinations: the B0 trunk's (BN prologues, BN-stat epilogue, residual) and the
+  // ViT's (bias, bias + residual, GELU prologue + bias + residual, GELU-derivative epilogue)
+  if (pro_mode == PRO_NONE && epi == EPI_RESID && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_RESID);
+  else if (pro_mode == PRO_NONE && epi == 0) {
+    if (st) DFD_GEMM_LAUNCH(PRO_NONE, true, 0); else DFD_GEMM_LAUNCH(PRO_NONE, false, 0);
+  } else if (pro_mode == PRO_BN_SILU && epi == 0) {
+    if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU, true, 0); else DFD_GEMM_LAUNCH(PRO_BN_SILU, false, 0);
+  } else if (pro_mode == PRO_BN_SILU_G && epi == 0) {
+    if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU_G, true, 0); else DFD_GEMM_LAUNCH(PRO_BN_SILU_G, false, 0);
+  } else if (pro_mode == PRO_NONE && epi == EPI_BIAS && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_BIAS);
+  else if (pro_mode == PRO_NONE && epi == (EPI_BIAS | EPI_RESID) && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_BIAS | EPI_RESID);
+  else if (pro_mode == PRO_GELU && epi == (EPI_BIAS | EPI_RESID) && !st) DFD_GEMM_LAUNCH(PRO_GELU, false, EPI_BIAS | EPI_RESID);
+  else if (pro_mode == PRO_NONE && epi == EPI_DGELU && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_DGELU);
+  else {
+    set_error("pw_gemm: unsupported prologue/epilogue combination", __FILE__, __LINE__);
+    return -1;
   }
 #undef DFD_GEMM_LAUNCH
   if (stat_rows) *stat_rows = gx;
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
+}
+
+template <typename T>
+int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K, int pro_mode,
+                   const Pro& pro, float* stats, int* stat_rows) {
+  if (R && (pro_mode != PRO_NONE || stats)) {
+    set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__);
+    return -1;
+  }
+  return gemm_dispatch<T>(s, A, B, C, R, nullptr, nullptr, M, N, K, pro_mode, R ? EPI_RESID : 0, pro, stats,
+                          stat_rows);
+}
+
+template <typename T>
+int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,
+                   int N, int K, int pro_mode, int epi) {
+  Pro none{};
+  return gemm_dispatch<T>(s, A, B, C, R, bias, Z, M, N, K, pro_mode, epi, none, nullptr, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -301,7 +346,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
   const bool yc = cv < nv, xc = cv < kv;
   const int kc = k0 + (xc ? cv : 0);
   float sc[8], sh[8];
-  if constexpr (MODE != PRO_NONE) {
+  if constexpr (pro_is_bn(MODE)) {
     ld8f(pro.scale + kc, sc);
     ld8f(pro.shift + kc, sh);
   }
@@ -342,6 +387,9 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
         if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * rg[i][j];
+        } else if constexpr (MODE == PRO_GELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]);
@@ -437,6 +485,8 @@ int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, in
     hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_NONE>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
   else if (pro_mode == PRO_BN_SILU)
     hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
+  else if (pro_mode == PRO_GELU)
+    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_GELU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
   else
     hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU_G>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
   DFD_HIP_CHECK(hipGetLastError());
@@ -447,6 +497,10 @@ template int launch_pw_gemm<float>(hipStream_t, const float*, const float*, floa
                                    int, const Pro&, float*, int*);
 template int launch_pw_gemm<bf16>(hipStream_t, const bf16*, const bf16*, bf16*, const bf16*, int64_t, int, int, int,
                                   const Pro&, float*, int*);
+template int launch_tf_gemm<float>(hipStream_t, const float*, const float*, float*, const float*, const float*,
+                                   const float*, int64_t, int, int, int, int);
+template int launch_tf_gemm<bf16>(hipStream_t, const bf16*, const bf16*, bf16*, const bf16*, const float*, const bf16*,
+                                  int64_t, int, int, int, int);
 template int launch_pw_wgrad<float>(hipStream_t, const float*, const float*, int64_t, int, int, int, const Pro&,
                                     float*, int64_t, float*, bool);
 template int launch_pw_wgrad<bf16>(hipStream_t, const bf16*, const bf16*, int64_t, int, int, int, const Pro&, float*,

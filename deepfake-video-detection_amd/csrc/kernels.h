@@ -14,6 +14,12 @@ namespace dfd {
 template <typename T>
 int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K,
                    int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+// Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
+// pro_mode PRO_NONE or PRO_GELU; epi a mask of GemmEpi.
+enum GemmEpi { EPI_RESID = 1, EPI_BIAS = 2, EPI_DGELU = 4 };
+template <typename T>
+int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,
+                   int N, int K, int pro_mode, int epi);
 // dW[N][K] = sum_m dY[m][n] * pro(X)[m][k]  -> written (or added) into dW (fp32) via slabs
 template <typename T>
 int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, int pro_mode,
@@ -92,6 +98,9 @@ template <typename T>
 int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat);
 // sum `splits` slabs of n floats into out (= or +=)
 int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate);
+// the same with slab rows `stride` floats apart
+int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, int64_t n, int64_t stride, float* out,
+                                bool accumulate);
 
 // ---------------- stem (3->32, k3 s2): k_stem.hip ----------------
 struct StemGeom {

@@ -164,6 +164,40 @@ DFD_API int dfd_cnnlstm_backward(void* stream, int B, int T, int H, int W, int h
                                  float* scratch, int training, uint64_t seed, float p, const float* dlogits,
                                  float* const* grads);
 
+/* ---------------- DeepfakeModel: ViT-B/16 trunk + SimpleGCN head (C5) ----------------
+ * Replaces ViTFeatureExtractor.forward (src/models.py:88-107: timm vit_base_patch16_224,
+ * num_classes=0 -> CLS features after the final norm) and SimpleGCN + pooling + classifier
+ * (src/models.py:199-219, 280-291), forward and backward (train.py:104-133 trains it).
+ * dtype 0 = fp32 storage (parity), 1 = bf16 storage; fp32 accumulation.  depth 12 is the
+ * reference's model (smaller depths only for tests).  Images: 224x224, fp32, element strides
+ * x_strides5 = (b, n, c, h, w) of a (B, N, 3, H, W) tensor; images = B*N.
+ * params: dfd_vit_param_count(depth) pointers in timm named_parameters() order (cls_token,
+ * pos_embed, patch_embed.proj.{weight,bias}, blocks.{i}.{norm1,attn.qkv,attn.proj,norm2,mlp.fc1,
+ * mlp.fc2}.{weight,bias}, norm.{weight,bias}).  feats: (images, 768) fp32.
+ * work (dfd_vit_work_bytes) is kept from forward to backward; backward overwrites grads. */
+DFD_API int dfd_vit_param_count(int depth);
+DFD_API int64_t dfd_vit_work_bytes(int dtype, int depth, int images, int height, int width);
+DFD_API int64_t dfd_vit_scratch_bytes(int dtype, int depth, int images, int height, int width);
+DFD_API int dfd_vit_forward(void* stream, int dtype, int depth, int images, int nodes, int height, int width,
+                            const float* x, const int64_t* x_strides5, const float* const* params, void* work,
+                            float* feats);
+DFD_API int dfd_vit_backward(void* stream, int dtype, int depth, int images, int height, int width,
+                             const float* const* params, void* work, void* scratch, const float* dfeats,
+                             float* const* grads);
+/* GCN head: feats (B*N, feat_dim) -> H = A_norm @ feats -> relu(fc1) -> dropout(p) -> relu(fc2) ->
+ * mean over N -> classifier Linear(out,64) / ReLU / Dropout(p) / Linear(64, classes).
+ * params (8): gcn.fc1.{weight,bias}, gcn.fc2.{weight,bias}, classifier.0.*, classifier.3.*.
+ * Dropout: the library's counter hash (streams 40, 41), p applied only when training. */
+DFD_API int64_t dfd_gcn_head_work_floats(int B, int N, int feat_dim, int hid, int out, int num_classes);
+DFD_API int64_t dfd_gcn_head_scratch_floats(int B, int N, int feat_dim, int hid, int out, int num_classes);
+DFD_API int dfd_gcn_head_forward(void* stream, int B, int N, int feat_dim, int hid, int out, int num_classes,
+                                 const float* feats, const float* a_norm, const float* const* params, float* work,
+                                 int training, uint64_t seed, float p, float* logits);
+DFD_API int dfd_gcn_head_backward(void* stream, int B, int N, int feat_dim, int hid, int out, int num_classes,
+                                  const float* a_norm, const float* const* params, const float* work,
+                                  float* scratch, int training, uint64_t seed, float p, const float* dlogits,
+                                  float* const* grads, float* dfeats);
+
 #ifdef __cplusplus
 }
 #endif
