@@ -53,6 +53,11 @@ _SIGS = {
     "dfd_ce_backward": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i64, c_p, c_p, c_p]),
     "dfd_grad_norm": (c_i, [c_p, c_p, c_i64, c_f, c_p, c_p]),
     "dfd_adam_step": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_i, c_d, c_i, c_p]),
+    "dfd_set_tuning": (c_i64, [ctypes.c_char_p, c_i64]),
+    "dfd_pw_conv": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p,
+                          ctypes.POINTER(c_i)]),
+    "dfd_pw_conv_wgrad": (c_i, [c_p, c_i, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i64, c_p,
+                                c_i]),
     "dfd_rnn_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_rnn_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_rnn_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_fpp, c_p, c_p, c_u64, c_f]),

@@ -255,6 +255,59 @@ int dfd_adam_step(void* stream, float* params, float* grads, float* m, float* v,
   DFD_GUARD_END
 }
 
+int64_t dfd_set_tuning(const char* key, int64_t value) {
+  if (key && strcmp(key, "stream_min_rows") == 0) return dfd::set_stream_min_rows(value);
+  dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
+  return -1;
+}
+
+static bool pw_args_ok(int dtype, int64_t M, int N, int K, int pro_mode, const float* scale, const float* shift,
+                       const float* gate, int rows_per_frame) {
+  if (dtype != DFD_DTYPE_F32 && dtype != DFD_DTYPE_BF16) { dfd::set_error("pw: bad dtype", __FILE__, __LINE__); return false; }
+  if (M < 0 || N <= 0 || K <= 0) { dfd::set_error("pw: bad shape", __FILE__, __LINE__); return false; }
+  if (pro_mode != dfd::PRO_NONE && pro_mode != dfd::PRO_BN_SILU && pro_mode != dfd::PRO_BN_SILU_G) {
+    dfd::set_error("pw: bad prologue mode", __FILE__, __LINE__);
+    return false;
+  }
+  if (pro_mode != dfd::PRO_NONE && (!scale || !shift)) { dfd::set_error("pw: scale/shift missing", __FILE__, __LINE__); return false; }
+  if (pro_mode == dfd::PRO_BN_SILU_G && (!gate || rows_per_frame <= 0)) {
+    dfd::set_error("pw: gate / rows_per_frame missing", __FILE__, __LINE__);
+    return false;
+  }
+  return true;
+}
+
+int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, const void* R, int64_t M, int N, int K,
+                int pro_mode, const float* scale, const float* shift, const float* gate, int rows_per_frame,
+                float* stats, int* stat_rows) {
+  DFD_GUARD_BEGIN
+  if (!pw_args_ok(dtype, M, N, K, pro_mode, scale, shift, gate, rows_per_frame)) return -1;
+  const dfd::Pro pro{scale, shift, gate, rows_per_frame, K};
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFD_DTYPE_BF16)
+    return dfd::launch_pw_gemm<dfd::bf16>(s, (const dfd::bf16*)A, (const dfd::bf16*)W, (dfd::bf16*)C,
+                                          (const dfd::bf16*)R, M, N, K, pro_mode, pro, stats, stat_rows);
+  return dfd::launch_pw_gemm<float>(s, (const float*)A, (const float*)W, (float*)C, (const float*)R, M, N, K, pro_mode,
+                                    pro, stats, stat_rows);
+  DFD_GUARD_END
+}
+
+int dfd_pw_conv_wgrad(void* stream, int dtype, const void* dY, const void* X, int64_t M, int N, int K, int pro_mode,
+                      const float* scale, const float* shift, const float* gate, int rows_per_frame, float* slab,
+                      int64_t slab_floats, float* dW, int accumulate) {
+  DFD_GUARD_BEGIN
+  if (!pw_args_ok(dtype, M, N, K, pro_mode, scale, shift, gate, rows_per_frame)) return -1;
+  if (!slab || slab_floats < (int64_t)N * K) { dfd::set_error("pw wgrad: slab smaller than N*K", __FILE__, __LINE__); return -1; }
+  const dfd::Pro pro{scale, shift, gate, rows_per_frame, K};
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == DFD_DTYPE_BF16)
+    return dfd::launch_pw_wgrad<dfd::bf16>(s, (const dfd::bf16*)dY, (const dfd::bf16*)X, M, N, K, pro_mode, pro, slab,
+                                           slab_floats, dW, accumulate != 0);
+  return dfd::launch_pw_wgrad<float>(s, (const float*)dY, (const float*)X, M, N, K, pro_mode, pro, slab, slab_floats,
+                                     dW, accumulate != 0);
+  DFD_GUARD_END
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------- LogicRNNLSTM

@@ -299,6 +299,10 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
     set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__);
     return -1;
   }
+  if constexpr (sizeof(T) == 2) {
+    const int rc = launch_pw_stream(s, A, B, C, R, M, N, K, pro_mode, pro, stats, stat_rows);
+    if (rc <= 0) return rc;
+  }
   return gemm_dispatch<T>(s, A, B, C, R, nullptr, nullptr, M, N, K, pro_mode, R ? EPI_RESID : 0, pro, stats,
                           stat_rows);
 }

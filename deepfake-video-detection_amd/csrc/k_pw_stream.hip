@@ -1,0 +1,373 @@
+// Streaming pointwise (1x1 conv) GEMM for the tall-skinny layers of EfficientNet-B0 (bf16).
+//
+// Same contract as pw_gemm_kernel (k_gemm.hip) -- C[M][N] = pro(A)[M][K] . B[N][K]^T with the
+// producer's BN+SiLU(+SE gate) prologue, BN-stat partials of C's columns and the residual add
+// of the dgrad -- for the high-resolution layers (M = frames*H*W rows large, K <= 256), where
+// the pass is a pure HBM stream: every A row is read once and every C row written once, and the
+// weight chunk (<= 128 x 256 bf16) sits in LDS for the whole launch.
+//
+// Per wave, independent of the other waves (no barrier after the LDS staging):
+//   * 16-row groups of A are loaded straight from HBM into MFMA operand fragments
+//     (lane = row lane&15, 8 consecutive k at 8*(lane>>4): one 16-B load per lane and k-block),
+//     the prologue is applied in registers, the next groups are in flight during the MFMAs;
+//   * v_mfma_f32_16x16x32_bf16 computes the TRANSPOSED tile D[n][m] = W[n][:] . A[m][:], so a
+//     lane ends up holding 4 consecutive output channels of one row; the rounded tile goes
+//     through a wave-private LDS slab (no workgroup barrier) so the global stores are 16 B per
+//     lane with consecutive lanes on consecutive bytes of a row (full 128-B lines);
+//   * BN-stat partials accumulate per lane across all groups of the wave (fixed order) and are
+//     reduced once at the end: 16-lane shuffles, then the 4 waves in order (bit-reproducible).
+// The SE gates of the (few) frames a workgroup's rows belong to are staged in LDS with the
+// weights and the producer's BN coefficients.  Grid: parts x N-chunks, chunk fastest, so the
+// workgroups that read the same A rows are adjacent in dispatch order (A re-reads hit L2).
+// Shapes it does not cover go to pw_gemm_kernel.
+#include "kernels.h"
+
+#include <algorithm>
+#include <atomic>
+
+namespace dfd {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+// Row threshold above which the streaming kernel takes a layer (below it the tiled kernel's
+// weight reuse wins); settable through dfd_set_tuning("stream_min_rows", v).
+static std::atomic<int64_t> g_stream_min_rows{100000};
+int64_t set_stream_min_rows(int64_t v) { return g_stream_min_rows.exchange(v); }
+
+template <int NB, int U>
+struct StreamTile {
+  static constexpr int NC = NB * 16;
+  static constexpr int CS = NC + 8;                // LDS row stride of the C slab (elements)
+  static constexpr int VPR = NC / 8;               // 16-B vectors per row
+  static constexpr int NV = (U * 16 * VPR + 63) / 64;  // vectors per lane per iteration
+  static constexpr int SLAB = U * 16 * CS * 2;     // bytes per wave
+};
+
+template <int KB, int U, bool RESID, int NV>
+struct StreamRegs {
+  Raw8<bf16> a[U][KB];
+  uint4 r[RESID ? NV : 1];
+};
+
+template <int NB, int KB, int U, int MODE, bool STATS, bool RESID>
+__global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           bf16* __restrict__ C, const bf16* __restrict__ R,
+                                                           int64_t M, int N, int K, Pro pro,
+                                                           float* __restrict__ stats, int nchunks,
+                                                           int64_t groups_per_part, int gate_frames) {
+  constexpr int NC = NB * 16, KP = KB * 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* Bs = reinterpret_cast<uint4*>(smem);                   // [NB][KB][64] operand fragments
+  float* psc = reinterpret_cast<float*>(smem + NB * KB * 1024);  // [KP] producer BN scale
+  float* psh = psc + KP;                                         // [KP] producer BN shift
+  float* red = psh + KP;                                         // [4][2][NC] stat partials
+  float* gl = red + 8 * NC;                                      // [gate_frames][KP] SE gates
+  using TL = StreamTile<NB, U>;
+  bf16* ct = reinterpret_cast<bf16*>(gl + gate_frames * KP) + (threadIdx.x >> 6) * (TL::SLAB / 2);  // wave's C slab
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int chunk = (int)(blockIdx.x % (unsigned)nchunks);
+  const int64_t part = blockIdx.x / (unsigned)nchunks;
+  const int n0 = chunk * NC;
+
+  for (int f = tid; f < NB * KB * 64; f += 256) {
+    const int ln = f & 63, kb = (f >> 6) % KB, nb = (f >> 6) / KB;
+    const int n = n0 + nb * 16 + (ln & 15), k = kb * 32 + 8 * (ln >> 4);
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (n < N && k < K) v = *reinterpret_cast<const uint4*>(B + (int64_t)n * K + k);
+    Bs[f] = v;
+  }
+  if constexpr (pro_is_bn(MODE)) {
+    for (int k = tid; k < KP; k += 256) {
+      psc[k] = k < K ? pro.scale[k] : 0.f;
+      psh[k] = k < K ? pro.shift[k] : 0.f;
+    }
+  }
+  const int64_t G = (M + 15) >> 4;
+  const int64_t gbeg = part * groups_per_part;
+  const int64_t gend = min(G, gbeg + groups_per_part);
+  // SE gates of the frames this part's rows belong to (at most gate_frames, sized at launch)
+  int f_first = 0;
+  if constexpr (MODE == PRO_BN_SILU_G) {
+    if (gbeg < gend) {
+      f_first = (int)((gbeg * 16) / pro.rows_per_frame);
+      const int f_last = (int)((min(gend * 16, M) - 1) / pro.rows_per_frame);
+      const int nfr = min(gate_frames, f_last - f_first + 1);
+      for (int i = tid; i < nfr * KP; i += 256) {
+        const int fr = i / KP, k = i - fr * KP;
+        gl[i] = k < K ? pro.gate[(int64_t)(f_first + fr) * pro.C + k] : 0.f;
+      }
+    }
+  }
+  __syncthreads();
+
+  const int lr = lane & 15, lk = 8 * (lane >> 4), ln4 = 4 * (lane >> 4);
+
+  StreamRegs<KB, U, RESID, TL::NV> rg;
+  auto load = [&](int64_t g0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = (g0 + u) * 16 + lr;
+      const bool rok = g0 + u < gend && row < M;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const int k = kb * 32 + lk;
+        raw_ld(rg.a[u][kb], A + row * K + k, A, rok && k < K);
+      }
+    }
+    if constexpr (RESID) {  // the residual in the store-phase layout (16 B per lane)
+#pragma unroll
+      for (int i = 0; i < TL::NV; ++i) {
+        const int v = lane + 64 * i, rr = v / TL::VPR, cv = (v - rr * TL::VPR) * 8;
+        const int64_t row = g0 * 16 + rr;
+        const bool ok = rr < U * 16 && g0 * 16 + rr < min(gend * 16, M) && n0 + cv < N;
+        rg.r[i] = *reinterpret_cast<const uint4*>(ok ? R + row * N + n0 + cv : R);
+      }
+    }
+  };
+
+  float s_acc[STATS ? NB : 1][4], q_acc[STATS ? NB : 1][4];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s_acc[nb][r] = 0.f; q_acc[nb][r] = 0.f; }
+  }
+
+  const int64_t step = 4 * U;
+  int64_t g = gbeg + (int64_t)wave * U;
+  if (g < gend) load(g);
+  for (; g < gend; g += step) {
+    // keep the LDS operand/coefficient reads inside the loop (hoisted, they would pin up to
+    // 2*KP + 4*NB*KB registers per lane and spill the gated variants)
+    asm volatile("" ::: "memory");
+    // ---- prologue in registers: raw A -> bf16 MFMA operands ----
+    bf16x8_t af[U][KB];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int fr = 0;
+      if constexpr (MODE == PRO_BN_SILU_G) {
+        const int64_t row = (g + u) * 16 + lr;
+        fr = (g + u < gend && row < M) ? (int)((uint32_t)row / (uint32_t)pro.rows_per_frame) - f_first : 0;
+      }
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const uint32_t m = rg.a[u][kb].ok ? 0xffffffffu : 0u;
+        if constexpr (MODE == PRO_NONE) {
+          const uint4 v = make_uint4(rg.a[u][kb].a.x & m, rg.a[u][kb].a.y & m, rg.a[u][kb].a.z & m,
+                                     rg.a[u][kb].a.w & m);
+          af[u][kb] = __builtin_bit_cast(bf16x8_t, v);
+        } else {
+          float x[8], sc[8], sh[8];
+          raw_to_f(rg.a[u][kb], x);
+          const int k = kb * 32 + lk;
+          ld8(psc + k, sc);
+          ld8(psh + k, sh);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]);
+          if constexpr (MODE == PRO_BN_SILU_G) {
+            float gv[8];
+            ld8(gl + fr * KP + k, gv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] *= gv[j];
+          }
+          const uint4 v = make_uint4(pack2bf(x[0], x[1]) & m, pack2bf(x[2], x[3]) & m, pack2bf(x[4], x[5]) & m,
+                                     pack2bf(x[6], x[7]) & m);
+          af[u][kb] = __builtin_bit_cast(bf16x8_t, v);
+          asm volatile("" ::: "memory");  // one k-block's coefficients live at a time
+        }
+      }
+    }
+    uint4 rres[RESID ? TL::NV : 1];
+    if constexpr (RESID) {
+#pragma unroll
+      for (int i = 0; i < TL::NV; ++i) rres[i] = rg.r[i];
+    }
+    // ---- next groups in flight before the MFMAs and stores of this one ----
+    if (g + step < gend) load(g + step);
+
+    f32x4_t acc[U][NB];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[u][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const bf16x8_t wf = __builtin_bit_cast(bf16x8_t, Bs[(nb * KB + kb) * 64 + lane]);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          acc[u][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af[u][kb], acc[u][nb], 0, 0, 0);
+      }
+
+    // ---- epilogue: lane = row lr, channels n .. n+3: stats from registers, bf16 into the slab ----
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = (g + u) * 16 + lr;
+      const bool rok = g + u < gend && row < M;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int n = n0 + nb * 16 + ln4;
+        const uint2 pk = make_uint2(pack2bf(acc[u][nb][0], acc[u][nb][1]), pack2bf(acc[u][nb][2], acc[u][nb][3]));
+        if constexpr (STATS) {
+          const bool ok = rok && n < N;
+          const float v[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                              __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float w = ok ? v[r] : 0.f;
+            s_acc[nb][r] += w;
+            q_acc[nb][r] += w * w;
+          }
+        }
+        *reinterpret_cast<uint2*>(ct + (u * 16 + lr) * TL::CS + nb * 16 + ln4) = pk;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // ---- row-contiguous 16-B stores (+ residual: C = bf16(bf16(acc) + R)) ----
+    const int64_t rend = min(gend * 16, M);
+#pragma unroll
+    for (int i = 0; i < TL::NV; ++i) {
+      const int v = lane + 64 * i, rr = v / TL::VPR, cv = (v - rr * TL::VPR) * 8;
+      const int64_t row = g * 16 + rr;
+      if (rr < U * 16 && row < rend && n0 + cv < N) {
+        uint4 o = *reinterpret_cast<const uint4*>(ct + rr * TL::CS + cv);
+        if constexpr (RESID) {
+          float x[8], y[8];
+          ld8(reinterpret_cast<const bf16*>(&o), x);
+          ld8(reinterpret_cast<const bf16*>(&rres[i]), y);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] += y[j];
+          o = make_uint4(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]), pack2bf(x[4], x[5]), pack2bf(x[6], x[7]));
+        }
+        *reinterpret_cast<uint4*>(C + row * N + n0 + cv) = o;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  if constexpr (STATS) {
+    // lanes sharing lane>>4 hold the same 4 channels for 16 different rows
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = s_acc[nb][r], q = q_acc[nb][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        if (lr == 0) {
+          red[(wave * 2 + 0) * NC + nb * 16 + ln4 + r] = s;
+          red[(wave * 2 + 1) * NC + nb * 16 + ln4 + r] = q;
+        }
+      }
+    __syncthreads();
+    for (int i = tid; i < NC; i += 256) {
+      if (n0 + i < N) {
+        stats[(part * 2 + 0) * N + n0 + i] =
+            ((red[0 * NC + i] + red[2 * NC + i]) + red[4 * NC + i]) + red[6 * NC + i];
+        stats[(part * 2 + 1) * N + n0 + i] =
+            ((red[1 * NC + i] + red[3 * NC + i]) + red[5 * NC + i]) + red[7 * NC + i];
+      }
+    }
+  }
+}
+
+template <int NB, int KB, int MODE, bool STATS, bool RESID>
+static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, int64_t M, int N, int K,
+                         const Pro& pro, float* stats, int* stat_rows) {
+  constexpr int U = KB <= 2 ? 2 : 1;
+  using TL = StreamTile<NB, U>;
+  auto kern = pw_stream_kernel<NB, KB, U, MODE, STATS, RESID>;
+  const int nchunks = cdiv(N, NB * 16);
+  const int64_t G = cdiv64(M, 16);
+  const size_t lds_fixed = (size_t)NB * KB * 1024 + 2 * (size_t)KB * 32 * 4 + 8 * (size_t)NB * 16 * 4 + 4 * TL::SLAB;
+  // persistent grid: exactly the workgroups that are co-resident (one wave of dispatch, no
+  // tail), measured once per instantiation at the LDS size without gate rows
+  static const int resident = [&] {
+    int dev = 0, cus = 256, per_cu = 2;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds_fixed) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    return std::max(1, cus * per_cu);
+  }();
+  int64_t parts = std::max<int64_t>(1, std::min<int64_t>(std::max(1, resident / nchunks), cdiv64(G, 4 * U)));
+  const int64_t gpp = cdiv64(cdiv64(G, parts), 4 * U) * (4 * U);
+  parts = cdiv64(G, gpp);
+  int gate_frames = 0;
+  if (MODE == PRO_BN_SILU_G) {
+    // frames one part's rows can touch; past 16 the gate table would crowd the LDS budget
+    gate_frames = (int)std::min<int64_t>(cdiv64(M, pro.rows_per_frame), cdiv64(gpp * 16, pro.rows_per_frame) + 1);
+    if (gate_frames > 16) return 1;
+  }
+  const size_t lds = lds_fixed + (size_t)gate_frames * KB * 32 * 4;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(parts * nchunks)), dim3(256), lds, s, A, B, C, R, M, N, K, pro, stats,
+                     nchunks, gpp, gate_frames);
+  DFD_HIP_CHECK(hipGetLastError());
+  if (stat_rows) *stat_rows = (int)parts;
+  return 0;
+}
+
+// 0: launched; 1: not covered (shape/mode without an instantiation, or M below the threshold;
+// the caller uses the tiled kernel); -1: launch error
+int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, int64_t M, int N, int K,
+                     int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
+  if (M <= 0 || M < g_stream_min_rows.load(std::memory_order_relaxed) || K > 256 || (N & 7) || (K & 7)) return 1;
+  const int nchunks = cdiv(N, 128);
+  const int NB = cdiv(cdiv(N, nchunks), 16), KB = cdiv(K, 32);
+  const bool st = stats != nullptr, rs = R != nullptr;
+  const int key = NB * 16 + KB;
+#define DFD_STREAM_CASE(NB_, KB_, MODE_, ST_, RS_) \
+  case NB_ * 16 + KB_:                             \
+    return stream_launch<NB_, KB_, MODE_, ST_, RS_>(s, A, B, C, R, M, N, K, pro, stats, stat_rows);
+  if (pro_mode == PRO_NONE && st && !rs) {  // conv_pw forward (expansion): N = mid, K = cin
+    switch (key) {
+      DFD_STREAM_CASE(6, 1, PRO_NONE, true, false)  // 16 -> 96
+      DFD_STREAM_CASE(5, 1, PRO_NONE, true, false)  // 24 -> 144
+      DFD_STREAM_CASE(8, 2, PRO_NONE, true, false)  // 40 -> 240
+      DFD_STREAM_CASE(8, 3, PRO_NONE, true, false)  // 80 -> 480
+      DFD_STREAM_CASE(7, 4, PRO_NONE, true, false)  // 112 -> 672
+      default: return 1;
+    }
+  }
+  if (pro_mode == PRO_BN_SILU_G && st && !rs) {  // conv_pwl forward: N = cout, K = mid
+    switch (key) {
+      DFD_STREAM_CASE(1, 1, PRO_BN_SILU_G, true, false)  // 32 -> 16 (stage 0)
+      DFD_STREAM_CASE(2, 3, PRO_BN_SILU_G, true, false)  // 96 -> 24
+      DFD_STREAM_CASE(2, 5, PRO_BN_SILU_G, true, false)  // 144 -> 24
+      DFD_STREAM_CASE(3, 5, PRO_BN_SILU_G, true, false)  // 144 -> 40
+      // 240 -> 40 (KB 8) spills at 256 VGPRs: left to the tiled kernel
+      default: return 1;
+    }
+  }
+  if (pro_mode == PRO_NONE && !st && !rs) {  // dgrads: conv_pw (N = cin, K = mid), conv_pwl (N = mid, K = cout)
+    switch (key) {
+      DFD_STREAM_CASE(1, 3, PRO_NONE, false, false)  // 96 -> 16
+      DFD_STREAM_CASE(2, 5, PRO_NONE, false, false)  // 144 -> 24
+      DFD_STREAM_CASE(3, 8, PRO_NONE, false, false)  // 240 -> 40
+      DFD_STREAM_CASE(2, 1, PRO_NONE, false, false)  // 16 -> 32 (stage 0)
+      DFD_STREAM_CASE(6, 1, PRO_NONE, false, false)  // 24 -> 96
+      DFD_STREAM_CASE(5, 1, PRO_NONE, false, false)  // 24 -> 144
+      DFD_STREAM_CASE(5, 2, PRO_NONE, false, false)  // 40 -> 144
+      DFD_STREAM_CASE(8, 2, PRO_NONE, false, false)  // 40 -> 240
+      DFD_STREAM_CASE(8, 3, PRO_NONE, false, false)  // 80 -> 240 / 480
+      default: return 1;
+    }
+  }
+  if (pro_mode == PRO_NONE && !st && rs) {  // conv_pw dgrad plus the block's skip gradient
+    switch (key) {
+      DFD_STREAM_CASE(2, 5, PRO_NONE, false, true)  // 144 -> 24
+      DFD_STREAM_CASE(3, 8, PRO_NONE, false, true)  // 240 -> 40
+      default: return 1;
+    }
+  }
+#undef DFD_STREAM_CASE
+  return 1;
+}
+
+}  // namespace dfd

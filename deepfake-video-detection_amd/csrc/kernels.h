@@ -14,6 +14,12 @@ namespace dfd {
 template <typename T>
 int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K,
                    int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+// Streaming variant for tall-skinny bf16 layers (k_pw_stream.hip): 0 launched, 1 not covered
+// (shape/mode without an instantiation, or M below the streaming threshold), -1 error.
+int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, int64_t M, int N, int K,
+                     int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+// rows threshold of the streaming kernels (returns the previous value)
+int64_t set_stream_min_rows(int64_t v);
 // Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
 // pro_mode PRO_NONE or PRO_GELU; epi a mask of GemmEpi.
 enum GemmEpi { EPI_RESID = 1, EPI_BIAS = 2, EPI_DGELU = 4 };

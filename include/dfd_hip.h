@@ -123,6 +123,29 @@ DFD_API int dfd_adam_step(void* stream, float* params, float* grads, float* exp_
                           double lr, double beta1, double beta2, double eps, double weight_decay, int step,
                           double grad_scale, int decoupled, const float* clip_out2);
 
+/* Kernel-selection knobs (process-wide; returns the previous value, -1 for an unknown key).
+ * "stream_min_rows": bf16 1x1 convs with at least this many rows use the streaming kernel
+ * (default 100000; 0 routes every covered shape there, a huge value routes none). */
+DFD_API int64_t dfd_set_tuning(const char* key, int64_t value);
+
+/* ---- pointwise (1x1) convolution, the trunk's conv_pw / conv_pwl / conv_head kernels ----------
+ * Replaces aten conv2d(kernel_size=1, bias=False) on NHWC activations as timm's MBConv blocks
+ * run it inside self.backbone(x_flat) (src/pretrained_detector.py:116), with the producing
+ * layer's BatchNorm+SiLU (+ squeeze-excite gate) applied to the input on the fly:
+ *   C[M][N] = pro(A)[M][K] . W[N][K]^T (+ R[M][N])
+ *   pro_mode 0: a = x;  1: a = silu(x*scale[k] + shift[k]);  2: the same times gate[m / rows_per_frame][k].
+ * dtype DFD_DTYPE_F32 (fp32 storage) or DFD_DTYPE_BF16 (bf16 storage); fp32 accumulation; N, K
+ * multiples of 8.  stats (optional, R must then be NULL): per-column partial sums of C and C^2 in
+ * rows [*stat_rows][2][N] (room for 1024*2*N floats).  Used by the trunk and the kernel tests. */
+DFD_API int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, const void* R, int64_t M,
+                        int N, int K, int pro_mode, const float* scale, const float* shift, const float* gate,
+                        int rows_per_frame, float* stats, int* stat_rows);
+/* Weight gradient of the same conv: dW[N][K] (=, or += if accumulate) sum_m dY[m][n] * pro(X)[m][k],
+ * fp32 output; slab: fp32 scratch of slab_floats >= N*K (deterministic split-M partials). */
+DFD_API int dfd_pw_conv_wgrad(void* stream, int dtype, const void* dY, const void* X, int64_t M, int N, int K,
+                              int pro_mode, const float* scale, const float* shift, const float* gate,
+                              int rows_per_frame, float* slab, int64_t slab_floats, float* dW, int accumulate);
+
 /* ---- LogicRNNLSTM (src/RNNModel.py:43-147), fp32 ----
  * Replaces LogicRNNLSTM.forward (RNNModel.py:81-133) and its autograd backward.
  * x: (B, T, IN) fp32 contiguous.  order: the reference's sort_idx of lengths.sort(0, descending=True)

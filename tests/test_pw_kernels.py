@@ -1,0 +1,123 @@
+"""1x1-conv kernels (dfd_pw_conv / dfd_pw_conv_wgrad) against a plain PyTorch fp32 reference.
+
+The trunk's conv_pw / conv_pwl / conv_head run as C[M][N] = pro(A)[M][K] . W[N][K]^T on NHWC
+rows, where pro() is the producing layer's BatchNorm+SiLU (+ squeeze-excite gate), replacing
+aten conv2d(kernel_size=1) inside timm's MBConv blocks (reached from
+src/pretrained_detector.py:116).  bf16 storage: the reference takes the same bf16-rounded
+operands (the kernel rounds pro(A) to bf16 before the MFMA) and accumulates in fp32; the output
+is bf16-rounded, so it is compared at bf16 resolution.  Both the streaming kernel (tall layers)
+and the tiled kernel (everything else) are exercised via dfd_set_tuning("stream_min_rows").
+"""
+import ctypes
+
+import pytest
+import torch
+
+from deepfake_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib_():
+    return _lib.load()
+
+
+def _pro(a, mode, scale, shift, gate, rpf):
+    x = a.float()
+    if mode == 0:
+        return x
+    x = torch.nn.functional.silu(x * scale + shift)
+    if mode == 2:
+        f = torch.arange(x.shape[0], device=x.device) // rpf
+        x = x * gate[f]
+    return x
+
+
+def _inputs(M, N, K, mode, rpf, seed, dev):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    a = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=g, device=dev) / K ** 0.5).to(torch.bfloat16)
+    scale = torch.rand(K, generator=g, device=dev) + 0.5
+    shift = torch.randn(K, generator=g, device=dev) * 0.1
+    frames = (M + rpf - 1) // rpf
+    gate = torch.rand(frames, K, generator=g, device=dev)
+    return a, w, scale, shift, gate
+
+
+def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0):
+    lib = _lib_()
+    a, w, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed, dev)
+    r = torch.randn(M, N, device=dev).to(torch.bfloat16) if resid else None
+    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(1024 * 2 * N, device=dev) if stats else None
+    rows = ctypes.c_int(0)
+    prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
+    try:
+        _lib.check(lib.dfd_pw_conv(_lib.stream_of(dev), 1, a.data_ptr(), w.data_ptr(), c.data_ptr(), _lib.ptr(r), M,
+                                   N, K, mode, scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf,
+                                   _lib.ptr(st), ctypes.byref(rows)))
+        torch.cuda.synchronize()
+    finally:
+        lib.dfd_set_tuning(b"stream_min_rows", prev)
+    ap = _pro(a, mode, scale, shift, gate, rpf).to(torch.bfloat16).float()
+    ref = ap @ w.float().t()
+    if resid:
+        ref = ref.to(torch.bfloat16).float() + r.float()
+    got = c.float()
+    err = (got - ref).abs()
+    tol = 1e-2 * ref.abs() + 1e-2 * ref.abs().mean()
+    assert bool((err <= tol).all()), f"max err {float(err.max())} (ref mean {float(ref.abs().mean())})"
+    if stats:
+        n = rows.value
+        assert 1 <= n <= 1024
+        s = st.view(-1)[: n * 2 * N].view(n, 2, N).double().sum(0)
+        torch.testing.assert_close(s[0], got.double().sum(0), rtol=1e-4, atol=1e-2)
+        torch.testing.assert_close(s[1], (got.double() ** 2).sum(0), rtol=1e-4, atol=1e-2)
+
+
+# (M, N, K, mode, resid, stats): the B0 1x1 shapes of the high-resolution stages, ragged M
+STREAM_CASES = [
+    (100355, 96, 16, 0, False, True),    # blocks.1.0 conv_pw
+    (50021, 144, 24, 0, False, True),    # blocks.1.1 conv_pw (two N chunks)
+    (20007, 240, 40, 0, False, True),    # blocks.2.1 conv_pw
+    (20007, 480, 80, 0, False, True),    # blocks.3.x conv_pw
+    (9999, 672, 112, 0, False, True),    # blocks.4.x conv_pw
+    (100355, 16, 32, 2, False, True),    # blocks.0.0 conv_pw (project, gated)
+    (50021, 24, 96, 2, False, True),     # blocks.1.0 conv_pwl
+    (50021, 24, 144, 2, False, True),    # blocks.1.1 conv_pwl
+    (20007, 40, 144, 2, False, True),    # blocks.2.0 conv_pwl
+    (100355, 16, 96, 0, False, False),   # blocks.1.0 conv_pw dgrad
+    (50021, 24, 144, 0, True, False),    # blocks.1.1 conv_pw dgrad + skip
+    (20007, 40, 240, 0, True, False),    # blocks.2.1 conv_pw dgrad + skip
+    (20007, 40, 240, 0, False, False),   # blocks.3.0 conv_pw dgrad
+    (100355, 32, 16, 0, False, False),   # blocks.0.0 conv_pw dgrad
+    (50021, 96, 24, 0, False, False),    # blocks.1.0 conv_pwl dgrad
+    (50021, 144, 40, 0, False, False),   # blocks.2.0 conv_pwl dgrad
+    (20007, 240, 40, 0, False, False),   # blocks.2.1 conv_pwl dgrad
+    (20007, 480, 80, 0, False, False),   # blocks.3.x conv_pwl dgrad
+]
+
+
+@pytest.mark.parametrize("case", STREAM_CASES, ids=lambda c: "x".join(map(str, c[:3])) + f"_m{c[3]}r{int(c[4])}")
+@pytest.mark.parametrize("path", ["stream", "tiled"])
+def test_pw_conv_bf16(cuda, case, path):
+    M, N, K, mode, resid, stats = case
+    _run(M, N, K, mode, resid, stats, 0 if path == "stream" else 1 << 60, cuda, rpf=784 if M < 30000 else 3136)
+
+
+@pytest.mark.parametrize("case", [(12544, 192, 1152, 2, False, True), (12544, 1152, 192, 0, False, True),
+                                  (12544, 1280, 320, 0, False, True), (12544, 320, 1280, 0, False, False)])
+def test_pw_conv_bf16_late_layers(cuda, case):
+    M, N, K, mode, resid, stats = case
+    _run(M, N, K, mode, resid, stats, 0, cuda, rpf=49)
+
+
+def test_pw_conv_rejects_bad_args(cuda):
+    lib = _lib_()
+    rows = ctypes.c_int(0)
+    assert lib.dfd_pw_conv(None, 7, None, None, None, None, 16, 8, 8, 0, None, None, None, 0, None,
+                           ctypes.byref(rows)) == -1
+    assert b"dtype" in lib.dfd_last_error()
+    assert lib.dfd_pw_conv(None, 1, None, None, None, None, 16, 8, 8, 2, None, None, None, 0, None,
+                           ctypes.byref(rows)) == -1
