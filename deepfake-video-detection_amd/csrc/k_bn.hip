@@ -446,6 +446,311 @@ int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro,
   return 0;
 }
 
+// ------------------------------------------------------------------ SE + BN backward, one pass
+// Backward of  out = silu(z) * gate[f][c] (feeding conv_pwl),  z = y*scale + shift (BN, batch
+// stats), sq = mean_hw silu(z) (SE squeeze).  With ge = dL/dout and bc[f][c] = dL/dsq / HW the
+// BN's input gradient is g = (ge*gate + bc) * silu'(z); since gate and bc are constant per
+// (frame, channel), every reduction the backward needs decomposes into per-frame sums that one
+// pass over (ge, y) produces before bc is known:
+//   D  = sum ge*silu(z)      (-> dgate, the SE branch)
+//   P1 = sum ge*silu'(z)     P2 = sum silu'(z)     P3 = sum ge*silu'(z)*xhat     P4 = sum silu'(z)*xhat
+// so that  sum g = sum_f gate*P1 + bc*P2  and  sum g*xhat = sum_f gate*P3 + bc*P4.  This replaces
+// the separate SE-backward reduction and BN-backward reduction (two full passes over ge and y).
+template <typename T>
+__global__ __launch_bounds__(256) void se_bn_bwd_kernel(const T* __restrict__ dZ, const T* __restrict__ Y,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        const float* __restrict__ mean,
+                                                        const float* __restrict__ invstd, int frames, int HW, int C,
+                                                        int hsplit, int vpg, float* __restrict__ part) {
+  __shared__ float sh[5][256][8];
+  const int tid = threadIdx.x;
+  const int vec = tid % vpg, pl = tid / vpg, npl = 256 / vpg;
+  const int f = blockIdx.x / hsplit, h = blockIdx.x % hsplit;
+  const int c = (blockIdx.y * vpg + vec) * 8;
+  const int chunk = (HW + hsplit - 1) / hsplit;
+  const int p0 = h * chunk, p1 = min(HW, p0 + chunk);
+  float acc[5][8];
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+  if (pl < npl && c < C) {
+    float sc[8], shf[8], mu[8], is[8];
+    ld8f(scale + c, sc);
+    ld8f(shift + c, shf);
+    ld8f(mean + c, mu);
+    ld8f(invstd + c, is);
+    for (int p = p0 + pl; p < p1; p += npl) {
+      const int64_t row = (int64_t)f * HW + p;
+      float y[8], d[8];
+      ld8(Y + row * C + c, y);
+      ld8(dZ + row * C + c, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float z = y[j] * sc[j] + shf[j];
+        const float sg = sigmoidf_(z);
+        const float sp = sg * (1.0f + z * (1.0f - sg));
+        const float xh = (y[j] - mu[j]) * is[j];
+        const float dsp = d[j] * sp;
+        acc[0][j] += d[j] * (z * sg);
+        acc[1][j] += dsp;
+        acc[2][j] += sp;
+        acc[3][j] += dsp * xh;
+        acc[4][j] += sp * xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sh[q][tid][j] = acc[q][j];
+  __syncthreads();
+  if (tid < vpg && c < C) {
+    for (int r = 1; r < npl; ++r)
+#pragma unroll
+      for (int q = 0; q < 5; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[q][j] += sh[q][r * vpg + tid][j];
+    const int64_t n = (int64_t)frames * C;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      float* o = part + ((int64_t)q * hsplit + h) * n + (int64_t)f * C + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = acc[q][j];
+    }
+  }
+}
+
+// out[q][i] = sum_h part[q][h][i], q < 5 (h in order)
+__global__ void sum_parts5_kernel(const float* __restrict__ part, int hsplit, int64_t n, float* __restrict__ dgate,
+                                  float* __restrict__ pf) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < 5 * n; i += (int64_t)gridDim.x * 256) {
+    const int64_t q = i / n, k = i - q * n;
+    float a = 0.f;
+    for (int h = 0; h < hsplit; ++h) a += part[(q * hsplit + h) * n + k];
+    if (q == 0) dgate[k] = a;
+    else pf[(q - 1) * n + k] = a;
+  }
+}
+
+template <typename T>
+int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, int frames, int HW, int C, float* part,
+                            int64_t part_cap, float* dgate, float* pf) {
+  int vpg, groups;
+  bn_vpg_groups(C, vpg, groups);
+  const int npl = 256 / vpg;
+  if (5 * (int64_t)frames * C > part_cap) { set_error("se/bn bwd: partial buffer too small", __FILE__, __LINE__); return -1; }
+  int hsplit = 1;
+  while ((int64_t)frames * groups * hsplit < 1024 && HW / (hsplit * 2) >= npl * 2 &&
+         5 * (int64_t)(hsplit * 2) * frames * C <= part_cap)
+    hsplit *= 2;
+  hipLaunchKernelGGL((se_bn_bwd_kernel<T>), dim3(frames * hsplit, groups), dim3(256), 0, s, dZ, Y, scale, shift, mean,
+                     invstd, frames, HW, C, hsplit, vpg, part);
+  DFD_HIP_CHECK(hipGetLastError());
+  const int64_t n = (int64_t)frames * C;
+  hipLaunchKernelGGL(sum_parts5_kernel, dim3(ew_grid(5 * n)), dim3(256), 0, s, part, hsplit, n, dgate, pf);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// BN backward finalize from the per-frame sums of se_bn_bwd_kernel once bc is known:
+// dbeta = sum g, dgamma = sum g*xhat, coefficients k1..k3 of dy = k1*g + k2*y + k3 (fp64).
+// Block = 64 channels x 16 frame slices (the slices' frames unrolled by 4, all loads issued
+// up front); slices added in order.
+constexpr int FF_SL = 16;
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
+    const float* __restrict__ pf, const float* __restrict__ gate, const float* __restrict__ bc, int frames, int C,
+    int64_t count, const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
+    int training, float* dgamma, float* dbeta, int accumulate, float* coef) {
+  __shared__ double red[2][FF_SL][64];
+  const int tid = threadIdx.x, cl = tid & 63, sl = tid >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int64_t n = (int64_t)frames * C;
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    const int per = (frames + FF_SL - 1) / FF_SL;
+    const int f0 = sl * per, f1 = min(frames, f0 + per);
+    int f = f0;
+    for (; f + 4 <= f1; f += 4) {
+      float gt[4], b[4], p1[4], p2[4], p3[4], p4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = (int64_t)(f + u) * C + c;
+        gt[u] = gate[i]; b[u] = bc[i];
+        p1[u] = pf[i]; p2[u] = pf[n + i]; p3[u] = pf[2 * n + i]; p4[u] = pf[3 * n + i];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s += (double)gt[u] * (double)p1[u] + (double)b[u] * (double)p2[u];
+        q += (double)gt[u] * (double)p3[u] + (double)b[u] * (double)p4[u];
+      }
+    }
+    for (; f < f1; ++f) {
+      const int64_t i = (int64_t)f * C + c;
+      s += (double)gate[i] * (double)pf[i] + (double)bc[i] * (double)pf[n + i];
+      q += (double)gate[i] * (double)pf[2 * n + i] + (double)bc[i] * (double)pf[3 * n + i];
+    }
+  }
+  red[0][sl][cl] = s;
+  red[1][sl][cl] = q;
+  __syncthreads();
+  if (sl == 0 && c < C) {
+    s = 0.0;
+    q = 0.0;
+    for (int k = 0; k < FF_SL; ++k) { s += red[0][k][cl]; q += red[1][k][cl]; }
+    const float db = (float)s, dg = (float)q;
+    if (accumulate) { dbeta[c] += db; dgamma[c] += dg; }
+    else { dbeta[c] = db; dgamma[c] = dg; }
+    const double gm = gamma[c], is = invstd[c];
+    double k2 = 0.0, k3 = 0.0;
+    if (training) {
+      const double cnt = (double)count;
+      k2 = -gm * is * is * q / cnt;
+      k3 = -gm * is * s / cnt + gm * is * is * (double)mean[c] * q / cnt;
+    }
+    coef[c] = (float)(gm * is);
+    coef[C + c] = (float)k2;
+    coef[2 * C + c] = (float)k3;
+  }
+}
+
+int launch_bn_bwd_finalize_frames(hipStream_t s, const float* pf, const float* gate, const float* bc, int frames,
+                                  int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
+                                  bool training, float* dgamma, float* dbeta, bool accumulate, float* coef) {
+  hipLaunchKernelGGL(bn_bwd_finalize_frames_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, pf, gate, bc, frames, C, count,
+                     gamma, mean, invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ conv_pw backward through its BN
+// The BN after conv_pw (no activation) has the input gradient ge1 = k1*g + k2*y1 + k3 (per output
+// channel k of the conv; bn_bwd_finalize), and y1 = x . W^T is itself a linear function of the
+// block input x.  By linearity the conv's gradients need g and x only -- never y1, and no
+// materialised ge1 (three full passes over the 6x-expanded tensor saved):
+//   dX = g . (diag(k1) W) + x . (W^T diag(k2) W) + W^T k3
+//   dW = diag(k1) (g^T x) + diag(k2) W (x^T x) + k3 (1^T x)
+// bn_fold_pw: W1t[c][k] = W[k][c] k1[k] (dgrad operand), Q[c][c'] = sum_k W[k][c] k2[k] W[k][c'],
+// bv[c] = sum_k k3[k] W[k][c]  (W: fp32 master weights [mid][cin]; sums in fp64, k ascending).
+// One workgroup per input channel c (plus one more block per 256 W1t elements): row c of Q and
+// bv[c] as k-sliced dot products (4 slices of k per output, fp64, slices added in order).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_fold_pw_kernel(const float* __restrict__ W, const float* __restrict__ coef,
+                                                         int mid, int cin, T* __restrict__ w1t, T* __restrict__ q,
+                                                         float* __restrict__ bv) {
+  __shared__ double red[4][64];
+  if ((int)blockIdx.x >= cin) {  // W1t[c][k] = W[k][c] k1[k]
+    const int64_t i = (int64_t)(blockIdx.x - cin) * 256 + threadIdx.x;
+    if (i < (int64_t)cin * mid) {
+      const int c = (int)(i / mid), k = (int)(i - (int64_t)c * mid);
+      w1t[i] = Tr<T>::from_f(W[(int64_t)k * cin + c] * coef[k]);
+    }
+    return;
+  }
+  const int c = blockIdx.x, tid = threadIdx.x, cl = tid & 63, sl = tid >> 6;
+  const int per = (mid + 3) / 4, k0 = sl * per, k1 = min(mid, k0 + per);
+  for (int c2b = 0; c2b <= cin; c2b += 64) {  // column cin = bv
+    const int c2 = c2b + cl;
+    double a = 0.0;
+    if (c2 < cin) {
+      for (int k = k0; k < k1; ++k) a += (double)(W[(int64_t)k * cin + c] * coef[mid + k]) * W[(int64_t)k * cin + c2];
+    } else if (c2 == cin) {
+      for (int k = k0; k < k1; ++k) a += (double)coef[2 * mid + k] * W[(int64_t)k * cin + c];
+    }
+    red[sl][cl] = a;
+    __syncthreads();
+    if (sl == 0 && c2 <= cin) {
+      const double v = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+      if (c2 < cin) q[(int64_t)c * cin + c2] = Tr<T>::from_f((float)v);
+      else bv[c] = (float)v;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+int launch_bn_fold_pw(hipStream_t s, const float* W, const float* coef, int mid, int cin, T* w1t, T* q, float* bv) {
+  const int blocks = cin + (int)cdiv64((int64_t)cin * mid, 256);
+  hipLaunchKernelGGL((bn_fold_pw_kernel<T>), dim3((unsigned)blocks), dim3(256), 0, s, W, coef, mid, cin, w1t, q, bv);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// dW[k][c] (+)= k1[k] Tg[k][c] + k2[k] sum_c' W[k][c'] G[c'][c] + k3[k] cs[c]: one workgroup per k,
+// W row in LDS, thread c sums c' in order (fp64)
+__global__ __launch_bounds__(256) void pw_wgrad_bn_combine_kernel(const float* __restrict__ Tg,
+                                                                  const float* __restrict__ G,
+                                                                  const float* __restrict__ cs,
+                                                                  const float* __restrict__ W,
+                                                                  const float* __restrict__ coef, int mid, int cin,
+                                                                  float* dW, int accumulate) {
+  __shared__ float wr[256];
+  const int k = blockIdx.x;
+  for (int i = threadIdx.x; i < cin; i += 256) wr[i] = W[(int64_t)k * cin + i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < cin; c += 256) {
+    double t = 0.0;
+    for (int c2 = 0; c2 < cin; ++c2) t += (double)wr[c2] * G[(int64_t)c2 * cin + c];
+    const int64_t i = (int64_t)k * cin + c;
+    const double a = (double)coef[k] * Tg[i] + (double)coef[mid + k] * t + (double)coef[2 * mid + k] * cs[c];
+    dW[i] = accumulate ? dW[i] + (float)a : (float)a;
+  }
+}
+
+int launch_pw_wgrad_bn_combine(hipStream_t s, const float* Tg, const float* G, const float* cs, const float* W,
+                               const float* coef, int mid, int cin, float* dW, bool accumulate) {
+  if (cin > 256) { set_error("pw bn combine: cin > 256", __FILE__, __LINE__); return -1; }
+  hipLaunchKernelGGL(pw_wgrad_bn_combine_kernel, dim3((unsigned)mid), dim3(256), 0, s, Tg, G, cs, W, coef, mid, cin,
+                     dW, accumulate ? 1 : 0);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// column sums of X [M][C]: part rows [gx][C] (vpg threads per row, rows strided, fixed-order
+// tree over the block's row lanes), then the slab reducer
+template <typename T>
+__global__ __launch_bounds__(256) void col_sums_kernel(const T* __restrict__ X, int64_t M, int C, int vpg,
+                                                       float* __restrict__ part) {
+  __shared__ float sh[256][8];
+  const int tid = threadIdx.x, vec = tid % vpg, rl = tid / vpg, nrl = 256 / vpg;
+  const int c = (blockIdx.y * vpg + vec) * 8;
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  if (rl < nrl && c < C) {
+    for (int64_t r = (int64_t)blockIdx.x * nrl + rl; r < M; r += (int64_t)gridDim.x * nrl) {
+      float x[8];
+      ld8(X + r * C + c, x);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += x[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sh[tid][j] = a[j];
+  __syncthreads();
+  if (tid < vpg && c < C) {
+    for (int r = 1; r < nrl; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += sh[r * vpg + tid][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[(int64_t)blockIdx.x * C + c + j] = a[j];
+  }
+}
+
+template <typename T>
+int launch_col_sums(hipStream_t s, const T* X, int64_t M, int C, float* part, int64_t part_cap, float* out) {
+  int vpg, groups;
+  bn_vpg_groups(C, vpg, groups);
+  const int nrl = 256 / vpg;
+  int64_t gx = std::max<int64_t>(1, std::min<int64_t>(cdiv64(M, nrl * 8), std::max(1, 1024 / groups)));
+  gx = std::max<int64_t>(1, std::min<int64_t>(gx, part_cap / C));
+  hipLaunchKernelGGL((col_sums_kernel<T>), dim3((unsigned)gx, groups), dim3(256), 0, s, X, M, C, vpg, part);
+  DFD_HIP_CHECK(hipGetLastError());
+  return launch_reduce_slabs(s, part, (int)gx, C, out, false);
+}
+
 template <typename T>
 int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat) {
   // HW is tiny (7x7 at 224^2): one partial per frame, write means directly
@@ -480,22 +785,21 @@ __device__ __forceinline__ void block_sum_rd(float (&acc)[RD], float* red, float
   __syncthreads();
 }
 
+// rpre[f][j] = br[j] + sum_c wr[j][c] sq[f][c]: one workgroup per frame, wave w owns the reduce
+// channels j = w, w+4, ...: a coalesced dot product over c per j (ascending c per lane, then a
+// fixed-order wave sum).
 template <int RD>
 __global__ __launch_bounds__(256) void se_rd_kernel(const float* __restrict__ sq, const float* __restrict__ wr,
                                                     const float* __restrict__ br, int C, float* __restrict__ rpre) {
-  __shared__ float red[4 * RD];
-  __shared__ float s_o[RD];
-  const int f = blockIdx.x, tid = threadIdx.x;
-  float acc[RD];
-#pragma unroll
-  for (int j = 0; j < RD; ++j) acc[j] = 0.f;
-  for (int c = tid; c < C; c += 256) {
-    const float v = sq[(int64_t)f * C + c];
-#pragma unroll
-    for (int j = 0; j < RD; ++j) acc[j] = fmaf(wr[(int64_t)j * C + c], v, acc[j]);
+  const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* x = sq + (int64_t)f * C;
+  for (int j = wave; j < RD; j += 4) {
+    const float* w = wr + (int64_t)j * C;
+    float a = 0.f;
+    for (int c = lane; c < C; c += 64) a = fmaf(w[c], x[c], a);
+    a = wave_sum(a);
+    if (lane == 0) rpre[(int64_t)f * RD + j] = a + br[j];
   }
-  block_sum_rd<RD>(acc, red, s_o);
-  if (tid < RD) rpre[(int64_t)f * RD + tid] = s_o[tid] + br[tid];
 }
 
 template <int RD>
@@ -695,7 +999,11 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
   template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, float*);     \
   template int launch_se_bwd_reduce<T>(hipStream_t, const T*, const T*, const Pro&, int, int, int, float*, int64_t, \
                                        float*);                                                                     \
-  template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);
+  template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);                            \
+  template int launch_se_bn_bwd_reduce<T>(hipStream_t, const T*, const T*, const float*, const float*, const float*, \
+                                          const float*, int, int, int, float*, int64_t, float*, float*);      \
+  template int launch_bn_fold_pw<T>(hipStream_t, const float*, const float*, int, int, T*, T*, float*);             \
+  template int launch_col_sums<T>(hipStream_t, const T*, int64_t, int, float*, int64_t, float*);
 DFD_BN_INST(float)
 DFD_BN_INST(bf16)
 #undef DFD_BN_INST

@@ -300,7 +300,7 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
     return -1;
   }
   if constexpr (sizeof(T) == 2) {
-    const int rc = launch_pw_stream(s, A, B, C, R, M, N, K, pro_mode, pro, stats, stat_rows);
+    const int rc = launch_pw_stream(s, A, B, C, R, nullptr, M, N, K, pro_mode, pro, stats, stat_rows);
     if (rc <= 0) return rc;
   }
   return gemm_dispatch<T>(s, A, B, C, R, nullptr, nullptr, M, N, K, pro_mode, R ? EPI_RESID : 0, pro, stats,
@@ -311,6 +311,13 @@ template <typename T>
 int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,
                    int N, int K, int pro_mode, int epi) {
   Pro none{};
+  if constexpr (sizeof(T) == 2) {
+    if (pro_mode == PRO_NONE && (epi & EPI_BIAS) && !(epi & EPI_DGELU) && bias && (R || !(epi & EPI_RESID))) {
+      const int rc = launch_pw_stream(s, A, B, C, (epi & EPI_RESID) ? R : nullptr, bias, M, N, K, PRO_NONE, none,
+                                      nullptr, nullptr);
+      if (rc <= 0) return rc;
+    }
+  }
   return gemm_dispatch<T>(s, A, B, C, R, bias, Z, M, N, K, pro_mode, epi, none, nullptr, nullptr);
 }
 
@@ -477,6 +484,10 @@ int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, in
                     float* slab, int64_t slab_cap, float* dW, bool accumulate) {
   if ((N & 7) || (K & 7)) { set_error("pw_wgrad: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
   if (M > (int64_t)UINT32_MAX) { set_error("pw_wgrad: M exceeds 2^32 rows", __FILE__, __LINE__); return -1; }
+  if constexpr (sizeof(T) == 2) {
+    const int rc = launch_pw_wgrad_stream(s, dY, X, M, N, K, pro_mode, pro, slab, slab_cap, dW, accumulate);
+    if (rc <= 0) return rc;
+  }
   const int tnn = cdiv(N, WT), tnk = cdiv(K, WT);
   const int tiles = tnn * tnk;
   int64_t splits = std::max<int64_t>(1, 1024 / tiles);

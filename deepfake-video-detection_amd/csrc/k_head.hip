@@ -291,10 +291,20 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 }
 
 // out[0] = total norm, out[1] = clip coefficient min(1, max_norm/(norm+1e-6)) (1 if max_norm <= 0)
-__global__ void norm_finalize_kernel(const double* __restrict__ part, int nparts, float max_norm, float* out) {
+// (256 threads: strided partial sums, then a fixed-order tree; deterministic)
+__global__ __launch_bounds__(256) void norm_finalize_kernel(const double* __restrict__ part, int nparts, float max_norm,
+                                                            float* out) {
+  __shared__ double sh[256];
+  double v = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) v += part[i];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
   if (threadIdx.x != 0) return;
-  double a = 0.0;
-  for (int i = 0; i < nparts; ++i) a += part[i];
+  const double a = sh[0];
   const float nrm = (float)sqrt(a);
   out[0] = nrm;
   float c = 1.f;
@@ -425,7 +435,7 @@ int ce_backward(hipStream_t s, const float* z, const int64_t* y, const float* w,
 int grad_norm(hipStream_t s, const float* g, int64_t n, float max_norm, double* part, int nparts, float* out) {
   const int gx = std::max(1, std::min<int>(nparts, (int)nblk(n)));
   hipLaunchKernelGGL(sumsq_kernel, dim3(gx), dim3(256), 0, s, g, n, part);
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(64), 0, s, part, gx, max_norm, out);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, s, part, gx, max_norm, out);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

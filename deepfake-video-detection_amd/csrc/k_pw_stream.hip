@@ -50,9 +50,10 @@ struct StreamRegs {
   uint4 r[RESID ? NV : 1];
 };
 
-template <int NB, int KB, int U, int MODE, bool STATS, bool RESID>
+template <int NB, int KB, int U, int MODE, bool STATS, bool RESID, bool BIAS>
 __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                            bf16* __restrict__ C, const bf16* __restrict__ R,
+                                                           const float* __restrict__ bias,
                                                            int64_t M, int N, int K, Pro pro,
                                                            float* __restrict__ stats, int nchunks,
                                                            int64_t groups_per_part, int gate_frames) {
@@ -62,7 +63,8 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
   float* psc = reinterpret_cast<float*>(smem + NB * KB * 1024);  // [KP] producer BN scale
   float* psh = psc + KP;                                         // [KP] producer BN shift
   float* red = psh + KP;                                         // [4][2][NC] stat partials
-  float* gl = red + 8 * NC;                                      // [gate_frames][KP] SE gates
+  float* bl = red + 8 * NC;                                      // [NC] bias
+  float* gl = bl + NC;                                           // [gate_frames][KP] SE gates
   using TL = StreamTile<NB, U>;
   bf16* ct = reinterpret_cast<bf16*>(gl + gate_frames * KP) + (threadIdx.x >> 6) * (TL::SLAB / 2);  // wave's C slab
 
@@ -83,6 +85,9 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
       psc[k] = k < K ? pro.scale[k] : 0.f;
       psh[k] = k < K ? pro.shift[k] : 0.f;
     }
+  }
+  if constexpr (BIAS) {
+    for (int i = tid; i < NC; i += 256) bl[i] = n0 + i < N ? bias[n0 + i] : 0.f;
   }
   const int64_t G = (M + 15) >> 4;
   const int64_t gbeg = part * groups_per_part;
@@ -210,6 +215,10 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         const int n = n0 + nb * 16 + ln4;
+        if constexpr (BIAS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[u][nb][r] += bl[nb * 16 + ln4 + r];
+        }
         const uint2 pk = make_uint2(pack2bf(acc[u][nb][0], acc[u][nb][1]), pack2bf(acc[u][nb][2], acc[u][nb][3]));
         if constexpr (STATS) {
           const bool ok = rok && n < N;
@@ -278,15 +287,15 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
   }
 }
 
-template <int NB, int KB, int MODE, bool STATS, bool RESID>
-static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, int64_t M, int N, int K,
-                         const Pro& pro, float* stats, int* stat_rows) {
+template <int NB, int KB, int MODE, bool STATS, bool RESID, bool BIAS = false>
+static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias,
+                         int64_t M, int N, int K, const Pro& pro, float* stats, int* stat_rows) {
   constexpr int U = KB <= 2 ? 2 : 1;
   using TL = StreamTile<NB, U>;
-  auto kern = pw_stream_kernel<NB, KB, U, MODE, STATS, RESID>;
+  auto kern = pw_stream_kernel<NB, KB, U, MODE, STATS, RESID, BIAS>;
   const int nchunks = cdiv(N, NB * 16);
   const int64_t G = cdiv64(M, 16);
-  const size_t lds_fixed = (size_t)NB * KB * 1024 + 2 * (size_t)KB * 32 * 4 + 8 * (size_t)NB * 16 * 4 + 4 * TL::SLAB;
+  const size_t lds_fixed = (size_t)NB * KB * 1024 + 2 * (size_t)KB * 32 * 4 + 9 * (size_t)NB * 16 * 4 + 4 * TL::SLAB;
   // persistent grid: exactly the workgroups that are co-resident (one wave of dispatch, no
   // tail), measured once per instantiation at the LDS size without gate rows
   static const int resident = [&] {
@@ -306,8 +315,8 @@ static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, c
     if (gate_frames > 16) return 1;
   }
   const size_t lds = lds_fixed + (size_t)gate_frames * KB * 32 * 4;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(parts * nchunks)), dim3(256), lds, s, A, B, C, R, M, N, K, pro, stats,
-                     nchunks, gpp, gate_frames);
+  hipLaunchKernelGGL(kern, dim3((unsigned)(parts * nchunks)), dim3(256), lds, s, A, B, C, R, bias, M, N, K, pro,
+                     stats, nchunks, gpp, gate_frames);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)parts;
   return 0;
@@ -315,16 +324,36 @@ static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, c
 
 // 0: launched; 1: not covered (shape/mode without an instantiation, or M below the threshold;
 // the caller uses the tiled kernel); -1: launch error
-int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, int64_t M, int N, int K,
-                     int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
+int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
+                     int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
   if (M <= 0 || M < g_stream_min_rows.load(std::memory_order_relaxed) || K > 256 || (N & 7) || (K & 7)) return 1;
   const int nchunks = cdiv(N, 128);
   const int NB = cdiv(cdiv(N, nchunks), 16), KB = cdiv(K, 32);
-  const bool st = stats != nullptr, rs = R != nullptr;
+  const bool st = stats != nullptr, rs = R != nullptr, bs = bias != nullptr;
+  if (bs && (st || pro_mode != PRO_NONE)) return 1;
   const int key = NB * 16 + KB;
 #define DFD_STREAM_CASE(NB_, KB_, MODE_, ST_, RS_) \
   case NB_ * 16 + KB_:                             \
-    return stream_launch<NB_, KB_, MODE_, ST_, RS_>(s, A, B, C, R, M, N, K, pro, stats, stat_rows);
+    return stream_launch<NB_, KB_, MODE_, ST_, RS_>(s, A, B, C, R, bias, M, N, K, pro, stats, stat_rows);
+#define DFD_STREAM_BIAS(NB_, KB_, RS_) \
+  case NB_ * 16 + KB_:                 \
+    return stream_launch<NB_, KB_, PRO_NONE, false, RS_, true>(s, A, B, C, R, bias, M, N, K, pro, stats, stat_rows);
+  if (bs) {  // x . Q + bv (+ skip gradient): the linear part of the conv_pw input gradient (bn_fold_pw)
+    if (rs) {
+      switch (key) {
+        DFD_STREAM_BIAS(2, 1, true)  // 24 -> 24
+        DFD_STREAM_BIAS(3, 2, true)  // 40 -> 40
+        default: return 1;
+      }
+    }
+    switch (key) {
+      DFD_STREAM_BIAS(1, 1, false)  // 16 -> 16
+      DFD_STREAM_BIAS(2, 1, false)  // 24 -> 24
+      DFD_STREAM_BIAS(3, 2, false)  // 40 -> 40
+      default: return 1;
+    }
+  }
+#undef DFD_STREAM_BIAS
   if (pro_mode == PRO_NONE && st && !rs) {  // conv_pw forward (expansion): N = mid, K = cin
     switch (key) {
       DFD_STREAM_CASE(6, 1, PRO_NONE, true, false)  // 16 -> 96
@@ -361,12 +390,249 @@ int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const
   }
   if (pro_mode == PRO_NONE && !st && rs) {  // conv_pw dgrad plus the block's skip gradient
     switch (key) {
+      DFD_STREAM_CASE(1, 3, PRO_NONE, false, true)  // 96 -> 16
       DFD_STREAM_CASE(2, 5, PRO_NONE, false, true)  // 144 -> 24
       DFD_STREAM_CASE(3, 8, PRO_NONE, false, true)  // 240 -> 40
       default: return 1;
     }
   }
 #undef DFD_STREAM_CASE
+  return 1;
+}
+
+// ------------------------------------------------------------------------------------------
+// Streaming weight gradient for the same layers:  dW[N][K] = sum_m dY[m][n] * pro(X)[m][k].
+//
+// A workgroup owns one (N-chunk x K-chunk) of dW (<= 16 MFMA blocks of 16x16) for a slice of the
+// rows; its 4 waves sweep disjoint 32*S-row steps of that slice, each through a wave-private
+// LDS slab (no workgroup barrier inside the loop): the rows are staged with 16-B loads in their
+// natural row-major layout (X through the producer's BN+SiLU(+gate) prologue), then read back as
+// COLUMNS with ds_read_b64_tr_b16 to form the MFMA operands (the contraction runs over rows).
+// The next step's global loads are in flight during the current step's MFMAs.  The four waves'
+// accumulators are added in a fixed order and written to the part's slab row; the slabs are
+// summed in order afterwards (deterministic).
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+
+template <int NBW, int KBW, int S>
+struct WgsTile {
+  static constexpr int NW = NBW * 16, KW = KBW * 16, R = 32 * S;
+  static constexpr int YS = NW + 8, XS = KW + 8;  // LDS row strides (elements)
+  static constexpr int VY = NW / 8, VX = KW / 8;  // 16-B vectors per row
+  static constexpr int NVY = R * VY / 64, NVX = R * VX / 64;
+  static constexpr int WAVE_BYTES = R * (YS + XS) * 2;
+  static_assert((R * VY) % 64 == 0 && (R * VX) % 64 == 0, "step must be whole wave loads");
+};
+
+template <int NBW, int KBW, int S, int MODE>
+__global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __restrict__ dY,
+                                                                 const bf16* __restrict__ X, int64_t M, int N,
+                                                                 int K, Pro pro, float* __restrict__ slab,
+                                                                 int nch_n, int nch_k, int64_t rows_per_part,
+                                                                 int gate_frames) {
+  using TL = WgsTile<NBW, KBW, S>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* psc = reinterpret_cast<float*>(smem);  // [KW]
+  float* psh = psc + TL::KW;                     // [KW]
+  float* gl = psh + TL::KW;                      // [gate_frames][KW]
+  char* wave_base = reinterpret_cast<char*>(gl + gate_frames * TL::KW);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int chunk = (int)(blockIdx.x % (unsigned)(nch_n * nch_k));
+  const int64_t part = blockIdx.x / (unsigned)(nch_n * nch_k);
+  const int cn = chunk / nch_k, ck = chunk - cn * nch_k;
+  const int n0 = cn * TL::NW, k0 = ck * TL::KW;
+  const int64_t mbeg = part * rows_per_part, mend = min(M, mbeg + rows_per_part);
+  bf16* Ys = reinterpret_cast<bf16*>(wave_base + wave * TL::WAVE_BYTES);
+  bf16* Xs = Ys + TL::R * TL::YS;
+
+  int f_first = 0;
+  if constexpr (pro_is_bn(MODE)) {
+    for (int i = tid; i < TL::KW; i += 256) {
+      const bool ok = k0 + i < K;
+      psc[i] = ok ? pro.scale[k0 + i] : 0.f;
+      psh[i] = ok ? pro.shift[k0 + i] : 0.f;
+    }
+    if constexpr (MODE == PRO_BN_SILU_G) {
+      if (mbeg < mend) {
+        f_first = (int)(mbeg / pro.rows_per_frame);
+        const int nfr = min(gate_frames, (int)((mend - 1) / pro.rows_per_frame) - f_first + 1);
+        for (int i = tid; i < nfr * TL::KW; i += 256) {
+          const int fr = i / TL::KW, k = i - fr * TL::KW;
+          gl[i] = k0 + k < K ? pro.gate[(int64_t)(f_first + fr) * pro.C + k0 + k] : 0.f;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  Raw8<bf16> ry[TL::NVY], rx[TL::NVX];
+  auto load = [&](int64_t ms) {
+#pragma unroll
+    for (int i = 0; i < TL::NVY; ++i) {
+      const int v = lane + 64 * i, rr = v / TL::VY, cv = (v - rr * TL::VY) * 8;
+      const int64_t row = ms + rr;
+      raw_ld(ry[i], dY + row * N + n0 + cv, dY, row < mend && n0 + cv < N);
+    }
+#pragma unroll
+    for (int i = 0; i < TL::NVX; ++i) {
+      const int v = lane + 64 * i, rr = v / TL::VX, cv = (v - rr * TL::VX) * 8;
+      const int64_t row = ms + rr;
+      raw_ld(rx[i], X + row * K + k0 + cv, X, row < mend && k0 + cv < K);
+    }
+  };
+
+  f32x4_t acc[NBW][KBW];
+#pragma unroll
+  for (int a = 0; a < NBW; ++a)
+#pragma unroll
+    for (int b = 0; b < KBW; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int64_t wstep = 4 * TL::R;
+  int64_t ms = mbeg + wave * TL::R;
+  if (ms < mend) load(ms);
+  for (; ms < mend; ms += wstep) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < TL::NVY; ++i) {
+      const int v = lane + 64 * i, rr = v / TL::VY, cv = (v - rr * TL::VY) * 8;
+      raw_st(Ys + rr * TL::YS + cv, ry[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < TL::NVX; ++i) {
+      const int v = lane + 64 * i, rr = v / TL::VX, cv = (v - rr * TL::VX) * 8;
+      if constexpr (MODE == PRO_NONE) {
+        raw_st(Xs + rr * TL::XS + cv, rx[i]);
+      } else {
+        float x[8], sc[8], sh[8];
+        raw_to_f(rx[i], x);
+        ld8(psc + cv, sc);
+        ld8(psh + cv, sh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]);
+        if constexpr (MODE == PRO_BN_SILU_G) {
+          const int64_t row = ms + rr;
+          const int fr = row < mend ? (int)((uint32_t)row / (uint32_t)pro.rows_per_frame) - f_first : 0;
+          float gv[8];
+          ld8(gl + fr * TL::KW + cv, gv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] *= gv[j];
+        }
+        const uint32_t m = rx[i].ok ? 0xffffffffu : 0u;
+        *reinterpret_cast<uint4*>(Xs + rr * TL::XS + cv) =
+            make_uint4(pack2bf(x[0], x[1]) & m, pack2bf(x[2], x[3]) & m, pack2bf(x[4], x[5]) & m,
+                       pack2bf(x[6], x[7]) & m);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (ms + wstep < mend) load(ms + wstep);
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int sub = 0; sub < S; ++sub) {
+      const bf16* Yb = Ys + sub * 32 * TL::YS;
+      const bf16* Xb = Xs + sub * 32 * TL::XS;
+      bf16x8_t bfr[KBW];
+#pragma unroll
+      for (int kb = 0; kb < KBW; ++kb) {
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Xb + (8 * g + q) * TL::XS + kb * 16 + 4 * p));
+        const s16x4_t hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Xb + (8 * g + 4 + q) * TL::XS + kb * 16 + 4 * p));
+        bfr[kb] = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) {
+        const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Yb + (8 * g + q) * TL::YS + nb * 16 + 4 * p));
+        const s16x4_t hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Yb + (8 * g + 4 + q) * TL::YS + nb * 16 + 4 * p));
+        const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int kb = 0; kb < KBW; ++kb) acc[nb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kb], acc[nb][kb], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- the 4 waves' tiles added in a fixed order, then this part's slab row ----
+  float* red = reinterpret_cast<float*>(wave_base);  // [NW][KW], reuses the wave slabs
+  static_assert(TL::NW * TL::KW * 4 <= 4 * TL::WAVE_BYTES, "reduction tile exceeds the wave slabs");
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wave == w) {
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+        for (int kb = 0; kb < KBW; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int idx = (nb * 16 + 4 * (lane >> 4) + r) * TL::KW + kb * 16 + (lane & 15);
+            red[idx] = (w == 0 ? 0.f : red[idx]) + acc[nb][kb][r];
+          }
+    }
+  }
+  __syncthreads();
+  float* out = slab + part * (int64_t)N * K;
+  for (int i = tid; i < TL::NW * TL::KW; i += 256) {
+    const int nn = i / TL::KW, kk = i - nn * TL::KW;
+    if (n0 + nn < N && k0 + kk < K) out[(int64_t)(n0 + nn) * K + k0 + kk] = red[i];
+  }
+}
+
+template <int NBW, int KBW, int S, int MODE>
+static int wgs_launch(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, const Pro& pro,
+                      float* slab, int64_t slab_cap, float* dW, bool accumulate) {
+  using TL = WgsTile<NBW, KBW, S>;
+  auto kern = pw_wgrad_stream_kernel<NBW, KBW, S, MODE>;
+  const int nch_n = cdiv(N, TL::NW), nch_k = cdiv(K, TL::KW), chunks = nch_n * nch_k;
+  const size_t lds_fixed = 2 * (size_t)TL::KW * 4 + 4 * (size_t)TL::WAVE_BYTES;
+  static const int resident = [&] {
+    int dev = 0, cus = 256, per_cu = 2;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds_fixed) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    return std::max(1, cus * per_cu);
+  }();
+  const int64_t unit = 4 * TL::R;  // one sweep of the 4 waves
+  int64_t parts = std::max<int64_t>(1, std::min<int64_t>(std::max(1, resident / chunks), cdiv64(M, unit)));
+  parts = std::min<int64_t>(parts, std::max<int64_t>(1, slab_cap / ((int64_t)N * K)));
+  const int64_t rpp = cdiv64(cdiv64(M, parts), unit) * unit;
+  parts = cdiv64(M, rpp);
+  int gate_frames = 0;
+  if (MODE == PRO_BN_SILU_G) {
+    gate_frames = (int)std::min<int64_t>(cdiv64(M, pro.rows_per_frame), cdiv64(rpp, pro.rows_per_frame) + 1);
+    if (gate_frames > 16) return 1;
+  }
+  const size_t lds = lds_fixed + (size_t)gate_frames * TL::KW * 4;
+  hipLaunchKernelGGL(kern, dim3((unsigned)(parts * chunks)), dim3(256), lds, s, dY, X, M, N, K, pro, slab, nch_n,
+                     nch_k, rpp, gate_frames);
+  DFD_HIP_CHECK(hipGetLastError());
+  return launch_reduce_slabs(s, slab, (int)parts, (int64_t)N * K, dW, accumulate);
+}
+
+// 0: launched; 1: not covered (the caller uses the tiled wgrad kernel); -1: launch error
+int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
+                           const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate) {
+  if (M <= 0 || M < g_stream_min_rows.load(std::memory_order_relaxed) || (N & 7) || (K & 7)) return 1;
+#define DFD_WGS(NBW_, KBW_, S_, MODE_) \
+  return wgs_launch<NBW_, KBW_, S_, MODE_>(s, dY, X, M, N, K, pro, slab, slab_cap, dW, accumulate)
+  if (pro_mode == PRO_NONE) {  // conv_pw (expansion): N = mid, K = cin;  Gram x^T x: N = K = cin
+    if (N == 96 && K == 16) DFD_WGS(6, 1, 2, PRO_NONE);
+    if (N == 16 && K == 16) DFD_WGS(1, 1, 4, PRO_NONE);
+    if (N == 24 && K == 24) DFD_WGS(2, 2, 2, PRO_NONE);
+    if (N == 40 && K == 40) DFD_WGS(3, 3, 2, PRO_NONE);
+    if (N == 144 && K == 24) DFD_WGS(5, 2, 2, PRO_NONE);   // N in 2 chunks of 80
+    if (N == 240 && K == 40) DFD_WGS(5, 3, 1, PRO_NONE);   // N in 3 chunks of 80
+    return 1;
+  }
+  if (pro_mode == PRO_BN_SILU_G) {  // conv_pwl: N = cout, K = mid
+    if (N == 16 && K == 32) DFD_WGS(1, 2, 4, PRO_BN_SILU_G);
+    if (N == 24 && K == 96) DFD_WGS(2, 6, 1, PRO_BN_SILU_G);
+    if (N == 24 && K == 144) DFD_WGS(2, 5, 1, PRO_BN_SILU_G);  // K in 2 chunks of 80
+    if (N == 40 && (K == 144 || K == 240)) DFD_WGS(3, 5, 1, PRO_BN_SILU_G);
+    return 1;
+  }
+#undef DFD_WGS
   return 1;
 }
 

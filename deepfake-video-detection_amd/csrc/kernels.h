@@ -16,8 +16,10 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
                    int pro_mode, const Pro& pro, float* stats, int* stat_rows);
 // Streaming variant for tall-skinny bf16 layers (k_pw_stream.hip): 0 launched, 1 not covered
 // (shape/mode without an instantiation, or M below the streaming threshold), -1 error.
-int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, int64_t M, int N, int K,
-                     int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
+                     int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
+                           const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
 // rows threshold of the streaming kernels (returns the previous value)
 int64_t set_stream_min_rows(int64_t v);
 // Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
@@ -99,6 +101,23 @@ int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro,
 int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
                      const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
                      float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
+// SE + BN(+SiLU) backward sums in one pass over (dZ, Y): dgate[f][c] (SE branch) and the per-frame
+// sums pf[4][frames][C] that bn_bwd_finalize_frames combines with the gate and bc (k_bn.hip)
+template <typename T>
+int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
+                            const float* mean, const float* invstd, int frames, int HW, int C, float* part,
+                            int64_t part_cap, float* dgate, float* pf);
+int launch_bn_bwd_finalize_frames(hipStream_t s, const float* pf, const float* gate, const float* bc, int frames,
+                                  int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
+                                  bool training, float* dgamma, float* dbeta, bool accumulate, float* coef);
+// conv_pw backward through its BN (no activation), by linearity (k_bn.hip): fold the BN-backward
+// coefficients coef = [k1; k2; k3] into the dgrad operands, combine the weight-gradient terms
+template <typename T>
+int launch_bn_fold_pw(hipStream_t s, const float* W, const float* coef, int mid, int cin, T* w1t, T* q, float* bv);
+int launch_pw_wgrad_bn_combine(hipStream_t s, const float* Tg, const float* G, const float* cs, const float* W,
+                               const float* coef, int mid, int cin, float* dW, bool accumulate);
+template <typename T>
+int launch_col_sums(hipStream_t s, const T* X, int64_t M, int C, float* part, int64_t part_cap, float* out);
 // head global average pool: feat[f][c] = mean_hw silu(Y*scale+shift)
 template <typename T>
 int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat);

@@ -8,6 +8,7 @@
 #include "plan.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 
 namespace dfd {
@@ -186,13 +187,14 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   // scratch
   p.stats_cap = (int64_t)2048 * 2 * kHead;
   p.slab_cap = (int64_t)8 << 20;
-  p.part_cap = std::max<int64_t>((int64_t)4 << 20, F * kHead);
+  p.part_cap = std::max<int64_t>((int64_t)4 << 20, 5 * F * std::max<int64_t>(kHead, maxSE));
   p.o_stats = alloc(p.stats_cap * 4);
   p.o_slab = alloc(p.slab_cap * 4);
   p.o_part = alloc(p.part_cap * 4);
   p.o_coef = alloc(3 * kHead * 4);
   p.o_dgate = alloc(F * maxSE * 4);
   p.o_bc = alloc(F * maxSE * 4);
+  p.o_pf = alloc(4 * F * maxSE * 4);  // per-frame SE/BN backward sums
   p.o_de = alloc(F * maxSE * 4);
   p.o_dz = alloc(F * maxRD * 2 * 4);  // dz and r = silu(rpre)
   p.o_gx[0] = alloc(maxX * es);
@@ -200,6 +202,15 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.o_gs = alloc(maxS * es);
   p.o_ge1 = alloc(maxE1 * es);
   p.o_ge2 = alloc(maxE2 * es);
+  int64_t maxPW = 0, maxCin = 0;
+  for (const Block& b : p.blocks)
+    if (!b.ds) { maxPW = std::max<int64_t>(maxPW, (int64_t)b.mid * b.cin); maxCin = std::max<int64_t>(maxCin, b.cin); }
+  p.o_w1t = alloc(maxPW * es);
+  p.o_q = alloc(maxCin * maxCin * es);
+  p.o_bv = alloc(maxCin * 4);
+  p.o_tg = alloc(maxPW * 4);
+  p.o_gram = alloc(maxCin * maxCin * 4);
+  p.o_cs = alloc(maxCin * 4);
   p.ws_bytes = cur;
   p.offs.assign(p.tensors.size(), -1);
   p.bound = false;
@@ -346,6 +357,11 @@ int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, cons
   return 0;
 }
 
+// blocks with at least this many conv_pw rows take the BN-folded backward (bn_fold_pw); below it
+// the extra small passes over x cost more than the expanded-tensor passes they save
+// (dfd_set_tuning("fold_min_rows", v); tests force both paths)
+std::atomic<int64_t> g_fold_min_rows{100000};
+
 template <typename T>
 int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat, const float* P,
                   char* ws, float* G, int tr, int seg_begin, int seg_end, int acc) {
@@ -400,18 +416,24 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         PROBED(PK_PWL_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(b.o_y2), Mout, b.cout, b.mid, PRO_BN_SILU_G,
                                                      r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), r.f(p.o_slab), p.slab_cap,
                                                      grad(b.pwl.t_w), acc != 0)));
-        // squeeze-excite
-        DFD_TRY(launch_se_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
-                                        r.f(p.o_part), p.part_cap, r.f(p.o_dgate)));
+        // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE
+        // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
+        DFD_TRY(launch_se_bn_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
+                                           r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), p.frames, hwo, b.mid,
+                                           r.f(p.o_part), p.part_cap, r.f(p.o_dgate), r.f(p.o_pf)));
         DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_dgate), r.f(b.o_gate), r.f(b.o_sq), r.f(b.o_rpre), r.prm(b.t_se_wr),
                                  r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo, r.f(p.o_de), r.f(p.o_dz),
                                  r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we), grad(b.t_se_be),
                                  acc != 0));
-        // BN+SiLU after the depthwise conv (input grad = gated path + squeeze path)
+        DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_pf), r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid, Mout,
+                                              r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), tr != 0,
+                                              grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
         BnBwdIn i2{};
         i2.dZ = r.a(p.o_ge2); i2.gate = r.f(b.o_gate); i2.bc = r.f(p.o_bc); i2.bc_scale = 1.f;
         i2.rows_per_frame = hwo; i2.silu = true;
-        DFD_TRY(bwd_bn(i2, bn_dw, r.a(b.o_y2), Mout, r.a(p.o_ge2)));
+        i2.mean = r.f(bn_dw.o_mean); i2.invstd = r.f(bn_dw.o_invstd);
+        i2.scale = r.f(bn_dw.o_scale); i2.shift = r.f(bn_dw.o_shift);
+        DFD_TRY(launch_bn_bwd_apply<T>(s, i2, r.a(b.o_y2), r.f(p.o_coef), r.a(p.o_ge2), Mout, b.mid));
         // depthwise conv
         // depthwise dgrad fused with the backward reduction of the producer's BN+SiLU
         // (stem BN for the stage-0 block, bn1 otherwise): ge1 = g, stats = partials of g, g*xhat
@@ -425,7 +447,7 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         p.pending_rows = rows;
         PROBED(PK_DW_WGRAD, &b, (launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), y_in, r.pro_bn(bn_in, b.hin * b.win),
                                                     PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0)));
-        if (!b.ds) {
+        if (!b.ds && Min < g_fold_min_rows.load(std::memory_order_relaxed)) {
           BnBwdIn i1{};
           i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = false;
           DFD_TRY(bwd_bn_from_stats(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1), p.pending_rows));
@@ -435,6 +457,29 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
                                                      nullptr, nullptr)));
           PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
                                                       r.f(p.o_slab), p.slab_cap, grad(b.pw.t_w), acc != 0)));
+        } else if (!b.ds) {
+          // conv_pw + its BN (no activation): ge1 = k1*g + k2*y1 + k3 is never materialised; by
+          // linearity (y1 = x . W^T) the gradients need only g (in ge1) and the block input x:
+          //   dX = g . diag(k1)W + x . W^T diag(k2) W + W^T k3 (+ skip);  dW = diag(k1) g^T x +
+          //   diag(k2) W x^T x + k3 1^T x   (bn_fold_pw, k_bn.hip)
+          const T* xin = r.a(p.blocks[i - 1].o_x);
+          T* gxo = r.a(p.o_gx[(i - 1) & 1]);
+          DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), p.pending_rows, Min, b.mid, r.prm(b.bn1.t_w),
+                                         r.f(b.bn1.o_mean), r.f(b.bn1.o_invstd), tr != 0, grad(b.bn1.t_w),
+                                         grad(b.bn1.t_b), acc != 0, r.f(p.o_coef)));
+          DFD_TRY(launch_bn_fold_pw<T>(s, r.prm(b.pw.t_w), r.f(p.o_coef), b.mid, b.cin, r.a(p.o_w1t), r.a(p.o_q),
+                                       r.f(p.o_bv)));
+          DFD_TRY(launch_tf_gemm<T>(s, xin, r.a(p.o_q), r.a(p.o_gs), b.skip ? gout : nullptr, r.f(p.o_bv), nullptr,
+                                    Min, b.cin, b.cin, PRO_NONE, EPI_BIAS | (b.skip ? EPI_RESID : 0)));
+          PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(p.o_w1t), gxo, r.a(p.o_gs), Min, b.cin,
+                                                     b.mid, PRO_NONE, Pro{}, nullptr, nullptr)));
+          PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
+                                                      r.f(p.o_slab), p.slab_cap, r.f(p.o_tg), false)));
+          DFD_TRY(launch_pw_wgrad<T>(s, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, r.f(p.o_slab), p.slab_cap,
+                                     r.f(p.o_gram), false));
+          DFD_TRY(launch_col_sums<T>(s, xin, Min, b.cin, r.f(p.o_stats), p.stats_cap, r.f(p.o_cs)));
+          DFD_TRY(launch_pw_wgrad_bn_combine(s, r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs), r.prm(b.pw.t_w),
+                                             r.f(p.o_coef), b.mid, b.cin, grad(b.pw.t_w), acc != 0));
         }
       }
     } else {
@@ -450,6 +495,8 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
 }
 
 }  // namespace
+
+int64_t set_fold_min_rows(int64_t v) { return g_fold_min_rows.exchange(v); }
 
 int plan_forward(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* params, float* bnbuf,
                  char* ws, float* feat, int training, float momentum) {

@@ -63,8 +63,9 @@ struct Plan {
   std::vector<Block> blocks;
   // workspace
   int64_t ws_bytes = 0;
-  int64_t o_ystem, o_yh, o_stats, o_slab, o_part, o_coef, o_dgate, o_bc, o_de, o_dz;
+  int64_t o_ystem, o_yh, o_stats, o_slab, o_part, o_coef, o_dgate, o_bc, o_de, o_dz, o_pf;
   int64_t o_gx[2], o_gs, o_ge1, o_ge2;
+  int64_t o_w1t, o_q, o_bv, o_tg, o_gram, o_cs;  // conv_pw backward through its BN (bn_fold_pw)
   int64_t stats_cap, slab_cap, part_cap;
   // cast table (device copy)
   std::vector<CastSeg> cast_host;
@@ -91,6 +92,8 @@ int plan_backward_x(Plan& p, hipStream_t s, const float* x, const int64_t* xs, c
 // gradients are final once the segment has run.
 void plan_segment_range(const Plan& p, int seg, int* lo, int* hi);
 constexpr int kNumSegments = 9;
+// rows threshold of the BN-folded conv_pw backward (returns the previous value)
+int64_t set_fold_min_rows(int64_t v);
 // static topology (shape-independent)
 const std::vector<TensorSpec>& b0_tensor_table();
 

@@ -19,6 +19,24 @@ from deepfake_amd.weights import deterministic_init_
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["default", "forced"])
+def kernel_paths(request):
+    """Run a test with the production kernel selection ("default": the streaming 1x1 kernels and the
+    BN-folded conv_pw backward only on >= 100K-row layers) and with both forced onto every covered
+    layer ("forced"), so the small parity shapes exercise the high-resolution code paths too."""
+    from deepfake_amd import _lib
+    lib = _lib.load()
+    if request.param == "default":
+        yield request.param
+        return
+    prev = [lib.dfd_set_tuning(k, 0) for k in (b"stream_min_rows", b"fold_min_rows")]
+    try:
+        yield request.param
+    finally:
+        for k, v in zip((b"stream_min_rows", b"fold_min_rows"), prev):
+            lib.dfd_set_tuning(k, v)
+
+
 def _det(seed, dtype="fp32", dropout=0.5, cuda=None):
     torch.manual_seed(0)
     det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=dropout,
@@ -86,7 +104,7 @@ def _check_grads(det, g, rtol_norm=1e-3, atol_head=1e-5, rtol_head=1e-3):
     return bad
 
 
-def test_detector_train_golden_fp32(cuda, golden_dir):
+def test_detector_train_golden_fp32(cuda, golden_dir, kernel_paths):
     g = np.load(os.path.join(golden_dir, "b0_train_64.npz"))
     det = _det(int(g["seed"]), "fp32", dropout=0.0, cuda=cuda).train()
     x = torch.from_numpy(g["x"]).to(cuda)
@@ -107,7 +125,7 @@ def test_detector_train_golden_fp32(cuda, golden_dir):
         assert abs(float(t.norm()) - float(g["bn_norm"][i])) <= 1e-4 * float(g["bn_norm"][i]) + 1e-6, n
 
 
-def test_detector_train_bf16_close(cuda, golden_dir):
+def test_detector_train_bf16_close(cuda, golden_dir, kernel_paths):
     """bf16 activations / fp32 accumulation vs the fp32 reference: loss within 2e-2 relative,
     gradient direction (cosine) > 0.98 for every large tensor."""
     g = np.load(os.path.join(golden_dir, "b0_train_64.npz"))
@@ -129,7 +147,7 @@ def test_detector_train_bf16_close(cuda, golden_dir):
     assert norms_ok >= 0.9 * len(names), (norms_ok, len(names))
 
 
-def test_detector_train_bf16_deterministic(cuda, golden_dir):
+def test_detector_train_bf16_deterministic(cuda, golden_dir, kernel_paths):
     """Two identical bf16 training steps give bit-identical logits, gradients and BN running
     statistics: every reduction (BN statistics, weight gradients, SE squeezes) is fixed-order."""
     g = np.load(os.path.join(golden_dir, "b0_train_64.npz"))

@@ -121,3 +121,52 @@ def test_pw_conv_rejects_bad_args(cuda):
     assert b"dtype" in lib.dfd_last_error()
     assert lib.dfd_pw_conv(None, 1, None, None, None, None, 16, 8, 8, 2, None, None, None, 0, None,
                            ctypes.byref(rows)) == -1
+
+
+def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate=False):
+    """dW[N][K] = sum_m dY[m][n] * pro(X)[m][k] (conv_pw / conv_pwl weight gradient)."""
+    lib = _lib_()
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    dy = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16)
+    x, _, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed + 1, dev)
+    dw = torch.randn(N, K, device=dev) if accumulate else torch.empty(N, K, device=dev)
+    dw0 = dw.clone()
+    slab = torch.empty(8 << 20, device=dev)
+    prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
+    try:
+        _lib.check(lib.dfd_pw_conv_wgrad(_lib.stream_of(dev), 1, dy.data_ptr(), x.data_ptr(), M, N, K, mode,
+                                         scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf, slab.data_ptr(),
+                                         slab.numel(), dw.data_ptr(), 1 if accumulate else 0))
+        torch.cuda.synchronize()
+    finally:
+        lib.dfd_set_tuning(b"stream_min_rows", prev)
+    xp = _pro(x, mode, scale, shift, gate, rpf).to(torch.bfloat16).double()
+    ref = dy.double().t() @ xp
+    if accumulate:
+        ref = ref + dw0.double()
+    torch.testing.assert_close(dw.double(), ref, rtol=1e-4, atol=1e-4 * float(ref.abs().max()))
+
+
+WGRAD_CASES = [
+    (100355, 96, 16, 0),    # blocks.1.0 conv_pw
+    (50021, 144, 24, 0),    # blocks.1.1 / 2.0 conv_pw
+    (20007, 240, 40, 0),    # blocks.2.1 / 3.0 conv_pw
+    (100355, 16, 32, 2),    # blocks.0.0 conv_pw (gated)
+    (50021, 24, 96, 2),     # blocks.1.0 conv_pwl
+    (50021, 24, 144, 2),    # blocks.1.1 conv_pwl
+    (20007, 40, 144, 2),    # blocks.2.0 conv_pwl
+    (20007, 40, 240, 2),    # blocks.2.1 conv_pwl
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_CASES, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("path", ["stream", "tiled"])
+def test_pw_conv_wgrad_bf16(cuda, case, path):
+    M, N, K, mode = case
+    _run_wgrad(M, N, K, mode, 0 if path == "stream" else 1 << 60, cuda, rpf=784 if M < 30000 else 3136)
+
+
+def test_pw_conv_wgrad_accumulate(cuda):
+    _run_wgrad(50021, 24, 96, 2, 0, cuda, accumulate=True)
+    _run_wgrad(12544, 192, 1152, 2, 0, cuda, rpf=49, accumulate=True)

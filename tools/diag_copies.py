@@ -1,0 +1,27 @@
+"""Which host-side ops enqueue device copies in a bench train step (development diagnostic)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+import bench
+from deepfake_amd.pretrained_detector import PretrainedBackboneDetector
+from deepfake_amd.trainer import DataParallelTrainer
+from deepfake_amd.weights import deterministic_init_
+from deepfake_amd.optim import _flat_view
+
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+m = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, dropout_rate=0.5, compute_dtype="bf16")
+deterministic_init_(m, seed=0)
+m = m.to(dev).train()
+step = DataParallelTrainer(m, lr=1e-4, weight_decay=1e-5, max_grad_norm=1.0, class_weights=torch.tensor([1.0, 1.0]))
+x, y = bench.synthetic_batch(0, dev)
+for _ in range(2):
+    step(x, y)
+torch.cuda.synchronize()
+gs = [p.grad for p in m.parameters()]
+print("flat view of grads:", _flat_view(gs) is not None, "n params", len(gs))
+from torch.profiler import profile, ProfilerActivity
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    step(x, y)
+    torch.cuda.synchronize()
+print(prof.key_averages().table(sort_by="count", row_limit=25))
