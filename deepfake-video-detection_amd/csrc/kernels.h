@@ -50,6 +50,14 @@ int launch_dw_dgrad(hipStream_t s, const DwGeom& g, const T* dY, const float* w,
 template <typename T>
 int launch_dw_wgrad(hipStream_t s, const DwGeom& g, const T* dY, const T* X, const Pro& pro,
                     int pro_mode, float* slab, int64_t slab_cap, float* dW, bool accumulate);
+// fused dgrad (+ producer BN+SiLU backward reduction) + wgrad, k_dw_bwd.hip: 0 launched, 1 not
+// covered (use the two kernels above), -1 error
+template <typename T>
+int launch_dw_bwd(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* out, const T* Yp,
+                  const BnBwdIn* bn, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
+                  bool accumulate);
+int64_t set_dw_bwd_fused(int64_t v);
+bool dw_bwd_fused_enabled();
 
 // ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------
 // finalize training stats: mean/invstd/scale/shift + running update (momentum); eval: from running

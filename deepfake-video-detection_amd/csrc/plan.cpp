@@ -442,11 +442,19 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         BnBwdIn fz{};
         fz.mean = r.f(bn_in.o_mean); fz.invstd = r.f(bn_in.o_invstd);
         fz.scale = r.f(bn_in.o_scale); fz.shift = r.f(bn_in.o_shift); fz.silu = true;
-        PROBED(PK_DW_DGRAD, &b, (launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in, &fz,
-                                                    r.f(p.o_stats), &rows)));
+        int fused = 1;
+        PROBED(PK_DW_DGRAD, &b, ((fused = launch_dw_bwd<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in,
+                                                           &fz, r.f(p.o_stats), &rows, r.f(p.o_slab), p.slab_cap,
+                                                           grad(b.t_dw), acc != 0)) < 0 ? -1 : 0));
+        if (fused == 1) {
+          PROBED(PK_DW_DGRAD, &b, (launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in, &fz,
+                                                      r.f(p.o_stats), &rows)));
+          p.pending_rows = rows;
+          PROBED(PK_DW_WGRAD, &b, (launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), y_in, r.pro_bn(bn_in, b.hin * b.win),
+                                                      PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw),
+                                                      acc != 0)));
+        }
         p.pending_rows = rows;
-        PROBED(PK_DW_WGRAD, &b, (launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), y_in, r.pro_bn(bn_in, b.hin * b.win),
-                                                    PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw), acc != 0)));
         if (!b.ds && Min < g_fold_min_rows.load(std::memory_order_relaxed)) {
           BnBwdIn i1{};
           i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = false;

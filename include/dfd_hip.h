@@ -127,7 +127,9 @@ DFD_API int dfd_adam_step(void* stream, float* params, float* grads, float* exp_
  * "stream_min_rows": bf16 1x1 convs with at least this many rows use the streaming kernel
  * (default 100000; 0 routes every covered shape there, a huge value routes none).
  * "fold_min_rows": IR blocks whose conv_pw has at least this many rows run its backward through
- * the BN-folded form (no materialised BN input gradient; default 100000). */
+ * the BN-folded form (no materialised BN input gradient; default 100000).
+ * "dw_bwd_fused": 1 (default) runs the depthwise input and weight gradients as one fused pass,
+ * 0 as two kernels. */
 DFD_API int64_t dfd_set_tuning(const char* key, int64_t value);
 
 /* ---- pointwise (1x1) convolution, the trunk's conv_pw / conv_pwl / conv_head kernels ----------
