@@ -767,11 +767,10 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
 
 // ------------------------------------------------------------------ SE excitation (per frame)
 // SE excitation, forward:  rpre = Wr sq + br ; r = silu(rpre) ; gate = sigmoid(We r + be)
-// (timm SqueezeExcite conv_reduce / act / conv_expand / sigmoid).  Two kernels per direction,
-// templated on the reduce width RD (4..48 in B0) so every accumulator array is exact:
-//   se_rd_kernel   one workgroup per frame: each thread accumulates all RD products over its
-//                  channel subset (coalesced Wr rows), fixed-order block reduction;
-//   se_gate_kernel one thread per (frame, channel): RD-long dot product with an LDS copy of r.
+// (timm SqueezeExcite conv_reduce / act / conv_expand / sigmoid).  Per direction:
+//   reduce FC      frames x RD x C on the fp32 MFMA small GEMM (launch_mfma_small_gemm);
+//   se_gate_kernel one thread per (frame, channel): RD-long dot product with an LDS copy of r,
+//                  templated on the reduce width RD (4..48 in B0) so the accumulators are exact.
 template <int RD>
 __device__ __forceinline__ void block_sum_rd(float (&acc)[RD], float* red, float* out) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -783,23 +782,6 @@ __device__ __forceinline__ void block_sum_rd(float (&acc)[RD], float* red, float
   __syncthreads();
   if (tid < RD) out[tid] = red[tid] + red[RD + tid] + red[2 * RD + tid] + red[3 * RD + tid];
   __syncthreads();
-}
-
-// rpre[f][j] = br[j] + sum_c wr[j][c] sq[f][c]: one workgroup per frame, wave w owns the reduce
-// channels j = w, w+4, ...: a coalesced dot product over c per j (ascending c per lane, then a
-// fixed-order wave sum).
-template <int RD>
-__global__ __launch_bounds__(256) void se_rd_kernel(const float* __restrict__ sq, const float* __restrict__ wr,
-                                                    const float* __restrict__ br, int C, float* __restrict__ rpre) {
-  const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const float* x = sq + (int64_t)f * C;
-  for (int j = wave; j < RD; j += 4) {
-    const float* w = wr + (int64_t)j * C;
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a = fmaf(w[c], x[c], a);
-    a = wave_sum(a);
-    if (lane == 0) rpre[(int64_t)f * RD + j] = a + br[j];
-  }
 }
 
 template <int RD>
@@ -862,7 +844,8 @@ __global__ __launch_bounds__(256) void se_bc_kernel(const float* __restrict__ dz
 template <int RD>
 static void se_fwd_launch(hipStream_t s, dim3 g2, int frames, const float* sq, const float* wr, const float* br,
                           const float* we, const float* be, int C, float* rpre, float* gate) {
-  hipLaunchKernelGGL(se_rd_kernel<RD>, dim3(frames), dim3(256), 0, s, sq, wr, br, C, rpre);
+  // rpre[f][j] = br[j] + sum_c sq[f][c] wr[j][c]   (frames x rd x C on fp32 MFMA)
+  (void)launch_mfma_small_gemm(s, sq, C, 1, wr, 1, C, rpre, RD, frames, RD, C, br, nullptr, nullptr, false, 0, 0u, 0.f, 0);
   hipLaunchKernelGGL(se_gate_kernel<RD>, g2, dim3(256), 0, s, rpre, we, be, C, gate);
 }
 template <int RD>
@@ -893,59 +876,8 @@ int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const floa
   return 0;
 }
 
-// weight grads: gwe[c][j] = sum_f de[f][c] * r[f][j]; gbe[c] = sum_f de[f][c]   (r = silu(rpre))
-//               gwr[j][c] = sum_f dz[f][j] * sq[f][c]; gbr[j] = sum_f dz[f][j]
-// One thread per output element, channel fastest: the [f][c] operand is read coalesced and the
-// [f][j] operand is a wave-uniform broadcast; frames are summed in order (deterministic).
-__global__ __launch_bounds__(256) void se_wgrad_kernel(const float* __restrict__ de, const float* __restrict__ dz,
-                                                       const float* __restrict__ sq, const float* __restrict__ r,
-                                                       int frames, int C, int rd, float* gwr, float* gbr, float* gwe,
-                                                       float* gbe, int accumulate) {
-  const int64_t n_w = (int64_t)C * rd;
-  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const float* a;  // [f][C] operand (stride C)
-  const float* b;  // [f][rd] operand (stride rd), or nullptr for a bias
-  int64_t ai, bi = 0, stride_a, stride_b = rd;
-  float* out;
-  int64_t oi;
-  if (i < n_w) {                      // gwe
-    const int j = (int)(i / C), c = (int)(i - (int64_t)j * C);
-    a = de; ai = c; stride_a = C; b = r; bi = j; out = gwe; oi = (int64_t)c * rd + j;
-  } else if ((i -= n_w) < n_w) {      // gwr
-    const int j = (int)(i / C), c = (int)(i - (int64_t)j * C);
-    a = sq; ai = c; stride_a = C; b = dz; bi = j; out = gwr; oi = (int64_t)j * C + c;
-  } else if ((i -= n_w) < C) {        // gbe
-    a = de; ai = i; stride_a = C; b = nullptr; out = gbe; oi = i;
-  } else if ((i -= C) < rd) {         // gbr
-    a = dz; ai = i; stride_a = rd; b = nullptr; out = gbr; oi = i;
-  } else {
-    return;
-  }
-  float acc = 0.f;
-  if (b) {
-    int f = 0;
-    for (; f + 8 <= frames; f += 8) {
-      float va[8], vb[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) { va[u] = a[(f + u) * stride_a + ai]; vb[u] = b[(f + u) * stride_b + bi]; }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = fmaf(va[u], vb[u], acc);
-    }
-    for (; f < frames; ++f) acc = fmaf(a[f * stride_a + ai], b[f * stride_b + bi], acc);
-  } else {
-    int f = 0;
-    for (; f + 8 <= frames; f += 8) {
-      float va[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) va[u] = a[(f + u) * stride_a + ai];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += va[u];
-    }
-    for (; f < frames; ++f) acc += a[f * stride_a + ai];
-  }
-  out[oi] = accumulate ? out[oi] + acc : acc;
-}
-
+// weight grads (launch_se_fc_bwd): gwe[c][j] = sum_f de[f][c] r[f][j], gwr[j][c] = sum_f dz[f][j] sq[f][c]
+// (fp32 MFMA, frames ascending), gbe / gbr = column sums of de / dz.
 int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
                      const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
                      float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
@@ -954,10 +886,10 @@ int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const
   DFD_SE_RD_SWITCH(rd, se_bwd_launch<RD>(s, g2, frames, dgate, gate, rpre, wr, we, C, inv_hw, tmp_de, tmp_dr, tmp_r,
                                           bc_out));
   DFD_HIP_CHECK(hipGetLastError());
-  const int64_t n = 2 * (int64_t)C * rd + C + rd;
-  hipLaunchKernelGGL(se_wgrad_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, tmp_de, tmp_dr, sq, tmp_r,
-                     frames, C, rd, gwr, gbr, gwe, gbe, accumulate ? 1 : 0);
-  DFD_HIP_CHECK(hipGetLastError());
+  DFD_TRY(launch_mfma_small_gemm(s, tmp_de, 1, C, tmp_r, rd, 1, gwe, rd, C, rd, frames, nullptr, nullptr, gbe,
+                                 accumulate, 0, 0u, 0.f, 0));
+  DFD_TRY(launch_mfma_small_gemm(s, tmp_dr, 1, rd, sq, C, 1, gwr, C, rd, C, frames, nullptr, nullptr, gbr,
+                                 accumulate, 0, 0u, 0.f, 0));
   return 0;
 }
 

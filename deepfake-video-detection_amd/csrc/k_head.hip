@@ -125,6 +125,101 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ fp32 MFMA small GEMM
+// C[m][n] (+)= post( sum_k A(m,k) B(k,n) ), A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn],
+// on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation).  For the small, deep-K
+// products around the head and the squeeze-excite FCs (frames x channels x reduce width), where
+// per-output dot-product threads are latency-bound: one workgroup per 16x16 output tile, its
+// waves splitting K round-robin in 32-k chunks (operands of a chunk loaded before its MFMAs),
+// then a fixed-order LDS reduction over the waves (bit-reproducible).  Options: bias[n],
+// post-multiplication by silu'(pre[m][n]), counter-hash dropout on B (index k*drop_ld + n), and
+// asum[m] (+)= sum_k A(m,k) (the bias gradient of a weight-gradient product) from n-tile 0.
+struct MfmaGemm {
+  const float* A; int64_t sam, sak;
+  const float* B; int64_t sbk, sbn;
+  float* C; int64_t ldc;
+  int M, N, K;
+  const float* bias;
+  const float* dsilu_pre;  // [M][ldc] or null
+  float* asum;             // [M] or null
+  int accumulate;
+  uint64_t seed; uint32_t stream; float p; int64_t drop_ld;  // dropout on B if p > 0
+};
+
+typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
+constexpr int MG_MAXW = 16;
+
+__global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a) {
+  __shared__ float red[MG_MAXW][5][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int tn = (a.N + 15) / 16;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / tn) * 16, n0 = (tile % tn) * 16;
+  const int li = lane & 15, lk = lane >> 4;
+  const int m = m0 + li, n = n0 + li;
+  const bool mok = m < a.M, nok = n < a.N;
+  const bool drop = a.p > 0.f;
+  const bool want_asum = a.asum != nullptr && n0 == 0;
+  mf_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float as = 0.f;
+  constexpr int U = 8;  // MFMA steps per chunk (32 k)
+  for (int k0 = 32 * wave; k0 < a.K; k0 += 32 * nw) {
+    float av[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + 4 * u + lk;
+      const bool kok = k < a.K;
+      av[u] = (mok && kok) ? a.A[(int64_t)m * a.sam + (int64_t)k * a.sak] : 0.f;
+      float b = (nok && kok) ? a.B[(int64_t)k * a.sbk + (int64_t)n * a.sbn] : 0.f;
+      if (drop && nok && kok) b *= drop_mul(a.seed, a.stream, (int64_t)k * a.drop_ld + n, a.p);
+      bv[u] = b;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    if (want_asum) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) as += av[u];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wave][r][lane] = acc[r];
+  red[wave][4][lane] = as;
+  __syncthreads();
+  if (wave != 0) return;
+  // D layout: lane holds rows 4*(lane>>4) + r of column lane & 15
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = 0.f;
+    for (int w = 0; w < nw; ++w) v += red[w][r][lane];
+    const int mm = m0 + 4 * lk + r, nn = n0 + li;
+    if (mm >= a.M || nn >= a.N) continue;
+    if (a.bias) v += a.bias[nn];
+    if (a.dsilu_pre) v *= dsiluf_(a.dsilu_pre[(int64_t)mm * a.ldc + nn]);
+    float* c = a.C + (int64_t)mm * a.ldc + nn;
+    *c = a.accumulate ? *c + v : v;
+  }
+  if (want_asum && lane < 16 && mok) {
+    float v = 0.f;
+    for (int w = 0; w < nw; ++w) v += (red[w][4][lane] + red[w][4][lane + 16]) + (red[w][4][lane + 32] + red[w][4][lane + 48]);
+    a.asum[m] = a.accumulate ? a.asum[m] + v : v;
+  }
+}
+
+int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                           int64_t sbn, float* C, int64_t ldc, int M, int N, int K, const float* bias,
+                           const float* dsilu_pre, float* asum, bool accumulate, uint64_t seed, uint32_t stream,
+                           float p, int64_t drop_ld) {
+  if (M <= 0 || N <= 0) return 0;
+  const MfmaGemm g{A, sam, sak, B, sbk, sbn, C, ldc, M, N, K, bias, dsilu_pre, asum, accumulate ? 1 : 0,
+                   seed, stream, p, drop_ld};
+  const int tiles = cdiv(M, 16) * cdiv(N, 16);
+  // waves per tile: enough K-splitting to put ~2 chunks on each wave, at most MG_MAXW
+  const int nw = std::max(1, std::min(MG_MAXW, cdiv(K, 64)));
+  hipLaunchKernelGGL(mfma_small_gemm_kernel, dim3((unsigned)tiles), dim3(64 * nw), 0, s, g);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 // Y[r] = post( dot(X[r], w) + b ) for a single output (the 64->1 attention scorer)
 // ------------------------------------------------------------------ temporal attention (per clip)
 // e[bt] = sigmoid(w2 . hid[bt] + b2) ; a[b] = softmax_t(e[b]) ; g[b] = sum_t a[b][t] f[bt]
@@ -391,15 +486,16 @@ int head_forward(hipStream_t s, const HeadDims& d, const HeadParams& P, const fl
 int head_backward(hipStream_t s, const HeadDims& d, const HeadParams& P, const float* F, HeadWork& w, uint64_t seed,
                   float p, const float* scores, const float* dlogits, const float* dscores, float* dF, HeadParams& G) {
   // fc2: dW2 = dlogits^T . drop(h1) ; db2 ; dh1 = dlogits . W2 (then * drop2 * relu')
-  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.NC * d.F1)), dim3(256), 0, s, dlogits, w.h1,
-                     (float*)G.fc2_w, (float*)G.fc2_b, d.B, d.F1, d.NC, seed, 2u, p);
+  // dW[o][i] = sum_r dY[r][o] drop(X)[r][i] ;  db = column sums of dY
+  DFD_TRY(launch_mfma_small_gemm(s, dlogits, 1, d.NC, w.h1, d.F1, 1, (float*)G.fc2_w, d.F1, d.NC, d.F1, d.B, nullptr,
+                                 nullptr, (float*)G.fc2_b, false, seed, 2u, p, d.F1));
   hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)d.B * d.F1)), dim3(256), 0, s, dlogits, P.fc2_w, w.dh1,
                      d.B, d.F1, d.NC, 0, seed, 2u, p);
   hipLaunchKernelGGL(relu_drop_bwd_kernel, dim3(nblk((int64_t)d.B * d.F1)), dim3(256), 0, s, w.dh1, w.h1,
                      (int64_t)d.B * d.F1, seed, 0u, 0.f);
   // fc1: dW1 = dh1^T . drop(g) ; db1 ; dg = dh1 . W1 * drop1
-  hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.F1 * d.D)), dim3(256), 0, s, w.dh1, w.g,
-                     (float*)G.fc1_w, (float*)G.fc1_b, d.B, d.D, d.F1, seed, 1u, p);
+  DFD_TRY(launch_mfma_small_gemm(s, w.dh1, 1, d.F1, w.g, d.D, 1, (float*)G.fc1_w, d.D, d.F1, d.D, d.B, nullptr,
+                                 nullptr, (float*)G.fc1_b, false, seed, 1u, p, d.D));
   hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)d.B * d.D)), dim3(256), 0, s, w.dh1, P.fc1_w, w.dg, d.B,
                      d.D, d.F1, 0, seed, 1u, p);
   // attention pooling
@@ -407,10 +503,10 @@ int head_backward(hipStream_t s, const HeadDims& d, const HeadParams& P, const f
                      scores, w.dg, dscores, d.T, d.D, d.H, d.use_attn, dF, w.dpe, w.dhid);
   if (d.use_attn) {
     const int R = d.B * d.T;
-    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.H)), dim3(256), 0, s, w.dpe, w.hid,
-                       (float*)G.ta_w2, (float*)G.ta_b2, R, d.H, 1, seed, 0u, 0.f);
-    hipLaunchKernelGGL(linear_wgrad_kernel, dim3(nblk((int64_t)d.H * d.D)), dim3(256), 0, s, w.dhid, F,
-                       (float*)G.ta_w1, (float*)G.ta_b1, R, d.D, d.H, seed, 0u, 0.f);
+    DFD_TRY(launch_mfma_small_gemm(s, w.dpe, 1, 1, w.hid, d.H, 1, (float*)G.ta_w2, d.H, 1, d.H, R, nullptr, nullptr,
+                                   (float*)G.ta_b2, false, seed, 0u, 0.f, d.H));
+    DFD_TRY(launch_mfma_small_gemm(s, w.dhid, 1, d.H, F, d.D, 1, (float*)G.ta_w1, d.D, d.H, d.D, R, nullptr, nullptr,
+                                   (float*)G.ta_b1, false, seed, 0u, 0.f, d.D));
     hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)R * d.D)), dim3(256), 0, s, w.dhid, P.ta_w1, dF, R,
                        d.D, d.H, 1, seed, 0u, 0.f);
   }

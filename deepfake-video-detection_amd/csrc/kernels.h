@@ -126,6 +126,13 @@ int launch_pw_wgrad_bn_combine(hipStream_t s, const float* Tg, const float* G, c
                                const float* coef, int mid, int cin, float* dW, bool accumulate);
 template <typename T>
 int launch_col_sums(hipStream_t s, const T* X, int64_t M, int C, float* part, int64_t part_cap, float* out);
+// fp32 MFMA small GEMM (k_head.hip): C[m][n] (+)= sum_k A(m,k) B(k,n) (+bias[n]) (* silu'(pre[m][n])),
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn], optional dropout on B (p > 0),
+// optional asum[m] (+)= sum_k A(m,k)
+int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
+                           int64_t sbn, float* C, int64_t ldc, int M, int N, int K, const float* bias,
+                           const float* dsilu_pre, float* asum, bool accumulate, uint64_t seed, uint32_t stream,
+                           float p, int64_t drop_ld);
 // head global average pool: feat[f][c] = mean_hw silu(Y*scale+shift)
 template <typename T>
 int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat);

@@ -48,7 +48,9 @@ def _inputs(M, N, K, mode, rpf, seed, dev):
 def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0):
     lib = _lib_()
     a, w, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed, dev)
-    r = torch.randn(M, N, device=dev).to(torch.bfloat16) if resid else None
+    gr = torch.Generator(device=dev)
+    gr.manual_seed(seed + 1)
+    r = torch.randn(M, N, generator=gr, device=dev).to(torch.bfloat16) if resid else None
     c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     st = torch.zeros(1024 * 2 * N, device=dev) if stats else None
     rows = ctypes.c_int(0)
@@ -62,11 +64,15 @@ def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0):
         lib.dfd_set_tuning(b"stream_min_rows", prev)
     ap = _pro(a, mode, scale, shift, gate, rpf).to(torch.bfloat16).float()
     ref = ap @ w.float().t()
+    mag = ref.abs()
     if resid:
+        # the kernel adds the residual to the fp32 accumulator and rounds once; a bf16 framework
+        # rounds the conv output first, so near-cancelling sums may differ by one ulp of |conv|
+        mag = mag + r.float().abs()
         ref = ref.to(torch.bfloat16).float() + r.float()
     got = c.float()
     err = (got - ref).abs()
-    tol = 1e-2 * ref.abs() + 1e-2 * ref.abs().mean()
+    tol = 1e-2 * mag + 1e-2 * ref.abs().mean()
     assert bool((err <= tol).all()), f"max err {float(err.max())} (ref mean {float(ref.abs().mean())})"
     if stats:
         n = rows.value
