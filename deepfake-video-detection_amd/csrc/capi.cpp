@@ -259,6 +259,7 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "stream_min_rows") == 0) return dfd::set_stream_min_rows(value);
   if (key && strcmp(key, "fold_min_rows") == 0) return dfd::set_fold_min_rows(value);
   if (key && strcmp(key, "dw_bwd_fused") == 0) return dfd::set_dw_bwd_fused(value);
+  if (key && strcmp(key, "gemm_tile") == 0) return dfd::set_gemm_tile((int)value);
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }

@@ -9,7 +9,19 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace dfd {
+
+// compile-time loop: f(std::integral_constant<int, I>) for I = 0 .. N-1 (static register-array indices)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
 
 struct bf16 {
   uint16_t x;

@@ -523,21 +523,26 @@ __global__ __launch_bounds__(256) void se_bn_bwd_kernel(const T* __restrict__ dZ
 }
 
 // out[q][i] = sum_h part[q][h][i], q < 5 (h in order)
-__global__ void sum_parts5_kernel(const float* __restrict__ part, int hsplit, int64_t n, float* __restrict__ dgate,
-                                  float* __restrict__ pf) {
+// adds the hsplit partials; the SE gate gradient leaves as de = dgate * sigmoid'(.) = dgate g (1-g)
+__global__ void sum_parts5_kernel(const float* __restrict__ part, int hsplit, int64_t n,
+                                  const float* __restrict__ gate, float* __restrict__ de, float* __restrict__ pf) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < 5 * n; i += (int64_t)gridDim.x * 256) {
     const int64_t q = i / n, k = i - q * n;
     float a = 0.f;
     for (int h = 0; h < hsplit; ++h) a += part[(q * hsplit + h) * n + k];
-    if (q == 0) dgate[k] = a;
-    else pf[(q - 1) * n + k] = a;
+    if (q == 0) {
+      const float g = gate[k];
+      de[k] = a * g * (1.f - g);
+    } else {
+      pf[(q - 1) * n + k] = a;
+    }
   }
 }
 
 template <typename T>
 int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
                             const float* mean, const float* invstd, int frames, int HW, int C, float* part,
-                            int64_t part_cap, float* dgate, float* pf) {
+                            int64_t part_cap, const float* gate, float* de, float* pf) {
   int vpg, groups;
   bn_vpg_groups(C, vpg, groups);
   const int npl = 256 / vpg;
@@ -550,7 +555,7 @@ int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float*
                      invstd, frames, HW, C, hsplit, vpg, part);
   DFD_HIP_CHECK(hipGetLastError());
   const int64_t n = (int64_t)frames * C;
-  hipLaunchKernelGGL(sum_parts5_kernel, dim3(ew_grid(5 * n)), dim3(256), 0, s, part, hsplit, n, dgate, pf);
+  hipLaunchKernelGGL(sum_parts5_kernel, dim3(ew_grid(5 * n)), dim3(256), 0, s, part, hsplit, n, gate, de, pf);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -801,33 +806,6 @@ __global__ __launch_bounds__(256) void se_gate_kernel(const float* __restrict__ 
 
 // backward:  de = dgate*g*(1-g) ; dz = (We^T de) * silu'(rpre) ; bc = (Wr^T dz) * inv_hw
 template <int RD>
-__global__ __launch_bounds__(256) void se_dz_kernel(const float* __restrict__ dgate, const float* __restrict__ gate,
-                                                    const float* __restrict__ rpre, const float* __restrict__ we,
-                                                    int C, float* __restrict__ de_out, float* __restrict__ dz_out,
-                                                    float* __restrict__ r_out) {
-  __shared__ float red[4 * RD];
-  __shared__ float s_o[RD];
-  const int f = blockIdx.x, tid = threadIdx.x;
-  float acc[RD];
-#pragma unroll
-  for (int j = 0; j < RD; ++j) acc[j] = 0.f;
-  for (int c = tid; c < C; c += 256) {
-    const float g = gate[(int64_t)f * C + c];
-    const float d = dgate[(int64_t)f * C + c] * g * (1.f - g);
-    de_out[(int64_t)f * C + c] = d;
-    const float* w = we + (int64_t)c * RD;
-#pragma unroll
-    for (int j = 0; j < RD; ++j) acc[j] = fmaf(w[j], d, acc[j]);
-  }
-  block_sum_rd<RD>(acc, red, s_o);
-  if (tid < RD) {
-    const float rp = rpre[(int64_t)f * RD + tid];
-    dz_out[(int64_t)f * RD + tid] = s_o[tid] * dsiluf_(rp);
-    r_out[(int64_t)f * RD + tid] = siluf_(rp);
-  }
-}
-
-template <int RD>
 __global__ __launch_bounds__(256) void se_bc_kernel(const float* __restrict__ dz, const float* __restrict__ wr, int C,
                                                     float inv_hw, float* __restrict__ bc_out) {
   __shared__ float s_dz[RD];
@@ -849,10 +827,7 @@ static void se_fwd_launch(hipStream_t s, dim3 g2, int frames, const float* sq, c
   hipLaunchKernelGGL(se_gate_kernel<RD>, g2, dim3(256), 0, s, rpre, we, be, C, gate);
 }
 template <int RD>
-static void se_bwd_launch(hipStream_t s, dim3 g2, int frames, const float* dgate, const float* gate, const float* rpre,
-                          const float* wr, const float* we, int C, float inv_hw, float* de, float* dz, float* r,
-                          float* bc) {
-  hipLaunchKernelGGL(se_dz_kernel<RD>, dim3(frames), dim3(256), 0, s, dgate, gate, rpre, we, C, de, dz, r);
+static void se_bwd_launch(hipStream_t s, dim3 g2, const float* dz, const float* wr, int C, float inv_hw, float* bc) {
   hipLaunchKernelGGL(se_bc_kernel<RD>, g2, dim3(256), 0, s, dz, wr, C, inv_hw, bc);
 }
 
@@ -876,20 +851,30 @@ int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const floa
   return 0;
 }
 
-// weight grads (launch_se_fc_bwd): gwe[c][j] = sum_f de[f][c] r[f][j], gwr[j][c] = sum_f dz[f][j] sq[f][c]
-// (fp32 MFMA, frames ascending), gbe / gbr = column sums of de / dz.
-int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
-                     const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
-                     float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
-  float* tmp_r = tmp_dr + (int64_t)frames * rd;  // tmp_dr holds 2 * frames * rd floats
+// SE excitation backward from de = dgate * sigmoid'(.) (launch_se_bn_bwd_reduce), all on the fp32
+// MFMA small GEMM except the bc broadcast:
+//   dz[f][j]  = silu'(rpre[f][j]) sum_c de[f][c] we[c][j]
+//   gwe[c][j] = sum_f de[f][c] silu(rpre[f][j]),  gbe = sum_f de      (frames ascending)
+//   gwr[j][c] = sum_f dz[f][j] sq[f][c],          gbr = sum_f dz
+//   bc[f][c]  = inv_hw sum_j dz[f][j] wr[j][c]    (se_bc_kernel)
+int launch_se_fc_bwd(hipStream_t s, const float* de, const float* sq, const float* rpre, const float* wr,
+                     const float* we, int frames, int C, int rd, float inv_hw, float* tmp_dz, float* bc_out,
+                     float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
+  MfmaGemm g{};
+  g.A = de; g.sam = C; g.sak = 1; g.B = we; g.sbk = rd; g.sbn = 1; g.C = tmp_dz; g.ldc = rd;
+  g.M = frames; g.N = rd; g.K = C; g.dsilu_pre = rpre;
+  DFD_TRY(launch_mfma_small_gemm(s, g));
+  g = MfmaGemm{};
+  g.A = de; g.sam = 1; g.sak = C; g.B = rpre; g.sbk = rd; g.sbn = 1; g.b_silu = 1; g.C = gwe; g.ldc = rd;
+  g.M = C; g.N = rd; g.K = frames; g.asum = gbe; g.accumulate = accumulate;
+  DFD_TRY(launch_mfma_small_gemm(s, g));
+  g = MfmaGemm{};
+  g.A = tmp_dz; g.sam = 1; g.sak = rd; g.B = sq; g.sbk = C; g.sbn = 1; g.C = gwr; g.ldc = C;
+  g.M = rd; g.N = C; g.K = frames; g.asum = gbr; g.accumulate = accumulate;
+  DFD_TRY(launch_mfma_small_gemm(s, g));
   const dim3 g2((unsigned)cdiv(C, 256), (unsigned)frames);
-  DFD_SE_RD_SWITCH(rd, se_bwd_launch<RD>(s, g2, frames, dgate, gate, rpre, wr, we, C, inv_hw, tmp_de, tmp_dr, tmp_r,
-                                          bc_out));
+  DFD_SE_RD_SWITCH(rd, se_bwd_launch<RD>(s, g2, tmp_dz, wr, C, inv_hw, bc_out));
   DFD_HIP_CHECK(hipGetLastError());
-  DFD_TRY(launch_mfma_small_gemm(s, tmp_de, 1, C, tmp_r, rd, 1, gwe, rd, C, rd, frames, nullptr, nullptr, gbe,
-                                 accumulate, 0, 0u, 0.f, 0));
-  DFD_TRY(launch_mfma_small_gemm(s, tmp_dr, 1, rd, sq, C, 1, gwr, C, rd, C, frames, nullptr, nullptr, gbr,
-                                 accumulate, 0, 0u, 0.f, 0));
   return 0;
 }
 
@@ -933,7 +918,8 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
                                        float*);                                                                     \
   template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);                            \
   template int launch_se_bn_bwd_reduce<T>(hipStream_t, const T*, const T*, const float*, const float*, const float*, \
-                                          const float*, int, int, int, float*, int64_t, float*, float*);      \
+                                          const float*, int, int, int, float*, int64_t, const float*, float*,  \
+                                          float*);                                                             \
   template int launch_bn_fold_pw<T>(hipStream_t, const float*, const float*, int, int, T*, T*, float*);             \
   template int launch_col_sums<T>(hipStream_t, const T*, int64_t, int, float*, int64_t, float*);
 DFD_BN_INST(float)

@@ -13,6 +13,8 @@
 // row=4*(lane>>4)+r for both.
 #include "kernels.h"
 
+#include <atomic>
+
 namespace dfd {
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -20,16 +22,22 @@ typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
-constexpr int GBM = 128;  // rows per tile
-constexpr int GBN = 128;  // output columns per tile
-constexpr int GBK = 32;   // contraction per step
-
-template <typename T> struct GemmCfg {
-  static constexpr int AS = sizeof(T) == 2 ? GBK + 8 : GBK + 4;   // LDS row stride (elements) of A/B tiles
-  static constexpr int CS = sizeof(T) == 2 ? GBN + 8 : GBN + 4;   // LDS row stride of the C tile
-  static constexpr int AB_BYTES = 2 * GBM * AS * (int)sizeof(T);
-  static constexpr int C_BYTES = GBM * CS * (int)sizeof(T);
+// Tile shape: BM x BN outputs per workgroup of 4 waves laid out WM x WN (WM * WN = 4); each wave
+// owns RB x CB 16x16 MFMA blocks; BK = contraction per k-step (one LDS hand-off, BK / 32 MFMA
+// k-slices).  D = global-load pipeline depth: the loads of k-step k + D are issued while step k
+// computes (register ring, static stage index via a D-unrolled k loop).
+template <typename T, int BM, int BN, int WN, int D, int BK>
+struct GemmCfg {
+  static constexpr int WM = 4 / WN;
+  static constexpr int RB = BM / WM / 16, CB = BN / WN / 16;
+  static constexpr int VPR = BK / 8, RPP = 256 / VPR;       // 8-vectors per row, rows per staging pass
+  static constexpr int PA = BM / RPP, PB = BN / RPP;        // 8-vectors per thread per k-step
+  static constexpr int AS = sizeof(T) == 2 ? BK + 8 : BK + 4;  // LDS row stride (elements) of A/B tiles
+  static constexpr int CS = sizeof(T) == 2 ? BN + 8 : BN + 4;    // LDS row stride of the C tile
+  static constexpr int AB_BYTES = (BM + BN) * AS * (int)sizeof(T);
+  static constexpr int C_BYTES = BM * CS * (int)sizeof(T);
   static constexpr int SMEM = AB_BYTES > C_BYTES ? AB_BYTES : C_BYTES;
+  static_assert(WM * WN == 4 && RB >= 1 && CB >= 1 && PA >= 1 && PB >= 1 && BK % 32 == 0, "tile shape");
 };
 
 template <typename T>
@@ -37,38 +45,43 @@ __device__ __forceinline__ void lds_st8(T* p, const float (&v)[8]) { st8(p, v); 
 template <typename T>
 __device__ __forceinline__ void lds_ld8(const T* p, float (&v)[8]) { ld8(p, v); }
 
-template <typename T, int MODE, bool STATS, int EPI>
-__global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
-                                                      T* __restrict__ C, const T* __restrict__ R,
-                                                      const float* __restrict__ bias, const T* __restrict__ Z,
-                                                      int64_t M, int N, int K, Pro pro, float* __restrict__ stats,
-                                                      int64_t tiles_m, int ntn) {
+template <typename T, int MODE, bool STATS, int EPI, int BM, int BN, int WN, int D, int BK, int OCC>
+__global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                        T* __restrict__ C, const T* __restrict__ R,
+                                                        const float* __restrict__ bias, const T* __restrict__ Z,
+                                                        int64_t M, int N, int K, Pro pro, float* __restrict__ stats,
+                                                        int64_t tiles_m, int ntn) {
   constexpr bool RESID = (EPI & EPI_RESID) != 0, BIAS = (EPI & EPI_BIAS) != 0, DGELU = (EPI & EPI_DGELU) != 0;
-  using G = GemmCfg<T>;
+  using G = GemmCfg<T, BM, BN, WN, D, BK>;
+  constexpr int GBK = BK;
+  constexpr int WM = G::WM, RB = G::RB, CB = G::CB, PA = G::PA, PB = G::PB;
+  constexpr bool GATE = MODE == PRO_BN_SILU_G;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  __shared__ float st_sum[GBN];
-  __shared__ float st_sq[GBN];
-  __shared__ float st_part[STATS ? 4 : 1][2][GBN];  // per-wave column partials (fixed-order sum)
+  __shared__ float st_sum[BN];
+  __shared__ float st_sq[BN];
+  __shared__ float st_part[STATS ? WM : 1][2][BN];  // per-wave-row column partials (fixed-order sum)
   T* As = reinterpret_cast<T*>(smem);
-  T* Bs = As + GBM * G::AS;
+  T* Bs = As + BM * G::AS;
   T* Cs = reinterpret_cast<T*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
+  const int rbase = wm * (BM / WM), cbase = wn * (BN / WN);
   // 1-D grid, N tile fastest: the ntn workgroups that share an A row-tile are adjacent in
   // dispatch order, so A is read from HBM once and from L2 by the others.
   const int nt = (int)(blockIdx.x % ntn);
   const int64_t mg = blockIdx.x / ntn, mstep = gridDim.x / ntn;
-  const int n0 = nt * GBN;
-  const int nvalid = min(GBN, N - n0);
-  const int nb = (nvalid + 15) >> 4;
+  const int n0 = nt * BN;
+  const int nvalid = min(BN, N - n0);
+  const int nk = (K + GBK - 1) / GBK;
   if constexpr (STATS) {
-    for (int i = tid; i < GBN; i += 256) { st_sum[i] = 0.f; st_sq[i] = 0.f; }
+    for (int i = tid; i < BN; i += 256) { st_sum[i] = 0.f; st_sq[i] = 0.f; }
   }
 
-  // staging: this thread owns rows srow, srow + 64 and k-vector skc of each 128 x 32 A/B step
-  const int srow = tid >> 2, skc = (tid & 3) * 8;
-  Raw8<T> ra[2], rb[2];
-  float pg[MODE == PRO_BN_SILU_G ? 2 : 1][8];
+  // staging: this thread owns rows srow + RPP i and k-vector skc of each k-step
+  const int srow = tid / G::VPR, skc = (tid % G::VPR) * 8;
+  Raw8<T> ra[D][PA], rb[D][PB];
+  float pg[GATE ? D : 1][GATE ? PA : 1][8];
   // producer BN scale/shift of all K columns, staged once per workgroup (dynamic LDS, 2K floats)
   extern __shared__ float pro_lds[];
   if constexpr (pro_is_bn(MODE)) {
@@ -78,122 +91,141 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
     }
     lds_barrier();
   }
-  auto load = [&](int64_t m0, int k0) {
-    const int gk = k0 + skc;
+  // issue the global loads of k-step k of the tile at row m0 into ring stage d
+  auto load = [&](auto dc, int64_t m0, int k) {
+    constexpr int d = decltype(dc)::value;
+    const int gk = k * GBK + skc;
     const bool kok = gk < K;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t gm = m0 + srow + 64 * i;
-      raw_ld(ra[i], A + gm * K + gk, A, gm < M && kok);
-      raw_ld(rb[i], B + (int64_t)(n0 + srow + 64 * i) * K + gk, B, srow + 64 * i < nvalid && kok);
+    for (int i = 0; i < PA; ++i) {
+      const int64_t gm = m0 + srow + G::RPP * i;
+      raw_ld(ra[d][i], A + gm * K + gk, A, gm < M && kok);
     }
-    if constexpr (MODE == PRO_BN_SILU_G) {
-      const int kc = kok ? gk : 0;
-      {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int64_t gm = m0 + srow + 64 * i;
-          const uint32_t f = (uint32_t)(gm < M ? gm : m0) / (uint32_t)pro.rows_per_frame;
-          ld8f(pro.gate + (int64_t)f * pro.C + kc, pg[i]);
-        }
+    for (int i = 0; i < PB; ++i)
+      raw_ld(rb[d][i], B + (int64_t)(n0 + srow + G::RPP * i) * K + gk, B, srow + G::RPP * i < nvalid && kok);
+    if constexpr (GATE) {
+      const int kc = kok ? gk : 0;
+#pragma unroll
+      for (int i = 0; i < PA; ++i) {
+        const int64_t gm = m0 + srow + G::RPP * i;
+        const uint32_t f = (uint32_t)(gm < M ? gm : m0) / (uint32_t)pro.rows_per_frame;
+        ld8f(pro.gate + (int64_t)f * pro.C + kc, pg[d][i]);
       }
     }
   };
+  auto issue_first = [&](int64_t m0) {
+    static_for<D>([&](auto dc) {
+      if (decltype(dc)::value < nk) load(dc, m0, decltype(dc)::value);
+    });
+  };
 
-  // The first k-step of the NEXT tile is loaded before this tile's epilogue stores: vmcnt
+  // The first D k-steps of the NEXT tile are issued before this tile's epilogue stores: vmcnt
   // counts loads and stores together, so loads issued after the stores would wait for them.
-  if (mg < tiles_m) load(mg * GBM, 0);
+  if (mg < tiles_m) issue_first(mg * BM);
   for (int64_t mt = mg; mt < tiles_m; mt += mstep) {
-    const int64_t m0 = mt * GBM;
-    f32x4_t acc[2][8];
+    const int64_t m0 = mt * BM;
+    f32x4_t acc[RB][CB];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < RB; ++a)
 #pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      for (int b = 0; b < CB; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    if (MODE != PRO_NONE && mt != mg) load(m0, 0);
-    for (int k0 = 0; k0 < K; k0 += GBK) {
-      // ---- registers -> LDS (A through the consumer-side BN/SiLU/gate prologue) ----
+    for (int kc = 0; kc < nk; kc += D) {
+      static_for<D>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        const int k = kc + d;
+        if (k >= nk) return;
+        const int k0 = k * GBK;
+        // ---- registers -> LDS (A through the consumer-side BN/SiLU/gate prologue) ----
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = srow + 64 * i;
-        if constexpr (MODE == PRO_NONE) {
-          raw_st(As + row * G::AS + skc, ra[i]);
-        } else if constexpr (MODE == PRO_GELU) {
-          float x[8];
-          raw_to_f(ra[i], x);
+        for (int i = 0; i < PA; ++i) {
+          const int row = srow + G::RPP * i;
+          if constexpr (MODE == PRO_NONE) {
+            raw_st(As + row * G::AS + skc, ra[d][i]);
+          } else if constexpr (MODE == PRO_GELU) {
+            float x[8];
+            raw_to_f(ra[d][i], x);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);  // masked lanes hold 0 and gelu(0) = 0
-          lds_st8(As + row * G::AS + skc, x);
-        } else {
-          float x[8], psc[8], psh[8];
-          raw_to_f(ra[i], x);
-          const int kc = k0 + skc < K ? k0 + skc : 0;
-          ld8(pro_lds + kc, psc);
-          ld8(pro_lds + K + kc, psh);
-          if constexpr (MODE == PRO_BN_SILU_G) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]) * pg[i][j];
+            for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);  // masked lanes hold 0 and gelu(0) = 0
+            lds_st8(As + row * G::AS + skc, x);
           } else {
+            float x[8], psc[8], psh[8];
+            raw_to_f(ra[d][i], x);
+            const int kcol = k0 + skc < K ? k0 + skc : 0;
+            ld8(pro_lds + kcol, psc);
+            ld8(pro_lds + K + kcol, psh);
+            if constexpr (GATE) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]);
-          }
-          const bool ok = m0 + row < M && k0 + skc < K;
+              for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]) * pg[d][i][j];
+            } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = ok ? x[j] : 0.f;
-          lds_st8(As + row * G::AS + skc, x);
-        }
-        raw_st(Bs + row * G::AS + skc, rb[i]);
-      }
-      lds_barrier();
-      if (k0 + GBK < K) load(m0, k0 + GBK);
-      else if (MODE == PRO_NONE && mt + mstep < tiles_m) load((mt + mstep) * GBM, 0);
-      // ---- MFMA (partial N tiles are zero padded: the sequence is unconditional) ----
-      if constexpr (sizeof(T) == 2) {
-        bf16x8_t af[2];
+              for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * psc[j] + psh[j]);
+            }
+            const bool ok = m0 + row < M && k0 + skc < K;
 #pragma unroll
-        for (int rb_ = 0; rb_ < 2; ++rb_)
-          af[rb_] = *reinterpret_cast<const bf16x8_t*>(As + (wave * 32 + rb_ * 16 + (lane & 15)) * G::AS +
-                                                       8 * (lane >> 4));
-#pragma unroll
-        for (int cb = 0; cb < 8; ++cb) {
-          const bf16x8_t bfr =
-              *reinterpret_cast<const bf16x8_t*>(Bs + (cb * 16 + (lane & 15)) * G::AS + 8 * (lane >> 4));
-#pragma unroll
-          for (int rb_ = 0; rb_ < 2; ++rb_)
-            acc[rb_][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[rb_], bfr, acc[rb_][cb], 0, 0, 0);
-        }
-      } else {
-#pragma unroll
-        for (int s = 0; s < GBK / 4; ++s) {
-          const int kk = 4 * s + (lane >> 4);
-          const float a0 = reinterpret_cast<const float*>(As)[(wave * 32 + (lane & 15)) * G::AS + kk];
-          const float a1 = reinterpret_cast<const float*>(As)[(wave * 32 + 16 + (lane & 15)) * G::AS + kk];
-#pragma unroll
-          for (int cb = 0; cb < 8; ++cb) {
-            const float b = reinterpret_cast<const float*>(Bs)[(cb * 16 + (lane & 15)) * G::AS + kk];
-            acc[0][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b, acc[0][cb], 0, 0, 0);
-            acc[1][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b, acc[1][cb], 0, 0, 0);
+            for (int j = 0; j < 8; ++j) x[j] = ok ? x[j] : 0.f;
+            lds_st8(As + row * G::AS + skc, x);
           }
         }
-      }
-      lds_barrier();
+#pragma unroll
+        for (int i = 0; i < PB; ++i) raw_st(Bs + (srow + G::RPP * i) * G::AS + skc, rb[d][i]);
+        lds_barrier();
+        if (k + D < nk) load(dc, m0, k + D);
+        // ---- MFMA (partial N tiles are zero padded: the sequence is unconditional) ----
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int ks = 0; ks < BK / 32; ++ks) {
+            bf16x8_t af[RB];
+#pragma unroll
+            for (int r_ = 0; r_ < RB; ++r_)
+              af[r_] = *reinterpret_cast<const bf16x8_t*>(As + (rbase + r_ * 16 + (lane & 15)) * G::AS + ks * 32 +
+                                                         8 * (lane >> 4));
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+              const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(
+                  Bs + (cbase + cb * 16 + (lane & 15)) * G::AS + ks * 32 + 8 * (lane >> 4));
+#pragma unroll
+              for (int r_ = 0; r_ < RB; ++r_)
+                acc[r_][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[r_], bfr, acc[r_][cb], 0, 0, 0);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int s4 = 0; s4 < GBK / 4; ++s4) {
+            const int kk = 4 * s4 + (lane >> 4);
+            float av[RB];
+#pragma unroll
+            for (int r_ = 0; r_ < RB; ++r_)
+              av[r_] = reinterpret_cast<const float*>(As)[(rbase + r_ * 16 + (lane & 15)) * G::AS + kk];
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+              const float bv = reinterpret_cast<const float*>(Bs)[(cbase + cb * 16 + (lane & 15)) * G::AS + kk];
+#pragma unroll
+              for (int r_ = 0; r_ < RB; ++r_)
+                acc[r_][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r_], bv, acc[r_][cb], 0, 0, 0);
+            }
+          }
+        }
+        lds_barrier();
+      });
     }
+    if (mt + mstep < tiles_m) issue_first((mt + mstep) * BM);
 
     // ---- epilogue: round, BN-stat partials, stage C tile in LDS ----
 #pragma unroll
-    for (int cb = 0; cb < 8; ++cb) {
-      if (cb < nb) {
-        const int col = cb * 16 + (lane & 15);
+    for (int cb = 0; cb < CB; ++cb) {
+      const int col = cbase + cb * 16 + (lane & 15);
+      if (cbase + cb * 16 < nvalid) {
         float bcol = 0.f;
         if constexpr (BIAS) bcol = col < nvalid ? bias[n0 + col] : 0.f;
         float s = 0.f, q = 0.f;
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
+        for (int r_ = 0; r_ < RB; ++r_) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int row = wave * 32 + rb * 16 + 4 * (lane >> 4) + r;
-            const float v = Tr<T>::round(acc[rb][cb][r] + bcol);
+            const int row = rbase + r_ * 16 + 4 * (lane >> 4) + r;
+            const float v = Tr<T>::round(acc[r_][cb][r] + bcol);
             Cs[row * G::CS + col] = Tr<T>::from_f(v);
             if constexpr (STATS) {
               if (m0 + row < M) { s += v; q += v * v; }
@@ -204,22 +236,25 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
           s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
           q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
           if (lane < 16) {
-            st_part[wave][0][col] = s;
-            st_part[wave][1][col] = q;
+            st_part[wm][0][col] = s;
+            st_part[wm][1][col] = q;
           }
         }
       }
     }
     lds_barrier();
     if constexpr (STATS) {
-      // waves 0..3 in order: bit-reproducible BN statistics
-      if (tid < nvalid) {
-        st_sum[tid] += ((st_part[0][0][tid] + st_part[1][0][tid]) + st_part[2][0][tid]) + st_part[3][0][tid];
-        st_sq[tid] += ((st_part[0][1][tid] + st_part[1][1][tid]) + st_part[2][1][tid]) + st_part[3][1][tid];
+      // wave rows in order: bit-reproducible BN statistics
+      for (int i = tid; i < nvalid; i += 256) {
+        float a = st_part[0][0][i], b = st_part[0][1][i];
+#pragma unroll
+        for (int w = 1; w < WM; ++w) { a += st_part[w][0][i]; b += st_part[w][1][i]; }
+        st_sum[i] += a;
+        st_sq[i] += b;
       }
     }
     const int vpr = nvalid >> 3;
-    for (int v = tid; v < GBM * vpr; v += 256) {
+    for (int v = tid; v < BM * vpr; v += 256) {
       const int row = v / vpr, cv = (v - row * vpr) * 8;
       const int64_t gm = m0 + row;
       if (gm >= M) continue;
@@ -249,6 +284,48 @@ __global__ __launch_bounds__(256, 2) void pw_gemm_kernel(const T* __restrict__ A
   }
 }
 
+// tile configurations (BM, BN, WN, D, OCC); g_gemm_tile forces one for experiments (-1 = auto)
+static std::atomic<int> g_gemm_tile{-1};
+int set_gemm_tile(int v) { return g_gemm_tile.exchange(v); }
+
+template <typename T, int MODE, bool ST, int EP, int BM, int BN, int WN, int D, int BK, int OCC>
+static void gemm_go(hipStream_t s, int gx_m, int ntn, size_t dyn, const T* A, const T* B, T* C, const T* R,
+                    const float* bias, const T* Z, int64_t M, int N, int K, const Pro& pro, float* stats,
+                    int64_t tiles_m) {
+  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, EP, BM, BN, WN, D, BK, OCC>), dim3((unsigned)(gx_m * ntn)),
+                     dim3(256), dyn, s, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m, ntn);
+}
+
+template <typename T, int MODE, bool ST, int EP>
+static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z,
+                      int64_t M, int N, int K, const Pro& pro, float* stats, int* stat_rows, size_t dyn) {
+  // 0: 128x128 (4x1 waves), 1: 128x64 (4x1), 2: 64x64 (2x2), 3: 32x64 (2x2, 64-deep k-steps).
+  // Chosen per shape from tools/kbench on MI355X (tools/gemm_tiles.sh): one 128-wide N tile while
+  // N <= 128 (the A prologue then runs once per row tile); 128x64 for narrow N; the 14x14 / 7x7
+  // stages (few row tiles) want the small tiles for enough workgroups in flight.
+  int cfg = g_gemm_tile.load();
+  if (cfg < 0 || cfg > 3) {
+    if (N <= 64) cfg = 1;
+    else if (N <= 128) cfg = 0;
+    else if (M <= 16384) cfg = N <= 256 ? 3 : 1;
+    else if (M <= 65536) cfg = 2;
+    else cfg = N <= 160 ? 1 : 2;
+  }
+  const int bm = cfg == 3 ? 32 : cfg == 2 ? 64 : 128, bn = cfg == 0 ? 128 : 64;
+  const int ntn = cdiv(N, bn);
+  const int64_t tiles_m = cdiv64(M, bm);
+  const int64_t cap = std::max<int64_t>(1, 1024 / ntn);  // <= 1024 BN-stat partial rows (plan's stats buffer)
+  const int gx = (int)std::min<int64_t>(tiles_m, cap);
+  constexpr int DW = sizeof(T) == 4 ? 1 : 0;  // fp32 (parity mode): shallower ring, no spills
+  constexpr int O64 = (MODE == PRO_BN_SILU_G || sizeof(T) == 4) ? 2 : 4;
+  if (cfg == 0) gemm_go<T, MODE, ST, EP, 128, 128, 1, 2 - DW, 32, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 1) gemm_go<T, MODE, ST, EP, 128, 64, 1, 3 - DW, 32, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 2) gemm_go<T, MODE, ST, EP, 64, 64, 2, 3, 32, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else gemm_go<T, MODE, ST, EP, 32, 64, 2, 2, 64, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  if (stat_rows) *stat_rows = gx;
+  return 0;
+}
+
 template <typename T>
 static int gemm_dispatch(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z,
                          int64_t M, int N, int K, int pro_mode, int epi, const Pro& pro, float* stats, int* stat_rows) {
@@ -259,16 +336,10 @@ static int gemm_dispatch(hipStream_t s, const T* A, const T* B, T* C, const T* R
     set_error("pw_gemm: epilogue operand missing", __FILE__, __LINE__);
     return -1;
   }
-  const int ntn = cdiv(N, GBN);
-  const int64_t tiles_m = cdiv64(M, GBM);
-  const int64_t cap = std::max<int64_t>(1, 1024 / ntn);
-  const int gx = (int)std::min<int64_t>(tiles_m, cap);
-  dim3 grid((unsigned)(gx * ntn)), block(256);
   const bool st = stats != nullptr;
   const size_t dyn = pro_is_bn(pro_mode) ? 2 * (size_t)K * sizeof(float) : 0;
 #define DFD_GEMM_LAUNCH(MODE, ST, EP) \
-  hipLaunchKernelGGL((pw_gemm_kernel<T, MODE, ST, EP>), grid, block, dyn, s, A, B, C, R, bias, Z, M, N, K, pro, stats, \
-                     tiles_m, ntn)
+  gemm_tiles<T, MODE, ST, EP>(s, A, B, C, R, bias, Z, M, N, K, pro, stats, stat_rows, dyn)
   // instantiated combinations: the B0 trunk's (BN prologues, BN-stat epilogue, residual) and the
   // ViT's (bias, bias + residual, GELU prologue + bias + residual, GELU-derivative epilogue)
   if (pro_mode == PRO_NONE && epi == EPI_RESID && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_RESID);
@@ -287,7 +358,6 @@ static int gemm_dispatch(hipStream_t s, const T* A, const T* B, T* C, const T* R
     return -1;
   }
 #undef DFD_GEMM_LAUNCH
-  if (stat_rows) *stat_rows = gx;
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

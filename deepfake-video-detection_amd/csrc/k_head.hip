@@ -132,20 +132,8 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
 // per-output dot-product threads are latency-bound: one workgroup per 16x16 output tile, its
 // waves splitting K round-robin in 32-k chunks (operands of a chunk loaded before its MFMAs),
 // then a fixed-order LDS reduction over the waves (bit-reproducible).  Options: bias[n],
-// post-multiplication by silu'(pre[m][n]), counter-hash dropout on B (index k*drop_ld + n), and
+// post-multiplication by silu'(pre[m][n]), silu(B), counter-hash dropout on B (index k*drop_ld + n), and
 // asum[m] (+)= sum_k A(m,k) (the bias gradient of a weight-gradient product) from n-tile 0.
-struct MfmaGemm {
-  const float* A; int64_t sam, sak;
-  const float* B; int64_t sbk, sbn;
-  float* C; int64_t ldc;
-  int M, N, K;
-  const float* bias;
-  const float* dsilu_pre;  // [M][ldc] or null
-  float* asum;             // [M] or null
-  int accumulate;
-  uint64_t seed; uint32_t stream; float p; int64_t drop_ld;  // dropout on B if p > 0
-};
-
 typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MG_MAXW = 16;
 
@@ -171,6 +159,7 @@ __global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a) {
       const bool kok = k < a.K;
       av[u] = (mok && kok) ? a.A[(int64_t)m * a.sam + (int64_t)k * a.sak] : 0.f;
       float b = (nok && kok) ? a.B[(int64_t)k * a.sbk + (int64_t)n * a.sbn] : 0.f;
+      if (a.b_silu) b = siluf_(b);
       if (drop && nok && kok) b *= drop_mul(a.seed, a.stream, (int64_t)k * a.drop_ld + n, a.p);
       bv[u] = b;
     }
@@ -209,9 +198,16 @@ int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t s
                            int64_t sbn, float* C, int64_t ldc, int M, int N, int K, const float* bias,
                            const float* dsilu_pre, float* asum, bool accumulate, uint64_t seed, uint32_t stream,
                            float p, int64_t drop_ld) {
+  MfmaGemm g;
+  g.A = A; g.sam = sam; g.sak = sak; g.B = B; g.sbk = sbk; g.sbn = sbn; g.C = C; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.bias = bias; g.dsilu_pre = dsilu_pre; g.asum = asum;
+  g.accumulate = accumulate ? 1 : 0; g.seed = seed; g.stream = stream; g.p = p; g.drop_ld = drop_ld;
+  return launch_mfma_small_gemm(s, g);
+}
+
+int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g) {
+  const int M = g.M, N = g.N, K = g.K;
   if (M <= 0 || N <= 0) return 0;
-  const MfmaGemm g{A, sam, sak, B, sbk, sbn, C, ldc, M, N, K, bias, dsilu_pre, asum, accumulate ? 1 : 0,
-                   seed, stream, p, drop_ld};
   const int tiles = cdiv(M, 16) * cdiv(N, 16);
   // waves per tile: enough K-splitting to put ~2 chunks on each wave, at most MG_MAXW
   const int nw = std::max(1, std::min(MG_MAXW, cdiv(K, 64)));

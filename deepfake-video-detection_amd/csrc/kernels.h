@@ -22,6 +22,7 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
 // rows threshold of the streaming kernels (returns the previous value)
 int64_t set_stream_min_rows(int64_t v);
+int set_gemm_tile(int v);  // tiled pw GEMM: force tile config 0/1/2, -1 = auto (returns previous)
 // Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
 // pro_mode PRO_NONE or PRO_GELU; epi a mask of GemmEpi.
 enum GemmEpi { EPI_RESID = 1, EPI_BIAS = 2, EPI_DGELU = 4 };
@@ -106,15 +107,15 @@ int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro,
                          float* part, int64_t part_cap, float* dgate);
 // SE FC backward: from dgate -> dsq (written, scaled by 1/HW into bc), grads of wr,br,we,be.
 // tmp_de: frames*C floats; tmp_dr: 2*frames*rd floats
-int launch_se_fc_bwd(hipStream_t s, const float* dgate, const float* gate, const float* sq, const float* rpre,
-                     const float* wr, const float* we, int frames, int C, int rd, float inv_hw, float* tmp_de,
-                     float* tmp_dr, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
-// SE + BN(+SiLU) backward sums in one pass over (dZ, Y): dgate[f][c] (SE branch) and the per-frame
+int launch_se_fc_bwd(hipStream_t s, const float* de, const float* sq, const float* rpre, const float* wr,
+                     const float* we, int frames, int C, int rd, float inv_hw, float* tmp_dz, float* bc_out,
+                     float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
+// SE + BN(+SiLU) backward sums in one pass over (dZ, Y): de[f][c] = dgate g (1-g) (SE branch) and the per-frame
 // sums pf[4][frames][C] that bn_bwd_finalize_frames combines with the gate and bc (k_bn.hip)
 template <typename T>
 int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
                             const float* mean, const float* invstd, int frames, int HW, int C, float* part,
-                            int64_t part_cap, float* dgate, float* pf);
+                            int64_t part_cap, const float* gate, float* de, float* pf);
 int launch_bn_bwd_finalize_frames(hipStream_t s, const float* pf, const float* gate, const float* bc, int frames,
                                   int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
                                   bool training, float* dgamma, float* dbeta, bool accumulate, float* coef);
@@ -126,9 +127,22 @@ int launch_pw_wgrad_bn_combine(hipStream_t s, const float* Tg, const float* G, c
                                const float* coef, int mid, int cin, float* dW, bool accumulate);
 template <typename T>
 int launch_col_sums(hipStream_t s, const T* X, int64_t M, int C, float* part, int64_t part_cap, float* out);
-// fp32 MFMA small GEMM (k_head.hip): C[m][n] (+)= sum_k A(m,k) B(k,n) (+bias[n]) (* silu'(pre[m][n])),
-// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn], optional dropout on B (p > 0),
-// optional asum[m] (+)= sum_k A(m,k)
+// fp32 MFMA small GEMM (k_head.hip): C[m][n] (+)= post( sum_k A(m,k) B(k,n) ),
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn] (silu(B) if b_silu, dropout on B if p > 0);
+// post: + bias[n], * silu'(dsilu_pre[m][n]);  asum[m] (+)= sum_k A(m,k) when non-null
+struct MfmaGemm {
+  const float* A = nullptr; int64_t sam = 0, sak = 0;
+  const float* B = nullptr; int64_t sbk = 0, sbn = 0;
+  float* C = nullptr; int64_t ldc = 0;
+  int M = 0, N = 0, K = 0;
+  const float* bias = nullptr;
+  const float* dsilu_pre = nullptr;  // [M][ldc]
+  float* asum = nullptr;             // [M]
+  int accumulate = 0;
+  int b_silu = 0;
+  uint64_t seed = 0; uint32_t stream = 0; float p = 0.f; int64_t drop_ld = 0;
+};
+int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g);
 int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                            int64_t sbn, float* C, int64_t ldc, int M, int N, int K, const float* bias,
                            const float* dsilu_pre, float* asum, bool accumulate, uint64_t seed, uint32_t stream,

@@ -192,11 +192,10 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.o_slab = alloc(p.slab_cap * 4);
   p.o_part = alloc(p.part_cap * 4);
   p.o_coef = alloc(3 * kHead * 4);
-  p.o_dgate = alloc(F * maxSE * 4);
   p.o_bc = alloc(F * maxSE * 4);
   p.o_pf = alloc(4 * F * maxSE * 4);  // per-frame SE/BN backward sums
   p.o_de = alloc(F * maxSE * 4);
-  p.o_dz = alloc(F * maxRD * 2 * 4);  // dz and r = silu(rpre)
+  p.o_dz = alloc(F * maxRD * 4);
   p.o_gx[0] = alloc(maxX * es);
   p.o_gx[1] = alloc(maxX * es);
   p.o_gs = alloc(maxS * es);
@@ -420,11 +419,10 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
         DFD_TRY(launch_se_bn_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                            r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), p.frames, hwo, b.mid,
-                                           r.f(p.o_part), p.part_cap, r.f(p.o_dgate), r.f(p.o_pf)));
-        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_dgate), r.f(b.o_gate), r.f(b.o_sq), r.f(b.o_rpre), r.prm(b.t_se_wr),
-                                 r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo, r.f(p.o_de), r.f(p.o_dz),
-                                 r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we), grad(b.t_se_be),
-                                 acc != 0));
+                                           r.f(p.o_part), p.part_cap, r.f(b.o_gate), r.f(p.o_de), r.f(p.o_pf)));
+        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_de), r.f(b.o_sq), r.f(b.o_rpre), r.prm(b.t_se_wr), r.prm(b.t_se_we),
+                                 p.frames, b.mid, b.rd, 1.0f / (float)hwo, r.f(p.o_dz), r.f(p.o_bc), grad(b.t_se_wr),
+                                 grad(b.t_se_br), grad(b.t_se_we), grad(b.t_se_be), acc != 0));
         DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_pf), r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid, Mout,
                                               r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), tr != 0,
                                               grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));

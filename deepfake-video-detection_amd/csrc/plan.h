@@ -63,7 +63,7 @@ struct Plan {
   std::vector<Block> blocks;
   // workspace
   int64_t ws_bytes = 0;
-  int64_t o_ystem, o_yh, o_stats, o_slab, o_part, o_coef, o_dgate, o_bc, o_de, o_dz, o_pf;
+  int64_t o_ystem, o_yh, o_stats, o_slab, o_part, o_coef, o_bc, o_de, o_dz, o_pf;
   int64_t o_gx[2], o_gs, o_ge1, o_ge2;
   int64_t o_w1t, o_q, o_bv, o_tg, o_gram, o_cs;  // conv_pw backward through its BN (bn_fold_pw)
   int64_t stats_cap, slab_cap, part_cap;

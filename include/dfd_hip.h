@@ -129,7 +129,9 @@ DFD_API int dfd_adam_step(void* stream, float* params, float* grads, float* exp_
  * "fold_min_rows": IR blocks whose conv_pw has at least this many rows run its backward through
  * the BN-folded form (no materialised BN input gradient; default 100000).
  * "dw_bwd_fused": 1 (default) runs the depthwise input and weight gradients as one fused pass,
- * 0 as two kernels. */
+ * 0 as two kernels.
+ * "gemm_tile": tile of the (non-streaming) 1x1-conv GEMM: 0 = 128x128, 1 = 128x64, 2 = 64x64, 3 = 32x64,
+ * -1 (default) = chosen per shape. */
 DFD_API int64_t dfd_set_tuning(const char* key, int64_t value);
 
 /* ---- pointwise (1x1) convolution, the trunk's conv_pw / conv_pwl / conv_head kernels ----------

@@ -45,7 +45,7 @@ def _inputs(M, N, K, mode, rpf, seed, dev):
     return a, w, scale, shift, gate
 
 
-def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0):
+def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, tile=-1):
     lib = _lib_()
     a, w, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed, dev)
     gr = torch.Generator(device=dev)
@@ -55,6 +55,7 @@ def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0):
     st = torch.zeros(1024 * 2 * N, device=dev) if stats else None
     rows = ctypes.c_int(0)
     prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
+    prev_tile = lib.dfd_set_tuning(b"gemm_tile", tile)
     try:
         _lib.check(lib.dfd_pw_conv(_lib.stream_of(dev), 1, a.data_ptr(), w.data_ptr(), c.data_ptr(), _lib.ptr(r), M,
                                    N, K, mode, scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf,
@@ -62,6 +63,7 @@ def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0):
         torch.cuda.synchronize()
     finally:
         lib.dfd_set_tuning(b"stream_min_rows", prev)
+        lib.dfd_set_tuning(b"gemm_tile", prev_tile)
     ap = _pro(a, mode, scale, shift, gate, rpf).to(torch.bfloat16).float()
     ref = ap @ w.float().t()
     mag = ref.abs()
@@ -106,17 +108,23 @@ STREAM_CASES = [
 
 
 @pytest.mark.parametrize("case", STREAM_CASES, ids=lambda c: "x".join(map(str, c[:3])) + f"_m{c[3]}r{int(c[4])}")
-@pytest.mark.parametrize("path", ["stream", "tiled"])
+@pytest.mark.parametrize("path", ["stream", "tiled", "tiled128x128", "tiled128x64", "tiled64x64", "tiled32x64"])
 def test_pw_conv_bf16(cuda, case, path):
     M, N, K, mode, resid, stats = case
-    _run(M, N, K, mode, resid, stats, 0 if path == "stream" else 1 << 60, cuda, rpf=784 if M < 30000 else 3136)
+    tile = {"tiled128x128": 0, "tiled128x64": 1, "tiled64x64": 2, "tiled32x64": 3}.get(path, -1)
+    _run(M, N, K, mode, resid, stats, 0 if path == "stream" else 1 << 60, cuda, rpf=784 if M < 30000 else 3136,
+         tile=tile)
 
 
+# the tiled GEMM's shapes (late stages, 14x14 / 7x7 maps), every tile configuration
 @pytest.mark.parametrize("case", [(12544, 192, 1152, 2, False, True), (12544, 1152, 192, 0, False, True),
-                                  (12544, 1280, 320, 0, False, True), (12544, 320, 1280, 0, False, False)])
-def test_pw_conv_bf16_late_layers(cuda, case):
+                                  (12544, 1280, 320, 0, False, True), (12544, 320, 1280, 0, False, False),
+                                  (50176, 112, 672, 2, False, True), (50176, 80, 480, 0, True, False),
+                                  (3001, 200, 104, 1, False, True)])
+@pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3])
+def test_pw_conv_bf16_late_layers(cuda, case, tile):
     M, N, K, mode, resid, stats = case
-    _run(M, N, K, mode, resid, stats, 0, cuda, rpf=49)
+    _run(M, N, K, mode, resid, stats, 0, cuda, rpf=49, tile=tile)
 
 
 def test_pw_conv_rejects_bad_args(cuda):
