@@ -771,111 +771,149 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
 }
 
 // ------------------------------------------------------------------ SE excitation (per frame)
-// SE excitation, forward:  rpre = Wr sq + br ; r = silu(rpre) ; gate = sigmoid(We r + be)
-// (timm SqueezeExcite conv_reduce / act / conv_expand / sigmoid).  Per direction:
-//   reduce FC      frames x RD x C on the fp32 MFMA small GEMM (launch_mfma_small_gemm);
-//   se_gate_kernel one thread per (frame, channel): RD-long dot product with an LDS copy of r,
-//                  templated on the reduce width RD (4..48 in B0) so the accumulators are exact.
-template <int RD>
-__device__ __forceinline__ void block_sum_rd(float (&acc)[RD], float* red, float* out) {
+// timm SqueezeExcite conv_reduce / act / conv_expand / sigmoid on the per-frame channel means,
+// forward and input-gradient backward, as ONE launch each: two chained small GEMMs per tile of
+// 16 frames on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact products, fixed summation order):
+//   T[f][j]   = epi1( sum_c A[f][c] B1(c, j) )      j < rd  (the 16 waves split c; LDS sum in order)
+//   out[f][c] = epi2( sum_j T[f][j] B2(j, c) )      c in this workgroup's channel slice
+// forward  A = sq: B1(c,j) = Wr[j][c], T1 = rpre = . + br (saved), T = silu(rpre);
+//          B2(j,c) = We[c][j], out = gate = sigmoid(. + be)
+// backward A = de = dgate g (1-g): B1(c,j) = We[c][j], T = dz = . * silu'(rpre) (saved);
+//          B2(j,c) = Wr[j][c], out = bc = inv_hw * .   (the squeeze path's input gradient)
+// The channel slices (gridDim.y) recompute the small first product instead of a second launch.
+constexpr int SE_RDMAX = 48, SE_TS = SE_RDMAX + 4, SE_CSL = 256, SE_W = 16;  // SE_W waves per workgroup
+typedef float se_f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool FWD>
+__global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __restrict__ A, int frames, int C, int rd,
+                                                       const float* __restrict__ W1, const float* __restrict__ b1,
+                                                       const float* __restrict__ rpre_in,
+                                                       const float* __restrict__ W2, const float* __restrict__ b2,
+                                                       float scale2, float* __restrict__ t1_out,
+                                                       float* __restrict__ out) {
+  __shared__ float red[SE_W][3][4][64];
+  __shared__ float Ts[16][SE_TS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int f0 = blockIdx.x * 16;
+  const int nt1 = (rd + 15) / 16;
+  // ---- T = A[16 frames][C] . B1[C][rd] ----
+  se_f32x4 acc1[3];
 #pragma unroll
-  for (int j = 0; j < RD; ++j) {
-    const float v = wave_sum(acc[j]);
-    if (lane == 0) red[wave * RD + j] = v;
+  for (int t = 0; t < 3; ++t) acc1[t] = se_f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool fok = f0 + li < frames;
+  // 16 k per iteration; lane group lk takes k = k0 + 4 lk + u in MFMA step u (the same
+  // permutation on both operands), so the row-major operands load as 16-B vectors (C % 8 == 0)
+  for (int k0 = 16 * wave; k0 < C; k0 += 16 * SE_W) {
+    const int kq = k0 + 4 * lk;
+    const bool kok = kq < C;
+    float av[4], bv[4][3];
+    {
+      const float4 a4 = (fok && kok) ? *reinterpret_cast<const float4*>(A + (int64_t)(f0 + li) * C + kq)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int n = 16 * t + li;
+      const bool ok = t < nt1 && n < rd && kok;
+      if constexpr (FWD) {
+        const float4 b4 = ok ? *reinterpret_cast<const float4*>(W1 + (int64_t)n * C + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[0][t] = b4.x; bv[1][t] = b4.y; bv[2][t] = b4.z; bv[3][t] = b4.w;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bv[u][t] = ok ? W1[(int64_t)(kq + u) * rd + n] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+        if (t < nt1) acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u][t], acc1[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave][t][r][lane] = acc1[t][r];
+  __syncthreads();
+  // element (fl, j): MFMA D layout lane = 16 * (fl / 4) + j % 16, register fl % 4, tile j / 16
+  for (int e = tid; e < 16 * SE_TS; e += 64 * SE_W) {
+    const int fl = e / SE_TS, j = e - fl * SE_TS;
+    float tv = 0.f;
+    if (j < rd) {
+      const int t = j >> 4, ln = 16 * (fl >> 2) + (j & 15), r = fl & 3;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < SE_W; ++w) v += red[w][t][r][ln];
+      const int f = f0 + fl;
+      if (f < frames) {
+        if constexpr (FWD) {
+          v += b1[j];
+          if (blockIdx.y == 0) t1_out[(int64_t)f * rd + j] = v;
+          tv = siluf_(v);
+        } else {
+          v *= dsiluf_(rpre_in[(int64_t)f * rd + j]);
+          if (blockIdx.y == 0) t1_out[(int64_t)f * rd + j] = v;
+          tv = v;
+        }
+      }
+    }
+    Ts[fl][j] = tv;  // zero for j >= rd and for frames past the end
   }
   __syncthreads();
-  if (tid < RD) out[tid] = red[tid] + red[RD + tid] + red[2 * RD + tid] + red[3 * RD + tid];
-  __syncthreads();
-}
-
-template <int RD>
-__global__ __launch_bounds__(256) void se_gate_kernel(const float* __restrict__ rpre, const float* __restrict__ we,
-                                                      const float* __restrict__ be, int C, float* __restrict__ gate) {
-  __shared__ float s_r[RD];
-  const int f = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
-  if (threadIdx.x < RD) s_r[threadIdx.x] = siluf_(rpre[(int64_t)f * RD + threadIdx.x]);
-  __syncthreads();
-  if (c >= C) return;
-  const float* w = we + (int64_t)c * RD;
-  float a = be[c];
+  // ---- out = T[16][rd] . B2[rd][C slice] ----
+  const int cbeg = blockIdx.y * SE_CSL, cend = min(C, cbeg + SE_CSL);
+  for (int n0 = cbeg + 16 * wave; n0 < cend; n0 += 16 * SE_W) {
+    const int n = n0 + li;
+    const bool nok = n < cend;
+    se_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < rd; k0 += 4) {
+      const int k = k0 + lk;
+      const float a = Ts[li][k];
+      const bool ok = nok && k < rd;
+      const float b = ok ? (FWD ? W2[(int64_t)n * rd + k] : W2[(int64_t)k * C + n]) : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
 #pragma unroll
-  for (int j = 0; j < RD; ++j) a = fmaf(w[j], s_r[j], a);
-  gate[(int64_t)f * C + c] = sigmoidf_(a);
-}
-
-// backward:  de = dgate*g*(1-g) ; dz = (We^T de) * silu'(rpre) ; bc = (Wr^T dz) * inv_hw
-template <int RD>
-__global__ __launch_bounds__(256) void se_bc_kernel(const float* __restrict__ dz, const float* __restrict__ wr, int C,
-                                                    float inv_hw, float* __restrict__ bc_out) {
-  __shared__ float s_dz[RD];
-  const int f = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
-  if (threadIdx.x < RD) s_dz[threadIdx.x] = dz[(int64_t)f * RD + threadIdx.x];
-  __syncthreads();
-  if (c >= C) return;
-  float a = 0.f;
-#pragma unroll
-  for (int j = 0; j < RD; ++j) a = fmaf(wr[(int64_t)j * C + c], s_dz[j], a);
-  bc_out[(int64_t)f * C + c] = a * inv_hw;
-}
-
-template <int RD>
-static void se_fwd_launch(hipStream_t s, dim3 g2, int frames, const float* sq, const float* wr, const float* br,
-                          const float* we, const float* be, int C, float* rpre, float* gate) {
-  // rpre[f][j] = br[j] + sum_c sq[f][c] wr[j][c]   (frames x rd x C on fp32 MFMA)
-  (void)launch_mfma_small_gemm(s, sq, C, 1, wr, 1, C, rpre, RD, frames, RD, C, br, nullptr, nullptr, false, 0, 0u, 0.f, 0);
-  hipLaunchKernelGGL(se_gate_kernel<RD>, g2, dim3(256), 0, s, rpre, we, be, C, gate);
-}
-template <int RD>
-static void se_bwd_launch(hipStream_t s, dim3 g2, const float* dz, const float* wr, int C, float inv_hw, float* bc) {
-  hipLaunchKernelGGL(se_bc_kernel<RD>, g2, dim3(256), 0, s, dz, wr, C, inv_hw, bc);
-}
-
-#define DFD_SE_RD_SWITCH(RDV, CALL)                                                        \
-  switch (RDV) {                                                                           \
-    case 4: { constexpr int RD = 4; CALL; } break;                                         \
-    case 6: { constexpr int RD = 6; CALL; } break;                                         \
-    case 8: { constexpr int RD = 8; CALL; } break;                                         \
-    case 10: { constexpr int RD = 10; CALL; } break;                                       \
-    case 20: { constexpr int RD = 20; CALL; } break;                                       \
-    case 28: { constexpr int RD = 28; CALL; } break;                                       \
-    case 48: { constexpr int RD = 48; CALL; } break;                                       \
-    default: set_error("se: reduce width not instantiated", __FILE__, __LINE__); return -1; \
+    for (int r = 0; r < 4; ++r) {
+      const int f = f0 + 4 * lk + r;
+      if (f < frames && nok) {
+        const float v = FWD ? sigmoidf_(acc[r] + b2[n]) : acc[r] * scale2;
+        out[(int64_t)f * C + n] = v;
+      }
+    }
   }
+}
 
 int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
                      const float* be, int frames, int C, int rd, float* rpre, float* gate) {
-  const dim3 g2((unsigned)cdiv(C, 256), (unsigned)frames);
-  DFD_SE_RD_SWITCH(rd, se_fwd_launch<RD>(s, g2, frames, sq, wr, br, we, be, C, rpre, gate));
+  if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
+  const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
+  hipLaunchKernelGGL(se_chain_kernel<true>, grid, dim3(64 * SE_W), 0, s, sq, frames, C, rd, wr, br, nullptr, we, be, 1.f,
+                     rpre, gate);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
 
-// SE excitation backward from de = dgate * sigmoid'(.) (launch_se_bn_bwd_reduce), all on the fp32
-// MFMA small GEMM except the bc broadcast:
-//   dz[f][j]  = silu'(rpre[f][j]) sum_c de[f][c] we[c][j]
+// SE excitation backward from de = dgate * sigmoid'(.) (launch_se_bn_bwd_reduce):
+//   dz[f][j]  = silu'(rpre[f][j]) sum_c de[f][c] we[c][j],  bc[f][c] = inv_hw sum_j dz[f][j] wr[j][c]
+//                                                          (se_chain_kernel, one launch)
 //   gwe[c][j] = sum_f de[f][c] silu(rpre[f][j]),  gbe = sum_f de      (frames ascending)
-//   gwr[j][c] = sum_f dz[f][j] sq[f][c],          gbr = sum_f dz
-//   bc[f][c]  = inv_hw sum_j dz[f][j] wr[j][c]    (se_bc_kernel)
+//   gwr[j][c] = sum_f dz[f][j] sq[f][c],          gbr = sum_f dz      (one paired MFMA launch)
 int launch_se_fc_bwd(hipStream_t s, const float* de, const float* sq, const float* rpre, const float* wr,
                      const float* we, int frames, int C, int rd, float inv_hw, float* tmp_dz, float* bc_out,
                      float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
-  MfmaGemm g{};
-  g.A = de; g.sam = C; g.sak = 1; g.B = we; g.sbk = rd; g.sbn = 1; g.C = tmp_dz; g.ldc = rd;
-  g.M = frames; g.N = rd; g.K = C; g.dsilu_pre = rpre;
-  DFD_TRY(launch_mfma_small_gemm(s, g));
-  g = MfmaGemm{};
-  g.A = de; g.sam = 1; g.sak = C; g.B = rpre; g.sbk = rd; g.sbn = 1; g.b_silu = 1; g.C = gwe; g.ldc = rd;
-  g.M = C; g.N = rd; g.K = frames; g.asum = gbe; g.accumulate = accumulate;
-  DFD_TRY(launch_mfma_small_gemm(s, g));
-  g = MfmaGemm{};
-  g.A = tmp_dz; g.sam = 1; g.sak = rd; g.B = sq; g.sbk = C; g.sbn = 1; g.C = gwr; g.ldc = C;
-  g.M = rd; g.N = C; g.K = frames; g.asum = gbr; g.accumulate = accumulate;
-  DFD_TRY(launch_mfma_small_gemm(s, g));
-  const dim3 g2((unsigned)cdiv(C, 256), (unsigned)frames);
-  DFD_SE_RD_SWITCH(rd, se_bwd_launch<RD>(s, g2, tmp_dz, wr, C, inv_hw, bc_out));
+  if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
+  const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
+  hipLaunchKernelGGL(se_chain_kernel<false>, grid, dim3(64 * SE_W), 0, s, de, frames, C, rd, we, nullptr, rpre, wr,
+                     nullptr, inv_hw, tmp_dz, bc_out);
   DFD_HIP_CHECK(hipGetLastError());
-  return 0;
+  MfmaGemm ge{}, gr{};
+  ge.A = de; ge.sam = 1; ge.sak = C; ge.B = rpre; ge.sbk = rd; ge.sbn = 1; ge.b_silu = 1; ge.C = gwe; ge.ldc = rd;
+  ge.M = C; ge.N = rd; ge.K = frames; ge.asum = gbe; ge.accumulate = accumulate;
+  gr.A = tmp_dz; gr.sam = 1; gr.sak = rd; gr.B = sq; gr.sbk = C; gr.sbn = 1; gr.C = gwr; gr.ldc = C;
+  gr.M = rd; gr.N = C; gr.K = frames; gr.asum = gbr; gr.accumulate = accumulate;
+  return launch_mfma_small_gemm2(s, ge, gr);
 }
 
 // ------------------------------------------------------------------ slab reduce

@@ -137,11 +137,14 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
 typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MG_MAXW = 16;
 
-__global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a) {
+// two independent GEMMs of equal K may share one launch: workgroups [0, tiles0) run a0, the rest a1
+__global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a0, MfmaGemm a1, int tiles0) {
   __shared__ float red[MG_MAXW][5][64];
+  const bool second = (int)blockIdx.x >= tiles0;
+  const MfmaGemm& a = second ? a1 : a0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int tn = (a.N + 15) / 16;
-  const int tile = blockIdx.x;
+  const int tile = second ? (int)blockIdx.x - tiles0 : (int)blockIdx.x;
   const int m0 = (tile / tn) * 16, n0 = (tile % tn) * 16;
   const int li = lane & 15, lk = lane >> 4;
   const int m = m0 + li, n = n0 + li;
@@ -211,7 +214,18 @@ int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g) {
   const int tiles = cdiv(M, 16) * cdiv(N, 16);
   // waves per tile: enough K-splitting to put ~2 chunks on each wave, at most MG_MAXW
   const int nw = std::max(1, std::min(MG_MAXW, cdiv(K, 64)));
-  hipLaunchKernelGGL(mfma_small_gemm_kernel, dim3((unsigned)tiles), dim3(64 * nw), 0, s, g);
+  hipLaunchKernelGGL(mfma_small_gemm_kernel, dim3((unsigned)tiles), dim3(64 * nw), 0, s, g, g, tiles);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int launch_mfma_small_gemm2(hipStream_t s, const MfmaGemm& g0, const MfmaGemm& g1) {
+  if (g0.K != g1.K) { set_error("mfma_small_gemm2: the two products need the same K", __FILE__, __LINE__); return -1; }
+  const int t0 = (g0.M > 0 && g0.N > 0) ? cdiv(g0.M, 16) * cdiv(g0.N, 16) : 0;
+  const int t1 = (g1.M > 0 && g1.N > 0) ? cdiv(g1.M, 16) * cdiv(g1.N, 16) : 0;
+  if (t0 + t1 == 0) return 0;
+  const int nw = std::max(1, std::min(MG_MAXW, cdiv(g0.K, 64)));
+  hipLaunchKernelGGL(mfma_small_gemm_kernel, dim3((unsigned)(t0 + t1)), dim3(64 * nw), 0, s, g0, g1, t0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -143,6 +143,7 @@ struct MfmaGemm {
   uint64_t seed = 0; uint32_t stream = 0; float p = 0.f; int64_t drop_ld = 0;
 };
 int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g);
+int launch_mfma_small_gemm2(hipStream_t s, const MfmaGemm& g0, const MfmaGemm& g1);  // one launch, same K
 int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                            int64_t sbn, float* C, int64_t ldc, int M, int N, int K, const float* bias,
                            const float* dsilu_pre, float* asum, bool accumulate, uint64_t seed, uint32_t stream,

@@ -138,13 +138,23 @@ def test_detector_train_bf16_close(cuda, golden_dir, kernel_paths):
     assert abs(float(loss) - float(g["loss"])) <= 2e-2 * abs(float(g["loss"]))
     names = [str(n) for n in g["g_names"]]
     params = dict(det.named_parameters())
-    norms_ok = 0
+    # Parameters whose fp32 reference gradient is structurally zero (a BN bias feeding only
+    # shift-invariant consumers -- the next training-mode BN removes any per-channel constant)
+    # carry no signal: in bf16 they hold rounding residue. They are excluded from the count.
+    norms_ok, counted = 0, 0
+    bad = []
     for i, n in enumerate(names):
-        gr = params[n].grad.detach().double().flatten().cpu()
         ref_norm = float(g["g_norm"][i])
-        if ref_norm > 1e-6 and abs(float(gr.norm()) - ref_norm) <= 0.1 * ref_norm:
+        if ref_norm <= 1e-6:
+            continue
+        counted += 1
+        gr = params[n].grad.detach().double().flatten().cpu()
+        if abs(float(gr.norm()) - ref_norm) <= 0.1 * ref_norm:
             norms_ok += 1
-    assert norms_ok >= 0.9 * len(names), (norms_ok, len(names))
+        else:
+            bad.append((n, ref_norm, float(gr.norm())))
+    assert counted >= 0.85 * len(names), (counted, len(names))
+    assert norms_ok >= 0.9 * counted, (norms_ok, counted, bad)
 
 
 def test_detector_train_bf16_deterministic(cuda, golden_dir, kernel_paths):

@@ -146,6 +146,9 @@ int main(int argc, char** argv) {
     b.run("dw_dgrad", nm, dwb + 2.0 * Mi * C1, [&] {
       return launch_dw_dgrad<bf16>(b.s, g, A, W, C, B, &bi, stats, &rows);
     });
+    b.run("dw_bwd", nm, dwb + 2.0 * Mi * C1, [&] {
+      return launch_dw_bwd<bf16>(b.s, g, A, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
+    });
     b.run("dw_wgrad", nm, dwb, [&] {
       return launch_dw_wgrad<bf16>(b.s, g, A, B, pb, PRO_BN_SILU, slab, slab_cap, dW, false);
     });
