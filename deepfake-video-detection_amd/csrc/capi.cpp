@@ -268,12 +268,13 @@ static bool pw_args_ok(int dtype, int64_t M, int N, int K, int pro_mode, const f
                        const float* gate, int rows_per_frame) {
   if (dtype != DFD_DTYPE_F32 && dtype != DFD_DTYPE_BF16) { dfd::set_error("pw: bad dtype", __FILE__, __LINE__); return false; }
   if (M < 0 || N <= 0 || K <= 0) { dfd::set_error("pw: bad shape", __FILE__, __LINE__); return false; }
-  if (pro_mode != dfd::PRO_NONE && pro_mode != dfd::PRO_BN_SILU && pro_mode != dfd::PRO_BN_SILU_G) {
+  if (pro_mode != dfd::PRO_NONE && pro_mode != dfd::PRO_BN_SILU && pro_mode != dfd::PRO_BN_SILU_G &&
+      pro_mode != dfd::PRO_GATE) {
     dfd::set_error("pw: bad prologue mode", __FILE__, __LINE__);
     return false;
   }
-  if (pro_mode != dfd::PRO_NONE && (!scale || !shift)) { dfd::set_error("pw: scale/shift missing", __FILE__, __LINE__); return false; }
-  if (pro_mode == dfd::PRO_BN_SILU_G && (!gate || rows_per_frame <= 0)) {
+  if (dfd::pro_is_bn(pro_mode) && (!scale || !shift)) { dfd::set_error("pw: scale/shift missing", __FILE__, __LINE__); return false; }
+  if (dfd::pro_is_gated(pro_mode) && (!gate || rows_per_frame <= 0)) {
     dfd::set_error("pw: gate / rows_per_frame missing", __FILE__, __LINE__);
     return false;
   }

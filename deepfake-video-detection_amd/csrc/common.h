@@ -154,7 +154,9 @@ __host__ __device__ __forceinline__ int64_t cdiv64(int64_t a, int64_t b) { retur
 //   PRO_BN_SILU   a = silu(y*scale[c] + shift[c])
 //   PRO_BN_SILU_G a = silu(y*scale[c] + shift[c]) * gate[frame][c]
 //   PRO_GELU      a = gelu(y)   (exact erf form; ViT MLP, no per-channel parameters)
-enum ProMode { PRO_NONE = 0, PRO_BN_SILU = 1, PRO_BN_SILU_G = 2, PRO_GELU = 3 };
+//   PRO_GATE      a = y * gate[frame][c]   (y already activated: a materialised silu(bn(.)))
+enum ProMode { PRO_NONE = 0, PRO_BN_SILU = 1, PRO_BN_SILU_G = 2, PRO_GELU = 3, PRO_GATE = 4 };
+constexpr bool pro_is_gated(int mode) { return mode == PRO_BN_SILU_G || mode == PRO_GATE; }
 constexpr bool pro_is_bn(int mode) { return mode == PRO_BN_SILU || mode == PRO_BN_SILU_G; }
 
 // torch.nn.functional.gelu (approximate='none'): 0.5 x (1 + erf(x / sqrt 2)) and its derivative

@@ -349,11 +349,13 @@ int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const floa
 // ------------------------------------------------------------------ per-frame channel sums
 // part[h][f][c] = sum over pixel chunk h of frame f of val(p, c), where
 //   SQUEEZE: val = silu(y*scale+shift);   SEBWD: val = dZ * silu(y*scale+shift)
+// SQUEEZE with s_out also stores silu(y*scale+shift) (rounded to T): the materialised activation
+// the late-stage conv_pwl forward and weight gradient read instead of recomputing it per N tile.
 // grid (frames*hsplit, groups); threads: vec = tid % vpg, pl = tid / vpg
 template <typename T, bool SEBWD>
 __global__ __launch_bounds__(256) void frame_sum_kernel(const T* __restrict__ dZ, const T* __restrict__ Y, Pro pro,
                                                         int frames, int HW, int C, int hsplit, int vpg,
-                                                        float* __restrict__ part) {
+                                                        float* __restrict__ part, T* __restrict__ s_out) {
   __shared__ float sh[256][8];
   const int tid = threadIdx.x;
   const int vec = tid % vpg, pl = tid / vpg, npl = 256 / vpg;
@@ -374,6 +376,7 @@ __global__ __launch_bounds__(256) void frame_sum_kernel(const T* __restrict__ dZ
       ld8(Y + row * C + c, y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) y[j] = siluf_(y[j] * sc[j] + shf[j]);
+      if (!SEBWD && s_out) st8(s_out + row * C + c, y);
       if constexpr (SEBWD) {
         float d[8];
         ld8(dZ + row * C + c, d);
@@ -399,7 +402,7 @@ __global__ __launch_bounds__(256) void frame_sum_kernel(const T* __restrict__ dZ
 
 template <typename T, bool SEBWD>
 static int launch_frame_sum(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
-                            float* part, int64_t part_cap, int* hsplit_out) {
+                            float* part, int64_t part_cap, int* hsplit_out, T* s_out = nullptr) {
   int vpg, groups;
   bn_vpg_groups(C, vpg, groups);
   const int npl = 256 / vpg;
@@ -408,7 +411,7 @@ static int launch_frame_sum(hipStream_t s, const T* dZ, const T* Y, const Pro& p
          (int64_t)(hsplit * 2) * frames * C <= part_cap)
     hsplit *= 2;
   hipLaunchKernelGGL((frame_sum_kernel<T, SEBWD>), dim3(frames * hsplit, groups), dim3(256), 0, s, dZ, Y, pro, frames,
-                     HW, C, hsplit, vpg, part);
+                     HW, C, hsplit, vpg, part, s_out);
   DFD_HIP_CHECK(hipGetLastError());
   *hsplit_out = hsplit;
   return 0;
@@ -426,9 +429,9 @@ __global__ void sum_parts_kernel(const float* __restrict__ part, int hsplit, int
 
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
-                      int64_t part_cap, float* sq) {
+                      int64_t part_cap, float* sq, T* s_out) {
   int hs;
-  if (launch_frame_sum<T, false>(s, nullptr, Y, pro, frames, HW, C, part, part_cap, &hs)) return -1;
+  if (launch_frame_sum<T, false>(s, nullptr, Y, pro, frames, HW, C, part, part_cap, &hs, s_out)) return -1;
   const int64_t n = (int64_t)frames * C;
   hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, part, hs, n, 1.0f / (float)HW, sq);
   DFD_HIP_CHECK(hipGetLastError());
@@ -762,7 +765,7 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
   int vpg, groups;
   bn_vpg_groups(C, vpg, groups);
   hipLaunchKernelGGL((frame_sum_kernel<T, false>), dim3(frames, groups), dim3(256), 0, s, (const T*)nullptr, Y, pro,
-                     frames, HW, C, 1, vpg, feat);
+                     frames, HW, C, 1, vpg, feat, (T*)nullptr);
   DFD_HIP_CHECK(hipGetLastError());
   const int64_t n = (int64_t)frames * C;
   hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, feat, 1, n, 1.0f / (float)HW, feat);
@@ -951,7 +954,7 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
   template int launch_bn_apply<T>(hipStream_t, const T*, const float*, const float*, const T*, T*, int64_t, int);    \
   template int launch_bn_bwd_reduce<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, float*, int*);          \
   template int launch_bn_bwd_apply<T>(hipStream_t, const BnBwdIn&, const T*, const float*, T*, int64_t, int);       \
-  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, float*);     \
+  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, float*, T*); \
   template int launch_se_bwd_reduce<T>(hipStream_t, const T*, const T*, const Pro&, int, int, int, float*, int64_t, \
                                        float*);                                                                     \
   template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);                            \

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
   using G = GemmCfg<T, BM, BN, WN, D, BK>;
   constexpr int GBK = BK;
   constexpr int WM = G::WM, RB = G::RB, CB = G::CB, PA = G::PA, PB = G::PB;
-  constexpr bool GATE = MODE == PRO_BN_SILU_G;
+  constexpr bool GATE = pro_is_gated(MODE);
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   __shared__ float st_sum[BN];
   __shared__ float st_sq[BN];
@@ -148,6 +148,12 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
             raw_to_f(ra[d][i], x);
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);  // masked lanes hold 0 and gelu(0) = 0
+            lds_st8(As + row * G::AS + skc, x);
+          } else if constexpr (MODE == PRO_GATE) {
+            float x[8];
+            raw_to_f(ra[d][i], x);  // masked lanes hold 0
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] *= pg[d][i][j];
             lds_st8(As + row * G::AS + skc, x);
           } else {
             float x[8], psc[8], psh[8];
@@ -317,7 +323,7 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   const int64_t cap = std::max<int64_t>(1, 1024 / ntn);  // <= 1024 BN-stat partial rows (plan's stats buffer)
   const int gx = (int)std::min<int64_t>(tiles_m, cap);
   constexpr int DW = sizeof(T) == 4 ? 1 : 0;  // fp32 (parity mode): shallower ring, no spills
-  constexpr int O64 = (MODE == PRO_BN_SILU_G || sizeof(T) == 4) ? 2 : 4;
+  constexpr int O64 = (pro_is_gated(MODE) || sizeof(T) == 4) ? 2 : 4;
   if (cfg == 0) gemm_go<T, MODE, ST, EP, 128, 128, 1, 2 - DW, 32, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   else if (cfg == 1) gemm_go<T, MODE, ST, EP, 128, 64, 1, 3 - DW, 32, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   else if (cfg == 2) gemm_go<T, MODE, ST, EP, 64, 64, 2, 3, 32, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
@@ -349,6 +355,8 @@ static int gemm_dispatch(hipStream_t s, const T* A, const T* B, T* C, const T* R
     if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU, true, 0); else DFD_GEMM_LAUNCH(PRO_BN_SILU, false, 0);
   } else if (pro_mode == PRO_BN_SILU_G && epi == 0) {
     if (st) DFD_GEMM_LAUNCH(PRO_BN_SILU_G, true, 0); else DFD_GEMM_LAUNCH(PRO_BN_SILU_G, false, 0);
+  } else if (pro_mode == PRO_GATE && epi == 0) {
+    if (st) DFD_GEMM_LAUNCH(PRO_GATE, true, 0); else DFD_GEMM_LAUNCH(PRO_GATE, false, 0);
   } else if (pro_mode == PRO_NONE && epi == EPI_BIAS && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_BIAS);
   else if (pro_mode == PRO_NONE && epi == (EPI_BIAS | EPI_RESID) && !st) DFD_GEMM_LAUNCH(PRO_NONE, false, EPI_BIAS | EPI_RESID);
   else if (pro_mode == PRO_GELU && epi == (EPI_BIAS | EPI_RESID) && !st) DFD_GEMM_LAUNCH(PRO_GELU, false, EPI_BIAS | EPI_RESID);
@@ -408,7 +416,7 @@ template <typename T> struct WgCfg {
 };
 
 template <typename T, int MODE>
-__global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 : 2) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 2) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
                                                        int N, int K, Pro pro, float* __restrict__ slab, int tnk,
                                                        int64_t m_per_split) {
   using G = WgCfg<T>;
@@ -432,7 +440,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
     ld8f(pro.shift + kc, sh);
   }
   Raw8<T> ry[4], rx[4];
-  float rg[MODE == PRO_BN_SILU_G ? 4 : 1][8];
+  float rg[pro_is_gated(MODE) ? 4 : 1][8];
   auto load = [&](int64_t ms) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -440,7 +448,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
       const bool ok = gm < mend;
       raw_ld(ry[i], dY + gm * N + n0 + cv, dY, ok && yc);
       raw_ld(rx[i], X + gm * K + k0 + cv, X, ok && xc);
-      if constexpr (MODE == PRO_BN_SILU_G) {
+      if constexpr (pro_is_gated(MODE)) {
         const uint32_t f = (uint32_t)(ok ? gm : mbeg) / (uint32_t)pro.rows_per_frame;
         ld8f(pro.gate + (int64_t)f * pro.C + kc, rg[i]);
       }
@@ -468,6 +476,9 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && MODE != PRO_BN_SILU_G) ? 3 
         if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * rg[i][j];
+        } else if constexpr (MODE == PRO_GATE) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] *= rg[i][j];
         } else if constexpr (MODE == PRO_GELU) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);
@@ -572,6 +583,8 @@ int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, in
     hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
   else if (pro_mode == PRO_GELU)
     hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_GELU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
+  else if (pro_mode == PRO_GATE)
+    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_GATE>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
   else
     hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU_G>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
   DFD_HIP_CHECK(hipGetLastError());

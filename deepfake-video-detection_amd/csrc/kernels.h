@@ -97,7 +97,7 @@ int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const floa
 // SE squeeze: sq[f][c] = mean_hw pro(Y)   (pro = BN+SiLU)
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
-                      int64_t part_cap, float* sq);
+                      int64_t part_cap, float* sq, T* s_out);  // s_out: optional materialised silu(bn(Y))
 // SE excitation: r = silu(Wr sq + br) ; gate = sigmoid(We r + be) ; saves rpre
 int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
                      const float* be, int frames, int C, int rd, float* rpre, float* gate);

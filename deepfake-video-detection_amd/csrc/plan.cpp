@@ -23,6 +23,7 @@ struct ArchRow {
 const ArchRow kArch[7] = {{1, 1, 3, 1, 1, 16},  {0, 2, 3, 2, 6, 24},  {0, 2, 5, 2, 6, 40},  {0, 3, 3, 2, 6, 80},
                           {0, 3, 5, 1, 6, 112}, {0, 4, 5, 2, 6, 192}, {0, 1, 3, 1, 6, 320}};
 constexpr int kStem = 32, kHead = 1280;
+constexpr int64_t kMaterialiseRows = 20000;  // the 7x7 stages (see Block::o_s2)
 
 struct Topo {
   std::vector<TensorSpec> t;
@@ -160,6 +161,10 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
     b.o_sq = alloc(F * b.mid * 4);
     b.o_rpre = alloc(F * b.rd * 4);
     b.o_gate = alloc(F * b.mid * 4);
+    // below the streaming threshold conv_pwl runs on the tiled GEMMs, which would recompute the
+    // BN+SiLU prologue once per N tile (forward) and per N tile of the weight gradient: the SE
+    // squeeze writes the activation once instead (+1 write of the tensor)
+    b.o_s2 = Mout < kMaterialiseRows ? alloc(Mout * b.mid * es) : -1;
     maxX = std::max({maxX, Min * b.cin, Mout * b.cout});
     maxS = std::max(maxS, Mout * b.cout);
     if (!b.ds) maxE1 = std::max(maxE1, Min * b.mid);
@@ -336,13 +341,14 @@ int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, cons
                                               r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU, stats, &rows)));
     }
     DFD_TRY(fin(bn_dw, Mout));
+    T* s2 = b.o_s2 >= 0 ? r.a(b.o_s2) : nullptr;
     PROBED(PK_SE_SQUEEZE, &b, (launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
-                                                    r.f(p.o_part), p.part_cap, r.f(b.o_sq))));
+                                                    r.f(p.o_part), p.part_cap, r.f(b.o_sq), s2)));
     DFD_TRY(launch_se_fc_fwd(s, r.f(b.o_sq), r.prm(b.t_se_wr), r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be),
                              p.frames, b.mid, b.rd, r.f(b.o_rpre), r.f(b.o_gate)));
-    PROBED(PK_PWL_FWD, &b, (launch_pw_gemm<T>(s, r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout, b.cout,
-                                              b.mid, PRO_BN_SILU_G, r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats,
-                                              &rows)));
+    PROBED(PK_PWL_FWD, &b, (launch_pw_gemm<T>(s, s2 ? s2 : r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout,
+                                              b.cout, b.mid, s2 ? PRO_GATE : PRO_BN_SILU_G,
+                                              r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats, &rows)));
     DFD_TRY(fin(b.bn3, Mout));
     DFD_TRY(launch_bn_apply<T>(s, r.a(b.o_y3), r.f(b.bn3.o_scale), r.f(b.bn3.o_shift), b.skip ? xin : nullptr,
                                r.a(b.o_x), Mout, b.cout));
@@ -412,7 +418,9 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
         PROBED(PK_PWL_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout,
                                                     b.mid, b.cout, PRO_NONE, Pro{}, nullptr, nullptr)));
-        PROBED(PK_PWL_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(b.o_y2), Mout, b.cout, b.mid, PRO_BN_SILU_G,
+        const bool mat = b.o_s2 >= 0;
+        PROBED(PK_PWL_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_gs), mat ? r.a(b.o_s2) : r.a(b.o_y2), Mout, b.cout,
+                                                     b.mid, mat ? PRO_GATE : PRO_BN_SILU_G,
                                                      r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), r.f(p.o_slab), p.slab_cap,
                                                      grad(b.pwl.t_w), acc != 0)));
         // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE

@@ -40,6 +40,7 @@ struct Block {
   int t_dw, t_se_wr, t_se_br, t_se_we, t_se_be;
   // workspace byte offsets of saved tensors
   int64_t o_y1, o_y2, o_y3, o_x, o_sq, o_rpre, o_gate;
+  int64_t o_s2;  // materialised silu(bn2(y2)) for the late stages (-1: conv_pwl recomputes it)
 };
 
 // Live timing of one launch site inside the plan (HIP events; created when armed, never on the

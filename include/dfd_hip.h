@@ -139,7 +139,8 @@ DFD_API int64_t dfd_set_tuning(const char* key, int64_t value);
  * run it inside self.backbone(x_flat) (src/pretrained_detector.py:116), with the producing
  * layer's BatchNorm+SiLU (+ squeeze-excite gate) applied to the input on the fly:
  *   C[M][N] = pro(A)[M][K] . W[N][K]^T (+ R[M][N])
- *   pro_mode 0: a = x;  1: a = silu(x*scale[k] + shift[k]);  2: the same times gate[m / rows_per_frame][k].
+ *   pro_mode 0: a = x;  1: a = silu(x*scale[k] + shift[k]);  2: the same times gate[m / rows_per_frame][k];
+ *   4: a = x * gate[m / rows_per_frame][k] (x already activated).
  * dtype DFD_DTYPE_F32 (fp32 storage) or DFD_DTYPE_BF16 (bf16 storage); fp32 accumulation; N, K
  * multiples of 8.  stats (optional, R must then be NULL): per-column partial sums of C and C^2 in
  * rows [*stat_rows][2][N] (room for 1024*2*N floats).  Used by the trunk and the kernel tests. */

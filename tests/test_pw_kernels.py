@@ -26,6 +26,9 @@ def _pro(a, mode, scale, shift, gate, rpf):
     x = a.float()
     if mode == 0:
         return x
+    if mode == 4:  # already-activated input times the SE gate
+        f = torch.arange(x.shape[0], device=x.device) // rpf
+        return x * gate[f]
     x = torch.nn.functional.silu(x * scale + shift)
     if mode == 2:
         f = torch.arange(x.shape[0], device=x.device) // rpf
@@ -120,6 +123,7 @@ def test_pw_conv_bf16(cuda, case, path):
 @pytest.mark.parametrize("case", [(12544, 192, 1152, 2, False, True), (12544, 1152, 192, 0, False, True),
                                   (12544, 1280, 320, 0, False, True), (12544, 320, 1280, 0, False, False),
                                   (50176, 112, 672, 2, False, True), (50176, 80, 480, 0, True, False),
+                                  (12544, 192, 1152, 4, False, True), (50176, 112, 672, 4, False, True),
                                   (3001, 200, 104, 1, False, True)])
 @pytest.mark.parametrize("tile", [-1, 0, 1, 2, 3])
 def test_pw_conv_bf16_late_layers(cuda, case, tile):
@@ -179,6 +183,14 @@ WGRAD_CASES = [
 def test_pw_conv_wgrad_bf16(cuda, case, path):
     M, N, K, mode = case
     _run_wgrad(M, N, K, mode, 0 if path == "stream" else 1 << 60, cuda, rpf=784 if M < 30000 else 3136)
+
+
+@pytest.mark.parametrize("case", [(12544, 192, 1152, 4), (50176, 80, 480, 4), (3001, 40, 240, 4)],
+                         ids=lambda c: "x".join(map(str, c)))
+def test_pw_conv_wgrad_gate_bf16(cuda, case):
+    """conv_pwl weight gradient on the materialised activation (mode 4: x * gate)."""
+    M, N, K, mode = case
+    _run_wgrad(M, N, K, mode, 0, cuda, rpf=49 if M < 20000 else 196)
 
 
 def test_pw_conv_wgrad_accumulate(cuda):
