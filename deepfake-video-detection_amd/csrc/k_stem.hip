@@ -221,13 +221,134 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float
   }
 }
 
+// bf16 mode: the same weight gradient as a GEMM on v_mfma_f32_16x16x32_bf16 --
+// dW[co][tap] = sum_p dY[p][co] * patch[p][tap], K = pixels.  Per 16x16-pixel tile the dY tile
+// ([pix][co], 16-B row writes) and the im2col tile ([pix][tap], 27 taps padded to 32, bf16 as the
+// bf16 conv consumes its input) are staged in LDS; each wave takes 32-pixel k-steps and reads both
+// operands as columns with ds_read_b64_tr_b16 (the pw_wgrad_kernel pattern): per pixel the LDS
+// traffic is 27 reads + 4 writes instead of 28 reads per (pixel, channel) of the FMA kernel.
+constexpr int SWL = 40;  // LDS row stride (bf16) of the [pix][32] operand tiles
+typedef short stw_bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short stw_s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) stw_s16x4_t stw_lds_s16x4_t;
+typedef float stw_f32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, const float* __restrict__ x,
+                                                              const bf16* __restrict__ dY, float* __restrict__ slab,
+                                                              int64_t ntiles) {
+  __shared__ float tin[SNIN];
+  __shared__ __attribute__((aligned(16))) bf16 ys[ST * ST * SWL];  // dY tile [pix][co]; reused for the reduction
+  __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col tile [pix][tap]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
+  stw_f32x4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = stw_f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float nx[SNLD];
+  uint32_t nxok = 0u;
+  Raw8<bf16> nd[4];  // 256 px x 4 vectors / 256 threads
+  auto load = [&](int64_t t) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
+    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nx, nxok);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
+      const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
+      raw_ld(nd[i], dY + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8, dY, oy < g.Ho && ox < g.Wo);
+    }
+  };
+  const int gq = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  int64_t t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+    lds_barrier();
+    stem_store(tin, nx, nxok);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
+      raw_st(ys + pix * SWL + v * 8, nd[i]);  // masked pixels store zeros
+    }
+    lds_barrier();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);
+    {  // im2col: thread = output pixel of the tile, 27 taps (+5 zero pads) as 4 x 16 B
+      const int ly = tid / ST, lx = tid % ST;
+      float v[32];
+#pragma unroll
+      for (int tap = 0; tap < 32; ++tap) {
+        if (tap < 27) {
+          const int ci = tap / 9, kh = (tap % 9) / 3, kw = tap % 3;
+          v[tap] = tin[((ly * 2 + kh) * SIE + lx * 2 + kw) * 3 + ci];
+        } else {
+          v[tap] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float w8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w8[j] = v[8 * c + j];
+        st8(xs + tid * SWL + 8 * c, w8);
+      }
+    }
+    lds_barrier();
+    // this wave's two 32-pixel k-steps: D[co][tap] += dY^T . patches
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p0 = (wave * 2 + ks) * 32;
+      stw_bf16x8_t bfr[2], afr[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const stw_s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (stw_lds_s16x4_t*)(xs + (p0 + 8 * gq + q) * SWL + b * 16 + 4 * pq));
+        const stw_s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (stw_lds_s16x4_t*)(xs + (p0 + 8 * gq + 4 + q) * SWL + b * 16 + 4 * pq));
+        bfr[b] = stw_bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const stw_s16x4_t alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (stw_lds_s16x4_t*)(ys + (p0 + 8 * gq + q) * SWL + b * 16 + 4 * pq));
+        const stw_s16x4_t ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (stw_lds_s16x4_t*)(ys + (p0 + 8 * gq + 4 + q) * SWL + b * 16 + 4 * pq));
+        afr[b] = stw_bf16x8_t{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[a], bfr[b], acc[a][b], 0, 0, 0);
+    }
+  }
+  // ---- the 4 waves' 32x32 partials in a fixed order into this workgroup's slab row ----
+  lds_barrier();
+  float* red = reinterpret_cast<float*>(ys);  // [4][32 co][32 tap] = 16 KB <= 20 KB
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = a * 16 + 4 * (lane >> 4) + r, tap = b * 16 + (lane & 15);
+        red[(wave * 32 + co) * 32 + tap] = acc[a][b][r];
+      }
+  lds_barrier();
+  float* out = slab + (int64_t)blockIdx.x * 27 * SCO;
+  for (int i = tid; i < 27 * SCO; i += 256) {
+    const int co = i / 27, tap = i % 27;
+    out[i] = ((red[(0 * 32 + co) * 32 + tap] + red[(1 * 32 + co) * 32 + tap]) + red[(2 * 32 + co) * 32 + tap]) +
+             red[(3 * 32 + co) * 32 + tap];
+  }
+}
+
 template <typename T>
 int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const float* x, const T* dY, float* slab, int64_t slab_cap,
                       float* dW, bool accumulate) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
   int gx = (int)std::min<int64_t>(ntiles, 1024);
   gx = (int)std::max<int64_t>(1, std::min<int64_t>(gx, slab_cap / (27 * SCO)));
-  hipLaunchKernelGGL((stem_wgrad_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, slab, ntiles);
+  if constexpr (sizeof(T) == 2)
+    hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, dY, slab, ntiles);
+  else  // fp32 parity mode: exact fp32 products
+    hipLaunchKernelGGL((stem_wgrad_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, slab, ntiles);
   DFD_HIP_CHECK(hipGetLastError());
   return launch_reduce_slabs(s, slab, gx, 27 * SCO, dW, accumulate);
 }
