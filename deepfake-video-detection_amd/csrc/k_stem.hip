@@ -141,20 +141,6 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const floa
   }
 }
 
-template <typename T>
-int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const float* w, T* Y, float* stats,
-                    int* stat_rows) {
-  const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
-  const int gx = (int)std::min<int64_t>(ntiles, 1024);
-  if (stats)
-    hipLaunchKernelGGL((stem_fwd_kernel<T, true>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
-  else
-    hipLaunchKernelGGL((stem_fwd_kernel<T, false>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
-  DFD_HIP_CHECK(hipGetLastError());
-  if (stat_rows) *stat_rows = gx;
-  return 0;
-}
-
 // dW[co][ci][kh][kw] = sum dY[f,oy,ox,co] * x[f,ci,2oy-1+kh,2ox-1+kw]
 // thread (co = tid & 31, sub = tid >> 5) accumulates all 27 taps over pixels p = sub (mod 8);
 // the next tile's input and dY are loaded into registers while the current tile is reduced.
@@ -337,6 +323,157 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
     out[i] = ((red[(0 * 32 + co) * 32 + tap] + red[(1 * 32 + co) * 32 + tap]) + red[(2 * 32 + co) * 32 + tap]) +
              red[(3 * 32 + co) * 32 + tap];
   }
+}
+
+// bf16 mode forward on v_mfma_f32_16x16x32_bf16: the 27 taps (+5 zero pads) are ONE 32-deep
+// k-step, so per 16-pixel block and 16 output channels a single MFMA computes the transposed
+// tile D[co][pix] = W[co][:] . patch[pix][:] (lanes then hold 4 consecutive channels of one
+// pixel).  Per 16x16 tile: fp32 input + halo -> LDS (as the FMA kernel), im2col as bf16 rows
+// (thread = pixel), 8 MFMAs per wave, rounded tile through an LDS slab for 16-B row stores,
+// BN-stat partials from the rounded values (per lane, fixed-order reduction at the end).
+constexpr int SFC = SCO + 8;  // LDS row stride (bf16) of the output slab
+__global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const float* __restrict__ x,
+                                                            const float* __restrict__ w, bf16* __restrict__ Y,
+                                                            float* __restrict__ stats, int64_t ntiles) {
+  __shared__ float tin[SNIN];
+  __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col [pix][tap]
+  __shared__ __attribute__((aligned(16))) bf16 ct[ST * ST * SFC];  // output slab [pix][co]
+  __shared__ __attribute__((aligned(16))) bf16 wsb[SCO * SWL];     // weights [co][tap]
+  __shared__ float red[2][4][SCO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < SCO * 32; i += 256) {
+    const int co = i / 32, tap = i % 32;  // w[co][ci][kh][kw], tap = ci*9 + kh*3 + kw
+    wsb[co * SWL + tap] = Tr<bf16>::from_f(tap < 27 ? w[co * 27 + tap] : 0.f);
+  }
+  lds_barrier();
+  stw_bf16x8_t wf[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+    wf[a] = *reinterpret_cast<const stw_bf16x8_t*>(wsb + (a * 16 + (lane & 15)) * SWL + 8 * (lane >> 4));
+  const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
+  const bool stats_on = stats != nullptr;
+  float s_acc[2][4], q_acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s_acc[a][r] = 0.f; q_acc[a][r] = 0.f; }
+  float nxt[SNLD];
+  uint32_t nok = 0u;
+  int64_t t = blockIdx.x;
+  if (t < ntiles) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
+    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nxt, nok);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
+    lds_barrier();
+    stem_store(tin, nxt, nok);
+    lds_barrier();
+    if (t + gridDim.x < ntiles) {  // next tile in flight during this tile's math and stores
+      int f2, oy2, ox2;
+      tl.coords(t + gridDim.x, f2, oy2, ox2);
+      stem_load(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nxt, nok);
+    }
+    {  // im2col: thread = output pixel, 27 taps + 5 zero pads as 4 x 16 B
+      const int ly = tid / ST, lx = tid % ST;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float w8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int tap = 8 * c + j;
+          if (tap < 27) {
+            const int ci = tap / 9, kh = (tap % 9) / 3, kw = tap % 3;
+            w8[j] = tin[((ly * 2 + kh) * SIE + lx * 2 + kw) * 3 + ci];
+          } else {
+            w8[j] = 0.f;
+          }
+        }
+        st8(xs + tid * SWL + 8 * c, w8);
+      }
+    }
+    lds_barrier();
+    // this wave's 4 blocks of 16 pixels x 2 blocks of 16 channels
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+      const int p0 = (wave * 4 + pb) * 16;
+      const stw_bf16x8_t pf = *reinterpret_cast<const stw_bf16x8_t*>(xs + (p0 + (lane & 15)) * SWL + 8 * (lane >> 4));
+      const int pix = p0 + (lane & 15);
+      const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
+      const bool ok = oy < g.Ho && ox < g.Wo;
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        stw_f32x4_t d = {0.f, 0.f, 0.f, 0.f};
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], pf, d, 0, 0, 0);
+        const uint2 pk = make_uint2(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]));
+        if (stats_on) {
+          const float v[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                              __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float vv = ok ? v[r] : 0.f;
+            s_acc[a][r] += vv;
+            q_acc[a][r] += vv * vv;
+          }
+        }
+        *reinterpret_cast<uint2*>(ct + pix * SFC + a * 16 + 4 * (lane >> 4)) = pk;
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // 256 px x 4 vectors of 8 channels
+      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
+      const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
+      if (oy < g.Ho && ox < g.Wo)
+        *reinterpret_cast<uint4*>(Y + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8) =
+            *reinterpret_cast<const uint4*>(ct + pix * SFC + v * 8);
+    }
+  }
+  if (stats_on) {
+    // lanes with equal lane >> 4 hold the same 4 channels (per a): shuffles over lane & 15, then
+    // the 4 waves in order through LDS
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sv = s_acc[a][r], qv = q_acc[a][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          sv += __shfl_xor(sv, o, 64);
+          qv += __shfl_xor(qv, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          red[0][wave][a * 16 + 4 * (lane >> 4) + r] = sv;
+          red[1][wave][a * 16 + 4 * (lane >> 4) + r] = qv;
+        }
+      }
+    lds_barrier();
+    if (tid < 2 * SCO) {
+      const int which = tid / SCO, c = tid % SCO;
+      stats[((int64_t)blockIdx.x * 2 + which) * SCO + c] =
+          ((red[which][0][c] + red[which][1][c]) + red[which][2][c]) + red[which][3][c];
+    }
+  }
+}
+
+template <typename T>
+int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const float* w, T* Y, float* stats,
+                    int* stat_rows) {
+  const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
+  const int gx = (int)std::min<int64_t>(ntiles, 1024);
+  if constexpr (sizeof(T) == 2) {
+    hipLaunchKernelGGL(stem_fwd_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+  } else {  // fp32 parity mode: exact fp32 products
+    if (stats)
+      hipLaunchKernelGGL((stem_fwd_kernel<T, true>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+    else
+      hipLaunchKernelGGL((stem_fwd_kernel<T, false>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+  }
+  DFD_HIP_CHECK(hipGetLastError());
+  if (stat_rows) *stat_rows = gx;
+  return 0;
 }
 
 template <typename T>
