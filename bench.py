@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="kernel-selection knob for A/B runs (dfd_set_tuning), e.g. dw_bwd_pre=2")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,6 +96,12 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    if args.tune:
+        from deepfake_amd import _lib
+        lib = _lib.load()
+        for kv in args.tune:
+            k, v = kv.split("=", 1)
+            lib.dfd_set_tuning(k.encode(), int(v))
     torch.manual_seed(0)
     model = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.5,
                                        compute_dtype=args.dtype)
