@@ -25,3 +25,15 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
     step(x, y)
     torch.cuda.synchronize()
 print(prof.key_averages().table(sort_by="count", row_limit=25))
+print("copy-like events:")
+for e in prof.key_averages():
+    k = e.key.lower()
+    if "copy" in k or "memcpy" in k or "memset" in k:
+        print(f"  {e.key[:80]:80s} count {e.count}")
+ev = prof.events()
+names = [e.name for e in ev]
+for i, e in enumerate(ev):
+    if "memcpy" in e.name.lower() or "copybuffer" in e.name.lower():
+        ctx = [x.name[:40] for x in ev[max(0, i - 3):i]]
+        print("  context:", ctx, "->", e.name[:60])
+        break
