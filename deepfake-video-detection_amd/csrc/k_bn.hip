@@ -920,32 +920,105 @@ int launch_se_fc_bwd(hipStream_t s, const float* de, const float* sq, const floa
 }
 
 // ------------------------------------------------------------------ slab reduce
-// out[i] (+)= sum_s slab[s][i]; block = 64 consecutive elements x 16 split lanes (fixed order)
+// out[i] (+)= sum_s slab[s][i]: a workgroup owns 256 consecutive elements (64 lanes x 4, 16-B loads
+// when the row stride allows) x SL split lanes; lane sl adds rows sl, sl+SL, ... in order, then
+// the SL lanes are added in order through LDS (deterministic, fixed for a given SL).
+constexpr int RS_MAXSL = 16;
+__device__ __forceinline__ void reduce_cols(const float* __restrict__ slab, int splits, int64_t n, int64_t stride,
+                                            float* out, int accumulate, int64_t blk, float (*sh)[64][4]) {
+  const int tid = threadIdx.x, il = tid & 63, sl = tid >> 6, nsl = blockDim.x >> 6;
+  const int64_t e = (blk * 64 + il) * 4;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (e < n) {
+    if (e + 3 < n && ((stride | e) & 3) == 0) {
+#pragma unroll 4
+      for (int sp = sl; sp < splits; sp += nsl) {
+        const float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)sp * stride + e);
+        a[0] += v.x; a[1] += v.y; a[2] += v.z; a[3] += v.w;
+      }
+    } else {
+      for (int sp = sl; sp < splits; sp += nsl)
+        for (int j = 0; j < 4; ++j)
+          if (e + j < n) a[j] += slab[(int64_t)sp * stride + e + j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sh[sl][il][j] = a[j];
+  __syncthreads();
+  if (sl == 0 && e < n) {
+    for (int l = 1; l < nsl; ++l)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] += sh[l][il][j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (e + j < n) out[e + j] = accumulate ? out[e + j] + a[j] : a[j];
+  }
+}
+
 __global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* __restrict__ slab, int splits, int64_t n,
                                                             int64_t stride, float* out, int accumulate) {
-  __shared__ float sh[1024];
-  const int tid = threadIdx.x, il = tid & 63, sl = tid >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + il;
-  float a = 0.f;
-  if (i < n)
-    for (int sp = sl; sp < splits; sp += 16) a += slab[(int64_t)sp * stride + i];
-  sh[tid] = a;
-  __syncthreads();
-  for (int o = 8; o > 0; o >>= 1) {
-    if (sl < o) sh[tid] += sh[tid + o * 64];
-    __syncthreads();
-  }
-  if (sl == 0 && i < n) out[i] = accumulate ? out[i] + sh[il] : sh[il];
+  __shared__ float sh[RS_MAXSL][64][4];
+  reduce_cols(slab, splits, n, stride, out, accumulate, blockIdx.x, sh);
 }
+
+static int rs_lanes(int splits) { return splits > 96 ? 16 : splits > 24 ? 8 : 4; }
 
 int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate) {
   return launch_reduce_slabs_strided(s, slab, splits, n, n, out, accumulate);
 }
 
+// ------------------------------------------------------------------ deferred slab reductions
+// Every weight gradient ends in a slab reduce; queued while a SlabDefer is active, a backward
+// segment's reductions run as ONE launch (workgroup ranges per job).
+struct SlabBatchArgs {
+  SlabJob j[SlabDefer::kMax];
+  int start[SlabDefer::kMax + 1];
+  int nj;
+};
+
+__global__ __launch_bounds__(1024) void reduce_slabs_batch_kernel(SlabBatchArgs a) {
+  __shared__ float sh[RS_MAXSL][64][4];
+  int k = 0;
+  while (k + 1 < a.nj && (int)blockIdx.x >= a.start[k + 1]) ++k;
+  const SlabJob& jb = a.j[k];
+  reduce_cols(jb.slab, jb.splits, jb.n, jb.n, jb.out, jb.accumulate, (int)blockIdx.x - a.start[k], sh);
+}
+
+static thread_local SlabDefer* t_slab_defer = nullptr;
+SlabDefer* set_slab_defer(SlabDefer* d) {
+  SlabDefer* prev = t_slab_defer;
+  t_slab_defer = d;
+  return prev;
+}
+
+int SlabDefer::flush() {
+  if (n == 0) return 0;
+  SlabBatchArgs a{};
+  int blocks = 0, lanes = 4;
+  for (int k = 0; k < n; ++k) {
+    a.j[k] = jobs[k];
+    a.start[k] = blocks;
+    blocks += (int)cdiv64(jobs[k].n, 256);
+    lanes = std::max(lanes, rs_lanes(jobs[k].splits));
+  }
+  a.start[n] = blocks;
+  a.nj = n;
+  n = 0;
+  hipLaunchKernelGGL(reduce_slabs_batch_kernel, dim3((unsigned)blocks), dim3(64 * lanes), 0, stream, a);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, int64_t n, int64_t stride, float* out,
                                 bool accumulate) {
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)cdiv64(n, 64)), dim3(1024), 0, s, slab, splits, n, stride,
-                     out, accumulate ? 1 : 0);
+  SlabDefer* d = t_slab_defer;
+  if (d && d->stream == s && stride == n && out >= d->lo && out + n <= d->hi && n <= ((int64_t)1 << 30)) {
+    if (d->n == SlabDefer::kMax) DFD_TRY(d->flush());
+    d->jobs[d->n++] = SlabJob{slab, n, out, splits, accumulate ? 1 : 0};
+    return 0;
+  }
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(64 * rs_lanes(splits)), 0, s, slab,
+                     splits, n, stride, out, accumulate ? 1 : 0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

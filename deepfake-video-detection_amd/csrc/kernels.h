@@ -152,6 +152,25 @@ int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t s
 template <typename T>
 int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat);
 // sum `splits` slabs of n floats into out (= or +=)
+// Deferred weight-gradient reductions: while a SlabDefer is active on the calling thread, slab
+// reductions on `stream` whose output lies inside [lo, hi) (the gradient buffer) are queued and
+// flush() runs them as one launch.  The caller keeps every queued slab region intact until then.
+struct SlabJob {
+  const float* slab;
+  int64_t n;
+  float* out;
+  int splits, accumulate;
+};
+struct SlabDefer {
+  static constexpr int kMax = 16;
+  hipStream_t stream;
+  const float* lo;
+  const float* hi;
+  SlabJob jobs[kMax];
+  int n = 0;
+  int flush();
+};
+SlabDefer* set_slab_defer(SlabDefer* d);  // returns the previous one
 int launch_reduce_slabs(hipStream_t s, const float* slab, int splits, int64_t n, float* out, bool accumulate);
 // the same with slab rows `stride` floats apart
 int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, int64_t n, int64_t stride, float* out,

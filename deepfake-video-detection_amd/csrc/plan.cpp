@@ -24,6 +24,9 @@ const ArchRow kArch[7] = {{1, 1, 3, 1, 1, 16},  {0, 2, 3, 2, 6, 24},  {0, 2, 5, 
                           {0, 3, 5, 1, 6, 112}, {0, 4, 5, 2, 6, 192}, {0, 1, 3, 1, 6, 320}};
 constexpr int kStem = 32, kHead = 1280;
 constexpr int64_t kMaterialiseRows = 20000;  // the 7x7 stages (see Block::o_s2)
+// weight-gradient slab regions: a backward segment's wgrad partials each get their own region so
+// their reductions can be deferred to one batched launch at the end of the segment (SlabDefer)
+constexpr int kSlabRegions = 16;
 
 struct Topo {
   std::vector<TensorSpec> t;
@@ -191,10 +194,10 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   alloc_pw(p.head);
   // scratch
   p.stats_cap = (int64_t)2048 * 2 * kHead;
-  p.slab_cap = (int64_t)8 << 20;
+  p.slab_cap = (int64_t)4 << 20;  // floats per slab region; kSlabRegions regions (see backward_impl)
   p.part_cap = std::max<int64_t>((int64_t)4 << 20, 5 * F * std::max<int64_t>(kHead, maxSE));
   p.o_stats = alloc(p.stats_cap * 4);
-  p.o_slab = alloc(p.slab_cap * 4);
+  p.o_slab = alloc(kSlabRegions * p.slab_cap * 4);
   p.o_part = alloc(p.part_cap * 4);
   p.o_coef = alloc(3 * kHead * 4);
   p.o_bc = alloc(F * maxSE * 4);
@@ -391,6 +394,30 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
     return 0;
   };
   const int nb = (int)p.blocks.size();
+  // the gradient buffer's extent: slab reductions into it are deferred (one launch per segment)
+  int64_t gext = 0;
+  for (size_t t = 0; t < p.tensors.size(); ++t) {
+    if (p.tensors[t].kind != TK_PARAM) continue;
+    int64_t nel = 1;
+    for (int64_t d : p.tensors[t].shape) nel *= d;
+    gext = std::max(gext, p.offs[t] + nel);
+  }
+  SlabDefer defer{};
+  defer.stream = s;
+  defer.lo = G;
+  defer.hi = G + gext;
+  struct DeferScope {
+    SlabDefer* prev;
+    ~DeferScope() { set_slab_defer(prev); }
+  } scope{set_slab_defer(&defer)};
+  int region = 0, slab_err = 0;
+  auto slab = [&]() -> float* {
+    if (region == kSlabRegions) {  // every region holds a pending slab: reduce them first
+      slab_err |= defer.flush();
+      region = 0;
+    }
+    return r.f(p.o_slab) + (int64_t)(region++) * p.slab_cap;
+  };
   for (int seg = seg_begin; seg < seg_end; ++seg) {
     if (seg == 0) {
       const int64_t Mf = F * p.Hf * p.Wf;
@@ -401,7 +428,7 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
       DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(p.head.o_wt), r.a(p.o_gx[(nb - 1) & 1]), nullptr, Mf, p.head.cin,
                                 kHead, PRO_NONE, Pro{}, nullptr, nullptr));
       DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(last.o_x), Mf, kHead, p.head.cin, PRO_NONE, Pro{},
-                                 r.f(p.o_slab), p.slab_cap, grad(p.head.t_w), acc != 0));
+                                 slab(), p.slab_cap, grad(p.head.t_w), acc != 0));
     } else if (seg <= 7) {
       const int st = 7 - seg;
       for (int i = nb - 1; i >= 0; --i) {
@@ -421,7 +448,7 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         const bool mat = b.o_s2 >= 0;
         PROBED(PK_PWL_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_gs), mat ? r.a(b.o_s2) : r.a(b.o_y2), Mout, b.cout,
                                                      b.mid, mat ? PRO_GATE : PRO_BN_SILU_G,
-                                                     r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), r.f(p.o_slab), p.slab_cap,
+                                                     r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), slab(), p.slab_cap,
                                                      grad(b.pwl.t_w), acc != 0)));
         // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE
         // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
@@ -450,14 +477,14 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
         fz.scale = r.f(bn_in.o_scale); fz.shift = r.f(bn_in.o_shift); fz.silu = true;
         int fused = 1;
         PROBED(PK_DW_DGRAD, &b, ((fused = launch_dw_bwd<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in,
-                                                           &fz, r.f(p.o_stats), &rows, r.f(p.o_slab), p.slab_cap,
+                                                           &fz, r.f(p.o_stats), &rows, slab(), p.slab_cap,
                                                            grad(b.t_dw), acc != 0)) < 0 ? -1 : 0));
         if (fused == 1) {
           PROBED(PK_DW_DGRAD, &b, (launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in, &fz,
                                                       r.f(p.o_stats), &rows)));
           p.pending_rows = rows;
           PROBED(PK_DW_WGRAD, &b, (launch_dw_wgrad<T>(s, g, r.a(p.o_ge2), y_in, r.pro_bn(bn_in, b.hin * b.win),
-                                                      PRO_BN_SILU, r.f(p.o_slab), p.slab_cap, grad(b.t_dw),
+                                                      PRO_BN_SILU, slab(), p.slab_cap, grad(b.t_dw),
                                                       acc != 0)));
         }
         p.pending_rows = rows;
@@ -470,7 +497,7 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
                                                      b.skip ? gout : nullptr, Min, b.cin, b.mid, PRO_NONE, Pro{},
                                                      nullptr, nullptr)));
           PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
-                                                      r.f(p.o_slab), p.slab_cap, grad(b.pw.t_w), acc != 0)));
+                                                      slab(), p.slab_cap, grad(b.pw.t_w), acc != 0)));
         } else if (!b.ds) {
           // conv_pw + its BN (no activation): ge1 = k1*g + k2*y1 + k3 is never materialised; by
           // linearity (y1 = x . W^T) the gradients need only g (in ge1) and the block input x:
@@ -488,8 +515,8 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
           PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(p.o_w1t), gxo, r.a(p.o_gs), Min, b.cin,
                                                      b.mid, PRO_NONE, Pro{}, nullptr, nullptr)));
           PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
-                                                      r.f(p.o_slab), p.slab_cap, r.f(p.o_tg), false)));
-          DFD_TRY(launch_pw_wgrad<T>(s, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, r.f(p.o_slab), p.slab_cap,
+                                                      slab(), p.slab_cap, r.f(p.o_tg), false)));
+          DFD_TRY(launch_pw_wgrad<T>(s, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, slab(), p.slab_cap,
                                      r.f(p.o_gram), false));
           DFD_TRY(launch_col_sums<T>(s, xin, Min, b.cin, r.f(p.o_stats), p.stats_cap, r.f(p.o_cs)));
           DFD_TRY(launch_pw_wgrad_bn_combine(s, r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs), r.prm(b.pw.t_w),
@@ -502,8 +529,11 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
       in.dZ = r.a(p.o_ge1); in.rows_per_frame = p.H1 * p.W1; in.silu = false;  // ge1 holds g (fused in dw dgrad)
       DFD_TRY(bwd_bn_from_stats(in, p.bn_stem, r.a(p.o_ystem), M, r.a(p.o_ge1), p.pending_rows));
       StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3]};
-      DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), r.f(p.o_slab), p.slab_cap, grad(p.t_stem), acc != 0));
+      DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), slab(), p.slab_cap, grad(p.t_stem), acc != 0));
     }
+    DFD_TRY(defer.flush());  // this segment's weight gradients are final
+    DFD_TRY(slab_err);
+    region = 0;
   }
   return 0;
 }
