@@ -1,4 +1,7 @@
-"""Per-kernel PMC summary from tools/pmc_kb.sh output: python3 tools/pmc_table.py DIR [name-filter]"""
+"""Per-kernel PMC summary from tools/pmc_kb.sh output: python3 tools/pmc_table.py DIR [name-filter]
+
+FETCH MB is the raw FETCH_SIZE (KiB -> MB): exact for 64-B read requests, HALF the bytes of wide
+128-B-request streams on gfx950 (MI355X_MICROARCH.md §HBM); WR MB is WRITE_SIZE."""
 import collections
 import csv
 import sys
@@ -41,4 +44,4 @@ for key, e1 in g["p1"].items():
           f"{100*avg('p1','SQ_ACTIVE_INST_VALU')/wc:5.0f} {100*avg('p1','SQ_ACTIVE_INST_LDS')/wc:5.0f} "
           f"{avg('p2','SQ_LDS_BANK_CONFLICT')/max(1,avg('p2','SQ_LDS_IDX_ACTIVE'))*100:8.1f} "
           f"{avg('p2','SQ_INSTS_VALU')/waves:7.0f} {avg('p2','SQ_INSTS_LDS')/waves:6.0f} "
-          f"{2*avg('p3','FETCH_SIZE')/1024:8.1f} {avg('p4','WRITE_SIZE')/1024:6.1f}")
+          f"{avg('p3','FETCH_SIZE')/1024:8.1f} {avg('p4','WRITE_SIZE')/1024:6.1f}")
