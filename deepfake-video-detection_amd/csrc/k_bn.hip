@@ -22,7 +22,19 @@ __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int 
   const int c = blockIdx.x * FIN_CH + cl;
   double a = 0.0, b = 0.0;
   if (c < C) {
-    for (int r = rl; r < rows; r += FIN_RL) {
+    // loads of 8 rows issued before their adds (same summation order as one row at a time)
+    int r = rl;
+    for (; r + 7 * FIN_RL < rows; r += 8 * FIN_RL) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        va[u] = stats[((int64_t)(r + u * FIN_RL) * 2 + 0) * C + c];
+        vb[u] = stats[((int64_t)(r + u * FIN_RL) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { a += va[u]; b += vb[u]; }
+    }
+    for (; r < rows; r += FIN_RL) {
       a += stats[((int64_t)r * 2 + 0) * C + c];
       b += stats[((int64_t)r * 2 + 1) * C + c];
     }
@@ -422,7 +434,15 @@ __global__ void sum_parts_kernel(const float* __restrict__ part, int hsplit, int
                                  float* __restrict__ out) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float a = 0.f;
-    for (int h = 0; h < hsplit; ++h) a += part[h * n + i];
+    int h = 0;
+    for (; h + 4 <= hsplit; h += 4) {  // 4 loads in flight, added in order
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[(h + u) * n + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a += v[u];
+    }
+    for (; h < hsplit; ++h) a += part[h * n + i];
     out[i] = a * scale;
   }
 }
@@ -532,7 +552,15 @@ __global__ void sum_parts5_kernel(const float* __restrict__ part, int hsplit, in
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < 5 * n; i += (int64_t)gridDim.x * 256) {
     const int64_t q = i / n, k = i - q * n;
     float a = 0.f;
-    for (int h = 0; h < hsplit; ++h) a += part[(q * hsplit + h) * n + k];
+    int h = 0;
+    for (; h + 4 <= hsplit; h += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[(q * hsplit + h + u) * n + k];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a += v[u];
+    }
+    for (; h < hsplit; ++h) a += part[(q * hsplit + h) * n + k];
     if (q == 0) {
       const float g = gate[k];
       de[k] = a * g * (1.f - g);

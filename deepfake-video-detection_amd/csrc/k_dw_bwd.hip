@@ -10,7 +10,8 @@
 // Thread = (channel vector of VW channels, pixel slot); a thread visits P pixels of the tile.
 // Stride 2: a thread's pixels share their row and column parity, so only the taps of that
 // parity class are valid for it (k3: <= 2x2, k5: <= 3x3) and its weight-gradient accumulators
-// are NA x NA x VW registers.  Stride 1 k5 uses VW = 4 (25 x 4 accumulators).  At the end the
+// are NA x NA x VW registers.  Stride 1 uses VW = 4 (k5: 25 x 4 accumulators) except
+// the 8x28 tile (VW = 8); fewer registers there buy co-resident workgroups.  At the end the
 // accumulators are reduced over the lanes of a class (shuffles), then over the 4 waves in a fixed
 // order (LDS) into the workgroup's slab row (summed by the deterministic slab reducer).
 #include "dw_common.h"
@@ -352,10 +353,19 @@ static int bwd_launch(hipStream_t s, const DwGeom& g, const T* dY, const float* 
   const int ntiles = g.frames * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
-  int64_t rows = std::min<int64_t>(ntiles, std::max<int64_t>(1, 1024 / groups));
+  // persistent grid of exactly the co-resident workgroups (one dispatch wave: measured faster than
+  // two waves of 1024 on every B0 shape), measured once per instantiation
+  auto kern = dw_bwd_kernel<T, TH, TW, K, S, VW, PF>;
+  static const int resident = [&] {
+    int dev = 0, cus = 256, per_cu = 2;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    return std::max(1, cus * per_cu);
+  }();
+  int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   const int gx = (int)(rows * groups);
-  hipLaunchKernelGGL((dw_bwd_kernel<T, TH, TW, K, S, VW, PF>), dim3(gx), dim3(256), 0, s, g, dY, w, out, Yp, bn, stats,
+  hipLaunchKernelGGL(kern, dim3(gx), dim3(256), 0, s, g, dY, w, out, Yp, bn, stats,
                      slab, ntiles, groups, tiles_x, tiles_y);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
@@ -378,12 +388,12 @@ int launch_dw_bwd(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T
     return bwd_launch<T, 8, 8, 5, 2, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
   if (g.k == 3 && g.s == 1) {
     if (H % 16 == 0 && W % 16 == 0)
-      return bwd_launch<T, 16, 16, 3, 1, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
+      return bwd_launch<T, 16, 16, 3, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
     if (H % 8 == 0 && W % 28 == 0)
       return bwd_launch<T, 8, 28, 3, 1, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
     if (H % 14 == 0 && W % 14 == 0)
-      return bwd_launch<T, 14, 14, 3, 1, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
-    return bwd_launch<T, 7, 7, 3, 1, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
+      return bwd_launch<T, 14, 14, 3, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    return bwd_launch<T, 7, 7, 3, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
   }
   if (g.k == 5 && g.s == 1) {
     if (H % 14 == 0 && W % 14 == 0)
