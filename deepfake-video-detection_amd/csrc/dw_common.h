@@ -117,6 +117,18 @@ constexpr int kNumDwTiles = 6;
 constexpr TileChoice kDwTiles[kNumDwTiles] = {{16, 16}, {8, 28}, {14, 14}, {14, 7}, {8, 8}, {7, 7}};
 constexpr int kDwFallback = 4;  // 8x8
 
+// workgroups of KERN (NT threads, no dynamic LDS) co-resident on the whole device, measured once per kernel
+template <auto KERN, int NT>
+int resident_wgs() {
+  static const int r = [] {
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERN, NT, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    return std::max(1, cus * per_cu);
+  }();
+  return r;
+}
+
 static inline int dw_grid(int64_t ntiles, int groups) {
   const int64_t per_group = std::min<int64_t>(ntiles, std::max<int64_t>(1, 1024 / groups));
   return (int)(per_group * groups);

@@ -354,14 +354,9 @@ static int bwd_launch(hipStream_t s, const DwGeom& g, const T* dY, const float* 
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
   // persistent grid of exactly the co-resident workgroups (one dispatch wave: measured faster than
-  // two waves of 1024 on every B0 shape), measured once per instantiation
+  // two waves of 1024 on every B0 shape)
   auto kern = dw_bwd_kernel<T, TH, TW, K, S, VW, PF>;
-  static const int resident = [&] {
-    int dev = 0, cus = 256, per_cu = 2;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    return std::max(1, cus * per_cu);
-  }();
+  const int resident = resident_wgs<dw_bwd_kernel<T, TH, TW, K, S, VW, PF>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   const int gx = (int)(rows * groups);

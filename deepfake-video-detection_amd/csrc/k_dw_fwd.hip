@@ -98,7 +98,10 @@ static int fwd_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w
     const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
     const int ntiles = g.frames * tiles_x * tiles_y;
     const int groups = cdiv(g.C, DCG);
-    const int gx = dw_grid(ntiles, groups);
+    // persistent grid: the co-resident workgroups, at most 1024 (stat rows)
+    const int res = stats ? resident_wgs<dw_fwd_kernel<T, TH, TW, K, S, true>, 256>()
+                          : resident_wgs<dw_fwd_kernel<T, TH, TW, K, S, false>, 256>();
+    const int gx = (int)(std::min<int64_t>(ntiles, std::max(1, std::min(res, 1024) / groups)) * groups);
     if (stats)
       hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, true>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
                          ntiles, groups, tiles_x, tiles_y);

@@ -179,7 +179,15 @@ static int strip_launch(hipStream_t s, const DwGeom& g, const T* X, const float*
   const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
   const int ntiles = g.frames * tiles_x * tiles_y;
   const int groups = cdiv(g.C, Cf::CVW);
-  const int per_group = std::min(ntiles, std::max(1, 4096 / groups));
+  // grid: up to 4096 workgroups for the 8x28 k3 tile; the others run exactly the co-resident
+  // workgroups (one dispatch wave; measured 4-9% faster there, 5% slower on 8x28 k3)
+  int cap = 4096;
+  if (!(K == 3 && TH == 8)) {
+    const int res = stats ? resident_wgs<dw_fwd_strip_kernel<T, LT, K, TH, TW, R, CV, NT, OCC, PF, true>, NT>()
+                          : resident_wgs<dw_fwd_strip_kernel<T, LT, K, TH, TW, R, CV, NT, OCC, PF, false>, NT>();
+    cap = std::min(4096, res);
+  }
+  const int per_group = std::min(ntiles, std::max(1, cap / groups));
   const int gx = per_group * groups;
   if (stats)
     hipLaunchKernelGGL((dw_fwd_strip_kernel<T, LT, K, TH, TW, R, CV, NT, OCC, PF, true>), dim3(gx), dim3(NT), 0, s, g, X, w, Y, pro,
