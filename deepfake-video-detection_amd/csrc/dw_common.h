@@ -47,7 +47,14 @@ __host__ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0)
 // Stage an NR x NC pixel window (origin y0, x0; zero outside the map) of channel vector c of
 // a [frames][H][W][C] tensor into fp32 LDS [NR*NC][32] (this thread's 8 channels), applying the
 // producer's BN+SiLU when MODE != PRO_NONE.  All loads are issued before any is consumed.
-template <typename T, int MODE, int NR, int NC>
+// DI: columns stored de-interleaved (even columns, then odd: LDS column (rx&1)*ceil(NC/2) + rx/2),
+// so the stride-2 forward's neighbouring output pixels read LDS pixels 128 B apart (the other half
+// of the 64 banks) instead of 256 B apart (the same banks: 2-way conflicts on every tap read).
+template <int NC, bool DI>
+__device__ __forceinline__ int di_col(int rx) {
+  return DI ? (rx & 1) * ((NC + 1) / 2) + (rx >> 1) : rx;
+}
+template <typename T, int MODE, int NR, int NC, bool DI = false>
 __device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src, int f, int y0, int x0, int H, int W,
                                            int C, int c, bool cok, const float (&sc)[8], const float (&sh)[8]) {
   constexpr int N = NR * NC;
@@ -73,7 +80,12 @@ __device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = in[i] ? siluf_(x[j] * sc[j] + sh[j]) : 0.f;
       }
-      st8(dst + pix * DCG + vec * 8, x);
+      if constexpr (DI) {
+        const int ry = pix / NC, rx = pix - (pix / NC) * NC;
+        st8(dst + (ry * NC + di_col<NC, true>(rx)) * DCG + vec * 8, x);
+      } else {
+        st8(dst + pix * DCG + vec * 8, x);
+      }
     }
   }
 }

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
     const int p = tp + 64 * i;
     ly[i] = p / TW;
     lx[i] = p - (p / TW) * TW;
-    lofs[i] = ((ly[i] * S) * D::IW + lx[i] * S) * DCG + vec * 8;
+    lofs[i] = ((ly[i] * S) * D::IW + (S == 2 ? lx[i] : lx[i] * S)) * DCG + vec * 8;  // S == 2: de-interleaved
   }
   float st_s[8], st_q[8];
 #pragma unroll
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
     const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
     const int oy0 = ty * TH, ox0 = tx * TW;
     lds_barrier();
-    stage_tile<T, PRO_BN_SILU, D::IH, D::IW>(tin, X, f, oy0 * S - g.pad, ox0 * S - g.pad, g.H, g.W, C, c, cok, sc,
+    stage_tile<T, PRO_BN_SILU, D::IH, D::IW, S == 2>(tin, X, f, oy0 * S - g.pad, ox0 * S - g.pad, g.H, g.W, C, c, cok, sc,
                                              sh);
     lds_barrier();
     float acc[D::P][8];
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
         for (int i = 0; i < D::P; ++i) {
           if (i == D::P - 1 && tp + 64 * i >= D::NPX) continue;
           float x[8];
-          ld8(tin + lofs[i] + (kh * D::IW + kw) * DCG, x);
+          ld8(tin + lofs[i] + (kh * D::IW + (S == 2 ? di_col<D::IW, true>(kw) : kw)) * DCG, x);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(x[j], wv[j], acc[i][j]);
         }
