@@ -226,13 +226,22 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdIn in, const T*
     bn_bwd_ch<FL>(in, c, ch);
     ld8f(in.mean + c, mu);
     ld8f(in.invstd + c, is);
-    for (int64_t r = (int64_t)blockIdx.x * nrl + rl; r < M; r += (int64_t)gridDim.x * nrl) {
-      float g[8], y[8];
-      bn_bwd_g8<T, FL>(in, Y, r, bn_frame<FL>(in, r), c, C, ch, g, y);
+    // rows in pairs (both rows' loads issued before either is summed; same summation order)
+    const int64_t rs = (int64_t)gridDim.x * nrl;
+    int64_t r = (int64_t)blockIdx.x * nrl + rl;
+    for (; r < M; r += 2 * rs) {
+      float g[2][8], y[2][8];
+      const bool two = r + rs < M;
+      bn_bwd_g8<T, FL>(in, Y, r, bn_frame<FL>(in, r), c, C, ch, g[0], y[0]);
+      if (two) bn_bwd_g8<T, FL>(in, Y, r + rs, bn_frame<FL>(in, r + rs), c, C, ch, g[1], y[1]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        as[j] += g[j];
-        aq[j] += g[j] * (y[j] - mu[j]) * is[j];
+      for (int u = 0; u < 2; ++u) {
+        if (u == 1 && !two) break;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          as[j] += g[u][j];
+          aq[j] += g[u][j] * (y[u][j] - mu[j]) * is[j];
+        }
       }
     }
   }
@@ -382,21 +391,37 @@ __global__ __launch_bounds__(256) void frame_sum_kernel(const T* __restrict__ dZ
     float sc[8], shf[8];
     ld8f(pro.scale + c, sc);
     ld8f(pro.shift + c, shf);
-    for (int p = p0 + pl; p < p1; p += npl) {
-      const int64_t row = (int64_t)f * HW + p;
-      float y[8];
-      ld8(Y + row * C + c, y);
+    // pixels in groups of FS_U with every load of a group issued first (same summation order)
+    auto one = [&](int64_t row, float (&y)[8], const float (&d)[8]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) y[j] = siluf_(y[j] * sc[j] + shf[j]);
       if (!SEBWD && s_out) st8(s_out + row * C + c, y);
       if constexpr (SEBWD) {
-        float d[8];
-        ld8(dZ + row * C + c, d);
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[j] *= d[j];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += y[j];
+    };
+    constexpr int FS_U = 4;
+    int p = p0 + pl;
+    for (; p + (FS_U - 1) * npl < p1; p += FS_U * npl) {
+      float y[FS_U][8], d[FS_U][8];
+#pragma unroll
+      for (int u = 0; u < FS_U; ++u) {
+        const int64_t row = (int64_t)f * HW + p + u * npl;
+        ld8(Y + row * C + c, y[u]);
+        if constexpr (SEBWD) ld8(dZ + row * C + c, d[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < FS_U; ++u) one((int64_t)f * HW + p + u * npl, y[u], d[u]);
+    }
+    for (; p < p1; p += npl) {
+      const int64_t row = (int64_t)f * HW + p;
+      float y[8], d[8];
+      ld8(Y + row * C + c, y);
+      if constexpr (SEBWD) ld8(dZ + row * C + c, d);
+      one(row, y, d);
     }
   }
 #pragma unroll
