@@ -1,9 +1,9 @@
 """Turn the PMC passes of tools/pmc_traffic.sh into profiles/traffic.json (read by bench.py).
 
 The probed launch is dw_fwd of blocks.1.0 (112x112x96 -> 56x56x96, k3 s2, bf16): kernel
-dw_fwd_kernel<bf16, 14, 7, 3, 2, true> with 1023 workgroups (8192 tiles x 3 channel groups,
-341 rows per group) = grid 261,888 work-items; blocks.3.0 uses the same instance with 1024
-workgroups.  Units: FETCH_SIZE / WRITE_SIZE are KiB.  The guide (MI355X_MICROARCH.md §HBM)
+dw_fwd_kernel<bf16, 14, 7, 3, 2, true> on a persistent grid sized to the co-resident
+workgroups: 510 workgroups = grid 130,560 work-items (blocks.3.0 uses the same instance with
+512 workgroups, grid 131,072).  Units: FETCH_SIZE / WRITE_SIZE are KiB.  The guide (MI355X_MICROARCH.md §HBM)
 documents FETCH_SIZE = RDREQ x 64 B, i.e. HALF the bytes of wide coalesced reads that issue
 128-B requests.  This kernel's reads are 64-B requests -- each workgroup loads one 32-channel
 bf16 slice (64 B) per pixel, the other channel groups of the pixel belong to neighbouring
@@ -21,7 +21,7 @@ import statistics
 import sys
 
 NAME = "dw_fwd_kernel<dfd::bf16, 14, 7, 3, 2, true>"
-GRID = 261888
+GRID = 130560
 
 
 def values(d, counter):
