@@ -18,6 +18,14 @@
 
 #include <atomic>
 
+// which tiles bound the tap loop's LDS-read hoisting to one kernel row (compiler fence per row):
+// 1 = k5 stride 1 (without it the 14x14 k5 tile spills), 2 = k3 stride 1, 4 = stride 2
+#ifndef DFD_DWB_ROWFENCE
+#define DFD_DWB_ROWFENCE 1
+#endif
+#ifndef DFD_DWB_PF1
+#define DFD_DWB_PF1 1  // bit mask of the stride-1 tiles that also prefetch the next tile (A/B knob)
+#endif
 namespace dfd {
 
 // 1: fused (default); 0: the two kernels (dgrad, wgrad)
@@ -206,6 +214,8 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_kernel(DwGeom g, const T* __res
 #pragma unroll
         for (int ah = 0; ah < NA; ++ah) {
           if (ah >= nah) break;
+          if constexpr ((DFD_DWB_ROWFENCE & (S == 2 ? 4 : K == 5 ? 1 : 2)) != 0)
+            asm volatile("" ::: "memory");  // one kernel row's LDS reads in flight at a time
           const int kh = kh0 + S * ah;
           const int tyv = iy + g.pad - kh;
           const int gyl = (S == 2 ? (tyv >> 1) : tyv) - gy0;
@@ -345,7 +355,12 @@ __global__ __launch_bounds__(256, 2) void dw_bwd_kernel(DwGeom g, const T* __res
   }
 }
 
-template <typename T, int TH, int TW, int K, int S, int VW, bool PF = (S == 2)>
+template <int TH, int TW, int K> constexpr int pf1_bit() {
+  return (TH == 16 && K == 3) ? 1 : (TH == 8 && K == 3) ? 2 : (TH == 14 && K == 3) ? 4 : (TH == 7 && K == 3) ? 8
+       : (TH == 14 && K == 5) ? 16 : 32;
+}
+template <typename T, int TH, int TW, int K, int S, int VW,
+          bool PF = (S == 2 || (DFD_DWB_PF1 & pf1_bit<TH, TW, K>()) != 0)>
 static int bwd_launch(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* out, const T* Yp,
                       const BnBwdIn& bn, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
                       bool accumulate) {
