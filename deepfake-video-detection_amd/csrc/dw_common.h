@@ -54,31 +54,43 @@ template <int NC, bool DI>
 __device__ __forceinline__ int di_col(int rx) {
   return DI ? (rx & 1) * ((NC + 1) / 2) + (rx >> 1) : rx;
 }
-template <typename T, int MODE, int NR, int NC, bool DI = false>
-__device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src, int f, int y0, int x0, int H, int W,
-                                           int C, int c, bool cok, const float (&sc)[8], const float (&sh)[8]) {
-  constexpr int N = NR * NC;
-  constexpr int NLD = (N + 63) / 64;
-  const int tp = threadIdx.x >> 2, vec = threadIdx.x & 3;
+// The two halves of stage_tile: stage_issue puts the window's global loads in flight (registers),
+// stage_commit converts, applies the producer and stores them to LDS.  Split so a kernel can
+// issue the next tile's loads before it computes the current one.
+template <typename T, int NR, int NC>
+struct StageRegs {
+  static constexpr int NLD = (NR * NC + 63) / 64;
   Raw8<T> raw[NLD];
   bool in[NLD];
+};
+template <typename T, int NR, int NC>
+__device__ __forceinline__ void stage_issue(StageRegs<T, NR, NC>& r, const T* __restrict__ src, int f, int y0, int x0,
+                                            int H, int W, int C, int c, bool cok, bool valid = true) {
+  constexpr int N = NR * NC;
+  const int tp = threadIdx.x >> 2;
 #pragma unroll
-  for (int i = 0; i < NLD; ++i) {
+  for (int i = 0; i < StageRegs<T, NR, NC>::NLD; ++i) {
     const int pix = tp + 64 * i;
     const int ry = pix / NC, rx = pix - (pix / NC) * NC;
     const int iy = y0 + ry, ix = x0 + rx;
-    in[i] = pix < N && cok && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    raw_ld(raw[i], src + (((int64_t)f * H + iy) * W + ix) * C + c, src, in[i]);
+    r.in[i] = valid && pix < N && cok && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    raw_ld(r.raw[i], src + (((int64_t)f * H + iy) * W + ix) * C + c, src, r.in[i]);
   }
+}
+template <typename T, int MODE, int NR, int NC, bool DI = false>
+__device__ __forceinline__ void stage_commit(float* dst, const StageRegs<T, NR, NC>& r, const float (&sc)[8],
+                                             const float (&sh)[8]) {
+  constexpr int N = NR * NC;
+  const int tp = threadIdx.x >> 2, vec = threadIdx.x & 3;
 #pragma unroll
-  for (int i = 0; i < NLD; ++i) {
+  for (int i = 0; i < StageRegs<T, NR, NC>::NLD; ++i) {
     const int pix = tp + 64 * i;
     if (pix < N) {
       float x[8];
-      raw_to_f(raw[i], x);
+      raw_to_f(r.raw[i], x);
       if (MODE != PRO_NONE) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = in[i] ? siluf_(x[j] * sc[j] + sh[j]) : 0.f;
+        for (int j = 0; j < 8; ++j) x[j] = r.in[i] ? siluf_(x[j] * sc[j] + sh[j]) : 0.f;
       }
       if constexpr (DI) {
         const int ry = pix / NC, rx = pix - (pix / NC) * NC;
@@ -88,6 +100,13 @@ __device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src
       }
     }
   }
+}
+template <typename T, int MODE, int NR, int NC, bool DI = false>
+__device__ __forceinline__ void stage_tile(float* dst, const T* __restrict__ src, int f, int y0, int x0, int H, int W,
+                                           int C, int c, bool cok, const float (&sc)[8], const float (&sh)[8]) {
+  StageRegs<T, NR, NC> r;
+  stage_issue<T, NR, NC>(r, src, f, y0, x0, H, W, C, c, cok);
+  stage_commit<T, MODE, NR, NC, DI>(dst, r, sc, sh);
 }
 
 // Reduce per-thread 8-channel partials a (sum) and b over all threads with the same vec

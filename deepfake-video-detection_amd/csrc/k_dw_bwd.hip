@@ -23,6 +23,9 @@
 #ifndef DFD_DWB_ROWFENCE
 #define DFD_DWB_ROWFENCE 1
 #endif
+#ifndef DFD_DWB_ALT
+#define DFD_DWB_ALT 0  // tile-choice A/B knob (bits: see launch_dw_bwd)
+#endif
 #ifndef DFD_DWB_PF1
 #define DFD_DWB_PF1 1  // bit mask of the stride-1 tiles that also prefetch the next tile (A/B knob)
 #endif
@@ -391,22 +394,22 @@ int launch_dw_bwd(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T
   if (!dw_bwd_fused_enabled()) return 1;
   const int H = g.H, W = g.W;
   if (g.k == 3 && g.s == 2) {
-    if (H >= 56) return bwd_launch<T, 16, 16, 3, 2, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    if (H >= 56 && !(DFD_DWB_ALT & 1)) return bwd_launch<T, 16, 16, 3, 2, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
     return bwd_launch<T, 8, 8, 3, 2, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
   }
   if (g.k == 5 && g.s == 2)
     return bwd_launch<T, 8, 8, 5, 2, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
   if (g.k == 3 && g.s == 1) {
-    if (H % 16 == 0 && W % 16 == 0)
+    if (H % 16 == 0 && W % 16 == 0 && !(DFD_DWB_ALT & 8))
       return bwd_launch<T, 16, 16, 3, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
-    if (H % 8 == 0 && W % 28 == 0)
+    if (H % 8 == 0 && W % 28 == 0 && !(DFD_DWB_ALT & 2))
       return bwd_launch<T, 8, 28, 3, 1, 8>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
     if (H % 14 == 0 && W % 14 == 0)
       return bwd_launch<T, 14, 14, 3, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
     return bwd_launch<T, 7, 7, 3, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
   }
   if (g.k == 5 && g.s == 1) {
-    if (H % 14 == 0 && W % 14 == 0)
+    if (H % 14 == 0 && W % 14 == 0 && !(DFD_DWB_ALT & 4))
       return bwd_launch<T, 14, 14, 5, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
     return bwd_launch<T, 7, 7, 5, 1, 4>(s, g, dY, w, out, Yp, *bn, stats, stat_rows, slab, slab_cap, dW, accumulate);
   }

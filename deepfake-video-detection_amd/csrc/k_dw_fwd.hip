@@ -2,9 +2,20 @@
 // s = 1/2, pad k//2, producer BN+SiLU fused into staging, BN-stat partials in the epilogue.
 #include "dw_common.h"
 
+// bit mask of the tile shapes whose kernel prefetches the next tile's input window while it computes
+// the current one (A/B knob): 1 = 16x16, 2 = 8x28, 4 = 14x14, 8 = 14x7, 16 = 8x8, 32 = 7x7
+#ifndef DFD_DWF_PF
+#define DFD_DWF_PF 0
+#endif
+
 namespace dfd {
 
-template <typename T, int TH, int TW, int K, int S, bool STATS>
+template <int TH, int TW> constexpr bool dwf_pf() {
+  return (DFD_DWF_PF & ((TH == 16) ? 1 : (TH == 8 && TW == 28) ? 2 : (TH == 14 && TW == 14) ? 4
+                        : (TH == 14) ? 8 : (TH == 8) ? 16 : 32)) != 0;
+}
+
+template <typename T, int TH, int TW, int K, int S, bool STATS, bool PF = dwf_pf<TH, TW>()>
 __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __restrict__ X, const float* __restrict__ w,
                                                      T* __restrict__ Y, Pro pro, float* __restrict__ stats, int ntiles,
                                                      int groups, int tiles_x, int tiles_y) {
@@ -40,14 +51,23 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
 #pragma unroll
   for (int j = 0; j < 8; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
   const int tpf = tiles_x * tiles_y;
-  for (int t = blockIdx.x / groups; t < ntiles; t += gridDim.x / groups) {
+  const int tstep = gridDim.x / groups;
+  StageRegs<T, D::IH, D::IW> sr;
+  auto issue = [&](int t) {  // input window of tile t (nothing when t is past the end)
+    const int f = t / tpf, r = t - (t / tpf) * tpf;
+    const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
+    stage_issue<T, D::IH, D::IW>(sr, X, f, ty * TH * S - g.pad, tx * TW * S - g.pad, g.H, g.W, C, c, cok, t < ntiles);
+  };
+  if (PF) issue(blockIdx.x / groups);
+  for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
     const int f = t / tpf, r = t - (t / tpf) * tpf;
     const int ty = r / tiles_x, tx = r - (r / tiles_x) * tiles_x;
     const int oy0 = ty * TH, ox0 = tx * TW;
+    if (!PF) issue(t);
     lds_barrier();
-    stage_tile<T, PRO_BN_SILU, D::IH, D::IW, S == 2>(tin, X, f, oy0 * S - g.pad, ox0 * S - g.pad, g.H, g.W, C, c, cok, sc,
-                                             sh);
+    stage_commit<T, PRO_BN_SILU, D::IH, D::IW, S == 2>(tin, sr, sc, sh);
     lds_barrier();
+    if (PF && t + tstep < ntiles) issue(t + tstep);  // in flight while this tile computes
     float acc[D::P][8];
 #pragma unroll
     for (int i = 0; i < D::P; ++i)
@@ -120,6 +140,9 @@ static int fwd_ks(hipStream_t s, const DwGeom& g, const T* X, const float* w, T*
   const bool ok[kNumDwTiles] = {DwT<16, 16, K, S>::fwd_ok, DwT<8, 28, K, S>::fwd_ok, DwT<14, 14, K, S>::fwd_ok,
                                 DwT<14, 7, K, S>::fwd_ok, DwT<8, 8, K, S>::fwd_ok, DwT<7, 7, K, S>::fwd_ok};
   int pick = -1;
+  // stride 2: the 8x8 tile first where it divides the map -- its 17x17 fp32 input window lets
+  // 4 workgroups share a CU (14x7's 29x15 window: 2), measured 231 -> 213 us on blocks.1.0
+  if (S == 2 && ok[4] && g.Ho % 8 == 0 && g.Wo % 8 == 0) pick = 4;
   for (int i = 0; i < kNumDwTiles && pick < 0; ++i)
     if (ok[i] && g.Ho % kDwTiles[i].th == 0 && g.Wo % kDwTiles[i].tw == 0) pick = i;
   if (pick < 0) pick = kDwFallback;  // 8x8 with masked partial tiles

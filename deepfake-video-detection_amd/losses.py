@@ -51,5 +51,9 @@ class WeightedCrossEntropyLoss(nn.Module):
 
     def forward(self, logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         _lib.require_hip(logits, "logits")
-        w = None if self.weight is None else self.weight.to(logits.device).contiguous()
+        if self.weight is not None and (self.weight.device != logits.device or not self.weight.is_contiguous()):
+            # moved once: a per-step host->device copy of a pageable tensor blocks the host until the
+            # queue drains (measured 7 ms/step of host stall in the bench step, tools/host_prof.py)
+            self.weight = self.weight.to(logits.device).contiguous()
+        w = self.weight
         return _CEFn.apply(logits, target, w, self.ignore_index)

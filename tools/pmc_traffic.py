@@ -1,14 +1,13 @@
 """Turn the PMC passes of tools/pmc_traffic.sh into profiles/traffic.json (read by bench.py).
 
 The probed launch is dw_fwd of blocks.1.0 (112x112x96 -> 56x56x96, k3 s2, bf16): kernel
-dw_fwd_kernel<bf16, 14, 7, 3, 2, true> on a persistent grid sized to the co-resident
-workgroups: 510 workgroups = grid 130,560 work-items (blocks.3.0 uses the same instance with
-512 workgroups, grid 131,072).  Units: FETCH_SIZE / WRITE_SIZE are KiB.  The guide (MI355X_MICROARCH.md §HBM)
+dw_fwd_kernel<bf16, 8, 8, 3, 2, true, ...> on a persistent grid sized to the co-resident
+workgroups; no other B0 layer uses that instance (the other stride-2 maps are not multiples of 8).  Units: FETCH_SIZE / WRITE_SIZE are KiB.  The guide (MI355X_MICROARCH.md §HBM)
 documents FETCH_SIZE = RDREQ x 64 B, i.e. HALF the bytes of wide coalesced reads that issue
 128-B requests.  This kernel's reads are 64-B requests -- each workgroup loads one 32-channel
 bf16 slice (64 B) per pixel, the other channel groups of the pixel belong to neighbouring
-workgroups -- so the raw FETCH_SIZE is taken as bytes (it equals the algorithmic input bytes x
-1.07, the tile-halo re-read of 29x15 input pixels per 14x7 s2 tile); the doubled value is
+workgroups -- so the raw FETCH_SIZE is taken as bytes (the input window of an 8x8 s2 tile is
+17x17 pixels, a halo re-read of 17^2/16^2 = 1.13x; L2 absorbs part of it); the doubled value is
 recorded next to it.  WRITE_SIZE is exact for 16-B-per-lane stores.
 
 usage: python tools/pmc_traffic.py gpurun_out/pmc_traffic [profiles/traffic.json]
@@ -20,15 +19,14 @@ import os
 import statistics
 import sys
 
-NAME = "dw_fwd_kernel<dfd::bf16, 14, 7, 3, 2, true>"
-GRID = 130560
+NAME = "dw_fwd_kernel<dfd::bf16, 8, 8, 3, 2, true"
 
 
 def values(d, counter):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     out = []
     for r in csv.DictReader(open(f)):
-        if NAME in r["Kernel_Name"] and int(r["Grid_Size"]) == GRID and r["Counter_Name"] == counter:
+        if NAME in r["Kernel_Name"] and r["Counter_Name"] == counter:
             out.append(float(r["Counter_Value"]))
     return out
 
