@@ -571,7 +571,11 @@ int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, in
   }
   const int tnn = cdiv(N, WT), tnk = cdiv(K, WT);
   const int tiles = tnn * tnk;
-  int64_t splits = std::max<int64_t>(1, 1024 / tiles);
+#ifndef DFD_WGRAD_SPLIT_WGS
+#define DFD_WGRAD_SPLIT_WGS 512  // target workgroups of the M-split (A/B knob; 512 measured best over
+                                 // 256/384/1024/2048 on the B0 shapes: less slab traffic)
+#endif
+  int64_t splits = std::max<int64_t>(1, DFD_WGRAD_SPLIT_WGS / tiles);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, cdiv64(M, 4 * WMS)));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, slab_cap / ((int64_t)N * K)));
   int64_t mps = cdiv64(cdiv64(std::max<int64_t>(M, 1), splits), 4 * WMS) * (4 * WMS);
