@@ -77,8 +77,8 @@ __device__ __forceinline__ void stage_issue(StageRegs<T, NR, NC>& r, const T* __
     raw_ld(r.raw[i], src + (((int64_t)f * H + iy) * W + ix) * C + c, src, r.in[i]);
   }
 }
-template <typename T, int MODE, int NR, int NC, bool DI = false>
-__device__ __forceinline__ void stage_commit(float* dst, const StageRegs<T, NR, NC>& r, const float (&sc)[8],
+template <typename T, int MODE, int NR, int NC, bool DI = false, typename LT = float>
+__device__ __forceinline__ void stage_commit(LT* dst, const StageRegs<T, NR, NC>& r, const float (&sc)[8],
                                              const float (&sh)[8]) {
   constexpr int N = NR * NC;
   const int tp = threadIdx.x >> 2, vec = threadIdx.x & 3;

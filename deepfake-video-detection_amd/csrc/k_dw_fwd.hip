@@ -8,6 +8,12 @@
 #define DFD_DWF_PF 0
 #endif
 
+// 1: the stride-2 bf16 kernels stage the producer's SiLU output as bf16 in LDS (half the window:
+// twice the co-resident workgroups) instead of fp32
+#ifndef DFD_DWF_BF16LDS
+#define DFD_DWF_BF16LDS 0
+#endif
+
 namespace dfd {
 
 template <int TH, int TW> constexpr bool dwf_pf() {
@@ -20,7 +26,8 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
                                                      T* __restrict__ Y, Pro pro, float* __restrict__ stats, int ntiles,
                                                      int groups, int tiles_x, int tiles_y) {
   using D = DwT<TH, TW, K, S>;
-  __shared__ __attribute__((aligned(16))) float tin[D::NIN * DCG];
+  using LT = std::conditional_t<(DFD_DWF_BF16LDS != 0 && S == 2 && sizeof(T) == 2), bf16, float>;
+  __shared__ __attribute__((aligned(16))) LT tin[D::NIN * DCG];
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];
   const int tid = threadIdx.x, vec = tid & 3, tp = tid >> 2;
   const int grp = blockIdx.x % groups;
@@ -105,7 +112,7 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
       }
     }
   }
-  if constexpr (STATS) reduce_write_stats(st_s, st_q, tin, stats + (int64_t)(blockIdx.x / groups) * 2 * C, C, c0);
+  if constexpr (STATS) reduce_write_stats(st_s, st_q, reinterpret_cast<float*>(tin), stats + (int64_t)(blockIdx.x / groups) * 2 * C, C, c0);
 }
 
 template <typename T, int TH, int TW, int K, int S>
