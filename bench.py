@@ -4,39 +4,88 @@ One step = the reference train step (``EnsembleTrainer.train_epoch``,
 src/ensemble_trainer.py:182-200) on one synthetic batch of 32 clips x 8 frames x 224x224x3
 per GPU: HIP forward (trunk + temporal-attention head, dropout 0.5), weighted CE, HIP
 backward, clip_grad_norm_(1.0) + AdamW(lr 1e-4, wd 1e-5) fused -- with every input already
-resident in HBM.  N GPUs = N ranks (torch.distributed, RCCL), clips sharded, bucketed
-gradient all-reduce overlapped with backward; value = frames of all ranks / max-over-ranks
-time.  Rank 0 prints one JSON line.
+resident in HBM.  N GPUs = N ranks (one process per GPU, torch.distributed over RCCL), clips
+sharded, bucketed gradient all-reduce overlapped with backward; value = frames of all ranks /
+max-over-ranks time.  Rank 0 prints one JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32] [--no-cpu-baseline]
+
+``--gpus N`` without a launcher: this process spawns ``torch.distributed.run`` with N ranks on
+127.0.0.1 BEFORE touching the GPU and exits with its status (the driver's own
+``torch.distributed.run ... bench.py --gpus N`` arrives with WORLD_SIZE=N and runs directly).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-import deepfake_amd  # noqa: E402,F401
-from deepfake_amd import roofline  # noqa: E402
-from deepfake_amd.pretrained_detector import PretrainedBackboneDetector  # noqa: E402
-from deepfake_amd.trainer import DataParallelTrainer  # noqa: E402
-from deepfake_amd.weights import deterministic_init_  # noqa: E402
-
 CLIPS, T, H, W = 32, 8, 224, 224
 METRIC = "face-frames/sec training EfficientNet-B0 224² bs=256/GPU"
+# SURVEY.md §8(d): algorithmic HBM bytes of one 256-frame bf16/fp16 train step (every conv layer's
+# fwd X+Y+W, dgrad dY+W+dX, wgrad X+dY+dW; BN/SiLU/SE assumed fused) -> 2.69 ms floor at 8 TB/s
+STEP_BYTES_256 = 21.53e9
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline: timed steps of 32 frames, all threads")
+    ap.add_argument("--no-dp-exposure", action="store_true", help="skip the comm-off timing pass (N > 1)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher/rendezvous self-test on CPU (gloo): ranks report and exit, no GPU use")
+    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
+                    help="kernel-selection knob for A/B runs (dfd_set_tuning), e.g. dw_bwd_pre=2")
+    return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """Re-run this script under torch.distributed.run with n ranks (child processes; this process
+    never initialises the GPU, so no exec-after-GPU-init hazard)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(world, rank, local):
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank)])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "rank_sum": float(t.item()),
+                          "expected": float(sum(range(world)))}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def synthetic_batch(rank: int, device):
     """uint8 frames (seed 0+rank) -> /255 -> ImageNet normalise (app.py:1772-1780), NHWC storage
     viewed as (B, T, 3, H, W) like the reference's permute; labels Bernoulli(0.5) seed 1."""
+    import torch
+
     g = torch.Generator(device=device)
     g.manual_seed(0 + rank)
     u8 = torch.randint(0, 256, (CLIPS, T, H, W, 3), generator=g, device=device, dtype=torch.uint8)
@@ -49,52 +98,100 @@ def synthetic_batch(rank: int, device):
     return x, labels
 
 
-def cpu_baseline(seconds: float = 15.0):
-    """The oracle's fp32 PyTorch-CPU restatement of the same step (oracle/detector_cpu.py), on a bounded
-    sample: 2 clips x 8 frames of 224^2 per step, timed for ~`seconds`."""
-    from oracle import detector_cpu
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+
+def _physical_cores():
+    try:
+        pairs = set()
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                core = line.split(":")[1].strip()
+                pairs.add((phys, core))
+        return len(pairs) or None
+    except OSError:
+        return None
+
+
+def cpu_baseline(steps: int):
+    """SURVEY §8(d) CPU baseline: the oracle's fp32 PyTorch-CPU restatement of the same step recipe
+    (fwd, weighted CE, backward, clip_grad_norm_(1.0), AdamW; oracle/detector_cpu.py) -- the
+    reference's own B0 path cannot run (timm is absent and reference code does not travel).
+    bs=32 frames (4 clips x 8) x `steps` timed steps on all threads of this GPU's CPU share, plus
+    one timed 32-frame step on 1 thread (the app's TORCH_NUM_THREADS=1 default, app.py:103)."""
+    import torch
+
+    from oracle import detector_cpu
+    from deepfake_amd.weights import deterministic_init_
+
+    nproc = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or nproc
+    threads = max(1, min(share, nproc))
+    clips = 4
     torch.manual_seed(0)
     m = detector_cpu.DetectorCPU(dropout_rate=0.5)
     deterministic_init_(m, seed=0)
     m.train()
     opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-5)
-    x = torch.randn(2, 8, 3, H, W)
-    y = torch.tensor([0, 1])
-    detector_cpu.train_step(m, x, y, opt)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        detector_cpu.train_step(m, x, y, opt)
-        n += 1
-        if time.perf_counter() - t0 >= seconds:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(n * 16 / dt, 3), "unit": "face-frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} steps x 16 frames (2 clips x 8) 224^2, fp32, oracle/detector_cpu.py train_step "
-                      f"(AdamW+clip), torch {torch.__version__} threads={threads}"}
+    x = torch.randn(clips, T, 3, H, W)
+    y = torch.tensor([0, 1] * (clips // 2))
+
+    def run(nthreads, n):
+        torch.set_num_threads(nthreads)
+        detector_cpu.train_step(m, x, y, opt)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(n):
+            detector_cpu.train_step(m, x, y, opt)
+        return n * clips * T / (time.perf_counter() - t0)
+
+    fps = run(threads, steps)
+    fps1 = run(1, 1)
+    torch.set_num_threads(threads)
+    return {"value": round(fps, 3), "unit": "face-frames/s", "cores": threads, "kind": "port",
+            "value_1thread": round(fps1, 3),
+            "sample": f"{steps} timed steps x 32 frames (4 clips x 8) 224^2 fp32 on {threads} threads + 1 step on "
+                      f"1 thread; oracle/detector_cpu.py train_step (weighted CE, clip 1.0, AdamW), torch "
+                      f"{torch.__version__}",
+            "cpu_model": _cpu_model(), "nproc": nproc, "physical_cores": _physical_cores()}
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
-                    help="kernel-selection knob for A/B runs (dfd_set_tuning), e.g. dw_bwd_pre=2")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run "
+                         f"as {args.gpus} GPUs")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.launch_check:
+        return launch_check(world, rank, local)
+
+    import torch
+    import torch.distributed as dist
+
+    import deepfake_amd  # noqa: F401
+    from deepfake_amd import roofline
+    from deepfake_amd.pretrained_detector import PretrainedBackboneDetector
+    from deepfake_amd.trainer import DataParallelTrainer
+    from deepfake_amd.weights import deterministic_init_
+
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     if args.tune:
         from deepfake_amd import _lib
@@ -110,51 +207,82 @@ def main():
     step = DataParallelTrainer(model, lr=1e-4, weight_decay=1e-5, max_grad_norm=1.0,
                                class_weights=torch.tensor([1.0, 1.0]))
     x, labels = synthetic_batch(rank, dev)
-    probe = roofline.KernelProbe(model, "dw_fwd", stage=1, block=0)
+    # the dominant launch of the step: the fused depthwise backward of blocks.1.0
+    # (dw_bwd<16,16,3,2>, 112x112x96 <- 56x56x96, the largest single kernel in the rocprof trace)
+    probe = roofline.KernelProbe(model, "dw_bwd", stage=1, block=0)
+
+    def timed(n, arm=False):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if arm:
+            probe.arm(n)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step(x, labels)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        if arm:
+            probe.disarm()
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el.item())
 
     for _ in range(args.warmup):
         step(x, labels)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    probe.arm(args.steps)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(x, labels)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    probe.disarm()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = timed(args.steps, arm=True)
     loss, _ = step.forward_backward(x, labels)
     finite = bool(torch.isfinite(loss).item())
+    step.sync_grads()
+
+    dp = None
+    if world > 1:
+        nb = len(step.bucket_log)
+        local_el = None
+        if not args.no_dp_exposure:
+            step.comm_enabled = False  # same step, no all-reduce: what the exchange costs on top
+            local_el = timed(args.steps)
+            step.comm_enabled = True
+        ms, ms_local = 1000 * elapsed / args.steps, (1000 * local_el / args.steps if local_el else None)
+        dp = {"buckets_per_step": nb, "bucket_elems": step.bucket_elems,
+              "grad_bytes": int(model._flat_p.numel() * 4), "ms_per_step_no_allreduce": ms_local and round(ms_local, 3),
+              "allreduce_exposed_ms": None if ms_local is None else round(ms - ms_local, 3),
+              "backend": dist.get_backend()}
 
     frames = CLIPS * T * world * args.steps
     value = frames / elapsed
     if rank == 0:
         rl = probe.report()
+        es = 2 if args.dtype == "bf16" else 4
+        step_bytes = STEP_BYTES_256 * es / 2
+        ms_step = 1000 * elapsed / args.steps
+        if rl is not None:
+            rl["step"] = {"algorithmic_bytes": step_bytes, "achieved": round(step_bytes / (ms_step / 1e3) / 1e9, 1),
+                          "frac": round(step_bytes / (ms_step / 1e3) / roofline.HBM_PEAK, 4),
+                          "floor_ms": round(step_bytes / roofline.HBM_PEAK * 1e3, 3),
+                          "source": "SURVEY.md §8(d) algorithmic bytes per 256-frame step"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds)
+            cpu = cpu_baseline(args.cpu_steps)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "face-frames/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic uint8 frames (seeded, on device) -> ImageNet-normalised fp32, random-init weights",
+            "data": "synthetic uint8 frames (seeded 0+rank, on device) -> ImageNet-normalised fp32, random-init weights",
             "config": {"workload": "EfficientNet-B0 detector train step (PretrainedBackboneDetector, temporal "
                                    "attention head, weighted CE, clip 1.0 + AdamW)",
                        "clips_per_gpu": CLIPS, "frames_per_clip": T, "frames_per_gpu": CLIPS * T,
                        "global_frames": CLIPS * T * world, "image": [H, W, 3], "parallelism": f"dp{world}"},
             "loss_finite": finite,
             "roofline": rl,
+            "dp": dp,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -48,26 +48,51 @@ class _FusedAdamBase(torch.optim.Optimizer):
         n = self._flat_p.numel()
         self._m = torch.zeros(n, dtype=torch.float32, device=dev)
         self._v = torch.zeros(n, dtype=torch.float32, device=dev)
-        self._step_count = 0
-        self._norm = torch.zeros(2, dtype=torch.float32, device=dev)
-        self._scratch = torch.empty(1024, dtype=torch.float64, device=dev)
+        # per-parameter step counts, as torch.optim keeps them (a parameter without a gradient is
+        # skipped: no decay, no moment update, no step -- torch/optim/adamw.py semantics)
+        self._steps = [0] * len(ps)
+        self._offs = []
         o = 0
         for p in ps:
-            k = p.numel()
-            self.state[p] = {"exp_avg": self._m[o:o + k].view(p.shape), "exp_avg_sq": self._v[o:o + k].view(p.shape)}
-            o += k
+            self._offs.append(o)
+            o += p.numel()
+        self._norm = torch.zeros(2, dtype=torch.float32, device=dev)
+        self._scratch = torch.empty(1024, dtype=torch.float64, device=dev)
+        self._bind_state()
 
-    def _flat_grad(self):
+    def _bind_state(self):
+        """``self.state[p]`` holds views of the flat moment buffers (what the kernel updates)."""
+        for i, p in enumerate(self.param_groups[0]["params"]):
+            o, k = self._offs[i], p.numel()
+            self.state[p] = {"step": torch.tensor(float(self._steps[i])),
+                             "exp_avg": self._m[o:o + k].view(p.shape), "exp_avg_sq": self._v[o:o + k].view(p.shape)}
+
+    @property
+    def _step_count(self) -> int:
+        return max(self._steps) if self._steps else 0
+
+    def _active_ranges(self):
+        """[(lo, hi, first_param, last_param+1)] of consecutive parameters that have a gradient and the
+        same step count (one range -- the whole buffer -- in the usual case)."""
         ps = self.param_groups[0]["params"]
+        out = []
+        for i, p in enumerate(ps):
+            if p.grad is None or not p.requires_grad:
+                continue
+            lo, hi = self._offs[i], self._offs[i] + p.numel()
+            if out and out[-1][1] == lo and self._steps[out[-1][2]] == self._steps[i]:
+                out[-1] = (out[-1][0], hi, out[-1][2], i + 1)
+            else:
+                out.append((lo, hi, i, i + 1))
+        return out
+
+    def _grad_range(self, i0, i1):
+        """Flat view of the gradients of parameters [i0, i1) (gathered when they are not one buffer)."""
+        ps = self.param_groups[0]["params"][i0:i1]
         gs = [p.grad for p in ps]
-        if any(g is None for g in gs):
-            gs = [torch.zeros_like(p) if p.grad is None else p.grad for p in ps]
-            for p, g in zip(ps, gs):
-                p.grad = g
         flat = _flat_view(gs)
-        if flat is None:  # gradients not adopted from one flat sink: gather once, scatter back below
-            flat = torch.cat([g.reshape(-1) for g in gs])
-            return flat, gs
+        if flat is None:
+            return torch.cat([g.reshape(-1) for g in gs]), gs
         return flat, None
 
     @torch.no_grad()
@@ -78,27 +103,57 @@ class _FusedAdamBase(torch.optim.Optimizer):
                 loss = closure()
         g = self.param_groups[0]
         lib = _lib.load()
-        flat_g, scatter = self._flat_grad()
-        dev = flat_g.device
+        ranges = self._active_ranges()
+        if not ranges:
+            return loss
+        grads = [self._grad_range(r[2], r[3]) for r in ranges]
+        dev = self._flat_p.device
         stream = _lib.stream_of(dev)
-        n = flat_g.numel()
         clip = None
         if self.max_grad_norm is not None:
-            _lib.check(lib.dfd_grad_norm(stream, flat_g.data_ptr(), n, float(self.max_grad_norm),
+            allg = grads[0][0] if len(grads) == 1 else torch.cat([fg for fg, _ in grads])
+            _lib.check(lib.dfd_grad_norm(stream, allg.data_ptr(), allg.numel(), float(self.max_grad_norm),
                                          self._scratch.data_ptr(), self._norm.data_ptr()))
             clip = self._norm.data_ptr()
-        self._step_count += 1
         b1, b2 = g["betas"]
-        _lib.check(lib.dfd_adam_step(stream, self._flat_p.data_ptr(), flat_g.data_ptr(), self._m.data_ptr(),
-                                     self._v.data_ptr(), n, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                     float(g["weight_decay"]), self._step_count, float(self.grad_scale),
-                                     1 if self.decoupled else 0, clip))
-        if scatter is not None:
-            o = 0
-            for t in scatter:
-                t.copy_(flat_g[o:o + t.numel()].view(t.shape))
-                o += t.numel()
+        for (lo, hi, i0, i1), (flat_g, scatter) in zip(ranges, grads):
+            step = self._steps[i0] + 1
+            for i in range(i0, i1):
+                self._steps[i] = step
+            _lib.check(lib.dfd_adam_step(stream, self._flat_p[lo:hi].data_ptr(), flat_g.data_ptr(),
+                                         self._m[lo:hi].data_ptr(), self._v[lo:hi].data_ptr(), hi - lo, float(g["lr"]),
+                                         float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), step,
+                                         float(self.grad_scale), 1 if self.decoupled else 0, clip))
+            if scatter is not None:  # gradients were gathered: leave the clipped values in .grad
+                o = 0
+                for t in scatter:
+                    t.copy_(flat_g[o:o + t.numel()].view(t.shape))
+                    o += t.numel()
         return loss
+
+    # -- checkpoints: torch.optim.Adam(W)-format state ({step, exp_avg, exp_avg_sq} per parameter), so
+    # a resume (src/train.py:349-387,401) works across this optimizer and torch's in both directions
+    def state_dict(self):
+        for i, p in enumerate(self.param_groups[0]["params"]):
+            self.state[p]["step"] = torch.tensor(float(self._steps[i]))
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)  # casts moments to the parameters' device/dtype
+        ps = self.param_groups[0]["params"]
+        with torch.no_grad():
+            for i, p in enumerate(ps):
+                st = self.state.get(p, {})
+                o, k = self._offs[i], p.numel()
+                if "exp_avg" in st:
+                    self._m[o:o + k].copy_(st["exp_avg"].reshape(-1))
+                    self._v[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+                    self._steps[i] = int(float(st.get("step", 0)))
+                else:
+                    self._m[o:o + k].zero_()
+                    self._v[o:o + k].zero_()
+                    self._steps[i] = 0
+        self._bind_state()
 
     @property
     def last_grad_norm(self) -> torch.Tensor:

@@ -5,6 +5,8 @@ output, weights once; BN/SiLU/SE applied in the consumers' prologues so they add
 
 * depthwise fwd:   es*(N*Hin*Win*C + N*Ho*Wo*C) + 4*k*k*C          (dgrad: same tensors swapped)
 * depthwise wgrad: es*(N*Ho*Wo*C + N*Hin*Win*C) + 4*k*k*C
+* fused depthwise backward (dgrad + producer BN/SiLU backward + wgrad in one pass):
+                   es*(2*N*Hin*Win*C + N*Ho*Wo*C) + 8*k*k*C
 * 1x1 fwd/dgrad:   es*(M*K + M*N) + es*N*K,  flops 2*M*N*K
 * 1x1 wgrad:       es*(M*N + M*K) + 4*N*K
 * SE squeeze:      es*M*C
@@ -23,7 +25,9 @@ from . import _lib
 HBM_PEAK = 8.0e12
 MFMA_BF16_PEAK = 2.5e15
 KINDS = {"pw_fwd": 0, "dw_fwd": 1, "pwl_fwd": 2, "dw_dgrad": 3, "dw_wgrad": 4, "pw_dgrad": 5, "pw_wgrad": 6,
-         "pwl_dgrad": 7, "pwl_wgrad": 8, "se_squeeze": 9}
+         "pwl_dgrad": 7, "pwl_wgrad": 8, "se_squeeze": 9,
+         # the fused depthwise backward (k_dw_bwd.hip) is launched at the dgrad site
+         "dw_bwd": 3}
 _ARCH = [(1, 1, 3, 1, 1, 16), (0, 2, 3, 2, 6, 24), (0, 2, 5, 2, 6, 40), (0, 3, 3, 2, 6, 80), (0, 3, 5, 1, 6, 112),
          (0, 4, 5, 2, 6, 192), (0, 1, 3, 1, 6, 320)]
 
@@ -51,6 +55,8 @@ def algorithmic(kind: str, stage: int, idx: int, frames: int, H: int, W: int, es
     g = block_geometry(H, W)[(stage, idx)]
     Mi, Mo = frames * g["hin"] * g["win"], frames * g["hout"] * g["wout"]
     C, k = g["mid"], g["k"]
+    if kind == "dw_bwd":  # reads dY (out map) and the producer's y (in map), writes dX (in map); dW fp32
+        return es * (2 * Mi * C + Mo * C) + 8 * k * k * C, 4 * Mo * C * k * k
     if kind in ("dw_fwd", "dw_dgrad", "dw_wgrad"):
         return es * (Mi * C + Mo * C) + 4 * k * k * C, 2 * Mo * C * k * k
     if kind == "se_squeeze":

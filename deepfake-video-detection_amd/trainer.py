@@ -25,9 +25,11 @@ from .optim import FusedAdam, FusedAdamW
 
 class TrainStep:
     def __init__(self, model, lr=1e-4, weight_decay=1e-5, class_weights=None, max_grad_norm=1.0,
-                 optimizer="adamw", world_size: int = 1):
+                 optimizer="adamw", world_size: int = 1, criterion=None):
         self.model = model
-        self.criterion = WeightedCrossEntropyLoss(weight=class_weights)
+        # the reference trainers hand the criterion in (ensemble_trainer.py:358 -> train_epoch); default:
+        # the HIP weighted cross entropy
+        self.criterion = criterion if criterion is not None else WeightedCrossEntropyLoss(weight=class_weights)
         cls = FusedAdamW if optimizer == "adamw" else FusedAdam
         self.optimizer = cls(model.parameters(), lr=lr, weight_decay=weight_decay, max_grad_norm=max_grad_norm)
         self.world_size = world_size
@@ -61,6 +63,8 @@ class DataParallelTrainer(TrainStep):
         self._works = []
         self._pending = None  # (lo, hi) accumulated but not yet launched
         self._flat = None
+        self.comm_enabled = True  # False: skip the exchange (bench's comm-off timing pass only)
+        self.bucket_log = []  # (lo, hi) of the buckets launched by the last backward
         if ws > 1:
             self._broadcast_params()
             model.register_grad_ready_hook(self._on_ready)
@@ -71,10 +75,28 @@ class DataParallelTrainer(TrainStep):
             dist.broadcast(self.model._flat_b, src=0, group=self.pg)
 
     def _launch(self, flat, lo, hi):
+        self.bucket_log.append((lo, hi))
         self._works.append(dist.all_reduce(flat[lo:hi], op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+
+    def _check_adoption(self):
+        """The buckets are all-reduced in the GradSink buffer while backward runs; that is only the
+        gradient if autograd ADOPTS the sink views as ``p.grad``, i.e. every ``p.grad`` is None when
+        backward starts.  An existing ``.grad`` (``zero_grad(set_to_none=False)``, gradient
+        accumulation) would be added to the unreduced view instead -- refuse that loudly."""
+        stale = [n for n, p in self.model.named_parameters() if p.requires_grad and p.grad is not None]
+        if stale:
+            raise RuntimeError(
+                f"DataParallelTrainer: {len(stale)} parameters (e.g. {stale[0]}) already hold a .grad at backward; "
+                "the overlapped all-reduce needs zero_grad(set_to_none=True) before every backward "
+                "(gradient accumulation is not supported)")
 
     def _on_ready(self, flat, lo, hi):
         # segments arrive in reverse order of the flat layout: merge adjacent ranges into buckets
+        if not self.comm_enabled:
+            return
+        if self._pending is None and not self._works:  # first segment of this backward
+            self._check_adoption()
+            self.bucket_log = []
         self._flat = flat
         if self._pending is None:
             self._pending = (lo, hi)
@@ -88,7 +110,7 @@ class DataParallelTrainer(TrainStep):
             self._pending = None
 
     def sync_grads(self):
-        if self.world_size <= 1:
+        if self.world_size <= 1 or not self.comm_enabled:
             return
         if self._pending is not None:
             self._launch(self._flat, *self._pending)

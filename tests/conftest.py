@@ -38,3 +38,21 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=["default", "forced", "split_dw"])
+def kernel_paths(request):
+    """Run a test with the production kernel selection ("default": the streaming 1x1 kernels and the
+    BN-folded conv_pw backward only on >= 100K-row layers, fused depthwise backward), with the first
+    two forced onto every covered layer ("forced", so the small parity shapes exercise the
+    high-resolution code paths too), and with the depthwise backward as two kernels ("split_dw")."""
+    from deepfake_amd import _lib
+    lib = _lib.load()
+    knobs = {"default": {}, "forced": {b"stream_min_rows": 0, b"fold_min_rows": 0},
+             "split_dw": {b"dw_bwd_fused": 0}}[request.param]
+    prev = {k: lib.dfd_set_tuning(k, v) for k, v in knobs.items()}
+    try:
+        yield request.param
+    finally:
+        for k, v in prev.items():
+            lib.dfd_set_tuning(k, v)

@@ -1,16 +1,20 @@
-"""Turn the PMC passes of tools/pmc_traffic.sh into profiles/traffic.json (read by bench.py).
+"""Turn the PMC passes of tools/pmc_calib.sh into profiles/traffic.json (read by bench.py).
 
-The probed launch is dw_fwd of blocks.1.0 (112x112x96 -> 56x56x96, k3 s2, bf16): kernel
-dw_fwd_kernel<bf16, 8, 8, 3, 2, true, ...> on a persistent grid sized to the co-resident
-workgroups; no other B0 layer uses that instance (the other stride-2 maps are not multiples of 8).  Units: FETCH_SIZE / WRITE_SIZE are KiB.  The guide (MI355X_MICROARCH.md §HBM)
-documents FETCH_SIZE = RDREQ x 64 B, i.e. HALF the bytes of wide coalesced reads that issue
-128-B requests.  This kernel's reads are 64-B requests -- each workgroup loads one 32-channel
-bf16 slice (64 B) per pixel, the other channel groups of the pixel belong to neighbouring
-workgroups -- so the raw FETCH_SIZE is taken as bytes (the input window of an 8x8 s2 tile is
-17x17 pixels, a halo re-read of 17^2/16^2 = 1.13x; L2 absorbs part of it); the doubled value is
-recorded next to it.  WRITE_SIZE is exact for 16-B-per-lane stores.
+Calibration (tools/fetch_calib.hip, every byte of a 616.6 MB NHWC bf16 [256*112*112][96] tensor
+read or written once per dispatch; the tensor exceeds the 256 MiB Infinity Cache):
 
-usage: python tools/pmc_traffic.py gpurun_out/pmc_traffic [profiles/traffic.json]
+  mode 0  contiguous 16 B/lane read      -> FETCH_SIZE = 0.5 x bytes  (MI355X_MICROARCH.md §HBM)
+  mode 1  64-B channel slices, 16 B/lane -> FETCH_SIZE = 1.0 x bytes
+  mode 2  64-B channel slices,  8 B/lane -> FETCH_SIZE = 1.0 x bytes
+  mode 3/4  slice / contiguous writes    -> WRITE_SIZE = 1.0 x bytes
+
+The probed launch (dw_bwd<bf16,16,16,3,2> of blocks.1.0, C = 96) reads 64-B slices of 32
+channels (one channel group per workgroup, pixels 192 B apart), i.e. the mode-1 pattern, so its
+FETCH_SIZE is divided by the mode-1 factor.  (Layers with C = 32 -- blocks.0.0 -- read adjacent
+64-B slices that merge into 128-B requests and count like mode 0: that is the round-1
+"279 MB fetched vs 411 MB algorithmic" reading of dw_bwd<16,16,3,1>.)
+
+usage: python tools/pmc_traffic.py gpurun_out/pmc_calib [profiles/traffic.json]
 """
 import csv
 import glob
@@ -19,36 +23,52 @@ import os
 import statistics
 import sys
 
-NAME = "dw_fwd_kernel<dfd::bf16, 8, 8, 3, 2, true"
+PROBE = ("dw_bwd:1.0", "dw_bwd_kernel<dfd::bf16, 16, 16, 3, 2, 8", 1)  # key, kernel name, calibration mode
+KNOWN = 256 * 112 * 112 * 96 * 2
 
 
-def values(d, counter):
-    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+def _csv(d):
+    return glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+
+
+def values(d, counter, name_sub):
     out = []
-    for r in csv.DictReader(open(f)):
-        if NAME in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            out.append(float(r["Counter_Value"]))
+    for r in csv.DictReader(open(_csv(d))):
+        if name_sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            out.append(float(r["Counter_Value"]) * 1024)
     return out
+
+
+def factor(d, mode, counter, kernel):
+    v = values(os.path.join(d, f"calib_{mode}"), counter, kernel)
+    return statistics.median(v) / KNOWN
 
 
 def main():
     d = sys.argv[1]
     dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/traffic.json"
-    fe = values(os.path.join(d, "fetch"), "FETCH_SIZE")
-    wr = values(os.path.join(d, "write"), "WRITE_SIZE")
-    fetch = statistics.median(fe) * 1024
-    write = statistics.median(wr) * 1024
-    ent = {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch),
-           "fetch_bytes_if_128B_requests_x2": round(2 * fetch),
-           "write_bytes": round(write), "fetch_size_kib_raw": statistics.median(fe),
-           "write_size_kib_raw": statistics.median(wr), "dispatches": [len(fe), len(wr)],
-           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel trace only); "
-                     "64-B read requests -> raw FETCH_SIZE taken as bytes (see tools/pmc_traffic.py)",
-           "algorithmic_bytes": 2 * (256 * 112 * 112 * 96 + 256 * 56 * 56 * 96) + 4 * 9 * 96}
+    key, name, mode = PROBE
+    calib = {"fetch_contig16": factor(d, 0, "FETCH_SIZE", "k_contig"),
+             "fetch_slice64_16B": factor(d, 1, "FETCH_SIZE", "k_slice16"),
+             "fetch_slice64_8B": factor(d, 2, "FETCH_SIZE", "k_slice8"),
+             "write_slice64": factor(d, 3, "WRITE_SIZE", "k_wslice16"),
+             "write_contig16": factor(d, 4, "WRITE_SIZE", "k_wcontig")}
+    fe = values(os.path.join(d, "fetch"), "FETCH_SIZE", name)
+    wr = values(os.path.join(d, "write"), "WRITE_SIZE", name)
+    fetch = statistics.median(fe) / calib["fetch_slice64_16B"]
+    write = statistics.median(wr) / calib["write_slice64"]
+    alg = 2 * (2 * 256 * 112 * 112 * 96 + 256 * 56 * 56 * 96) + 8 * 9 * 96
+    ent = {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
+           "fetch_size_raw_bytes": statistics.median(fe), "write_size_raw_bytes": statistics.median(wr),
+           "calibration": {k: round(v, 4) for k, v in calib.items()},
+           "dispatches": [len(fe), len(wr)], "algorithmic_bytes": alg,
+           "traffic_over_algorithmic": round((fetch + write) / alg, 4),
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one counter per pass, kernel trace only; FETCH divided "
+                     "by the measured factor of the same 64-B channel-slice read pattern (tools/fetch_calib.hip)"}
     db = json.load(open(dst)) if os.path.exists(dst) else {}
-    db["dw_fwd:1.0"] = ent
+    db[key] = ent
     json.dump(db, open(dst, "w"), indent=1)
-    print(json.dumps(ent))
+    print(json.dumps(ent, indent=1))
 
 
 if __name__ == "__main__":
