@@ -33,6 +33,7 @@ def _bare_trainer(bucket_elems):
     tr.bucket_elems = bucket_elems
     tr._works, tr._pending, tr._flat = [], None, None
     tr.model = torch.nn.Module()  # no parameters: the adoption check has nothing to inspect
+    tr.comm_enabled, tr.bucket_log = True, []
     return tr
 
 
