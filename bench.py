@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--input", default="uint8", choices=["uint8", "fp32"],
+                    help="frames handed to the model: raw uint8 crops (normalised in the stem) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline: timed steps of 32 frames, all threads")
     ap.add_argument("--no-dp-exposure", action="store_true", help="skip the comm-off timing pass (N > 1)")
@@ -81,17 +83,22 @@ def launch_check(world, rank, local):
         dist.destroy_process_group()
 
 
-def synthetic_batch(rank: int, device):
-    """uint8 frames (seed 0+rank) -> /255 -> ImageNet normalise (app.py:1772-1780), NHWC storage
-    viewed as (B, T, 3, H, W) like the reference's permute; labels Bernoulli(0.5) seed 1."""
+def synthetic_batch(rank: int, device, fmt="uint8"):
+    """uint8 face crops (seed 0+rank), NHWC storage viewed as (B, T, 3, H, W) like the reference's
+    permute; labels Bernoulli(0.5) seed 1.  "uint8": the crops go to the model as they
+    come out of the .npz feed and the app's /255 + ImageNet normalisation (app.py:1772-1780) runs in
+    the stem kernel (bit-identical, tests/test_serving.py); "fp32": normalised by torch first."""
     import torch
 
     g = torch.Generator(device=device)
     g.manual_seed(0 + rank)
     u8 = torch.randint(0, 256, (CLIPS, T, H, W, 3), generator=g, device=device, dtype=torch.uint8)
-    mean = torch.tensor([0.485, 0.456, 0.406], device=device)
-    std = torch.tensor([0.229, 0.224, 0.225], device=device)
-    x = ((u8.float() / 255.0) - mean) / std
+    if fmt == "uint8":
+        x = u8
+    else:
+        mean = torch.tensor([0.485, 0.456, 0.406], device=device)
+        std = torch.tensor([0.229, 0.224, 0.225], device=device)
+        x = ((u8.float() / 255.0) - mean) / std
     x = x.permute(0, 1, 4, 2, 3)  # (B, T, 3, H, W), channels-last strides
     g.manual_seed(1 + 1000 * rank)
     labels = torch.randint(0, 2, (CLIPS,), generator=g, device=device)
@@ -206,7 +213,7 @@ def main():
     model = model.to(dev).train()
     step = DataParallelTrainer(model, lr=1e-4, weight_decay=1e-5, max_grad_norm=1.0,
                                class_weights=torch.tensor([1.0, 1.0]))
-    x, labels = synthetic_batch(rank, dev)
+    x, labels = synthetic_batch(rank, dev, args.input)
     # the dominant launch of the step: the fused depthwise backward of blocks.1.0
     # (dw_bwd<16,16,3,2>, 112x112x96 <- 56x56x96, the largest single kernel in the rocprof trace)
     probe = roofline.KernelProbe(model, "dw_bwd", stage=1, block=0)
@@ -272,7 +279,8 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "face-frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic uint8 frames (seeded 0+rank, on device) -> ImageNet-normalised fp32, random-init weights",
+            "data": (f"synthetic uint8 face crops (seeded 0+rank, on device), {args.input} frames into the model "
+                     "(uint8: ImageNet normalisation inside the stem kernel), random-init weights"),
             "config": {"workload": "EfficientNet-B0 detector train step (PretrainedBackboneDetector, temporal "
                                    "attention head, weighted CE, clip 1.0 + AdamW)",
                        "clips_per_gpu": CLIPS, "frames_per_clip": T, "frames_per_gpu": CLIPS * T,

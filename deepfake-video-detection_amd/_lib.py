@@ -39,6 +39,11 @@ _SIGS = {
     "dfd_b0_bind": (c_i, [c_p, ctypes.POINTER(c_i64), c_i]),
     "dfd_b0_forward": (c_i, [c_p, c_p, c_p, ctypes.POINTER(c_i64), c_p, c_p, c_p, c_p, c_i, c_f]),
     "dfd_b0_backward": (c_i, [c_p, c_p, c_p, ctypes.POINTER(c_i64), c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i]),
+    "dfd_b0_forward_ex": (c_i, [c_p, c_p, c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_f), c_p, c_p, c_p, c_p,
+                                c_i, c_f]),
+    "dfd_b0_backward_ex": (c_i, [c_p, c_p, c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_f), c_p, c_p, c_p, c_p,
+                                 c_i, c_i, c_i, c_i]),
+    "dfd_b0_plan_set_tuning": (c_i, [c_p, ctypes.c_char_p, c_i64]),
     "dfd_b0_segment_count": (c_i, []),
     "dfd_b0_saved_tensor": (c_i, [c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "dfd_b0_probe_arm": (c_i, [c_p, c_i, c_i, c_i, c_i]),
@@ -52,6 +57,7 @@ _SIGS = {
     "dfd_ce_forward": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i64, c_p, c_p]),
     "dfd_ce_backward": (c_i, [c_p, c_p, c_p, c_p, c_i, c_i, c_i64, c_p, c_p, c_p]),
     "dfd_grad_norm": (c_i, [c_p, c_p, c_i64, c_f, c_p, c_p]),
+    "dfd_collate_frames": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i, c_p]),
     "dfd_adam_step": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_i, c_d, c_i, c_p]),
     "dfd_set_tuning": (c_i64, [ctypes.c_char_p, c_i64]),
     "dfd_pw_conv": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p,

@@ -27,6 +27,12 @@ BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 FEATURE_DIM = 1280
 DTYPES = {"fp32": 0, "float32": 0, torch.float32: 0, "bf16": 1, "bfloat16": 1, torch.bfloat16: 1}
+INPUT_F32, INPUT_U8 = 0, 1
+# normalisation applied in the stem to uint8 frames: ((v / 255) - mean) / std
+NORMALIZATIONS = {
+    "imagenet": ((0.485, 0.456, 0.406), (0.229, 0.224, 0.225)),  # app.imagenet_normalize (app.py:1772-1780)
+    "unit": ((0.0, 0.0, 0.0), (1.0, 1.0, 1.0)),                  # `.float() / 255.0` only (src/train.py:59)
+}
 
 
 class _Holder(nn.Module):
@@ -68,17 +74,23 @@ def _timm_init_(name: str, t: torch.Tensor) -> None:
 
 
 class EfficientNetB0Trunk(FlatModule):
+    accepts_uint8_frames = True  # raw uint8 crops are normalised inside the stem kernel
     """The 6-child trunk Sequential (conv_stem, bn1, blocks, conv_head, bn2, global_pool).
 
     Args:
-        compute_dtype: activation storage / MFMA dtype of the trunk: ``"bf16"`` (default,
-            fp32 accumulation, fp32 master weights and BN statistics) or ``"fp32"`` (exact
-            fp32 MFMA; the parity mode).
+        compute_dtype: activation storage / MFMA dtype of the trunk: ``"fp32"`` (default: exact
+            fp32 MFMA, the reference's arithmetic within the north-star tolerance) or ``"bf16"``
+            (fp32 accumulation, fp32 master weights and BN statistics; the training/serving
+            performance mode, bound tested in tests/test_b0_224_gpu.py and tests/test_serving.py).
+        input_normalization: how uint8 frames are normalised inside the stem (``"imagenet"``
+            as app.py:2084-2085, ``"unit"`` = /255 only as src/train.py:59, or ``(mean3, std3)``).
+            fp32 frames are used as given.
     """
 
-    def __init__(self, compute_dtype="bf16"):
+    def __init__(self, compute_dtype="fp32", input_normalization="imagenet"):
         super().__init__()
         self.compute_dtype = compute_dtype
+        self.input_normalization = input_normalization
         self._table = tensor_table()
         for name, kind, shape in self._table:
             *path, leaf = name.split(".")
@@ -167,7 +179,7 @@ class EfficientNetB0Trunk(FlatModule):
         _lib.require_hip(x, "frames")
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected (N, 3, H, W) frames, got {tuple(x.shape)}")
-        if x.dtype != torch.float32:
+        if x.dtype != torch.float32 and x.dtype != torch.uint8:
             x = x.float()
         if owner._flat_p.device != x.device:
             raise RuntimeError(f"frames on {x.device} but weights on {owner._flat_p.device}")
@@ -180,6 +192,8 @@ class EfficientNetB0Trunk(FlatModule):
         if need_grad and x.requires_grad:
             raise NotImplementedError("gradient w.r.t. the input frames is not provided by the HIP trunk")
         dt = DTYPES[self.compute_dtype]
+        if x.dtype == torch.uint8:
+            self.runtime().set_input_norm(self.input_normalization)
         if not need_grad:
             feats, _ = self.runtime().forward(x, owner, dt, training)
             return feats
@@ -195,30 +209,57 @@ class EfficientNetB0Trunk(FlatModule):
 
 
 class B0Runtime:
-    """Per-model plan cache: one native plan per (frames, H, W, dtype, device)."""
+    """Per-model plan cache: one native plan per (frames, H, W, dtype, device).
+
+    Thread-safe: the cache is guarded by a lock (inference may run on a ThreadPoolExecutor worker,
+    app.py:127-129,234, next to other callers), and the native plan serialises the enqueue of
+    concurrent calls itself.  Kernel-selection knobs set through ``set_tuning`` belong to this
+    runtime's plans only (``dfd_b0_plan_set_tuning``); no process-wide state is touched."""
 
     def __init__(self, offsets):
+        import threading
+
         self.lib = _lib.load()
         self.offsets = list(offsets)
         self.plans: dict = {}
+        self.tuning: dict = {}
+        self._lock = threading.Lock()
+        self._norm = (ctypes.c_float * 6)(*NORMALIZATIONS["imagenet"][0], *NORMALIZATIONS["imagenet"][1])
+
+    def set_input_norm(self, spec) -> None:
+        mean, std = NORMALIZATIONS[spec] if isinstance(spec, str) else spec
+        if len(mean) != 3 or len(std) != 3:
+            raise ValueError("input normalisation needs 3 means and 3 stds")
+        self._norm = (ctypes.c_float * 6)(*[float(v) for v in mean], *[float(v) for v in std])
+
+    def set_tuning(self, key: str, value: int) -> None:
+        """Per-runtime kernel-selection override (same keys as dfd_set_tuning)."""
+        with self._lock:
+            self.tuning[key] = int(value)
+            for h in self.plans.values():
+                _lib.check(self.lib.dfd_b0_plan_set_tuning(h, key.encode(), int(value)))
 
     def rebind(self, offsets):
-        self.offsets = list(offsets)
-        arr = (ctypes.c_int64 * len(self.offsets))(*self.offsets)
-        for h in self.plans.values():
-            _lib.check(self.lib.dfd_b0_bind(h, arr, len(self.offsets)))
+        with self._lock:
+            self.offsets = list(offsets)
+            arr = (ctypes.c_int64 * len(self.offsets))(*self.offsets)
+            for h in self.plans.values():
+                _lib.check(self.lib.dfd_b0_bind(h, arr, len(self.offsets)))
 
     def plan(self, frames, H, W, dtype, device):
         key = (frames, H, W, dtype, device.index)
-        h = self.plans.get(key)
-        if h is None:
-            h = ctypes.c_void_p()
-            with torch.cuda.device(device):
-                _lib.check(self.lib.dfd_b0_plan_create(frames, H, W, dtype, ctypes.byref(h)))
-                arr = (ctypes.c_int64 * len(self.offsets))(*self.offsets)
-                _lib.check(self.lib.dfd_b0_bind(h, arr, len(self.offsets)))
-            self.plans[key] = h
-        return h
+        with self._lock:
+            h = self.plans.get(key)
+            if h is None:
+                h = ctypes.c_void_p()
+                with torch.cuda.device(device):
+                    _lib.check(self.lib.dfd_b0_plan_create(frames, H, W, dtype, ctypes.byref(h)))
+                    arr = (ctypes.c_int64 * len(self.offsets))(*self.offsets)
+                    _lib.check(self.lib.dfd_b0_bind(h, arr, len(self.offsets)))
+                    for k, v in self.tuning.items():
+                        _lib.check(self.lib.dfd_b0_plan_set_tuning(h, k.encode(), v))
+                self.plans[key] = h
+            return h
 
     def workspace_bytes(self, h) -> int:
         return int(self.lib.dfd_b0_workspace_bytes(h))
@@ -229,16 +270,19 @@ class B0Runtime:
         ws = torch.empty(self.workspace_bytes(h), dtype=torch.uint8, device=x.device)
         feats = torch.empty(N, FEATURE_DIM, dtype=torch.float32, device=x.device)
         xs = (ctypes.c_int64 * 4)(*x.stride())
-        _lib.check(self.lib.dfd_b0_forward(h, _lib.stream_of(x.device), x.data_ptr(), xs, owner._flat_p.data_ptr(),
-                                           owner._flat_b.data_ptr(), ws.data_ptr(), feats.data_ptr(),
-                                           1 if training else 0, BN_MOMENTUM))
+        fmt = INPUT_U8 if x.dtype == torch.uint8 else INPUT_F32
+        _lib.check(self.lib.dfd_b0_forward_ex(h, _lib.stream_of(x.device), x.data_ptr(), fmt, xs, self._norm,
+                                              owner._flat_p.data_ptr(), owner._flat_b.data_ptr(), ws.data_ptr(),
+                                              feats.data_ptr(), 1 if training else 0, BN_MOMENTUM))
         return feats, (h, ws)
 
     def backward(self, h, ws, x, dfeat, owner, grads, training, seg_begin, seg_end, accumulate=False):
         xs = (ctypes.c_int64 * 4)(*x.stride())
-        _lib.check(self.lib.dfd_b0_backward(h, _lib.stream_of(x.device), x.data_ptr(), xs, dfeat.data_ptr(),
-                                            owner._flat_p.data_ptr(), ws.data_ptr(), grads.data_ptr(),
-                                            1 if training else 0, seg_begin, seg_end, 1 if accumulate else 0))
+        fmt = INPUT_U8 if x.dtype == torch.uint8 else INPUT_F32
+        _lib.check(self.lib.dfd_b0_backward_ex(h, _lib.stream_of(x.device), x.data_ptr(), fmt, xs, self._norm,
+                                               dfeat.data_ptr(), owner._flat_p.data_ptr(), ws.data_ptr(),
+                                               grads.data_ptr(), 1 if training else 0, seg_begin, seg_end,
+                                               1 if accumulate else 0))
 
     def __del__(self):
         try:
@@ -276,22 +320,11 @@ class _TrunkFn(torch.autograd.Function):
         return (None, None, None, None, None, *views)
 
 
-class B0FrameExtractor(nn.Module):
-    """Frame feature extractor for the detector seam (``src/detector.py:88-100``):
-    ``(N, 3, 224, 224) -> (N, 1280)`` = trunk + global average pool."""
-
-    def __init__(self, trunk: EfficientNetB0Trunk | None = None, compute_dtype="bf16"):
-        super().__init__()
-        if trunk is None:
-            trunk = EfficientNetB0Trunk(compute_dtype)
-            trunk._flatten()
-        self.trunk = trunk
-
-    def forward(self, x):
-        return self.trunk(x)
-
-
 class B0FrameExtractor(EfficientNetB0Trunk):
     """Frame feature extractor for the ``DeepfakeDetector(model_type='rnn')`` seam
     (``src/detector.py:88-100``): ``(N, 3, H, W)`` face crops -> ``(N, 1280)`` pooled B0 features,
-    feeding a ``LogicRNNLSTM(input_size=1280)``.  A standalone trunk owning its flat buffers."""
+    feeding a ``LogicRNNLSTM(input_size=1280)``.  A standalone trunk owning its flat buffers.
+    uint8 crops are normalised as the detector does (``/255`` only, ``detector.py:59-60``)."""
+
+    def __init__(self, compute_dtype="fp32", input_normalization="unit"):
+        super().__init__(compute_dtype, input_normalization)

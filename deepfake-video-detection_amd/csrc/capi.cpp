@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -22,8 +23,12 @@ void set_error(const char* msg, const char* file, int line) {
 }
 }  // namespace dfd
 
+// A plan is shared by every call of one model at one shape; its host-side enqueue state
+// (pending BN-stat rows, probe events) is guarded so calls from several threads serialise their
+// ENQUEUE (the kernels still run asynchronously on each caller's stream).
 struct dfd_b0_plan {
   dfd::Plan p;
+  std::mutex mu;
 };
 
 #define DFD_GUARD_BEGIN try {
@@ -82,47 +87,97 @@ int64_t dfd_b0_workspace_bytes(const dfd_b0_plan* plan) { return plan ? plan->p.
 int dfd_b0_bind(dfd_b0_plan* plan, const int64_t* offsets, int n) {
   DFD_GUARD_BEGIN
   if (!plan || !offsets) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  std::lock_guard<std::mutex> lk(plan->mu);
   return dfd::plan_bind(plan->p, offsets, n);
   DFD_GUARD_END
 }
 
-int dfd_b0_forward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* xs, const float* params,
-                   float* bn_buffers, void* workspace, float* features, int training, float momentum) {
+static bool input_fmt(int x_format, const float* norm6, dfd::InputFmt* in) {
+  *in = dfd::InputFmt{};
+  if (x_format == DFD_INPUT_F32) return true;
+  if (x_format != DFD_INPUT_U8) { dfd::set_error("bad input format", __FILE__, __LINE__); return false; }
+  in->u8 = 1;
+  for (int c = 0; c < 3; ++c) {
+    in->mean[c] = norm6 ? norm6[c] : 0.f;
+    in->stdv[c] = norm6 ? norm6[3 + c] : 1.f;
+    if (!(in->stdv[c] != 0.f)) { dfd::set_error("input normalisation: std must be nonzero", __FILE__, __LINE__); return false; }
+  }
+  return true;
+}
+
+int dfd_b0_forward_ex(dfd_b0_plan* plan, void* stream, const void* x, int x_format, const int64_t* xs,
+                      const float* norm6, const float* params, float* bn_buffers, void* workspace, float* features,
+                      int training, float momentum) {
   DFD_GUARD_BEGIN
   if (!plan || !x || !xs || !params || !bn_buffers || !workspace || !features) {
     dfd::set_error("null argument", __FILE__, __LINE__);
     return -1;
   }
-  return dfd::plan_forward(plan->p, (hipStream_t)stream, x, xs, params, bn_buffers, (char*)workspace, features,
+  dfd::InputFmt in;
+  if (!input_fmt(x_format, norm6, &in)) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return dfd::plan_forward(plan->p, (hipStream_t)stream, x, xs, in, params, bn_buffers, (char*)workspace, features,
                            training, momentum);
+  DFD_GUARD_END
+}
+
+int dfd_b0_forward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* xs, const float* params,
+                   float* bn_buffers, void* workspace, float* features, int training, float momentum) {
+  return dfd_b0_forward_ex(plan, stream, x, DFD_INPUT_F32, xs, nullptr, params, bn_buffers, workspace, features,
+                           training, momentum);
+}
+
+int dfd_b0_backward_ex(dfd_b0_plan* plan, void* stream, const void* x, int x_format, const int64_t* xs,
+                       const float* norm6, const float* dfeatures, const float* params, void* workspace, float* grads,
+                       int training, int seg_begin, int seg_end, int accumulate) {
+  DFD_GUARD_BEGIN
+  if (!plan || !x || !xs || !dfeatures || !params || !workspace || !grads) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  dfd::InputFmt in;
+  if (!input_fmt(x_format, norm6, &in)) return -1;
+  std::lock_guard<std::mutex> lk(plan->mu);
+  return dfd::plan_backward_x(plan->p, (hipStream_t)stream, x, xs, in, dfeatures, params, (char*)workspace, grads,
+                              training, seg_begin, seg_end, accumulate);
   DFD_GUARD_END
 }
 
 int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* xs, const float* dfeatures,
                     const float* params, void* workspace, float* grads, int training, int seg_begin, int seg_end,
                     int accumulate) {
-  DFD_GUARD_BEGIN
-  if (!plan || !x || !xs || !dfeatures || !params || !workspace || !grads) {
-    dfd::set_error("null argument", __FILE__, __LINE__);
-    return -1;
-  }
-  return dfd::plan_backward_x(plan->p, (hipStream_t)stream, x, xs, dfeatures, params, (char*)workspace, grads,
-                              training, seg_begin, seg_end, accumulate);
-  DFD_GUARD_END
+  return dfd_b0_backward_ex(plan, stream, x, DFD_INPUT_F32, xs, nullptr, dfeatures, params, workspace, grads,
+                            training, seg_begin, seg_end, accumulate);
+}
+
+int dfd_b0_plan_set_tuning(dfd_b0_plan* plan, const char* key, int64_t value) {
+  if (!plan || !key) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  static const char* names[dfd::TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile"};
+  for (int k = 0; k < dfd::TK_COUNT; ++k)
+    if (strcmp(key, names[k]) == 0) {
+      std::lock_guard<std::mutex> lk(plan->mu);
+      plan->p.tune.v[k] = value;
+      return 0;
+    }
+  dfd::set_error("plan_set_tuning: unknown key", __FILE__, __LINE__);
+  return -1;
 }
 
 int dfd_b0_segment_count(void) { return dfd::kNumSegments; }
 
 int dfd_b0_probe_arm(dfd_b0_plan* plan, int kind, int stage, int idx, int n) {
   if (!plan || n <= 0) { dfd::set_error("bad probe arguments", __FILE__, __LINE__); return -1; }
+  std::lock_guard<std::mutex> lk(plan->mu);
   return dfd::probe_arm(plan->p, kind, stage, idx, n);
 }
 int dfd_b0_probe_read(dfd_b0_plan* plan, float* ms, int cap, int* count) {
   if (!plan || !ms || !count) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  std::lock_guard<std::mutex> lk(plan->mu);
   return dfd::probe_read(plan->p, ms, cap, count);
 }
 int dfd_b0_probe_disarm(dfd_b0_plan* plan) {
   if (!plan) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  std::lock_guard<std::mutex> lk(plan->mu);
   dfd::probe_disarm(plan->p);
   return 0;
 }
@@ -252,6 +307,14 @@ int dfd_adam_step(void* stream, float* params, float* grads, float* m, float* v,
   h.grad_scale = (float)grad_scale;
   h.decoupled = decoupled;
   return dfd::adam_step((hipStream_t)stream, params, grads, m, v, n, h, clip_out2);
+  DFD_GUARD_END
+}
+
+int dfd_collate_frames(void* stream, const uint8_t* src, const int64_t* sel, int64_t nsel, int64_t frame_bytes,
+                       int out_f32, void* out) {
+  DFD_GUARD_BEGIN
+  if (nsel > 0 && (!src || !sel || !out)) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::launch_collate_gather((hipStream_t)stream, src, sel, nsel, frame_bytes, out_f32 != 0, out);
   DFD_GUARD_END
 }
 

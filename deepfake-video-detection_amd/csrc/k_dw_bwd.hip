@@ -34,7 +34,7 @@ namespace dfd {
 // 1: fused (default); 0: the two kernels (dgrad, wgrad)
 static std::atomic<int64_t> g_dw_bwd_fused{1};
 int64_t set_dw_bwd_fused(int64_t v) { return g_dw_bwd_fused.exchange(v); }
-bool dw_bwd_fused_enabled() { return g_dw_bwd_fused.load(std::memory_order_relaxed) != 0; }
+bool dw_bwd_fused_enabled() { return tune_or(TK_DW_BWD_FUSED, g_dw_bwd_fused.load(std::memory_order_relaxed)) != 0; }
 
 template <int TH, int TW, int K, int S, int VW>
 struct DwB {

@@ -309,7 +309,7 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   // Chosen per shape from tools/kbench on MI355X (tools/gemm_tiles.sh): one 128-wide N tile while
   // N <= 128 (the A prologue then runs once per row tile); 128x64 for narrow N; the 14x14 / 7x7
   // stages (few row tiles) want the small tiles for enough workgroups in flight.
-  int cfg = g_gemm_tile.load();
+  int cfg = (int)tune_or(TK_GEMM_TILE, g_gemm_tile.load());
   if (cfg < 0 || cfg > 3) {
     if (N <= 64) cfg = 1;
     else if (N <= 128) cfg = 0;

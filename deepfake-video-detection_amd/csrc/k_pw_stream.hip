@@ -326,7 +326,7 @@ static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, c
 // the caller uses the tiled kernel); -1: launch error
 int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
                      int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
-  if (M <= 0 || M < g_stream_min_rows.load(std::memory_order_relaxed) || K > 256 || (N & 7) || (K & 7)) return 1;
+  if (M <= 0 || M < tune_or(TK_STREAM_MIN_ROWS, g_stream_min_rows.load(std::memory_order_relaxed)) || K > 256 || (N & 7) || (K & 7)) return 1;
   const int nchunks = cdiv(N, 128);
   const int NB = cdiv(cdiv(N, nchunks), 16), KB = cdiv(K, 32);
   const bool st = stats != nullptr, rs = R != nullptr, bs = bias != nullptr;
@@ -613,7 +613,7 @@ static int wgs_launch(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, i
 // 0: launched; 1: not covered (the caller uses the tiled wgrad kernel); -1: launch error
 int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate) {
-  if (M <= 0 || M < g_stream_min_rows.load(std::memory_order_relaxed) || (N & 7) || (K & 7)) return 1;
+  if (M <= 0 || M < tune_or(TK_STREAM_MIN_ROWS, g_stream_min_rows.load(std::memory_order_relaxed)) || (N & 7) || (K & 7)) return 1;
 #define DFD_WGS(NBW_, KBW_, S_, MODE_) \
   return wgs_launch<NBW_, KBW_, S_, MODE_>(s, dY, X, M, N, K, pro, slab, slab_cap, dW, accumulate)
   if (pro_mode == PRO_NONE) {  // conv_pw (expansion): N = mid, K = cin;  Gram x^T x: N = K = cin

@@ -1,7 +1,10 @@
 // EfficientNet-B0 stem: conv2d 3->32, k3, s2, pad 1 (timm conv_stem), forward with BN-stat
-// epilogue and weight gradient.  The fp32 input frames are read IN PLACE with arbitrary
+// epilogue and weight gradient.  The input frames are read IN PLACE with arbitrary
 // (frame, channel, row, col) strides -- the reference hands over channels-last-strided
-// (B*T,3,H,W) tensors (app.py:2084-2086) -- so no transpose/copy precedes it.
+// (B*T,3,H,W) tensors (app.py:2084-2086) -- so no transpose/copy precedes it.  They
+// are either fp32 (normalised by the caller) or the raw uint8 face crops of the .npz feed
+// (data_prepare.py:278-281), normalised while staging the tile (InputFmt): 1 B instead of 4 B
+// per input element in both the forward and the weight-gradient pass.
 #include "kernels.h"
 
 namespace dfd {
@@ -26,33 +29,102 @@ struct StemTiles {
 
 // input tile [pix][ci] (pix = row*SIE + col) of frame f at origin (iy0, ix0): branch-free
 // masked loads through the caller's strides, all issued together (register prefetch).
-__device__ __forceinline__ void stem_load(const StemGeom& g, const float* __restrict__ x, int f, int iy0, int ix0,
+// uint8 frames (InputFmt.u8 = 1): the raw bytes are loaded here and normalised in stem_store
+// through a 3 x 256 table in LDS.  Dense NHWC uint8 (u8 = 2, the .npz crops / the app's permute):
+// each tile row is 33 px x 3 B = 99 contiguous bytes, loaded as <= 26 aligned dwords per row
+// (4 loads per lane instead of 13 byte loads), staged as bytes in LDS and unpacked in stem_store.
+// The loads stay in flight across the current tile's math in both cases.
+constexpr int SRW = 26;                // dwords per staged row (99 B + alignment slack)
+constexpr int SNW = SIE * SRW;         // 858 dwords per tile
+constexpr int SNWL = (SNW + 255) / 256;
+static_assert(SNWL <= SNLD, "the dword path reuses the tile's load registers");
+__device__ __forceinline__ void stem_load(const StemGeom& g, const void* __restrict__ x, int f, int iy0, int ix0,
                                           float (&r)[SNLD], uint32_t& okm) {
   okm = 0u;
   const int tid = threadIdx.x;
+  if (g.in.u8 == 2) {
+    const int xa = max(ix0, 0), xb = min(ix0 + SIE - 1, g.W - 1);
+    const int off0 = (xa * 3) & ~3;
+    const int nw = ((xb * 3 + 2) - off0) / 4 + 1;
+    const uint8_t* base = static_cast<const uint8_t*>(x) + (int64_t)f * g.sf + off0;
+#pragma unroll
+    for (int i = 0; i < SNWL; ++i) {
+      const int w = tid + 256 * i, row = w / SRW, k = w - row * SRW, iy = iy0 + row;
+      const bool ok = w < SNW && k < nw && iy >= 0 && iy < g.H;
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(ok ? base + (int64_t)iy * g.sh + 4 * k
+                                                               : static_cast<const uint8_t*>(x));
+      r[i] = __uint_as_float(ok ? v : 0u);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < SNLD; ++i) {
     const int e = tid + 256 * i;
     const int pix = e / 3, ci = e - 3 * (e / 3);
     const int iy = iy0 + pix / SIE, ix = ix0 + pix % SIE;
     const bool ok = e < SNIN && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-    r[i] = *(ok ? x + ((int64_t)f * g.sf + ci * g.sc + (int64_t)iy * g.sh + (int64_t)ix * g.sw) : x);
+    const int64_t o = ok ? ((int64_t)f * g.sf + ci * g.sc + (int64_t)iy * g.sh + (int64_t)ix * g.sw) : 0;
+    if (g.in.u8)
+      r[i] = (float)static_cast<const uint8_t*>(x)[o];
+    else
+      r[i] = static_cast<const float*>(x)[o];
     okm |= ok ? (1u << i) : 0u;
   }
 }
-__device__ __forceinline__ void stem_store(float* tin, const float (&r)[SNLD], uint32_t okm) {
+// The normalised value of every (channel, byte) pair: (v / 255 - mean) / std in fp32 with correctly
+// rounded divisions -- torch's operations in torch's order -- computed once per workgroup (768
+// entries) instead of two divisions per staged element.  Visible after the caller's next barrier.
+constexpr int SLUT = 3 * 256;
+__device__ __forceinline__ void stem_lut_init(const StemGeom& g, float* lut) {
+  if (!g.in.u8) return;
+  for (int i = threadIdx.x; i < SLUT; i += 256) {
+    const int c = i >> 8;
+    const float m = c == 0 ? g.in.mean[0] : c == 1 ? g.in.mean[1] : g.in.mean[2];
+    const float sd = c == 0 ? g.in.stdv[0] : c == 1 ? g.in.stdv[1] : g.in.stdv[2];
+    lut[i] = ((float)(i & 255) / 255.0f - m) / sd;
+  }
+}
+// tin[pix][ci] of the tile at input origin (iy0, ix0); the dword path stages its bytes in u8s
+// (an extra LDS barrier: every thread of the workgroup calls this uniformly).
+__device__ __forceinline__ void stem_store(const StemGeom& g, const float* lut, uint32_t* u8s, float* tin,
+                                           const float (&r)[SNLD], uint32_t okm, int iy0, int ix0) {
+  if (g.in.u8 == 2) {
+#pragma unroll
+    for (int i = 0; i < SNWL; ++i) {
+      const int w = threadIdx.x + 256 * i;
+      if (w < SNW) u8s[w] = __float_as_uint(r[i]);
+    }
+    lds_barrier();
+    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(u8s);
+    const int off0 = (max(ix0, 0) * 3) & ~3;
+#pragma unroll
+    for (int i = 0; i < SNLD; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      const int pix = e / 3, ci = e - 3 * (e / 3);
+      const int row = pix / SIE, ix = ix0 + pix % SIE, iy = iy0 + row;
+      const bool ok = e < SNIN && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+      const int b = ok ? bytes[row * (SRW * 4) + ix * 3 + ci - off0] : 0;
+      if (e < SNIN) tin[e] = ok ? lut[ci * 256 + b] : 0.f;  // zero padding AFTER normalisation
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < SNLD; ++i) {
     const int e = threadIdx.x + 256 * i;
-    if (e < SNIN) tin[e] = ((okm >> i) & 1u) ? r[i] : 0.f;
+    float v = r[i];
+    if (g.in.u8) v = lut[(e - 3 * (e / 3)) * 256 + (int)v];
+    if (e < SNIN) tin[e] = ((okm >> i) & 1u) ? v : 0.f;  // zero padding AFTER normalisation, as conv2d pads
   }
 }
 
 template <typename T, bool STATS>
-__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const float* __restrict__ x,
+__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const void* __restrict__ x,
                                                        const float* __restrict__ w, T* __restrict__ Y,
                                                        float* __restrict__ stats, int64_t ntiles) {
   __shared__ float tin[SNIN];
+  __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
+  __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
+  stem_lut_init(g, lut);
   __shared__ __attribute__((aligned(16))) float wts[27][SCO];  // [ci*9+tap][co]
   __shared__ float red[2][4][SCO];
   const int tid = threadIdx.x, vec = tid & 3, pt = tid >> 2;
@@ -76,7 +148,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const floa
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
     lds_barrier();
-    stem_store(tin, nxt, nok);
+    stem_store(g, lut, u8s, tin, nxt, nok, oy0 * 2 - 1, ox0 * 2 - 1);
     lds_barrier();
     if (t + gridDim.x < ntiles) {  // next tile in flight during this tile's math and stores
       int f2, oy2, ox2;
@@ -145,10 +217,13 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const floa
 // thread (co = tid & 31, sub = tid >> 5) accumulates all 27 taps over pixels p = sub (mod 8);
 // the next tile's input and dY are loaded into registers while the current tile is reduced.
 template <typename T>
-__global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float* __restrict__ x,
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const void* __restrict__ x,
                                                          const T* __restrict__ dY, float* __restrict__ slab,
                                                          int64_t ntiles) {
   __shared__ float tin[SNIN];
+  __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
+  __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
+  stem_lut_init(g, lut);
   __shared__ __attribute__((aligned(16))) float tg[ST * ST * SCO];  // [pix][co]; reused as red[8][27][32]
   const int tid = threadIdx.x, co = tid & 31, sub = tid >> 5;
   const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
@@ -172,8 +247,10 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const float
   int64_t t = blockIdx.x;
   if (t < ntiles) load(t);
   for (; t < ntiles; t += gridDim.x) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
     lds_barrier();
-    stem_store(tin, nx, nxok);
+    stem_store(g, lut, u8s, tin, nx, nxok, oy0 * 2 - 1, ox0 * 2 - 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
@@ -219,10 +296,13 @@ typedef short stw_s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) stw_s16x4_t stw_lds_s16x4_t;
 typedef float stw_f32x4_t __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, const float* __restrict__ x,
+__global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, const void* __restrict__ x,
                                                               const bf16* __restrict__ dY, float* __restrict__ slab,
                                                               int64_t ntiles) {
   __shared__ float tin[SNIN];
+  __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
+  __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
+  stem_lut_init(g, lut);
   __shared__ __attribute__((aligned(16))) bf16 ys[ST * ST * SWL];  // dY tile [pix][co]; reused for the reduction
   __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col tile [pix][tap]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -250,8 +330,10 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
   int64_t t = blockIdx.x;
   if (t < ntiles) load(t);
   for (; t < ntiles; t += gridDim.x) {
+    int f, oy0, ox0;
+    tl.coords(t, f, oy0, ox0);
     lds_barrier();
-    stem_store(tin, nx, nxok);
+    stem_store(g, lut, u8s, tin, nx, nxok, oy0 * 2 - 1, ox0 * 2 - 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
@@ -332,10 +414,13 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 // (thread = pixel), 8 MFMAs per wave, rounded tile through an LDS slab for 16-B row stores,
 // BN-stat partials from the rounded values (per lane, fixed-order reduction at the end).
 constexpr int SFC = SCO + 8;  // LDS row stride (bf16) of the output slab
-__global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const float* __restrict__ x,
+__global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const void* __restrict__ x,
                                                             const float* __restrict__ w, bf16* __restrict__ Y,
                                                             float* __restrict__ stats, int64_t ntiles) {
   __shared__ float tin[SNIN];
+  __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
+  __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
+  stem_lut_init(g, lut);
   __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col [pix][tap]
   __shared__ __attribute__((aligned(16))) bf16 ct[ST * ST * SFC];  // output slab [pix][co]
   __shared__ __attribute__((aligned(16))) bf16 wsb[SCO * SWL];     // weights [co][tap]
@@ -369,7 +454,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
     lds_barrier();
-    stem_store(tin, nxt, nok);
+    stem_store(g, lut, u8s, tin, nxt, nok, oy0 * 2 - 1, ox0 * 2 - 1);
     lds_barrier();
     if (t + gridDim.x < ntiles) {  // next tile in flight during this tile's math and stores
       int f2, oy2, ox2;
@@ -459,7 +544,7 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const
 }
 
 template <typename T>
-int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const float* w, T* Y, float* stats,
+int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float* w, T* Y, float* stats,
                     int* stat_rows) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
   const int gx = (int)std::min<int64_t>(ntiles, 1024);
@@ -477,7 +562,7 @@ int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const floa
 }
 
 template <typename T>
-int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const float* x, const T* dY, float* slab, int64_t slab_cap,
+int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* dY, float* slab, int64_t slab_cap,
                       float* dW, bool accumulate) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
   int gx = (int)std::min<int64_t>(ntiles, 1024);
@@ -490,11 +575,11 @@ int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const float* x, const T*
   return launch_reduce_slabs(s, slab, gx, 27 * SCO, dW, accumulate);
 }
 
-template int launch_stem_fwd<float>(hipStream_t, const StemGeom&, const float*, const float*, float*, float*, int*);
-template int launch_stem_fwd<bf16>(hipStream_t, const StemGeom&, const float*, const float*, bf16*, float*, int*);
-template int launch_stem_wgrad<float>(hipStream_t, const StemGeom&, const float*, const float*, float*, int64_t,
+template int launch_stem_fwd<float>(hipStream_t, const StemGeom&, const void*, const float*, float*, float*, int*);
+template int launch_stem_fwd<bf16>(hipStream_t, const StemGeom&, const void*, const float*, bf16*, float*, int*);
+template int launch_stem_wgrad<float>(hipStream_t, const StemGeom&, const void*, const float*, float*, int64_t,
                                       float*, bool);
-template int launch_stem_wgrad<bf16>(hipStream_t, const StemGeom&, const float*, const bf16*, float*, int64_t, float*,
+template int launch_stem_wgrad<bf16>(hipStream_t, const StemGeom&, const void*, const bf16*, float*, int64_t, float*,
                                      bool);
 
 }  // namespace dfd

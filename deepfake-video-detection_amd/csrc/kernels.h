@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 #include "common.h"
 
@@ -21,6 +22,26 @@ int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const
 int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
 // rows threshold of the streaming kernels (returns the previous value)
+// Kernel-selection knobs.  Process-wide defaults (set_* below, dfd_set_tuning), overridden per plan:
+// a plan's forward/backward installs its own Tuning for the enqueuing thread (TuningScope), so
+// concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
+// training step -- never read each other's knobs.
+enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_COUNT };
+constexpr int64_t kTuneUnset = INT64_MIN;
+struct Tuning {
+  int64_t v[TK_COUNT];
+  Tuning() { for (auto& x : v) x = kTuneUnset; }
+};
+int64_t tune_override(TuneKey k);  // the calling thread's plan override, or kTuneUnset
+inline int64_t tune_or(TuneKey k, int64_t dflt) {
+  const int64_t o = tune_override(k);
+  return o == kTuneUnset ? dflt : o;
+}
+struct TuningScope {
+  const Tuning* prev;
+  explicit TuningScope(const Tuning* t);
+  ~TuningScope();
+};
 int64_t set_stream_min_rows(int64_t v);
 int set_gemm_tile(int v);  // tiled pw GEMM: force tile config 0/1/2, -1 = auto (returns previous)
 // Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
@@ -177,16 +198,29 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
                                 bool accumulate);
 
 // ---------------- stem (3->32, k3 s2): k_stem.hip ----------------
+// Input frames of the trunk: fp32 (already normalised by the caller, app.py:2084-2085) or raw
+// uint8 pixels normalised in the stem's load as ((v / 255) - mean[c]) / std[c] -- the same fp32
+// operations, in the same order, as the reference's `.float() / 255.0` + imagenet_normalize
+// (app.py:1772-1780), so both formats give bit-identical stem inputs.
+struct InputFmt {
+  int u8;                 // 0: fp32 frames, 1: uint8 pixels (any strides), 2: dense NHWC uint8
+  float mean[3], stdv[3]; // u8 only (mean 0 / std 1: the /255-only feed of train.py:59)
+};
 struct StemGeom {
   int frames, H, W, Ho, Wo;
-  int64_t sf, sc, sh, sw;  // element strides of the fp32 input (frame, channel, row, col)
+  int64_t sf, sc, sh, sw;  // element strides of the input (frame, channel, row, col)
+  InputFmt in;
 };
 template <typename T>
-int launch_stem_fwd(hipStream_t s, const StemGeom& g, const float* x, const float* w, T* Y, float* stats,
+int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float* w, T* Y, float* stats,
                     int* stat_rows);
 template <typename T>
-int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const float* x, const T* dY, float* slab,
+int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* dY, float* slab,
                       int64_t slab_cap, float* dW, bool accumulate);
+
+// ---------------- input pipeline: k_input.hip ----------------
+int launch_collate_gather(hipStream_t s, const uint8_t* src, const int64_t* sel, int64_t nsel, int64_t frame_bytes,
+                          bool f32, void* out);
 
 // ---------------- misc: k_misc.hip ----------------
 struct CastSeg {

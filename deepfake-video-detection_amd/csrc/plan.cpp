@@ -309,9 +309,17 @@ struct Run {
   }
 };
 
+// dense NHWC uint8 frames (channel stride 1, pixel stride 3, 4-B aligned rows) take the stem's
+// dword-staged load (InputFmt.u8 = 2)
+static InputFmt stem_fmt(const InputFmt& in, const void* x, const int64_t* xs) {
+  InputFmt o = in;
+  if (in.u8 && xs[1] == 1 && xs[3] == 3 && xs[2] % 4 == 0 && xs[0] % 4 == 0 && ((uintptr_t)x & 3) == 0) o.u8 = 2;
+  return o;
+}
+
 template <typename T>
-int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* P, float* bnb, char* ws,
-                 float* feat, int tr, float mom) {
+int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& in, const float* P,
+                 float* bnb, char* ws, float* feat, int tr, float mom) {
   Run<T> r{p, s, ws, P, tr};
   const float eps = 1e-5f;
   float* stats = tr ? r.f(p.o_stats) : nullptr;
@@ -323,7 +331,7 @@ int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, cons
   };
   DFD_TRY(launch_cast_params<T>(s, P, reinterpret_cast<T*>(ws), p.cast_dev, (int)p.cast_host.size(), p.cast_max));
   const int64_t F = p.frames;
-  StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3]};
+  StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3], stem_fmt(in, x, xs)};
   DFD_TRY(launch_stem_fwd<T>(s, sg, x, r.prm(p.t_stem), r.a(p.o_ystem), stats, &rows));
   DFD_TRY(fin(p.bn_stem, F * p.H1 * p.W1));
   const T* xin = nullptr;
@@ -371,8 +379,8 @@ int forward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, cons
 std::atomic<int64_t> g_fold_min_rows{100000};
 
 template <typename T>
-int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat, const float* P,
-                  char* ws, float* G, int tr, int seg_begin, int seg_end, int acc) {
+int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& ifmt, const float* dfeat,
+                  const float* P, char* ws, float* G, int tr, int seg_begin, int seg_end, int acc) {
   Run<T> r{p, s, ws, P, tr};
   int rows = 0;
   const int64_t F = p.frames;
@@ -488,7 +496,7 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
                                                       acc != 0)));
         }
         p.pending_rows = rows;
-        if (!b.ds && Min < g_fold_min_rows.load(std::memory_order_relaxed)) {
+        if (!b.ds && Min < tune_or(TK_FOLD_MIN_ROWS, g_fold_min_rows.load(std::memory_order_relaxed))) {
           BnBwdIn i1{};
           i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = false;
           DFD_TRY(bwd_bn_from_stats(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1), p.pending_rows));
@@ -528,7 +536,7 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
       BnBwdIn in{};
       in.dZ = r.a(p.o_ge1); in.rows_per_frame = p.H1 * p.W1; in.silu = false;  // ge1 holds g (fused in dw dgrad)
       DFD_TRY(bwd_bn_from_stats(in, p.bn_stem, r.a(p.o_ystem), M, r.a(p.o_ge1), p.pending_rows));
-      StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3]};
+      StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3], stem_fmt(ifmt, x, xs)};
       DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), slab(), p.slab_cap, grad(p.t_stem), acc != 0));
     }
     DFD_TRY(defer.flush());  // this segment's weight gradients are final
@@ -542,23 +550,31 @@ int backward_impl(Plan& p, hipStream_t s, const float* x, const int64_t* xs, con
 
 int64_t set_fold_min_rows(int64_t v) { return g_fold_min_rows.exchange(v); }
 
-int plan_forward(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* params, float* bnbuf,
-                 char* ws, float* feat, int training, float momentum) {
+static thread_local const Tuning* t_tune = nullptr;
+int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }
+TuningScope::TuningScope(const Tuning* t) : prev(t_tune) { t_tune = t; }
+TuningScope::~TuningScope() { t_tune = prev; }
+
+int plan_forward(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& in, const float* params,
+                 float* bnbuf, char* ws, float* feat, int training, float momentum) {
   if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
-  if (p.dtype == 1) return forward_impl<bf16>(p, s, x, xs, params, bnbuf, ws, feat, training, momentum);
-  return forward_impl<float>(p, s, x, xs, params, bnbuf, ws, feat, training, momentum);
+  const TuningScope ts(&p.tune);
+  if (p.dtype == 1) return forward_impl<bf16>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
+  return forward_impl<float>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
 }
 
-int plan_backward_x(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat, const float* params,
-                    char* ws, float* grads, int training, int seg_begin, int seg_end, int accumulate) {
+int plan_backward_x(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& in, const float* dfeat,
+                    const float* params, char* ws, float* grads, int training, int seg_begin, int seg_end,
+                    int accumulate) {
   if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
   if (seg_begin < 0 || seg_end > kNumSegments || seg_begin > seg_end) {
     set_error("backward: bad segment range", __FILE__, __LINE__);
     return -1;
   }
+  const TuningScope ts(&p.tune);
   if (p.dtype == 1)
-    return backward_impl<bf16>(p, s, x, xs, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
-  return backward_impl<float>(p, s, x, xs, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
+    return backward_impl<bf16>(p, s, x, xs, in, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
+  return backward_impl<float>(p, s, x, xs, in, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
 }
 
 }  // namespace dfd

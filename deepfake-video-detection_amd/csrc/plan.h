@@ -75,6 +75,7 @@ struct Plan {
   int device = 0;
   int pending_rows = 0;  // stat rows written by the stage-0 dw dgrad, consumed by the stem segment
   Probe probe;
+  Tuning tune;  // per-plan kernel-selection overrides (dfd_b0_plan_set_tuning)
 };
 
 int probe_arm(Plan& p, int kind, int stage, int idx, int n);
@@ -84,9 +85,9 @@ void probe_disarm(Plan& p);
 int plan_build(Plan& p, int frames, int H, int W, int dtype);
 int plan_bind(Plan& p, const int64_t* offs, int n);
 void plan_free(Plan& p);
-int plan_forward(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* params, float* bnbuf,
-                 char* ws, float* feat, int training, float momentum);
-int plan_backward_x(Plan& p, hipStream_t s, const float* x, const int64_t* xs, const float* dfeat,
+int plan_forward(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& in, const float* params,
+                 float* bnbuf, char* ws, float* feat, int training, float momentum);
+int plan_backward_x(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& in, const float* dfeat,
                     const float* params, char* ws, float* grads, int training, int seg_begin, int seg_end,
                     int accumulate);
 // segments: 0 = conv_head+bn2, 1..7 = stage 6..0, 8 = stem.  Tensor index range [lo, hi) whose

@@ -7,12 +7,20 @@ Mirrors ``src/pretrained_detector.py`` of the reference:
   ``dropout``, ``fc1``, ``fc2``), same head initialisation (``_init_head_weights`` ``:80-85``)
   and the same ``state_dict`` keys (``backbone.*`` = timm efficientnet_b0 names,
   ``temporal_attention.{0,2}.*``, ``fc1.*``, ``fc2.*``).
-* ``forward`` (``:103-143``): ``(B, T, 3, H, W) -> (logits (B, C), frame_scores (B, T))``;
+* ``forward`` (``:103-143``): ``(B, T, 3, H, W) -> (logits (B, C), frame_scores (B, T))``; the frames
+  are the reference's normalised fp32 tensors, or -- new -- the raw uint8 face crops
+  (``torch.from_numpy(faces).permute(0, 3, 1, 2)`` per clip) normalised inside the stem kernel
+  (``input_normalization``, default the app's ImageNet constants), bit-identical to normalising
+  first;
   the trunk runs as one native HIP plan, the head (temporal attention, softmax over T,
   weighted pooling, dropout, fc1/ReLU, fc2) as HIP kernels; autograd flows into every
   parameter (gradients land in one flat buffer).
 * ``unfreeze_backbone`` (``:87-101``) is a no-op for EfficientNet, exactly as in the
   reference (its Sequential trunk has no ``.blocks``).
+
+Arithmetic: ``compute_dtype="fp32"`` (default -- the drop-in meets the north-star rtol 1e-3 /
+atol 1e-5 on logits and loss) or ``"bf16"`` (the training/serving performance mode; bounds in
+tests/test_b0_224_gpu.py and tests/test_serving.py).
 
 Only ``efficientnet_b0`` (the hot path) is provided; ``pretrained=True`` would download
 timm weights in the reference and is refused here (offline; load a checkpoint instead).
@@ -35,9 +43,10 @@ FC1_DIM = 256
 
 
 class PretrainedBackboneDetector(FlatModule):
+    accepts_uint8_frames = True  # raw uint8 crops are normalised inside the stem kernel
     def __init__(self, backbone_name: str = "efficientnet_b0", pretrained: bool = True, num_classes: int = 2,
                  dropout_rate: float = 0.5, freeze_backbone: bool = False, use_temporal_attention: bool = True,
-                 compute_dtype: str = "bf16"):
+                 compute_dtype: str = "fp32", input_normalization="imagenet"):
         super().__init__()
         if backbone_name != "efficientnet_b0":
             raise ValueError(f"Unsupported backbone: {backbone_name} (the MI355X hot path implements "
@@ -48,7 +57,7 @@ class PretrainedBackboneDetector(FlatModule):
         self.backbone_name = backbone_name
         self.num_classes = num_classes
         self.use_temporal_attention = use_temporal_attention
-        self.backbone = EfficientNetB0Trunk(compute_dtype)
+        self.backbone = EfficientNetB0Trunk(compute_dtype, input_normalization)
         self.feature_dim = FEATURE_DIM
         if freeze_backbone:
             for p in self.backbone.parameters():
@@ -186,8 +195,10 @@ class EnsembleDetector(nn.Module):
     """``src/pretrained_detector.py:146-218`` restricted to efficientnet_b0 members (the members run on
     the HIP path; the ensemble combination is a few ops on (M, B, C) logits)."""
 
+    accepts_uint8_frames = True
+
     def __init__(self, backbone_names: List[str], pretrained: bool = True, num_classes: int = 2,
-                 dropout_rate: float = 0.5, ensemble_method: str = "average", compute_dtype: str = "bf16"):
+                 dropout_rate: float = 0.5, ensemble_method: str = "average", compute_dtype: str = "fp32"):
         super().__init__()
         self.models = nn.ModuleList([
             PretrainedBackboneDetector(backbone_name=name, pretrained=pretrained, num_classes=num_classes,

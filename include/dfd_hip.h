@@ -71,6 +71,25 @@ DFD_API int dfd_b0_forward(dfd_b0_plan* plan, void* stream, const float* x, cons
 DFD_API int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64_t* x_strides4,
                             const float* dfeatures, const float* params, void* workspace, float* grads,
                             int training, int seg_begin, int seg_end, int accumulate);
+/* Input-format variants.  x_format DFD_INPUT_F32: as above.  DFD_INPUT_U8: raw uint8 face crops
+ * (the .npz `faces` arrays, data_prepare.py:278-281 / dataset.py:51-81) with the same element
+ * strides (e.g. torch.from_numpy(faces).permute(0,3,1,2), app.py:2084), normalised inside the stem
+ * as ((v / 255) - mean[c]) / std[c], norm6 = {mean[3], std[3]} -- exactly the fp32 operations of
+ * `.float() / 255.0` + imagenet_normalize (app.py:1772-1780); mean 0 / std 1 is the /255-only
+ * feed of src/train.py:59.  Both formats give bit-identical results for the same pixels.
+ * Calls on one plan from several threads serialise their enqueue (per-plan lock). */
+#define DFD_INPUT_F32 0
+#define DFD_INPUT_U8 1
+DFD_API int dfd_b0_forward_ex(dfd_b0_plan* plan, void* stream, const void* x, int x_format,
+                              const int64_t* x_strides4, const float* norm6, const float* params,
+                              float* bn_buffers, void* workspace, float* features, int training, float momentum);
+DFD_API int dfd_b0_backward_ex(dfd_b0_plan* plan, void* stream, const void* x, int x_format,
+                               const int64_t* x_strides4, const float* norm6, const float* dfeatures,
+                               const float* params, void* workspace, float* grads, int training, int seg_begin,
+                               int seg_end, int accumulate);
+/* Per-plan kernel-selection override of a dfd_set_tuning key (INT64_MIN clears it); the
+ * process-wide dfd_set_tuning values stay the defaults of plans that set nothing. */
+DFD_API int dfd_b0_plan_set_tuning(dfd_b0_plan* plan, const char* key, int64_t value);
 DFD_API int dfd_b0_segment_count(void);
 /* Introspection of the activations a forward saved in the workspace (pre-BN conv outputs and
  * block outputs, NHWC [rows][cols] in the plan dtype): 0 = conv_stem, then per block
@@ -112,6 +131,14 @@ DFD_API int dfd_ce_forward(void* stream, const float* logits, const int64_t* lab
 DFD_API int dfd_ce_backward(void* stream, const float* logits, const int64_t* labels, const float* weight, int B,
                             int NC, int64_t ignore_index, const float* wsum, const float* grad_out,
                             float* dlogits);
+
+/* ---- input pipeline ----------------------------------------------------------------------
+ * Replaces the frame gather of collate_batch_cnn_lstm / collate_batch (src/train.py:38-61,
+ * 62-100): out[s] = src[sel[s]] for s < nsel, frames of frame_bytes uint8 each (sel[s] < 0: an
+ * all-zero frame), written as uint8 (out_f32 = 0) or as fp32 v / 255 (out_f32 = 1, the
+ * reference's `.float() / 255.0`, bit-identical).  src / out are device pointers. */
+DFD_API int dfd_collate_frames(void* stream, const uint8_t* src, const int64_t* sel, int64_t nsel,
+                               int64_t frame_bytes, int out_f32, void* out);
 
 /* ---- optimizer ----------------------------------------------------------------------------
  * Replaces torch.nn.utils.clip_grad_norm_(params, max_norm) (src/ensemble_trainer.py:199) and
