@@ -472,15 +472,12 @@ __global__ void sum_parts_kernel(const float* __restrict__ part, int hsplit, int
   }
 }
 
+// the squeeze's per-frame partial sums part[h][f][c] (h < *hsplit); the excitation (se_chain_kernel)
+// adds the partials and scales by 1/HW while loading them
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
-                      int64_t part_cap, float* sq, T* s_out) {
-  int hs;
-  if (launch_frame_sum<T, false>(s, nullptr, Y, pro, frames, HW, C, part, part_cap, &hs, s_out)) return -1;
-  const int64_t n = (int64_t)frames * C;
-  hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, part, hs, n, 1.0f / (float)HW, sq);
-  DFD_HIP_CHECK(hipGetLastError());
-  return 0;
+                      int64_t part_cap, int* hsplit, T* s_out) {
+  return launch_frame_sum<T, false>(s, nullptr, Y, pro, frames, HW, C, part, part_cap, hsplit, s_out);
 }
 
 template <typename T>
@@ -570,35 +567,10 @@ __global__ __launch_bounds__(256) void se_bn_bwd_kernel(const T* __restrict__ dZ
   }
 }
 
-// out[q][i] = sum_h part[q][h][i], q < 5 (h in order)
-// adds the hsplit partials; the SE gate gradient leaves as de = dgate * sigmoid'(.) = dgate g (1-g)
-__global__ void sum_parts5_kernel(const float* __restrict__ part, int hsplit, int64_t n,
-                                  const float* __restrict__ gate, float* __restrict__ de, float* __restrict__ pf) {
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < 5 * n; i += (int64_t)gridDim.x * 256) {
-    const int64_t q = i / n, k = i - q * n;
-    float a = 0.f;
-    int h = 0;
-    for (; h + 4 <= hsplit; h += 4) {
-      float v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = part[(q * hsplit + h + u) * n + k];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a += v[u];
-    }
-    for (; h < hsplit; ++h) a += part[(q * hsplit + h) * n + k];
-    if (q == 0) {
-      const float g = gate[k];
-      de[k] = a * g * (1.f - g);
-    } else {
-      pf[(q - 1) * n + k] = a;
-    }
-  }
-}
-
 template <typename T>
 int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
                             const float* mean, const float* invstd, int frames, int HW, int C, float* part,
-                            int64_t part_cap, const float* gate, float* de, float* pf) {
+                            int64_t part_cap, int* hsplit_out) {
   int vpg, groups;
   bn_vpg_groups(C, vpg, groups);
   const int npl = 256 / vpg;
@@ -610,25 +582,55 @@ int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float*
   hipLaunchKernelGGL((se_bn_bwd_kernel<T>), dim3(frames * hsplit, groups), dim3(256), 0, s, dZ, Y, scale, shift, mean,
                      invstd, frames, HW, C, hsplit, vpg, part);
   DFD_HIP_CHECK(hipGetLastError());
-  const int64_t n = (int64_t)frames * C;
-  hipLaunchKernelGGL(sum_parts5_kernel, dim3(ew_grid(5 * n)), dim3(256), 0, s, part, hsplit, n, gate, de, pf);
-  DFD_HIP_CHECK(hipGetLastError());
+  *hsplit_out = hsplit;
   return 0;
 }
 
 // BN backward finalize from the per-frame sums of se_bn_bwd_kernel once bc is known:
 // dbeta = sum g, dgamma = sum g*xhat, coefficients k1..k3 of dy = k1*g + k2*y + k3 (fp64).
+// The sums P1..P4 are the partials part[1..4][h][f][c] of se_bn_bwd_kernel, added over h in order.
 // Block = 64 channels x 16 frame slices (the slices' frames unrolled by 4, all loads issued
 // up front); slices added in order.
 constexpr int FF_SL = 16;
+struct PartSum {  // P[q][i] = sum_h part[(q + 1) * hsplit + h][i]  (q = 0..3 -> P1..P4)
+  const float* part;
+  int hsplit;
+  int64_t n;
+  __device__ __forceinline__ float operator()(int q, int64_t i) const {
+    const float* b = part + ((int64_t)(q + 1) * hsplit) * n + i;
+    float a = b[0];
+    for (int h = 1; h < hsplit; ++h) a += b[(int64_t)h * n];
+    return a;
+  }
+};
+// ONE: chunk 0 of each q already holds the sum (hsplit == 1, or added by sum_parts4_kernel) -- plain
+// loads, all issued up front
+template <bool ONE>
+__device__ __forceinline__ float part_sum(const PartSum& ps, int q, int64_t i) {
+  if constexpr (ONE) return ps.part[(int64_t)(q + 1) * ps.hsplit * ps.n + i];
+  return ps(q, i);
+}
+// part[q][h][i] (q = 1..4) -> part[q][0][i] = sum over h in order (in place: element (q, i) is read
+// and written by one thread only); the finalize then reads chunk 0 of each q
+__global__ void sum_parts4_kernel(float* __restrict__ part, int hsplit, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < 4 * n; i += (int64_t)gridDim.x * 256) {
+    const int64_t q = i / n + 1, k = i - (q - 1) * n;
+    float a = 0.f;
+    for (int h = 0; h < hsplit; ++h) a += part[(q * hsplit + h) * n + k];
+    part[q * hsplit * n + k] = a;
+  }
+}
+
+template <bool ONE>
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
-    const float* __restrict__ pf, const float* __restrict__ gate, const float* __restrict__ bc, int frames, int C,
-    int64_t count, const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ invstd,
-    int training, float* dgamma, float* dbeta, int accumulate, float* coef) {
+    const float* __restrict__ part, int hsplit, const float* __restrict__ gate, const float* __restrict__ bc, int frames,
+    int C, int64_t count, const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ invstd, int training, float* dgamma, float* dbeta, int accumulate, float* coef) {
   __shared__ double red[2][FF_SL][64];
   const int tid = threadIdx.x, cl = tid & 63, sl = tid >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int64_t n = (int64_t)frames * C;
+  const PartSum pf{part, hsplit, n};
   double s = 0.0, q = 0.0;
   if (c < C) {
     const int per = (frames + FF_SL - 1) / FF_SL;
@@ -640,7 +642,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
       for (int u = 0; u < 4; ++u) {
         const int64_t i = (int64_t)(f + u) * C + c;
         gt[u] = gate[i]; b[u] = bc[i];
-        p1[u] = pf[i]; p2[u] = pf[n + i]; p3[u] = pf[2 * n + i]; p4[u] = pf[3 * n + i];
+        p1[u] = part_sum<ONE>(pf, 0, i); p2[u] = part_sum<ONE>(pf, 1, i);
+        p3[u] = part_sum<ONE>(pf, 2, i); p4[u] = part_sum<ONE>(pf, 3, i);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -650,8 +653,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
     }
     for (; f < f1; ++f) {
       const int64_t i = (int64_t)f * C + c;
-      s += (double)gate[i] * (double)pf[i] + (double)bc[i] * (double)pf[n + i];
-      q += (double)gate[i] * (double)pf[2 * n + i] + (double)bc[i] * (double)pf[3 * n + i];
+      s += (double)gate[i] * (double)part_sum<ONE>(pf, 0, i) + (double)bc[i] * (double)part_sum<ONE>(pf, 1, i);
+      q += (double)gate[i] * (double)part_sum<ONE>(pf, 2, i) + (double)bc[i] * (double)part_sum<ONE>(pf, 3, i);
     }
   }
   red[0][sl][cl] = s;
@@ -677,11 +680,19 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
   }
 }
 
-int launch_bn_bwd_finalize_frames(hipStream_t s, const float* pf, const float* gate, const float* bc, int frames,
-                                  int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
-                                  bool training, float* dgamma, float* dbeta, bool accumulate, float* coef) {
-  hipLaunchKernelGGL(bn_bwd_finalize_frames_kernel, dim3(cdiv(C, 64)), dim3(1024), 0, s, pf, gate, bc, frames, C, count,
-                     gamma, mean, invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef);
+int launch_bn_bwd_finalize_frames(hipStream_t s, float* part, int hsplit, const float* gate, const float* bc,
+                                  int frames, int C, int64_t count, const float* gamma, const float* mean,
+                                  const float* invstd, bool training, float* dgamma, float* dbeta, bool accumulate,
+                                  float* coef) {
+  if (hsplit > 1) {
+    // the finalize has only C/64 workgroups: add the pixel-chunk partials of q = 1..4 in a parallel
+    // pass first (in place into chunk 0, h ascending)
+    const int64_t n = (int64_t)frames * C;
+    hipLaunchKernelGGL(sum_parts4_kernel, dim3(ew_grid(4 * n)), dim3(256), 0, s, part, hsplit, n);
+    DFD_HIP_CHECK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_frames_kernel<true>, dim3(cdiv(C, 64)), dim3(1024), 0, s, part, hsplit, gate, bc,
+                     frames, C, count, gamma, mean, invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -840,8 +851,14 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
 constexpr int SE_RDMAX = 48, SE_TS = SE_RDMAX + 4, SE_CSL = 256, SE_W = 16;  // SE_W waves per workgroup
 typedef float se_f32x4 __attribute__((ext_vector_type(4)));
 
+// A is read from the squeeze / SE-backward partials A[h][f][c] (h < hsplit, added in order):
+// forward A = a_scale * sum (the squeeze mean), backward A = sum * g (1 - g) with g = a_gate[f][c]
+// (de = dgate * sigmoid'); the workgroups of channel slice 0 store A to a_out (sq / de), which the
+// backward's weight gradients read.
 template <bool FWD>
-__global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __restrict__ A, int frames, int C, int rd,
+__global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __restrict__ A, int hsplit, float a_scale,
+                                                       const float* __restrict__ a_gate, float* __restrict__ a_out,
+                                                       int frames, int C, int rd,
                                                        const float* __restrict__ W1, const float* __restrict__ b1,
                                                        const float* __restrict__ rpre_in,
                                                        const float* __restrict__ W2, const float* __restrict__ b2,
@@ -864,10 +881,25 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
     const int kq = k0 + 4 * lk;
     const bool kok = kq < C;
     float av[4], bv[4][3];
-    {
-      const float4 a4 = (fok && kok) ? *reinterpret_cast<const float4*>(A + (int64_t)(f0 + li) * C + kq)
-                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (fok && kok) {
+      const int64_t ai = (int64_t)(f0 + li) * C + kq, hn = (int64_t)frames * C;
+      float4 a4 = *reinterpret_cast<const float4*>(A + ai);
+      if (hsplit > 1)
+      for (int h = 1; h < hsplit; ++h) {
+        const float4 v = *reinterpret_cast<const float4*>(A + h * hn + ai);
+        a4.x += v.x; a4.y += v.y; a4.z += v.z; a4.w += v.w;
+      }
+      if constexpr (FWD) {
+        a4.x *= a_scale; a4.y *= a_scale; a4.z *= a_scale; a4.w *= a_scale;
+      } else {
+        const float4 g = *reinterpret_cast<const float4*>(a_gate + ai);
+        a4.x = a4.x * g.x * (1.f - g.x); a4.y = a4.y * g.y * (1.f - g.y);
+        a4.z = a4.z * g.z * (1.f - g.z); a4.w = a4.w * g.w * (1.f - g.w);
+      }
+      if (blockIdx.y == 0) *reinterpret_cast<float4*>(a_out + ai) = a4;
       av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+    } else {
+      av[0] = av[1] = av[2] = av[3] = 0.f;
     }
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
@@ -941,12 +973,13 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
   }
 }
 
-int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
-                     const float* be, int frames, int C, int rd, float* rpre, float* gate) {
+int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw, float* sq, const float* wr,
+                     const float* br, const float* we, const float* be, int frames, int C, int rd, float* rpre,
+                     float* gate) {
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
   const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
-  hipLaunchKernelGGL(se_chain_kernel<true>, grid, dim3(64 * SE_W), 0, s, sq, frames, C, rd, wr, br, nullptr, we, be, 1.f,
-                     rpre, gate);
+  hipLaunchKernelGGL(se_chain_kernel<true>, grid, dim3(64 * SE_W), 0, s, part, hsplit, inv_hw, nullptr, sq, frames, C,
+                     rd, wr, br, nullptr, we, be, 1.f, rpre, gate);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -956,13 +989,13 @@ int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const floa
 //                                                          (se_chain_kernel, one launch)
 //   gwe[c][j] = sum_f de[f][c] silu(rpre[f][j]),  gbe = sum_f de      (frames ascending)
 //   gwr[j][c] = sum_f dz[f][j] sq[f][c],          gbr = sum_f dz      (one paired MFMA launch)
-int launch_se_fc_bwd(hipStream_t s, const float* de, const float* sq, const float* rpre, const float* wr,
-                     const float* we, int frames, int C, int rd, float inv_hw, float* tmp_dz, float* bc_out,
-                     float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
+int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
+                     const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
+                     float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
   const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
-  hipLaunchKernelGGL(se_chain_kernel<false>, grid, dim3(64 * SE_W), 0, s, de, frames, C, rd, we, nullptr, rpre, wr,
-                     nullptr, inv_hw, tmp_dz, bc_out);
+  hipLaunchKernelGGL(se_chain_kernel<false>, grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames, C, rd,
+                     we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out);
   DFD_HIP_CHECK(hipGetLastError());
   MfmaGemm ge{}, gr{};
   ge.A = de; ge.sam = 1; ge.sak = C; ge.B = rpre; ge.sbk = rd; ge.sbn = 1; ge.b_silu = 1; ge.C = gwe; ge.ldc = rd;
@@ -1080,13 +1113,12 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
   template int launch_bn_apply<T>(hipStream_t, const T*, const float*, const float*, const T*, T*, int64_t, int);    \
   template int launch_bn_bwd_reduce<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, float*, int*);          \
   template int launch_bn_bwd_apply<T>(hipStream_t, const BnBwdIn&, const T*, const float*, T*, int64_t, int);       \
-  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, float*, T*); \
+  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, int*, T*); \
   template int launch_se_bwd_reduce<T>(hipStream_t, const T*, const T*, const Pro&, int, int, int, float*, int64_t, \
                                        float*);                                                                     \
   template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);                            \
   template int launch_se_bn_bwd_reduce<T>(hipStream_t, const T*, const T*, const float*, const float*, const float*, \
-                                          const float*, int, int, int, float*, int64_t, const float*, float*,  \
-                                          float*);                                                             \
+                                          const float*, int, int, int, float*, int64_t, int*);                 \
   template int launch_bn_fold_pw<T>(hipStream_t, const float*, const float*, int, int, T*, T*, float*);             \
   template int launch_col_sums<T>(hipStream_t, const T*, int64_t, int, float*, int64_t, float*);
 DFD_BN_INST(float)

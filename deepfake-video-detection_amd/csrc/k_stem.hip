@@ -213,12 +213,32 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_kernel(StemGeom g, const void
   }
 }
 
+// The BN after the stem (batch statistics) backward, applied while staging the wgrad's dY tile:
+// dY = k1*g + k2*y + k3 per channel (coef = [k1; k2; k3], bn_bwd_finalize) -- the separate
+// bn_bwd_apply pass over the 112x112x32 map (read g, y; write dY) is not needed.
+// coefficients staged in LDS (bnk[3][32], visible after the loop's first barrier)
+__device__ __forceinline__ void stem_bn_coef(const float* coef, float (*bnk)[SCO]) {
+  if (coef && threadIdx.x < 3 * SCO) bnk[threadIdx.x / SCO][threadIdx.x % SCO] = coef[threadIdx.x];
+}
+template <typename T>
+__device__ __forceinline__ void stem_bn_apply(bool ok, float (&d)[8], const Raw8<T>& ry, const float (*bnk)[SCO],
+                                              int v) {
+  float y[8], k1[8], k2[8], k3[8];
+  raw_to_f(ry, y);
+  ld8(&bnk[0][v * 8], k1);
+  ld8(&bnk[1][v * 8], k2);
+  ld8(&bnk[2][v * 8], k3);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) d[j] = ok ? k1[j] * d[j] + k2[j] * y[j] + k3[j] : 0.f;
+}
+
 // dW[co][ci][kh][kw] = sum dY[f,oy,ox,co] * x[f,ci,2oy-1+kh,2ox-1+kw]
 // thread (co = tid & 31, sub = tid >> 5) accumulates all 27 taps over pixels p = sub (mod 8);
 // the next tile's input and dY are loaded into registers while the current tile is reduced.
 template <typename T>
 __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const void* __restrict__ x,
-                                                         const T* __restrict__ dY, float* __restrict__ slab,
+                                                         const T* __restrict__ dY, const T* __restrict__ Yb,
+                                                         const float* __restrict__ coef, float* __restrict__ slab,
                                                          int64_t ntiles) {
   __shared__ float tin[SNIN];
   __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
@@ -233,6 +253,9 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const void*
   float nx[SNLD];
   uint32_t nxok = 0u;
   Raw8<T> nd[4];  // 256 px x 4 vectors / 256 threads
+  Raw8<T> ny[4];  // fused BN backward: the stem's pre-BN output at the same pixels
+  __shared__ __attribute__((aligned(16))) float bnk[3][SCO];
+  stem_bn_coef(coef, bnk);
   auto load = [&](int64_t t) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
@@ -241,7 +264,9 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const void*
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
       const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
-      raw_ld(nd[i], dY + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8, dY, oy < g.Ho && ox < g.Wo);
+      const int64_t o = (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8;
+      raw_ld(nd[i], dY + o, dY, oy < g.Ho && ox < g.Wo);
+      if (coef) raw_ld(ny[i], Yb + o, Yb, oy < g.Ho && ox < g.Wo);
     }
   };
   int64_t t = blockIdx.x;
@@ -256,6 +281,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const void*
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
       float d[8];
       raw_to_f(nd[i], d);
+      if (coef) stem_bn_apply(nd[i].ok, d, ny[i], bnk, v);
       st8(&tg[pix * SCO + v * 8], d);
     }
     lds_barrier();
@@ -297,8 +323,9 @@ typedef __attribute__((address_space(3))) stw_s16x4_t stw_lds_s16x4_t;
 typedef float stw_f32x4_t __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, const void* __restrict__ x,
-                                                              const bf16* __restrict__ dY, float* __restrict__ slab,
-                                                              int64_t ntiles) {
+                                                              const bf16* __restrict__ dY, const bf16* __restrict__ Yb,
+                                                              const float* __restrict__ coef,
+                                                              float* __restrict__ slab, int64_t ntiles) {
   __shared__ float tin[SNIN];
   __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
   __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
@@ -315,6 +342,9 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
   float nx[SNLD];
   uint32_t nxok = 0u;
   Raw8<bf16> nd[4];  // 256 px x 4 vectors / 256 threads
+  Raw8<bf16> ny[4];  // fused BN backward: the stem's pre-BN output at the same pixels
+  __shared__ __attribute__((aligned(16))) float bnk[3][SCO];
+  stem_bn_coef(coef, bnk);
   auto load = [&](int64_t t) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
@@ -323,7 +353,9 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
       const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
-      raw_ld(nd[i], dY + (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8, dY, oy < g.Ho && ox < g.Wo);
+      const int64_t o = (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8;
+      raw_ld(nd[i], dY + o, dY, oy < g.Ho && ox < g.Wo);
+      if (coef) raw_ld(ny[i], Yb + o, Yb, oy < g.Ho && ox < g.Wo);
     }
   };
   const int gq = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
@@ -337,7 +369,14 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
-      raw_st(ys + pix * SWL + v * 8, nd[i]);  // masked pixels store zeros
+      if (coef) {
+        float d[8];
+        raw_to_f(nd[i], d);
+        stem_bn_apply(nd[i].ok, d, ny[i], bnk, v);
+        st8(ys + pix * SWL + v * 8, d);
+      } else {
+        raw_st(ys + pix * SWL + v * 8, nd[i]);  // masked pixels store zeros
+      }
     }
     lds_barrier();
     if (t + gridDim.x < ntiles) load(t + gridDim.x);
@@ -562,24 +601,24 @@ int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float
 }
 
 template <typename T>
-int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* dY, float* slab, int64_t slab_cap,
-                      float* dW, bool accumulate) {
+int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* dY, const T* Yb, const float* coef,
+                      float* slab, int64_t slab_cap, float* dW, bool accumulate) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
   int gx = (int)std::min<int64_t>(ntiles, 1024);
   gx = (int)std::max<int64_t>(1, std::min<int64_t>(gx, slab_cap / (27 * SCO)));
   if constexpr (sizeof(T) == 2)
-    hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, dY, slab, ntiles);
+    hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
   else  // fp32 parity mode: exact fp32 products
-    hipLaunchKernelGGL((stem_wgrad_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, slab, ntiles);
+    hipLaunchKernelGGL((stem_wgrad_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
   DFD_HIP_CHECK(hipGetLastError());
   return launch_reduce_slabs(s, slab, gx, 27 * SCO, dW, accumulate);
 }
 
 template int launch_stem_fwd<float>(hipStream_t, const StemGeom&, const void*, const float*, float*, float*, int*);
 template int launch_stem_fwd<bf16>(hipStream_t, const StemGeom&, const void*, const float*, bf16*, float*, int*);
-template int launch_stem_wgrad<float>(hipStream_t, const StemGeom&, const void*, const float*, float*, int64_t,
-                                      float*, bool);
-template int launch_stem_wgrad<bf16>(hipStream_t, const StemGeom&, const void*, const bf16*, float*, int64_t, float*,
-                                     bool);
+template int launch_stem_wgrad<float>(hipStream_t, const StemGeom&, const void*, const float*, const float*,
+                                      const float*, float*, int64_t, float*, bool);
+template int launch_stem_wgrad<bf16>(hipStream_t, const StemGeom&, const void*, const bf16*, const bf16*,
+                                     const float*, float*, int64_t, float*, bool);
 
 }  // namespace dfd

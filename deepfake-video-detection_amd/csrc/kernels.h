@@ -115,31 +115,35 @@ int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t 
 template <typename T>
 int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const float* coef, T* dY, int64_t M,
                         int C);
-// SE squeeze: sq[f][c] = mean_hw pro(Y)   (pro = BN+SiLU)
+// SE squeeze partials: part[h][f][c] = sum over pixel chunk h of pro(Y)   (pro = BN+SiLU), h < *hsplit
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
-                      int64_t part_cap, float* sq, T* s_out);  // s_out: optional materialised silu(bn(Y))
-// SE excitation: r = silu(Wr sq + br) ; gate = sigmoid(We r + be) ; saves rpre
-int launch_se_fc_fwd(hipStream_t s, const float* sq, const float* wr, const float* br, const float* we,
-                     const float* be, int frames, int C, int rd, float* rpre, float* gate);
+                      int64_t part_cap, int* hsplit, T* s_out);  // s_out: optional materialised silu(bn(Y))
+// SE excitation: sq = inv_hw * sum_h part (stored) ; r = silu(Wr sq + br) ; gate = sigmoid(We r + be) ; saves rpre
+int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw, float* sq, const float* wr,
+                     const float* br, const float* we, const float* be, int frames, int C, int rd, float* rpre,
+                     float* gate);
 // SE backward reduce: dgate[f][c] = sum_hw dZ * pro(Y)   (pro = BN+SiLU, no gate)
 template <typename T>
 int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
                          float* part, int64_t part_cap, float* dgate);
 // SE FC backward: from dgate -> dsq (written, scaled by 1/HW into bc), grads of wr,br,we,be.
 // tmp_de: frames*C floats; tmp_dr: 2*frames*rd floats
-int launch_se_fc_bwd(hipStream_t s, const float* de, const float* sq, const float* rpre, const float* wr,
-                     const float* we, int frames, int C, int rd, float inv_hw, float* tmp_dz, float* bc_out,
-                     float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
-// SE + BN(+SiLU) backward sums in one pass over (dZ, Y): de[f][c] = dgate g (1-g) (SE branch) and the per-frame
-// sums pf[4][frames][C] that bn_bwd_finalize_frames combines with the gate and bc (k_bn.hip)
+// (de = dgate g (1-g) from the q = 0 partials of launch_se_bn_bwd_reduce, stored to `de`)
+int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
+                     const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
+                     float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
+// SE + BN(+SiLU) backward sums in one pass over (dZ, Y): per-frame partials part[5][hsplit][frames][C] -- q = 0
+// the SE gate gradient (added by launch_se_fc_bwd), q = 1..4 the sums bn_bwd_finalize_frames combines with the
+// gate and bc (k_bn.hip)
 template <typename T>
 int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
                             const float* mean, const float* invstd, int frames, int HW, int C, float* part,
-                            int64_t part_cap, const float* gate, float* de, float* pf);
-int launch_bn_bwd_finalize_frames(hipStream_t s, const float* pf, const float* gate, const float* bc, int frames,
-                                  int C, int64_t count, const float* gamma, const float* mean, const float* invstd,
-                                  bool training, float* dgamma, float* dbeta, bool accumulate, float* coef);
+                            int64_t part_cap, int* hsplit);
+int launch_bn_bwd_finalize_frames(hipStream_t s, float* part, int hsplit, const float* gate, const float* bc,
+                                  int frames, int C, int64_t count, const float* gamma, const float* mean,
+                                  const float* invstd, bool training, float* dgamma, float* dbeta, bool accumulate,
+                                  float* coef);
 // conv_pw backward through its BN (no activation), by linearity (k_bn.hip): fold the BN-backward
 // coefficients coef = [k1; k2; k3] into the dgrad operands, combine the weight-gradient terms
 template <typename T>
@@ -215,8 +219,8 @@ template <typename T>
 int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float* w, T* Y, float* stats,
                     int* stat_rows);
 template <typename T>
-int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* dY, float* slab,
-                      int64_t slab_cap, float* dW, bool accumulate);
+int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* dY, const T* Yb, const float* coef,
+                      float* slab, int64_t slab_cap, float* dW, bool accumulate);  // coef: fused BN backward
 
 // ---------------- input pipeline: k_input.hip ----------------
 int launch_collate_gather(hipStream_t s, const uint8_t* src, const int64_t* sel, int64_t nsel, int64_t frame_bytes,

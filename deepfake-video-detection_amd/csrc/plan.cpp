@@ -353,10 +353,12 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
     }
     DFD_TRY(fin(bn_dw, Mout));
     T* s2 = b.o_s2 >= 0 ? r.a(b.o_s2) : nullptr;
+    int hs = 1;
     PROBED(PK_SE_SQUEEZE, &b, (launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
-                                                    r.f(p.o_part), p.part_cap, r.f(b.o_sq), s2)));
-    DFD_TRY(launch_se_fc_fwd(s, r.f(b.o_sq), r.prm(b.t_se_wr), r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be),
-                             p.frames, b.mid, b.rd, r.f(b.o_rpre), r.f(b.o_gate)));
+                                                    r.f(p.o_part), p.part_cap, &hs, s2)));
+    DFD_TRY(launch_se_fc_fwd(s, r.f(p.o_part), hs, 1.0f / (float)hwo, r.f(b.o_sq), r.prm(b.t_se_wr),
+                             r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be), p.frames, b.mid, b.rd,
+                             r.f(b.o_rpre), r.f(b.o_gate)));
     PROBED(PK_PWL_FWD, &b, (launch_pw_gemm<T>(s, s2 ? s2 : r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout,
                                               b.cout, b.mid, s2 ? PRO_GATE : PRO_BN_SILU_G,
                                               r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats, &rows)));
@@ -460,15 +462,17 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                                      grad(b.pwl.t_w), acc != 0)));
         // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE
         // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
+        int hs = 1;
         DFD_TRY(launch_se_bn_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                            r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), p.frames, hwo, b.mid,
-                                           r.f(p.o_part), p.part_cap, r.f(b.o_gate), r.f(p.o_de), r.f(p.o_pf)));
-        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_de), r.f(b.o_sq), r.f(b.o_rpre), r.prm(b.t_se_wr), r.prm(b.t_se_we),
-                                 p.frames, b.mid, b.rd, 1.0f / (float)hwo, r.f(p.o_dz), r.f(p.o_bc), grad(b.t_se_wr),
-                                 grad(b.t_se_br), grad(b.t_se_we), grad(b.t_se_be), acc != 0));
-        DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_pf), r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid, Mout,
-                                              r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), tr != 0,
-                                              grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
+                                           r.f(p.o_part), p.part_cap, &hs));
+        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_de), r.f(b.o_sq), r.f(b.o_rpre),
+                                 r.prm(b.t_se_wr), r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo,
+                                 r.f(p.o_dz), r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we),
+                                 grad(b.t_se_be), acc != 0));
+        DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid,
+                                              Mout, r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd),
+                                              tr != 0, grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
         BnBwdIn i2{};
         i2.dZ = r.a(p.o_ge2); i2.gate = r.f(b.o_gate); i2.bc = r.f(p.o_bc); i2.bc_scale = 1.f;
         i2.rows_per_frame = hwo; i2.silu = true;
@@ -533,11 +537,14 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
       }
     } else {
       const int64_t M = F * p.H1 * p.W1;
-      BnBwdIn in{};
-      in.dZ = r.a(p.o_ge1); in.rows_per_frame = p.H1 * p.W1; in.silu = false;  // ge1 holds g (fused in dw dgrad)
-      DFD_TRY(bwd_bn_from_stats(in, p.bn_stem, r.a(p.o_ystem), M, r.a(p.o_ge1), p.pending_rows));
+      // ge1 holds g (the stage-0 depthwise backward fused the BN+SiLU part and the stats); the BN's
+      // dY = k1*g + k2*y + k3 is applied inside the stem weight gradient's tile staging
+      const BNL& b = p.bn_stem;
+      DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), p.pending_rows, M, b.C, r.prm(b.t_w), r.f(b.o_mean),
+                                     r.f(b.o_invstd), tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
       StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3], stem_fmt(ifmt, x, xs)};
-      DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), slab(), p.slab_cap, grad(p.t_stem), acc != 0));
+      DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), r.a(p.o_ystem), r.f(p.o_coef), slab(), p.slab_cap,
+                                   grad(p.t_stem), acc != 0));
     }
     DFD_TRY(defer.flush());  // this segment's weight gradients are final
     DFD_TRY(slab_err);
