@@ -35,6 +35,12 @@ namespace dfd {
 static std::atomic<int64_t> g_dw_bwd_fused{1};
 int64_t set_dw_bwd_fused(int64_t v) { return g_dw_bwd_fused.exchange(v); }
 bool dw_bwd_fused_enabled() { return tune_or(TK_DW_BWD_FUSED, g_dw_bwd_fused.load(std::memory_order_relaxed)) != 0; }
+// 1: the stride-1 blocks take dw_bwd1_kernel (k_dw_bwd1.hip) with both BN backward passes fused
+static std::atomic<int64_t> g_dw_bwd1{1};
+int64_t set_dw_bwd1(int64_t v) { return g_dw_bwd1.exchange(v); }
+bool dw_bwd1_enabled() {
+  return dw_bwd_fused_enabled() && tune_or(TK_DW_BWD1, g_dw_bwd1.load(std::memory_order_relaxed)) != 0;
+}
 
 template <int TH, int TW, int K, int S, int VW>
 struct DwB {

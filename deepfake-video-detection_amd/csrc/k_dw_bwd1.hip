@@ -1,0 +1,362 @@
+// Stride-1 depthwise-conv backward, one launch per MBConv block, with BOTH neighbouring BatchNorm
+// backward passes fused (timm conv_dw inside the blocks run by self.backbone(x_flat),
+// src/pretrained_detector.py:116):
+//   staging  dY[o]  = k1*g2 + k2*y2 + k3,  g2 = (dZ*gate[f] + bc[f]) * silu'(y2*sc2 + sh2)
+//            (the backward of BN2+SiLU and the SE gate after the depthwise conv -- formerly a
+//            separate bn_bwd_apply pass reading dZ, y2 and writing dY)
+//   strips   dA[p]  = sum_tap dY[p + pad - tap] * w[tap]
+//            g1[p]  = dA * silu'(y1*sc1 + sh1) -> out,   stats += [g1, g1*xhat1]  (BN1 backward sums)
+//            dW[tap] += act[p] * dY[p + pad - tap],  act = silu(y1*sc1 + sh1)
+// Design (MI355X, wave64).  The kernel is VALU-issue bound, so it is built to spend the fewest
+// instructions per output element:
+//   * one workgroup = one TH x TW tile of one frame x 32 channels; dY (+halo) is staged ONCE into
+//     LDS (fp32: no unpacking in the inner loop) through the fused BN2 backward, computed with packed
+//     fp32 math (v_pk_fma_f32) and skipped for halo pixels outside the map;
+//   * thread = (channel pair, strip of RS pixels).  Per kernel row the strip's RS+K-1 dY pairs are
+//     read once and feed BOTH the data gradient (acc[p] += dY * w) and the weight gradient
+//     (dW[row][tap] += act[p] * dY): the activations never go to LDS and no second pass re-reads dY;
+//   * the K*K x 2 weight-gradient accumulators stay in registers for the whole launch and are
+//     reduced once at the end (lanes, then waves, in a fixed order: bit-reproducible).
+#include "dw_common.h"
+
+namespace dfd {
+
+template <typename T, int K, int TH, int TW, int RS>
+struct Dw1 {
+  static constexpr int PAD = K / 2;
+  static constexpr int GH = TH + K - 1, GW = TW + K - 1, NG = GH * GW;
+  static constexpr int NLD = (NG * 4 + 255) / 256;  // 8-channel vector loads per thread per tensor
+  static constexpr int SPR = TW / RS;               // strips per tile row
+  static constexpr int NSTRIP = TH * SPR;
+  static constexpr int RW = RS + K - 1;             // dY pairs per strip row
+  static_assert(TW % RS == 0, "strips tile the row");
+  static constexpr int NP = DCG / 2;                // channel pairs per pixel
+  // rows hold an odd number of pixels: strips are numbered row-fastest, so the two 16-lane slot
+  // groups of each 32-lane half of a ds_read_b64 read consecutive rows, in opposite bank halves
+  static constexpr int DRS = (GW | 1) * NP;         // dys row stride (float2 pairs)
+  static constexpr int RED = 4 * (K * K + 2) * DCG * 4;  // end-of-launch reduction scratch (bytes)
+  static constexpr int DYB = GH * DRS * 8 > RED ? GH * DRS * 8 : RED;
+  static constexpr int LDS = DYB + K * K * DCG * 4 + 9 * DCG * 4;
+  static constexpr int OCC = (sizeof(T) == 2 && K == 3) ? 3 : 2;  // workgroups per CU (= the kernel's launch bounds)
+  static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
+};
+
+struct Dw1Bn2 {           // the fused BN2(+SiLU, SE gate) backward of the staging
+  const float* gate;      // [frames][C]
+  const float* bc;        // [frames][C]
+  const float* sc;        // BN2 scale (gamma*invstd), shift
+  const float* sh;
+  const float* coef;      // [3][C]: k1, k2, k3 of bn_bwd_finalize_frames
+};
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// raw two-channel global load and its unpacking
+template <typename T> struct Raw2;
+template <> struct Raw2<bf16> { uint32_t v; };
+template <> struct Raw2<float> { float2 v; };
+__device__ __forceinline__ void raw2_ld(Raw2<bf16>& r, const bf16* p) { r.v = *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ void raw2_ld(Raw2<float>& r, const float* p) { r.v = *reinterpret_cast<const float2*>(p); }
+__device__ __forceinline__ v2f raw2_f(const Raw2<bf16>& r) {
+  return v2f{__uint_as_float(r.v << 16), __uint_as_float(r.v & 0xffff0000u)};
+}
+__device__ __forceinline__ v2f raw2_f(const Raw2<float>& r) { return v2f{r.v.x, r.v.y}; }
+// pairs of an 8-element raw vector
+__device__ __forceinline__ v2f raw8_pair(const Raw8<bf16>& r, int q) {
+  const uint32_t w = q == 0 ? r.a.x : q == 1 ? r.a.y : q == 2 ? r.a.z : r.a.w;
+  return v2f{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ v2f raw8_pair(const Raw8<float>& r, int q) {
+  return q == 0 ? v2f{r.a.x, r.a.y} : q == 1 ? v2f{r.a.z, r.a.w} : q == 2 ? v2f{r.b.x, r.b.y} : v2f{r.b.z, r.b.w};
+}
+__device__ __forceinline__ v2f round2(v2f v, bf16*) {
+  const uint32_t w = pack2bf(v.x, v.y);
+  return v2f{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+__device__ __forceinline__ v2f round2(v2f v, float*) { return v; }
+__device__ __forceinline__ void st2(bf16* p, v2f v) { *reinterpret_cast<uint32_t*>(p) = pack2bf(v.x, v.y); }
+__device__ __forceinline__ void st2(float* p, v2f v) { *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y); }
+__device__ __forceinline__ v2f lds2(const float* p) { return *reinterpret_cast<const v2f*>(p); }
+__device__ __forceinline__ v2f sigmoid2(v2f z) { return v2f{sigmoidf_(z.x), sigmoidf_(z.y)}; }
+__device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <typename T, int K, int TH, int TW, int RS>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bwd1_kernel(
+    DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
+    const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
+    int ntiles, int groups, int tiles_x, int tiles_y) {
+  using D = Dw1<T, K, TH, TW, RS>;
+  __shared__ __attribute__((aligned(16))) char dyraw[D::DYB];  // staged dY (fp32 pairs); reduction scratch
+  __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
+  __shared__ __attribute__((aligned(16))) float cst[9][DCG];       // sc2 sh2 k1 k2 k3 | sc1 sh1 mean1 invstd1
+  float* dys = reinterpret_cast<float*>(dyraw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = blockIdx.x % groups;
+  const int c0 = grp * DCG, C = g.C;
+  for (int i = tid; i < K * K * DCG; i += 256) {
+    const int tap = i / DCG, cl = i - tap * DCG;
+    wts[i] = (c0 + cl < C) ? w[(int64_t)(c0 + cl) * K * K + tap] : 0.f;
+  }
+  for (int i = tid; i < 9 * DCG; i += 256) {
+    const int k = i / DCG, cl = i - k * DCG, c = c0 + cl;
+    const bool ok = c < C;
+    float v = 0.f;
+    switch (k) {
+      case 0: v = ok ? b2.sc[c] : 0.f; break;
+      case 1: v = ok ? b2.sh[c] : 0.f; break;
+      case 2: v = ok ? b2.coef[c] : 0.f; break;
+      case 3: v = ok ? b2.coef[C + c] : 0.f; break;
+      case 4: v = ok ? b2.coef[2 * C + c] : 0.f; break;
+      case 5: v = ok ? bn1.scale[c] : 1.f; break;
+      case 6: v = ok ? bn1.shift[c] : 0.f; break;
+      case 7: v = ok ? bn1.mean[c] : 0.f; break;
+      default: v = ok ? bn1.invstd[c] : 1.f; break;
+    }
+    cst[k][cl] = v;
+  }
+  const int tpf = tiles_x * tiles_y;
+  const int tstep = gridDim.x / groups;
+  const int fstride = g.H * g.W * C;  // elements per frame (< 2^31: checked by the launcher)
+  const int v8 = tid & 3, c8 = c0 + v8 * 8;
+  const bool cok8 = c8 < C;
+  const int cp = tid & 15, slot = tid >> 4;  // channel pair; strip slot
+  const int ch = c0 + 2 * cp;
+  const bool cokp = ch < C;
+
+  // ---- weight-gradient accumulators and BN1 sums, live for the whole launch ----
+  v2f dw[K][K];
+#pragma unroll
+  for (int a = 0; a < K; ++a)
+#pragma unroll
+    for (int b = 0; b < K; ++b) dw[a][b] = v2f{0.f, 0.f};
+  v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
+
+  for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
+    const int f = t / tpf, r = t - f * tpf, ty = r / tiles_x;
+    const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
+    // ---- staging loads: dZ, y2 + halo (this thread's 8 channels); frame base + 32-bit offsets ----
+    Raw8<T> rz[D::NLD], r2[D::NLD];
+    {
+      const T* zf = dZ + (int64_t)f * fstride;
+      const T* yf = Y2 + (int64_t)f * fstride;
+#pragma unroll
+      for (int i = 0; i < D::NLD; ++i) {
+        const int pixl = (tid >> 2) + 64 * i;
+        const int oy = iy0 - D::PAD + pixl / D::GW, ox = ix0 - D::PAD + pixl % D::GW;
+        const bool in = pixl < D::NG && cok8 && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
+        const uint32_t o = in ? (uint32_t)((oy * g.W + ox) * C + c8) : 0u;
+        raw_ld(rz[i], zf + o, zf, in);
+        raw_ld(r2[i], yf + o, yf, in);
+      }
+    }
+    v2f gt[4], bcv[4];  // the frame's SE gate and squeeze-path gradient (tiny, L2-resident)
+    {
+      float a[8], b[8];
+      if (cok8) {
+        ld8f(b2.gate + (int64_t)f * C + c8, a);
+        ld8f(b2.bc + (int64_t)f * C + c8, b);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        gt[q] = v2f{a[2 * q], a[2 * q + 1]};
+        bcv[q] = v2f{b[2 * q], b[2 * q + 1]};
+      }
+    }
+    lds_barrier();  // the previous tile's strips are done with dys
+    // ---- commit: the fused BN2 backward into fp32 LDS (zero outside the map) ----
+#pragma unroll
+    for (int i = 0; i < D::NLD; ++i) {
+      const int pixl = (tid >> 2) + 64 * i;
+      asm volatile("" ::: "memory");  // the BN2 constants are re-read per pixel (few live registers)
+      if (pixl < D::NG) {
+        float* dst = dys + (pixl / D::GW) * D::DRS * 2 + (pixl % D::GW) * DCG + v8 * 8;
+        if (rz[i].ok) {
+          float o[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cq = v8 * 8 + 2 * q;
+            const v2f z = raw8_pair(rz[i], q), y = raw8_pair(r2[i], q);
+            const v2f tz = fma2(y, lds2(&cst[0][cq]), lds2(&cst[1][cq]));
+            const v2f sg = sigmoid2(tz);
+            const v2f ds = sg * fma2(tz, 1.0f - sg, v2f{1.f, 1.f});
+            const v2f g2 = fma2(z, gt[q], bcv[q]) * ds;
+            const v2f v = round2(fma2(lds2(&cst[2][cq]), g2, fma2(lds2(&cst[3][cq]), y, lds2(&cst[4][cq]))),
+                                 (T*)nullptr);
+            o[2 * q] = v.x;
+            o[2 * q + 1] = v.y;
+          }
+          st8(dst, o);
+        } else {
+          const float zero[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          st8(dst, zero);
+        }
+      }
+    }
+    lds_barrier();
+
+    // ---- strips: data gradient + weight gradient from one read of each dY row ----
+    const v2f sc1 = lds2(&cst[5][2 * cp]), sh1 = lds2(&cst[6][2 * cp]);
+    const v2f is1 = lds2(&cst[8][2 * cp]), mi1 = -lds2(&cst[7][2 * cp]) * is1;  // xhat = y*is + mi
+    const T* y1f = Y1 + (int64_t)f * fstride;
+    T* outf = out + (int64_t)f * fstride;
+#pragma unroll 1
+    for (int s = slot; s < D::NSTRIP; s += 16) {
+      const int pr = s % TH, xs = (s / TH) * RS;
+      const int iy = iy0 + pr;
+      const uint32_t so = (uint32_t)((iy * g.W + ix0 + xs) * C + ch);  // strip start within the frame
+      const bool rok = cokp && iy < g.H;
+      Raw2<T> ry[RS];
+#pragma unroll
+      for (int px = 0; px < RS; ++px) raw2_ld(ry[px], y1f + ((rok && ix0 + xs + px < g.W) ? so + px * C : 0u));
+      // activations (weight-gradient operand) and sigmoids (for silu') of the strip
+      v2f act[RS], sg[RS];
+#pragma unroll
+      for (int px = 0; px < RS; ++px) {
+        const bool ok = rok && ix0 + xs + px < g.W;
+        const v2f z = fma2(raw2_f(ry[px]), sc1, sh1);
+        sg[px] = sigmoid2(z);
+        act[px] = ok ? z * sg[px] : v2f{0.f, 0.f};
+      }
+      v2f acc[RS];
+#pragma unroll
+      for (int px = 0; px < RS; ++px) acc[px] = v2f{0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        asm volatile("" ::: "memory");  // one kernel row's LDS operands live at a time
+        const float* rowp = dys + (pr + K - 1 - kh) * D::DRS * 2 + xs * DCG + 2 * cp;
+        v2f dr[D::RW], wr[K];
+#pragma unroll
+        for (int j = 0; j < D::RW; ++j) dr[j] = lds2(rowp + j * DCG);
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) wr[kw] = lds2(wts + (kh * K + kw) * DCG + 2 * cp);
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+          for (int px = 0; px < RS; ++px) {
+            acc[px] = fma2(dr[px + K - 1 - kw], wr[kw], acc[px]);
+            dw[kh][kw] = fma2(act[px], dr[px + K - 1 - kw], dw[kh][kw]);
+          }
+        // the row's FMAs complete here (otherwise they sink into the per-pixel epilogue and every
+        // row's operands stay live at once)
+#pragma unroll
+        for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc[px]));
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) asm volatile("" : "+v"(dw[kh][kw]));
+      }
+      // ---- epilogue: g1 = dA * silu'(z1) -> out, BN1 backward sums ----
+#pragma unroll
+      for (int px = 0; px < RS; ++px) {
+        const bool ok = rok && ix0 + xs + px < g.W;
+        // silu'(z) = s (1 + z (1 - s)) = s + act (1 - s)
+        const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
+        const v2f gg = round2(acc[px] * dsl, (T*)nullptr);
+        if (ok) {
+          ss += gg;
+          sq = fma2(gg, fma2(raw2_f(ry[px]), is1, mi1), sq);
+          st2(outf + (so + px * C), gg);
+        }
+      }
+    }
+  }
+
+  // ---- fixed-order reductions: lanes of a wave sharing a channel pair, then the 4 waves ----
+#pragma unroll
+  for (int a = 0; a < K; ++a)
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      dw[a][b].x += __shfl_xor(dw[a][b].x, 16, 64);
+      dw[a][b].y += __shfl_xor(dw[a][b].y, 16, 64);
+      dw[a][b].x += __shfl_xor(dw[a][b].x, 32, 64);
+      dw[a][b].y += __shfl_xor(dw[a][b].y, 32, 64);
+    }
+  ss.x += __shfl_xor(ss.x, 16, 64); ss.y += __shfl_xor(ss.y, 16, 64);
+  ss.x += __shfl_xor(ss.x, 32, 64); ss.y += __shfl_xor(ss.y, 32, 64);
+  sq.x += __shfl_xor(sq.x, 16, 64); sq.y += __shfl_xor(sq.y, 16, 64);
+  sq.x += __shfl_xor(sq.x, 32, 64); sq.y += __shfl_xor(sq.y, 32, 64);
+  lds_barrier();
+  float* red = reinterpret_cast<float*>(dyraw);  // [4 waves][K*K + 2][32]
+  if (lane < 16) {
+    float* rw = red + wave * (K * K + 2) * DCG + 2 * cp;
+#pragma unroll
+    for (int a = 0; a < K; ++a)
+#pragma unroll
+      for (int b = 0; b < K; ++b) *reinterpret_cast<v2f*>(rw + (a * K + b) * DCG) = dw[a][b];
+    *reinterpret_cast<v2f*>(rw + (K * K) * DCG) = ss;
+    *reinterpret_cast<v2f*>(rw + (K * K + 1) * DCG) = sq;
+  }
+  lds_barrier();
+  const int64_t row = blockIdx.x / groups;
+  float* sout = slab + row * (int64_t)C * K * K;
+  for (int i = tid; i < (K * K + 2) * DCG; i += 256) {
+    const int e = i / DCG, cl = i - e * DCG;
+    constexpr int E = (K * K + 2) * DCG;
+    const float v = ((red[i] + red[E + i]) + red[2 * E + i]) + red[3 * E + i];
+    if (c0 + cl < C) {
+      if (e < K * K) sout[(int64_t)(c0 + cl) * K * K + e] = v;
+      else stats[(row * 2 + (e - K * K)) * C + c0 + cl] = v;
+    }
+  }
+}
+
+template <typename T, int K, int TH, int TW, int RS>
+static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const Dw1Bn2& b2, const float* w,
+                       const T* Y1, const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab,
+                       int64_t slab_cap, float* dW, bool accumulate) {
+  const int tiles_x = cdiv(g.W, TW), tiles_y = cdiv(g.H, TH);
+  const int ntiles = g.frames * tiles_x * tiles_y;
+  const int groups = cdiv(g.C, DCG);
+  const int64_t per = (int64_t)g.C * K * K;
+  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS>;
+  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS>, 256>();
+  int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
+  rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
+  rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
+  const int gx = (int)(rows * groups);
+  hipLaunchKernelGGL(kern, dim3(gx), dim3(256), 0, s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, slab, ntiles, groups,
+                     tiles_x, tiles_y);
+  DFD_HIP_CHECK(hipGetLastError());
+  if (stat_rows) *stat_rows = (int)rows;
+  return launch_reduce_slabs(s, slab, (int)rows, per, dW, accumulate);
+}
+
+bool dw_bwd1_covers(const DwGeom& g) {
+  if (g.s != 1 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2 || g.Ho != g.H || g.Wo != g.W) return false;
+  if (!dw_bwd1_enabled()) return false;
+  if (g.k == 3) return (g.H % 8 == 0 && g.W % 28 == 0) || (g.H % 14 == 0 && g.W % 14 == 0);
+  return g.H % 14 == 0 && g.W % 14 == 0;
+}
+
+// 0: launched; 1: shape not covered (use the BN2 apply + launch_dw_bwd path)
+template <typename T>
+int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const float* gate, const float* bc,
+                   const float* sc2, const float* sh2, const float* coef2, const float* w, const T* Y1,
+                   const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
+                   bool accumulate) {
+  if (!dw_bwd1_covers(g)) return 1;
+  if ((int64_t)g.H * g.W * g.C >= (1ll << 31)) return 1;  // 32-bit in-frame offsets
+  if (g.C % 2) return 1;                                  // channel-pair accesses
+  const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
+  const int H = g.H, W = g.W;
+  if (g.k == 3) {
+    if (H % 8 == 0 && W % 28 == 0)
+      return bwd1_launch<T, 3, 8, 28, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    if (H % 14 == 0 && W % 14 == 0)
+      return bwd1_launch<T, 3, 14, 14, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    return 1;
+  }
+  if (H % 14 == 0 && W % 14 == 0)
+    return bwd1_launch<T, 5, 14, 14, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+  return 1;
+}
+
+template int launch_dw_bwd1<float>(hipStream_t, const DwGeom&, const float*, const float*, const float*, const float*,
+                                   const float*, const float*, const float*, const float*, const float*,
+                                   const BnBwdIn&, float*, float*, int*, float*, int64_t, float*, bool);
+template int launch_dw_bwd1<bf16>(hipStream_t, const DwGeom&, const bf16*, const bf16*, const float*, const float*,
+                                  const float*, const float*, const float*, const float*, const bf16*,
+                                  const BnBwdIn&, bf16*, float*, int*, float*, int64_t, float*, bool);
+
+}  // namespace dfd

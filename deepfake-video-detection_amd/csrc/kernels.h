@@ -26,7 +26,7 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
 // a plan's forward/backward installs its own Tuning for the enqueuing thread (TuningScope), so
 // concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- never read each other's knobs.
-enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_COUNT };
+enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -80,6 +80,16 @@ int launch_dw_bwd(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T
                   bool accumulate);
 int64_t set_dw_bwd_fused(int64_t v);
 bool dw_bwd_fused_enabled();
+// stride-1 depthwise backward with the BN2 (after the conv) and BN1 (before it) backward fused,
+// k_dw_bwd1.hip: 0 launched, 1 not covered (BN2 apply + launch_dw_bwd instead)
+template <typename T>
+int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const float* gate, const float* bc,
+                   const float* sc2, const float* sh2, const float* coef2, const float* w, const T* Y1,
+                   const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
+                   bool accumulate);
+int64_t set_dw_bwd1(int64_t v);
+bool dw_bwd1_enabled();
+bool dw_bwd1_covers(const DwGeom& g);  // a tile configuration exists and the knob is on
 
 // ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------
 // finalize training stats: mean/invstd/scale/shift + running update (momentum); eval: from running

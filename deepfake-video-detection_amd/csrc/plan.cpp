@@ -473,12 +473,6 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid,
                                               Mout, r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd),
                                               tr != 0, grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
-        BnBwdIn i2{};
-        i2.dZ = r.a(p.o_ge2); i2.gate = r.f(b.o_gate); i2.bc = r.f(p.o_bc); i2.bc_scale = 1.f;
-        i2.rows_per_frame = hwo; i2.silu = true;
-        i2.mean = r.f(bn_dw.o_mean); i2.invstd = r.f(bn_dw.o_invstd);
-        i2.scale = r.f(bn_dw.o_scale); i2.shift = r.f(bn_dw.o_shift);
-        DFD_TRY(launch_bn_bwd_apply<T>(s, i2, r.a(b.o_y2), r.f(p.o_coef), r.a(p.o_ge2), Mout, b.mid));
         // depthwise conv
         // depthwise dgrad fused with the backward reduction of the producer's BN+SiLU
         // (stem BN for the stage-0 block, bn1 otherwise): ge1 = g, stats = partials of g, g*xhat
@@ -488,9 +482,25 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         fz.mean = r.f(bn_in.o_mean); fz.invstd = r.f(bn_in.o_invstd);
         fz.scale = r.f(bn_in.o_scale); fz.shift = r.f(bn_in.o_shift); fz.silu = true;
         int fused = 1;
-        PROBED(PK_DW_DGRAD, &b, ((fused = launch_dw_bwd<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in,
-                                                           &fz, r.f(p.o_stats), &rows, slab(), p.slab_cap,
-                                                           grad(b.t_dw), acc != 0)) < 0 ? -1 : 0));
+        // stride 1: one kernel also applies the BN2(+SiLU, gate) backward while staging dY
+        // (k_dw_bwd1.hip); otherwise the apply pass materialises dY first
+        if (dw_bwd1_covers(g)) {
+          PROBED(PK_DW_DGRAD, &b, (launch_dw_bwd1<T>(s, g, r.a(p.o_ge2), r.a(b.o_y2), r.f(b.o_gate), r.f(p.o_bc),
+                                                     r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(p.o_coef),
+                                                     r.prm(b.t_dw), y_in, fz, r.a(p.o_ge1), r.f(p.o_stats), &rows,
+                                                     slab(), p.slab_cap, grad(b.t_dw), acc != 0)));
+          fused = 0;
+        } else {
+          BnBwdIn i2{};
+          i2.dZ = r.a(p.o_ge2); i2.gate = r.f(b.o_gate); i2.bc = r.f(p.o_bc); i2.bc_scale = 1.f;
+          i2.rows_per_frame = hwo; i2.silu = true;
+          i2.mean = r.f(bn_dw.o_mean); i2.invstd = r.f(bn_dw.o_invstd);
+          i2.scale = r.f(bn_dw.o_scale); i2.shift = r.f(bn_dw.o_shift);
+          DFD_TRY(launch_bn_bwd_apply<T>(s, i2, r.a(b.o_y2), r.f(p.o_coef), r.a(p.o_ge2), Mout, b.mid));
+          PROBED(PK_DW_DGRAD, &b, ((fused = launch_dw_bwd<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in,
+                                                             &fz, r.f(p.o_stats), &rows, slab(), p.slab_cap,
+                                                             grad(b.t_dw), acc != 0)) < 0 ? -1 : 0));
+        }
         if (fused == 1) {
           PROBED(PK_DW_DGRAD, &b, (launch_dw_dgrad<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in, &fz,
                                                       r.f(p.o_stats), &rows)));

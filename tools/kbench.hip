@@ -149,6 +149,22 @@ int main(int argc, char** argv) {
     b.run("dw_bwd", nm, dwb + 2.0 * Mi * C1, [&] {
       return launch_dw_bwd<bf16>(b.s, g, A, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
     });
+    if (k.s == 1) {
+      // the stride-1 backward with the BN2(+SiLU, gate) backward: fused kernel vs apply pass + dw_bwd
+      BnBwdIn i2{};
+      i2.dZ = D; i2.gate = gate; i2.bc = gate; i2.bc_scale = 1.f; i2.rows_per_frame = k.hout * k.hout;
+      i2.silu = true; i2.mean = mean; i2.invstd = invstd; i2.scale = sc; i2.shift = sh;
+      const double b1 = 2.0 * 4 * Mi * C1;
+      if (dw_bwd1_covers(g))
+        b.run("dw_bwd1", nm, b1, [&] {
+          return launch_dw_bwd1<bf16>(b.s, g, D, A, gate, gate, sc, sh, coef, W, C, bi, B, stats, &rows, slab,
+                                      slab_cap, dW, false);
+        });
+      b.run("dw_bwdold", nm, b1, [&] {
+        int e = launch_bn_bwd_apply<bf16>(b.s, i2, A, coef, D, Mo, C1);
+        return e ? e : launch_dw_bwd<bf16>(b.s, g, D, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
+      });
+    }
     b.run("dw_wgrad", nm, dwb, [&] {
       return launch_dw_wgrad<bf16>(b.s, g, A, B, pb, PRO_BN_SILU, slab, slab_cap, dW, false);
     });
