@@ -123,6 +123,16 @@ __device__ __forceinline__ void raw_st(float* p, const Raw8<float>& r) {
   st8(p, v);
 }
 
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch): remap the
+// dispatch index so that LOGICALLY consecutive blocks share one XCD and its L2 (blocks that read the
+// same operand tile then fetch it once per XCD instead of once per block).  A speed hint only:
+// correctness never depends on the placement.
+__device__ __forceinline__ int xcd_swizzle(int b, int n) {
+  const int full = n & ~7;
+  if (b >= full) return b;
+  return (b & 7) * (full >> 3) + (b >> 3);
+}
+
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // outstanding global loads (prefetches stay in flight) or stores.  __syncthreads() carries a
 // workgroup-scope fence that drains vmcnt to 0 whenever a global store is pending.

@@ -15,6 +15,11 @@
 
 #include <atomic>
 
+#ifndef DFD_XCD_SWZ
+#define DFD_XCD_SWZ 1  // XCD-aware block order of the weight-gradient kernel (A/B knob; -5..-20 us
+                       // per 50176/12544-row layer: the 22-126 tiles of one M-split share an L2)
+#endif
+
 namespace dfd {
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -69,8 +74,10 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
   const int rbase = wm * (BM / WM), cbase = wn * (BN / WN);
   // 1-D grid, N tile fastest: the ntn workgroups that share an A row-tile are adjacent in
   // dispatch order, so A is read from HBM once and from L2 by the others.
-  const int nt = (int)(blockIdx.x % ntn);
-  const int64_t mg = blockIdx.x / ntn, mstep = gridDim.x / ntn;
+  const int bid = blockIdx.x;  // (XCD swizzle measured slower here: the persistent m-loop already
+                               // keeps each row tile's ntn workgroups adjacent in time)
+  const int nt = bid % ntn;
+  const int64_t mg = bid / ntn, mstep = gridDim.x / ntn;
   const int n0 = nt * BN;
   const int nvalid = min(BN, N - n0);
   const int nk = (K + GBK - 1) / GBK;
@@ -310,14 +317,16 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   // N <= 128 (the A prologue then runs once per row tile); 128x64 for narrow N; the 14x14 / 7x7
   // stages (few row tiles) want the small tiles for enough workgroups in flight.
   int cfg = (int)tune_or(TK_GEMM_TILE, g_gemm_tile.load());
-  if (cfg < 0 || cfg > 3) {
+  if (cfg < 0 || cfg > 7) {
     if (N <= 64) cfg = 1;
     else if (N <= 128) cfg = 0;
     else if (M <= 16384) cfg = N <= 256 ? 3 : 1;
     else if (M <= 65536) cfg = 2;
     else cfg = N <= 160 ? 1 : 2;
   }
-  const int bm = cfg == 3 ? 32 : cfg == 2 ? 64 : 128, bn = cfg == 0 ? 128 : 64;
+  static constexpr int kBM[8] = {128, 128, 64, 32, 128, 64, 64, 128};
+  static constexpr int kBN[8] = {128, 64, 64, 64, 64, 64, 64, 128};
+  const int bm = kBM[cfg], bn = kBN[cfg];
   const int ntn = cdiv(N, bn);
   const int64_t tiles_m = cdiv64(M, bm);
   const int64_t cap = std::max<int64_t>(1, 1024 / ntn);  // <= 1024 BN-stat partial rows (plan's stats buffer)
@@ -327,7 +336,12 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   if (cfg == 0) gemm_go<T, MODE, ST, EP, 128, 128, 1, 2 - DW, 32, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   else if (cfg == 1) gemm_go<T, MODE, ST, EP, 128, 64, 1, 3 - DW, 32, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   else if (cfg == 2) gemm_go<T, MODE, ST, EP, 64, 64, 2, 3, 32, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
-  else gemm_go<T, MODE, ST, EP, 32, 64, 2, 2, 64, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 3) gemm_go<T, MODE, ST, EP, 32, 64, 2, 2, 64, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  // deeper k-steps (fewer LDS hand-offs per tile) for the long-K late-stage shapes
+  else if (cfg == 4) gemm_go<T, MODE, ST, EP, 128, 64, 1, 2 - DW, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 5) gemm_go<T, MODE, ST, EP, 64, 64, 2, 2, 64, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 6) gemm_go<T, MODE, ST, EP, 64, 64, 2, 1, 128, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else gemm_go<T, MODE, ST, EP, 128, 128, 1, 1, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   if (stat_rows) *stat_rows = gx;
   return 0;
 }
@@ -422,10 +436,14 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 
   using G = WgCfg<T>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tn = blockIdx.x / tnk, tk = blockIdx.x - tn * tnk;
+  // 1-D dispatch order over (tile, split), tiles fastest: the tiles of one M-split share an XCD
+  const int nb = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + blockIdx.x;
+  const int bid = DFD_XCD_SWZ ? xcd_swizzle(lin, nb) : lin;
+  const int split = bid / gridDim.x, tile = bid - split * gridDim.x;
+  const int tn = tile / tnk, tk = tile - tn * tnk;
   const int n0 = tn * WT, k0 = tk * WT;
   const int nv = min(WT, N - n0), kv = min(WT, K - k0);
-  const int64_t mbeg = (int64_t)blockIdx.y * m_per_split;
+  const int64_t mbeg = (int64_t)split * m_per_split;
   const int64_t mend = min(M, mbeg + m_per_split);
   T* Ys = reinterpret_cast<T*>(smem + wave * G::WAVE_BYTES);
   T* Xs = Ys + WMS * G::LS;
@@ -553,7 +571,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 
     }
   }
   lds_barrier();
-  float* out = slab + (int64_t)blockIdx.y * N * K;
+  float* out = slab + (int64_t)split * N * K;
   for (int i = tid; i < WT * WT; i += 256) {
     const int nn = i / WT, kk = i - nn * WT;
     if (nn < nv && kk < kv) out[(int64_t)(n0 + nn) * K + k0 + kk] = red[i];

@@ -25,6 +25,13 @@
 #include <algorithm>
 #include <atomic>
 
+#ifndef DFD_XCD_SWZ_F
+#define DFD_XCD_SWZ_F 1  // XCD-aware block order, streaming forward (A/B knob)
+#endif
+#ifndef DFD_XCD_SWZ_W
+#define DFD_XCD_SWZ_W 1  // XCD-aware block order, streaming weight gradient (A/B knob)
+#endif
+
 namespace dfd {
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
@@ -69,8 +76,9 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
   bf16* ct = reinterpret_cast<bf16*>(gl + gate_frames * KP) + (threadIdx.x >> 6) * (TL::SLAB / 2);  // wave's C slab
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int chunk = (int)(blockIdx.x % (unsigned)nchunks);
-  const int64_t part = blockIdx.x / (unsigned)nchunks;
+  const int bid = DFD_XCD_SWZ_F ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int chunk = bid % nchunks;
+  const int64_t part = bid / nchunks;
   const int n0 = chunk * NC;
 
   for (int f = tid; f < NB * KB * 64; f += 256) {
@@ -438,8 +446,10 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
   char* wave_base = reinterpret_cast<char*>(gl + gate_frames * TL::KW);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int chunk = (int)(blockIdx.x % (unsigned)(nch_n * nch_k));
-  const int64_t part = blockIdx.x / (unsigned)(nch_n * nch_k);
+  // chunks of one row part share an XCD (and its L2): measured in tools/kbench
+  const int bid = DFD_XCD_SWZ_W ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int chunk = bid % (nch_n * nch_k);
+  const int64_t part = bid / (nch_n * nch_k);
   const int cn = chunk / nch_k, ck = chunk - cn * nch_k;
   const int n0 = cn * TL::NW, k0 = ck * TL::KW;
   const int64_t mbeg = part * rows_per_part, mend = min(M, mbeg + rows_per_part);

@@ -172,6 +172,12 @@ int main(int argc, char** argv) {
     b.run("pwl_fwd", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
       return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_BN_SILU_G, pg, stats, &rows);
     });
+    b.run("pwlG_fwd", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {  // pre-activated input: gate-only prologue
+      return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_GATE, pg, stats, &rows);
+    });
+    b.run("pwlG_wgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
+      return launch_pw_wgrad<bf16>(b.s, A, B, Mo, k.cout, C1, PRO_GATE, pg, slab, slab_cap, dW, false);
+    });
     b.run("pwl_dgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
       return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, C1, k.cout, PRO_NONE, pn, nullptr, nullptr);
     });
