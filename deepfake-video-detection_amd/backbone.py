@@ -20,7 +20,7 @@ import math
 import torch
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, ops  # noqa: F401  (registers torch.ops.dfd.*)
 from .flat import FlatModule, GradSink
 
 BN_EPS = 1e-5
@@ -224,13 +224,13 @@ class B0Runtime:
         self.plans: dict = {}
         self.tuning: dict = {}
         self._lock = threading.Lock()
-        self._norm = (ctypes.c_float * 6)(*NORMALIZATIONS["imagenet"][0], *NORMALIZATIONS["imagenet"][1])
+        self._norm = [*NORMALIZATIONS["imagenet"][0], *NORMALIZATIONS["imagenet"][1]]
 
     def set_input_norm(self, spec) -> None:
         mean, std = NORMALIZATIONS[spec] if isinstance(spec, str) else spec
         if len(mean) != 3 or len(std) != 3:
             raise ValueError("input normalisation needs 3 means and 3 stds")
-        self._norm = (ctypes.c_float * 6)(*[float(v) for v in mean], *[float(v) for v in std])
+        self._norm = [*[float(v) for v in mean], *[float(v) for v in std]]
 
     def set_tuning(self, key: str, value: int) -> None:
         """Per-runtime kernel-selection override (same keys as dfd_set_tuning)."""
@@ -265,24 +265,16 @@ class B0Runtime:
         return int(self.lib.dfd_b0_workspace_bytes(h))
 
     def forward(self, x, owner, dtype, training):
+        """torch.ops.dfd.b0_trunk_forward on this runtime's plan for x's shape."""
         N, _, H, W = x.shape
         h = self.plan(N, H, W, dtype, x.device)
-        ws = torch.empty(self.workspace_bytes(h), dtype=torch.uint8, device=x.device)
-        feats = torch.empty(N, FEATURE_DIM, dtype=torch.float32, device=x.device)
-        xs = (ctypes.c_int64 * 4)(*x.stride())
-        fmt = INPUT_U8 if x.dtype == torch.uint8 else INPUT_F32
-        _lib.check(self.lib.dfd_b0_forward_ex(h, _lib.stream_of(x.device), x.data_ptr(), fmt, xs, self._norm,
-                                              owner._flat_p.data_ptr(), owner._flat_b.data_ptr(), ws.data_ptr(),
-                                              feats.data_ptr(), 1 if training else 0, BN_MOMENTUM))
+        feats, ws = torch.ops.dfd.b0_trunk_forward(x, h.value, owner._flat_p, owner._flat_b, self._norm, training,
+                                                   BN_MOMENTUM)
         return feats, (h, ws)
 
     def backward(self, h, ws, x, dfeat, owner, grads, training, seg_begin, seg_end, accumulate=False):
-        xs = (ctypes.c_int64 * 4)(*x.stride())
-        fmt = INPUT_U8 if x.dtype == torch.uint8 else INPUT_F32
-        _lib.check(self.lib.dfd_b0_backward_ex(h, _lib.stream_of(x.device), x.data_ptr(), fmt, xs, self._norm,
-                                               dfeat.data_ptr(), owner._flat_p.data_ptr(), ws.data_ptr(),
-                                               grads.data_ptr(), 1 if training else 0, seg_begin, seg_end,
-                                               1 if accumulate else 0))
+        torch.ops.dfd.b0_trunk_backward(x, h.value, dfeat, owner._flat_p, ws, grads, self._norm, training, seg_begin,
+                                        seg_end, accumulate)
 
     def __del__(self):
         try:

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, ops  # noqa: F401  (registers torch.ops.dfd.*)
 
 
 def _flat_view(tensors):
@@ -102,28 +102,23 @@ class _FusedAdamBase(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         g = self.param_groups[0]
-        lib = _lib.load()
         ranges = self._active_ranges()
         if not ranges:
             return loss
         grads = [self._grad_range(r[2], r[3]) for r in ranges]
-        dev = self._flat_p.device
-        stream = _lib.stream_of(dev)
         clip = None
         if self.max_grad_norm is not None:
             allg = grads[0][0] if len(grads) == 1 else torch.cat([fg for fg, _ in grads])
-            _lib.check(lib.dfd_grad_norm(stream, allg.data_ptr(), allg.numel(), float(self.max_grad_norm),
-                                         self._scratch.data_ptr(), self._norm.data_ptr()))
-            clip = self._norm.data_ptr()
+            torch.ops.dfd.grad_norm(allg, float(self.max_grad_norm), self._scratch, self._norm)
+            clip = self._norm
         b1, b2 = g["betas"]
         for (lo, hi, i0, i1), (flat_g, scatter) in zip(ranges, grads):
             step = self._steps[i0] + 1
             for i in range(i0, i1):
                 self._steps[i] = step
-            _lib.check(lib.dfd_adam_step(stream, self._flat_p[lo:hi].data_ptr(), flat_g.data_ptr(),
-                                         self._m[lo:hi].data_ptr(), self._v[lo:hi].data_ptr(), hi - lo, float(g["lr"]),
-                                         float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), step,
-                                         float(self.grad_scale), 1 if self.decoupled else 0, clip))
+            torch.ops.dfd.adam_step(self._flat_p[lo:hi], flat_g, self._m[lo:hi], self._v[lo:hi], float(g["lr"]),
+                                    float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), step,
+                                    float(self.grad_scale), bool(self.decoupled), clip)
             if scatter is not None:  # gradients were gathered: leave the clipped values in .grad
                 o = 0
                 for t in scatter:
@@ -188,11 +183,9 @@ def clip_grad_norm_(parameters, max_norm: float) -> torch.Tensor:
     flat = _flat_view(gs)
     if flat is None:
         flat = torch.cat([g.reshape(-1) for g in gs])
-    lib = _lib.load()
     out = torch.empty(2, dtype=torch.float32, device=flat.device)
     scratch = torch.empty(1024, dtype=torch.float64, device=flat.device)
-    _lib.check(lib.dfd_grad_norm(_lib.stream_of(flat.device), flat.data_ptr(), flat.numel(), float(max_norm),
-                                 scratch.data_ptr(), out.data_ptr()))
+    torch.ops.dfd.grad_norm(flat, float(max_norm), scratch, out)
     for g in gs:
         g.mul_(out[1])
     return out[0]

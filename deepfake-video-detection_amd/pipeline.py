@@ -9,7 +9,7 @@ frame (zeros if M == 0), stack, permute and divide by 255 ON THE HOST, then ``.t
 
 Here the index rule stays on the host (a few integers per clip), the crops cross PCIe as uint8
 (4x fewer bytes than the fp32 batch) and the gather + ``/255`` run on the device
-(``dfd_collate_frames``, ``csrc/k_input.hip``), bit-identical to the reference's float batch.  For
+(``torch.ops.dfd.collate_frames`` -> ``dfd_collate_frames``, ``csrc/k_input.hip``), bit-identical to the reference's float batch.  For
 the B0 detector the uint8 batch itself can be handed to the model (normalised in the stem).
 """
 from __future__ import annotations
@@ -19,7 +19,7 @@ from pathlib import Path
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, ops  # noqa: F401  (registers torch.ops.dfd.*)
 from .detector import normalize_adjacency
 
 
@@ -100,11 +100,7 @@ def collate_clips(batch, max_frames=16, image_size=(224, 224), device="cuda", ou
     host = np.ascontiguousarray(np.concatenate(srcs)) if srcs else np.zeros((1, frame_bytes), np.uint8)
     src = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True)
     sel_d = sel.pin_memory().to(dev, non_blocking=True)
-    dt = torch.float32 if out == "float" else torch.uint8
-    o = torch.empty((b, max_frames, h, w, 3), dtype=dt, device=dev)
-    lib = _lib.load()
-    _lib.check(lib.dfd_collate_frames(_lib.stream_of(dev), src.data_ptr(), sel_d.data_ptr(), b * max_frames,
-                                      frame_bytes, 1 if out == "float" else 0, o.data_ptr()))
+    o = torch.ops.dfd.collate_frames(src, sel_d, [h, w, 3], out == "float").view(b, max_frames, h, w, 3)
     # (the pinned staging and the device source are stream-ordered: torch's allocators keep them
     # until the copy and the gather have run)
     return o.permute(0, 1, 4, 2, 3), torch.tensor(labels, dtype=torch.long)
