@@ -13,7 +13,10 @@ reference models behind their drop-in modules, one JSON line each:
 Each line carries a ``cpu_baseline``: the oracle restatement timed on the host cores for a
 bounded sample (the reference itself does not travel to the GPU box).
 
-    python bench_temporal.py [--model cnnlstm|rnn|both] [--clips 64] [--image 224] [--steps K] [--warmup W]
+* ``DeepfakeModel`` (src/models.py:222-291, timm ViT-B/16 + SimpleGCN, config C5) train step in
+  bf16 on 128 images (16 graphs x 8 nodes); unit: images/s, plus the MFMA fraction.
+
+    python bench_temporal.py [--model cnnlstm|rnn|vit|both|all] [--clips 64] [--image 224] [--steps K] [--warmup W]
 """
 from __future__ import annotations
 
@@ -143,9 +146,69 @@ def bench_rnn(args, dev):
     return line
 
 
+def bench_vit(args, dev):
+    """C5: ``DeepfakeModel`` (src/models.py:222-291, timm ViT-B/16 branch) train step in bf16 on
+    128 images = ``--graphs`` x ``--nodes`` face crops with the chain graph of collate_batch
+    (train.py:62-100); CE, backward, Adam.  Unit: images/s; ViT-B/16 is 35.1 GFLOP/img forward
+    (SURVEY §8(a)), about 3x that for a train step."""
+    from deepfake_amd.detector import chain_adjacency
+    from deepfake_amd.vit_gcn import DeepfakeModel
+
+    B, N, S = args.graphs, args.nodes, 224
+    m = DeepfakeModel(compute_dtype="bf16")
+    deterministic_init_(m, seed=0)
+    m = m.to(dev).train()
+    opt = FusedAdam(m.parameters(), lr=1e-4)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    u8 = torch.randint(0, 256, (B, N, S, S, 3), generator=g, device=dev, dtype=torch.uint8)
+    x = (u8.float() / 255.0).permute(0, 1, 4, 2, 3)
+    a = torch.from_numpy(chain_adjacency(N)).float().to(dev).expand(B, N, N).contiguous()
+    y = torch.randint(0, 2, (B,), generator=g, device=dev)
+    crit = torch.nn.CrossEntropyLoss()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = crit(m(x, a), y)
+        loss.backward()
+        opt.step()
+
+    dt = _time(step, args.steps, args.warmup)
+    imgs = B * N
+    tflops = 3 * 35.1e9 * imgs / dt / 1e12
+    line = {"metric": "images/sec training DeepfakeModel (ViT-B/16 + GCN)", "value": round(imgs / dt, 2),
+            "unit": "images/s", "n_gpus": 1, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "bf16", "data": "synthetic uint8 frames (seeded, on device) /255, random-init weights",
+            "config": {"workload": "DeepfakeModel train step (ViT-B/16 CLS features -> SimpleGCN -> classifier; CE, "
+                                   "backward, Adam lr 1e-4)", "graphs": B, "nodes": N, "images": imgs,
+                       "image": [S, S, 3]},
+            "mfma": {"achieved_tflops": round(tflops, 1), "peak_tflops": 2500.0, "frac": round(tflops / 2500.0, 4),
+                     "flops_per_image": "3 x 35.1 GFLOP (train step ~ 3x forward)"}}
+    if not args.no_cpu_baseline:
+        from oracle.vit_cpu import DeepfakeModelCPU
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
+        ref = DeepfakeModelCPU().train()
+        ropt = torch.optim.Adam(ref.parameters(), lr=1e-4)
+        xc = torch.rand(1, 2, 3, S, S)
+        ac = torch.from_numpy(chain_adjacency(2)).float().unsqueeze(0)
+        yc = torch.tensor([1])
+
+        def cstep():
+            ropt.zero_grad()
+            crit(ref(xc, ac), yc).backward()
+            ropt.step()
+
+        ct, n = _cpu_time(cstep, args.cpu_seconds)
+        line["cpu_baseline"] = {"value": round(2 / ct, 3), "unit": "images/s", "cores": torch.get_num_threads(),
+                                "kind": "port", "sample": f"{n} steps x 1 graph x 2 nodes {S}^2, fp32 oracle"}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "both"])
+    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "vit", "both", "all"])
+    ap.add_argument("--graphs", type=int, default=16)
+    ap.add_argument("--nodes", type=int, default=8)
     ap.add_argument("--clips", type=int, default=64)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--steps", type=int, default=5)
@@ -155,10 +218,12 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    if args.model in ("rnn", "both"):
+    if args.model in ("rnn", "both", "all"):
         print(json.dumps(bench_rnn(args, dev)), flush=True)
-    if args.model in ("cnnlstm", "both"):
+    if args.model in ("cnnlstm", "both", "all"):
         print(json.dumps(bench_cnnlstm(args, dev)), flush=True)
+    if args.model in ("vit", "all"):
+        print(json.dumps(bench_vit(args, dev)), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,159 @@
+// Plain library GEMMs through hipBLASLt (bf16 in, fp32 accumulate) for the large, compute-bound
+// transformer GEMMs of the ViT-B/16 branch (src/models.py:88-107, 280-291 -> timm
+// vit_base_patch16_224) and the dense convolutions of the ResNet-50 ensemble member
+// (src/pretrained_detector.py:37-40): there the fused prologues of k_gemm.hip buy nothing and
+// hipBLASLt's MFMA kernels run 2-5x faster (tools/torch_gemm_vit.py).  The EfficientNet-B0 hot
+// path keeps its own kernels (BN/SiLU prologues, BN-stat epilogues, skinny shapes where the library
+// is slower: tools/torch_gemm_ref.py).
+//
+// Row-major operands are passed to the column-major library as their transposes:
+//   C[M][N] = A[M][K] . B[N][K]^T (+ bias[N]) (+ R[M][N])  ==  C^T = B^T' . A'  (m = N, n = M)
+//   dW[N][K] (+)= dY[M][N]^T . X[M][K]                     ==  dW^T = X' . dY'^T (m = K, n = N)
+// Algorithms come from the library heuristic (no split-K with atomics requested; deterministic).
+// One handle per device and one workspace per stream, created on first use under a lock; the
+// descriptor/algorithm cache is keyed by shape and guarded by the same lock.
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "kernels.h"
+
+namespace dfd {
+namespace {
+
+constexpr size_t kWorkspace = 128u << 20;
+constexpr int kCand = 8;  // heuristic candidates; the first the library accepts at run time is kept
+
+struct Entry {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
+  hipblasLtMatmulHeuristicResult_t cand[kCand];
+  int ncand = 0, pick = 0;
+};
+
+using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, int>;  // dev, kind, m, n, k, dtypes...
+
+std::mutex g_mu;
+std::map<int, hipblasLtHandle_t> g_handles;
+std::map<std::pair<int, hipStream_t>, void*> g_ws;
+std::map<Key, Entry> g_cache;
+
+#define LT_CHECK(x)                                                                         \
+  do {                                                                                      \
+    hipblasStatus_t st_ = (x);                                                              \
+    if (st_ != HIPBLAS_STATUS_SUCCESS) {                                                    \
+      set_error((std::string("hipBLASLt: ") + #x + " failed (" + std::to_string((int)st_) + ")").c_str(), \
+                __FILE__, __LINE__);                                                        \
+      return -1;                                                                            \
+    }                                                                                       \
+  } while (0)
+
+int handle_and_ws(hipStream_t s, int dev, hipblasLtHandle_t* h, void** ws) {
+  auto it = g_handles.find(dev);
+  if (it == g_handles.end()) {
+    hipblasLtHandle_t nh;
+    LT_CHECK(hipblasLtCreate(&nh));
+    it = g_handles.emplace(dev, nh).first;
+  }
+  *h = it->second;
+  auto wk = std::make_pair(dev, s);
+  auto wi = g_ws.find(wk);
+  if (wi == g_ws.end()) {
+    void* p = nullptr;
+    DFD_HIP_CHECK(hipMalloc(&p, kWorkspace));
+    wi = g_ws.emplace(wk, p).first;
+  }
+  *ws = wi->second;
+  return 0;
+}
+
+// kind 0: C = A . B^T (+bias)(+R), D type = T; kind 1: dW (+)= dY^T . X, D fp32
+int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k,
+          bool bias, Entry& e) {
+  LT_CHECK(hipblasLtMatmulDescCreate(&e.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  const hipblasOperation_t opA = kind == 0 ? HIPBLAS_OP_T : HIPBLAS_OP_N;
+  const hipblasOperation_t opB = kind == 0 ? HIPBLAS_OP_N : HIPBLAS_OP_T;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
+  if (bias) {
+    const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = HIP_R_32F;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
+  if (kind == 0) {  // A' = weights B as K x N (ld K, transposed), B' = activations A as K x M (ld K)
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&e.a, ab, k, m, k));
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&e.b, ab, k, n, k));
+  } else {          // A' = X as K x M (ld K), B' = dY as N x M (ld N, transposed)
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&e.a, ab, m, k, m));
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&e.b, ab, n, k, n));
+  }
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&e.c, cd, m, n, m));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&e.d, cd, m, n, m));
+  hipblasLtMatmulPreference_t pref;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  const uint64_t wsb = kWorkspace;
+  LT_CHECK(hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb, sizeof(wsb)));
+  int got = 0;
+  const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, e.desc, e.a, e.b, e.c, e.d, pref, kCand, e.cand, &got);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || got < 1) {
+    set_error(("hipBLASLt: no algorithm for GEMM " + std::to_string(m) + "x" + std::to_string(n) + "x" +
+               std::to_string(k)).c_str(), __FILE__, __LINE__);
+    return -1;
+  }
+  e.ncand = got;
+  return 0;
+}
+
+int run(hipStream_t s, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k, const void* A,
+        const void* B, const void* C, void* D, const float* bias, float beta) {
+  int dev = 0;
+  DFD_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(g_mu);
+  hipblasLtHandle_t h;
+  void* ws;
+  DFD_TRY(handle_and_ws(s, dev, &h, &ws));
+  const Key key{dev, kind, m, n, k, (int)ab, (int)cd, bias ? 1 : 0, 0};
+  auto it = g_cache.find(key);
+  if (it == g_cache.end()) {
+    Entry e;
+    DFD_TRY(build(h, kind, ab, cd, m, n, k, bias != nullptr, e));
+    it = g_cache.emplace(key, e).first;
+  }
+  Entry& e = it->second;
+  if (bias) LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
+  const float alpha = 1.f;
+  // some heuristic picks are refused by the library at enqueue time for long reductions (status 6
+  // at k = 25216, tools/blaslt_check.hip): nothing was launched then, so the next candidate is tried
+  for (; e.pick < e.ncand; ++e.pick) {
+    const auto& c = e.cand[e.pick];
+    if (c.workspaceSize > kWorkspace) continue;
+    const hipblasStatus_t st = hipblasLtMatmul(h, e.desc, &alpha, A, e.a, B, e.b, &beta, C, e.c, D, e.d, &c.algo, ws,
+                                               c.workspaceSize, s);
+    if (st == HIPBLAS_STATUS_SUCCESS) return 0;
+  }
+  set_error(("hipBLASLt: every candidate algorithm failed for GEMM " + std::to_string(m) + "x" + std::to_string(n) +
+             "x" + std::to_string(k)).c_str(), __FILE__, __LINE__);
+  return -1;
+}
+
+}  // namespace
+
+// C[M][N] = A[M][K] . B[N][K]^T + bias[N] (+ R[M][N]); bf16 in/out, fp32 accumulate
+int blaslt_linear(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
+                  int N, int K) {
+  if (M <= 0) return 0;
+  return run(s, 0, HIP_R_16BF, HIP_R_16BF, N, M, K, B, A, R ? (const void*)R : (const void*)C, C, bias,
+             R ? 1.f : 0.f);
+}
+
+// dW[N][K] (+)= dY[M][N]^T . X[M][K]; bf16 in, fp32 out
+int blaslt_wgrad(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, bool accumulate) {
+  if (M <= 0) return 0;
+  return run(s, 1, HIP_R_16BF, HIP_R_32F, K, N, M, X, dY, dW, dW, nullptr, accumulate ? 1.f : 0.f);
+}
+
+}  // namespace dfd

@@ -621,6 +621,38 @@ int launch_node_mean_bwd(hipStream_t s, const float* dG, int B, int N, int D, fl
   return 0;
 }
 
+// ---- exact-erf GELU as separate passes for the hipBLASLt MLP (blaslt.cpp): G = gelu(Z) and, in
+// place, dZ *= gelu'(Z); bf16, 8 elements per lane ----
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16* __restrict__ Z, bf16* __restrict__ G, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float z[8];
+    ld8(Z + i * 8, z);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = geluf_(z[j]);
+    st8(G + i * 8, z);
+  }
+}
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16* __restrict__ Z, bf16* __restrict__ dZ, int64_t n8) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float z[8], d[8];
+    ld8(Z + i * 8, z);
+    ld8(dZ + i * 8, d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= dgeluf_(z[j]);
+    st8(dZ + i * 8, d);
+  }
+}
+int launch_gelu(hipStream_t s, const bf16* Z, bf16* out, int64_t n, bool backward) {
+  if (n <= 0) return 0;
+  if (n % 8) { set_error("gelu: element count must be a multiple of 8", __FILE__, __LINE__); return -1; }
+  const int64_t n8 = n / 8;
+  const int g = (int)std::min<int64_t>(cdiv64(n8, 256), 4096);
+  if (backward) hipLaunchKernelGGL(gelu_bwd_kernel, dim3(g), dim3(256), 0, s, Z, out, n8);
+  else hipLaunchKernelGGL(gelu_fwd_kernel, dim3(g), dim3(256), 0, s, Z, out, n8);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 #define DFD_VIT_INST(T)                                                                                              \
   template int launch_bgemm<T>(hipStream_t, bool, bool, int, int, int, int, float, const T*, const BgOp&, const T*,   \
                                const BgOp&, T*, const BgOp&);                                                        \

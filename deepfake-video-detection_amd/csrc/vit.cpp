@@ -51,7 +51,7 @@ struct VitLayout {
     int64_t wqkv, wqkvT, wp, wpT, w1, w1T, w2, w2T;
   };
   std::vector<Blk> blk;
-  int64_t wpe, ape, pe, xfin, mu_f, rs_f, S, total;
+  int64_t wpe, ape, pe, xfin, mu_f, rs_f, S, G, total;
   // scratch
   int64_t dx, dxm, dh, dZ, dqkv, dO, dS, part, slab, dpe, stotal;
   int64_t part_cap, slab_cap;
@@ -100,6 +100,7 @@ VitLayout vit_layout(const VitDims& d) {
   L.mu_f = take(4LL * d.images);
   L.rs_f = take(4LL * d.images);
   L.S = take(es * SR * SLD);
+  L.G = d.dtype == 1 ? take(es * M * FF) : 0;  // gelu(Z) of one block (bf16 library-GEMM path)
   L.total = off;
   // scratch
   off = 0;
@@ -157,6 +158,22 @@ int cast_weights(hipStream_t s, const VitDims& d, const VitLayout& L, const floa
 inline BgOp op_tok(int ld) { return BgOp{ld, HEADS, (int64_t)197 * ld, DH}; }
 inline BgOp op_score() { return BgOp{SLD, 1, (int64_t)197 * SLD, 0}; }
 
+// C[M][N] = A . B^T + bias (+ R): hipBLASLt in bf16 mode (plain GEMMs, blaslt.cpp), the k_gemm.hip
+// kernels in the fp32 parity mode
+template <typename T>
+int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N, int K) {
+  if constexpr (sizeof(T) == 2) return blaslt_linear(s, A, B, C, R, bias, M, N, K);
+  return launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE,
+                           (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0));
+}
+// dW[N][K] = dY^T . X
+template <typename T>
+int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float* slab, int64_t slab_cap, float* dW) {
+  if constexpr (sizeof(T) == 2) return blaslt_wgrad(s, dY, X, dW, M, N, K, false);
+  Pro none{};
+  return launch_pw_wgrad<T>(s, dY, X, M, N, K, PRO_NONE, none, slab, slab_cap, dW, false);
+}
+
 template <typename T>
 int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, const float* x,
                   const VitImg& im, char* work, float* feats) {
@@ -166,8 +183,7 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
   DFD_TRY(cast_weights<T>(s, d, L, P, w));
   // patch embedding (Conv2d 16x16/16 as a GEMM over gathered patches) + cls + pos
   DFD_TRY(launch_patch_gather<T>(s, x, im, I, w.at(L.ape)));
-  DFD_TRY(launch_tf_gemm<T>(s, w.at(L.ape), w.at(L.wpe), w.at(L.pe), nullptr, P[3], nullptr, M0, D, D, PRO_NONE,
-                            EPI_BIAS));
+  DFD_TRY(lin<T>(s, w.at(L.ape), w.at(L.wpe), w.at(L.pe), nullptr, P[3], M0, D, D));
   DFD_TRY(launch_tokens_fwd<T>(s, w.at(L.pe), P[0], P[1], I, nt, D, w.at(L.blk[0].x)));
   for (int l = 0; l < d.depth; ++l) {
     const float* const* q = P + 4 + 12 * l;
@@ -175,8 +191,7 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     T* xnext = l + 1 < d.depth ? w.at(L.blk[l + 1].x) : w.at(L.xfin);
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.x), D, q[0], q[1], w.at(b.h1), D, w.template at<float>(b.mu1),
                                 w.template at<float>(b.rs1), M, D, LN_EPS)));
-    DFD_TRY(launch_tf_gemm<T>(s, w.at(b.h1), w.at(b.wqkv), w.at(b.qkv), nullptr, q[3], nullptr, M, D3, D, PRO_NONE,
-                              EPI_BIAS));
+    DFD_TRY(lin<T>(s, w.at(b.h1), w.at(b.wqkv), w.at(b.qkv), nullptr, q[3], M, D3, D));
     T* qkv = w.at(b.qkv);
     // S = (q * 64^-0.5) k^T ; P = softmax(S) ; O = P v
     DFD_TRY(launch_bgemm<T>(s, false, true, BH, nt, nt, DH, 0.125f, qkv, op_tok(D3), qkv + D, op_tok(D3), w.at(L.S),
@@ -185,14 +200,17 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     DFD_TRY(launch_bgemm<T>(s, false, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), qkv + 2 * D, op_tok(D3),
                             w.at(b.O), op_tok(D)));
     // xm = x + proj(O) ; x' = xm + fc2(gelu(fc1(LN2(xm))))
-    DFD_TRY(launch_tf_gemm<T>(s, w.at(b.O), w.at(b.wp), w.at(b.xm), w.at(b.x), q[5], nullptr, M, D, D, PRO_NONE,
-                              EPI_BIAS | EPI_RESID));
+    DFD_TRY(lin<T>(s, w.at(b.O), w.at(b.wp), w.at(b.xm), w.at(b.x), q[5], M, D, D));
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.xm), D, q[6], q[7], w.at(b.h2), D, w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), M, D, LN_EPS)));
-    DFD_TRY(launch_tf_gemm<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], nullptr, M, FF, D, PRO_NONE,
-                              EPI_BIAS));
-    DFD_TRY(launch_tf_gemm<T>(s, w.at(b.Z), w.at(b.w2), xnext, w.at(b.xm), q[11], nullptr, M, D, FF, PRO_GELU,
-                              EPI_BIAS | EPI_RESID));
+    DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D));
+    if constexpr (sizeof(T) == 2) {  // gelu(Z) materialised once for the library GEMM
+      DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));
+      DFD_TRY(lin<T>(s, w.at(L.G), w.at(b.w2), xnext, w.at(b.xm), q[11], M, D, FF));
+    } else {
+      DFD_TRY(launch_tf_gemm<T>(s, w.at(b.Z), w.at(b.w2), xnext, w.at(b.xm), q[11], nullptr, M, D, FF, PRO_GELU,
+                                EPI_BIAS | EPI_RESID));
+    }
   }
   // final norm, CLS rows only (global_pool='token')
   const float* const* fn = P + 4 + 12 * d.depth;
@@ -230,18 +248,25 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     T* dO = sc.at(L.dO);
     T* dS = sc.at(L.dS);
     // ---- MLP: dZ = (dx W2) * gelu'(Z); dW2 = dx^T gelu(Z); dh2 = dZ W1 ----
-    DFD_TRY(launch_tf_gemm<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, w.at(b.Z), M, FF, D, PRO_NONE, EPI_DGELU));
-    DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
+    if constexpr (sizeof(T) == 2) {
+      DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D));
+      DFD_TRY(launch_gelu(s, w.at(b.Z), dZ, M * FF, true));   // dZ *= gelu'(Z)
+      DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));  // gelu(Z) for dW2
+      DFD_TRY(wgrad<T>(s, dx, w.at(L.G), M, D, FF, slab, L.slab_cap, g[10]));
+    } else {
+      DFD_TRY(launch_tf_gemm<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, w.at(b.Z), M, FF, D, PRO_NONE, EPI_DGELU));
+      DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
+    }
     DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
-    DFD_TRY(launch_tf_gemm<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, nullptr, M, D, FF, PRO_NONE, 0));
-    DFD_TRY(launch_pw_wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, PRO_NONE, none, slab, L.slab_cap, g[8], false));
+    DFD_TRY(lin<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, M, D, FF));
+    DFD_TRY(wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, slab, L.slab_cap, g[8]));
     DFD_TRY(launch_colsum<T>(s, dZ, M, FF, part, L.part_cap, g[9], false));
     // LN2: dxm = dx + LN2'(dh2)
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.xm), D, dh, D, q[6], w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), dx, dxm, M, D, part, L.part_cap, g[6], g[7], false)));
     // ---- attention projection ----
-    DFD_TRY(launch_tf_gemm<T>(s, dxm, w.at(b.wpT), dO, nullptr, nullptr, nullptr, M, D, D, PRO_NONE, 0));
-    DFD_TRY(launch_pw_wgrad<T>(s, dxm, w.at(b.O), M, D, D, PRO_NONE, none, slab, L.slab_cap, g[4], false));
+    DFD_TRY(lin<T>(s, dxm, w.at(b.wpT), dO, nullptr, nullptr, M, D, D));
+    DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4]));
     DFD_TRY(launch_colsum<T>(s, dxm, M, D, part, L.part_cap, g[5], false));
     // ---- attention core: dP = dO v^T ; dS = scale P (dP - rowdot) ; dq = dS k ; dk = dS^T q ; dv = P^T dO
     DFD_TRY(launch_bgemm<T>(s, false, true, BH, nt, nt, DH, 1.f, dO, op_tok(D), qkv + 2 * D, op_tok(D3), dS,
@@ -254,8 +279,8 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     DFD_TRY(launch_bgemm<T>(s, true, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), dO, op_tok(D),
                             dqkv + 2 * D, op_tok(D3)));
     // ---- qkv projection and LN1: dx_l = dxm + LN1'(dqkv Wqkv) ----
-    DFD_TRY(launch_tf_gemm<T>(s, dqkv, w.at(b.wqkvT), dh, nullptr, nullptr, nullptr, M, D, D3, PRO_NONE, 0));
-    DFD_TRY(launch_pw_wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, PRO_NONE, none, slab, L.slab_cap, g[2], false));
+    DFD_TRY(lin<T>(s, dqkv, w.at(b.wqkvT), dh, nullptr, nullptr, M, D, D3));
+    DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2]));
     DFD_TRY(launch_colsum<T>(s, dqkv, M, D3, part, L.part_cap, g[3], false));
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.x), D, dh, D, q[0], w.template at<float>(b.mu1), w.template at<float>(b.rs1),
                                 dxm, dx, M, D, part, L.part_cap, g[0], g[1], false)));
@@ -263,7 +288,7 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
   // tokens: dcls, dpos, patch rows -> patch-embedding weight / bias
   T* dpe = sc.at(L.dpe);
   DFD_TRY(launch_tokens_bwd<T>(s, dx, I, nt, D, dpe, G[1], G[0]));
-  DFD_TRY(launch_pw_wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, PRO_NONE, none, slab, L.slab_cap, G[2], false));
+  DFD_TRY(wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, slab, L.slab_cap, G[2]));
   return launch_colsum<T>(s, dpe, M0, D, part, L.part_cap, G[3], false);
 }
 

@@ -68,6 +68,8 @@ int launch_relu_drop_bwd(hipStream_t s, const float* Y, const float* dD, float* 
 int launch_node_mean(hipStream_t s, const float* H, int B, int N, int D, float* G);
 int launch_node_mean_bwd(hipStream_t s, const float* dG, int B, int N, int D, float* dH);
 
+int launch_gelu(hipStream_t s, const bf16* Z, bf16* out, int64_t n, bool backward);
+
 template <typename T>
 __device__ __forceinline__ void lds_st8v(T* p, const float (&v)[8]) { st8(p, v); }
 
