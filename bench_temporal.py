@@ -15,6 +15,8 @@ bounded sample (the reference itself does not travel to the GPU box).
 
 * ``DeepfakeModel`` (src/models.py:222-291, timm ViT-B/16 + SimpleGCN, config C5) train step in
   bf16 on 128 images (16 graphs x 8 nodes); unit: images/s, plus the MFMA fraction.
+* ``EnsembleDetector(['efficientnet_b0', 'resnet50'])`` serving forward (eval, bf16) on 32 clips x 8
+  uint8 crops; unit: frames/s (SURVEY §8(f)1,4).
 
     python bench_temporal.py [--model cnnlstm|rnn|vit|both|all] [--clips 64] [--image 224] [--steps K] [--warmup W]
 """
@@ -204,9 +206,40 @@ def bench_vit(args, dev):
     return line
 
 
+def bench_ensemble(args, dev):
+    """Serving (SURVEY §8(f)1,4): the app's default ``EnsembleDetector(['efficientnet_b0', 'resnet50'])``
+    (app.py:661,1597) in eval mode, bf16, on ``--clips`` x 8 uint8 face crops per call (app MAX_FRAMES,
+    app.py:2050); forward only.  Unit: frames/s; the B0-only detector is timed beside it."""
+    from deepfake_amd.pretrained_detector import EnsembleDetector, PretrainedBackboneDetector
+
+    B, T, S = args.clips, 8, 224
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    u8 = torch.randint(0, 256, (B, T, S, S, 3), generator=g, device=dev, dtype=torch.uint8)
+    x = u8.permute(0, 1, 4, 2, 3)  # uint8 crops, normalised inside the first convolution of each member
+    res = {}
+    for name, m in (("ensemble", EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False,
+                                                  compute_dtype="bf16")),
+                    ("b0", PretrainedBackboneDetector(pretrained=False, compute_dtype="bf16"))):
+        m = m.to(dev).eval()
+
+        def step():
+            with torch.no_grad():
+                m(x)
+
+        res[name] = _time(step, args.steps, args.warmup)
+    dt = res["ensemble"]
+    return {"metric": "frames/sec serving EnsembleDetector(efficientnet_b0 + resnet50)", "value": round(B * T / dt, 2),
+            "unit": "frames/s", "n_gpus": 1, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "bf16", "data": "synthetic uint8 face crops (seeded, on device), random-init weights",
+            "config": {"workload": "EnsembleDetector eval forward (average of both members)", "clips": B,
+                       "frames_per_clip": T, "image": [S, S, 3]},
+            "b0_only": {"value": round(B * T / res["b0"], 2), "ms_per_step": round(res["b0"] * 1e3, 3)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "vit", "both", "all"])
+    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "vit", "ensemble", "both", "all"])
     ap.add_argument("--graphs", type=int, default=16)
     ap.add_argument("--nodes", type=int, default=8)
     ap.add_argument("--clips", type=int, default=64)
@@ -224,6 +257,9 @@ def main():
         print(json.dumps(bench_cnnlstm(args, dev)), flush=True)
     if args.model in ("vit", "all"):
         print(json.dumps(bench_vit(args, dev)), flush=True)
+    if args.model in ("ensemble", "all"):
+        args.clips = min(args.clips, 32)
+        print(json.dumps(bench_ensemble(args, dev)), flush=True)
 
 
 if __name__ == "__main__":

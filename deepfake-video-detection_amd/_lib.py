@@ -60,6 +60,11 @@ _SIGS = {
     "dfd_collate_frames": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i, c_p]),
     "dfd_adam_step": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_i, c_d, c_i, c_p]),
     "dfd_set_tuning": (c_i64, [ctypes.c_char_p, c_i64]),
+    "dfd_rn_im2col": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p]),
+    "dfd_rn_stem_im2col": (c_i, [c_p, c_i, c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_f), c_i, c_i, c_i, c_p]),
+    "dfd_rn_gemm": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_i, c_i64, c_i, c_i]),
+    "dfd_rn_maxpool": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_p]),
+    "dfd_rn_avgpool": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_p]),
     "dfd_pw_conv": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p,
                           ctypes.POINTER(c_i)]),
     "dfd_pw_conv_wgrad": (c_i, [c_p, c_i, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i64, c_p,

@@ -70,18 +70,23 @@ int handle_and_ws(hipStream_t s, int dev, hipblasLtHandle_t* h, void** ws) {
 }
 
 // kind 0: C = A . B^T (+bias)(+R), D type = T; kind 1: dW (+)= dY^T . X, D fp32
+// epi: bit 0 bias, bit 1 ReLU (applied after bias and the residual: D = relu(A.B^T + R + bias))
 int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k,
-          bool bias, Entry& e) {
+          int epi_bits, Entry& e) {
+  const bool bias = (epi_bits & 1) != 0, relu = (epi_bits & 2) != 0;
   LT_CHECK(hipblasLtMatmulDescCreate(&e.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
   const hipblasOperation_t opA = kind == 0 ? HIPBLAS_OP_T : HIPBLAS_OP_N;
   const hipblasOperation_t opB = kind == 0 ? HIPBLAS_OP_N : HIPBLAS_OP_T;
   LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
   LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
-  if (bias) {
-    const hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_BIAS;
-    const hipDataType bt = HIP_R_32F;
+  if (bias || relu) {
+    const hipblasLtEpilogue_t epi = bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
+                                         : HIPBLASLT_EPILOGUE_RELU;
     LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
-    LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+    if (bias) {
+      const hipDataType bt = HIP_R_32F;
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(e.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+    }
   }
   if (kind == 0) {  // A' = weights B as K x N (ld K, transposed), B' = activations A as K x M (ld K)
     LT_CHECK(hipblasLtMatrixLayoutCreate(&e.a, ab, k, m, k));
@@ -109,18 +114,19 @@ int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t
 }
 
 int run(hipStream_t s, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k, const void* A,
-        const void* B, const void* C, void* D, const float* bias, float beta) {
+        const void* B, const void* C, void* D, const float* bias, float beta, bool relu = false) {
   int dev = 0;
   DFD_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_mu);
   hipblasLtHandle_t h;
   void* ws;
   DFD_TRY(handle_and_ws(s, dev, &h, &ws));
-  const Key key{dev, kind, m, n, k, (int)ab, (int)cd, bias ? 1 : 0, 0};
+  const int epi_bits = (bias ? 1 : 0) | (relu ? 2 : 0);
+  const Key key{dev, kind, m, n, k, (int)ab, (int)cd, epi_bits, 0};
   auto it = g_cache.find(key);
   if (it == g_cache.end()) {
     Entry e;
-    DFD_TRY(build(h, kind, ab, cd, m, n, k, bias != nullptr, e));
+    DFD_TRY(build(h, kind, ab, cd, m, n, k, epi_bits, e));
     it = g_cache.emplace(key, e).first;
   }
   Entry& e = it->second;
@@ -148,6 +154,14 @@ int blaslt_linear(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf
   if (M <= 0) return 0;
   return run(s, 0, HIP_R_16BF, HIP_R_16BF, N, M, K, B, A, R ? (const void*)R : (const void*)C, C, bias,
              R ? 1.f : 0.f);
+}
+
+// the same for either dtype (0 fp32, 1 bf16), optionally with a ReLU after bias + residual
+int blaslt_gemm(hipStream_t s, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
+                bool relu, int64_t M, int N, int K) {
+  if (M <= 0) return 0;
+  const hipDataType t = dtype == 1 ? HIP_R_16BF : HIP_R_32F;
+  return run(s, 0, t, t, N, M, K, B, A, R ? R : (const void*)C, C, bias, R ? 1.f : 0.f, relu);
 }
 
 // dW[N][K] (+)= dY[M][N]^T . X[M][K]; bf16 in, fp32 out

@@ -319,6 +319,58 @@ int dfd_collate_frames(void* stream, const uint8_t* src, const int64_t* sel, int
   DFD_GUARD_END
 }
 
+// ---- ResNet-50 ensemble member (inference; k_resnet.hip + hipBLASLt) ----
+int dfd_rn_im2col(void* stream, int dtype, const void* x, int N, int H, int W, int C, int kh, int kw, int stride,
+                  int pad, int Kp, void* out) {
+  DFD_GUARD_BEGIN
+  if (!x || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  if (dtype == 1)
+    return dfd::launch_rn_im2col((hipStream_t)stream, (const dfd::bf16*)x, N, H, W, C, kh, kw, stride, pad, Kp,
+                                 (dfd::bf16*)out);
+  return dfd::launch_rn_im2col((hipStream_t)stream, (const float*)x, N, H, W, C, kh, kw, stride, pad, Kp, (float*)out);
+  DFD_GUARD_END
+}
+
+int dfd_rn_stem_im2col(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
+                       const float* norm6, int N, int H, int W, void* out) {
+  DFD_GUARD_BEGIN
+  if (!x || !out || !strides4) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  dfd::InputFmt in{};
+  in.u8 = input_fmt == DFD_INPUT_U8 ? 1 : 0;
+  for (int c = 0; c < 3; ++c) {
+    in.mean[c] = norm6 ? norm6[c] : 0.f;
+    in.stdv[c] = norm6 ? norm6[3 + c] : 1.f;
+  }
+  if (dtype == 1) return dfd::launch_rn_stem_im2col((hipStream_t)stream, x, in, strides4, N, H, W, (dfd::bf16*)out);
+  return dfd::launch_rn_stem_im2col((hipStream_t)stream, x, in, strides4, N, H, W, (float*)out);
+  DFD_GUARD_END
+}
+
+int dfd_rn_gemm(void* stream, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
+                int relu, int64_t M, int N, int K) {
+  DFD_GUARD_BEGIN
+  if (!A || !B || !C) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::blaslt_gemm((hipStream_t)stream, dtype, A, B, C, R, bias, relu != 0, M, N, K);
+  DFD_GUARD_END
+}
+
+int dfd_rn_maxpool(void* stream, int dtype, const void* x, int N, int H, int W, int C, void* out) {
+  DFD_GUARD_BEGIN
+  if (!x || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  if (dtype == 1)
+    return dfd::launch_rn_maxpool((hipStream_t)stream, (const dfd::bf16*)x, N, H, W, C, (dfd::bf16*)out);
+  return dfd::launch_rn_maxpool((hipStream_t)stream, (const float*)x, N, H, W, C, (float*)out);
+  DFD_GUARD_END
+}
+
+int dfd_rn_avgpool(void* stream, int dtype, const void* x, int N, int HW, int C, float* out) {
+  DFD_GUARD_BEGIN
+  if (!x || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  if (dtype == 1) return dfd::launch_rn_avgpool((hipStream_t)stream, (const dfd::bf16*)x, N, HW, C, out);
+  return dfd::launch_rn_avgpool((hipStream_t)stream, (const float*)x, N, HW, C, out);
+  DFD_GUARD_END
+}
+
 int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "stream_min_rows") == 0) return dfd::set_stream_min_rows(value);
   if (key && strcmp(key, "fold_min_rows") == 0) return dfd::set_fold_min_rows(value);

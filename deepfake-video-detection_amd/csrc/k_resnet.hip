@@ -1,0 +1,154 @@
+// ResNet-50 member of EnsembleDetector (src/pretrained_detector.py:37-40: torchvision resnet50
+// minus fc, the app's default ensemble ENSEMBLE_BACKBONES, app.py:661,1597), inference path.
+// Layout NHWC.  Every convolution is a GEMM through hipBLASLt (blaslt.cpp) with the eval-mode
+// BatchNorm folded into its weights and bias, the ReLU and the bottleneck's identity add in the
+// library epilogue; what is not a plain GEMM lives here:
+//   im2col      NHWC T -> [N*Ho*Wo][Kp] T, column (ky*kw + kx)*C + c, zero padding (k > 1 or stride 2)
+//   stem im2col the (N,3,H,W) frames (any strides; fp32, or uint8 normalised like the B0 stem) for
+//               conv1 7x7/2 -> [N*112*112][152] (147 taps zero padded to 16-B rows)
+//   maxpool     3x3/2 pad 1 (torchvision resnet.maxpool)
+//   avgpool     global average -> (N, C) fp32 (AdaptiveAvgPool2d((1,1)), fixed-order sum)
+#include "kernels.h"
+
+namespace dfd {
+
+template <typename T>
+__global__ __launch_bounds__(256) void rn_im2col_vec_kernel(const T* __restrict__ x, int H, int W, int C, int kh,
+                                                            int kw, int stride, int pad, int Ho, int Wo, int Kp,
+                                                            int64_t rows, T* __restrict__ out) {
+  // one lane = 8 channels of one tap of one output pixel
+  const int cv = C / 8, per_row = kh * kw * cv;
+  const int64_t total = rows * per_row;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / per_row;
+    const int r = (int)(i - m * per_row), tap = r / cv, c8 = (r - tap * cv) * 8;
+    const int ky = tap / kw, kx = tap - ky * kw;
+    const int64_t n = m / ((int64_t)Ho * Wo);
+    const int rem = (int)(m - n * Ho * Wo), oy = rem / Wo, ox = rem - oy * Wo;
+    const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) ld8(x + ((n * H + iy) * W + ix) * C + c8, v);
+    st8(out + m * Kp + tap * C + c8, v);
+  }
+}
+
+// conv1 rows: Kp = 152 columns = 147 taps (ky, kx, c) + 5 zeros
+template <typename T>
+__global__ __launch_bounds__(256) void rn_stem_im2col_kernel(const void* __restrict__ x, int64_t sn, int64_t sc,
+                                                             int64_t sh, int64_t sw, InputFmt in, int H, int W,
+                                                             int Ho, int Wo, int64_t rows, T* __restrict__ out) {
+  constexpr int KS = 7, KP = 152;
+  const int64_t total = rows * KP;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / KP;
+    const int col = (int)(i - m * KP);
+    float v = 0.f;
+    if (col < KS * KS * 3) {
+      const int tap = col / 3, c = col - tap * 3, ky = tap / KS, kx = tap - ky * KS;
+      const int64_t n = m / ((int64_t)Ho * Wo);
+      const int rem = (int)(m - n * Ho * Wo), oy = rem / Wo, ox = rem - oy * Wo;
+      const int iy = oy * 2 - 3 + ky, ix = ox * 2 - 3 + kx;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const int64_t o = n * sn + c * sc + iy * sh + ix * sw;
+        // uint8: the reference's `.float() / 255.0` then (v - mean) / std, same operations in order
+        if (in.u8) v = ((float)static_cast<const uint8_t*>(x)[o] / 255.0f - in.mean[c]) / in.stdv[c];
+        else v = static_cast<const float*>(x)[o];
+      }
+    }
+    out[i] = Tr<T>::from_f(v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rn_maxpool_kernel(const T* __restrict__ x, int N, int H, int W, int C, int Ho,
+                                                         int Wo, T* __restrict__ out) {
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * Ho * Wo * cv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c8 = (int)(i % cv) * 8;
+    const int64_t p = i / cv;
+    const int64_t n = p / ((int64_t)Ho * Wo);
+    const int rem = (int)(p - n * Ho * Wo), oy = rem / Wo, ox = rem - oy * Wo;
+    float mx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx[j] = -INFINITY;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * 2 - 1 + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = ox * 2 - 1 + kx;
+        if (ix < 0 || ix >= W) continue;
+        float v[8];
+        ld8(x + ((n * H + iy) * W + ix) * C + c8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) mx[j] = fmaxf(mx[j], v[j]);
+      }
+    }
+    st8(out + p * C + c8, mx);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rn_avgpool_kernel(const T* __restrict__ x, int HW, int C, float inv,
+                                                         float* __restrict__ out) {
+  const int n = blockIdx.y;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += Tr<T>::to_f(x[((int64_t)n * HW + p) * C + c]);
+    out[(int64_t)n * C + c] = s * inv;
+  }
+}
+
+static int ew_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 8192)); }
+
+template <typename T>
+int launch_rn_im2col(hipStream_t s, const T* x, int N, int H, int W, int C, int kh, int kw, int stride, int pad,
+                     int Kp, T* out) {
+  if (C % 8 || Kp < kh * kw * C) { set_error("resnet im2col: C % 8 != 0 or Kp too small", __FILE__, __LINE__); return -1; }
+  const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
+  const int64_t rows = (int64_t)N * Ho * Wo;
+  hipLaunchKernelGGL(rn_im2col_vec_kernel<T>, dim3(ew_grid(rows * kh * kw * (C / 8))), dim3(256), 0, s, x, H, W, C, kh,
+                     kw, stride, pad, Ho, Wo, Kp, rows, out);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int launch_rn_stem_im2col(hipStream_t s, const void* x, const InputFmt& in, const int64_t* strides, int N, int H,
+                          int W, T* out) {
+  const int Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+  const int64_t rows = (int64_t)N * Ho * Wo;
+  hipLaunchKernelGGL(rn_stem_im2col_kernel<T>, dim3(ew_grid(rows * 152)), dim3(256), 0, s, x, strides[0], strides[1],
+                     strides[2], strides[3], in, H, W, Ho, Wo, rows, out);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* out) {
+  if (C % 8) { set_error("resnet maxpool: C % 8 != 0", __FILE__, __LINE__); return -1; }
+  const int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  hipLaunchKernelGGL(rn_maxpool_kernel<T>, dim3(ew_grid((int64_t)N * Ho * Wo * (C / 8))), dim3(256), 0, s, x, N, H, W,
+                     C, Ho, Wo, out);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
+int launch_rn_avgpool(hipStream_t s, const T* x, int N, int HW, int C, float* out) {
+  if (N > 65535) { set_error("resnet avgpool: at most 65535 frames", __FILE__, __LINE__); return -1; }
+  hipLaunchKernelGGL(rn_avgpool_kernel<T>, dim3(cdiv(C, 256), N), dim3(256), 0, s, x, HW, C, 1.0f / (float)HW, out);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+#define DFD_RN_INST(T)                                                                                           \
+  template int launch_rn_im2col<T>(hipStream_t, const T*, int, int, int, int, int, int, int, int, int, T*);       \
+  template int launch_rn_stem_im2col<T>(hipStream_t, const void*, const InputFmt&, const int64_t*, int, int, int, \
+                                        T*);                                                                    \
+  template int launch_rn_maxpool<T>(hipStream_t, const T*, int, int, int, int, T*);                                \
+  template int launch_rn_avgpool<T>(hipStream_t, const T*, int, int, int, float*);
+DFD_RN_INST(float)
+DFD_RN_INST(bf16)
+
+}  // namespace dfd

@@ -47,10 +47,25 @@ int set_gemm_tile(int v);  // tiled pw GEMM: force tile config 0/1/2, -1 = auto 
 // Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
 // pro_mode PRO_NONE or PRO_GELU; epi a mask of GemmEpi.
 enum GemmEpi { EPI_RESID = 1, EPI_BIAS = 2, EPI_DGELU = 4 };
+// ---------------- ResNet-50 ensemble member (inference): k_resnet.hip ----------------
+struct InputFmt;
+template <typename T>
+int launch_rn_im2col(hipStream_t s, const T* x, int N, int H, int W, int C, int kh, int kw, int stride, int pad,
+                     int Kp, T* out);
+template <typename T>
+int launch_rn_stem_im2col(hipStream_t s, const void* x, const InputFmt& in, const int64_t* strides, int N, int H,
+                          int W, T* out);
+template <typename T>
+int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* out);
+template <typename T>
+int launch_rn_avgpool(hipStream_t s, const T* x, int N, int HW, int C, float* out);
+
 // plain library GEMMs through hipBLASLt (blaslt.cpp): C = A . B^T + bias (+ R); dW (+)= dY^T . X
 int blaslt_linear(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
                   int N, int K);
 int blaslt_wgrad(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, bool accumulate);
+int blaslt_gemm(hipStream_t s, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
+                bool relu, int64_t M, int N, int K);
 
 template <typename T>
 int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,

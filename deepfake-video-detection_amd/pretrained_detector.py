@@ -22,8 +22,10 @@ Arithmetic: ``compute_dtype="fp32"`` (default -- the drop-in meets the north-sta
 atol 1e-5 on logits and loss) or ``"bf16"`` (the training/serving performance mode; bounds in
 tests/test_b0_224_gpu.py and tests/test_serving.py).
 
-Only ``efficientnet_b0`` (the hot path) is provided; ``pretrained=True`` would download
-timm weights in the reference and is refused here (offline; load a checkpoint instead).
+Backbones: ``efficientnet_b0`` (the hot path: training and inference) and ``resnet50`` (the app's
+default ensemble member, ``app.py:661,1597``: inference only -- ``resnet.ResNet50Trunk``, torchvision
+key names, eval BatchNorm folded into hipBLASLt GEMMs).  ``pretrained=True`` would download timm /
+torchvision weights in the reference and is refused here (offline; load a checkpoint instead).
 """
 from __future__ import annotations
 
@@ -36,6 +38,8 @@ import torch.nn.functional as F
 
 from . import _lib
 from .backbone import FEATURE_DIM, EfficientNetB0Trunk
+from .resnet import FEATURE_DIM as RESNET_FEATURE_DIM
+from .resnet import ResNet50Trunk
 from .flat import FlatModule, GradSink
 
 ATTN_HIDDEN = 64
@@ -48,17 +52,21 @@ class PretrainedBackboneDetector(FlatModule):
                  dropout_rate: float = 0.5, freeze_backbone: bool = False, use_temporal_attention: bool = True,
                  compute_dtype: str = "fp32", input_normalization="imagenet"):
         super().__init__()
-        if backbone_name != "efficientnet_b0":
-            raise ValueError(f"Unsupported backbone: {backbone_name} (the MI355X hot path implements "
-                             f"efficientnet_b0 only)")
+        if backbone_name not in ("efficientnet_b0", "resnet50"):
+            raise ValueError(f"Unsupported backbone: {backbone_name} (the MI355X path implements "
+                             f"efficientnet_b0 and, for inference, resnet50)")
         if pretrained:
             raise RuntimeError("pretrained=True fetches timm ImageNet weights, which is unavailable offline; "
                                "construct with pretrained=False and load a checkpoint (app.py:1691 does)")
         self.backbone_name = backbone_name
         self.num_classes = num_classes
         self.use_temporal_attention = use_temporal_attention
-        self.backbone = EfficientNetB0Trunk(compute_dtype, input_normalization)
-        self.feature_dim = FEATURE_DIM
+        if backbone_name == "resnet50":  # src/pretrained_detector.py:37-40 (fc.in_features = 2048)
+            self.backbone = ResNet50Trunk(compute_dtype, input_normalization)
+            self.feature_dim = RESNET_FEATURE_DIM
+        else:
+            self.backbone = EfficientNetB0Trunk(compute_dtype, input_normalization)
+            self.feature_dim = FEATURE_DIM
         if freeze_backbone:
             for p in self.backbone.parameters():
                 p.requires_grad = False
@@ -79,8 +87,13 @@ class PretrainedBackboneDetector(FlatModule):
         nn.init.constant_(self.fc2.bias, 0)
 
     def unfreeze_backbone(self, num_blocks: int = 2):
-        # reference: `if hasattr(self.backbone, 'blocks')` is False for the Sequential trunk -> no-op
-        if hasattr(self.backbone, "blocks"):
+        """pretrained_detector.py:87-101: resnet -> the last ``num_blocks`` children of the trunk;
+        efficientnet -> ``backbone.blocks`` (absent on the Sequential trunk: a no-op)."""
+        if self.backbone_name.startswith("resnet"):
+            for layer in list(self.backbone.children())[-num_blocks:]:
+                for p in layer.parameters():
+                    p.requires_grad = True
+        elif hasattr(self.backbone, "blocks"):
             for block in self.backbone.blocks[-num_blocks:]:
                 for p in block.parameters():
                     p.requires_grad = True
@@ -94,7 +107,8 @@ class PretrainedBackboneDetector(FlatModule):
         self.backbone.compute_dtype = v
 
     def _on_flatten(self) -> None:
-        self.backbone.attach(self, "backbone.")
+        if isinstance(self.backbone, EfficientNetB0Trunk):
+            self.backbone.attach(self, "backbone.")
         names = self._head_param_names()
         self._head_names = names
         lo = self._p_off[names[0]]
@@ -120,7 +134,10 @@ class PretrainedBackboneDetector(FlatModule):
         batch_size, num_frames, c, h, w = x.shape
         x_flat = x.reshape(batch_size * num_frames, c, h, w)
         sink = GradSink(self)
-        feats = self.backbone(x_flat, grad_sink=sink)  # (B*T, 1280)
+        if isinstance(self.backbone, ResNet50Trunk):
+            feats = self.backbone(x_flat)  # (B*T, 2048), inference only
+        else:
+            feats = self.backbone(x_flat, grad_sink=sink)  # (B*T, 1280)
         p = float(self.dropout.p) if self.training else 0.0
         seed = int(torch.randint(0, 2**62, (1,)).item()) if p > 0 else 0
         params = [dict(self._flat_params)[n] for n in self._head_names]
@@ -145,11 +162,11 @@ def _head_forward(det, feats, B, T, seed, p):
     lib = _lib.load()
     dev = feats.device
     params = [dict(det._flat_params)[n] for n in det._head_names]
-    work = torch.empty(int(lib.dfd_head_work_floats(B, T, FEATURE_DIM, ATTN_HIDDEN, FC1_DIM)),
+    work = torch.empty(int(lib.dfd_head_work_floats(B, T, det.feature_dim, ATTN_HIDDEN, FC1_DIM)),
                        dtype=torch.float32, device=dev)
     logits = torch.empty(B, det.num_classes, dtype=torch.float32, device=dev)
     scores = torch.empty(B, T, dtype=torch.float32, device=dev)
-    _lib.check(lib.dfd_head_forward(_lib.stream_of(dev), B, T, FEATURE_DIM, ATTN_HIDDEN, FC1_DIM, det.num_classes,
+    _lib.check(lib.dfd_head_forward(_lib.stream_of(dev), B, T, det.feature_dim, ATTN_HIDDEN, FC1_DIM, det.num_classes,
                                     1 if det.use_temporal_attention else 0, _head_ptrs(det, params),
                                     feats.data_ptr(), work.data_ptr(), seed, p, logits.data_ptr(),
                                     scores.data_ptr()))
@@ -181,7 +198,7 @@ class _HeadFn(torch.autograd.Function):
         dfeat = torch.empty_like(feats)
         params = [dict(det._flat_params)[n] for n in det._head_names]
         gviews = ctx.sink.views(det._head_names)
-        _lib.check(lib.dfd_head_backward(_lib.stream_of(dev), ctx.B, ctx.T, FEATURE_DIM, ATTN_HIDDEN, FC1_DIM,
+        _lib.check(lib.dfd_head_backward(_lib.stream_of(dev), ctx.B, ctx.T, det.feature_dim, ATTN_HIDDEN, FC1_DIM,
                                          det.num_classes, 1 if det.use_temporal_attention else 0,
                                          _head_ptrs(det, params), feats.data_ptr(), ctx.work.data_ptr(), ctx.seed,
                                          ctx.p, scores.data_ptr(), dlogits.data_ptr(), _lib.ptr(dscores),
@@ -192,8 +209,9 @@ class _HeadFn(torch.autograd.Function):
 
 
 class EnsembleDetector(nn.Module):
-    """``src/pretrained_detector.py:146-218`` restricted to efficientnet_b0 members (the members run on
-    the HIP path; the ensemble combination is a few ops on (M, B, C) logits)."""
+    """``src/pretrained_detector.py:146-218``: efficientnet_b0 and resnet50 members (the app's
+    default ``['efficientnet_b0', 'resnet50']``) run on the HIP path; the ensemble combination is a
+    few ops on (M, B, C) logits.  A resnet50 member is inference-only (``.eval()``)."""
 
     accepts_uint8_frames = True
 

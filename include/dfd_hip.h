@@ -140,6 +140,25 @@ DFD_API int dfd_ce_backward(void* stream, const float* logits, const int64_t* la
 DFD_API int dfd_collate_frames(void* stream, const uint8_t* src, const int64_t* sel, int64_t nsel,
                                int64_t frame_bytes, int out_f32, void* out);
 
+/* ---- ResNet-50 ensemble member, inference (src/pretrained_detector.py:37-40 -> torchvision
+ * resnet50 children[:-1]; EnsembleDetector default ENSEMBLE_BACKBONES, app.py:661,1597).  NHWC
+ * activations, dtype 0 = fp32, 1 = bf16.  Every convolution is dfd_rn_gemm over an im2col (or,
+ * for 1x1 stride 1, the activation itself) with the eval BatchNorm folded into weights + bias. ---- */
+/* NHWC x (N,H,W,C) -> rows [N*Ho*Wo][Kp], column (ky*kw + kx)*C + c, zero padding; C % 8 == 0 */
+DFD_API int dfd_rn_im2col(void* stream, int dtype, const void* x, int N, int H, int W, int C, int kh, int kw,
+                          int stride, int pad, int Kp, void* out);
+/* conv1 7x7/2 pad 3 rows of the (N,3,H,W) frames (element strides4; DFD_INPUT_F32 or DFD_INPUT_U8 with
+ * norm6 = mean[3], std[3]) -> [N*Ho*Wo][152] (147 taps + zero padding) */
+DFD_API int dfd_rn_stem_im2col(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
+                               const float* norm6, int N, int H, int W, void* out);
+/* C[M][N] = relu?(A[M][K] . B[N][K]^T + bias[N] (+ R[M][N])) through hipBLASLt, fp32 accumulate */
+DFD_API int dfd_rn_gemm(void* stream, int dtype, const void* A, const void* B, void* C, const void* R,
+                        const float* bias, int relu, int64_t M, int N, int K);
+/* 3x3/2 pad 1 max pooling, NHWC, C % 8 == 0 */
+DFD_API int dfd_rn_maxpool(void* stream, int dtype, const void* x, int N, int H, int W, int C, void* out);
+/* global average pooling (N, HW, C) -> (N, C) fp32 */
+DFD_API int dfd_rn_avgpool(void* stream, int dtype, const void* x, int N, int HW, int C, float* out);
+
 /* ---- optimizer ----------------------------------------------------------------------------
  * Replaces torch.nn.utils.clip_grad_norm_(params, max_norm) (src/ensemble_trainer.py:199) and
  * optim.AdamW / optim.Adam .step() (src/ensemble_trainer.py:146,200; src/train.py:323,126)
