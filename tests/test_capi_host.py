@@ -124,8 +124,8 @@ def test_pretrained_true_refuses_offline():
 
 
 def test_unknown_backbone_raises():
-    with pytest.raises(Exception):
-        PretrainedBackboneDetector("resnet50", pretrained=False)
+    with pytest.raises(ValueError):
+        PretrainedBackboneDetector("resnet18", pretrained=False)  # resnet50 is provided (inference)
 
 
 def test_forward_on_cpu_raises_no_fallback():
