@@ -21,13 +21,17 @@
 
 namespace dfd {
 
-template <typename T, int K, int TH, int TW, int RS>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1>
 struct Dw1 {
+  // FR > 1: the tile is FR whole frames (TH x TW = the map), stacked with their own halos -- fills
+  // the 16 strip slots on 7x7 maps
   static constexpr int PAD = K / 2;
-  static constexpr int GH = TH + K - 1, GW = TW + K - 1, NG = GH * GW;
+  static constexpr int GH1 = TH + K - 1, GW = TW + K - 1;
+  static constexpr int GH = FR * GH1, NG = GH * GW;
   static constexpr int NLD = (NG * 4 + 255) / 256;  // 8-channel vector loads per thread per tensor
   static constexpr int SPR = TW / RS;               // strips per tile row
-  static constexpr int NSTRIP = TH * SPR;
+  static constexpr int SPF = TH * SPR;              // strips per frame
+  static constexpr int NSTRIP = FR * SPF;
   static constexpr int RW = RS + K - 1;             // dY pairs per strip row
   static_assert(TW % RS == 0, "strips tile the row");
   static constexpr int NP = DCG / 2;                // channel pairs per pixel
@@ -36,7 +40,7 @@ struct Dw1 {
   static constexpr int DRS = (GW | 1) * NP;         // dys row stride (float2 pairs)
   static constexpr int RED = 4 * (K * K + 2) * DCG * 4;  // end-of-launch reduction scratch (bytes)
   static constexpr int DYB = GH * DRS * 8 > RED ? GH * DRS * 8 : RED;
-  static constexpr int LDS = DYB + K * K * DCG * 4 + 9 * DCG * 4;
+  static constexpr int LDS = DYB + K * K * DCG * 4 + 9 * DCG * 4 + FR * 2 * DCG * 4;
   static constexpr int OCC = (sizeof(T) == 2 && K == 3) ? 3 : 2;  // workgroups per CU (= the kernel's launch bounds)
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
@@ -80,13 +84,14 @@ __device__ __forceinline__ v2f lds2(const float* p) { return *reinterpret_cast<c
 __device__ __forceinline__ v2f sigmoid2(v2f z) { return v2f{sigmoidf_(z.x), sigmoidf_(z.y)}; }
 __device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
 
-template <typename T, int K, int TH, int TW, int RS>
+template <typename T, int K, int TH, int TW, int RS, int FR>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bwd1_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
     const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
     int ntiles, int groups, int tiles_x, int tiles_y) {
-  using D = Dw1<T, K, TH, TW, RS>;
+  using D = Dw1<T, K, TH, TW, RS, FR>;
   __shared__ __attribute__((aligned(16))) char dyraw[D::DYB];  // staged dY (fp32 pairs); reduction scratch
+  __shared__ __attribute__((aligned(16))) float gbl[FR][2][DCG];   // the tile frames' SE gate and bc
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
   __shared__ __attribute__((aligned(16))) float cst[9][DCG];       // sc2 sh2 k1 k2 k3 | sc1 sh1 mean1 invstd1
   float* dys = reinterpret_cast<float*>(dyraw);
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
   for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
-    const int f = t / tpf, r = t - f * tpf, ty = r / tiles_x;
+    const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;  // first frame of the tile
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
     // ---- staging loads: dZ, y2 + halo (this thread's 8 channels); frame base + 32-bit offsets ----
     Raw8<T> rz[D::NLD], r2[D::NLD];
@@ -142,30 +147,21 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
 #pragma unroll
       for (int i = 0; i < D::NLD; ++i) {
         const int pixl = (tid >> 2) + 64 * i;
-        const int oy = iy0 - D::PAD + pixl / D::GW, ox = ix0 - D::PAD + pixl % D::GW;
-        const bool in = pixl < D::NG && cok8 && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
-        const uint32_t o = in ? (uint32_t)((oy * g.W + ox) * C + c8) : 0u;
+        const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
+        const int oy = iy0 - D::PAD + pf / D::GW, ox = ix0 - D::PAD + pf % D::GW;
+        const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
+        const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
         raw_ld(rz[i], zf + o, zf, in);
         raw_ld(r2[i], yf + o, yf, in);
       }
     }
-    v2f gt[4], bcv[4];  // the frame's SE gate and squeeze-path gradient (tiny, L2-resident)
-    {
-      float a[8], b[8];
-      if (cok8) {
-        ld8f(b2.gate + (int64_t)f * C + c8, a);
-        ld8f(b2.bc + (int64_t)f * C + c8, b);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        gt[q] = v2f{a[2 * q], a[2 * q + 1]};
-        bcv[q] = v2f{b[2 * q], b[2 * q + 1]};
-      }
+    // the tile frames' SE gate and squeeze-path gradient (tiny, L2-resident) -> LDS
+    for (int i = tid; i < FR * 2 * DCG; i += 256) {
+      const int fi = i / (2 * DCG), w2 = (i / DCG) & 1, cl = i % DCG;
+      const bool ok = c0 + cl < C && f + fi < g.frames;
+      gbl[fi][w2][cl] = ok ? (w2 ? b2.bc : b2.gate)[(int64_t)(f + fi) * C + c0 + cl] : 0.f;
     }
-    lds_barrier();  // the previous tile's strips are done with dys
+    lds_barrier();  // the previous tile's strips are done with dys; gbl written
     // ---- commit: the fused BN2 backward into fp32 LDS (zero outside the map) ----
 #pragma unroll
     for (int i = 0; i < D::NLD; ++i) {
@@ -174,15 +170,17 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
       if (pixl < D::NG) {
         float* dst = dys + (pixl / D::GW) * D::DRS * 2 + (pixl % D::GW) * DCG + v8 * 8;
         if (rz[i].ok) {
+          const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0;
           float o[8];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int cq = v8 * 8 + 2 * q;
+            const v2f gtq = lds2(&gbl[fi][0][cq]), bcq = lds2(&gbl[fi][1][cq]);
             const v2f z = raw8_pair(rz[i], q), y = raw8_pair(r2[i], q);
             const v2f tz = fma2(y, lds2(&cst[0][cq]), lds2(&cst[1][cq]));
             const v2f sg = sigmoid2(tz);
             const v2f ds = sg * fma2(tz, 1.0f - sg, v2f{1.f, 1.f});
-            const v2f g2 = fma2(z, gt[q], bcv[q]) * ds;
+            const v2f g2 = fma2(z, gtq, bcq) * ds;
             const v2f v = round2(fma2(lds2(&cst[2][cq]), g2, fma2(lds2(&cst[3][cq]), y, lds2(&cst[4][cq]))),
                                  (T*)nullptr);
             o[2 * q] = v.x;
@@ -200,14 +198,15 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
     // ---- strips: data gradient + weight gradient from one read of each dY row ----
     const v2f sc1 = lds2(&cst[5][2 * cp]), sh1 = lds2(&cst[6][2 * cp]);
     const v2f is1 = lds2(&cst[8][2 * cp]), mi1 = -lds2(&cst[7][2 * cp]) * is1;  // xhat = y*is + mi
-    const T* y1f = Y1 + (int64_t)f * fstride;
-    T* outf = out + (int64_t)f * fstride;
 #pragma unroll 1
     for (int s = slot; s < D::NSTRIP; s += 16) {
-      const int pr = s % TH, xs = (s / TH) * RS;
+      const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
+      const int pr = sf % TH, xs = (sf / TH) * RS;
       const int iy = iy0 + pr;
+      const T* y1f = Y1 + (int64_t)(f + fi) * fstride;
+      T* outf = out + (int64_t)(f + fi) * fstride;
       const uint32_t so = (uint32_t)((iy * g.W + ix0 + xs) * C + ch);  // strip start within the frame
-      const bool rok = cokp && iy < g.H;
+      const bool rok = cokp && iy < g.H && f + fi < g.frames;
       Raw2<T> ry[RS];
 #pragma unroll
       for (int px = 0; px < RS; ++px) raw2_ld(ry[px], y1f + ((rok && ix0 + xs + px < g.W) ? so + px * C : 0u));
@@ -226,7 +225,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
 #pragma unroll
       for (int kh = 0; kh < K; ++kh) {
         asm volatile("" ::: "memory");  // one kernel row's LDS operands live at a time
-        const float* rowp = dys + (pr + K - 1 - kh) * D::DRS * 2 + xs * DCG + 2 * cp;
+        const float* rowp = dys + (fi * D::GH1 + pr + K - 1 - kh) * D::DRS * 2 + xs * DCG + 2 * cp;
         v2f dr[D::RW], wr[K];
 #pragma unroll
         for (int j = 0; j < D::RW; ++j) dr[j] = lds2(rowp + j * DCG);
@@ -301,16 +300,17 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1>
 static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const Dw1Bn2& b2, const float* w,
                        const T* Y1, const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab,
                        int64_t slab_cap, float* dW, bool accumulate) {
   const int tiles_x = cdiv(g.W, TW), tiles_y = cdiv(g.H, TH);
-  const int ntiles = g.frames * tiles_x * tiles_y;
+  if (FR > 1 && (tiles_x != 1 || tiles_y != 1)) { set_error("dw_bwd1: frame stacking needs whole-map tiles", __FILE__, __LINE__); return -1; }
+  const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
-  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS>;
-  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS>, 256>();
+  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS, FR>;
+  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS, FR>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
@@ -325,6 +325,7 @@ static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
 bool dw_bwd1_covers(const DwGeom& g) {
   if (g.s != 1 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2 || g.Ho != g.H || g.Wo != g.W) return false;
   if (!dw_bwd1_enabled()) return false;
+  if (g.H == 7 && g.W == 7) return true;  // two stacked frames per tile
   if (g.k == 3) return (g.H % 8 == 0 && g.W % 28 == 0) || (g.H % 14 == 0 && g.W % 14 == 0);
   return g.H % 14 == 0 && g.W % 14 == 0;
 }
@@ -340,6 +341,11 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
   if (g.C % 2) return 1;                                  // channel-pair accesses
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   const int H = g.H, W = g.W;
+  if (H == 7 && W == 7) {
+    if (g.k == 3)
+      return bwd1_launch<T, 3, 7, 7, 7, 2>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    return bwd1_launch<T, 5, 7, 7, 7, 2>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+  }
   if (g.k == 3) {
     if (H % 8 == 0 && W % 28 == 0)
       return bwd1_launch<T, 3, 8, 28, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
