@@ -41,6 +41,10 @@ int64_t set_dw_bwd1(int64_t v) { return g_dw_bwd1.exchange(v); }
 bool dw_bwd1_enabled() {
   return dw_bwd_fused_enabled() && tune_or(TK_DW_BWD1, g_dw_bwd1.load(std::memory_order_relaxed)) != 0;
 }
+// 1: the stride-1 forward takes dw_fwd1_kernel (k_dw_fwd1.hip, channel pairs)
+static std::atomic<int64_t> g_dw_fwd1{1};
+int64_t set_dw_fwd1(int64_t v) { return g_dw_fwd1.exchange(v); }
+bool dw_fwd1_enabled() { return tune_or(TK_DW_FWD1, g_dw_fwd1.load(std::memory_order_relaxed)) != 0; }
 
 template <int TH, int TW, int K, int S, int VW>
 struct DwB {

@@ -17,7 +17,7 @@
 //     (dW[row][tap] += act[p] * dY): the activations never go to LDS and no second pass re-reads dY;
 //   * the K*K x 2 weight-gradient accumulators stay in registers for the whole launch and are
 //     reduced once at the end (lanes, then waves, in a fixed order: bit-reproducible).
-#include "dw_common.h"
+#include "dw1_common.h"
 
 namespace dfd {
 
@@ -53,36 +53,7 @@ struct Dw1Bn2 {           // the fused BN2(+SiLU, SE gate) backward of the stagi
   const float* coef;      // [3][C]: k1, k2, k3 of bn_bwd_finalize_frames
 };
 
-typedef float v2f __attribute__((ext_vector_type(2)));
 
-// raw two-channel global load and its unpacking
-template <typename T> struct Raw2;
-template <> struct Raw2<bf16> { uint32_t v; };
-template <> struct Raw2<float> { float2 v; };
-__device__ __forceinline__ void raw2_ld(Raw2<bf16>& r, const bf16* p) { r.v = *reinterpret_cast<const uint32_t*>(p); }
-__device__ __forceinline__ void raw2_ld(Raw2<float>& r, const float* p) { r.v = *reinterpret_cast<const float2*>(p); }
-__device__ __forceinline__ v2f raw2_f(const Raw2<bf16>& r) {
-  return v2f{__uint_as_float(r.v << 16), __uint_as_float(r.v & 0xffff0000u)};
-}
-__device__ __forceinline__ v2f raw2_f(const Raw2<float>& r) { return v2f{r.v.x, r.v.y}; }
-// pairs of an 8-element raw vector
-__device__ __forceinline__ v2f raw8_pair(const Raw8<bf16>& r, int q) {
-  const uint32_t w = q == 0 ? r.a.x : q == 1 ? r.a.y : q == 2 ? r.a.z : r.a.w;
-  return v2f{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-}
-__device__ __forceinline__ v2f raw8_pair(const Raw8<float>& r, int q) {
-  return q == 0 ? v2f{r.a.x, r.a.y} : q == 1 ? v2f{r.a.z, r.a.w} : q == 2 ? v2f{r.b.x, r.b.y} : v2f{r.b.z, r.b.w};
-}
-__device__ __forceinline__ v2f round2(v2f v, bf16*) {
-  const uint32_t w = pack2bf(v.x, v.y);
-  return v2f{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
-}
-__device__ __forceinline__ v2f round2(v2f v, float*) { return v; }
-__device__ __forceinline__ void st2(bf16* p, v2f v) { *reinterpret_cast<uint32_t*>(p) = pack2bf(v.x, v.y); }
-__device__ __forceinline__ void st2(float* p, v2f v) { *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y); }
-__device__ __forceinline__ v2f lds2(const float* p) { return *reinterpret_cast<const v2f*>(p); }
-__device__ __forceinline__ v2f sigmoid2(v2f z) { return v2f{sigmoidf_(z.x), sigmoidf_(z.y)}; }
-__device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
 
 template <typename T, int K, int TH, int TW, int RS, int FR>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bwd1_kernel(

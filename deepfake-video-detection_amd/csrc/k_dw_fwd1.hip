@@ -1,0 +1,202 @@
+// Stride-1 depthwise-conv FORWARD in the channel-pair form of k_dw_bwd1.hip (timm conv_dw inside
+// the blocks run by self.backbone(x_flat), src/pretrained_detector.py:116), with the producer's
+// BN1 + SiLU applied while staging and the BN2 statistics of the output in the epilogue:
+//   staging  act[p] = silu(y1[p] * sc1 + sh1)   (fp32 LDS, zero outside the map; packed fp32 math,
+//            halo pixels outside the map skipped)
+//   strips   y2[o]  = sum_tap act[o - pad + tap] * w[tap] -> out (rounded to T),
+//            stats += [y2, y2^2]  (BN2 partial sums, fixed order)
+// Thread = (channel pair, strip of RS outputs of one row): per kernel row the strip's RS+K-1
+// activation pairs are read once (ds_read_b64) and feed RS*K packed FMAs.  Tiles as in the backward:
+// 8x28 (k3, 112/56 maps), 14x14 (28/14 maps), two stacked 7x7 frames.  Replaces the 8-channel
+// strip / tile kernels on these shapes (VALU-issue bound: fewer instructions per output).
+#include "dw1_common.h"
+
+namespace dfd {
+
+template <typename T, int K, int TH, int TW, int RS, int FR = 1>
+struct Dwf1 {
+  static constexpr int PAD = K / 2;
+  static constexpr int GH1 = TH + K - 1, GW = TW + K - 1;
+  static constexpr int GH = FR * GH1, NG = GH * GW;
+  static constexpr int NLD = (NG * 4 + 255) / 256;
+  static constexpr int SPR = TW / RS, SPF = TH * SPR, NSTRIP = FR * SPF;
+  static constexpr int RW = RS + K - 1;
+  static constexpr int NP = DCG / 2;
+  static constexpr int ARS = (GW | 1) * NP;  // act row stride (float2 pairs): odd pixel count (banks)
+  static constexpr int RED = 4 * 2 * DCG * 4;
+  static constexpr int AB = GH * ARS * 8 > RED ? GH * ARS * 8 : RED;
+  static constexpr int LDS = AB + K * K * DCG * 4 + 2 * DCG * 4;
+  static constexpr int OCC = sizeof(T) == 2 ? 3 : 2;
+  static_assert(TW % RS == 0, "strips tile the row");
+  static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
+};
+
+template <typename T, int K, int TH, int TW, int RS, int FR>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
+    DwGeom g, const T* __restrict__ Y1, const float* __restrict__ w, Pro bn1, T* __restrict__ out,
+    float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y) {
+  using D = Dwf1<T, K, TH, TW, RS, FR>;
+  __shared__ __attribute__((aligned(16))) char araw[D::AB];        // staged activations; reduction scratch
+  __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
+  __shared__ __attribute__((aligned(16))) float cst[2][DCG];       // BN1 scale, shift
+  float* acts = reinterpret_cast<float*>(araw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = blockIdx.x % groups;
+  const int c0 = grp * DCG, C = g.C;
+  for (int i = tid; i < K * K * DCG; i += 256) {
+    const int tap = i / DCG, cl = i - tap * DCG;
+    wts[i] = (c0 + cl < C) ? w[(int64_t)(c0 + cl) * K * K + tap] : 0.f;
+  }
+  for (int i = tid; i < 2 * DCG; i += 256) {
+    const int k = i / DCG, cl = i - k * DCG, c = c0 + cl;
+    cst[k][cl] = c < C ? (k ? bn1.shift[c] : bn1.scale[c]) : (k ? 0.f : 1.f);
+  }
+  const int tpf = tiles_x * tiles_y;
+  const int tstep = gridDim.x / groups;
+  const int fstride = g.H * g.W * C;
+  const int v8 = tid & 3, c8 = c0 + v8 * 8;
+  const bool cok8 = c8 < C;
+  const int cp = tid & 15, slot = tid >> 4;
+  const int ch = c0 + 2 * cp;
+  const bool cokp = ch < C;
+  v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
+
+  for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
+    const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;
+    const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
+    Raw8<T> ry[D::NLD];
+    {
+      const T* yf = Y1 + (int64_t)f * fstride;
+#pragma unroll
+      for (int i = 0; i < D::NLD; ++i) {
+        const int pixl = (tid >> 2) + 64 * i;
+        const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
+        const int oy = iy0 - D::PAD + pf / D::GW, ox = ix0 - D::PAD + pf % D::GW;
+        const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
+        const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
+        raw_ld(ry[i], yf + o, yf, in);
+      }
+    }
+    lds_barrier();  // the previous tile's strips are done with acts
+#pragma unroll
+    for (int i = 0; i < D::NLD; ++i) {
+      const int pixl = (tid >> 2) + 64 * i;
+      asm volatile("" ::: "memory");  // BN1 constants re-read per pixel (few live registers)
+      if (pixl < D::NG) {
+        float* dst = acts + (pixl / D::GW) * D::ARS * 2 + (pixl % D::GW) * DCG + v8 * 8;
+        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (ry[i].ok) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cq = v8 * 8 + 2 * q;
+            const v2f z = fma2(raw8_pair(ry[i], q), lds2(&cst[0][cq]), lds2(&cst[1][cq]));
+            const v2f a = z * sigmoid2(z);
+            o[2 * q] = a.x;
+            o[2 * q + 1] = a.y;
+          }
+        }
+        st8(dst, o);
+      }
+    }
+    lds_barrier();
+#pragma unroll 1
+    for (int s = slot; s < D::NSTRIP; s += 16) {
+      const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
+      const int pr = sf % TH, xs = (sf / TH) * RS;
+      const int iy = iy0 + pr;
+      T* outf = out + (int64_t)(f + fi) * fstride;
+      const uint32_t so = (uint32_t)((iy * g.W + ix0 + xs) * C + ch);
+      const bool rok = cokp && iy < g.H && f + fi < g.frames;
+      v2f acc[RS];
+#pragma unroll
+      for (int px = 0; px < RS; ++px) acc[px] = v2f{0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < K; ++kh) {
+        asm volatile("" ::: "memory");
+        const float* rowp = acts + (fi * D::GH1 + pr + kh) * D::ARS * 2 + xs * DCG + 2 * cp;
+        v2f ar[D::RW], wr[K];
+#pragma unroll
+        for (int j = 0; j < D::RW; ++j) ar[j] = lds2(rowp + j * DCG);
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw) wr[kw] = lds2(wts + (kh * K + kw) * DCG + 2 * cp);
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+          for (int px = 0; px < RS; ++px) acc[px] = fma2(ar[px + kw], wr[kw], acc[px]);
+#pragma unroll
+        for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc[px]));
+      }
+#pragma unroll
+      for (int px = 0; px < RS; ++px) {
+        if (rok && ix0 + xs + px < g.W) {
+          const v2f v = round2(acc[px], (T*)nullptr);
+          ss += v;
+          sq = fma2(v, v, sq);
+          st2(outf + (so + px * C), v);
+        }
+      }
+    }
+  }
+  // ---- BN2 partial sums: lanes sharing a channel pair, then the 4 waves, in a fixed order ----
+  lane_sum4(ss);
+  lane_sum4(sq);
+  lds_barrier();
+  float* red = reinterpret_cast<float*>(araw);  // [4 waves][2][32]
+  if (lane < 16) {
+    *reinterpret_cast<v2f*>(red + (wave * 2 + 0) * DCG + 2 * cp) = ss;
+    *reinterpret_cast<v2f*>(red + (wave * 2 + 1) * DCG + 2 * cp) = sq;
+  }
+  lds_barrier();
+  if (tid < 2 * DCG) {
+    const int which = tid / DCG, cl = tid - which * DCG;
+    const float v = ((red[(0 * 2 + which) * DCG + cl] + red[(1 * 2 + which) * DCG + cl]) +
+                     red[(2 * 2 + which) * DCG + cl]) + red[(3 * 2 + which) * DCG + cl];
+    const int64_t row = blockIdx.x / groups;
+    if (stats && c0 + cl < C) stats[(row * 2 + which) * C + c0 + cl] = v;
+  }
+}
+
+template <typename T, int K, int TH, int TW, int RS, int FR = 1>
+static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
+                       int* stat_rows) {
+  const int tiles_x = cdiv(g.W, TW), tiles_y = cdiv(g.H, TH);
+  if (FR > 1 && (tiles_x != 1 || tiles_y != 1)) { set_error("dw_fwd1: frame stacking needs whole-map tiles", __FILE__, __LINE__); return -1; }
+  const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
+  const int groups = cdiv(g.C, DCG);
+  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR>, 256>();
+  int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
+  rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
+  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
+                     pro, Y, stats, ntiles, groups, tiles_x, tiles_y);
+  DFD_HIP_CHECK(hipGetLastError());
+  if (stat_rows) *stat_rows = (int)rows;
+  return 0;
+}
+
+// 1: launched, 0: shape not covered, -1: error
+template <typename T>
+int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
+                int* stat_rows) {
+  if (g.s != 1 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2 || g.Ho != g.H || g.Wo != g.W) return 0;
+  if ((g.C & 1) || (int64_t)g.H * g.W * g.C >= (1ll << 31) || !dw_fwd1_enabled()) return 0;
+  const int H = g.H, W = g.W;
+  int rc;
+  if (H == 7 && W == 7)
+    rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+                  : fwd1_launch<T, 5, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+  else if (g.k == 3 && H % 8 == 0 && W % 28 == 0 && W >= 112)  // 56x56: the 8-channel strip kernel is 6% faster
+    rc = fwd1_launch<T, 3, 8, 28, 7>(s, g, X, w, Y, pro, stats, stat_rows);
+  else if (H % 14 == 0 && W % 14 == 0)
+    rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows)
+                  : fwd1_launch<T, 5, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows);
+  else
+    return 0;
+  return rc == 0 ? 1 : -1;
+}
+
+template int try_dw_fwd1<float>(hipStream_t, const DwGeom&, const float*, const float*, float*, const Pro&, float*,
+                                int*);
+template int try_dw_fwd1<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, float*,
+                               int*);
+
+}  // namespace dfd

@@ -26,7 +26,7 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
 // a plan's forward/backward installs its own Tuning for the enqueuing thread (TuningScope), so
 // concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- never read each other's knobs.
-enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_COUNT };
+enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -110,6 +110,12 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
 int64_t set_dw_bwd1(int64_t v);
 bool dw_bwd1_enabled();
 bool dw_bwd1_covers(const DwGeom& g);  // a tile configuration exists and the knob is on
+// k_dw_fwd1.hip: 1 launched, 0 not covered, -1 error
+template <typename T>
+int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
+                int* stat_rows);
+int64_t set_dw_fwd1(int64_t v);
+bool dw_fwd1_enabled();
 
 // ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------
 // finalize training stats: mean/invstd/scale/shift + running update (momentum); eval: from running
