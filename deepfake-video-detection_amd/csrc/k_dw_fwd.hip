@@ -168,7 +168,7 @@ int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T*
                   float* stats, int* stat_rows) {
   if (g.C & 7) { set_error("dw: C must be a multiple of 8", __FILE__, __LINE__); return -1; }
   if (pro_mode != PRO_BN_SILU) { set_error("dw fwd: input must be a BN+SiLU producer", __FILE__, __LINE__); return -1; }
-  if (g.s == 1) {
+  {
     const int rc = try_dw_fwd1<T>(s, g, X, w, Y, pro, stats, stat_rows);
     if (rc != 0) return rc > 0 ? 0 : -1;
   }

@@ -13,29 +13,33 @@
 
 namespace dfd {
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1>
 struct Dwf1 {
+  // TH x TW OUTPUT tile; the staged input window is ((TH-1)S+K) x ((TW-1)S+K) (+ FR stacked frames)
   static constexpr int PAD = K / 2;
-  static constexpr int GH1 = TH + K - 1, GW = TW + K - 1;
+  static constexpr int GH1 = (TH - 1) * S + K, GW = (TW - 1) * S + K;
   static constexpr int GH = FR * GH1, NG = GH * GW;
   static constexpr int NLD = (NG * 4 + 255) / 256;
   static constexpr int SPR = TW / RS, SPF = TH * SPR, NSTRIP = FR * SPF;
-  static constexpr int RW = RS + K - 1;
+  static constexpr int RW = (RS - 1) * S + K;
   static constexpr int NP = DCG / 2;
-  static constexpr int ARS = (GW | 1) * NP;  // act row stride (float2 pairs): odd pixel count (banks)
+  // act row stride (float2 pairs): the four strips of a wave read rows S apart; stride 1: an odd
+  // pixel count puts consecutive rows in opposite bank halves; stride 2: a half-pixel pad does so
+  // for rows two apart
+  static constexpr int ARS = S == 1 ? (GW | 1) * NP : GW * NP + NP / 2;
   static constexpr int RED = 4 * 2 * DCG * 4;
   static constexpr int AB = GH * ARS * 8 > RED ? GH * ARS * 8 : RED;
   static constexpr int LDS = AB + K * K * DCG * 4 + 2 * DCG * 4;
-  static constexpr int OCC = sizeof(T) == 2 ? 3 : 2;
+  static constexpr int OCC = (sizeof(T) == 2 && S == 1) ? 3 : 2;  // = the kernel's launch bounds
   static_assert(TW % RS == 0, "strips tile the row");
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
 
-template <typename T, int K, int TH, int TW, int RS, int FR>
-__global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
+template <typename T, int K, int TH, int TW, int RS, int FR, int S>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fwd1_kernel(
     DwGeom g, const T* __restrict__ Y1, const float* __restrict__ w, Pro bn1, T* __restrict__ out,
     float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y) {
-  using D = Dwf1<T, K, TH, TW, RS, FR>;
+  using D = Dwf1<T, K, TH, TW, RS, FR, S>;
   __shared__ __attribute__((aligned(16))) char araw[D::AB];        // staged activations; reduction scratch
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
   __shared__ __attribute__((aligned(16))) float cst[2][DCG];       // BN1 scale, shift
@@ -53,7 +57,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
   }
   const int tpf = tiles_x * tiles_y;
   const int tstep = gridDim.x / groups;
-  const int fstride = g.H * g.W * C;
+  const int fstride = g.H * g.W * C;          // input frame
+  const int ostride = g.Ho * g.Wo * C;        // output frame
   const int v8 = tid & 3, c8 = c0 + v8 * 8;
   const bool cok8 = c8 < C;
   const int cp = tid & 15, slot = tid >> 4;
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
       for (int i = 0; i < D::NLD; ++i) {
         const int pixl = (tid >> 2) + 64 * i;
         const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
-        const int oy = iy0 - D::PAD + pf / D::GW, ox = ix0 - D::PAD + pf % D::GW;
+        const int oy = iy0 * S - D::PAD + pf / D::GW, ox = ix0 * S - D::PAD + pf % D::GW;
         const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
         const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
         raw_ld(ry[i], yf + o, yf, in);
@@ -103,17 +108,17 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
     for (int s = slot; s < D::NSTRIP; s += 16) {
       const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
       const int pr = sf % TH, xs = (sf / TH) * RS;
-      const int iy = iy0 + pr;
-      T* outf = out + (int64_t)(f + fi) * fstride;
-      const uint32_t so = (uint32_t)((iy * g.W + ix0 + xs) * C + ch);
-      const bool rok = cokp && iy < g.H && f + fi < g.frames;
+      const int iy = iy0 + pr;  // output row
+      T* outf = out + (int64_t)(f + fi) * ostride;
+      const uint32_t so = (uint32_t)((iy * g.Wo + ix0 + xs) * C + ch);
+      const bool rok = cokp && iy < g.Ho && f + fi < g.frames;
       v2f acc[RS];
 #pragma unroll
       for (int px = 0; px < RS; ++px) acc[px] = v2f{0.f, 0.f};
 #pragma unroll
       for (int kh = 0; kh < K; ++kh) {
         asm volatile("" ::: "memory");
-        const float* rowp = acts + (fi * D::GH1 + pr + kh) * D::ARS * 2 + xs * DCG + 2 * cp;
+        const float* rowp = acts + (fi * D::GH1 + pr * S + kh) * D::ARS * 2 + xs * S * DCG + 2 * cp;
         v2f ar[D::RW], wr[K];
 #pragma unroll
         for (int j = 0; j < D::RW; ++j) ar[j] = lds2(rowp + j * DCG);
@@ -122,13 +127,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
 #pragma unroll
         for (int kw = 0; kw < K; ++kw)
 #pragma unroll
-          for (int px = 0; px < RS; ++px) acc[px] = fma2(ar[px + kw], wr[kw], acc[px]);
+          for (int px = 0; px < RS; ++px) acc[px] = fma2(ar[px * S + kw], wr[kw], acc[px]);
 #pragma unroll
         for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc[px]));
       }
 #pragma unroll
       for (int px = 0; px < RS; ++px) {
-        if (rok && ix0 + xs + px < g.W) {
+        if (rok && ix0 + xs + px < g.Wo) {
           const v2f v = round2(acc[px], (T*)nullptr);
           ss += v;
           sq = fma2(v, v, sq);
@@ -156,17 +161,17 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 3 : 2) void dw_fwd1_kernel(
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1>
 static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                        int* stat_rows) {
-  const int tiles_x = cdiv(g.W, TW), tiles_y = cdiv(g.H, TH);
+  const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
   if (FR > 1 && (tiles_x != 1 || tiles_y != 1)) { set_error("dw_fwd1: frame stacking needs whole-map tiles", __FILE__, __LINE__); return -1; }
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
-  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR>, 256>();
+  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR, S>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
-  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
+  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
                      pro, Y, stats, ntiles, groups, tiles_x, tiles_y);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
@@ -177,20 +182,34 @@ static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* 
 template <typename T>
 int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                 int* stat_rows) {
-  if (g.s != 1 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2 || g.Ho != g.H || g.Wo != g.W) return 0;
+  if ((g.k != 3 && g.k != 5) || g.pad != g.k / 2 || (g.s != 1 && g.s != 2)) return 0;
+  if (g.Ho != (g.H + 2 * g.pad - g.k) / g.s + 1 || g.Wo != (g.W + 2 * g.pad - g.k) / g.s + 1) return 0;
   if ((g.C & 1) || (int64_t)g.H * g.W * g.C >= (1ll << 31) || !dw_fwd1_enabled()) return 0;
-  const int H = g.H, W = g.W;
+  const int H = g.Ho, W = g.Wo;  // output map
   int rc;
-  if (H == 7 && W == 7)
+  if (g.s == 2) {
+    // k3 stride 2 (112->56, 28->14): the 8x8 tile kernel is as fast or faster (kbench: 214 vs 246,
+    // 42 vs 42 us); k5: 153 -> 126 and 43 -> 35 us
+    if (g.k == 3) return 0;
+    if (H == 7 && W == 7)
+      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+                    : fwd1_launch<T, 5, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+    else if (H % 7 == 0 && W % 14 == 0)
+      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+                    : fwd1_launch<T, 5, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+    else
+      return 0;
+  } else if (H == 7 && W == 7) {
     rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows)
                   : fwd1_launch<T, 5, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows);
-  else if (g.k == 3 && H % 8 == 0 && W % 28 == 0 && W >= 112)  // 56x56: the 8-channel strip kernel is 6% faster
+  } else if (g.k == 3 && H % 8 == 0 && W % 28 == 0 && W >= 112) {  // 56x56: the 8-channel strip kernel is 6% faster
     rc = fwd1_launch<T, 3, 8, 28, 7>(s, g, X, w, Y, pro, stats, stat_rows);
-  else if (H % 14 == 0 && W % 14 == 0)
+  } else if (H % 14 == 0 && W % 14 == 0) {
     rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows)
                   : fwd1_launch<T, 5, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows);
-  else
+  } else {
     return 0;
+  }
   return rc == 0 ? 1 : -1;
 }
 
