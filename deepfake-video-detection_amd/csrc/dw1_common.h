@@ -8,6 +8,14 @@ namespace dfd {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+struct Dw1Bn2 {           // the fused BN2(+SiLU, SE gate) backward of the staging
+  const float* gate;      // [frames][C]
+  const float* bc;        // [frames][C]
+  const float* sc;        // BN2 scale (gamma*invstd), shift
+  const float* sh;
+  const float* coef;      // [3][C]: k1, k2, k3 of bn_bwd_finalize_frames
+};
+
 // raw two-channel global load and its unpacking
 template <typename T> struct Raw2;
 template <> struct Raw2<bf16> { uint32_t v; };

@@ -45,16 +45,6 @@ struct Dw1 {
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
 
-struct Dw1Bn2 {           // the fused BN2(+SiLU, SE gate) backward of the staging
-  const float* gate;      // [frames][C]
-  const float* bc;        // [frames][C]
-  const float* sc;        // BN2 scale (gamma*invstd), shift
-  const float* sh;
-  const float* coef;      // [3][C]: k1, k2, k3 of bn_bwd_finalize_frames
-};
-
-
-
 template <typename T, int K, int TH, int TW, int RS, int FR>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bwd1_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,

@@ -110,6 +110,13 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
 int64_t set_dw_bwd1(int64_t v);
 bool dw_bwd1_enabled();
 bool dw_bwd1_covers(const DwGeom& g);  // a tile configuration exists and the knob is on
+// the stride-2 counterpart, k_dw_bwd2.hip (same contract; rides the dw_bwd1 knob)
+template <typename T>
+int launch_dw_bwd2(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const float* gate, const float* bc,
+                   const float* sc2, const float* sh2, const float* coef2, const float* w, const T* Y1,
+                   const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
+                   bool accumulate);
+bool dw_bwd2_covers(const DwGeom& g);
 // k_dw_fwd1.hip: 1 launched, 0 not covered, -1 error
 template <typename T>
 int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,

@@ -484,7 +484,13 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         int fused = 1;
         // stride 1: one kernel also applies the BN2(+SiLU, gate) backward while staging dY
         // (k_dw_bwd1.hip); otherwise the apply pass materialises dY first
-        if (dw_bwd1_covers(g)) {
+        if (dw_bwd2_covers(g)) {  // stride 2 (k_dw_bwd2.hip)
+          PROBED(PK_DW_DGRAD, &b, (launch_dw_bwd2<T>(s, g, r.a(p.o_ge2), r.a(b.o_y2), r.f(b.o_gate), r.f(p.o_bc),
+                                                     r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(p.o_coef),
+                                                     r.prm(b.t_dw), y_in, fz, r.a(p.o_ge1), r.f(p.o_stats), &rows,
+                                                     slab(), p.slab_cap, grad(b.t_dw), acc != 0)));
+          fused = 0;
+        } else if (dw_bwd1_covers(g)) {
           PROBED(PK_DW_DGRAD, &b, (launch_dw_bwd1<T>(s, g, r.a(p.o_ge2), r.a(b.o_y2), r.f(b.o_gate), r.f(p.o_bc),
                                                      r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(p.o_coef),
                                                      r.prm(b.t_dw), y_in, fz, r.a(p.o_ge1), r.f(p.o_stats), &rows,
