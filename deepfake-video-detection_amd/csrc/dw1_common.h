@@ -26,6 +26,10 @@ __device__ __forceinline__ v2f raw2_f(const Raw2<bf16>& r) {
   return v2f{__uint_as_float(r.v << 16), __uint_as_float(r.v & 0xffff0000u)};
 }
 __device__ __forceinline__ v2f raw2_f(const Raw2<float>& r) { return v2f{r.v.x, r.v.y}; }
+// "redefine" a raw pair at this point: values derived from it cannot be hoisted above (keeps the
+// 1-VGPR bf16 pair live instead of its 2-VGPR fp32 expansion across a long loop)
+__device__ __forceinline__ void pin2(Raw2<bf16>& r) { asm volatile("" : "+v"(r.v)); }
+__device__ __forceinline__ void pin2(Raw2<float>& r) { asm volatile("" : "+v"(r.v.x), "+v"(r.v.y)); }
 // pairs of an 8-element raw vector
 __device__ __forceinline__ v2f raw8_pair(const Raw8<bf16>& r, int q) {
   const uint32_t w = q == 0 ? r.a.x : q == 1 ? r.a.y : q == 2 ? r.a.z : r.a.w;
@@ -41,6 +45,14 @@ __device__ __forceinline__ v2f round2(v2f v, bf16*) {
 __device__ __forceinline__ v2f round2(v2f v, float*) { return v; }
 __device__ __forceinline__ void st2(bf16* p, v2f v) { *reinterpret_cast<uint32_t*>(p) = pack2bf(v.x, v.y); }
 __device__ __forceinline__ void st2(float* p, v2f v) { *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y); }
+// base + a 32-bit BYTE offset: the uniform frame base stays in SGPRs and each access is one
+// global_load/store with a 32-bit VGPR offset (no per-lane 64-bit address arithmetic)
+template <typename T> __device__ __forceinline__ const T* boff(const T* base, uint32_t off) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
+}
+template <typename T> __device__ __forceinline__ T* boff(T* base, uint32_t off) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+}
 __device__ __forceinline__ v2f lds2(const float* p) { return *reinterpret_cast<const v2f*>(p); }
 __device__ __forceinline__ v2f sigmoid2(v2f z) { return v2f{sigmoidf_(z.x), sigmoidf_(z.y)}; }
 __device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }

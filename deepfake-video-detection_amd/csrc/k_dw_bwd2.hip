@@ -143,19 +143,19 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
       const int par = (wave & 1) ^ it;
       const int pr = 2 * (slot & 3) + par;
       const int xs = ((wave >> 1) + 2 * it) * RS;
-      const int iy = iy0 + pr;
-      const uint32_t so = (uint32_t)((iy * g.W + ix0 + xs) * C + ch);
-      const bool rok = cokp && iy < g.H;
+      // tiles never cross the map (covers(): H % 8, W % 56): only the channel bound masks anything.
+      // Lanes past C read pixel 0 of the frame (pixel stride 0) and skip the epilogue
+      const uint32_t pb = cokp ? (uint32_t)(C * sizeof(T)) : 0u;
+      const uint32_t sb = cokp ? (uint32_t)((((iy0 + pr) * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
       Raw2<T> ry[RS];
 #pragma unroll
-      for (int px = 0; px < RS; ++px) raw2_ld(ry[px], y1f + ((rok && ix0 + xs + px < g.W) ? so + px * C : 0u));
+      for (int px = 0; px < RS; ++px) raw2_ld(ry[px], boff(y1f, sb + px * pb));
       v2f act[RS], sg[RS];
 #pragma unroll
       for (int px = 0; px < RS; ++px) {
-        const bool ok = rok && ix0 + xs + px < g.W;
         const v2f z = fma2(raw2_f(ry[px]), sc1, sh1);
         sg[px] = sigmoid2(z);
-        act[px] = ok ? z * sg[px] : v2f{0.f, 0.f};
+        act[px] = z * sg[px];
       }
       v2f acc[RS];
 #pragma unroll
@@ -189,14 +189,15 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
         }
       }
 #pragma unroll
-      for (int px = 0; px < RS; ++px) {
-        const bool ok = rok && ix0 + xs + px < g.W;
-        const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
-        const v2f gg = round2(acc[px] * dsl, (T*)nullptr);
-        if (ok) {
+      for (int px = 0; px < RS; ++px) pin2(ry[px]);
+      if (cokp) {
+#pragma unroll
+        for (int px = 0; px < RS; ++px) {
+          const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
+          const v2f gg = round2(acc[px] * dsl, (T*)nullptr);
           ss += gg;
           sq = fma2(gg, fma2(raw2_f(ry[px]), is1, mi1), sq);
-          st2(outf + (so + px * C), gg);
+          st2(boff(outf, sb + px * pb), gg);
         }
       }
     }
@@ -255,7 +256,8 @@ static int bwd2_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
 bool dw_bwd2_covers(const DwGeom& g) {
   if (g.s != 2 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2) return false;
   if (g.Ho != (g.H + 2 * g.pad - g.k) / 2 + 1 || g.Wo != (g.W + 2 * g.pad - g.k) / 2 + 1) return false;
-  if (g.H % 8 || g.W % 56 || (g.C & 1) || (int64_t)g.H * g.W * g.C >= (1ll << 31)) return false;
+  // exact tiling; 32-bit byte offsets within a frame (fp32 bound, for both dtypes)
+  if (g.H % 8 || g.W % 56 || (g.C & 1) || (int64_t)g.H * g.W * g.C * 4 >= (1ll << 32)) return false;
   return dw_bwd1_enabled();
 }
 

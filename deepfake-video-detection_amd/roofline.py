@@ -5,8 +5,10 @@ output, weights once; BN/SiLU/SE applied in the consumers' prologues so they add
 
 * depthwise fwd:   es*(N*Hin*Win*C + N*Ho*Wo*C) + 4*k*k*C          (dgrad: same tensors swapped)
 * depthwise wgrad: es*(N*Ho*Wo*C + N*Hin*Win*C) + 4*k*k*C
-* fused depthwise backward (dgrad + producer BN/SiLU backward + wgrad in one pass):
-                   es*(2*N*Hin*Win*C + N*Ho*Wo*C) + 8*k*k*C
+* fused depthwise backward (dgrad + wgrad + the BN2/SiLU/SE backward of its output in the staging +
+  the producer's BN1/SiLU backward in the epilogue, k_dw_bwd1.hip / k_dw_bwd2.hip): reads dZ and y2
+  (out map) and y1 (in map), writes dX (in map):
+                   es*(2*N*Hin*Win*C + 2*N*Ho*Wo*C) + 8*k*k*C
 * 1x1 fwd/dgrad:   es*(M*K + M*N) + es*N*K,  flops 2*M*N*K
 * 1x1 wgrad:       es*(M*N + M*K) + 4*N*K
 * SE squeeze:      es*M*C
@@ -55,8 +57,8 @@ def algorithmic(kind: str, stage: int, idx: int, frames: int, H: int, W: int, es
     g = block_geometry(H, W)[(stage, idx)]
     Mi, Mo = frames * g["hin"] * g["win"], frames * g["hout"] * g["wout"]
     C, k = g["mid"], g["k"]
-    if kind == "dw_bwd":  # reads dY (out map) and the producer's y (in map), writes dX (in map); dW fp32
-        return es * (2 * Mi * C + Mo * C) + 8 * k * k * C, 4 * Mo * C * k * k
+    if kind == "dw_bwd":  # reads dZ, y2 (out map) and the producer's y1 (in map), writes dX (in map); dW fp32
+        return es * (2 * Mi * C + 2 * Mo * C) + 8 * k * k * C, 4 * Mo * C * k * k
     if kind in ("dw_fwd", "dw_dgrad", "dw_wgrad"):
         return es * (Mi * C + Mo * C) + 4 * k * k * C, 2 * Mo * C * k * k
     if kind == "se_squeeze":

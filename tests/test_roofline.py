@@ -39,3 +39,11 @@ def test_probe_kernel_bytes():
     by, fl = R.algorithmic("dw_fwd", 1, 0, 256, 224, 224, 2)
     assert by == 2 * (256 * 112 * 112 * 96 + 256 * 56 * 56 * 96) + 4 * 9 * 96
     assert fl == 2 * 256 * 56 * 56 * 96 * 9
+
+
+def test_probe_fused_dw_bwd_bytes():
+    # bench.py probes the fused depthwise backward of blocks.1.0 (k_dw_bwd2.hip): dZ + y2 at 56x56x96,
+    # y1 read + dX written at 112x112x96 (bf16), dW fp32 read/written once
+    by, fl = R.algorithmic("dw_bwd", 1, 0, 256, 224, 224, 2)
+    assert by == 2 * (2 * 256 * 112 * 112 * 96 + 2 * 256 * 56 * 56 * 96) + 8 * 9 * 96
+    assert fl == 4 * 256 * 56 * 56 * 96 * 9

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC traffic of the bench's probed launch (dw_bwd<bf16,16,16,3,2> of blocks.1.0, the largest
+# PMC traffic of the bench's probed launch (dw_bwd2<bf16,3,8,56,14> of blocks.1.0, the largest
 # kernel of the step) and the FETCH_SIZE / WRITE_SIZE calibration it is corrected with
 # (tools/fetch_calib: known byte counts in the same 64-B channel-slice access pattern).
 # One counter per pass, kernel trace only (MI355X_MICROARCH.md: never with sys/runtime traces).
@@ -17,8 +17,8 @@ for m in 3 4; do
     > $OUT/calib_$m.log 2>&1 || { echo "CALIB $m FAILED"; exit 1; }
 done
 echo CALIB ok
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "dw_bwd_kernel" --output-format csv \
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "dw_bwd2_kernel" --output-format csv \
   -d $OUT/fetch -o run -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/fetch.log 2>&1 || { echo FETCH FAILED; exit 1; }
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "dw_bwd_kernel" --output-format csv \
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "dw_bwd2_kernel" --output-format csv \
   -d $OUT/write -o run -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/write.log 2>&1 || { echo WRITE FAILED; exit 1; }
 echo PMC ok

@@ -8,8 +8,9 @@ read or written once per dispatch; the tensor exceeds the 256 MiB Infinity Cache
   mode 2  64-B channel slices,  8 B/lane -> FETCH_SIZE = 1.0 x bytes
   mode 3/4  slice / contiguous writes    -> WRITE_SIZE = 1.0 x bytes
 
-The probed launch (dw_bwd<bf16,16,16,3,2> of blocks.1.0, C = 96) reads 64-B slices of 32
-channels (one channel group per workgroup, pixels 192 B apart), i.e. the mode-1 pattern, so its
+The probed launch (dw_bwd2<bf16,3,8,56,14> of blocks.1.0, C = 96, k_dw_bwd2.hip) reads 64-B slices
+of 32 channels (one channel group per workgroup, pixels 192 B apart: 16 B/lane staging loads of dZ
+and y2, 4 B/lane strip loads of y1), i.e. the mode-1/2 pattern (factor 1.0 for both), so its
 FETCH_SIZE is divided by the mode-1 factor.  (Layers with C = 32 -- blocks.0.0 -- read adjacent
 64-B slices that merge into 128-B requests and count like mode 0: that is the round-1
 "279 MB fetched vs 411 MB algorithmic" reading of dw_bwd<16,16,3,1>.)
@@ -23,7 +24,7 @@ import os
 import statistics
 import sys
 
-PROBE = ("dw_bwd:1.0", "dw_bwd_kernel<dfd::bf16, 16, 16, 3, 2, 8", 1)  # key, kernel name, calibration mode
+PROBE = ("dw_bwd:1.0", "dw_bwd2_kernel<dfd::bf16, 3, 8, 56, 14>", 1)  # key, kernel name, calibration mode
 KNOWN = 256 * 112 * 112 * 96 * 2
 
 
@@ -57,7 +58,7 @@ def main():
     wr = values(os.path.join(d, "write"), "WRITE_SIZE", name)
     fetch = statistics.median(fe) / calib["fetch_slice64_16B"]
     write = statistics.median(wr) / calib["write_slice64"]
-    alg = 2 * (2 * 256 * 112 * 112 * 96 + 256 * 56 * 56 * 96) + 8 * 9 * 96
+    alg = 2 * (2 * 256 * 112 * 112 * 96 + 2 * 256 * 56 * 56 * 96) + 8 * 9 * 96
     ent = {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
            "fetch_size_raw_bytes": statistics.median(fe), "write_size_raw_bytes": statistics.median(wr),
            "calibration": {k: round(v, 4) for k, v in calib.items()},
