@@ -164,21 +164,24 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
       const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
       const int pr = sf % TH, xs = (sf / TH) * RS;
       const int iy = iy0 + pr;
-      const T* y1f = Y1 + (int64_t)(f + fi) * fstride;
-      T* outf = out + (int64_t)(f + fi) * fstride;
-      const uint32_t so = (uint32_t)((iy * g.W + ix0 + xs) * C + ch);  // strip start within the frame
-      const bool rok = cokp && iy < g.H && f + fi < g.frames;
+      // tiles never cross the map (dw_bwd1_covers: exact tilings), so only the channel bound and,
+      // with stacked frames, a missing last frame mask anything: such lanes read pixel 0 of frame f
+      // (pixel stride 0; their zero dY gives zero dW terms) and skip the epilogue
+      const bool rok = cokp && f + fi < g.frames;
+      const T* y1f = Y1 + (int64_t)f * fstride;
+      T* outf = out + (int64_t)f * fstride;
+      const uint32_t pb = rok ? (uint32_t)(C * sizeof(T)) : 0u;
+      const uint32_t sb = rok ? (uint32_t)((fi * fstride + (iy * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
       Raw2<T> ry[RS];
 #pragma unroll
-      for (int px = 0; px < RS; ++px) raw2_ld(ry[px], y1f + ((rok && ix0 + xs + px < g.W) ? so + px * C : 0u));
+      for (int px = 0; px < RS; ++px) raw2_ld(ry[px], boff(y1f, sb + px * pb));
       // activations (weight-gradient operand) and sigmoids (for silu') of the strip
       v2f act[RS], sg[RS];
 #pragma unroll
       for (int px = 0; px < RS; ++px) {
-        const bool ok = rok && ix0 + xs + px < g.W;
         const v2f z = fma2(raw2_f(ry[px]), sc1, sh1);
         sg[px] = sigmoid2(z);
-        act[px] = ok ? z * sg[px] : v2f{0.f, 0.f};
+        act[px] = z * sg[px];
       }
       v2f acc[RS];
 #pragma unroll
@@ -208,15 +211,16 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
       }
       // ---- epilogue: g1 = dA * silu'(z1) -> out, BN1 backward sums ----
 #pragma unroll
-      for (int px = 0; px < RS; ++px) {
-        const bool ok = rok && ix0 + xs + px < g.W;
-        // silu'(z) = s (1 + z (1 - s)) = s + act (1 - s)
-        const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
-        const v2f gg = round2(acc[px] * dsl, (T*)nullptr);
-        if (ok) {
+      for (int px = 0; px < RS; ++px) pin2(ry[px]);
+      if (rok) {
+#pragma unroll
+        for (int px = 0; px < RS; ++px) {
+          // silu'(z) = s (1 + z (1 - s)) = s + act (1 - s)
+          const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
+          const v2f gg = round2(acc[px] * dsl, (T*)nullptr);
           ss += gg;
           sq = fma2(gg, fma2(raw2_f(ry[px]), is1, mi1), sq);
-          st2(outf + (so + px * C), gg);
+          st2(boff(outf, sb + px * pb), gg);
         }
       }
     }
@@ -298,7 +302,8 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
                    const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
                    bool accumulate) {
   if (!dw_bwd1_covers(g)) return 1;
-  if ((int64_t)g.H * g.W * g.C >= (1ll << 31)) return 1;  // 32-bit in-frame offsets
+  // 32-bit byte offsets within the tile's frames (FR <= 2; fp32 bound for both dtypes)
+  if ((int64_t)g.H * g.W * g.C * 8 >= (1ll << 32)) return 1;
   if (g.C % 2) return 1;                                  // channel-pair accesses
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   const int H = g.H, W = g.W;

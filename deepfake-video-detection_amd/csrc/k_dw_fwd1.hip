@@ -109,9 +109,11 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
       const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
       const int pr = sf % TH, xs = (sf / TH) * RS;
       const int iy = iy0 + pr;  // output row
-      T* outf = out + (int64_t)(f + fi) * ostride;
-      const uint32_t so = (uint32_t)((iy * g.Wo + ix0 + xs) * C + ch);
-      const bool rok = cokp && iy < g.Ho && f + fi < g.frames;
+      // output tiles never cross the map (try_dw_fwd1: exact tilings): only the channel bound and a
+      // missing last stacked frame mask the epilogue; frame base + 32-bit byte offsets
+      T* outf = out + (int64_t)f * ostride;
+      const uint32_t sb = (uint32_t)((fi * ostride + (iy * g.Wo + ix0 + xs) * C + ch) * sizeof(T));
+      const bool rok = cokp && f + fi < g.frames;
       v2f acc[RS];
 #pragma unroll
       for (int px = 0; px < RS; ++px) acc[px] = v2f{0.f, 0.f};
@@ -131,13 +133,13 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
 #pragma unroll
         for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc[px]));
       }
+      if (rok) {
 #pragma unroll
-      for (int px = 0; px < RS; ++px) {
-        if (rok && ix0 + xs + px < g.Wo) {
+        for (int px = 0; px < RS; ++px) {
           const v2f v = round2(acc[px], (T*)nullptr);
           ss += v;
           sq = fma2(v, v, sq);
-          st2(outf + (so + px * C), v);
+          st2(boff(outf, sb + px * (uint32_t)(C * sizeof(T))), v);
         }
       }
     }
@@ -184,7 +186,10 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
                 int* stat_rows) {
   if ((g.k != 3 && g.k != 5) || g.pad != g.k / 2 || (g.s != 1 && g.s != 2)) return 0;
   if (g.Ho != (g.H + 2 * g.pad - g.k) / g.s + 1 || g.Wo != (g.W + 2 * g.pad - g.k) / g.s + 1) return 0;
-  if ((g.C & 1) || (int64_t)g.H * g.W * g.C >= (1ll << 31) || !dw_fwd1_enabled()) return 0;
+  // 32-bit element offsets into the input frames; 32-bit byte offsets within two output frames
+  if ((g.C & 1) || (int64_t)g.H * g.W * g.C >= (1ll << 31) || (int64_t)g.Ho * g.Wo * g.C * 8 >= (1ll << 32) ||
+      !dw_fwd1_enabled())
+    return 0;
   const int H = g.Ho, W = g.Wo;  // output map
   int rc;
   if (g.s == 2) {
