@@ -5,41 +5,54 @@
 //              dA[p]       += dY[o] * w[tap]
 //              dW[kh][kw]  += act[p] * dY[o],      act = silu(y1*sc1 + sh1)
 //            g1[p] = dA * silu'(y1*sc1 + sh1) -> out,  stats += [g1, g1*xhat1]
-// Tile = 8 x 56 INPUT pixels x 32 channels; its dY window (4+2) x (28+2) is staged once (fp32).
-// Thread = (channel pair, two strips of 14 input pixels, one per pass).  Which taps meet a pixel
-// depends on its parity: the column parity is static (strips start at even x); the row parity is
-// uniform per wave and per pass, and flips between the two passes, so every wave does the same
-// number of kernel rows (even rows meet ceil(K/2) of them, odd rows floor(K/2)) and nothing
-// diverges.  Replaces the BN2 apply pass + dw_bwd_kernel on these layers (blocks.1.0: 112->56 k3,
-// blocks.2.0: 56->28 k5).
+// Tile = TH x TW INPUT pixels (x FR stacked frames) x 32 channels; its dY window
+// (TH/2+2) x (TW/2+2) per frame is staged once (fp32).  Thread = (channel pair, strip of RS input
+// pixels of one row).  Which taps meet a pixel depends on its parity: the column parity is static
+// (strips start at even x) and the row parity is uniform per wave:
+//   * 8 x 56 tiles (blocks.1.0 112->56 k3, blocks.2.0 56->28 k5): two passes of the 16 slots, the
+//     row parity flips between them, so every wave runs the same number of kernel rows (even rows
+//     meet ceil(K/2) of them, odd rows floor(K/2));
+//   * whole-frame tiles (blocks.3.0 28->14 k3; blocks.5.0 14->7 k5 with 4 stacked frames): strips
+//     numbered parity-major (all even-row strips, then the odd ones; 4 | #even strips), so every
+//     pass but the one at the boundary has a single parity.
+// Replaces the BN2 apply pass + dw_bwd_kernel on these layers.
 #include "dw1_common.h"
 
 namespace dfd {
 
-template <typename T, int K, int TH, int TW, int RS>
+template <typename T, int K, int TH, int TW, int RS, int FR>
 struct Dw2 {
   static constexpr int PAD = K / 2;
-  static constexpr int GH = TH / 2 + 2, GW = TW / 2 + 2, NG = GH * GW;  // staged dY window (output res)
+  static constexpr int GH1 = TH / 2 + 2, GW = TW / 2 + 2;  // staged dY window per frame (output res)
+  static constexpr int NG1 = GH1 * GW, GH = FR * GH1, NG = FR * NG1;
   static constexpr int NLD = (NG * 4 + 255) / 256;
-  static constexpr int SPR = TW / RS, NSTRIP = TH * SPR;  // 32: two passes of the 16 strip slots
+  static constexpr int CH = NLD < 3 ? NLD : 3;      // staging loads in flight per tensor
+  static constexpr int SPR = TW / RS;
+  static constexpr int HE = TH / 2;                 // even (= odd) input rows per frame
+  static constexpr int NE = FR * HE * SPR;          // even-row strips; the odd ones follow
+  static constexpr int NSTRIP = 2 * NE;
+  static constexpr bool BAL = FR == 1 && TH == 8 && SPR == 4;  // the two-pass balanced map
+  static constexpr int NPASS = BAL ? 2 : (NSTRIP + 15) / 16;
   static constexpr int RWO = RS / 2 + 2;  // staged dY columns a strip touches
   static constexpr int NP = DCG / 2;
   static constexpr int DRS = (GW | 1) * NP;  // pairs per staged row: odd pixel count (banks)
   static constexpr int RED = 4 * (K * K + 2) * DCG * 4;
   static constexpr int DYB = GH * DRS * 8 > RED ? GH * DRS * 8 : RED;
-  static_assert(TH == 8 && TW == 4 * RS && RS % 2 == 0, "the strip map below: 4 rows per parity, 4 strip columns");
+  static_assert(TH % 2 == 0 && TW % RS == 0 && RS % 2 == 0, "even tiles and strips");
+  static_assert(BAL || NE % 4 == 0, "a wave's 4 slots never straddle the parity boundary");
+  static_assert(GH * DRS * 8 + (K * K + 9 + 2 * FR) * DCG * 4 <= 80 * 1024, "two workgroups per CU");
 };
 
-template <typename T, int K, int TH, int TW, int RS>
+template <typename T, int K, int TH, int TW, int RS, int FR>
 __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
     const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
     int ntiles, int groups, int tiles_x, int tiles_y) {
-  using D = Dw2<T, K, TH, TW, RS>;
+  using D = Dw2<T, K, TH, TW, RS, FR>;
   __shared__ __attribute__((aligned(16))) char dyraw[D::DYB];
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];
   __shared__ __attribute__((aligned(16))) float cst[9][DCG];  // sc2 sh2 k1 k2 k3 | sc1 sh1 mean1 invstd1
-  __shared__ __attribute__((aligned(16))) float gbl[2][DCG];  // the tile frame's SE gate and bc
+  __shared__ __attribute__((aligned(16))) float gbl[FR][2][DCG];  // the tile frames' SE gate and bc
   float* dys = reinterpret_cast<float*>(dyraw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = blockIdx.x % groups;
@@ -82,51 +95,60 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
   for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
-    const int f = t / tpf, r = t - f * tpf, ty = r / tiles_x;
+    const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;  // first frame of the tile
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;  // input tile origin (even)
     const int ob = iy0 / 2 - 1, oxb = ix0 / 2 - 1;             // staged dY window origin
-    Raw8<T> rz[D::NLD], r2[D::NLD];
-    {
-      const T* zf = dZ + (int64_t)f * ostride;
-      const T* yf = Y2 + (int64_t)f * ostride;
+    // staging in chunks of at most CH 8-channel loads per tensor in flight (the stacked-frame tiles
+    // would otherwise hold 2 x 6 raw vectors next to the launch-long dW accumulators)
+    const T* zf = dZ + (int64_t)f * ostride;
+    const T* yf = Y2 + (int64_t)f * ostride;
 #pragma unroll
-      for (int i = 0; i < D::NLD; ++i) {
-        const int pixl = (tid >> 2) + 64 * i;
-        const int oy = ob + pixl / D::GW, ox = oxb + pixl % D::GW;
-        const bool in = pixl < D::NG && cok8 && oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo;
-        const uint32_t o = in ? (uint32_t)((oy * g.Wo + ox) * C + c8) : 0u;
-        raw_ld(rz[i], zf + o, zf, in);
-        raw_ld(r2[i], yf + o, yf, in);
+    for (int base = 0; base < D::NLD; base += D::CH) {
+      Raw8<T> rz[D::CH], r2[D::CH];
+#pragma unroll
+      for (int u = 0; u < D::CH; ++u) {
+        const int pixl = (tid >> 2) + 64 * (base + u);
+        const int fi = FR > 1 ? pixl / D::NG1 : 0, pf = pixl - fi * D::NG1;
+        const int oy = ob + pf / D::GW, ox = oxb + pf % D::GW;
+        const bool in = base + u < D::NLD && pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.Ho &&
+                        ox >= 0 && ox < g.Wo;
+        const uint32_t o = in ? (uint32_t)(fi * ostride + (oy * g.Wo + ox) * C + c8) : 0u;
+        raw_ld(rz[u], zf + o, zf, in);
+        raw_ld(r2[u], yf + o, yf, in);
       }
-    }
-    for (int i = tid; i < 2 * DCG; i += 256) {
-      const int w2 = i / DCG, cl = i % DCG;
-      gbl[w2][cl] = c0 + cl < C ? (w2 ? b2.bc : b2.gate)[(int64_t)f * C + c0 + cl] : 0.f;
-    }
-    lds_barrier();  // the previous tile's strips are done with dys; gbl written
-#pragma unroll
-    for (int i = 0; i < D::NLD; ++i) {
-      const int pixl = (tid >> 2) + 64 * i;
-      asm volatile("" ::: "memory");
-      if (pixl < D::NG) {
-        float* dst = dys + (pixl / D::GW) * D::DRS * 2 + (pixl % D::GW) * DCG + v8 * 8;
-        float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (rz[i].ok) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int cq = v8 * 8 + 2 * q;
-            const v2f z = raw8_pair(rz[i], q), y = raw8_pair(r2[i], q);
-            const v2f tz = fma2(y, lds2(&cst[0][cq]), lds2(&cst[1][cq]));
-            const v2f sg = sigmoid2(tz);
-            const v2f ds = sg * fma2(tz, 1.0f - sg, v2f{1.f, 1.f});
-            const v2f g2 = fma2(z, lds2(&gbl[0][cq]), lds2(&gbl[1][cq])) * ds;
-            const v2f v = round2(fma2(lds2(&cst[2][cq]), g2, fma2(lds2(&cst[3][cq]), y, lds2(&cst[4][cq]))),
-                                 (T*)nullptr);
-            o[2 * q] = v.x;
-            o[2 * q + 1] = v.y;
-          }
+      if (base == 0) {
+        for (int i = tid; i < FR * 2 * DCG; i += 256) {
+          const int fi = i / (2 * DCG), w2 = (i / DCG) & 1, cl = i % DCG;
+          const bool ok = c0 + cl < C && f + fi < g.frames;
+          gbl[fi][w2][cl] = ok ? (w2 ? b2.bc : b2.gate)[(int64_t)(f + fi) * C + c0 + cl] : 0.f;
         }
-        st8(dst, o);
+        lds_barrier();  // the previous tile's strips are done with dys; gbl written
+      }
+#pragma unroll
+      for (int u = 0; u < D::CH; ++u) {
+        const int pixl = (tid >> 2) + 64 * (base + u);
+        asm volatile("" ::: "memory");
+        if (base + u < D::NLD && pixl < D::NG) {
+          float* dst = dys + (pixl / D::GW) * D::DRS * 2 + (pixl % D::GW) * DCG + v8 * 8;
+          float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if (rz[u].ok) {
+            const int fi = FR > 1 ? pixl / D::NG1 : 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int cq = v8 * 8 + 2 * q;
+              const v2f z = raw8_pair(rz[u], q), y = raw8_pair(r2[u], q);
+              const v2f tz = fma2(y, lds2(&cst[0][cq]), lds2(&cst[1][cq]));
+              const v2f sg = sigmoid2(tz);
+              const v2f ds = sg * fma2(tz, 1.0f - sg, v2f{1.f, 1.f});
+              const v2f g2 = fma2(z, lds2(&gbl[fi][0][cq]), lds2(&gbl[fi][1][cq])) * ds;
+              const v2f v = round2(fma2(lds2(&cst[2][cq]), g2, fma2(lds2(&cst[3][cq]), y, lds2(&cst[4][cq]))),
+                                   (T*)nullptr);
+              o[2 * q] = v.x;
+              o[2 * q + 1] = v.y;
+            }
+          }
+          st8(dst, o);
+        }
       }
     }
     lds_barrier();
@@ -136,17 +158,32 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
     const T* y1f = Y1 + (int64_t)f * istride;
     T* outf = out + (int64_t)f * istride;
 #pragma unroll 1
-    for (int it = 0; it < 2; ++it) {
-      // wave w, slot q, pass it -> row 2q + par, par = (w&1)^it; column (w>>1) + 2 it.  Over the two
-      // passes the 32 (row, column) strips are each visited once; a wave's 4 slots read 4
-      // consecutive staged rows (odd row stride: opposite bank halves)
-      const int par = (wave & 1) ^ it;
-      const int pr = 2 * (slot & 3) + par;
-      const int xs = ((wave >> 1) + 2 * it) * RS;
-      // tiles never cross the map (covers(): H % 8, W % 56): only the channel bound masks anything.
-      // Lanes past C read pixel 0 of the frame (pixel stride 0) and skip the epilogue
-      const uint32_t pb = cokp ? (uint32_t)(C * sizeof(T)) : 0u;
-      const uint32_t sb = cokp ? (uint32_t)((((iy0 + pr) * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
+    for (int it = 0; it < D::NPASS; ++it) {
+      int fi = 0, par, pr, xs;
+      if constexpr (D::BAL) {
+        // wave w, slot q, pass it -> row 2q + par, par = (w&1)^it; column (w>>1) + 2 it.  Over the
+        // two passes the 32 (row, column) strips are each visited once; a wave's 4 slots read 4
+        // consecutive staged rows (odd row stride: opposite bank halves)
+        par = (wave & 1) ^ it;
+        pr = 2 * (slot & 3) + par;
+        xs = ((wave >> 1) + 2 * it) * RS;
+      } else {
+        const int s = slot + 16 * it;  // parity-major: [even-row strips of all frames][odd ...]
+        if (s >= D::NSTRIP) continue;  // uniform per wave (NSTRIP % 4 == 0)
+        par = s >= D::NE;
+        const int e = s - par * D::NE;
+        fi = e / (D::HE * D::SPR);
+        const int e2 = e - fi * (D::HE * D::SPR);
+        pr = 2 * (e2 % D::HE) + par;   // consecutive slots: consecutive staged rows
+        xs = (e2 / D::HE) * RS;
+      }
+      // tiles never cross the map (covers()): only the channel bound and a missing last stacked
+      // frame mask anything.  Such lanes read pixel 0 of frame f (pixel stride 0; their staged dY is
+      // zero, so their dW terms are too) and skip the epilogue
+      const bool rok = cokp && f + fi < g.frames;
+      const uint32_t pb = rok ? (uint32_t)(C * sizeof(T)) : 0u;
+      const uint32_t sb =
+          rok ? (uint32_t)((fi * istride + ((iy0 + pr) * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
       Raw2<T> ry[RS];
 #pragma unroll
       for (int px = 0; px < RS; ++px) raw2_ld(ry[px], boff(y1f, sb + px * pb));
@@ -165,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
         // output row (pr + pad - kh) / 2 exists for one row parity; uniform per wave
         if (((pr + D::PAD - kh) & 1) == 0) {
           asm volatile("" ::: "memory");
-          const int srow = (pr + D::PAD - kh) / 2 + 1;  // staged row (window origin iy0/2 - 1)
+          const int srow = fi * D::GH1 + (pr + D::PAD - kh) / 2 + 1;  // staged row (window origin iy0/2 - 1)
           const float* rowp = dys + srow * D::DRS * 2 + (xs / 2) * DCG + 2 * cp;
           v2f dr[D::RWO], wr[K];
 #pragma unroll
@@ -190,7 +227,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
       }
 #pragma unroll
       for (int px = 0; px < RS; ++px) pin2(ry[px]);
-      if (cokp) {
+      if (rok) {
 #pragma unroll
         for (int px = 0; px < RS; ++px) {
           const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
@@ -234,32 +271,39 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS>
+template <typename T, int K, int TH, int TW, int RS, int FR>
 static int bwd2_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const Dw1Bn2& b2, const float* w,
                        const T* Y1, const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab,
                        int64_t slab_cap, float* dW, bool accumulate) {
   const int tiles_x = g.W / TW, tiles_y = g.H / TH;
-  const int ntiles = g.frames * tiles_x * tiles_y;
+  const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
-  const int resident = resident_wgs<dw_bwd2_kernel<T, K, TH, TW, RS>, 256>();
+  const int resident = resident_wgs<dw_bwd2_kernel<T, K, TH, TW, RS, FR>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   rows = std::min<int64_t>(rows, 1024);
-  hipLaunchKernelGGL((dw_bwd2_kernel<T, K, TH, TW, RS>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, dZ, Y2,
-                     b2, w, Y1, bn1, out, stats, slab, ntiles, groups, tiles_x, tiles_y);
+  hipLaunchKernelGGL((dw_bwd2_kernel<T, K, TH, TW, RS, FR>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, dZ,
+                     Y2, b2, w, Y1, bn1, out, stats, slab, ntiles, groups, tiles_x, tiles_y);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
   return launch_reduce_slabs(s, slab, (int)rows, per, dW, accumulate);
 }
 
-bool dw_bwd2_covers(const DwGeom& g) {
-  if (g.s != 2 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2) return false;
-  if (g.Ho != (g.H + 2 * g.pad - g.k) / 2 + 1 || g.Wo != (g.W + 2 * g.pad - g.k) / 2 + 1) return false;
-  // exact tiling; 32-bit byte offsets within a frame (fp32 bound, for both dtypes)
-  if (g.H % 8 || g.W % 56 || (g.C & 1) || (int64_t)g.H * g.W * g.C * 4 >= (1ll << 32)) return false;
-  return dw_bwd1_enabled();
+// tile configuration for a stride-2 layer: 0 none, 1 8x56 tiles, 2 whole 28x28 frames (k3),
+// 3 four stacked 14x14 frames (k5)
+static int dw2_config(const DwGeom& g) {
+  if (g.s != 2 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2) return 0;
+  if (g.Ho != (g.H + 2 * g.pad - g.k) / 2 + 1 || g.Wo != (g.W + 2 * g.pad - g.k) / 2 + 1) return 0;
+  // channel pairs; 32-bit byte offsets within the (up to 4) frames of a tile, fp32 bound
+  if ((g.C & 1) || (int64_t)g.H * g.W * g.C * 16 >= (1ll << 32)) return 0;
+  if (g.H % 8 == 0 && g.W % 56 == 0) return 1;
+  if (g.k == 3 && g.H == 28 && g.W == 28) return 2;
+  if (g.k == 5 && g.H == 14 && g.W == 14) return 3;
+  return 0;
 }
+
+bool dw_bwd2_covers(const DwGeom& g) { return dw2_config(g) != 0 && dw_bwd1_enabled(); }
 
 template <typename T>
 int launch_dw_bwd2(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const float* gate, const float* bc,
@@ -268,9 +312,20 @@ int launch_dw_bwd2(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
                    bool accumulate) {
   if (!dw_bwd2_covers(g)) return 1;
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
-  if (g.k == 3)
-    return bwd2_launch<T, 3, 8, 56, 14>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
-  return bwd2_launch<T, 5, 8, 56, 14>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+  switch (dw2_config(g)) {
+    case 1:
+      if (g.k == 3)
+        return bwd2_launch<T, 3, 8, 56, 14, 1>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
+                                               accumulate);
+      return bwd2_launch<T, 5, 8, 56, 14, 1>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
+                                             accumulate);
+    case 2:
+      return bwd2_launch<T, 3, 28, 28, 14, 1>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
+                                              accumulate);
+    default:
+      return bwd2_launch<T, 5, 14, 14, 14, 4>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
+                                              accumulate);
+  }
 }
 
 template int launch_dw_bwd2<float>(hipStream_t, const DwGeom&, const float*, const float*, const float*, const float*,
