@@ -8,7 +8,7 @@ read or written once per dispatch; the tensor exceeds the 256 MiB Infinity Cache
   mode 2  64-B channel slices,  8 B/lane -> FETCH_SIZE = 1.0 x bytes
   mode 3/4  slice / contiguous writes    -> WRITE_SIZE = 1.0 x bytes
 
-The probed launch (dw_bwd2<bf16,3,8,56,14> of blocks.1.0, C = 96, k_dw_bwd2.hip) reads 64-B slices
+The probed launch (dw_bwd2<bf16,3,8,56,14,1> of blocks.1.0, C = 96, k_dw_bwd2.hip) reads 64-B slices
 of 32 channels (one channel group per workgroup, pixels 192 B apart: 16 B/lane staging loads of dZ
 and y2, 4 B/lane strip loads of y1), i.e. the mode-1/2 pattern (factor 1.0 for both), so its
 FETCH_SIZE is divided by the mode-1 factor.  (Layers with C = 32 -- blocks.0.0 -- read adjacent
@@ -24,7 +24,7 @@ import os
 import statistics
 import sys
 
-PROBE = ("dw_bwd:1.0", "dw_bwd2_kernel<dfd::bf16, 3, 8, 56, 14>", 1)  # key, kernel name, calibration mode
+PROBE = ("dw_bwd:1.0", "dw_bwd2_kernel<dfd::bf16, 3, 8, 56, 14, 1>", 1)  # key, kernel name, calibration mode
 KNOWN = 256 * 112 * 112 * 96 * 2
 
 
