@@ -153,7 +153,7 @@ int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64
 int dfd_b0_plan_set_tuning(dfd_b0_plan* plan, const char* key, int64_t value) {
   if (!plan || !key) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
   static const char* names[dfd::TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile",
-                                             "dw_bwd1", "dw_fwd1"};
+                                             "dw_bwd1", "dw_fwd1", "wgrad_stream"};
   for (int k = 0; k < dfd::TK_COUNT; ++k)
     if (strcmp(key, names[k]) == 0) {
       std::lock_guard<std::mutex> lk(plan->mu);
@@ -378,6 +378,7 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "gemm_tile") == 0) return dfd::set_gemm_tile((int)value);
   if (key && strcmp(key, "dw_bwd1") == 0) return dfd::set_dw_bwd1(value);
   if (key && strcmp(key, "dw_fwd1") == 0) return dfd::set_dw_fwd1(value);
+  if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }

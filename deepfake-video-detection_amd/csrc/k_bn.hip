@@ -1078,6 +1078,10 @@ SlabDefer* set_slab_defer(SlabDefer* d) {
 }
 
 int SlabDefer::flush() {
+  if (aux) {  // the aux stream's queued slabs (and direct gradient writes) complete first
+    DFD_HIP_CHECK(hipEventRecord(ev_aux, aux));
+    DFD_HIP_CHECK(hipStreamWaitEvent(stream, ev_aux, 0));
+  }
   if (n == 0) return 0;
   SlabBatchArgs a{};
   int blocks = 0, lanes = 4;
@@ -1092,13 +1096,17 @@ int SlabDefer::flush() {
   n = 0;
   hipLaunchKernelGGL(reduce_slabs_batch_kernel, dim3((unsigned)blocks), dim3(64 * lanes), 0, stream, a);
   DFD_HIP_CHECK(hipGetLastError());
+  if (aux) {  // the regions just reduced may be handed to aux-stream kernels next
+    DFD_HIP_CHECK(hipEventRecord(ev_main, stream));
+    DFD_HIP_CHECK(hipStreamWaitEvent(aux, ev_main, 0));
+  }
   return 0;
 }
 
 int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, int64_t n, int64_t stride, float* out,
                                 bool accumulate) {
   SlabDefer* d = t_slab_defer;
-  if (d && d->stream == s && stride == n && out >= d->lo && out + n <= d->hi && n <= ((int64_t)1 << 30)) {
+  if (d && (d->stream == s || (d->aux && d->aux == s)) && stride == n && out >= d->lo && out + n <= d->hi && n <= ((int64_t)1 << 30)) {
     if (d->n == SlabDefer::kMax) DFD_TRY(d->flush());
     d->jobs[d->n++] = SlabJob{slab, n, out, splits, accumulate ? 1 : 0};
     return 0;

@@ -26,7 +26,8 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
 // a plan's forward/backward installs its own Tuning for the enqueuing thread (TuningScope), so
 // concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- never read each other's knobs.
-enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1, TK_COUNT };
+enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
+               TK_WGRAD_STREAM, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -229,6 +230,9 @@ struct SlabJob {
   float* out;
   int splits, accumulate;
 };
+// With an aux stream (the backward's weight-gradient stream), jobs queued from either stream are
+// reduced on `stream`; flush() first makes `stream` wait for everything enqueued on `aux`, and
+// afterwards makes `aux` wait for the reduction (the slab regions are then free on both streams).
 struct SlabDefer {
   static constexpr int kMax = 16;
   hipStream_t stream;
@@ -236,6 +240,8 @@ struct SlabDefer {
   const float* hi;
   SlabJob jobs[kMax];
   int n = 0;
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_aux = nullptr, ev_main = nullptr;
   int flush();
 };
 SlabDefer* set_slab_defer(SlabDefer* d);  // returns the previous one

@@ -200,6 +200,8 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.o_slab = alloc(kSlabRegions * p.slab_cap * 4);
   p.o_part = alloc(p.part_cap * 4);
   p.o_coef = alloc(3 * kHead * 4);
+  p.o_coef1 = alloc(3 * kHead * 4);
+  p.o_stats2 = alloc(p.stats_cap * 4);
   p.o_bc = alloc(F * maxSE * 4);
   p.o_pf = alloc(4 * F * maxSE * 4);  // per-frame SE/BN backward sums
   p.o_de = alloc(F * maxSE * 4);
@@ -270,8 +272,38 @@ int probe_read(Plan& p, float* ms, int cap, int* count) {
   return 0;
 }
 
+static void aux_free(Plan& p) {
+  for (auto& e : p.ev)
+    if (e) { (void)hipEventDestroy(e); e = nullptr; }
+  if (p.aux) { (void)hipStreamDestroy(p.aux); p.aux = nullptr; }
+  p.aux_dev = -1;
+}
+
+// the weight-gradient stream on the device of the caller's stream (plans are per device, but the
+// stream of each call is the caller's)
+static int aux_init(Plan& p, hipStream_t s) {
+  int dev = 0;
+  DFD_HIP_CHECK(hipStreamGetDevice(s, &dev));
+  if (p.aux && p.aux_dev == dev) return 0;
+  aux_free(p);
+  int cur = 0;
+  DFD_HIP_CHECK(hipGetDevice(&cur));
+  if (cur != dev) DFD_HIP_CHECK(hipSetDevice(dev));
+  hipError_t e = hipStreamCreateWithFlags(&p.aux, hipStreamNonBlocking);
+  for (int i = 0; i < 6 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&p.ev[i], hipEventDisableTiming);
+  if (cur != dev) (void)hipSetDevice(cur);
+  if (e != hipSuccess) {
+    aux_free(p);
+    set_error((std::string("wgrad stream: ") + hipGetErrorString(e)).c_str(), __FILE__, __LINE__);
+    return -1;
+  }
+  p.aux_dev = dev;
+  return 0;
+}
+
 void plan_free(Plan& p) {
   probe_disarm(p);
+  aux_free(p);
   if (p.cast_dev) { (void)hipFree(p.cast_dev); p.cast_dev = nullptr; }
 }
 
@@ -284,13 +316,14 @@ inline bool probe_hit(const Plan& p, int kind, const Block* b) {
          b->idx == p.probe.idx;
 }
 // Wrap one launch: PROBED(kind, block, launch-expression)
-#define PROBED(KIND, BLK, EXPR)                                                    \
-  do {                                                                             \
-    const bool _hit = probe_hit(p, KIND, BLK);                                     \
-    if (_hit) (void)hipEventRecord(p.probe.b[p.probe.count], s);                   \
-    DFD_TRY(EXPR);                                                                 \
-    if (_hit) { (void)hipEventRecord(p.probe.e[p.probe.count], s); ++p.probe.count; } \
+#define PROBED_ON(KIND, BLK, STREAM, EXPR)                                                 \
+  do {                                                                                     \
+    const bool _hit = probe_hit(p, KIND, BLK);                                             \
+    if (_hit) (void)hipEventRecord(p.probe.b[p.probe.count], STREAM);                      \
+    DFD_TRY(EXPR);                                                                         \
+    if (_hit) { (void)hipEventRecord(p.probe.e[p.probe.count], STREAM); ++p.probe.count; } \
   } while (0)
+#define PROBED(KIND, BLK, EXPR) PROBED_ON(KIND, BLK, s, EXPR)
 
 template <typename T>
 struct Run {
@@ -379,6 +412,11 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
 // the extra small passes over x cost more than the expanded-tensor passes they save
 // (dfd_set_tuning("fold_min_rows", v); tests force both paths)
 std::atomic<int64_t> g_fold_min_rows{100000};
+// 1x1-conv weight gradients on the plan's second stream (dfd_set_tuning("wgrad_stream", v): 0 off,
+// 1 every block, N > 1 blocks with >= N gradient rows).  Off by default: measured 0.17-0.26 ms/step
+// SLOWER at every threshold (in-process A/B, tools/ab_bench.py) -- the persistent, occupancy-sized
+// depthwise kernels of the main chain lose resident workgroup slots to the concurrent gradients
+std::atomic<int64_t> g_wgrad_stream{0};
 
 template <typename T>
 int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& ifmt, const float* dfeat,
@@ -420,6 +458,42 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
     SlabDefer* prev;
     ~DeferScope() { set_slab_defer(prev); }
   } scope{set_slab_defer(&defer)};
+  // The 1x1-conv weight gradients run on the plan's second stream `w`, overlapping the main chain
+  // on `s` (BN/SE backward, depthwise backward, data gradients).  Events order the two: w starts
+  // a gradient once its operands are final on s (fork), and s waits for w (join) before it
+  // overwrites a scratch buffer a queued gradient still reads: o_gs (g3, read by the conv_pwl
+  // weight gradient) and o_ge1 / o_coef1 / o_stats2 (the conv_pw weight gradient).  Slab
+  // reductions from both streams are batched on s (SlabDefer joins both ways at every flush).
+  // knob: 0 off; 1 every block; N > 1 only blocks whose gradient rows reach N (the cross-stream
+  // waits cost a few us each: small late-stage gradients are not worth them)
+  const int64_t ws_min = tune_or(TK_WGRAD_STREAM, g_wgrad_stream.load(std::memory_order_relaxed));
+  hipStream_t w_aux = s;
+  if (ws_min != 0) {
+    DFD_TRY(aux_init(p, s));
+    w_aux = p.aux;
+    defer.aux = w_aux;
+    defer.ev_aux = p.ev[4];
+    defer.ev_main = p.ev[5];
+  }
+  hipStream_t w = s;  // the stream of the current block's weight gradients
+  bool gs_busy = false, ge1_busy = false;
+  auto fork = [&](hipEvent_t ev) -> int {  // w waits for everything enqueued on s so far
+    if (w == s) return 0;
+    DFD_HIP_CHECK(hipEventRecord(ev, s));
+    DFD_HIP_CHECK(hipStreamWaitEvent(w, ev, 0));
+    return 0;
+  };
+  auto mark = [&](hipEvent_t ev, bool& busy) -> int {  // the buffers read on w so far stay busy until ev
+    if (w == s) return 0;
+    DFD_HIP_CHECK(hipEventRecord(ev, w));
+    busy = true;
+    return 0;
+  };
+  auto join = [&](hipEvent_t ev, bool& busy) -> int {  // s waits for the last mark(ev)
+    if (busy) DFD_HIP_CHECK(hipStreamWaitEvent(s, ev, 0));
+    busy = false;
+    return 0;
+  };
   int region = 0, slab_err = 0;
   auto slab = [&]() -> float* {
     if (region == kSlabRegions) {  // every region holds a pending slab: reduce them first
@@ -449,17 +523,21 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         const BNL& bn_dw = b.ds ? b.bn1 : b.bn2;
         T* gout = r.a(p.o_gx[i & 1]);
         DwGeom g{p.frames, b.hin, b.win, b.mid, b.k, b.s, b.k / 2, b.hout, b.wout};
+        w = (ws_min != 0 && Mout >= ws_min) ? w_aux : s;
         // BN after the 1x1 projection (no activation)
         BnBwdIn i3{};
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
+        DFD_TRY(join(p.ev[1], gs_busy));  // the previous conv_pwl weight gradient is done with o_gs
         DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
         PROBED(PK_PWL_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout,
                                                     b.mid, b.cout, PRO_NONE, Pro{}, nullptr, nullptr)));
         const bool mat = b.o_s2 >= 0;
-        PROBED(PK_PWL_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_gs), mat ? r.a(b.o_s2) : r.a(b.o_y2), Mout, b.cout,
-                                                     b.mid, mat ? PRO_GATE : PRO_BN_SILU_G,
-                                                     r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), slab(), p.slab_cap,
-                                                     grad(b.pwl.t_w), acc != 0)));
+        DFD_TRY(fork(p.ev[0]));
+        PROBED_ON(PK_PWL_WGRAD, &b, w,
+                  (launch_pw_wgrad<T>(w, r.a(p.o_gs), mat ? r.a(b.o_s2) : r.a(b.o_y2), Mout, b.cout, b.mid,
+                                      mat ? PRO_GATE : PRO_BN_SILU_G, r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), slab(),
+                                      p.slab_cap, grad(b.pwl.t_w), acc != 0)));
+        DFD_TRY(mark(p.ev[1], gs_busy));
         // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE
         // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
         int hs = 1;
@@ -481,6 +559,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         BnBwdIn fz{};
         fz.mean = r.f(bn_in.o_mean); fz.invstd = r.f(bn_in.o_invstd);
         fz.scale = r.f(bn_in.o_scale); fz.shift = r.f(bn_in.o_shift); fz.silu = true;
+        DFD_TRY(join(p.ev[3], ge1_busy));  // the previous conv_pw weight gradient is done with o_ge1
         int fused = 1;
         // stride 1: one kernel also applies the BN2(+SiLU, gate) backward while staging dY
         // (k_dw_bwd1.hip); otherwise the apply pass materialises dY first
@@ -524,8 +603,10 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
           PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(b.pw.o_wt), r.a(p.o_gx[(i - 1) & 1]),
                                                      b.skip ? gout : nullptr, Min, b.cin, b.mid, PRO_NONE, Pro{},
                                                      nullptr, nullptr)));
-          PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
-                                                      slab(), p.slab_cap, grad(b.pw.t_w), acc != 0)));
+          DFD_TRY(fork(p.ev[2]));
+          PROBED_ON(PK_PW_WGRAD, &b, w, (launch_pw_wgrad<T>(w, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
+                                                            slab(), p.slab_cap, grad(b.pw.t_w), acc != 0)));
+          DFD_TRY(mark(p.ev[3], ge1_busy));
         } else if (!b.ds) {
           // conv_pw + its BN (no activation): ge1 = k1*g + k2*y1 + k3 is never materialised; by
           // linearity (y1 = x . W^T) the gradients need only g (in ge1) and the block input x:
@@ -535,20 +616,24 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
           T* gxo = r.a(p.o_gx[(i - 1) & 1]);
           DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), p.pending_rows, Min, b.mid, r.prm(b.bn1.t_w),
                                          r.f(b.bn1.o_mean), r.f(b.bn1.o_invstd), tr != 0, grad(b.bn1.t_w),
-                                         grad(b.bn1.t_b), acc != 0, r.f(p.o_coef)));
-          DFD_TRY(launch_bn_fold_pw<T>(s, r.prm(b.pw.t_w), r.f(p.o_coef), b.mid, b.cin, r.a(p.o_w1t), r.a(p.o_q),
+                                         grad(b.bn1.t_b), acc != 0, r.f(p.o_coef1)));
+          DFD_TRY(launch_bn_fold_pw<T>(s, r.prm(b.pw.t_w), r.f(p.o_coef1), b.mid, b.cin, r.a(p.o_w1t), r.a(p.o_q),
                                        r.f(p.o_bv)));
+          DFD_TRY(join(p.ev[1], gs_busy));  // the conv_pwl weight gradient is done with o_gs
           DFD_TRY(launch_tf_gemm<T>(s, xin, r.a(p.o_q), r.a(p.o_gs), b.skip ? gout : nullptr, r.f(p.o_bv), nullptr,
                                     Min, b.cin, b.cin, PRO_NONE, EPI_BIAS | (b.skip ? EPI_RESID : 0)));
           PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(p.o_w1t), gxo, r.a(p.o_gs), Min, b.cin,
                                                      b.mid, PRO_NONE, Pro{}, nullptr, nullptr)));
-          PROBED(PK_PW_WGRAD, &b, (launch_pw_wgrad<T>(s, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
-                                                      slab(), p.slab_cap, r.f(p.o_tg), false)));
-          DFD_TRY(launch_pw_wgrad<T>(s, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, slab(), p.slab_cap,
+          // the weight gradient through the BN on w: g (o_ge1), x, the BN1 coefficients (o_coef1)
+          DFD_TRY(fork(p.ev[2]));
+          PROBED_ON(PK_PW_WGRAD, &b, w, (launch_pw_wgrad<T>(w, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
+                                                            slab(), p.slab_cap, r.f(p.o_tg), false)));
+          DFD_TRY(launch_pw_wgrad<T>(w, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, slab(), p.slab_cap,
                                      r.f(p.o_gram), false));
-          DFD_TRY(launch_col_sums<T>(s, xin, Min, b.cin, r.f(p.o_stats), p.stats_cap, r.f(p.o_cs)));
-          DFD_TRY(launch_pw_wgrad_bn_combine(s, r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs), r.prm(b.pw.t_w),
-                                             r.f(p.o_coef), b.mid, b.cin, grad(b.pw.t_w), acc != 0));
+          DFD_TRY(launch_col_sums<T>(w, xin, Min, b.cin, r.f(p.o_stats2), p.stats_cap, r.f(p.o_cs)));
+          DFD_TRY(launch_pw_wgrad_bn_combine(w, r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs), r.prm(b.pw.t_w),
+                                             r.f(p.o_coef1), b.mid, b.cin, grad(b.pw.t_w), acc != 0));
+          DFD_TRY(mark(p.ev[3], ge1_busy));
         }
       }
     } else {
@@ -572,6 +657,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
 }  // namespace
 
 int64_t set_fold_min_rows(int64_t v) { return g_fold_min_rows.exchange(v); }
+int64_t set_wgrad_stream(int64_t v) { return g_wgrad_stream.exchange(v); }
 
 static thread_local const Tuning* t_tune = nullptr;
 int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }

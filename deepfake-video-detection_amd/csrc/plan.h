@@ -67,6 +67,7 @@ struct Plan {
   int64_t o_ystem, o_yh, o_stats, o_slab, o_part, o_coef, o_bc, o_de, o_dz, o_pf;
   int64_t o_gx[2], o_gs, o_ge1, o_ge2;
   int64_t o_w1t, o_q, o_bv, o_tg, o_gram, o_cs;  // conv_pw backward through its BN (bn_fold_pw)
+  int64_t o_coef1, o_stats2;  // BN1 backward coefficients / col_sums partials read on the wgrad stream
   int64_t stats_cap, slab_cap, part_cap;
   // cast table (device copy)
   std::vector<CastSeg> cast_host;
@@ -76,6 +77,11 @@ struct Plan {
   int pending_rows = 0;  // stat rows written by the stage-0 dw dgrad, consumed by the stem segment
   Probe probe;
   Tuning tune;  // per-plan kernel-selection overrides (dfd_b0_plan_set_tuning)
+  // the backward's weight-gradient stream (created on first use, on the caller stream's device)
+  // and the events that order it against the caller's stream
+  hipStream_t aux = nullptr;
+  int aux_dev = -1;
+  hipEvent_t ev[6] = {};
 };
 
 int probe_arm(Plan& p, int kind, int stage, int idx, int n);
@@ -96,6 +102,9 @@ void plan_segment_range(const Plan& p, int seg, int* lo, int* hi);
 constexpr int kNumSegments = 9;
 // rows threshold of the BN-folded conv_pw backward (returns the previous value)
 int64_t set_fold_min_rows(int64_t v);
+// 1x1-conv weight gradients on a second stream, overlapping the backward's main chain (0 off -- the
+// default --, 1 every block, N > 1 blocks with >= N gradient rows)
+int64_t set_wgrad_stream(int64_t v);
 // static topology (shape-independent)
 const std::vector<TensorSpec>& b0_tensor_table();
 

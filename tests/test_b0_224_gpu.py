@@ -1,13 +1,14 @@
 """224x224 training-step parity of the HIP EfficientNet-B0 detector -- the map sizes the bench runs.
 
-The depthwise kernels pick their tiles from the feature-map size (``k_dw_bwd.hip`` launch_dw_bwd,
-``k_dw_strip.hip``), so only a 224x224 input reaches the tiles the 256-frame bench step runs:
-``dw_bwd<16,16,3,2>`` (blocks.1.0), ``<16,16,3,1>`` (blocks.0.0), ``<8,28,3,1>`` (blocks.1.1),
-``<8,8,5,2>`` (blocks.2.0), ``<14,14,5,1>`` (blocks.2.1, 4.x), ``<8,8,3,2>`` (blocks.3.0),
-``<14,14,3,1>`` (blocks.3.x), ``<7,7,5,1>`` / ``<7,7,3,1>`` (stages 5/6) and, in bf16, the k5
-14x14 strip forward.  Two batches:
+The depthwise kernels pick their tiles from the feature-map size, so only a 224x224 input reaches
+the launches the 256-frame bench step runs: the fused stride-1 backward ``dw_bwd1`` on 8x28 tiles
+(blocks.0.0, 1.1), 14x14 tiles (k3/k5 on 28x28 and 14x14 maps) and two stacked 7x7 frames
+(stages 5/6); the fused stride-2 backward ``dw_bwd2`` on 8x56 tiles (blocks.1.0 k3, 2.0 k5),
+whole 28x28 frames (blocks.3.0) and four stacked 14x14 frames (blocks.5.0); the channel-pair
+forwards ``dw_fwd1`` and the remaining stride-2 forwards.  Two batches:
 
-* 1 clip x 2 frames: the smallest batch with a non-trivial temporal softmax;
+* 1 clip x 2 frames: the smallest batch with a non-trivial temporal softmax (and a partly empty
+  four-frame tile);
 * 4 clips x 8 frames (32 frames, the reference's clip shape): the >=100K-row layers take the
   streaming 1x1 kernels and the BN-folded expansion backward on the default path, and the 28x28
   stage takes the 64x64 GEMM tile -- the bench's selections.
@@ -151,3 +152,22 @@ def test_train_step_224_bf16(cuda, case, kernel_paths):
     assert not low, low
     for n, rb in ref["bufs"].items():
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
+
+
+def test_wgrad_stream_bit_identical(cuda):
+    """The 1x1 weight gradients on the plan's second stream (dfd_set_tuning("wgrad_stream", 1); off by
+    default) give bit-identical results to the single-stream schedule: same kernels, same fixed-order reductions; only the overlap changes
+    (a missing event would show up as a race here)."""
+    from deepfake_amd import _lib
+    lib = _lib.load()
+    prev = lib.dfd_set_tuning(b"wgrad_stream", 1)
+    try:
+        _, _, loss_a, grads_a, bufs_a = hip_step("b4t8", "bf16", cuda)
+        lib.dfd_set_tuning(b"wgrad_stream", 0)
+        _, _, loss_b, grads_b, bufs_b = hip_step("b4t8", "bf16", cuda)
+    finally:
+        lib.dfd_set_tuning(b"wgrad_stream", prev)
+    assert loss_a == loss_b
+    diff = [n for n in grads_a if not torch.equal(grads_a[n], grads_b[n])]
+    assert not diff, diff[:10]
+    assert all(torch.equal(bufs_a[n], bufs_b[n]) for n in bufs_a)
