@@ -264,10 +264,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdIn in, const T*
   }
 }
 
+// channel groups of <= 16 eight-channel vectors, as EVEN as possible: C = 144 (18 vectors) is two
+// groups of 9, not 16 + 2 (whose second group's workgroups ran a full-length loop with 2 of 16
+// vectors busy: 2x the time of the layer's data on blocks.2.x)
 static void bn_vpg_groups(int C, int& vpg, int& groups) {
   const int nv = C / 8;
-  vpg = nv < 16 ? nv : 16;
-  groups = cdiv(nv, vpg);
+  groups = cdiv(nv, 16);
+  vpg = cdiv(nv, groups);
 }
 
 template <typename T>
