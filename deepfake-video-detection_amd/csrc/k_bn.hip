@@ -957,14 +957,19 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
   for (int n0 = cbeg + 16 * wave; n0 < cend; n0 += 16 * SE_W) {
     const int n = n0 + li;
     const bool nok = n < cend;
-    se_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < rd; k0 += 4) {
-      const int k = k0 + lk;
-      const float a = Ts[li][k];
+    // all of B2's column for this lane first (<= 12 independent loads in flight), then the MFMA
+    // chain in the same k order (one serialized load per MFMA step was the kernel's latency chain)
+    float bw[SE_RDMAX / 4];
+#pragma unroll
+    for (int i = 0; i < SE_RDMAX / 4; ++i) {
+      const int k = 4 * i + lk;
       const bool ok = nok && k < rd;
-      const float b = ok ? (FWD ? W2[(int64_t)n * rd + k] : W2[(int64_t)k * C + n]) : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+      bw[i] = ok ? (FWD ? W2[(int64_t)n * rd + k] : W2[(int64_t)k * C + n]) : 0.f;
     }
+    se_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < SE_RDMAX / 4; ++i)
+      if (4 * i < rd) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Ts[li][4 * i + lk], bw[i], acc, 0, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = f0 + 4 * lk + r;
