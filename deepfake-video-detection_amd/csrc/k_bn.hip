@@ -999,7 +999,8 @@ int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw,
 //   gwr[j][c] = sum_f dz[f][j] sq[f][c],          gbr = sum_f dz      (one paired MFMA launch)
 int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
                      const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
-                     float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate) {
+                     float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate,
+                     MfmaGemm* defer2) {
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
   const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
   hipLaunchKernelGGL(se_chain_kernel<false>, grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames, C, rd,
@@ -1010,6 +1011,11 @@ int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* 
   ge.M = C; ge.N = rd; ge.K = frames; ge.asum = gbe; ge.accumulate = accumulate;
   gr.A = tmp_dz; gr.sam = 1; gr.sak = rd; gr.B = sq; gr.sbk = C; gr.sbn = 1; gr.C = gwr; gr.ldc = C;
   gr.M = rd; gr.N = C; gr.K = frames; gr.asum = gbr; gr.accumulate = accumulate;
+  if (defer2) {
+    defer2[0] = ge;
+    defer2[1] = gr;
+    return 0;
+  }
   return launch_mfma_small_gemm2(s, ge, gr);
 }
 

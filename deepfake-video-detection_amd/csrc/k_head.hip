@@ -137,14 +137,10 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(const float* __restri
 typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int MG_MAXW = 16;
 
-// two independent GEMMs of equal K may share one launch: workgroups [0, tiles0) run a0, the rest a1
-__global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a0, MfmaGemm a1, int tiles0) {
-  __shared__ float red[MG_MAXW][5][64];
-  const bool second = (int)blockIdx.x >= tiles0;
-  const MfmaGemm& a = second ? a1 : a0;
+// one 16x16 output tile of product `a` (the workgroup's waves split K)
+__device__ __forceinline__ void mg_tile(const MfmaGemm& a, int tile, float (&red)[MG_MAXW][5][64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int tn = (a.N + 15) / 16;
-  const int tile = second ? (int)blockIdx.x - tiles0 : (int)blockIdx.x;
   const int m0 = (tile / tn) * 16, n0 = (tile % tn) * 16;
   const int li = lane & 15, lk = lane >> 4;
   const int m = m0 + li, n = n0 + li;
@@ -195,6 +191,47 @@ __global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a0, Mfma
     for (int w = 0; w < nw; ++w) v += (red[w][4][lane] + red[w][4][lane + 16]) + (red[w][4][lane + 32] + red[w][4][lane + 48]);
     a.asum[m] = a.accumulate ? a.asum[m] + v : v;
   }
+}
+
+// two independent GEMMs of equal K may share one launch: workgroups [0, tiles0) run a0, the rest a1
+__global__ __launch_bounds__(1024) void mfma_small_gemm_kernel(MfmaGemm a0, MfmaGemm a1, int tiles0) {
+  __shared__ float red[MG_MAXW][5][64];
+  const bool second = (int)blockIdx.x >= tiles0;
+  mg_tile(second ? a1 : a0, second ? (int)blockIdx.x - tiles0 : (int)blockIdx.x, red);
+}
+
+// up to kMfmaBatch products of equal K in one launch: workgroups [start[k], start[k+1]) run g[k]
+struct MfmaGemmBatch {
+  MfmaGemm g[kMfmaBatch];
+  int start[kMfmaBatch + 1];
+  int n;
+};
+__global__ __launch_bounds__(1024) void mfma_small_gemm_batch_kernel(MfmaGemmBatch b) {
+  __shared__ float red[MG_MAXW][5][64];
+  int k = 0;
+  while (k + 1 < b.n && (int)blockIdx.x >= b.start[k + 1]) ++k;
+  mg_tile(b.g[k], (int)blockIdx.x - b.start[k], red);
+}
+
+int launch_mfma_small_gemm_batch(hipStream_t s, const MfmaGemm* g, int n) {
+  for (int i0 = 0; i0 < n; i0 += kMfmaBatch) {
+    MfmaGemmBatch b{};
+    int tiles = 0;
+    b.n = 0;
+    for (int i = i0; i < std::min(n, i0 + kMfmaBatch); ++i) {
+      if (g[i].K != g[i0].K) { set_error("mfma_small_gemm_batch: the products need the same K", __FILE__, __LINE__); return -1; }
+      if (g[i].M <= 0 || g[i].N <= 0) continue;
+      b.g[b.n] = g[i];
+      b.start[b.n++] = tiles;
+      tiles += cdiv(g[i].M, 16) * cdiv(g[i].N, 16);
+    }
+    b.start[b.n] = tiles;
+    if (tiles == 0) continue;
+    const int nw = std::max(1, std::min(MG_MAXW, cdiv(g[i0].K, 64)));
+    hipLaunchKernelGGL(mfma_small_gemm_batch_kernel, dim3((unsigned)tiles), dim3(64 * nw), 0, s, b);
+    DFD_HIP_CHECK(hipGetLastError());
+  }
+  return 0;
 }
 
 int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,

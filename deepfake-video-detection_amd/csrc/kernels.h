@@ -174,9 +174,13 @@ int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro,
 // SE FC backward: from dgate -> dsq (written, scaled by 1/HW into bc), grads of wr,br,we,be.
 // tmp_de: frames*C floats; tmp_dr: 2*frames*rd floats
 // (de = dgate g (1-g) from the q = 0 partials of launch_se_bn_bwd_reduce, stored to `de`)
+// defer2 != nullptr: the two weight-gradient products are returned there (MfmaGemm[2]) for a later
+// launch_mfma_small_gemm_batch instead of being launched (de and tmp_dz must then stay intact)
+struct MfmaGemm;
 int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
                      const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
-                     float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate);
+                     float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate,
+                     MfmaGemm* defer2 = nullptr);
 // SE + BN(+SiLU) backward sums in one pass over (dZ, Y): per-frame partials part[5][hsplit][frames][C] -- q = 0
 // the SE gate gradient (added by launch_se_fc_bwd), q = 1..4 the sums bn_bwd_finalize_frames combines with the
 // gate and bc (k_bn.hip)
@@ -213,6 +217,9 @@ struct MfmaGemm {
 };
 int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g);
 int launch_mfma_small_gemm2(hipStream_t s, const MfmaGemm& g0, const MfmaGemm& g1);  // one launch, same K
+// n independent products of equal K in one launch per kMaxBatch (workgroup ranges per product)
+constexpr int kMfmaBatch = 8;
+int launch_mfma_small_gemm_batch(hipStream_t s, const MfmaGemm* g, int n);
 int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk,
                            int64_t sbn, float* C, int64_t ldc, int M, int N, int K, const float* bias,
                            const float* dsilu_pre, float* asum, bool accumulate, uint64_t seed, uint32_t stream,

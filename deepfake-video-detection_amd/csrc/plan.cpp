@@ -164,6 +164,8 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
     b.o_sq = alloc(F * b.mid * 4);
     b.o_rpre = alloc(F * b.rd * 4);
     b.o_gate = alloc(F * b.mid * 4);
+    b.o_de = alloc(F * b.mid * 4);
+    b.o_dz = alloc(F * b.rd * 4);
     // below the streaming threshold conv_pwl runs on the tiled GEMMs, which would recompute the
     // BN+SiLU prologue once per N tile (forward) and per N tile of the weight gradient: the SE
     // squeeze writes the activation once instead (+1 write of the tensor)
@@ -494,6 +496,13 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
     busy = false;
     return 0;
   };
+  MfmaGemm se_jobs[2 * kMfmaBatch];
+  int n_se = 0;
+  auto flush_se = [&]() -> int {
+    const int n = n_se;
+    n_se = 0;
+    return n ? launch_mfma_small_gemm_batch(s, se_jobs, n) : 0;
+  };
   int region = 0, slab_err = 0;
   auto slab = [&]() -> float* {
     if (region == kSlabRegions) {  // every region holds a pending slab: reduce them first
@@ -544,10 +553,14 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         DFD_TRY(launch_se_bn_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                            r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), p.frames, hwo, b.mid,
                                            r.f(p.o_part), p.part_cap, &hs));
-        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_de), r.f(b.o_sq), r.f(b.o_rpre),
+        // the SE weight gradients (two small products per block, off the critical chain) are
+        // batched into one launch per segment: de / dz stay in per-block buffers until then
+        if (n_se + 2 > (int)(sizeof(se_jobs) / sizeof(se_jobs[0]))) DFD_TRY(flush_se());
+        DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(b.o_de), r.f(b.o_sq), r.f(b.o_rpre),
                                  r.prm(b.t_se_wr), r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo,
-                                 r.f(p.o_dz), r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we),
-                                 grad(b.t_se_be), acc != 0));
+                                 r.f(b.o_dz), r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we),
+                                 grad(b.t_se_be), acc != 0, se_jobs + n_se));
+        n_se += 2;
         DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid,
                                               Mout, r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd),
                                               tr != 0, grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
@@ -647,6 +660,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
       DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), r.a(p.o_ystem), r.f(p.o_coef), slab(), p.slab_cap,
                                    grad(p.t_stem), acc != 0));
     }
+    DFD_TRY(flush_se());
     DFD_TRY(defer.flush());  // this segment's weight gradients are final
     DFD_TRY(slab_err);
     region = 0;

@@ -41,6 +41,7 @@ struct Block {
   // workspace byte offsets of saved tensors
   int64_t o_y1, o_y2, o_y3, o_x, o_sq, o_rpre, o_gate;
   int64_t o_s2;  // materialised silu(bn2(y2)) for the late stages (-1: conv_pwl recomputes it)
+  int64_t o_de, o_dz;  // SE backward operands of the deferred SE weight gradients ([F][mid], [F][rd] fp32)
 };
 
 // Live timing of one launch site inside the plan (HIP events; created when armed, never on the
