@@ -145,7 +145,7 @@ __device__ __forceinline__ void mg_tile(const MfmaGemm& a, int tile, float (&red
   const int li = lane & 15, lk = lane >> 4;
   const int m = m0 + li, n = n0 + li;
   const bool mok = m < a.M, nok = n < a.N;
-  const bool drop = a.p > 0.f;
+  const bool drop = a.p > 0.f && !a.drop_c;
   const bool want_asum = a.asum != nullptr && n0 == 0;
   mf_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float as = 0.f;
@@ -182,7 +182,9 @@ __device__ __forceinline__ void mg_tile(const MfmaGemm& a, int tile, float (&red
     const int mm = m0 + 4 * lk + r, nn = n0 + li;
     if (mm >= a.M || nn >= a.N) continue;
     if (a.bias) v += a.bias[nn];
+    if (a.relu) v = fmaxf(v, 0.f);
     if (a.dsilu_pre) v *= dsiluf_(a.dsilu_pre[(int64_t)mm * a.ldc + nn]);
+    if (a.drop_c && a.p > 0.f) v *= drop_mul(a.seed, a.stream, (int64_t)mm * a.ldc + nn, a.p);
     float* c = a.C + (int64_t)mm * a.ldc + nn;
     *c = a.accumulate ? *c + v : v;
   }
@@ -543,8 +545,12 @@ int head_backward(hipStream_t s, const HeadDims& d, const HeadParams& P, const f
   // fc1: dW1 = dh1^T . drop(g) ; db1 ; dg = dh1 . W1 * drop1
   DFD_TRY(launch_mfma_small_gemm(s, w.dh1, 1, d.F1, w.g, d.D, 1, (float*)G.fc1_w, d.D, d.F1, d.D, d.B, nullptr,
                                  nullptr, (float*)G.fc1_b, false, seed, 1u, p, d.D));
-  hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)d.B * d.D)), dim3(256), 0, s, w.dh1, P.fc1_w, w.dg, d.B,
-                     d.D, d.F1, 0, seed, 1u, p);
+  {  // dg = drop1(dh1 . W1): [B][F1] x [F1][D] on fp32 MFMA, the dropout mask on the product (index b*D + i)
+    MfmaGemm g{};
+    g.A = w.dh1; g.sam = d.F1; g.sak = 1; g.B = P.fc1_w; g.sbk = d.D; g.sbn = 1; g.C = w.dg; g.ldc = d.D;
+    g.M = d.B; g.N = d.D; g.K = d.F1; g.seed = seed; g.stream = 1u; g.p = p; g.drop_c = 1;
+    DFD_TRY(launch_mfma_small_gemm(s, g));
+  }
   // attention pooling
   hipLaunchKernelGGL(attn_bwd_kernel, dim3(d.B), dim3(256), 2 * d.T * sizeof(float), s, F, w.hid, P.ta_w2, w.e,
                      scores, w.dg, dscores, d.T, d.D, d.H, d.use_attn, dF, w.dpe, w.dhid);
@@ -554,8 +560,11 @@ int head_backward(hipStream_t s, const HeadDims& d, const HeadParams& P, const f
                                    (float*)G.ta_b2, false, seed, 0u, 0.f, d.H));
     DFD_TRY(launch_mfma_small_gemm(s, w.dhid, 1, d.H, F, d.D, 1, (float*)G.ta_w1, d.D, d.H, d.D, R, nullptr, nullptr,
                                    (float*)G.ta_b1, false, seed, 0u, 0.f, d.D));
-    hipLaunchKernelGGL(linear_dgrad_kernel, dim3(nblk((int64_t)R * d.D)), dim3(256), 0, s, w.dhid, P.ta_w1, dF, R,
-                       d.D, d.H, 1, seed, 0u, 0.f);
+    // dF += dhid . W1: [R][H] x [H][D] on fp32 MFMA (the per-output dot-product loop was latency-bound)
+    MfmaGemm g{};
+    g.A = w.dhid; g.sam = d.H; g.sak = 1; g.B = P.ta_w1; g.sbk = d.D; g.sbn = 1; g.C = dF; g.ldc = d.D;
+    g.M = R; g.N = d.D; g.K = d.H; g.accumulate = 1;
+    DFD_TRY(launch_mfma_small_gemm(s, g));
   }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;

@@ -213,6 +213,8 @@ struct MfmaGemm {
   float* asum = nullptr;             // [M]
   int accumulate = 0;
   int b_silu = 0;
+  int relu = 0;    // post: max(., 0) after the bias
+  int drop_c = 0;  // the dropout (p, seed, stream) multiplies C[m][n] (index m*ldc + n) instead of B
   uint64_t seed = 0; uint32_t stream = 0; float p = 0.f; int64_t drop_ld = 0;
 };
 int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g);
