@@ -420,12 +420,19 @@ __global__ void ce_bwd_kernel(const float* __restrict__ z, const int64_t* __rest
 // ------------------------------------------------------------------ grad norm + Adam(W)
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part) {
   __shared__ double sh[256];
-  double a = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double v = g[i];
-    a += v * v;
+  // four strided elements per iteration, loads issued together, one accumulator each (fixed order)
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  const int64_t st = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * st < n; i += 4 * st) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = g[i + u * st];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] += (double)v[u] * (double)v[u];
   }
-  sh[threadIdx.x] = a;
+  for (int u = 0; i < n; i += st, ++u) a[u & 3] += (double)g[i] * (double)g[i];
+  sh[threadIdx.x] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
@@ -484,19 +491,36 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 }
 
 // ------------------------------------------------------------------ param cast (+ transpose)
+// Transposed segments go through 32x32 LDS tiles: rows read along the input's contiguous axis,
+// written along the output's (an output-indexed gather read one 4-B element per 64-B line).
 template <typename T>
 __global__ __launch_bounds__(256) void cast_params_kernel(const float* __restrict__ params, T* __restrict__ out,
                                                           const CastSeg* __restrict__ segs) {
+  __shared__ float tile[32][33];
   const CastSeg sg = segs[blockIdx.y];
   const int64_t n = (int64_t)sg.rows * sg.cols;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    if (sg.transpose) {
-      // out[c][r] = in[r][c]; i indexes the output
-      const int c = (int)(i / sg.rows), r = (int)(i % sg.rows);
-      out[sg.dst + i] = Tr<T>::from_f(params[sg.src + (int64_t)r * sg.cols + c]);
-    } else {
+  if (!sg.transpose) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
       out[sg.dst + i] = Tr<T>::from_f(params[sg.src + i]);
+    return;
+  }
+  // out[c][r] = in[r][c], in = [rows][cols]
+  const int tr = (sg.rows + 31) / 32, tc = (sg.cols + 31) / 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+    const int r0 = (t / tc) * 32, c0 = (t % tc) * 32;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = r0 + ty + 8 * k, c = c0 + tx;
+      tile[ty + 8 * k][tx] = (r < sg.rows && c < sg.cols) ? params[sg.src + (int64_t)r * sg.cols + c] : 0.f;
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c0 + ty + 8 * k, r = r0 + tx;
+      if (r < sg.rows && c < sg.cols) out[sg.dst + (int64_t)c * sg.rows + r] = Tr<T>::from_f(tile[tx][ty + 8 * k]);
+    }
+    __syncthreads();
   }
 }
 
