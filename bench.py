@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--input", default="uint8", choices=["uint8", "fp32"],
                     help="frames handed to the model: raw uint8 crops (normalised in the stem) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pw-sweep", action="store_true",
+                    help="skip the per-site timing of the 1x1-conv GEMMs (MFMA utilisation block, N = 1)")
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline: timed steps of 32 frames, all threads")
     ap.add_argument("--no-dp-exposure", action="store_true", help="skip the comm-off timing pass (N > 1)")
     ap.add_argument("--launch-check", action="store_true",
@@ -272,6 +274,10 @@ def main():
                           "frac": round(step_bytes / (ms_step / 1e3) / roofline.HBM_PEAK, 4),
                           "floor_ms": round(step_bytes / roofline.HBM_PEAK * 1e3, 3),
                           "source": "SURVEY.md §8(d) algorithmic bytes per 256-frame step"}
+        pw = None
+        if world == 1 and not args.no_pw_sweep:  # after the timed region; one extra step per site
+            pw = roofline.pointwise_sweep(model, lambda: step(x, labels), H, W, CLIPS * T, es)
+            torch.cuda.synchronize()
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_steps)
@@ -287,6 +293,7 @@ def main():
                        "global_frames": CLIPS * T * world, "image": [H, W, 3], "parallelism": f"dp{world}"},
             "loss_finite": finite,
             "roofline": rl,
+            "pointwise": pw,
             "dp": dp,
             "cpu_baseline": cpu,
         }

@@ -54,14 +54,21 @@ __device__ __forceinline__ void sg_store(float (*S)[SG_K + 1], const float (&v)[
   }
 }
 
+// K is split over blockIdx.z: slice z covers k in [z*kc, min(K, z*kc + kc)) and writes its
+// partial product to C + z*zstride (beta = 0, no bias when split).  The recurrent steps have
+// M = B = 64 rows, so without the split a (64 x 512, K = 3584) product is 8 workgroups that walk
+// 224 K-steps each; with it every step fills the chip (consumers add the slices in order).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void sgemm_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                     int ldb, float* __restrict__ C, int ldc, int M, int N, int K,
-                                                    float beta, const float* __restrict__ bias) {
+                                                    float beta, const float* __restrict__ bias, int kc,
+                                                    int64_t zstride) {
   __shared__ float As[SG_T][SG_K + 1], Bs[SG_T][SG_K + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.y * SG_T, n0 = blockIdx.x * SG_T;
   const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
+  C += (int64_t)blockIdx.z * zstride;
   f32x4_t acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -69,16 +76,16 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const float* __restrict__ A,
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float va[4], vb[4];
   bool oa[4], ob[4];
-  sg_load<TA>(A, lda, m0, 0, M, K, va, oa);
-  sg_load<TB>(B, ldb, n0, 0, N, K, vb, ob);
-  for (int k0 = 0; k0 < K; k0 += SG_K) {
+  sg_load<TA>(A, lda, m0, kb, M, ke, va, oa);
+  sg_load<TB>(B, ldb, n0, kb, N, ke, vb, ob);
+  for (int k0 = kb; k0 < ke; k0 += SG_K) {
     lds_barrier();
     sg_store<TA>(As, va, oa);
     sg_store<TB>(Bs, vb, ob);
     lds_barrier();
-    if (k0 + SG_K < K) {
-      sg_load<TA>(A, lda, m0, k0 + SG_K, M, K, va, oa);
-      sg_load<TB>(B, ldb, n0, k0 + SG_K, N, K, vb, ob);
+    if (k0 + SG_K < ke) {
+      sg_load<TA>(A, lda, m0, k0 + SG_K, M, ke, va, oa);
+      sg_load<TB>(B, ldb, n0, k0 + SG_K, N, ke, vb, ob);
     }
 #pragma unroll
     for (int s = 0; s < SG_K / 4; ++s) {
@@ -107,16 +114,46 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const float* __restrict__ A,
       }
 }
 
+static int sgemm_go(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C,
+                    int ldc, int M, int N, int K, float beta, const float* bias, int splits, int kc, int64_t zs) {
+  const dim3 grid((unsigned)cdiv(N, SG_T), (unsigned)cdiv(M, SG_T), (unsigned)splits);
+#define DFD_SG(a_, b_) \
+  hipLaunchKernelGGL((sgemm_kernel<a_, b_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias, kc, zs)
+  if (!ta && !tb) DFD_SG(false, false);
+  else if (!ta && tb) DFD_SG(false, true);
+  else if (ta && !tb) DFD_SG(true, false);
+  else DFD_SG(true, true);
+#undef DFD_SG
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int launch_sgemm(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
                  int M, int N, int K, float beta, const float* bias) {
   if (M <= 0 || N <= 0) return 0;
-  const dim3 grid((unsigned)cdiv(N, SG_T), (unsigned)cdiv(M, SG_T));
-  if (!ta && !tb) hipLaunchKernelGGL((sgemm_kernel<false, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
-  else if (!ta && tb) hipLaunchKernelGGL((sgemm_kernel<false, true>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
-  else if (ta && !tb) hipLaunchKernelGGL((sgemm_kernel<true, false>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
-  else hipLaunchKernelGGL((sgemm_kernel<true, true>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
-  DFD_HIP_CHECK(hipGetLastError());
-  return 0;
+  return sgemm_go(s, ta, tb, A, lda, B, ldb, C, ldc, M, N, K, beta, bias, 1, std::max(K, 1), 0);
+}
+
+// K slices for a product of few output tiles: aim at ~256 workgroups, at least 64 k per slice;
+// returns the slice count and (kc) the slice length, a multiple of the 16-deep K step
+int sgemm_splits(int M, int N, int K, int* kc) {
+  const int tiles = cdiv(N, SG_T) * cdiv(M, SG_T);
+  int sp = std::max(1, 256 / std::max(tiles, 1));
+  sp = std::min(std::min(sp, std::max(1, K / 64)), 64);
+  *kc = cdiv(cdiv(std::max(K, 1), sp), SG_K) * SG_K;
+  return cdiv(std::max(K, 1), *kc);
+}
+
+// part[z][M][N] = the K-slice z (k in [z*kc, z*kc + kc)) of A.B^T: fixed slice boundaries, so the
+// consumer's in-order sum over z is deterministic
+int launch_sgemm_part(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* part,
+                      int M, int N, int K, int splits, int kc) {
+  if (M <= 0 || N <= 0) return 0;
+  if (kc <= 0 || kc % SG_K || cdiv(std::max(K, 1), kc) != splits) {
+    set_error("sgemm_part: slice length/count mismatch", __FILE__, __LINE__);
+    return -1;
+  }
+  return sgemm_go(s, ta, tb, A, lda, B, ldb, part, N, M, N, K, 0.f, nullptr, splits, kc, (int64_t)M * N);
 }
 
 // ------------------------------------------------------------------ helpers
@@ -177,23 +214,40 @@ __global__ void rnn_pack_kernel(RnnLayerW w, int in, int H, int layer, float* __
   }
 }
 
+// sum_{s < n} p[s * st], added in slice order; four slices' loads are issued before their adds
+__device__ __forceinline__ float slice_sum(const float* __restrict__ p, int n, int64_t st) {
+  float v = p[0];
+  int sp = 1;
+  for (; sp + 4 <= n; sp += 4) {
+    const float a0 = p[sp * st], a1 = p[(sp + 1) * st], a2 = p[(sp + 2) * st], a3 = p[(sp + 3) * st];
+    v += a0; v += a1; v += a2; v += a3;
+  }
+  for (; sp < n; ++sp) v += p[sp * st];
+  return v;
+}
+
 // forward cell of one (step, layer) for all B rows:
-//   z[b][:] = G[b][:] (recurrent, 7H) + X0[b*T+t][:6H] (layer 0) + bias7
-// saved (row = b*T + t): ACT[row][7H] activated gates, CN, CL; outputs h' (+dropout for the
-// next layer's input), c'.
-__global__ void rnn_cell_fwd_kernel(const float* __restrict__ G, const float* __restrict__ X0, const float* __restrict__ bias7,
+//   z[b][:] = sum_s G[s][b][:] (recurrent product, K-sliced, 7H) + bias7 (+ X0[b*T+t][:6H], layer 0)
+// saved (row = b*T + t): ACT[row][7H] activated gates, CN, CL.  Outputs (each optional): h' to
+// h_out, h' (times the layer's dropout keep-scale if h2_drop) to h2_out, c' to c_out -- the
+// caller points them straight at the next consumer's rows (O, UH, CI), so no state copies.
+__global__ void rnn_cell_fwd_kernel(const float* __restrict__ G, int gsplit, int64_t gstride,
+                                    const float* __restrict__ X0, const float* __restrict__ bias7,
                                     const float* __restrict__ c_in, int c_in_ld, int B, int T, int t, int H,
                                     float* __restrict__ ACT, float* __restrict__ CN, float* __restrict__ CL,
-                                    float* __restrict__ h_out, int h_out_ld, float* __restrict__ c_out,
-                                    float* __restrict__ hd_out, float p, uint64_t seed, uint32_t stream) {
+                                    float* __restrict__ h_out, int h_ld, float* __restrict__ h2_out, int h2_ld,
+                                    int h2_drop, float* __restrict__ c_out, int c_ld, float p, uint64_t seed,
+                                    uint32_t stream) {
   const int n = B * H;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int b = i / H, j = i - b * H;
     const int64_t row = (int64_t)b * T + t;
     float z[7];
 #pragma unroll
+    for (int g = 0; g < 7; ++g) z[g] = slice_sum(G + (int64_t)b * 7 * H + g * H + j, gsplit, gstride);
+#pragma unroll
     for (int g = 0; g < 7; ++g) {
-      float v = G[(int64_t)b * 7 * H + g * H + j] + bias7[g * H + j];
+      float v = z[g] + bias7[g * H + j];
       if (X0 && g < 6) v += X0[row * 6 * H + g * H + j];
       z[g] = v;
     }
@@ -208,25 +262,31 @@ __global__ void rnn_cell_fwd_kernel(const float* __restrict__ G, const float* __
     act[4 * H + j] = gg; act[5 * H + j] = ou; act[6 * H + j] = nn;
     CN[row * H + j] = cn;
     CL[row * H + j] = cl;
-    h_out[(int64_t)b * h_out_ld + j] = h;
-    c_out[(int64_t)b * H + j] = cl;
-    if (hd_out) hd_out[(int64_t)b * H + j] = h * rnn_drop(seed, stream, row * H + j, p);
+    if (h_out) h_out[(int64_t)b * h_ld + j] = h;
+    if (h2_out) h2_out[(int64_t)b * h2_ld + j] = h2_drop ? h * rnn_drop(seed, stream, row * H + j, p) : h;
+    if (c_out) c_out[(int64_t)b * c_ld + j] = cl;
   }
 }
 
 // backward cell: from dh (gradient of h') and dc (gradient of c' = cl) -> dz (7H pre-activation
-// grads, row b*T+t) and dc_in.  dh = dh_a[b] (+ dh_b[b]) , dc = dc_a[b]
+// grads, row b*T+t) and dc_in.  dh = dh_a[b] (+ sum_s dh_b[s][b], times the layer's dropout
+// keep-scale if b_drop: the K-sliced product from the layer above), dc = dc_a[b].  dc_a and
+// dc_out may alias (each element is read, then written, by the same thread).
 __global__ void rnn_cell_bwd_kernel(const float* __restrict__ dh_a, int dh_a_ld, const float* __restrict__ dh_b,
-                                    const float* __restrict__ dc_a, const float* __restrict__ ACT,
-                                    const float* __restrict__ CN, const float* __restrict__ CL,
-                                    const float* __restrict__ c_in, int c_in_ld, int B, int T, int t, int H,
-                                    float* __restrict__ DZ, float* __restrict__ dc_in) {
+                                    int bsplit, int64_t bstride, int b_drop, float p, uint64_t seed, uint32_t stream,
+                                    const float* dc_a, const float* __restrict__ ACT, const float* __restrict__ CN,
+                                    const float* __restrict__ CL, const float* __restrict__ c_in, int c_in_ld, int B,
+                                    int T, int t, int H, float* __restrict__ DZ, float* dc_out) {
   const int n = B * H;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     const int b = i / H, j = i - b * H;
     const int64_t row = (int64_t)b * T + t;
     float dh = dh_a ? dh_a[(int64_t)b * dh_a_ld + j] : 0.f;
-    if (dh_b) dh += dh_b[(int64_t)b * H + j];
+    if (dh_b) {
+      float v = slice_sum(dh_b + i, bsplit, bstride);
+      if (b_drop) v *= rnn_drop(seed, stream, row * H + j, p);
+      dh += v;
+    }
     const float dcl0 = dc_a ? dc_a[(int64_t)b * H + j] : 0.f;
     const float* act = ACT + row * 7 * H;
     const float a = act[0 * H + j], o_ = act[1 * H + j], f = act[2 * H + j], ii = act[3 * H + j];
@@ -246,27 +306,8 @@ __global__ void rnn_cell_bwd_kernel(const float* __restrict__ dh_a, int dh_a_ld,
     dz[4 * H + j] = dg * (1.f - gg * gg);
     dz[5 * H + j] = dou * ou * (1.f - ou);
     dz[6 * H + j] = dnn * (1.f - nn * nn);
-    dc_in[(int64_t)b * H + j] = dcn * f;
+    dc_out[(int64_t)b * H + j] = dcn * f;
   }
-}
-
-// dh *= dropout scale (the inter-layer dropout of RNNModel.py:113-114)
-__global__ void rnn_drop_bwd_kernel(float* __restrict__ dh, int B, int T, int t, int H, float p, uint64_t seed,
-                                    uint32_t stream) {
-  const int n = B * H;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const int b = i / H, j = i - b * H;
-    dh[i] *= rnn_drop(seed, stream, ((int64_t)b * T + t) * H + j, p);
-  }
-}
-
-// colsum[n] (+)= sum_m X[m][n]   (bias gradients), one thread per column, fixed row order
-__global__ void rnn_colsum_kernel(const float* __restrict__ X, int M, int N, int ld, float* __restrict__ out, int acc) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
-  float a = 0.f;
-  for (int m = 0; m < M; ++m) a += X[(int64_t)m * ld + n];
-  out[n] = acc ? out[n] + a : a;
 }
 
 // scatter packed gradients back into the per-gate weight gradients of layer l (accumulating)
@@ -358,25 +399,37 @@ __global__ void rnn_cls_fwd_kernel(float* __restrict__ h1, const float* __restri
 }
 
 // backward of the tail: dy -> dz = dy*y*(1-y) ; dw2 = sum_b dz*h1d ; db2 ; dh1 = dz*w2*drop*relu'
-__global__ void rnn_cls_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y, const float* __restrict__ h1,
-                                   const float* __restrict__ w2, int B, int H, float p, uint64_t seed,
-                                   float* __restrict__ dh1, float* __restrict__ gw2, float* __restrict__ gb2) {
-  // one thread per hidden unit j (and b loop) for gw2; dh1 per (b, j)
-  const int j = blockIdx.x * 256 + threadIdx.x;
+// 1024 threads = 64 hidden units x 16 clip lanes; lane bl takes clips bl, bl+16, ... in order and
+// the 16 partial sums of dw2 are added in lane order (deterministic)
+__global__ __launch_bounds__(1024) void rnn_cls_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                           const float* __restrict__ h1, const float* __restrict__ w2,
+                                                           int B, int H, float p, uint64_t seed,
+                                                           float* __restrict__ dh1, float* __restrict__ gw2,
+                                                           float* __restrict__ gb2) {
+  __shared__ float sh[16][64];
+  const int cl = threadIdx.x & 63, bl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  float a = 0.f;
   if (j < H) {
-    float a = 0.f;
-    for (int b = 0; b < B; ++b) {
+    for (int b = bl; b < B; b += 16) {
       const float dz = dy[b] * y[b] * (1.f - y[b]);
       const float d = rnn_drop(seed, 9u, (int64_t)b * H + j, p);
-      a += dz * h1[(int64_t)b * H + j] * d;
-      dh1[(int64_t)b * H + j] = h1[(int64_t)b * H + j] > 0.f ? dz * w2[j] * d : 0.f;
+      const float hv = h1[(int64_t)b * H + j];
+      a += dz * hv * d;
+      dh1[(int64_t)b * H + j] = hv > 0.f ? dz * w2[j] * d : 0.f;
     }
-    gw2[j] = a;
+  }
+  sh[bl][cl] = a;
+  __syncthreads();
+  if (bl == 0 && j < H) {
+    float v = 0.f;
+    for (int l = 0; l < 16; ++l) v += sh[l][cl];
+    gw2[j] = v;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float a = 0.f;
-    for (int b = 0; b < B; ++b) a += dy[b] * y[b] * (1.f - y[b]);
-    gb2[0] = a;
+    float v = 0.f;
+    for (int b = 0; b < B; ++b) v += dy[b] * y[b] * (1.f - y[b]);
+    gb2[0] = v;
   }
 }
 
@@ -419,19 +472,35 @@ __global__ void rnn_attn_bwd_kernel(const float* __restrict__ Om, const float* _
     }
   }
 }
-// gw2[j] = sum_{b,t} ds[b][t] * E[b][t][j] ; gb2 = sum ds
-__global__ void rnn_attn_w2_kernel(const float* __restrict__ E, const float* __restrict__ ds, int BT, int H,
-                                   float* __restrict__ gw2, float* __restrict__ gb2) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j < H) {
-    float a = 0.f;
-    for (int r = 0; r < BT; ++r) a += ds[r] * E[(int64_t)r * H + j];
-    gw2[j] = a;
+// gw2[j] = sum_{b,t} ds[b][t] * E[b][t][j] ; gb2 = sum ds.  1024 threads = 64 columns x 16 row
+// lanes (lane rl takes rows rl, rl+16, ... in order; lanes added in order: deterministic)
+__global__ __launch_bounds__(1024) void rnn_attn_w2_kernel(const float* __restrict__ E, const float* __restrict__ ds,
+                                                           int BT, int H, float* __restrict__ gw2,
+                                                           float* __restrict__ gb2) {
+  __shared__ float sh[16][64];
+  __shared__ float sb[1024];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  float a = 0.f;
+  if (j < H)
+    for (int r = rl; r < BT; r += 16) a += ds[r] * E[(int64_t)r * H + j];
+  sh[rl][cl] = a;
+  __syncthreads();
+  if (rl == 0 && j < H) {
+    float v = 0.f;
+    for (int l = 0; l < 16; ++l) v += sh[l][cl];
+    gw2[j] = v;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float a = 0.f;
-    for (int r = 0; r < BT; ++r) a += ds[r];
-    gb2[0] = a;
+  if (blockIdx.x == 0) {  // uniform per block
+    float v = 0.f;
+    for (int r = threadIdx.x; r < BT; r += 1024) v += ds[r];
+    sb[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) sb[threadIdx.x] += sb[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) gb2[0] = sb[0];
   }
 }
 // dO = (dOm_ctx + dOm_att) * mask   (in place into dOm)
@@ -449,46 +518,39 @@ __global__ void rnn_mask_bwd_kernel(float* __restrict__ dOm, const float* __rest
 static int ew_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 2048)); }
 
 // ------------------------------------------------------------------ host orchestration
-int64_t rnn_work_floats(const RnnDims& d) {
-  const int64_t BT = (int64_t)d.B * d.T, H = d.H;
-  int64_t n = 0;
-  n += BT * d.IN;                          // xs (sorted input)
-  n += BT * 6 * H;                         // X0 (layer-0 x projection)
-  n += (int64_t)d.B * 7 * H;               // G (one step's recurrent gates)
-  n += (int64_t)d.L * (7 * H * H + 7 * H); // packed weights + biases per layer
-  n += 6 * H * d.IN;                       // WX0
-  n += (int64_t)d.L * BT * (7 * H + 4 * H); // per layer ACT, CN, CL, UH (hidden input), CI (c input)
-  n += BT * H * 3;                         // O (outputs), Om, E
-  n += BT * 2 + (int64_t)d.B * H * 3 + d.B; // att, (spare), ctx, h1, spare, y
-  n += (int64_t)d.B * H * 4;               // h/c state ping-pong
-  return n + 64;
-}
+// K slices of the per-step recurrent products (fixed per shape; the workspace holds them)
+static int fwd_splits(const RnnDims& d, int* kc) { return sgemm_splits(d.B, 7 * d.H, d.H, kc); }
+static int bwd_splits(const RnnDims& d, int* kc) { return sgemm_splits(d.B, d.H, 7 * d.H, kc); }
 
 struct RnnWs {
   float *xs, *X0, *G, *P[8], *bias7[8], *WX0, *ACT[8], *CN[8], *CL[8], *UH[8], *CI[8], *O, *Om, *E, *att, *ctx, *h1,
-      *y, *st;
+      *y;
+  int64_t floats;  // extent of the layout (rnn_work_floats)
 };
+// one layout function for both the size query (w = nullptr) and the pointers
 static RnnWs rnn_ws(const RnnDims& d, float* w) {
   RnnWs s{};
   const int64_t BT = (int64_t)d.B * d.T, H = d.H;
-  float* p = w;
-  auto take = [&](int64_t n) { float* r = p; p += (n + 63) & ~int64_t(63); return r; };
-  s.xs = take(BT * d.IN);
-  s.X0 = take(BT * 6 * H);
-  s.G = take((int64_t)d.B * 7 * H);
+  int64_t off = 0;
+  auto take = [&](int64_t n) { float* r = w ? w + off : nullptr; off += (n + 63) & ~int64_t(63); return r; };
+  int kc;
+  s.xs = take(BT * d.IN);                        // sorted input
+  s.X0 = take(BT * 6 * H);                       // layer-0 x projection, all rows
+  s.G = take((int64_t)fwd_splits(d, &kc) * d.B * 7 * H);  // one step's recurrent product, K slices
   for (int l = 0; l < d.L; ++l) { s.P[l] = take(7 * H * H); s.bias7[l] = take(7 * H); }
   s.WX0 = take(6 * H * d.IN);
-  for (int l = 0; l < d.L; ++l) {
+  for (int l = 0; l < d.L; ++l) {  // saved: gates, c', cl, hidden input, c input (rows b*T+t)
     s.ACT[l] = take(BT * 7 * H); s.CN[l] = take(BT * H); s.CL[l] = take(BT * H); s.UH[l] = take(BT * H);
     s.CI[l] = take(BT * H);
   }
   s.O = take(BT * H); s.Om = take(BT * H); s.E = take(BT * H);
-  s.att = take(BT); take(BT);
-  s.ctx = take((int64_t)d.B * H); s.h1 = take((int64_t)d.B * H); take((int64_t)d.B * H);
+  s.att = take(BT);
+  s.ctx = take((int64_t)d.B * H); s.h1 = take((int64_t)d.B * H);
   s.y = take(d.B);
-  s.st = take((int64_t)d.B * H * 4);
+  s.floats = off;
   return s;
 }
+int64_t rnn_work_floats(const RnnDims& d) { return rnn_ws(d, nullptr).floats; }
 
 int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,
                 const int64_t* lens, float* work, float* y, uint64_t seed, float p) {
@@ -508,39 +570,37 @@ int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float
   DFD_HIP_CHECK(hipGetLastError());
   // layer-0 x projection for all rows (b*T + t)
   DFD_TRY(launch_sgemm(s, false, false, xs, IN, w.WX0, IN, w.X0, 6 * H, (int)BT, 6 * H, IN, 0.f, nullptr));
-  float* h = w.st;                       // [B][H] state of the last layer, previous step
-  float* c = w.st + (int64_t)B * H;
-  float* hd = w.st + 2LL * B * H;        // dropped-out inter-layer h
-  float* ctmp = w.st + 3LL * B * H;
-  DFD_HIP_CHECK(hipMemsetAsync(h, 0, sizeof(float) * 2 * B * H, s));
+  // Every step's hidden/cell inputs live in the saved UH/CI rows (row b*T+t, ld T*H): the cell
+  // kernels write their outputs there directly.  Step 0 of layer 0 starts from h = c = 0.
+  const int64_t ldr = (int64_t)T * H;
+  DFD_HIP_CHECK(hipMemset2DAsync(w.UH[0], (size_t)ldr * 4, 0, (size_t)H * 4, B, s));
+  DFD_HIP_CHECK(hipMemset2DAsync(w.CI[0], (size_t)ldr * 4, 0, (size_t)H * 4, B, s));
+  int kc;
+  const int sf = fwd_splits(d, &kc);
   const int eb = ew_blocks((int64_t)B * H);
   for (int t = 0; t < T; ++t) {
     for (int l = 0; l < d.L; ++l) {
-      const float* hin = l == 0 ? h : hd;      // layer input hidden (== x for l >= 1)
-      const float* cin = l == 0 ? c : ctmp;
-      // save inputs for backward (row b*T+t)
-      DFD_HIP_CHECK(hipMemcpy2DAsync(w.UH[l] + (int64_t)t * H, (size_t)T * H * 4, hin, (size_t)H * 4, (size_t)H * 4, B,
-                                     hipMemcpyDeviceToDevice, s));
-      DFD_HIP_CHECK(hipMemcpy2DAsync(w.CI[l] + (int64_t)t * H, (size_t)T * H * 4, cin, (size_t)H * 4, (size_t)H * 4, B,
-                                     hipMemcpyDeviceToDevice, s));
-      DFD_TRY(launch_sgemm(s, false, false, hin, H, w.P[l], H, w.G, 7 * H, B, 7 * H, H, 0.f, nullptr));
+      // recurrent product h_in @ P_l^T in K slices (summed by the cell kernel)
+      DFD_TRY(launch_sgemm_part(s, false, false, w.UH[l] + (int64_t)t * H, (int)ldr, w.P[l], H, w.G, B, 7 * H, H, sf,
+                                kc));
       const bool last = l == d.L - 1;
-      // outputs: last layer -> O[b][t] (ld T*H) and state h (copied below); others -> hd (dropout)
+      const float* cin = w.CI[l] + (int64_t)t * H;
       if (last) {
-        hipLaunchKernelGGL(rnn_cell_fwd_kernel, dim3(eb), dim3(256), 0, s, w.G, l == 0 ? w.X0 : nullptr, w.bias7[l], cin,
-                           H, B, T, t, H, w.ACT[l], w.CN[l], w.CL[l], w.O + (int64_t)t * H, T * H, ctmp, nullptr, p,
-                           seed, (uint32_t)l);
+        // h' -> O[b][t] and the next step's layer-0 hidden input; c' -> its cell input
+        const bool more = t + 1 < T;
+        hipLaunchKernelGGL(rnn_cell_fwd_kernel, dim3(eb), dim3(256), 0, s, w.G, sf, (int64_t)B * 7 * H,
+                           l == 0 ? w.X0 : nullptr, w.bias7[l], cin, (int)ldr, B, T, t, H, w.ACT[l], w.CN[l], w.CL[l],
+                           w.O + (int64_t)t * H, (int)ldr, more ? w.UH[0] + (int64_t)(t + 1) * H : nullptr, (int)ldr,
+                           0, more ? w.CI[0] + (int64_t)(t + 1) * H : nullptr, (int)ldr, p, seed, (uint32_t)l);
       } else {
-        // raw h' of a non-last layer is only consumed through dropout (hd); c' -> ctmp
-        hipLaunchKernelGGL(rnn_cell_fwd_kernel, dim3(eb), dim3(256), 0, s, w.G, l == 0 ? w.X0 : nullptr, w.bias7[l], cin,
-                           H, B, T, t, H, w.ACT[l], w.CN[l], w.CL[l], w.h1, H, ctmp, hd, p, seed, (uint32_t)l);
+        // dropout(h') is both x and h of layer l+1 (RNNModel.py:113-114); c' its cell input
+        hipLaunchKernelGGL(rnn_cell_fwd_kernel, dim3(eb), dim3(256), 0, s, w.G, sf, (int64_t)B * 7 * H,
+                           l == 0 ? w.X0 : nullptr, w.bias7[l], cin, (int)ldr, B, T, t, H, w.ACT[l], w.CN[l], w.CL[l],
+                           nullptr, 0, w.UH[l + 1] + (int64_t)t * H, (int)ldr, 1, w.CI[l + 1] + (int64_t)t * H,
+                           (int)ldr, p, seed, (uint32_t)l);
       }
       DFD_HIP_CHECK(hipGetLastError());
     }
-    // state for the next step = last layer's (h', c')
-    DFD_HIP_CHECK(hipMemcpy2DAsync(h, (size_t)H * 4, w.O + (int64_t)t * H, (size_t)T * H * 4, (size_t)H * 4, B,
-                                   hipMemcpyDeviceToDevice, s));
-    DFD_HIP_CHECK(hipMemcpyAsync(c, ctmp, sizeof(float) * B * H, hipMemcpyDeviceToDevice, s));
   }
   // mask, attention, classifier
   hipLaunchKernelGGL(rnn_mask_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, w.O, lens, w.Om, B, T, H);
@@ -565,6 +625,8 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   //                 DZ per layer [BT][7H], dP [7H][H], dWX0 [6H][IN], dbias [7H], dh/dc state
   float* q = scratch;
   auto take = [&](int64_t n) { float* r = q; q += (n + 63) & ~int64_t(63); return r; };
+  int kc;
+  const int sb = bwd_splits(d, &kc);
   float* dh1 = take((int64_t)B * H);
   float* dctx = take((int64_t)B * H);
   float* dE = take(BT * H);
@@ -576,53 +638,45 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   float* dP = take((int64_t)7 * H * H);
   float* dWX0 = take((int64_t)6 * H * IN);
   float* dbias = take(7 * H);
-  float* dh = take((int64_t)B * H);      // gradient into the last layer's h' of the current step
-  float* dc = take((int64_t)B * H);      // gradient into the last layer's c'
-  float* dhl = take((int64_t)B * H);     // gradient into an inner layer's output (through dropout)
-  float* dcl = take((int64_t)B * H);
-  float* dcin = take((int64_t)B * H);
+  float* dhs = take((int64_t)sb * B * H);   // K slices: gradient into the last layer's h' of step t-1
+  float* dhls = take((int64_t)sb * B * H);  // K slices: gradient into an inner layer's output
+  float* dc = take((int64_t)B * H);         // gradient into the last layer's c'
+  float* dcl = take((int64_t)B * H);        // gradient into an inner layer's c'
   // classifier tail
-  const dim3 gH((unsigned)cdiv(H, 256));
-  hipLaunchKernelGGL(rnn_cls_bwd_kernel, gH, dim3(256), 0, s, dy, w.y, w.h1, P.cls_w2, B, H, p, seed, dh1, Gr.cls_w2,
-                     Gr.cls_b2);
+  const dim3 gH((unsigned)cdiv(H, 256)), gH64((unsigned)cdiv(H, 64));
+  hipLaunchKernelGGL(rnn_cls_bwd_kernel, gH64, dim3(1024), 0, s, dy, w.y, w.h1, P.cls_w2, B, H, p, seed, dh1,
+                     Gr.cls_w2, Gr.cls_b2);
   DFD_TRY(launch_sgemm(s, true, true, dh1, H, w.ctx, H, Gr.cls_w1, H, H, H, B, 0.f, nullptr));   // dW1 = dh1^T ctx
-  hipLaunchKernelGGL(rnn_colsum_kernel, gH, dim3(256), 0, s, dh1, B, H, H, Gr.cls_b1, 0);
+  DFD_TRY(launch_reduce_slabs(s, dh1, B, H, Gr.cls_b1, false));
   DFD_TRY(launch_sgemm(s, false, true, dh1, H, P.cls_w1, H, dctx, H, B, H, H, 0.f, nullptr));     // dctx = dh1 W1
   // attention
   hipLaunchKernelGGL(rnn_attn_bwd_kernel, dim3(B), dim3(256), 2 * T * sizeof(float), s, w.Om, w.E, w.att, dctx,
                      P.att_w2, T, H, dOm, dE, ds);
-  hipLaunchKernelGGL(rnn_attn_w2_kernel, gH, dim3(256), 0, s, w.E, ds, (int)BT, H, Gr.att_w2, Gr.att_b2);
+  hipLaunchKernelGGL(rnn_attn_w2_kernel, gH64, dim3(1024), 0, s, w.E, ds, (int)BT, H, Gr.att_w2, Gr.att_b2);
   DFD_TRY(launch_sgemm(s, true, true, dE, H, w.Om, H, Gr.att_w1, H, H, H, (int)BT, 0.f, nullptr));  // dWa1 = dE^T Om
-  hipLaunchKernelGGL(rnn_colsum_kernel, gH, dim3(256), 0, s, dE, (int)BT, H, H, Gr.att_b1, 0);
+  DFD_TRY(launch_reduce_slabs(s, dE, (int)BT, H, Gr.att_b1, false));
   DFD_TRY(launch_sgemm(s, false, true, dE, H, P.att_w1, H, dOm2, H, (int)BT, H, H, 0.f, nullptr));  // dOm2 = dE Wa1
   hipLaunchKernelGGL(rnn_mask_bwd_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, dOm, dOm2, lens, B, T, H);
   DFD_HIP_CHECK(hipGetLastError());
-  // BPTT
-  DFD_HIP_CHECK(hipMemsetAsync(dh, 0, sizeof(float) * B * H, s));
-  DFD_HIP_CHECK(hipMemsetAsync(dc, 0, sizeof(float) * B * H, s));
+  // BPTT.  The recurrent products into h are K-sliced (dhs/dhls) and summed by the consuming
+  // cell kernel; the c gradients are updated in place (dc for the last layer, dcl inside).
+  const int64_t ldr = (int64_t)T * H, slab = (int64_t)B * H;
   const int eb = ew_blocks((int64_t)B * H);
   for (int t = T - 1; t >= 0; --t) {
     for (int l = d.L - 1; l >= 0; --l) {
       const bool last = l == d.L - 1;
-      // gradient of this layer's h' and c'
-      const float* gh_a = last ? dOm + (int64_t)t * H : dhl;
-      const int gh_ld = last ? T * H : H;
-      const float* gh_b = last ? dh : nullptr;
-      const float* gc = last ? dc : dcl;
-      hipLaunchKernelGGL(rnn_cell_bwd_kernel, dim3(eb), dim3(256), 0, s, gh_a, gh_ld, gh_b, gc, w.ACT[l], w.CN[l],
-                         w.CL[l], w.CI[l] + (int64_t)t * H, T * H, B, T, t, H, DZ[l], dcin);
+      const bool first = t == T - 1;  // nothing flows back from step T yet
+      const float* gh_a = last ? dOm + (int64_t)t * H : nullptr;
+      const float* gh_b = last ? (first ? nullptr : dhs) : dhls;
+      const float* gc = last ? (first ? nullptr : dc) : dcl;
+      hipLaunchKernelGGL(rnn_cell_bwd_kernel, dim3(eb), dim3(256), 0, s, gh_a, (int)ldr, gh_b, sb, slab, last ? 0 : 1,
+                         p, seed, (uint32_t)l, gc, w.ACT[l], w.CN[l], w.CL[l], w.CI[l] + (int64_t)t * H, (int)ldr, B,
+                         T, t, H, DZ[l], l > 0 ? dcl : dc);
       DFD_HIP_CHECK(hipGetLastError());
-      // gradient into the layer's hidden input: dz (rows b*T+t) @ P_l
-      float* dst = l == 0 ? dh : dhl;
-      DFD_TRY(launch_sgemm(s, false, true, DZ[l] + (int64_t)t * 7 * H, T * 7 * H, w.P[l], H, dst, H, B, H, 7 * H, 0.f,
-                           nullptr));
-      if (l > 0) {
-        // into layer l-1's output through the inter-layer dropout; its c' gradient = dc_in
-        hipLaunchKernelGGL(rnn_drop_bwd_kernel, dim3(eb), dim3(256), 0, s, dhl, B, T, t, H, p, seed, (uint32_t)(l - 1));
-        DFD_HIP_CHECK(hipMemcpyAsync(dcl, dcin, sizeof(float) * B * H, hipMemcpyDeviceToDevice, s));
-      } else {
-        DFD_HIP_CHECK(hipMemcpyAsync(dc, dcin, sizeof(float) * B * H, hipMemcpyDeviceToDevice, s));
-      }
+      // gradient into the layer's hidden input: dz (rows b*T+t) @ P_l (none needed into step 0's h = 0)
+      if (l > 0 || t > 0)
+        DFD_TRY(launch_sgemm_part(s, false, true, DZ[l] + (int64_t)t * 7 * H, T * 7 * H, w.P[l], H, l == 0 ? dhs : dhls,
+                                  B, H, 7 * H, sb, kc));
     }
   }
   // weight gradients, one GEMM per layer over all B*T rows
@@ -632,8 +686,7 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
     if (l == 0)
       DFD_TRY(launch_sgemm(s, true, true, DZ[0], 7 * H, order ? w.xs : x, IN, dWX0, IN, 6 * H, IN, (int)BT, 0.f,
                            nullptr));
-    hipLaunchKernelGGL(rnn_colsum_kernel, dim3((unsigned)cdiv(7 * H, 256)), dim3(256), 0, s, DZ[l], (int)BT, 7 * H,
-                       7 * H, dbias, 0);
+    DFD_TRY(launch_reduce_slabs(s, DZ[l], (int)BT, 7 * H, dbias, false));
     hipLaunchKernelGGL(rnn_scatter_kernel, dim3(ew_blocks((int64_t)6 * H * (IN + H) + (int64_t)H * H + 7 * H)),
                        dim3(256), 0, s, Gr.layer[l], l == 0 ? IN : H, H, l, dP, dWX0, dbias);
     DFD_HIP_CHECK(hipGetLastError());
@@ -685,9 +738,9 @@ int attn_backward(hipStream_t s, const float* O, const float* E, const float* at
   const dim3 gH((unsigned)cdiv(H, 256));
   hipLaunchKernelGGL(rnn_attn_bwd_kernel, dim3(B), dim3(256), 2 * T * sizeof(float), s, O, E, att, dctx, w2, T, H, dO,
                      dE, ds);
-  hipLaunchKernelGGL(rnn_attn_w2_kernel, gH, dim3(256), 0, s, E, ds, (int)BT, H, gw2, gb2);
+  hipLaunchKernelGGL(rnn_attn_w2_kernel, dim3((unsigned)cdiv(H, 64)), dim3(1024), 0, s, E, ds, (int)BT, H, gw2, gb2);
   DFD_TRY(launch_sgemm(s, true, true, dE, H, O, H, gw1, H, H, H, (int)BT, 0.f, nullptr));
-  hipLaunchKernelGGL(rnn_colsum_kernel, gH, dim3(256), 0, s, dE, (int)BT, H, H, gb1, 0);
+  DFD_TRY(launch_reduce_slabs(s, dE, (int)BT, H, gb1, false));
   DFD_TRY(launch_sgemm(s, false, true, dE, H, w1, H, dO2, H, (int)BT, H, H, 0.f, nullptr));
   hipLaunchKernelGGL(rnn_mask_bwd_kernel, dim3(ew_blocks(BT * H)), dim3(256), 0, s, dO, dO2, (const int64_t*)nullptr,
                      B, T, H);
@@ -695,15 +748,18 @@ int attn_backward(hipStream_t s, const float* O, const float* E, const float* at
   return 0;
 }
 int colsum(hipStream_t s, const float* X, int M, int N, int ld, float* out) {
-  hipLaunchKernelGGL(rnn_colsum_kernel, dim3((unsigned)cdiv(N, 256)), dim3(256), 0, s, X, M, N, ld, out, 0);
-  DFD_HIP_CHECK(hipGetLastError());
-  return 0;
+  return launch_reduce_slabs_strided(s, X, M, N, ld, out, false);
 }
 
-int64_t rnn_scratch_floats(const RnnDims& d) {
+int64_t rnn_scratch_floats(const RnnDims& d) {  // the takes of rnn_backward, padded the same way
   const int64_t BT = (int64_t)d.B * d.T, H = d.H;
-  return 64 * 20 + (int64_t)d.B * H * 7 + BT * H * 3 + BT + (int64_t)d.L * BT * 7 * H + 7 * H * H + 6 * H * d.IN +
-         7 * H;
+  int kc;
+  const int64_t sb = bwd_splits(d, &kc);
+  const int64_t sizes[] = {d.B * H, d.B * H, BT * H, BT * H, BT * H, BT, 7 * H * H, 6 * H * d.IN, 7 * H,
+                           sb * d.B * H, sb * d.B * H, d.B * H, d.B * H};
+  int64_t n = d.L * ((BT * 7 * H + 63) & ~int64_t(63));
+  for (int64_t v : sizes) n += (v + 63) & ~int64_t(63);
+  return n;
 }
 
 }  // namespace dfd

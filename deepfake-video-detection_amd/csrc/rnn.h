@@ -24,6 +24,11 @@ struct RnnDims {
 
 int launch_sgemm(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
                  int M, int N, int K, float beta, const float* bias);
+// K-sliced form for products with few output tiles: sgemm_splits picks the slice count and
+// length (kc); launch_sgemm_part writes part[z][M][N], the consumer sums z = 0.. in order
+int sgemm_splits(int M, int N, int K, int* kc);
+int launch_sgemm_part(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* part,
+                      int M, int N, int K, int splits, int kc);
 int64_t rnn_work_floats(const RnnDims& d);
 int64_t rnn_scratch_floats(const RnnDims& d);
 int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float* x, const int64_t* order,

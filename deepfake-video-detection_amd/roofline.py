@@ -122,3 +122,47 @@ class KernelProbe:
                 "frac": round(achieved / (HBM_PEAK / 1e9), 4), "traffic": traffic,
                 "kernel": f"{self.kind} blocks.{self.stage}.{self.block}", "algorithmic_bytes": nbytes,
                 "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(self.ms)}
+
+
+PW_KINDS = ("pw_fwd", "pw_dgrad", "pw_wgrad", "pwl_fwd", "pwl_dgrad", "pwl_wgrad")
+
+
+def pointwise_sweep(model, step, H: int, W: int, frames: int, es: int):
+    """MFMA utilisation of the 1x1-conv GEMMs (north star: "MFMA utilisation on the pointwise kernels
+    against the MI355X roofline"): every pointwise launch site of the 16 MBConv blocks (expansion and
+    projection; forward, data and weight gradient) is timed with HIP events over one extra training
+    step each, and summed: FLOPs 2*M*N*K and algorithmic bytes per launch (``algorithmic``) against
+    the dense bf16 MFMA peak and the HBM peak.  The arithmetic intensity of these shapes (K, N <=
+    1152) sits far below the ridge point (peak FLOP/s / peak B/s = 312 FLOP/B), so they are
+    HBM-bound by construction and the MFMA fraction is reported as evidence of that, not as a target
+    they can reach.  The conv_head 1x1 (320 -> 1280 at 7x7) is not a block site and is left out."""
+    sites = []
+    for (st, bi), g in block_geometry(H, W).items():
+        for kind in PW_KINDS:
+            if kind.startswith("pw_") and g["mid"] == g["cin"]:
+                continue  # blocks.0.0 has no expansion conv
+            sites.append((kind, st, bi))
+    rows, tot_s, tot_f, tot_b = [], 0.0, 0, 0
+    for kind, st, bi in sites:
+        p = KernelProbe(model, kind, st, bi)
+        p.arm(4)
+        step()
+        p.disarm()
+        if not p.ms:
+            continue
+        t = sum(p.ms) / len(p.ms) / 1e3
+        nb, fl = algorithmic(kind, st, bi, frames, H, W, es)
+        rows.append({"site": f"{kind} blocks.{st}.{bi}", "us": round(t * 1e6, 2),
+                     "tflops": round(fl / t / 1e12, 2), "hbm_frac": round(nb / t / HBM_PEAK, 3)})
+        tot_s += t
+        tot_f += fl
+        tot_b += nb
+    if not rows:
+        return None
+    best = max(rows, key=lambda r: r["tflops"])
+    return {"launch_sites": len(rows), "gpu_us_per_step": round(tot_s * 1e6, 1), "flops_per_step": tot_f,
+            "algorithmic_bytes_per_step": tot_b, "achieved_tflops": round(tot_f / tot_s / 1e12, 2),
+            "mfma_peak_tflops": MFMA_BF16_PEAK / 1e12, "mfma_frac": round(tot_f / tot_s / MFMA_BF16_PEAK, 4),
+            "hbm_frac": round(tot_b / tot_s / HBM_PEAK, 4), "arith_intensity": round(tot_f / tot_b, 1),
+            "ridge_flop_per_byte": round(MFMA_BF16_PEAK / HBM_PEAK, 1), "bound": "hbm",
+            "best_site": best, "sites": rows}

@@ -47,3 +47,30 @@ def test_probe_fused_dw_bwd_bytes():
     by, fl = R.algorithmic("dw_bwd", 1, 0, 256, 224, 224, 2)
     assert by == 2 * (2 * 256 * 112 * 112 * 96 + 2 * 256 * 56 * 56 * 96) + 8 * 9 * 96
     assert fl == 4 * 256 * 56 * 56 * 96 * 9
+
+
+def test_pointwise_sweep_sites_and_totals(monkeypatch):
+    """The MFMA-utilisation sweep visits every 1x1 launch site once (93 = 16 blocks x 6 kinds minus
+    blocks.0.0's missing expansion) and sums FLOPs / bytes / time consistently (fake probe, no GPU)."""
+    armed, steps = [], []
+
+    class FakeProbe:
+        def __init__(self, model, kind, stage, block):
+            self.site = (kind, stage, block)
+            self.ms = []
+
+        def arm(self, n):
+            armed.append(self.site)
+
+        def disarm(self):
+            self.ms = [0.010]  # 10 us per launch
+
+    monkeypatch.setattr(R, "KernelProbe", FakeProbe)
+    out = R.pointwise_sweep(None, lambda: steps.append(1), 224, 224, 256, 2)
+    assert len(armed) == len(set(armed)) == 93 == out["launch_sites"] == len(steps)
+    assert all(k.startswith(("pw_", "pwl_")) for k, _, _ in armed)
+    fl = sum(R.algorithmic(k, s, b, 256, 224, 224, 2)[1] for k, s, b in armed)
+    assert out["flops_per_step"] == fl
+    assert out["gpu_us_per_step"] == pytest.approx(930.0)
+    assert out["mfma_frac"] == pytest.approx(fl / 930e-6 / R.MFMA_BF16_PEAK, rel=1e-3)
+    assert out["arith_intensity"] < out["ridge_flop_per_byte"]  # HBM-bound shapes

@@ -16,5 +16,5 @@ while [ $# -ge 2 ]; do
     objs=$(echo "$objs" | grep -v "/$src.o$")
     objs="$objs var/${src}_$name.o"
   done
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -o var/kbench_$name kbench.o $objs
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -o var/kbench_$name kbench.o $objs -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib
 done
