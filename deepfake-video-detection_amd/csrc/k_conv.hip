@@ -18,6 +18,22 @@ namespace dfd {
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 constexpr int CG_T = 64, CG_K = 16;
 
+// Division by a launch-invariant divisor without the ~30-instruction integer division: q = x / d
+// for every 32-bit x as (mulhi(x, m) + x) >> l with l = ceil(log2 d), m = 2^32 (2^l - d) / d + 1
+// (round-up multiplier, 33-bit intermediate).  The gathers below divide pixel and k indices by map
+// sizes and channel counts on every element of every k-step (the wgrad B gather: two per element).
+struct FDiv {
+  uint32_t m, l;
+};
+static FDiv fdiv_make(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  return FDiv{(uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d + 1) & 0xffffffffu), l};
+}
+__device__ __forceinline__ int fdiv(int x, FDiv f) {
+  return (int)((((uint64_t)__umulhi((uint32_t)x, f.m)) + (uint32_t)x) >> f.l);
+}
+
 // ------------------------------------------------------------------ operand policies
 // load(): the thread's 4 elements of the (64 rows x 16 k) tile at (r0, k0) into v / ok.
 // kR == false: element e = tid + 256 i -> (r = e / 16, k = e % 16)   (contiguous along k)
@@ -57,6 +73,7 @@ struct OpConvA {
   const float* x;
   int64_t sn, sy, sx, sc;  // element strides of the source (n, y, x, c)
   int H, W, C, KW, S, P, Ho, Wo, R, K;
+  FDiv fC, fKW, fHW, fWo;  // set by the launcher (fdiv_make)
   int iy0[4], ix0[4];
   int64_t base[4];
   static constexpr bool kR = false;
@@ -65,7 +82,7 @@ struct OpConvA {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = min(r0 + (tid + 256 * i) / CG_K, R - 1);
-      const int hw = Ho * Wo, n = r / hw, q = r - n * hw, oy = q / Wo, ox = q - oy * Wo;
+      const int hw = Ho * Wo, n = fdiv(r, fHW), q = r - n * hw, oy = fdiv(q, fWo), ox = q - oy * Wo;
       iy0[i] = oy * S - P;
       ix0[i] = ox * S - P;
       base[i] = (int64_t)n * sn;
@@ -74,7 +91,7 @@ struct OpConvA {
   __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
     const int tid = threadIdx.x;
     const int k = k0 + (tid & 15);
-    const int tap = k / C, ci = k - tap * C, ky = tap / KW, kx = tap - ky * KW;
+    const int tap = fdiv(k, fC), ci = k - tap * C, ky = fdiv(tap, fKW), kx = tap - ky * KW;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + (tid + 256 * i) / CG_K;
@@ -89,6 +106,7 @@ struct OpConvA {
 struct OpConvDgradA {
   const float* dy;
   int Ho, Wo, Co, KW, P, H, W, R, K;
+  FDiv fCo, fKW, fHW, fW;  // set by the launcher (fdiv_make)
   int iy[4], ix[4];
   int64_t base[4];
   static constexpr bool kR = false;
@@ -97,16 +115,16 @@ struct OpConvDgradA {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = min(r0 + (tid + 256 * i) / CG_K, R - 1);
-      const int hw = H * W, n = r / hw, q = r - n * hw;
-      iy[i] = q / W + P;
-      ix[i] = q - (q / W) * W + P;
+      const int hw = H * W, n = fdiv(r, fHW), q = r - n * hw;
+      iy[i] = fdiv(q, fW) + P;
+      ix[i] = q - fdiv(q, fW) * W + P;
       base[i] = (int64_t)n * Ho * Wo * Co;
     }
   }
   __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
     const int tid = threadIdx.x;
     const int k = k0 + (tid & 15);
-    const int tap = k / Co, co = k - tap * Co, ky = tap / KW, kx = tap - ky * KW;
+    const int tap = fdiv(k, fCo), co = k - tap * Co, ky = fdiv(tap, fKW), kx = tap - ky * KW;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + (tid + 256 * i) / CG_K;
@@ -121,6 +139,7 @@ struct OpConvBT {
   const float* x;
   int64_t sn, sy, sx, sc;
   int H, W, C, KW, S, P, Ho, Wo, R /* = KH*KW*C */, K /* = M */;
+  FDiv fHW, fWo;  // set by the launcher (fdiv_make)
   int ky, kx, ci;
   bool jok;
   static constexpr bool kR = true;
@@ -138,7 +157,7 @@ struct OpConvBT {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + (tid >> 6) + 4 * i;
-      const int hw = Ho * Wo, n = m / hw, q = m - n * hw, oy = q / Wo, ox = q - oy * Wo;
+      const int hw = Ho * Wo, n = fdiv(m, fHW), q = m - n * hw, oy = fdiv(q, fWo), ox = q - oy * Wo;
       const int iy = oy * S - P + ky, ix = ox * S - P + kx;
       ok[i] = jok && m < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
       v[i] = *(ok[i] ? x + (int64_t)n * sn + iy * sy + ix * sx + ci * sc : x);
@@ -159,12 +178,16 @@ __device__ __forceinline__ void cg_store(float (*S)[CG_K + 1], const float (&v)[
 
 enum { CEPI_STORE = 0, CEPI_STATS = 1, CEPI_SLAB = 2 };
 
-// C[m][n] = sum_k A(m,k) B(n,k) (+ bias[n]); grid.x = n-tiles * m-tiles (n fastest), grid.y = k splits
+// C[m][n] = sum_k A(m,k) B(n,k) (+ bias[n]); grid.x = n-tiles * m-tiles (n fastest), grid.y = k splits.
+// Main loop: 32-deep k-steps (two 16-deep halves per operand policy load) through two LDS stages --
+// the next step's gathers are in flight while this step's MFMAs run, and one barrier per step
+// (four per 32 k in the single-buffered form) hands the stages over.  The MFMA sequence over k is
+// unchanged (exact fp32 products, same order).
 template <class PA, class PB, int EPI>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __restrict__ C, int ldc, int M, int N,
                                                         int K, int ksplit, const float* __restrict__ bias,
                                                         float* __restrict__ stats) {
-  __shared__ float As[CG_T][CG_K + 1], Bs[CG_T][CG_K + 1];
+  __shared__ float As[2][2][CG_T][CG_K + 1], Bs[2][2][CG_T][CG_K + 1];  // [stage][half]
   __shared__ float red[2][2][CG_T];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (N + CG_T - 1) / CG_T;
@@ -179,39 +202,62 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float va[4], vb[4];
-  bool oa[4], ob[4];
+  float va[2][4], vb[2][4];
+  bool oa[2][4], ob[2][4];
+  // gathers of the 32-deep step at k0 (a half past ke loads nothing)
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kh = k0 + h * CG_K;
+      if (kh < ke) {
+        pa.load(m0, kh, va[h], oa[h]);
+        pb.load(n0, kh, vb[h], ob[h]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { oa[h][i] = false; ob[h][i] = false; }
+      }
+    }
+  };
+  // registers -> LDS stage st; elements past ke belong to the next split: zero
+  auto commit = [&](int st, int k0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kh = k0 + h * CG_K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int e = tid + 256 * i;
+        const int ka = kh + (PA::kR ? e / CG_T : e % CG_K), kbb = kh + (PB::kR ? e / CG_T : e % CG_K);
+        oa[h][i] = oa[h][i] && ka < ke;
+        ob[h][i] = ob[h][i] && kbb < ke;
+      }
+      cg_store<PA::kR>(As[st][h], va[h], oa[h]);
+      cg_store<PB::kR>(Bs[st][h], vb[h], ob[h]);
+    }
+  };
   if (kb < ke) {
-    pa.load(m0, kb, va, oa);
-    pb.load(n0, kb, vb, ob);
+    fetch(kb);
+    commit(0, kb);
   }
-  for (int k0 = kb; k0 < ke; k0 += CG_K) {
-    lds_barrier();
-    // elements past ke belong to the next split: mask them
+  lds_barrier();
+  int cur = 0;
+  for (int k0 = kb; k0 < ke; k0 += 2 * CG_K) {
+    const bool more = k0 + 2 * CG_K < ke;
+    if (more) fetch(k0 + 2 * CG_K);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i;
-      const int ka = k0 + (PA::kR ? e / CG_T : e % CG_K), kbb = k0 + (PB::kR ? e / CG_T : e % CG_K);
-      oa[i] = oa[i] && ka < ke;
-      ob[i] = ob[i] && kbb < ke;
-    }
-    cg_store<PA::kR>(As, va, oa);
-    cg_store<PB::kR>(Bs, vb, ob);
-    lds_barrier();
-    if (k0 + CG_K < ke) {
-      pa.load(m0, k0 + CG_K, va, oa);
-      pb.load(n0, k0 + CG_K, vb, ob);
-    }
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int s = 0; s < CG_K / 4; ++s) {
-      const int kk = 4 * s + (lane >> 4);
-      const float a0 = As[wm + (lane & 15)][kk], a1 = As[wm + 16 + (lane & 15)][kk];
-      const float b0 = Bs[wn + (lane & 15)][kk], b1 = Bs[wn + 16 + (lane & 15)][kk];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
+      for (int s = 0; s < CG_K / 4; ++s) {
+        const int kk = 4 * s + (lane >> 4);
+        const float a0 = As[cur][h][wm + (lane & 15)][kk], a1 = As[cur][h][wm + 16 + (lane & 15)][kk];
+        const float b0 = Bs[cur][h][wn + (lane & 15)][kk], b1 = Bs[cur][h][wn + 16 + (lane & 15)][kk];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    if (more) commit(cur ^ 1, k0 + 2 * CG_K);
+    lds_barrier();
+    cur ^= 1;
   }
   float* Cz = EPI == CEPI_SLAB ? C + (int64_t)blockIdx.y * M * N : C;
   float cs[2] = {0.f, 0.f}, cq[2] = {0.f, 0.f};
@@ -385,6 +431,7 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
                      (float*)nullptr);
   const int M = g.N * g.Ho * g.Wo, K = KK * g.Ci;
   OpConvA pa{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, M, K};
+  pa.fC = fdiv_make(g.Ci); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.Ho * g.Wo); pa.fWo = fdiv_make(g.Wo);
   OpRows pb{wf, K, g.Co, K};
   if (stat_rows) *stat_rows = cdiv(M, CG_T);
   return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats);
@@ -397,6 +444,7 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
                      wd);
   const int M = g.N * g.H * g.W, K = KK * g.Co;
   OpConvDgradA pa{dY, g.Ho, g.Wo, g.Co, g.KW, g.P, g.H, g.W, M, K};
+  pa.fCo = fdiv_make(g.Co); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.H * g.W); pa.fW = fdiv_make(g.W);
   OpRows pb{wd, K, g.Ci, K};
   return conv_gemm<OpConvDgradA, OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr);
 }
@@ -411,6 +459,7 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
   splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / per));
   OpCols pa{dY, g.Co, g.Co, M};
   OpConvBT pb{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, Kp, M};
+  pb.fHW = fdiv_make(g.Ho * g.Wo); pb.fWo = fdiv_make(g.Wo);
   const int ksplit = cdiv(cdiv(M, splits), CG_K) * CG_K;
   const int used = cdiv(M, ksplit);
   DFD_TRY((conv_gemm<OpCols, OpConvBT, CEPI_SLAB>(s, pa, pb, slab, Kp, g.Co, Kp, M, splits, nullptr, nullptr)));
