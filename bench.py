@@ -48,6 +48,9 @@ def parse():
                     help="skip the per-site timing of the 1x1-conv GEMMs (MFMA utilisation block, N = 1)")
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU baseline: timed steps of 32 frames, all threads")
     ap.add_argument("--no-dp-exposure", action="store_true", help="skip the comm-off timing pass (N > 1)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend of the N-rank path (nccl = RCCL over xGMI; gloo only for the "
+                         "1-GPU rehearsal with DFD_BENCH_DEVICE=0)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher/rendezvous self-test on CPU (gloo): ranks report and exit, no GPU use")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
@@ -197,10 +200,15 @@ def main():
     from deepfake_amd.trainer import DataParallelTrainer
     from deepfake_amd.weights import deterministic_init_
 
-    dev = torch.device("cuda", local)
+    # DFD_BENCH_DEVICE pins every rank to one device: the 1-GPU rehearsal of the N-rank path
+    # (--backend gloo, since RCCL refuses two ranks on one device); never set by the driver
+    dev = torch.device("cuda", int(os.environ.get("DFD_BENCH_DEVICE", local)))
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     if args.tune:
         from deepfake_amd import _lib
