@@ -639,11 +639,27 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                                      b.mid, PRO_NONE, Pro{}, nullptr, nullptr)));
           // the weight gradient through the BN on w: g (o_ge1), x, the BN1 coefficients (o_coef1)
           DFD_TRY(fork(p.ev[2]));
-          PROBED_ON(PK_PW_WGRAD, &b, w, (launch_pw_wgrad<T>(w, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
-                                                            slab(), p.slab_cap, r.f(p.o_tg), false)));
-          DFD_TRY(launch_pw_wgrad<T>(w, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, slab(), p.slab_cap,
-                                     r.f(p.o_gram), false));
-          DFD_TRY(launch_col_sums<T>(w, xin, Min, b.cin, r.f(p.o_stats2), p.stats_cap, r.f(p.o_cs)));
+          {
+            // the three partial products' slab reductions (into o_tg, o_gram, o_cs) run as ONE
+            // batched launch before the combine reads them
+            float* const parts[3] = {r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs)};
+            const int64_t extent[3] = {(int64_t)b.mid * b.cin, (int64_t)b.cin * b.cin, (int64_t)b.cin};
+            SlabDefer loc{};
+            loc.stream = w;
+            loc.lo = parts[0];
+            loc.hi = parts[0] + extent[0];
+            for (int q = 1; q < 3; ++q) {
+              loc.lo = std::min<const float*>(loc.lo, parts[q]);
+              loc.hi = std::max<const float*>(loc.hi, parts[q] + extent[q]);
+            }
+            const DeferScope inner{set_slab_defer(&loc)};  // the segment's defer again on exit
+            PROBED_ON(PK_PW_WGRAD, &b, w, (launch_pw_wgrad<T>(w, r.a(p.o_ge1), xin, Min, b.mid, b.cin, PRO_NONE, Pro{},
+                                                              slab(), p.slab_cap, parts[0], false)));
+            DFD_TRY(launch_pw_wgrad<T>(w, xin, xin, Min, b.cin, b.cin, PRO_NONE, Pro{}, slab(), p.slab_cap, parts[1],
+                                       false));
+            DFD_TRY(launch_col_sums<T>(w, xin, Min, b.cin, r.f(p.o_stats2), p.stats_cap, parts[2]));
+            DFD_TRY(loc.flush());
+          }
           DFD_TRY(launch_pw_wgrad_bn_combine(w, r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs), r.prm(b.pw.t_w),
                                              r.f(p.o_coef1), b.mid, b.cin, grad(b.pw.t_w), acc != 0));
           DFD_TRY(mark(p.ev[3], ge1_busy));
