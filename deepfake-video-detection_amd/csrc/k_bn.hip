@@ -12,7 +12,9 @@ namespace dfd {
 
 // ------------------------------------------------------------------ partial-row reduction
 // Sums rows of a [rows][2][C] slab for channels [blockIdx.x*16, +16) in fp64:
-// 1024 threads = 16 channels x 64 row lanes, then a fixed-order LDS tree (deterministic).
+// 1024 threads = 16 channels x 64 row lanes; the 4 row lanes of a wave are added by two shuffles,
+// the 16 waves by threads 0..15 in wave order (deterministic; one barrier instead of a 6-level
+// LDS tree).  Valid in threads 0..15 (channel tid).
 constexpr int FIN_CH = 16;
 constexpr int FIN_RL = 64;
 
@@ -39,18 +41,25 @@ __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int 
       b += stats[((int64_t)r * 2 + 1) * C + c];
     }
   }
-  sh_s[tid] = a;
-  sh_q[tid] = b;
-  __syncthreads();
-  for (int o = FIN_RL / 2; o > 0; o >>= 1) {
-    if (rl < o) {
-      sh_s[tid] += sh_s[tid + o * FIN_CH];
-      sh_q[tid] += sh_q[tid + o * FIN_CH];
-    }
-    __syncthreads();
+  // lanes l, l^16, l^32, l^48 of a wave hold the same channel
+  a += __shfl_xor(a, 16, 64);
+  b += __shfl_xor(b, 16, 64);
+  a += __shfl_xor(a, 32, 64);
+  b += __shfl_xor(b, 32, 64);
+  const int wave = tid >> 6;
+  if ((tid & 63) < FIN_CH) {
+    sh_s[wave * FIN_CH + cl] = a;
+    sh_q[wave * FIN_CH + cl] = b;
   }
-  s = sh_s[cl];
-  q = sh_q[cl];
+  __syncthreads();
+  s = 0.0;
+  q = 0.0;
+  if (tid < FIN_CH) {
+    for (int w = 0; w < 1024 / 64; ++w) {
+      s += sh_s[w * FIN_CH + tid];
+      q += sh_q[w * FIN_CH + tid];
+    }
+  }
 }
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
@@ -58,7 +67,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
                                                            const float* __restrict__ beta, float* run_mean,
                                                            float* run_var, float momentum, float eps, int training,
                                                            float* mean, float* invstd, float* scale, float* shift) {
-  __shared__ double sh_s[1024], sh_q[1024];
+  __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
   double s = 0.0, q = 0.0;
   if (training) reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
                                                               const float* __restrict__ invstd, int training,
                                                               float* dgamma, float* dbeta, int accumulate,
                                                               float* coef) {
-  __shared__ double sh_s[1024], sh_q[1024];
+  __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
   double s = 0.0, q = 0.0;
   reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
