@@ -37,7 +37,15 @@ struct GemmCfg {
   static constexpr int RB = BM / WM / 16, CB = BN / WN / 16;
   static constexpr int VPR = BK / 8, RPP = 256 / VPR;       // 8-vectors per row, rows per staging pass
   static constexpr int PA = BM / RPP, PB = BN / RPP;        // 8-vectors per thread per k-step
-  static constexpr int AS = sizeof(T) == 2 ? BK + 8 : BK + 4;  // LDS row stride (elements) of A/B tiles
+  // LDS row stride (elements) of the A/B tiles.  bf16: unpadded rows whose 16-B chunks are XOR-
+  // swizzled by row group (lds_off), so both the staging stores (rows x chunks of one k-step) and
+  // the MFMA fragment reads (16 rows, one chunk) hit 16 distinct 4-bank groups; fp32: padded rows.
+  static constexpr int AS = sizeof(T) == 2 ? BK : BK + 4;
+  static constexpr int CPR = BK / 8;                         // 16-B chunks per bf16 row (4, 8, 16)
+  __device__ __forceinline__ static int lds_off(int row, int k) {  // element offset of (row, k), k % 8 == 0
+    if constexpr (sizeof(T) == 2) return row * AS + (((k >> 3) ^ ((row / (16 / CPR)) & (CPR - 1))) << 3);
+    else return row * AS + k;
+  }
   static constexpr int CS = sizeof(T) == 2 ? BN + 8 : BN + 4;    // LDS row stride of the C tile
   static constexpr int AB_BYTES = (BM + BN) * AS * (int)sizeof(T);
   static constexpr int C_BYTES = BM * CS * (int)sizeof(T);
@@ -149,19 +157,19 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
         for (int i = 0; i < PA; ++i) {
           const int row = srow + G::RPP * i;
           if constexpr (MODE == PRO_NONE) {
-            raw_st(As + row * G::AS + skc, ra[d][i]);
+            raw_st(As + G::lds_off(row, skc), ra[d][i]);
           } else if constexpr (MODE == PRO_GELU) {
             float x[8];
             raw_to_f(ra[d][i], x);
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);  // masked lanes hold 0 and gelu(0) = 0
-            lds_st8(As + row * G::AS + skc, x);
+            lds_st8(As + G::lds_off(row, skc), x);
           } else if constexpr (MODE == PRO_GATE) {
             float x[8];
             raw_to_f(ra[d][i], x);  // masked lanes hold 0
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] *= pg[d][i][j];
-            lds_st8(As + row * G::AS + skc, x);
+            lds_st8(As + G::lds_off(row, skc), x);
           } else {
             float x[8], psc[8], psh[8];
             raw_to_f(ra[d][i], x);
@@ -178,11 +186,11 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
             const bool ok = m0 + row < M && k0 + skc < K;
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] = ok ? x[j] : 0.f;
-            lds_st8(As + row * G::AS + skc, x);
+            lds_st8(As + G::lds_off(row, skc), x);
           }
         }
 #pragma unroll
-        for (int i = 0; i < PB; ++i) raw_st(Bs + (srow + G::RPP * i) * G::AS + skc, rb[d][i]);
+        for (int i = 0; i < PB; ++i) raw_st(Bs + G::lds_off(srow + G::RPP * i, skc), rb[d][i]);
         lds_barrier();
         if (k + D < nk) load(dc, m0, k + D);
         // ---- MFMA (partial N tiles are zero padded: the sequence is unconditional) ----
@@ -192,12 +200,12 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
             bf16x8_t af[RB];
 #pragma unroll
             for (int r_ = 0; r_ < RB; ++r_)
-              af[r_] = *reinterpret_cast<const bf16x8_t*>(As + (rbase + r_ * 16 + (lane & 15)) * G::AS + ks * 32 +
-                                                         8 * (lane >> 4));
+              af[r_] = *reinterpret_cast<const bf16x8_t*>(
+                  As + G::lds_off(rbase + r_ * 16 + (lane & 15), ks * 32 + 8 * (lane >> 4)));
 #pragma unroll
             for (int cb = 0; cb < CB; ++cb) {
               const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(
-                  Bs + (cbase + cb * 16 + (lane & 15)) * G::AS + ks * 32 + 8 * (lane >> 4));
+                  Bs + G::lds_off(cbase + cb * 16 + (lane & 15), ks * 32 + 8 * (lane >> 4)));
 #pragma unroll
               for (int r_ = 0; r_ < RB; ++r_)
                 acc[r_][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[r_], bfr, acc[r_][cb], 0, 0, 0);
