@@ -179,6 +179,9 @@ class IncompatibleCheckpoint(RuntimeError):
     pass
 
 
+SUPPORTED_BACKBONES = ("efficientnet_b0", "resnet50")  # PretrainedBackboneDetector's implemented trunks
+
+
 def read_checkpoint(path_or_obj, map_location="cpu"):
     if isinstance(path_or_obj, (str, Path)):
         return torch.load(str(path_or_obj), map_location=map_location, weights_only=True)
@@ -208,6 +211,12 @@ def load_pretrained(path_or_obj, device=None, compute_dtype="fp32", checkpoint_n
     base = {"model_type": "pretrained"}
     if not (isinstance(sd, dict) and sd):
         raise IncompatibleCheckpoint("No state_dict found")
+    if backbone not in SUPPORTED_BACKBONES:
+        # app.load_model builds the timm/torchvision model and fails the match-ratio gate; the MI355X
+        # path has no kernels for it: report it the same way (IncompatibleCheckpoint, with the stats)
+        stats = {"backbone": backbone, "keys": len(sd), **base}
+        raise IncompatibleCheckpoint(f"Unsupported backbone for the MI355X path: {backbone} "
+                                     f"(supported: {', '.join(SUPPORTED_BACKBONES)}); stats={stats}")
     model = PretrainedBackboneDetector(backbone_name=backbone, pretrained=False, num_classes=2, dropout_rate=0.5,
                                        use_temporal_attention=True, compute_dtype=compute_dtype)
     stats = load_stats(model, sd)

@@ -203,6 +203,26 @@ int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* off, int64_t*
   return 0;
 }
 
+int dfd_b0_grad_tensor(const dfd_b0_plan* plan, int block, int64_t* off, int64_t* rows, int64_t* cols) {
+  if (!plan || !off || !rows || !cols) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  const dfd::Plan& p = plan->p;
+  const int nb = (int)p.blocks.size();
+  if (block < 1 || block > nb) { dfd::set_error("grad tensor: block out of range", __FILE__, __LINE__); return -1; }
+  const int64_t F = p.frames;
+  // backward_impl: block i writes the gradient of its input into o_gx[(i - 1) & 1]; the head
+  // segment writes the gradient of the last block's output into o_gx[(nb - 1) & 1]
+  *off = p.o_gx[(block - 1) & 1];
+  if (block == nb) {
+    *rows = F * p.Hf * p.Wf;
+    *cols = p.head.cin;
+  } else {
+    const auto& b = p.blocks[block];
+    *rows = F * b.hin * b.win;
+    *cols = b.cin;
+  }
+  return 0;
+}
+
 int dfd_b0_segment_tensors(int seg, int* lo, int* hi) {
   if (seg < 0 || seg >= dfd::kNumSegments || !lo || !hi) {
     dfd::set_error("bad segment", __FILE__, __LINE__);

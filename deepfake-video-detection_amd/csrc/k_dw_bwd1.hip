@@ -290,6 +290,9 @@ static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
 bool dw_bwd1_covers(const DwGeom& g) {
   if (g.s != 1 || (g.k != 3 && g.k != 5) || g.pad != g.k / 2 || g.Ho != g.H || g.Wo != g.W) return false;
   if (!dw_bwd1_enabled()) return false;
+  // channel-pair accesses; 32-bit byte offsets within the tile's frames (FR <= 2; fp32 bound for
+  // both dtypes) -- checked here so the caller falls back to the split path instead of failing
+  if (g.C % 2 || (int64_t)g.H * g.W * g.C * 8 >= (1ll << 32)) return false;
   if (g.H == 7 && g.W == 7) return true;  // two stacked frames per tile
   if (g.k == 3) return (g.H % 8 == 0 && g.W % 28 == 0) || (g.H % 14 == 0 && g.W % 14 == 0);
   return g.H % 14 == 0 && g.W % 14 == 0;
@@ -302,9 +305,6 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
                    const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
                    bool accumulate) {
   if (!dw_bwd1_covers(g)) return 1;
-  // 32-bit byte offsets within the tile's frames (FR <= 2; fp32 bound for both dtypes)
-  if ((int64_t)g.H * g.W * g.C * 8 >= (1ll << 32)) return 1;
-  if (g.C % 2) return 1;                                  // channel-pair accesses
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   const int H = g.H, W = g.W;
   if (H == 7 && W == 7) {

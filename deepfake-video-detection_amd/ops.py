@@ -63,7 +63,8 @@ def _(frames, plan, params, buffers, norm, training, momentum):
     return frames.new_empty(frames.shape[0], FEATURE_DIM, dtype=torch.float32), frames.new_empty(n, dtype=torch.uint8)
 
 
-@torch.library.custom_op("dfd::b0_trunk_backward", mutates_args=("grads",), device_types="cuda")
+# workspace: the backward reuses its scratch regions (activation gradients, BN/SE partials, slabs)
+@torch.library.custom_op("dfd::b0_trunk_backward", mutates_args=("workspace", "grads"), device_types="cuda")
 def b0_trunk_backward(frames: Tensor, plan: int, dfeat: Tensor, params: Tensor, workspace: Tensor, grads: Tensor,
                       norm: List[float], training: bool, seg_begin: int, seg_end: int, accumulate: bool) -> None:
     """Backward of trunk segments [seg_begin, seg_end) (output side first) into the flat ``grads``."""
@@ -137,7 +138,8 @@ weighted_cross_entropy.register_autograd(_ce_backward, setup_context=_ce_setup)
 
 
 # ---------------------------------------------------------------- optimizer
-@torch.library.custom_op("dfd::grad_norm", mutates_args=("out",), device_types="cuda")
+# scratch: the kernel's fixed-order partial sums (written); out: [norm, clip coefficient]
+@torch.library.custom_op("dfd::grad_norm", mutates_args=("scratch", "out"), device_types="cuda")
 def grad_norm(grads: Tensor, max_norm: float, scratch: Tensor, out: Tensor) -> None:
     """out[0] = ||grads||_2 (fp64 accumulation, fixed order), out[1] = clip coefficient
     min(1, max_norm / (norm + 1e-6)) -- clip_grad_norm_ (torch/nn/utils/clip_grad.py)."""
@@ -150,7 +152,10 @@ def _(grads, max_norm, scratch, out):
     return None
 
 
-@torch.library.custom_op("dfd::adam_step", mutates_args=("params", "exp_avg", "exp_avg_sq"), device_types="cuda")
+# grads: with `clip` the kernel writes the clipped gradient back (FusedAdam leaves it in .grad, as
+# clip_grad_norm_ does in place)
+@torch.library.custom_op("dfd::adam_step", mutates_args=("params", "grads", "exp_avg", "exp_avg_sq"),
+                         device_types="cuda")
 def adam_step(params: Tensor, grads: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, lr: float, beta1: float,
               beta2: float, eps: float, weight_decay: float, step: int, grad_scale: float, decoupled: bool,
               clip: Optional[Tensor]) -> None:

@@ -77,7 +77,11 @@ def collate_clips(batch, max_frames=16, image_size=(224, 224), device="cuda", ou
     """Device collate of ``[{'faces': uint8 (M,H,W,3), 'label': ...}]`` -> ``(x (B,T,3,H,W), labels)``.
 
     ``out="float"``: fp32 ``v / 255`` (exactly ``collate_batch_cnn_lstm``'s tensor, channels-last
-    strides); ``out="uint8"``: the raw crops (for the B0 detector, normalised in its stem)."""
+    strides); ``out="uint8"``: the raw crops, for a B0 detector that normalises them in its stem.
+    Which normalisation the stem applies is the DETECTOR's ``input_normalization``: the reference
+    TRAINING feed is ``/255`` only (src/train.py:59), so a training model fed these uint8 batches must
+    be built with ``input_normalization="unit"`` to see the reference trainer's tensor; the default
+    ``"imagenet"`` is the serving feed (app.py:2084-2085)."""
     dev = torch.device(device)
     if dev.type != "cuda":
         raise _lib.DFDError("collate_clips runs on a HIP device; the MI355X path has no CPU fallback")

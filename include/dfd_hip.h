@@ -97,6 +97,13 @@ DFD_API int dfd_b0_segment_count(void);
  * Returns -1 past the end.  Used by the layer-by-layer parity tests. */
 DFD_API int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* byte_offset, int64_t* rows,
                                 int64_t* cols);
+/* Introspection of a backward's activation gradient (NHWC [rows][cols], plan dtype): the gradient
+ * w.r.t. the INPUT of MBConv block `block` (1..nblocks-1, flat block order), or for block =
+ * nblocks w.r.t. the last block's output (the conv_head input).  Valid right after the backward
+ * segment that contains that block (the head segment for block = nblocks) and before the next
+ * segment runs: the buffers are reused.  Used by the per-stage parity tests. */
+DFD_API int dfd_b0_grad_tensor(const dfd_b0_plan* plan, int block, int64_t* byte_offset, int64_t* rows,
+                               int64_t* cols);
 /* Tensor index range [*lo, *hi) whose gradients are final after segment `seg`. */
 DFD_API int dfd_b0_segment_tensors(int seg, int* lo, int* hi);
 

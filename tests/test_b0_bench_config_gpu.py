@@ -1,0 +1,460 @@
+"""Parity at the bench's OWN configuration: 32 clips x 8 frames x 224x224 (256 frames), uint8 crops
+normalised in the stem, default kernel selection -- exactly the launches behind the headline number.
+
+Kernel selection depends on the row count M = frames x H x W, so the smaller parity batches
+(``test_b0_224_gpu.py``: 2 and 32 frames) do not reach every launch configuration the 256-frame
+step runs: the 14x14-stage 1x1 GEMMs take the 64x64 tile (cfg 2, ``k_gemm.hip`` gemm_tiles) at
+M = 50,176 instead of the 32x64 tile, the persistent-grid cap and the weight-gradient M-split /
+slab counts change (``launch_pw_wgrad``), the streaming 1x1 kernels cover more layers, and every
+depthwise kernel (``dw_fwd1``, ``dw_fwd``, ``dw_bwd1``, ``dw_bwd2``, ``dw_bwd``) runs its full
+persistent grid.  Three checks:
+
+1. **fp32 step** (HIP fp32 storage, exact fp32 MFMA) against the oracle ``DetectorCPU``
+   (``oracle/detector_cpu.py``: the reference's ``PretrainedBackboneDetector`` head around the timm-B0
+   restatement) run as plain PyTorch fp32 on the GPU -- test infrastructure only; cuDNN/MIOpen off,
+   so torch's own native conv / BN kernels compute it (no JIT).  Reference step:
+   ``model(images)`` -> ``CrossEntropyLoss(weight)`` -> ``backward`` (``src/ensemble_trainer.py:188-198``).
+   North-star tolerance: logits / frame scores / loss rtol 1e-3 atol 1e-5; every gradient norm
+   within 1e-3 and its 64 leading elements within rtol 1e-3; BN running stats rtol 1e-4.
+2. **bf16 step** (the bench's dtype) against the same fp32 oracle: loss within 2 %, and the
+   gradient bound of ``test_b0_224_gpu.py`` for the 32-frame batch (90 % of the tensors within 10 %
+   in norm and cosine >= 0.98, every tensor cosine >= 0.85).
+3. **bf16, layer by layer** (what a fault confined to a few channels of one layer cannot escape):
+   every conv of the forward is recomputed in fp32 torch from the HIP run's OWN bf16 inputs
+   (saved in the workspace, ``dfd_b0_saved_tensor``) and compared PER CHANNEL; the backward runs
+   segment by segment and each stage's backward is recomputed in fp32 torch (autograd through the
+   oracle's blocks) from the HIP's bf16 stage input and the HIP's gradient at the stage output
+   (``dfd_b0_grad_tensor``), comparing the gradient at the stage input and every parameter
+   gradient of the stage -- the depthwise weight gradients per channel.  Bounds are stated at
+   ``FWD_CH_TOL`` / ``BWD_*`` below (bf16 storage rounding is 2^-9 relative per element).
+
+Trunk numerics are "parity unpinned" at the timm boundary (timm is absent); the head
+and step recipe are pinned by the reference goldens (``test_oracle_golden.py``).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deepfake_amd import _lib
+from deepfake_amd.pretrained_detector import PretrainedBackboneDetector
+from deepfake_amd.weights import deterministic_init_
+from oracle import b0_cpu
+from oracle.detector_cpu import DetectorCPU
+
+pytestmark = pytest.mark.gpu
+
+B, T, HW = 32, 8, 224
+N = B * T
+SEED = 33
+CLASS_W = torch.tensor([0.7, 1.3])
+MEAN = (0.485, 0.456, 0.406)
+STD = (0.229, 0.224, 0.225)
+EPS = 1e-5
+
+# bf16 layer-by-layer bounds: per-channel relative L2 error of a conv output recomputed from the
+# kernel's own bf16 inputs (output rounding 2^-9 + the bf16 rounding of the 1x1 GEMMs' A operand)
+FWD_CH_TOL = 1e-2  # measured worst 3.2e-3 (conv_pwl of stages 5-6)
+# per-stage backward: relative L2 error of the stage-input gradient and of each parameter gradient
+# (the recompute keeps fp32 intermediates where the HIP step stores bf16 ones), and the minimum
+# cosine of every depthwise-weight-gradient channel
+BWD_REL_TOL = 5e-2  # measured worst 2.6e-2 (blocks.1.0 SE reduce, BN1 gamma, stem)
+BWD_DW_CH_COS = 0.98
+# The last BN of every block (bn3, the DS block's bn2) has no activation and its output reaches the
+# loss only through 1x1 convs into TRAINING-mode BatchNorms (directly or along the residual chain):
+# a per-channel shift there is annihilated, so its bias gradient is structurally zero and both sides
+# hold rounding residue only -- judged against the stage's gradient scale instead.
+STRUCT_ZERO_TOL = 5e-3
+
+_CACHE = {}
+
+
+def _u8_frames():
+    g = torch.Generator().manual_seed(5)
+    return torch.randint(0, 256, (B, T, HW, HW, 3), generator=g, dtype=torch.uint8)
+
+
+def _labels():
+    return torch.tensor([(i * 7 + 1) % 2 for i in range(B)])
+
+
+def _normalised(u8, device):
+    """app.py:2084-2085: .float()/255 then ImageNet mean/std; (B,T,3,H,W) with channels-last strides."""
+    x = u8.to(device).float() / 255.0
+    x = (x - torch.tensor(MEAN, device=device)) / torch.tensor(STD, device=device)
+    return x.permute(0, 1, 4, 2, 3)
+
+
+def _gpu_oracle(cuda):
+    """fp32 DetectorCPU step on the GPU (plain torch, cuDNN/MIOpen disabled), cached."""
+    if "oracle" not in _CACHE:
+        with torch.backends.cudnn.flags(enabled=False):
+            m = DetectorCPU(dropout_rate=0.0)
+            deterministic_init_(m, seed=SEED)
+            m = m.to(cuda).train()
+            x = _normalised(_u8_frames(), cuda)
+            logits, scores = m(x)
+            loss = F.cross_entropy(logits, _labels().to(cuda), weight=CLASS_W.to(cuda))
+            loss.backward()
+            torch.cuda.synchronize()
+            _CACHE["oracle"] = dict(
+                logits=logits.detach().cpu(), scores=scores.detach().cpu(), loss=float(loss),
+                grads={n: p.grad.detach().cpu() for n, p in m.named_parameters()},
+                bufs={n: b.detach().cpu() for n, b in m.named_buffers() if "running" in n})
+            del m, x, logits, scores, loss
+            torch.cuda.empty_cache()
+    return _CACHE["oracle"]
+
+
+def _hip_step(dtype, cuda):
+    torch.manual_seed(0)
+    det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
+                                     compute_dtype=dtype)
+    deterministic_init_(det, seed=SEED)
+    det = det.to(cuda).train()
+    x = _u8_frames().to(cuda).permute(0, 1, 4, 2, 3)  # the bench's feed: uint8, normalised in the stem
+    logits, scores = det(x)
+    loss = F.cross_entropy(logits, _labels().to(cuda), weight=CLASS_W.to(cuda))
+    loss.backward()
+    torch.cuda.synchronize()
+    out = (logits.detach().cpu(), scores.detach().cpu(), float(loss),
+           {n: p.grad.detach().cpu() for n, p in det.named_parameters()},
+           {n: b.detach().cpu() for n, b in det.named_buffers() if "running" in n})
+    del det
+    torch.cuda.empty_cache()
+    return out
+
+
+def test_bench_config_fp32_vs_oracle(cuda):
+    ref = _gpu_oracle(cuda)
+    logits, scores, loss, grads, bufs = _hip_step("fp32", cuda)
+    torch.testing.assert_close(logits, ref["logits"], rtol=1e-3, atol=1e-5)
+    torch.testing.assert_close(scores, ref["scores"], rtol=1e-3, atol=1e-5)
+    assert abs(loss - ref["loss"]) <= 1e-3 * abs(ref["loss"]) + 1e-5
+    assert sorted(grads) == sorted(ref["grads"])
+    scale = max(float(g.double().norm()) for g in ref["grads"].values())
+    bad = []
+    for n, rg in ref["grads"].items():
+        g = grads[n].double().flatten()
+        r = rg.double().flatten()
+        rn = float(r.norm())
+        if rn <= 1e-4 * scale:  # structurally ~zero (a BN shift feeding only a training-mode BN)
+            if float(g.norm()) > 1e-4 * scale:
+                bad.append((n, "zero", float(g.norm()), rn))
+            continue
+        if abs(float(g.norm()) - rn) > 1e-3 * rn + 1e-6:
+            bad.append((n, "norm", float(g.norm()), rn))
+        k = min(64, r.numel())
+        atol = 1e-5 + 1e-3 * float(r[:k].abs().max())
+        if not np.allclose(g[:k].numpy(), r[:k].numpy(), rtol=1e-3, atol=atol):
+            bad.append((n, "head", float((g[:k] - r[:k]).abs().max())))
+    print(f"fp32 256 frames: {len(ref['grads'])} gradients, mismatches {len(bad)}: {bad[:12]}")
+    assert not bad
+    for n, rb in ref["bufs"].items():
+        torch.testing.assert_close(bufs[n], rb, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n}: {m}")
+
+
+def test_bench_config_bf16_vs_oracle(cuda):
+    ref = _gpu_oracle(cuda)
+    logits, _, loss, grads, bufs = _hip_step("bf16", cuda)
+    assert abs(loss - ref["loss"]) <= 2e-2 * abs(ref["loss"]), (loss, ref["loss"])
+    torch.testing.assert_close(logits, ref["logits"], rtol=5e-2, atol=5e-2)
+    scale = max(float(g.double().norm()) for g in ref["grads"].values())
+    outside, low, counted, cos_all = [], [], 0, []
+    for n, rg in ref["grads"].items():
+        r = rg.double().flatten()
+        rn = float(r.norm())
+        if rn <= 1e-4 * scale:
+            continue
+        counted += 1
+        g = grads[n].double().flatten()
+        cos = float(g @ r) / (float(g.norm()) * rn + 1e-30)
+        cos_all.append(cos)
+        if abs(float(g.norm()) - rn) > 0.1 * rn or cos < 0.98:
+            outside.append((n, round(float(g.norm()) / rn, 4), round(cos, 5)))
+        if cos < 0.85:
+            low.append((n, round(cos, 5)))
+    print(f"bf16 256 frames: {counted} gradients, min cos {min(cos_all):.5f}, median {np.median(cos_all):.5f}, "
+          f"{len(outside)} outside (10 %, cos 0.98): {outside}")
+    assert counted >= 0.85 * len(ref["grads"])
+    assert len(outside) <= 0.10 * counted, (len(outside), counted)
+    assert not low, low
+    for n, rb in ref["bufs"].items():
+        torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
+
+
+# ---------------------------------------------------------------- 3. layer by layer (bf16)
+
+def _nhwc(t2d, hw):
+    """[rows][C] NHWC rows -> (N, C, H, W) fp32."""
+    h, w = hw
+    c = t2d.shape[1]
+    return t2d.float().view(-1, h, w, c).permute(0, 3, 1, 2)
+
+
+def _rows(t4):
+    return t4.permute(0, 2, 3, 1).reshape(-1, t4.shape[1])
+
+
+def _ch_err(got, ref):
+    """Per-channel relative L2 error of [rows][C] tensors (denominator floored at 5 % of the median
+    channel norm, so dead channels are judged on the layer's scale)."""
+    got = got.float()
+    ref = ref.float()
+    num = (got - ref).norm(dim=0)
+    den = ref.norm(dim=0)
+    den = torch.maximum(den, 0.05 * den.median())
+    return (num / (den + 1e-30))
+
+
+def _bn_act(y, gamma, beta, act=True):
+    """training-mode BatchNorm (batch statistics over rows, biased var) (+ SiLU) on [rows][C] fp32."""
+    mean = y.mean(0)
+    var = y.var(0, unbiased=False)
+    z = (y - mean) * torch.rsqrt(var + EPS) * gamma + beta
+    return F.silu(z) if act else z
+
+
+def _view(ws, off, rows, cols):
+    n = rows * cols
+    return ws[off:off + 2 * n].view(torch.bfloat16).view(rows, cols)
+
+
+def _saved(lib, h, ws):
+    off, rows, cols = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    out, i = [], 0
+    while lib.dfd_b0_saved_tensor(h, i, ctypes.byref(off), ctypes.byref(rows), ctypes.byref(cols)) == 0:
+        out.append(_view(ws, off.value, rows.value, cols.value).float().clone())
+        i += 1
+    return out
+
+
+def _grad_in(lib, h, ws, block):
+    off, rows, cols = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(lib.dfd_b0_grad_tensor(h, block, ctypes.byref(off), ctypes.byref(rows), ctypes.byref(cols)))
+    return _view(ws, off.value, rows.value, cols.value).float().clone()
+
+
+@pytest.fixture(scope="module")
+def bf16_run(cuda):
+    """One bf16 trunk forward + segment-by-segment backward at the bench shape, with every saved
+    activation and every stage-boundary gradient copied out."""
+    lib = _lib.load()
+    det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
+                                     compute_dtype="bf16")
+    deterministic_init_(det, seed=SEED)
+    det = det.to(cuda).train()
+    trunk = det.backbone
+    det.ensure_flat()
+    rt = trunk.runtime()
+    rt.set_input_norm("imagenet")
+    x = _u8_frames().to(cuda).permute(0, 1, 4, 2, 3).reshape(N, 3, HW, HW)
+    with torch.no_grad():
+        feats, (h, ws) = rt.forward(x, det, 1, True)
+        torch.cuda.synchronize()
+        saved = _saved(lib, h, ws)
+        g = torch.Generator(device=cuda).manual_seed(9)
+        dfeat = torch.randn(N, 1280, device=cuda, generator=g) * 1e-3
+        grads = torch.zeros_like(det._flat_p)
+        nb = 16
+        # block index whose input gradient is final after segment s (0 = head ... 7 = stage 0)
+        first = [0, 0, 0, 0, 0, 0, 0]
+        i = 0
+        for si, cnt in enumerate([1, 2, 2, 3, 3, 4, 1]):
+            first[si] = i
+            i += cnt
+        gin = {}
+        for s in range(9):
+            rt.backward(h, ws, x, dfeat, det, grads, True, s, s + 1)
+            torch.cuda.synchronize()
+            if s == 0:
+                gin[nb] = _grad_in(lib, h, ws, nb)
+            elif s <= 7 and first[7 - s] > 0:
+                gin[first[7 - s]] = _grad_in(lib, h, ws, first[7 - s])
+    sd = {k: v.detach() for k, v in det.state_dict().items()}
+    po = det.param_offsets()
+    hip_grads = {n: grads[po[n]:po[n] + p.numel()].view_as(p).detach().clone() for n, p in det.named_parameters()}
+    out = dict(x=x, feats=feats.detach().clone(), saved=saved, dfeat=dfeat, gin=gin, sd=sd, grads=hip_grads,
+               first=first)
+    yield out
+    del det, ws
+
+
+def _pw_bf16(w):
+    """1x1 conv weights as the bf16 GEMMs see them (launch_cast_params rounds the fp32 masters)."""
+    return w.reshape(w.shape[0], w.shape[1]).bfloat16().float()
+
+
+def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
+    r = bf16_run
+    sd, sv = r["sd"], r["saved"]
+    bad, worst = [], []
+
+    def check(name, got, ref):
+        e = _ch_err(got, ref)
+        worst.append((name, float(e.max())))
+        if float(e.max()) > FWD_CH_TOL:
+            bad.append((name, float(e.max()), int(e.argmax())))
+
+    with torch.backends.cudnn.flags(enabled=False):
+        xn = r["x"].float() / 255.0
+        xn = (xn - torch.tensor(MEAN, device=cuda).view(1, 3, 1, 1)) / torch.tensor(STD, device=cuda).view(1, 3, 1, 1)
+        ystem = F.conv2d(xn, sd["backbone.0.weight"], stride=2, padding=1)
+        check("conv_stem", sv[0], _rows(ystem))
+        hw = (112, 112)
+        a_in = _bn_act(sv[0], sd["backbone.1.weight"], sd["backbone.1.bias"])  # stem BN+SiLU (rows, 32)
+        k = 1
+        x_prev = None
+        for si, bi, bt, cin, cout, ks, s, e in b0_cpu.block_specs():
+            pre = f"backbone.2.{si}.{bi}."
+            if bt == "ir":
+                y1 = sv[k]; k += 1
+                check(pre + "conv_pw", y1, x_prev @ _pw_bf16(sd[pre + "conv_pw.weight"]).t())
+                a1 = _bn_act(y1, sd[pre + "bn1.weight"], sd[pre + "bn1.bias"])
+                bn_dw = "bn2"
+            else:
+                a1 = a_in
+                bn_dw = "bn1"
+            mid = a1.shape[1]
+            y2 = sv[k]; k += 1
+            y2_ref = F.conv2d(_nhwc(a1, hw), sd[pre + "conv_dw.weight"], stride=s, padding=((s - 1) + (ks - 1)) // 2,
+                              groups=mid)
+            hw = (y2_ref.shape[2], y2_ref.shape[3])
+            check(pre + "conv_dw", y2, _rows(y2_ref))
+            a2 = _bn_act(y2, sd[pre + bn_dw + ".weight"], sd[pre + bn_dw + ".bias"])
+            sq = a2.view(N, hw[0] * hw[1], mid).mean(1)
+            z = F.silu(sq @ sd[pre + "se.conv_reduce.weight"].view(-1, mid).t() + sd[pre + "se.conv_reduce.bias"])
+            gate = torch.sigmoid(z @ sd[pre + "se.conv_expand.weight"].view(mid, -1).t() + sd[pre + "se.conv_expand.bias"])
+            a2g = (a2.view(N, hw[0] * hw[1], mid) * gate.unsqueeze(1)).view(-1, mid)
+            y3 = sv[k]; k += 1
+            pwl = "conv_pwl" if bt == "ir" else "conv_pw"
+            bn3 = "bn3" if bt == "ir" else "bn2"
+            check(pre + pwl, y3, a2g @ _pw_bf16(sd[pre + pwl + ".weight"]).t())
+            xo = sv[k]; k += 1
+            xo_ref = _bn_act(y3, sd[pre + bn3 + ".weight"], sd[pre + bn3 + ".bias"], act=False)
+            if s == 1 and cin == cout:
+                xo_ref = xo_ref + x_prev
+            check(pre + "out", xo, xo_ref)
+            x_prev = xo
+        yh = sv[k]
+        check("conv_head", yh, x_prev @ _pw_bf16(sd["backbone.3.weight"]).t())
+        ah = _bn_act(yh, sd["backbone.4.weight"], sd["backbone.4.bias"])
+        feats_ref = ah.view(N, hw[0] * hw[1], -1).mean(1)
+        fe = float((r["feats"] - feats_ref).norm() / feats_ref.norm())
+        worst.append(("features", fe))
+        if fe > 1e-2:
+            bad.append(("features", fe))
+    worst.sort(key=lambda t: -t[1])
+    print(f"per-layer forward, {len(worst)} tensors, worst per-channel rel errors: {worst[:8]}")
+    assert not bad, bad
+
+
+def _oracle_trunk(sd, cuda):
+    """The oracle trunk on the GPU with the detector's weights; 1x1 conv weights rounded to bf16 as the
+    HIP GEMMs use them (depthwise, stem and SE weights are fp32 in the HIP step)."""
+    t = b0_cpu.trunk(b0_cpu.EfficientNetB0())
+    tsd = {}
+    for k, v in sd.items():
+        if not k.startswith("backbone."):
+            continue
+        name = k[len("backbone."):]
+        if v.dim() == 4 and v.shape[2] == 1 and v.shape[3] == 1 and ".se." not in name:
+            v = v.bfloat16().float()
+        tsd[name] = v
+    t.load_state_dict(tsd)
+    return t.to(cuda).train()
+
+
+def _stage_io(r, si):
+    """(input rows, (H, W), gradient rows at the stage output) for stage si >= 1."""
+    sv = r["saved"]
+    # index of the block output saved tensor of the block before stage si's first block
+    k = 1
+    outs = []
+    for _, _, bt, *_ in b0_cpu.block_specs():
+        k += (3 if bt == "ir" else 2)
+        outs.append(k)
+        k += 1
+    i0 = r["first"][si]
+    x_in = sv[outs[i0 - 1]]
+    nxt = r["first"][si + 1] if si < 6 else 16
+    return x_in, nxt
+
+
+def test_bench_config_bf16_backward_per_stage(bf16_run, cuda):
+    r = bf16_run
+    sd, gin, hg = r["sd"], r["gin"], r["grads"]
+    otr = _oracle_trunk(sd, cuda)
+    report, bad = [], []
+    maps = {1: 112, 2: 56, 3: 28, 4: 14, 5: 14, 6: 7}
+
+    def cmp_param(name, ref_grad, scale):
+        g = hg[name].double().flatten()
+        rr = ref_grad.double().flatten()
+        rn = float(rr.norm())
+        if name.endswith("bn3.bias") or name == "backbone.2.0.0.bn2.bias":
+            res = float((g - rr).norm()) / scale
+            report.append((name + "[structural zero, /scale]", res))
+            if res > STRUCT_ZERO_TOL:
+                bad.append((name, "structural zero", res))
+            return
+        if rn <= 1e-4 * scale:
+            return
+        rel = float((g - rr).norm()) / rn
+        report.append((name, rel))
+        if rel > BWD_REL_TOL:
+            bad.append((name, "rel", rel))
+        if name.endswith("conv_dw.weight"):
+            gc = hg[name].double().flatten(1)
+            rc = ref_grad.double().flatten(1)
+            cos = (gc * rc).sum(1) / (gc.norm(dim=1) * rc.norm(dim=1) + 1e-30)
+            live = rc.norm(dim=1) > 1e-3 * rc.norm(dim=1).max()
+            mc = float(cos[live].min())
+            report.append((name + "[min ch cos]", 1 - mc))
+            if mc < BWD_DW_CH_COS:
+                bad.append((name, "channel cos", mc, int(torch.nonzero(live)[cos[live].argmin()])))
+
+    with torch.backends.cudnn.flags(enabled=False):
+        # head segment: conv_head + bn2 + SiLU + global pool
+        x_last = _nhwc(r["saved"][-2], (7, 7)).clone().requires_grad_(True)
+        f = otr[5](otr[4](otr[3](x_last)))
+        f.backward(r["dfeat"])
+        e = float((_rows(x_last.grad) - gin[16]).norm() / _rows(x_last.grad).norm())
+        report.append(("grad into conv_head", e))
+        if e > BWD_REL_TOL:
+            bad.append(("grad into conv_head", e))
+        scale = max(float(p.grad.norm()) for p in list(otr[3].parameters()) + list(otr[4].parameters()))
+        for n, p in list(otr[3].named_parameters(prefix="backbone.3")) + list(otr[4].named_parameters(prefix="backbone.4")):
+            cmp_param(n, p.grad, scale)
+        # stages 6 .. 1: input = the HIP's bf16 stage input, output gradient = the HIP's
+        for si in range(6, 0, -1):
+            x_rows, nxt = _stage_io(r, si)
+            xi = _nhwc(x_rows, (maps[si], maps[si])).clone().requires_grad_(True)
+            stage = otr[2][si]
+            out = stage(xi)
+            dout = _nhwc(gin[nxt], (out.shape[2], out.shape[3]))
+            out.backward(dout)
+            e = float((_rows(xi.grad) - gin[r["first"][si]]).norm() / _rows(xi.grad).norm())
+            report.append((f"grad into stage {si}", e))
+            if e > BWD_REL_TOL:
+                bad.append((f"grad into stage {si}", e))
+            ps = list(stage.named_parameters(prefix=f"backbone.2.{si}"))
+            scale = max(float(p.grad.norm()) for _, p in ps)
+            for n, p in ps:
+                cmp_param(n, p.grad, scale)
+            del xi, out, dout
+        # stem + stage 0 from the exact input frames, output gradient = the HIP's at block 1's input
+        xn = r["x"].float() / 255.0
+        xn = (xn - torch.tensor(MEAN, device=cuda).view(1, 3, 1, 1)) / torch.tensor(STD, device=cuda).view(1, 3, 1, 1)
+        out = otr[2][0](otr[1](otr[0](xn)))
+        out.backward(_nhwc(gin[1], (112, 112)))
+        ps = (list(otr[0].named_parameters(prefix="backbone.0")) + list(otr[1].named_parameters(prefix="backbone.1"))
+              + list(otr[2][0].named_parameters(prefix="backbone.2.0")))
+        scale = max(float(p.grad.norm()) for _, p in ps)
+        for n, p in ps:
+            cmp_param(n, p.grad, scale)
+    report.sort(key=lambda t: -t[1])
+    print(f"per-stage backward: {len(report)} checks, worst: {report[:10]}")
+    assert not bad, bad

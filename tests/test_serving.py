@@ -111,6 +111,17 @@ def test_checkpoint_loader_matches_reference_app(name, tmp_path):
             assert torch.equal(msd[k].cpu(), v), k
 
 
+@pytest.mark.parametrize("fname", ["model_resnet18.pt", "vit_base_patch16_224_best.pt"])
+def test_loader_refuses_unimplemented_backbone(fname, tmp_path):
+    """A checkpoint naming a backbone the MI355X path does not implement (resnet18 / ViT keyed files,
+    which app.load_model would build with timm/torchvision) raises IncompatibleCheckpoint -- the
+    loader's documented failure -- not the detector's ValueError."""
+    p = tmp_path / fname
+    torch.save({"fc1.weight": torch.zeros(256, 512), "fc1.bias": torch.zeros(256)}, p)
+    with pytest.raises(ck.IncompatibleCheckpoint, match="Unsupported backbone"):
+        ck.load_pretrained(p)
+
+
 def test_training_checkpoint_roundtrip(tmp_path):
     """Trainer save formats (src/train.py:398-411, ensemble_trainer.py:549-571) load back through the
     app's rules with every key matched; the fused optimizer's state round-trips too."""

@@ -10,21 +10,24 @@ import torch
 import deepfake_amd  # noqa: F401
 from deepfake_amd import ops
 
-SCHEMA_BITS = {
-    "b0_trunk_forward": "Tensor(a3!) buffers",
-    "b0_trunk_backward": "Tensor(a5!) grads",
-    "weighted_cross_entropy": "Tensor? weight",
-    "adam_step": "Tensor(a0!) params",
-    "grad_norm": "Tensor(a3!) out",
-    "collate_frames": "bool to_float",
-}
+SCHEMA_BITS = [
+    ("b0_trunk_forward", "Tensor(a3!) buffers"),
+    ("b0_trunk_backward", "Tensor(a4!) workspace"),
+    ("b0_trunk_backward", "Tensor(a5!) grads"),
+    ("weighted_cross_entropy", "Tensor? weight"),
+    ("adam_step", "Tensor(a0!) params"),
+    ("adam_step", "Tensor(a1!) grads"),  # the clipped gradient is written back
+    ("grad_norm", "Tensor(a2!) scratch"),
+    ("grad_norm", "Tensor(a3!) out"),
+    ("collate_frames", "bool to_float"),
+]
 
 
 def test_ops_registered_with_schemas():
     for name in ops.OPS:
         op = getattr(torch.ops.dfd, name)
         assert op.default._schema.name == f"dfd::{name}"
-    for name, bit in SCHEMA_BITS.items():
+    for name, bit in SCHEMA_BITS:
         assert bit in str(getattr(torch.ops.dfd, name).default._schema), name
 
 
@@ -97,3 +100,21 @@ def test_grad_norm_and_adam_ops():
     opt.step()
     torch.ops.dfd.adam_step(p, grad, m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-5, 1, 1.0, True, out)
     torch.testing.assert_close(p, ref_p.detach(), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_opcheck_optimizer_ops():
+    """torch.library.opcheck: the declared mutations (incl. the clipped gradient adam_step writes back and
+    grad_norm's scratch) match what the kernels write, and the fake registrations agree."""
+    g = torch.Generator().manual_seed(7)
+    grad = (torch.randn(4096, generator=g) * 3).cuda()
+    out = torch.zeros(2).cuda()
+    scratch = torch.zeros(1024, dtype=torch.float64).cuda()
+    torch.library.opcheck(torch.ops.dfd.grad_norm.default, (grad, 1.0, scratch, out))
+    p = torch.randn(4096, generator=g).cuda()
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    torch.ops.dfd.grad_norm(grad, 1.0, scratch, out)
+    torch.library.opcheck(torch.ops.dfd.adam_step.default,
+                          (p, grad.clone(), m, v, 1e-3, 0.9, 0.999, 1e-8, 1e-5, 1, 1.0, True, out))
+    torch.library.opcheck(torch.ops.dfd.adam_step.default,
+                          (p, grad.clone(), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, 2, 1.0, False, None))
