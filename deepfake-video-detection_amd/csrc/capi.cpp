@@ -369,8 +369,36 @@ int dfd_rn_stem_im2col(void* stream, int dtype, const void* x, int input_fmt, co
 int dfd_rn_gemm(void* stream, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
                 int relu, int64_t M, int N, int K) {
   DFD_GUARD_BEGIN
-  if (!A || !B || !C) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
-  return dfd::blaslt_gemm((hipStream_t)stream, dtype, A, B, C, R, bias, relu != 0, M, N, K);
+  if (!A || !B || !C || !bias) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  dfd::RnConvGeom g{};
+  g.KH = g.KW = g.stride = 1;
+  if (dtype == 1)
+    return dfd::launch_rn_conv((hipStream_t)stream, (const dfd::bf16*)A, (const dfd::bf16*)B, (dfd::bf16*)C,
+                               (const dfd::bf16*)R, bias, relu, g, M, N, K);
+  return dfd::launch_rn_conv((hipStream_t)stream, (const float*)A, (const float*)B, (float*)C, (const float*)R, bias,
+                             relu, g, M, N, K);
+  DFD_GUARD_END
+}
+
+int dfd_rn_conv(void* stream, int dtype, const void* x, int N, int H, int W, int Cin, int kh, int kw, int stride,
+                int pad, const void* w, const float* bias, const void* res, int relu, int Cout, void* out) {
+  DFD_GUARD_BEGIN
+  if (!x || !w || !bias || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  if (N <= 0 || H <= 0 || W <= 0 || Cin <= 0 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 || Cout <= 0) {
+    dfd::set_error("rn_conv: bad shape", __FILE__, __LINE__);
+    return -1;
+  }
+  dfd::RnConvGeom g{N, H, W, Cin, kh, kw, stride, pad, (H + 2 * pad - kh) / stride + 1,
+                    (W + 2 * pad - kw) / stride + 1, 0};
+  while ((1 << g.cin_log2) < Cin && g.cin_log2 < 30) ++g.cin_log2;
+  if (g.Ho <= 0 || g.Wo <= 0) { dfd::set_error("rn_conv: empty output", __FILE__, __LINE__); return -1; }
+  const int64_t M = (int64_t)N * g.Ho * g.Wo;
+  const int K = kh * kw * Cin;
+  if (dtype == 1)
+    return dfd::launch_rn_conv((hipStream_t)stream, (const dfd::bf16*)x, (const dfd::bf16*)w, (dfd::bf16*)out,
+                               (const dfd::bf16*)res, bias, relu, g, M, Cout, K);
+  return dfd::launch_rn_conv((hipStream_t)stream, (const float*)x, (const float*)w, (float*)out, (const float*)res,
+                             bias, relu, g, M, Cout, K);
   DFD_GUARD_END
 }
 

@@ -4,6 +4,12 @@
 #pragma once
 #include "dw_common.h"
 
+#ifndef DFD_DW_XCD
+// XCD-aware workgroup order of the channel-pair depthwise kernels: the channel groups of one
+// spatial tile (and consecutive tiles) are dealt to workgroups that share an XCD (A/B knob)
+#define DFD_DW_XCD 0
+#endif
+
 namespace dfd {
 
 typedef float v2f __attribute__((ext_vector_type(2)));

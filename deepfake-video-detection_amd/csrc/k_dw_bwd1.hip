@@ -57,7 +57,8 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
   __shared__ __attribute__((aligned(16))) float cst[9][DCG];       // sc2 sh2 k1 k2 k3 | sc1 sh1 mean1 invstd1
   float* dys = reinterpret_cast<float*>(dyraw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = blockIdx.x % groups;
+  const int bid = DFD_DW_XCD ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int grp = bid % groups;
   const int c0 = grp * DCG, C = g.C;
   for (int i = tid; i < K * K * DCG; i += 256) {
     const int tap = i / DCG, cl = i - tap * DCG;
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
     for (int b = 0; b < K; ++b) dw[a][b] = v2f{0.f, 0.f};
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
-  for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
+  for (int t = bid / groups; t < ntiles; t += tstep) {
     const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;  // first frame of the tile
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
     // ---- staging loads: dZ, y2 + halo (this thread's 8 channels); frame base + 32-bit offsets ----
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
     *reinterpret_cast<v2f*>(rw + (K * K + 1) * DCG) = sq;
   }
   lds_barrier();
-  const int64_t row = blockIdx.x / groups;
+  const int64_t row = bid / groups;
   float* sout = slab + row * (int64_t)C * K * K;
   for (int i = tid; i < (K * K + 2) * DCG; i += 256) {
     const int e = i / DCG, cl = i - e * DCG;

@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
   __shared__ __attribute__((aligned(16))) float gbl[FR][2][DCG];  // the tile frames' SE gate and bc
   float* dys = reinterpret_cast<float*>(dyraw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = blockIdx.x % groups;
+  const int bid = DFD_DW_XCD ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int grp = bid % groups;
   const int c0 = grp * DCG, C = g.C;
   for (int i = tid; i < K * K * DCG; i += 256) {
     const int tap = i / DCG, cl = i - tap * DCG;
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
     for (int b = 0; b < K; ++b) dw[a][b] = v2f{0.f, 0.f};
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
-  for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
+  for (int t = bid / groups; t < ntiles; t += tstep) {
     const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;  // first frame of the tile
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;  // input tile origin (even)
     const int ob = iy0 / 2 - 1, oxb = ix0 / 2 - 1;             // staged dY window origin
@@ -258,7 +259,7 @@ __global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
     *reinterpret_cast<v2f*>(rw + (K * K + 1) * DCG) = sq;
   }
   lds_barrier();
-  const int64_t row = blockIdx.x / groups;
+  const int64_t row = bid / groups;
   float* sout = slab + row * (int64_t)C * K * K;
   for (int i = tid; i < (K * K + 2) * DCG; i += 256) {
     const int e = i / DCG, cl = i - e * DCG;

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
   __shared__ __attribute__((aligned(16))) float cst[2][DCG];       // BN1 scale, shift
   float* acts = reinterpret_cast<float*>(araw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = blockIdx.x % groups;
+  const int bid = DFD_DW_XCD ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int grp = bid % groups;
   const int c0 = grp * DCG, C = g.C;
   for (int i = tid; i < K * K * DCG; i += 256) {
     const int tap = i / DCG, cl = i - tap * DCG;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
   const bool cokp = ch < C;
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
-  for (int t = blockIdx.x / groups; t < ntiles; t += tstep) {
+  for (int t = bid / groups; t < ntiles; t += tstep) {
     const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
     Raw8<T> ry[D::NLD];
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
     const int which = tid / DCG, cl = tid - which * DCG;
     const float v = ((red[(0 * 2 + which) * DCG + cl] + red[(1 * 2 + which) * DCG + cl]) +
                      red[(2 * 2 + which) * DCG + cl]) + red[(3 * 2 + which) * DCG + cl];
-    const int64_t row = blockIdx.x / groups;
+    const int64_t row = bid / groups;
     if (stats && c0 + cl < C) stats[(row * 2 + which) * C + c0 + cl] = v;
   }
 }

@@ -325,15 +325,15 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   // N <= 128 (the A prologue then runs once per row tile); 128x64 for narrow N; the 14x14 / 7x7
   // stages (few row tiles) want the small tiles for enough workgroups in flight.
   int cfg = (int)tune_or(TK_GEMM_TILE, g_gemm_tile.load());
-  if (cfg < 0 || cfg > 7) {
+  if (cfg < 0 || cfg > 12) {
     if (N <= 64) cfg = 1;
     else if (N <= 128) cfg = 0;
     else if (M <= 16384) cfg = N <= 256 ? 3 : 1;
     else if (M <= 65536) cfg = 2;
     else cfg = N <= 160 ? 1 : 2;
   }
-  static constexpr int kBM[8] = {128, 128, 64, 32, 128, 64, 64, 128};
-  static constexpr int kBN[8] = {128, 64, 64, 64, 64, 64, 64, 128};
+  static constexpr int kBM[13] = {128, 128, 64, 32, 128, 64, 64, 128, 64, 64, 64, 32, 128};
+  static constexpr int kBN[13] = {128, 64, 64, 64, 64, 64, 64, 128, 192, 128, 320, 192, 192};
   const int bm = kBM[cfg], bn = kBN[cfg];
   const int ntn = cdiv(N, bn);
   const int64_t tiles_m = cdiv64(M, bm);
@@ -349,7 +349,15 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   else if (cfg == 4) gemm_go<T, MODE, ST, EP, 128, 64, 1, 2 - DW, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   else if (cfg == 5) gemm_go<T, MODE, ST, EP, 64, 64, 2, 2, 64, O64>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   else if (cfg == 6) gemm_go<T, MODE, ST, EP, 64, 64, 2, 1, 128, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
-  else gemm_go<T, MODE, ST, EP, 128, 128, 1, 1, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 7) gemm_go<T, MODE, ST, EP, 128, 128, 1, 1, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  // wide-N tiles (4 waves side by side along N): one tile spans the whole N of the narrow
+  // projection / dgrad shapes (N 112..320), so each A row tile is read and put through the
+  // producer prologue exactly once
+  else if (cfg == 8) gemm_go<T, MODE, ST, EP, 64, 192, 4, 2, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 9) gemm_go<T, MODE, ST, EP, 64, 128, 4, 2, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 10) gemm_go<T, MODE, ST, EP, 64, 320, 4, 2, 32, 1>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else if (cfg == 11) gemm_go<T, MODE, ST, EP, 32, 192, 4, 2, 64, 2>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
+  else gemm_go<T, MODE, ST, EP, 128, 192, 4, 2, 32, 1>(s, gx, ntn, dyn, A, B, C, R, bias, Z, M, N, K, pro, stats, tiles_m);
   if (stat_rows) *stat_rows = gx;
   return 0;
 }

@@ -61,6 +61,13 @@ int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* 
 template <typename T>
 int launch_rn_avgpool(hipStream_t s, const T* x, int N, int HW, int C, float* out);
 
+// ResNet-50 convolutions as implicit-GEMM MFMA kernels (k_rnconv.hip): C = relu?(conv(X) + bias (+ R))
+struct RnConvGeom {
+  int N, H, W, Cin, KH, KW, stride, pad, Ho, Wo, cin_log2;
+};
+template <typename T>
+int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, const float* bias, int relu,
+                   const RnConvGeom& g, int64_t M, int N, int K);
 // plain library GEMMs through hipBLASLt (blaslt.cpp): C = A . B^T + bias (+ R); dW (+)= dY^T . X
 int blaslt_linear(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
                   int N, int K);

@@ -9,13 +9,13 @@ which serving runs in eval mode (``app.load_model`` -> ``model.eval()``, ``predi
 ``1.*`` (bn1), ``4.0.conv1.weight`` ... under the detector's ``backbone.`` prefix) and runs the
 INFERENCE forward on HIP, NHWC:
 
-* every convolution is ``dfd_rn_gemm`` (hipBLASLt, fp32 accumulate) over an im2col
-  (``dfd_rn_im2col``; the 1x1 stride-1 convs read the activation directly) with the eval-mode
-  BatchNorm folded into the weights and a bias; ReLU and the bottleneck's identity add run in the
-  GEMM epilogue: ``relu(conv3(x) * s3 + b3 + identity)``;
-* conv1 reads the (N,3,H,W) frames through ``dfd_rn_stem_im2col`` (any strides, fp32 or uint8
-  with the input normalisation inside, like the B0 stem); maxpool and the global average pool are
-  HIP kernels (``csrc/k_resnet.hip``).
+* every convolution is ``dfd_rn_conv``, an implicit-GEMM MFMA kernel (``csrc/k_rnconv.hip``: the
+  im2col rows are gathered inside the A-tile staging, never materialised; fp32 accumulation) with
+  the eval-mode BatchNorm folded into the weights and a bias; ReLU and the bottleneck's identity
+  add run in its epilogue: ``relu(conv3(x) * s3 + b3 + identity)``.  No library GEMM;
+* conv1 (Cin = 3) reads the (N,3,H,W) frames through ``dfd_rn_stem_im2col`` (any strides, fp32 or
+  uint8 with the input normalisation inside, like the B0 stem) and runs on the same MFMA kernel
+  (``dfd_rn_gemm``); maxpool and the global average pool are HIP kernels (``csrc/k_resnet.hip``).
 
 Training mode is not provided for this member (the hot path trains EfficientNet-B0): calling it
 with gradients enabled, or in ``.train()`` mode, raises instead of silently using batch statistics.
@@ -179,17 +179,14 @@ def _forward(f, x, dt, norm):
         return out
 
     def conv(h, hw, c, res=None, relu=True):
+        """one folded conv (+ identity) (+ ReLU): the implicit-GEMM MFMA kernel (k_rnconv.hip)"""
         (hh, ww) = hw
         ho = (hh + 2 * c.pad - c.k) // c.stride + 1
         wo = (ww + 2 * c.pad - c.k) // c.stride + 1
-        m = N * ho * wo
-        if c.k == 1 and c.stride == 1:
-            a = h
-        else:
-            a = torch.empty(m, c.kp, dtype=tdt, device=dev)
-            _lib.check(lib.dfd_rn_im2col(st, dt, h.data_ptr(), N, hh, ww, c.cin, c.k, c.k, c.stride, c.pad, c.kp,
-                                         a.data_ptr()))
-        return gemm(a, c, m, res, relu), (ho, wo)
+        out = torch.empty(N * ho * wo, c.cout, dtype=tdt, device=dev)
+        _lib.check(lib.dfd_rn_conv(st, dt, h.data_ptr(), N, hh, ww, c.cin, c.k, c.k, c.stride, c.pad, c.w.data_ptr(),
+                                   c.b.data_ptr(), _lib.ptr(res), 1 if relu else 0, c.cout, out.data_ptr()))
+        return out, (ho, wo)
 
     # conv1 7x7/2 + bn1 + relu (frames gathered straight from the caller's tensor)
     stem = f["stem"]

@@ -149,8 +149,9 @@ DFD_API int dfd_collate_frames(void* stream, const uint8_t* src, const int64_t* 
 
 /* ---- ResNet-50 ensemble member, inference (src/pretrained_detector.py:37-40 -> torchvision
  * resnet50 children[:-1]; EnsembleDetector default ENSEMBLE_BACKBONES, app.py:661,1597).  NHWC
- * activations, dtype 0 = fp32, 1 = bf16.  Every convolution is dfd_rn_gemm over an im2col (or,
- * for 1x1 stride 1, the activation itself) with the eval BatchNorm folded into weights + bias. ---- */
+ * activations, dtype 0 = fp32, 1 = bf16.  Every convolution is dfd_rn_conv, an implicit-GEMM MFMA
+ * kernel with the eval BatchNorm folded into weights + bias (conv1: dfd_rn_gemm over the stem
+ * gather).  No library GEMM on this path. ---- */
 /* NHWC x (N,H,W,C) -> rows [N*Ho*Wo][Kp], column (ky*kw + kx)*C + c, zero padding; C % 8 == 0 */
 DFD_API int dfd_rn_im2col(void* stream, int dtype, const void* x, int N, int H, int W, int C, int kh, int kw,
                           int stride, int pad, int Kp, void* out);
@@ -158,9 +159,17 @@ DFD_API int dfd_rn_im2col(void* stream, int dtype, const void* x, int N, int H, 
  * norm6 = mean[3], std[3]) -> [N*Ho*Wo][152] (147 taps + zero padding) */
 DFD_API int dfd_rn_stem_im2col(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
                                const float* norm6, int N, int H, int W, void* out);
-/* C[M][N] = relu?(A[M][K] . B[N][K]^T + bias[N] (+ R[M][N])) through hipBLASLt, fp32 accumulate */
+/* C[M][N] = relu?(A[M][K] . B[N][K]^T + bias[N] (+ R[M][N])), fp32 accumulate (the MFMA kernel of
+ * dfd_rn_conv on an explicit A; K % 8 == 0) */
 DFD_API int dfd_rn_gemm(void* stream, int dtype, const void* A, const void* B, void* C, const void* R,
                         const float* bias, int relu, int64_t M, int N, int K);
+/* One folded convolution + BN (+ identity) (+ ReLU) of torchvision's Bottleneck / downsample
+ * (resnet.py:Bottleneck.forward): x NHWC (N,H,W,Cin) -> out NHWC (N,Ho,Wo,Cout),
+ * out = relu?(conv(x, w) + bias (+ res)); w [Cout][kh*kw*Cin] (column (ky*kw + kx)*Cin + c);
+ * Cin a power of two >= 8 unless kh = kw = stride = 1; kw 1 or 3. */
+DFD_API int dfd_rn_conv(void* stream, int dtype, const void* x, int N, int H, int W, int Cin, int kh, int kw,
+                        int stride, int pad, const void* w, const float* bias, const void* res, int relu, int Cout,
+                        void* out);
 /* 3x3/2 pad 1 max pooling, NHWC, C % 8 == 0 */
 DFD_API int dfd_rn_maxpool(void* stream, int dtype, const void* x, int N, int H, int W, int C, void* out);
 /* global average pooling (N, HW, C) -> (N, C) fp32 */

@@ -126,3 +126,52 @@ def test_ensemble_matches_oracle_and_refuses_training():
     ens.train()
     with pytest.raises(NotImplementedError):
         ens(x.cuda())
+
+
+# every distinct convolution of the ResNet-50 trunk at 224x224 (torchvision v1.5 Bottleneck):
+# (Cin, H, Cout, k, stride) -- 1x1 s1 (direct A), 3x3 s1/s2 and 1x1 s2 (implicit im2col gather)
+RN_CONV_SHAPES = [(64, 56, 64, 1, 1), (64, 56, 64, 3, 1), (64, 56, 256, 1, 1), (256, 56, 128, 1, 1),
+                  (128, 56, 128, 3, 2), (256, 56, 512, 1, 2), (128, 28, 128, 3, 1), (512, 28, 256, 1, 1),
+                  (256, 28, 256, 3, 2), (512, 28, 1024, 1, 2), (256, 14, 256, 3, 1), (1024, 14, 512, 1, 1),
+                  (512, 14, 512, 3, 2), (1024, 14, 2048, 1, 2), (512, 7, 512, 3, 1), (512, 7, 2048, 1, 1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_rn_conv_kernel_every_shape(dt):
+    """dfd_rn_conv (k_rnconv.hip, implicit-GEMM MFMA) against torch conv2d on the same (rounded)
+    operands, with the folded-BN bias, the identity add and ReLU of the bottleneck epilogue."""
+    import ctypes
+    from deepfake_amd import _lib
+    lib = _lib.load()
+    tdt = {"fp32": torch.float32, "bf16": torch.bfloat16}[dt]
+    g = torch.Generator().manual_seed(11)
+    n = 3
+    with torch.backends.cudnn.flags(enabled=False):
+        for cin, h, cout, k, s in RN_CONV_SHAPES:
+            x = torch.randn(n, h, h, cin, generator=g).to(tdt).cuda()
+            w = (torch.randn(cout, k, k, cin, generator=g) / (k * k * cin) ** 0.5).to(tdt).cuda()
+            b = torch.randn(cout, generator=g).cuda()
+            p = (k - 1) // 2
+            ho = (h + 2 * p - k) // s + 1
+            res = torch.randn(n, ho, ho, cout, generator=g).to(tdt).cuda()
+            out = torch.empty(n, ho, ho, cout, dtype=tdt, device="cuda")
+            for use_res, relu in ((False, True), (True, True), (False, False)):
+                st = _lib.stream_of(out.device)
+                _lib.check(lib.dfd_rn_conv(st, 0 if dt == "fp32" else 1, x.data_ptr(), n, h, h, cin, k, k, s, p,
+                                           w.data_ptr(), b.data_ptr(), res.data_ptr() if use_res else None,
+                                           1 if relu else 0, cout, out.data_ptr()))
+                ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2),
+                                                 stride=s, padding=p).permute(0, 2, 3, 1) + b
+                if dt == "bf16":
+                    ref = ref.to(tdt).float()  # the epilogue rounds acc + bias before the identity add
+                if use_res:
+                    ref = ref + res.float()
+                if relu:
+                    ref = torch.relu(ref)
+                got = out.float()
+                if dt == "fp32":
+                    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-4, msg=lambda m: f"{(cin, h, cout, k, s)}: {m}")
+                else:
+                    rel = float((got - ref).norm() / ref.norm())
+                    assert rel < 8e-3, ((cin, h, cout, k, s), use_res, relu, rel)
