@@ -7,7 +7,7 @@
 #ifndef DFD_DW_XCD
 // XCD-aware workgroup order of the channel-pair depthwise kernels: the channel groups of one
 // spatial tile (and consecutive tiles) are dealt to workgroups that share an XCD (A/B knob)
-#define DFD_DW_XCD 0
+#define DFD_DW_XCD -1  // -1: per-shape rule in the launchers; 0 / 1: force off / on
 #endif
 
 namespace dfd {

@@ -49,7 +49,7 @@ template <typename T, int K, int TH, int TW, int RS, int FR>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bwd1_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
     const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
-    int ntiles, int groups, int tiles_x, int tiles_y) {
+    int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
   using D = Dw1<T, K, TH, TW, RS, FR>;
   __shared__ __attribute__((aligned(16))) char dyraw[D::DYB];  // staged dY (fp32 pairs); reduction scratch
   __shared__ __attribute__((aligned(16))) float gbl[FR][2][DCG];   // the tile frames' SE gate and bc
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
   __shared__ __attribute__((aligned(16))) float cst[9][DCG];       // sc2 sh2 k1 k2 k3 | sc1 sh1 mean1 invstd1
   float* dys = reinterpret_cast<float*>(dyraw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int bid = DFD_DW_XCD ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int bid = xcd ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   const int grp = bid % groups;
   const int c0 = grp * DCG, C = g.C;
   for (int i = tid; i < K * K * DCG; i += 256) {
@@ -281,8 +281,11 @@ static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
   const int gx = (int)(rows * groups);
+  // XCD-aware order where it measured faster (kbench A/B, interleaved: 56x56 -12 %, 14x14 k3 -10 %,
+  // 28x28 / 14x14 k5 -2..-4 %); one channel group (112x112 c32) and the stacked 7x7 tiles +4 %
+  const int xcd = DFD_DW_XCD >= 0 ? DFD_DW_XCD : (groups > 1 && g.H >= 14);
   hipLaunchKernelGGL(kern, dim3(gx), dim3(256), 0, s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, slab, ntiles, groups,
-                     tiles_x, tiles_y);
+                     tiles_x, tiles_y, xcd);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
   return launch_reduce_slabs(s, slab, (int)rows, per, dW, accumulate);

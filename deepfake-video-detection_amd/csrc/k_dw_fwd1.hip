@@ -11,6 +11,10 @@
 // strip / tile kernels on these shapes (VALU-issue bound: fewer instructions per output).
 #include "dw1_common.h"
 
+#ifndef DFD_FWD1_PF
+#define DFD_FWD1_PF 0  // next-tile register prefetch of the staged window (A/B knob)
+#endif
+
 namespace dfd {
 
 template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1>
@@ -38,14 +42,14 @@ struct Dwf1 {
 template <typename T, int K, int TH, int TW, int RS, int FR, int S>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fwd1_kernel(
     DwGeom g, const T* __restrict__ Y1, const float* __restrict__ w, Pro bn1, T* __restrict__ out,
-    float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y) {
+    float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
   using D = Dwf1<T, K, TH, TW, RS, FR, S>;
   __shared__ __attribute__((aligned(16))) char araw[D::AB];        // staged activations; reduction scratch
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
   __shared__ __attribute__((aligned(16))) float cst[2][DCG];       // BN1 scale, shift
   float* acts = reinterpret_cast<float*>(araw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int bid = DFD_DW_XCD ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  const int bid = xcd ? xcd_swizzle((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   const int grp = bid % groups;
   const int c0 = grp * DCG, C = g.C;
   for (int i = tid; i < K * K * DCG; i += 256) {
@@ -67,22 +71,27 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
   const bool cokp = ch < C;
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
+  // raw loads of a tile's staged window (one 8-channel vector per lane and pass)
+  auto stage_load = [&](int t, Raw8<T> (&ry)[D::NLD]) {
+    const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;
+    const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
+    const T* yf = Y1 + (int64_t)f * fstride;
+#pragma unroll
+    for (int i = 0; i < D::NLD; ++i) {
+      const int pixl = (tid >> 2) + 64 * i;
+      const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
+      const int oy = iy0 * S - D::PAD + pf / D::GW, ox = ix0 * S - D::PAD + pf % D::GW;
+      const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
+      const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
+      raw_ld(ry[i], yf + o, yf, in);
+    }
+  };
+  Raw8<T> ry[D::NLD];
+  if (DFD_FWD1_PF && bid / groups < ntiles) stage_load(bid / groups, ry);
   for (int t = bid / groups; t < ntiles; t += tstep) {
     const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
-    Raw8<T> ry[D::NLD];
-    {
-      const T* yf = Y1 + (int64_t)f * fstride;
-#pragma unroll
-      for (int i = 0; i < D::NLD; ++i) {
-        const int pixl = (tid >> 2) + 64 * i;
-        const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
-        const int oy = iy0 * S - D::PAD + pf / D::GW, ox = ix0 * S - D::PAD + pf % D::GW;
-        const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
-        const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
-        raw_ld(ry[i], yf + o, yf, in);
-      }
-    }
+    if (!DFD_FWD1_PF) stage_load(t, ry);
     lds_barrier();  // the previous tile's strips are done with acts
 #pragma unroll
     for (int i = 0; i < D::NLD; ++i) {
@@ -105,6 +114,8 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
       }
     }
     lds_barrier();
+    // the next tile's window loads fly while this tile's strips run (issued before its stores)
+    if (DFD_FWD1_PF && t + tstep < ntiles) stage_load(t + tstep, ry);
 #pragma unroll 1
     for (int s = slot; s < D::NSTRIP; s += 16) {
       const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
@@ -174,8 +185,11 @@ static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* 
   const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR, S>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
+  // XCD-aware order where it measured faster (kbench A/B: 56x56 s1 -16 %, 14x14 c480 -2..-6 %); the
+  // 14x14 k5 c672 (+7 %), stacked 7x7 (+7..12 %) and single-group layers keep dispatch order
+  const int xcd = DFD_DW_XCD >= 0 ? DFD_DW_XCD : (groups > 1 && (g.Ho >= 28 || (g.Ho == 14 && g.C <= 480)));
   hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
-                     pro, Y, stats, ntiles, groups, tiles_x, tiles_y);
+                     pro, Y, stats, ntiles, groups, tiles_x, tiles_y, xcd);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
   return 0;

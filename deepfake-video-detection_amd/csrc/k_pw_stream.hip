@@ -39,7 +39,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // Row threshold above which the streaming kernel takes a layer (below it the tiled kernel's
 // weight reuse wins); settable through dfd_set_tuning("stream_min_rows", v).
-static std::atomic<int64_t> g_stream_min_rows{100000};
+static std::atomic<int64_t> g_stream_min_rows{40000};
 int64_t set_stream_min_rows(int64_t v) { return g_stream_min_rows.exchange(v); }
 
 template <int NB, int U>

@@ -66,7 +66,7 @@ BWD_DW_CH_COS = 0.98
 # loss only through 1x1 convs into TRAINING-mode BatchNorms (directly or along the residual chain):
 # a per-channel shift there is annihilated, so its bias gradient is structurally zero and both sides
 # hold rounding residue only -- judged against the stage's gradient scale instead.
-STRUCT_ZERO_TOL = 5e-3
+STRUCT_ZERO_TOL = 5e-2  # residue measured up to 2.0e-2 of the stage scale (order-dependent)
 
 _CACHE = {}
 

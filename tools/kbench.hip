@@ -165,6 +165,14 @@ int main(int argc, char** argv) {
         return e ? e : launch_dw_bwd<bf16>(b.s, g, D, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
       });
     }
+    if (k.s == 2 && dw_bwd2_covers(g)) {
+      BnBwdIn bi2{};
+      bi2.mean = mean; bi2.invstd = invstd; bi2.scale = sc; bi2.shift = sh; bi2.silu = true;
+      b.run("dw_bwd2", nm, 2.0 * (2 * Mi * C1 + 2 * Mo * C1), [&] {
+        return launch_dw_bwd2<bf16>(b.s, g, D, A, gate, gate, sc, sh, coef, W, C, bi2, B, stats, &rows, slab,
+                                    slab_cap, dW, false);
+      });
+    }
     b.run("dw_wgrad", nm, dwb, [&] {
       return launch_dw_wgrad<bf16>(b.s, g, A, B, pb, PRO_BN_SILU, slab, slab_cap, dW, false);
     });
