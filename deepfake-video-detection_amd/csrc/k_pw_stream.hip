@@ -369,6 +369,7 @@ int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const
       DFD_STREAM_CASE(8, 2, PRO_NONE, true, false)  // 40 -> 240
       DFD_STREAM_CASE(8, 3, PRO_NONE, true, false)  // 80 -> 480
       DFD_STREAM_CASE(7, 4, PRO_NONE, true, false)  // 112 -> 672
+      DFD_STREAM_CASE(8, 6, PRO_NONE, true, false)  // 192 -> 1152 (7x7 stages, chunks of 128)
       default: return 1;
     }
   }
@@ -393,6 +394,8 @@ int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const
       DFD_STREAM_CASE(5, 2, PRO_NONE, false, false)  // 40 -> 144
       DFD_STREAM_CASE(8, 2, PRO_NONE, false, false)  // 40 -> 240
       DFD_STREAM_CASE(8, 3, PRO_NONE, false, false)  // 80 -> 240 / 480
+      DFD_STREAM_CASE(7, 4, PRO_NONE, false, false)  // 112 -> 672
+      DFD_STREAM_CASE(8, 6, PRO_NONE, false, false)  // 192 -> 1152
       default: return 1;
     }
   }
