@@ -153,7 +153,7 @@ int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64
 int dfd_b0_plan_set_tuning(dfd_b0_plan* plan, const char* key, int64_t value) {
   if (!plan || !key) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
   static const char* names[dfd::TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile",
-                                             "dw_bwd1", "dw_fwd1", "wgrad_stream"};
+                                             "dw_bwd1", "dw_fwd1", "wgrad_stream", "mbconv7"};
   for (int k = 0; k < dfd::TK_COUNT; ++k)
     if (strcmp(key, names[k]) == 0) {
       std::lock_guard<std::mutex> lk(plan->mu);
@@ -220,6 +220,13 @@ int dfd_b0_grad_tensor(const dfd_b0_plan* plan, int block, int64_t* off, int64_t
     *rows = F * b.hin * b.win;
     *cols = b.cin;
   }
+  return 0;
+}
+
+int dfd_b0_fused_info(const dfd_b0_plan* plan, int* nblocks, int64_t* abort_offset) {
+  if (!plan || !nblocks || !abort_offset) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  *nblocks = dfd::plan_fused7_blocks(plan->p);
+  *abort_offset = plan->p.o_bar + 63 * 4;  // the int abort flag in the last word of the barrier region
   return 0;
 }
 
@@ -427,6 +434,7 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "dw_bwd1") == 0) return dfd::set_dw_bwd1(value);
   if (key && strcmp(key, "dw_fwd1") == 0) return dfd::set_dw_fwd1(value);
   if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
+  if (key && strcmp(key, "mbconv7") == 0) return dfd::set_mbconv7(value);
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }

@@ -27,7 +27,7 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
 // concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -60,6 +60,37 @@ template <typename T>
 int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* out);
 template <typename T>
 int launch_rn_avgpool(hipStream_t s, const T* x, int N, int HW, int C, float* out);
+
+// Fused 7x7-stage MBConv forward (k_mbconv7.hip): one workgroup per frame, the expanded tensor in LDS
+struct Mb7Bn {
+  const float* gamma;
+  const float* beta;
+  float* run_mean;
+  float* run_var;
+  float* mean;
+  float* invstd;
+  float* scale;
+  float* shift;
+};
+struct Mb7Args {
+  int frames, cin, mid, cout, rd, k, skip, training;
+  float momentum, eps;
+  const bf16* x;     // block input [F*49][cin]
+  const bf16* w1;    // conv_pw [mid][cin] (compute-dtype copy)
+  const float* wdw;  // conv_dw [mid][k*k] fp32
+  const float* wr;   // SE reduce [rd][mid], bias [rd]; expand [mid][rd], bias [mid]
+  const float* br;
+  const float* we;
+  const float* be;
+  const bf16* w3;    // conv_pwl [cout][mid]
+  Mb7Bn bn[3];       // bn1, bn2, bn3
+  bf16 *y1, *y2, *s2, *y3, *xo;     // saved tensors (training) and the block output
+  float *sq, *rpre, *gate, *part;   // SE saved vectors; per-frame BN partial sums [F][2][C]
+  unsigned* bar;                    // zeroed grid-barrier counter of this launch
+  int* abort;                       // zeroed; set if the grid was not co-resident
+};
+bool mbconv7_supported(int frames, int H, int W, int cin, int mid, int cout, int rd, int k, int s);
+int launch_mbconv7_fwd(hipStream_t s, const Mb7Args& a);
 
 // ResNet-50 convolutions as implicit-GEMM MFMA kernels (k_rnconv.hip): C = relu?(conv(X) + bias (+ R))
 struct RnConvGeom {

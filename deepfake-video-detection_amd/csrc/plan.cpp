@@ -27,6 +27,9 @@ constexpr int64_t kMaterialiseRows = 20000;  // the 7x7 stages (see Block::o_s2)
 // weight-gradient slab regions: a backward segment's wgrad partials each get their own region so
 // their reductions can be deferred to one batched launch at the end of the segment (SlabDefer)
 constexpr int kSlabRegions = 16;
+// fused 7x7 MBConv launches: one 16-B slot (barrier counter) each, the abort flag in the last word
+constexpr int kBarSlots = 15;
+constexpr int64_t kBarBytes = 256;
 
 struct Topo {
   std::vector<TensorSpec> t;
@@ -222,6 +225,7 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.o_tg = alloc(maxPW * 4);
   p.o_gram = alloc(maxCin * maxCin * 4);
   p.o_cs = alloc(maxCin * 4);
+  p.o_bar = alloc(kBarBytes);
   p.ws_bytes = cur;
   p.offs.assign(p.tensors.size(), -1);
   p.bound = false;
@@ -327,6 +331,14 @@ inline bool probe_hit(const Plan& p, int kind, const Block* b) {
   } while (0)
 #define PROBED(KIND, BLK, EXPR) PROBED_ON(KIND, BLK, s, EXPR)
 
+// the fused 7x7-stage MBConv forward (k_mbconv7.hip) for the bf16 plan: 1 on (default), 0 off
+std::atomic<int64_t> g_mbconv7{1};
+// blocks of the 7x7 stages that run as one fused launch (k_mbconv7.hip) in the bf16 forward
+static bool block_fused7(const Plan& p, const Block& b) {
+  return !b.ds && b.o_s2 >= 0 && tune_or(TK_MBCONV7, g_mbconv7.load(std::memory_order_relaxed)) != 0 &&
+         mbconv7_supported(p.frames, b.hin, b.win, b.cin, b.mid, b.cout, b.rd, b.k, b.s);
+}
+
 template <typename T>
 struct Run {
   Plan& p;
@@ -370,12 +382,40 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   DFD_TRY(launch_stem_fwd<T>(s, sg, x, r.prm(p.t_stem), r.a(p.o_ystem), stats, &rows));
   DFD_TRY(fin(p.bn_stem, F * p.H1 * p.W1));
   const T* xin = nullptr;
+  // fused 7x7-stage blocks (bf16): which blocks take the one-launch path, and their barrier slots
+  auto fused7 = [&](const Block& b) { return sizeof(T) == 2 && block_fused7(p, b); };
+  const int nfused = sizeof(T) == 2 ? plan_fused7_blocks(p) : 0;
+  if (nfused && tr) DFD_HIP_CHECK(hipMemsetAsync(ws + p.o_bar, 0, kBarBytes, s));
+  int slot = 0;
   for (size_t i = 0; i < p.blocks.size(); ++i) {
     Block& b = p.blocks[i];
     const int64_t Min = F * b.hin * b.win, Mout = F * b.hout * b.wout;
     const int hwo = b.hout * b.wout;
     const BNL& bn_dw = b.ds ? b.bn1 : b.bn2;  // BN after the depthwise conv
     DwGeom g{p.frames, b.hin, b.win, b.mid, b.k, b.s, b.k / 2, b.hout, b.wout};
+    if (nfused && fused7(b)) {
+      if constexpr (sizeof(T) == 2) {
+        auto bnp = [&](const BNL& q) {
+          return Mb7Bn{r.prm(q.t_w), r.prm(q.t_b), bnb + p.offs[q.t_rm], bnb + p.offs[q.t_rv], r.f(q.o_mean),
+                       r.f(q.o_invstd), r.f(q.o_scale), r.f(q.o_shift)};
+        };
+        Mb7Args a{};
+        a.frames = p.frames; a.cin = b.cin; a.mid = b.mid; a.cout = b.cout; a.rd = b.rd; a.k = b.k;
+        a.skip = b.skip ? 1 : 0; a.training = tr; a.momentum = mom; a.eps = eps;
+        a.x = xin; a.w1 = r.a(b.pw.o_w); a.wdw = r.prm(b.t_dw);
+        a.wr = r.prm(b.t_se_wr); a.br = r.prm(b.t_se_br); a.we = r.prm(b.t_se_we); a.be = r.prm(b.t_se_be);
+        a.w3 = r.a(b.pwl.o_w);
+        a.bn[0] = bnp(b.bn1); a.bn[1] = bnp(b.bn2); a.bn[2] = bnp(b.bn3);
+        a.y1 = r.a(b.o_y1); a.y2 = r.a(b.o_y2); a.s2 = r.a(b.o_s2); a.y3 = r.a(b.o_y3); a.xo = r.a(b.o_x);
+        a.sq = r.f(b.o_sq); a.rpre = r.f(b.o_rpre); a.gate = r.f(b.o_gate); a.part = r.f(p.o_stats);
+        a.bar = reinterpret_cast<unsigned*>(ws + p.o_bar) + 4 * slot;
+        a.abort = reinterpret_cast<int*>(ws + p.o_bar) + 63;
+        ++slot;
+        DFD_TRY(launch_mbconv7_fwd(s, a));
+      }
+      xin = r.a(b.o_x);
+      continue;
+    }
     if (b.ds) {
       DFD_TRY(launch_dw_fwd<T>(s, g, r.a(p.o_ystem), r.prm(b.t_dw), r.a(b.o_y2), r.pro_bn(p.bn_stem, b.hin * b.win),
                                PRO_BN_SILU, stats, &rows));
@@ -688,6 +728,14 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
 
 int64_t set_fold_min_rows(int64_t v) { return g_fold_min_rows.exchange(v); }
 int64_t set_wgrad_stream(int64_t v) { return g_wgrad_stream.exchange(v); }
+int64_t set_mbconv7(int64_t v) { return g_mbconv7.exchange(v); }
+int plan_fused7_blocks(const Plan& p) {
+  if (p.dtype != 1) return 0;  // bf16 plans only
+  int n = 0;
+  for (const Block& b : p.blocks) n += block_fused7(p, b) ? 1 : 0;
+  return n > kBarSlots ? 0 : n;
+}
+
 
 static thread_local const Tuning* t_tune = nullptr;
 int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }

@@ -69,6 +69,7 @@ struct Plan {
   int64_t o_gx[2], o_gs, o_ge1, o_ge2;
   int64_t o_w1t, o_q, o_bv, o_tg, o_gram, o_cs;  // conv_pw backward through its BN (bn_fold_pw)
   int64_t o_coef1, o_stats2;  // BN1 backward coefficients / col_sums partials read on the wgrad stream
+  int64_t o_bar;  // grid-barrier counters + abort flag of the fused 7x7 MBConv launches (zeroed per forward)
   int64_t stats_cap, slab_cap, part_cap;
   // cast table (device copy)
   std::vector<CastSeg> cast_host;
@@ -106,6 +107,9 @@ int64_t set_fold_min_rows(int64_t v);
 // 1x1-conv weight gradients on a second stream, overlapping the backward's main chain (0 off -- the
 // default --, 1 every block, N > 1 blocks with >= N gradient rows)
 int64_t set_wgrad_stream(int64_t v);
+int64_t set_mbconv7(int64_t v);
+// number of blocks the bf16 forward runs through the fused 7x7 MBConv kernel (0: none)
+int plan_fused7_blocks(const Plan& p);
 // static topology (shape-independent)
 const std::vector<TensorSpec>& b0_tensor_table();
 

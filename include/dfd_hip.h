@@ -104,6 +104,12 @@ DFD_API int dfd_b0_saved_tensor(const dfd_b0_plan* plan, int idx, int64_t* byte_
  * segment runs: the buffers are reused.  Used by the per-stage parity tests. */
 DFD_API int dfd_b0_grad_tensor(const dfd_b0_plan* plan, int block, int64_t* byte_offset, int64_t* rows,
                                int64_t* cols);
+/* The fused 7x7-stage MBConv forward (bf16 plans, tuning key "mbconv7"): the number of blocks the
+ * forward runs as one launch each, and the workspace byte offset of the int32 abort flag those
+ * launches raise if their grid-wide barriers found the grid not co-resident (the forward's output is
+ * then invalid; the flag is cleared at the start of each training forward).  No reference
+ * counterpart: the reference's forward is torch's eager timm module. */
+DFD_API int dfd_b0_fused_info(const dfd_b0_plan* plan, int* nblocks, int64_t* abort_offset);
 /* Tensor index range [*lo, *hi) whose gradients are final after segment `seg`. */
 DFD_API int dfd_b0_segment_tensors(int seg, int* lo, int* hi);
 

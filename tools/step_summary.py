@@ -11,7 +11,7 @@ import re
 import statistics
 import sys
 
-CLASSES = [("depthwise fwd", r"dw_fwd"), ("depthwise bwd", r"dw_bwd|dw_dgrad|dw_wgrad"),
+CLASSES = [("fused 7x7 MBConv fwd", r"mbconv7"), ("depthwise fwd", r"dw_fwd"), ("depthwise bwd", r"dw_bwd|dw_dgrad|dw_wgrad"),
            ("1x1 conv fwd/dgrad", r"pw_gemm|pw_stream_kernel"), ("1x1 conv wgrad", r"pw_wgrad|col_sums"),
            ("stem", r"stem_"), ("BN glue", r"bn_"), ("SE", r"se_|frame_sum|mfma_small|sum_parts"),
            ("slab reductions", r"slabs"), ("head / loss", r"linear_|ce_|attn|relu_drop|pool"),
