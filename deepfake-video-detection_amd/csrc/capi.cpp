@@ -435,6 +435,7 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "dw_fwd1") == 0) return dfd::set_dw_fwd1(value);
   if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
   if (key && strcmp(key, "mbconv7") == 0) return dfd::set_mbconv7(value);
+  if (key && strcmp(key, "rnn_persist") == 0) return dfd::set_rnn_persist(value);
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }

@@ -22,6 +22,7 @@
 // Requires frames <= the co-resident grid (one 156 KB workgroup per CU); the plan checks that and
 // otherwise keeps the unfused launches.
 #include "kernels.h"
+#include "grid_sync.h"
 
 namespace dfd {
 
@@ -122,36 +123,6 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
 
 }  // namespace
 
-// grid barrier: every storing wave drains its stores, the workgroup meets, lane 0 publishes with an
-// agent-scope release and arrives on the monotonic counter, polls it with relaxed agent loads
-// (bounded: a grid that is not co-resident raises the abort flag instead of hanging), acquires
-__device__ __forceinline__ bool mb7_grid_sync(unsigned* bar, unsigned target, int* abort_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  __shared__ int ok_sh;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    unsigned spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 22)) {
-        __hip_atomic_store(abort_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ok_sh = ok;
-  }
-  __syncthreads();
-  return ok_sh != 0;
-}
-
 // BN finalisation of this workgroup's channel slice from the per-frame partial rows
 // part[F][2][C] (training): the plan's BN buffers (mean, invstd, scale, shift) and running stats
 __device__ void mb7_bn_finalize(const Mb7Bn& bn, const float* __restrict__ part, int F, int C, float momentum,
@@ -246,9 +217,9 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
       const int r = v / (mid / 8), c8 = (v - r * (mid / 8)) * 8;
       *reinterpret_cast<uint4*>(a.y1 + (row0 + r) * mid + c8) = *reinterpret_cast<const uint4*>(yb + r * YS + c8);
     }
-    if (!mb7_grid_sync(a.bar, bar_target += G, a.abort)) return;
+    if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
     mb7_bn_finalize(a.bn[0], a.part, F, mid, a.momentum, a.eps, dsh);
-    if (!mb7_grid_sync(a.bar, bar_target += G, a.abort)) return;
+    if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
   }
 
   // ---- conv_dw on BN1+SiLU(y1), 64-channel chunks; y2 (bf16) replaces y1 in ybuf ----
@@ -310,9 +281,9 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
       const int r = v / (mid / 8), c8 = (v - r * (mid / 8)) * 8;
       *reinterpret_cast<uint4*>(a.y2 + (row0 + r) * mid + c8) = *reinterpret_cast<const uint4*>(yb + r * YS + c8);
     }
-    if (!mb7_grid_sync(a.bar, bar_target += G, a.abort)) return;
+    if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
     mb7_bn_finalize(a.bn[1], a.part, F, mid, a.momentum, a.eps, dsh);
-    if (!mb7_grid_sync(a.bar, bar_target += G, a.abort)) return;
+    if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
   }
 
   // ---- BN2 + SiLU: a2 (fp32) -> squeeze sums; s2 = bf16(a2) in place (and saved) ----
@@ -389,9 +360,9 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
       const int r = v / (cout / 8), c8 = (v - r * (cout / 8)) * 8;
       *reinterpret_cast<uint4*>(a.y3 + (row0 + r) * cout + c8) = *reinterpret_cast<const uint4*>(yt + r * TS + c8);
     }
-    if (!mb7_grid_sync(a.bar, bar_target += G, a.abort)) return;
+    if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
     mb7_bn_finalize(a.bn[2], a.part, F, cout, a.momentum, a.eps, dsh);
-    if (!mb7_grid_sync(a.bar, bar_target += G, a.abort)) return;
+    if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
   }
   // ---- BN3 (+ skip) -> block output ----
   for (int v = tid; v < HW7 * (cout / 8); v += 256) {

@@ -12,6 +12,7 @@
 // LDS-staged with coalesced loads along the contiguous dimension of either operand layout),
 // rnn_cell_fwd/bwd (fused gate nonlinearities + cell algebra + saved activations),
 // rnn_attn_* (attention pooling over T), weight pack/scatter, column sums.
+#include <atomic>
 #include "kernels.h"
 #include "rnn.h"
 
@@ -518,13 +519,20 @@ __global__ void rnn_mask_bwd_kernel(float* __restrict__ dOm, const float* __rest
 static int ew_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 2048)); }
 
 // ------------------------------------------------------------------ host orchestration
+// the persistent recurrence (k_rnn_persist.hip) where its shape rules hold: 1 on (default), 0 off
+static std::atomic<int64_t> g_rnn_persist{1};
+int64_t set_rnn_persist(int64_t v) { return g_rnn_persist.exchange(v); }
+static bool rnn_use_persist(const RnnDims& d) {
+  return g_rnn_persist.load(std::memory_order_relaxed) != 0 && rnn_persist_supported(d);
+}
+
 // K slices of the per-step recurrent products (fixed per shape; the workspace holds them)
 static int fwd_splits(const RnnDims& d, int* kc) { return sgemm_splits(d.B, 7 * d.H, d.H, kc); }
 static int bwd_splits(const RnnDims& d, int* kc) { return sgemm_splits(d.B, d.H, 7 * d.H, kc); }
 
 struct RnnWs {
   float *xs, *X0, *G, *P[8], *bias7[8], *WX0, *ACT[8], *CN[8], *CL[8], *UH[8], *CI[8], *O, *Om, *E, *att, *ctx, *h1,
-      *y;
+      *y, *sync;
   int64_t floats;  // extent of the layout (rnn_work_floats)
 };
 // one layout function for both the size query (w = nullptr) and the pointers
@@ -547,6 +555,7 @@ static RnnWs rnn_ws(const RnnDims& d, float* w) {
   s.att = take(BT);
   s.ctx = take((int64_t)d.B * H); s.h1 = take((int64_t)d.B * H);
   s.y = take(d.B);
+  s.sync = take(64);  // grid-barrier counter + abort flag of the persistent recurrence
   s.floats = off;
   return s;
 }
@@ -578,7 +587,18 @@ int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float
   int kc;
   const int sf = fwd_splits(d, &kc);
   const int eb = ew_blocks((int64_t)B * H);
-  for (int t = 0; t < T; ++t) {
+  if (rnn_use_persist(d)) {  // the whole recurrence as one launch (k_rnn_persist.hip)
+    RnnPersist a{};
+    a.B = B; a.T = T; a.H = H; a.L = d.L;
+    for (int l = 0; l < d.L; ++l) {
+      a.P[l] = w.P[l]; a.bias7[l] = w.bias7[l]; a.UH[l] = w.UH[l]; a.CI[l] = w.CI[l];
+      a.ACT[l] = w.ACT[l]; a.CN[l] = w.CN[l]; a.CL[l] = w.CL[l];
+    }
+    a.X0 = w.X0; a.O = w.O; a.p = p; a.seed = seed;
+    a.bar = reinterpret_cast<unsigned*>(w.sync); a.abort = reinterpret_cast<int*>(w.sync) + 1;
+    DFD_TRY(launch_rnn_fwd_persist(s, d, a));
+  }
+  for (int t = 0; t < T && !rnn_use_persist(d); ++t) {
     for (int l = 0; l < d.L; ++l) {
       // recurrent product h_in @ P_l^T in K slices (summed by the cell kernel)
       DFD_TRY(launch_sgemm_part(s, false, false, w.UH[l] + (int64_t)t * H, (int)ldr, w.P[l], H, w.G, B, 7 * H, H, sf,
@@ -642,6 +662,8 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   float* dhls = take((int64_t)sb * B * H);  // K slices: gradient into an inner layer's output
   float* dc = take((int64_t)B * H);         // gradient into the last layer's c'
   float* dcl = take((int64_t)B * H);        // gradient into an inner layer's c'
+  float* ppart = take(rnn_persist_scratch_floats(d));  // persistent path: product slices
+  float* psync = take(64);                              // persistent path: barrier counter + abort
   // classifier tail
   const dim3 gH((unsigned)cdiv(H, 256)), gH64((unsigned)cdiv(H, 64));
   hipLaunchKernelGGL(rnn_cls_bwd_kernel, gH64, dim3(1024), 0, s, dy, w.y, w.h1, P.cls_w2, B, H, p, seed, dh1,
@@ -662,7 +684,18 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   // cell kernel; the c gradients are updated in place (dc for the last layer, dcl inside).
   const int64_t ldr = (int64_t)T * H, slab = (int64_t)B * H;
   const int eb = ew_blocks((int64_t)B * H);
-  for (int t = T - 1; t >= 0; --t) {
+  const bool persist = rnn_use_persist(d);
+  if (persist) {
+    RnnPersist a{};
+    a.B = B; a.T = T; a.H = H; a.L = d.L;
+    for (int l = 0; l < d.L; ++l) {
+      a.P[l] = w.P[l]; a.CI[l] = w.CI[l]; a.ACT[l] = w.ACT[l]; a.CN[l] = w.CN[l]; a.CL[l] = w.CL[l]; a.DZ[l] = DZ[l];
+    }
+    a.dOm = dOm; a.part = ppart; a.dc = dc; a.dcl = dcl; a.p = p; a.seed = seed;
+    a.bar = reinterpret_cast<unsigned*>(psync); a.abort = reinterpret_cast<int*>(psync) + 1;
+    DFD_TRY(launch_rnn_bwd_persist(s, d, a));
+  }
+  for (int t = T - 1; t >= 0 && !persist; --t) {
     for (int l = d.L - 1; l >= 0; --l) {
       const bool last = l == d.L - 1;
       const bool first = t == T - 1;  // nothing flows back from step T yet
@@ -756,7 +789,7 @@ int64_t rnn_scratch_floats(const RnnDims& d) {  // the takes of rnn_backward, pa
   int kc;
   const int64_t sb = bwd_splits(d, &kc);
   const int64_t sizes[] = {d.B * H, d.B * H, BT * H, BT * H, BT * H, BT, 7 * H * H, 6 * H * d.IN, 7 * H,
-                           sb * d.B * H, sb * d.B * H, d.B * H, d.B * H};
+                           sb * d.B * H, sb * d.B * H, d.B * H, d.B * H, rnn_persist_scratch_floats(d), 64};
   int64_t n = d.L * ((BT * 7 * H + 63) & ~int64_t(63));
   for (int64_t v : sizes) n += (v + 63) & ~int64_t(63);
   return n;

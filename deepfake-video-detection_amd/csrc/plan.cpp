@@ -731,6 +731,7 @@ int64_t set_wgrad_stream(int64_t v) { return g_wgrad_stream.exchange(v); }
 int64_t set_mbconv7(int64_t v) { return g_mbconv7.exchange(v); }
 int plan_fused7_blocks(const Plan& p) {
   if (p.dtype != 1) return 0;  // bf16 plans only
+  const TuningScope ts(&p.tune);
   int n = 0;
   for (const Block& b : p.blocks) n += block_fused7(p, b) ? 1 : 0;
   return n > kBarSlots ? 0 : n;

@@ -42,6 +42,34 @@ int attn_backward(hipStream_t s, const float* O, const float* E, const float* at
                   const float* w2, int B, int T, int H, float* scratch, float* dO, float* gw1, float* gb1, float* gw2,
                   float* gb2);
 int colsum(hipStream_t s, const float* X, int M, int N, int ld, float* out);
+// persistent recurrence (k_rnn_persist.hip): the forward's T x L cells and the backward-through-time
+// each as one launch with grid-wide barriers
+struct RnnPersist {  // arguments of both persistent launches
+  int B, T, H, L;
+  const float* P[8];      // packed recurrent weights [7H][H]
+  const float* bias7[8];  // [7H]
+  const float* X0;        // layer-0 x projection [B*T][6H]
+  float* UH[8];           // hidden inputs (rows b*T + t, ld T*H)
+  float* CI[8];           // cell inputs
+  float* ACT[8];          // saved activated gates [B*T][7H]
+  float* CN[8];
+  float* CL[8];
+  float* O;               // last layer's h' [B*T][H]
+  float* DZ[8];           // backward: gate pre-activation gradients [B*T][7H]
+  const float* dOm;       // backward: gradient into O
+  float* part;            // backward: product slices [8][B][H]
+  float* dc;              // backward: gradient into the last layer's c' [B][H]
+  float* dcl;             // backward: gradient into an inner layer's c'
+  float p;
+  uint64_t seed;
+  unsigned* bar;
+  int* abort;
+};
+bool rnn_persist_supported(const RnnDims& d);
+int64_t rnn_persist_scratch_floats(const RnnDims& d);
+int launch_rnn_fwd_persist(hipStream_t s, const RnnDims& d, const RnnPersist& a);
+int launch_rnn_bwd_persist(hipStream_t s, const RnnDims& d, const RnnPersist& a);
+int64_t set_rnn_persist(int64_t v);  // 1 on (default), 0 off; returns the previous value
 // table of 14*L + 8 pointers in the reference's named_parameters() order -> RnnParams
 int rnn_params_from_table(float* const* t, int L, RnnParams& P);
 

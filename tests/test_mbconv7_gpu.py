@@ -5,11 +5,18 @@ projection GEMM -> BN3 finalize -> BN apply) on the same bf16 inputs and weights
 
 Both paths round every stored tensor to bf16 at the same points and sum the per-channel BatchNorm
 statistics in fp32 per frame then double over frames; only the summation order inside a frame
-differs, so a saved tensor may differ by one bf16 ulp in a few elements.  Bounds: relative L2 error
-of every saved activation <= ``SAVED_TOL`` (a 1-ulp flip in every element would be 2^-8 = 3.9e-3),
-BN buffers rtol 1e-4, features rtol 2e-2 (bf16 end to end), gradients cosine >= 0.9995.
-The end-to-end bf16 parity against the fp32 oracle runs through the fused path by default
-(``test_b0_bench_config_gpu.py``, ``test_b0_224_gpu.py``)."""
+differs (and the MFMA k order of the 1x1 products), so a saved tensor differs by one bf16 ulp in
+a few elements; through the training-mode BatchNorms of the following blocks these flips grow
+(measured at 256 frames: first fused block's y1 / y2 / y3 / output 1e-5 / 1.3e-4 / 1.5e-4 / 3.6e-4,
+growing to 7.2e-3 at the last block's output and 7.6e-3 at conv_head; eval mode, no batch
+statistics: 9.5e-5 at the features).  Bounds: the first fused block's tensors (identical inputs on
+both paths: where a fault of the fused kernel shows before propagation blurs it) <= ``FIRST_TOL``;
+every later tensor and the features <= ``DOWNSTREAM_TOL``; BN running buffers (relative L2) <= ``DOWNSTREAM_TOL``;
+gradients cosine >= 0.998 and norm within 3 % (measured worst 0.99937 / 1.2 %: the bf16-vs-fp32
+bound of the oracle tests is cosine 0.98 / 10 %).  Per-channel correctness of every fused output
+against fp32 recomputed from the kernel's own bf16 inputs, and the end-to-end bf16 parity against
+the fp32 oracle, run through the fused path by default (``test_b0_bench_config_gpu.py``,
+``test_b0_224_gpu.py``)."""
 import ctypes
 
 import pytest
@@ -23,7 +30,9 @@ pytestmark = pytest.mark.gpu
 
 HW = 224
 SEED = 41
-SAVED_TOL = 4e-3
+FIRST_TOL = 1e-3
+DOWNSTREAM_TOL = 1.5e-2
+FIRST_FUSED = 49  # saved-tensor index of blocks.5.1's y1 (dfd_b0_saved_tensor order)
 
 
 def _frames(n, cuda):
@@ -88,12 +97,14 @@ def test_fused_training_forward_matches_unfused(cuda, frames):
     assert len(got["saved"]) == len(ref["saved"])
     errs = [_rel(g, r) for g, r in zip(got["saved"], ref["saved"])]
     worst = max(range(len(errs)), key=lambda i: errs[i])
-    print(f"{frames} frames: worst saved-tensor rel err {errs[worst]:.2e} (saved #{worst} of {len(errs)})")
-    assert errs[worst] <= SAVED_TOL, (worst, errs[worst])
-    for n, rb in ref["bufs"].items():
-        torch.testing.assert_close(got["bufs"][n], rb, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n}: {m}")
-    torch.testing.assert_close(got["feats"], ref["feats"], rtol=2e-2, atol=2e-2)
-    assert _rel(got["feats"], ref["feats"]) <= SAVED_TOL
+    print(f"{frames} frames: worst saved-tensor rel err {errs[worst]:.2e} (saved #{worst} of {len(errs)}); "
+          f"all: {[(i, round(e, 5)) for i, e in enumerate(errs) if e > 0]}")
+    assert max(errs[:FIRST_FUSED]) == 0.0, "tensors before the first fused block must be bit-identical"
+    assert max(errs[FIRST_FUSED:FIRST_FUSED + 4]) <= FIRST_TOL, errs[FIRST_FUSED:FIRST_FUSED + 4]
+    assert errs[worst] <= DOWNSTREAM_TOL, (worst, errs[worst])
+    bad = [(n, _rel(got["bufs"][n], rb)) for n, rb in ref["bufs"].items() if _rel(got["bufs"][n], rb) > DOWNSTREAM_TOL]
+    assert not bad, bad
+    assert _rel(got["feats"], ref["feats"]) <= DOWNSTREAM_TOL
 
 
 def test_fused_eval_forward_matches_unfused(cuda):
@@ -102,7 +113,7 @@ def test_fused_eval_forward_matches_unfused(cuda):
     assert got["nb"] == 4
     err = _rel(got["feats"], ref["feats"])
     print(f"eval features rel err {err:.2e}")
-    assert err <= SAVED_TOL
+    assert err <= FIRST_TOL
 
 
 def test_fused_training_step_gradients(cuda):
@@ -127,7 +138,7 @@ def test_fused_training_step_gradients(cuda):
         if rn <= 1e-3 * scale:
             continue  # structurally ~zero (bn3 biases): rounding residue on both sides
         cos = float(gg @ rg) / (float(gg.norm()) * rn + 1e-30)
-        if cos < 0.9995 or abs(float(gg.norm()) - rn) > 1e-2 * rn:
+        if cos < 0.998 or abs(float(gg.norm()) - rn) > 3e-2 * rn:
             bad.append((n, round(cos, 6), round(float(gg.norm()) / rn, 5)))
     print(f"fused vs unfused gradients: {len(out[False])} tensors, outside {bad}")
     assert not bad
