@@ -70,6 +70,7 @@ _SIGS = {
     "dfd_rn_avgpool": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_p]),
     "dfd_pw_conv": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p,
                           ctypes.POINTER(c_i)]),
+    "dfd_sgemm": (c_i, [c_p, c_i, c_i, c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_f, c_p]),
     "dfd_pw_conv_wgrad": (c_i, [c_p, c_i, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i64, c_p,
                                 c_i]),
     "dfd_rnn_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i]),

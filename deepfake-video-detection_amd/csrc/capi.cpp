@@ -435,7 +435,7 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "dw_fwd1") == 0) return dfd::set_dw_fwd1(value);
   if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
   if (key && strcmp(key, "mbconv7") == 0) return dfd::set_mbconv7(value);
-  if (key && strcmp(key, "rnn_persist") == 0) return dfd::set_rnn_persist(value);
+  if (key && strcmp(key, "rnn_step") == 0) return dfd::set_rnn_step(value);
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }
@@ -469,6 +469,14 @@ int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, 
                                           (const dfd::bf16*)R, M, N, K, pro_mode, pro, stats, stat_rows);
   return dfd::launch_pw_gemm<float>(s, (const float*)A, (const float*)W, (float*)C, (const float*)R, M, N, K, pro_mode,
                                     pro, stats, stat_rows);
+  DFD_GUARD_END
+}
+
+int dfd_sgemm(void* stream, int ta, int tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc, int M,
+              int N, int K, float beta, const float* bias) {
+  DFD_GUARD_BEGIN
+  if (!A || !B || !C || M < 0 || N < 0 || K < 0) { dfd::set_error("sgemm: bad arguments", __FILE__, __LINE__); return -1; }
+  return dfd::launch_sgemm((hipStream_t)stream, ta != 0, tb != 0, A, lda, B, ldb, C, ldc, M, N, K, beta, bias);
   DFD_GUARD_END
 }
 

@@ -168,6 +168,10 @@ __device__ __forceinline__ void mb7_ss(const Mb7Bn& bn, int training, float eps,
   }
 }
 
+// development timing (tools/kbench mb7): wall-clock stamp of phase i of this workgroup
+#define MB7_TS(i) \
+  if (a.ts && threadIdx.x == 0) a.ts[blockIdx.x * 24 + (i)] = wall_clock64()
+
 template <int K>
 __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
   constexpr int PAD = K / 2, PW = 7 + K - 1;
@@ -186,6 +190,7 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
   const unsigned G = gridDim.x;
   uint16_t* yb = reinterpret_cast<uint16_t*>(ybuf);
   const int64_t row0 = (int64_t)f * HW7;
+  MB7_TS(0);
 
   // ---- x tile -> LDS (bf16 [49][cin + 8]) ----
   const int XS = cin + 8;
@@ -195,10 +200,12 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
     *reinterpret_cast<uint4*>(xbuf + r * XS + c8) = *reinterpret_cast<const uint4*>(a.x + (row0 + r) * cin + c8);
   }
   __syncthreads();
+  MB7_TS(1);
 
   // ---- conv_pw: y1 = x . W1^T (rounded to bf16) -> ybuf ----
   gemm49<3, 3>(xbuf, XS, cin, a.w1, mid, [&](int m, int n, float v) { ybuf[m * YS + n] = Tr<bf16>::from_f(v); });
   __syncthreads();
+  MB7_TS(2);
   // BN1 per-frame sums (of the rounded values, as the GEMM epilogues of the unfused path) and the
   // saved y1 (training)
   if (training) {
@@ -217,9 +224,13 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
       const int r = v / (mid / 8), c8 = (v - r * (mid / 8)) * 8;
       *reinterpret_cast<uint4*>(a.y1 + (row0 + r) * mid + c8) = *reinterpret_cast<const uint4*>(yb + r * YS + c8);
     }
+    MB7_TS(3);
     if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
+    MB7_TS(4);
     mb7_bn_finalize(a.bn[0], a.part, F, mid, a.momentum, a.eps, dsh);
+    MB7_TS(5);
     if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
+    MB7_TS(6);
   }
 
   // ---- conv_dw on BN1+SiLU(y1), 64-channel chunks; y2 (bf16) replaces y1 in ybuf ----
@@ -276,14 +287,19 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
     }
   }
   __syncthreads();
+  MB7_TS(7);
   if (training) {
     for (int v = tid; v < HW7 * (mid / 8); v += 256) {
       const int r = v / (mid / 8), c8 = (v - r * (mid / 8)) * 8;
       *reinterpret_cast<uint4*>(a.y2 + (row0 + r) * mid + c8) = *reinterpret_cast<const uint4*>(yb + r * YS + c8);
     }
+    MB7_TS(8);
     if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
+    MB7_TS(9);
     mb7_bn_finalize(a.bn[1], a.part, F, mid, a.momentum, a.eps, dsh);
+    MB7_TS(10);
     if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
+    MB7_TS(11);
   }
 
   // ---- BN2 + SiLU: a2 (fp32) -> squeeze sums; s2 = bf16(a2) in place (and saved) ----
@@ -306,6 +322,7 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
     sqs[c + 1] = sum.y * (1.0f / HW7);
   }
   __syncthreads();
+  MB7_TS(12);
   // ---- SE: rpre = Wr sq + br ; z = silu(rpre) ; gate = sigmoid(We z + be) ----
   for (int j = wave; j < rd; j += 4) {
     float v = 0.f;
@@ -330,6 +347,7 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
     }
   }
   __syncthreads();
+  MB7_TS(13);
   // ---- a2g = bf16(s2 * gate) in place (the PRO_GATE operand of the unfused projection) ----
   for (int v = tid; v < HW7 * (mid / 2); v += 256) {
     const int p = v / (mid / 2), c = (v - p * (mid / 2)) * 2;
@@ -338,12 +356,14 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
     *cell = pack2bf(x2.x * gts[c], x2.y * gts[c + 1]);
   }
   __syncthreads();
+  MB7_TS(14);
 
   // ---- conv_pwl: y3 = a2g . W3^T -> LDS tile (bf16 [49][cout + 8]) ----
   const int TS = cout + 8;
   bf16* ytile = reinterpret_cast<bf16*>(work);
   gemm49<3, 6>(ybuf, YS, mid, a.w3, cout, [&](int m, int n, float v) { ytile[m * TS + n] = Tr<bf16>::from_f(v); });
   __syncthreads();
+  MB7_TS(15);
   const uint16_t* yt = reinterpret_cast<const uint16_t*>(ytile);
   if (training) {
     for (int c = tid; c < cout; c += 256) {
@@ -360,9 +380,13 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
       const int r = v / (cout / 8), c8 = (v - r * (cout / 8)) * 8;
       *reinterpret_cast<uint4*>(a.y3 + (row0 + r) * cout + c8) = *reinterpret_cast<const uint4*>(yt + r * TS + c8);
     }
+    MB7_TS(16);
     if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
+    MB7_TS(17);
     mb7_bn_finalize(a.bn[2], a.part, F, cout, a.momentum, a.eps, dsh);
+    MB7_TS(18);
     if (!grid_sync(a.bar, bar_target += G, a.abort)) return;
+    MB7_TS(19);
   }
   // ---- BN3 (+ skip) -> block output ----
   for (int v = tid; v < HW7 * (cout / 8); v += 256) {
@@ -379,6 +403,7 @@ __global__ __launch_bounds__(256, 1) void mbconv7_fwd_kernel(Mb7Args a) {
     }
     st8(a.xo + (row0 + r) * cout + c8, o);
   }
+  MB7_TS(20);
 }
 
 bool mbconv7_supported(int frames, int H, int W, int cin, int mid, int cout, int rd, int k, int s) {

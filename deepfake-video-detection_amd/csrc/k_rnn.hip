@@ -115,8 +115,127 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const float* __restrict__ A,
       }
 }
 
+// Large-tile form for the big products (weight gradients over all B*T rows, input projections):
+// 128 x 64 tile per 256-thread block, BK = 16, LDS double-buffered (one barrier per k-step), k-major
+// LDS rows padded by 16 floats (the four k rows of an MFMA operand read hit disjoint bank quarters);
+// wave w owns a 64 x 32 quarter = 4 x 2 MFMA blocks.  Needs M % 128 == 0, N % 64 == 0, K % 16 == 0
+// and 16-B aligned rows (sgemm_go checks; other shapes take sgemm_kernel).
+constexpr int SB_M = 128, SB_N = 64, SB_K = 16, SB_PM = SB_M + 16, SB_PN = SB_N + 16;
+
+template <bool T_, int R>  // R rows (m or n) x SB_K of one operand -> registers (R*SB_K/4/256 float4 per thread)
+__device__ __forceinline__ void sb_load(const float* __restrict__ P, int ld, int r0, int k0, float4 (&v)[R / 64]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < R / 64; ++i) {
+    const int e = tid + 256 * i;
+    if (T_) {  // contiguous along r: k row e / (R/4), r4 = (e % (R/4)) * 4
+      const int k = e / (R / 4), r4 = (e % (R / 4)) * 4;
+      v[i] = *reinterpret_cast<const float4*>(P + (int64_t)(k0 + k) * ld + r0 + r4);
+    } else {   // contiguous along k: r = e / 4, k4 = (e % 4) * 4
+      const int r = e >> 2, k4 = (e & 3) * 4;
+      v[i] = *reinterpret_cast<const float4*>(P + (int64_t)(r0 + r) * ld + k0 + k4);
+    }
+  }
+}
+template <bool T_, int R, int PR>
+__device__ __forceinline__ void sb_store(float* S, const float4 (&v)[R / 64]) {  // S: [SB_K][PR] k-major
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < R / 64; ++i) {
+    const int e = tid + 256 * i;
+    if (T_) {
+      const int k = e / (R / 4), r4 = (e % (R / 4)) * 4;
+      *reinterpret_cast<float4*>(S + k * PR + r4) = v[i];
+    } else {
+      const int r = e >> 2, k4 = (e & 3) * 4;
+      S[(k4 + 0) * PR + r] = v[i].x;
+      S[(k4 + 1) * PR + r] = v[i].y;
+      S[(k4 + 2) * PR + r] = v[i].z;
+      S[(k4 + 3) * PR + r] = v[i].w;
+    }
+  }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void sgemm_big_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
+                                                        int ldb, float* __restrict__ C, int ldc, int K, float beta,
+                                                        const float* __restrict__ bias) {
+  __shared__ __attribute__((aligned(16))) float As[2][SB_K * SB_PM];
+  __shared__ __attribute__((aligned(16))) float Bs[2][SB_K * SB_PN];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.y * SB_M, n0 = blockIdx.x * SB_N;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 32;
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float4 va[SB_M / 64], vb[SB_N / 64];
+  sb_load<TA, SB_M>(A, lda, m0, 0, va);
+  sb_load<TB, SB_N>(B, ldb, n0, 0, vb);
+  sb_store<TA, SB_M, SB_PM>(As[0], va);
+  sb_store<TB, SB_N, SB_PN>(Bs[0], vb);
+  __syncthreads();
+  const int nk = K / SB_K;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      sb_load<TA, SB_M>(A, lda, m0, (kt + 1) * SB_K, va);
+      sb_load<TB, SB_N>(B, ldb, n0, (kt + 1) * SB_K, vb);
+    }
+    const float* as = As[cur] + (lane >> 4) * SB_PM + wm + (lane & 15);
+    const float* bs = Bs[cur] + (lane >> 4) * SB_PN + wn + (lane & 15);
+#pragma unroll
+    for (int s4 = 0; s4 < SB_K / 4; ++s4) {
+      float af[4], bf[2];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) af[a] = as[s4 * 4 * SB_PM + a * 16];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) bf[b] = bs[s4 * 4 * SB_PN + b * 16];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      sb_store<TA, SB_M, SB_PM>(As[cur ^ 1], va);
+      sb_store<TB, SB_N, SB_PN>(Bs[cur ^ 1], vb);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm + a * 16 + 4 * (lane >> 4) + r, n = n0 + wn + b * 16 + (lane & 15);
+        float v = acc[a][b][r];
+        if (bias) v += bias[n];
+        float* c = C + (int64_t)m * ldc + n;
+        *c = beta != 0.f ? beta * *c + v : v;
+      }
+}
+
+static bool sgemm_big_ok(const float* A, int lda, const float* B, int ldb, int M, int N, int K) {
+  return M % SB_M == 0 && N % SB_N == 0 && K % SB_K == 0 && K > 0 && lda % 4 == 0 && ldb % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0;
+}
+
 static int sgemm_go(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C,
                     int ldc, int M, int N, int K, float beta, const float* bias, int splits, int kc, int64_t zs) {
+  if (splits == 1 && sgemm_big_ok(A, lda, B, ldb, M, N, K)) {
+    const dim3 g((unsigned)(N / SB_N), (unsigned)(M / SB_M));
+#define DFD_SB(a_, b_) \
+  hipLaunchKernelGGL((sgemm_big_kernel<a_, b_>), g, dim3(256), 0, s, A, lda, B, ldb, C, ldc, K, beta, bias)
+    if (!ta && !tb) DFD_SB(false, false);
+    else if (!ta && tb) DFD_SB(false, true);
+    else if (ta && !tb) DFD_SB(true, false);
+    else DFD_SB(true, true);
+#undef DFD_SB
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   const dim3 grid((unsigned)cdiv(N, SG_T), (unsigned)cdiv(M, SG_T), (unsigned)splits);
 #define DFD_SG(a_, b_) \
   hipLaunchKernelGGL((sgemm_kernel<a_, b_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, beta, bias, kc, zs)
@@ -519,11 +638,11 @@ __global__ void rnn_mask_bwd_kernel(float* __restrict__ dOm, const float* __rest
 static int ew_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 2048)); }
 
 // ------------------------------------------------------------------ host orchestration
-// the persistent recurrence (k_rnn_persist.hip) where its shape rules hold: 1 on (default), 0 off
-static std::atomic<int64_t> g_rnn_persist{1};
-int64_t set_rnn_persist(int64_t v) { return g_rnn_persist.exchange(v); }
-static bool rnn_use_persist(const RnnDims& d) {
-  return g_rnn_persist.load(std::memory_order_relaxed) != 0 && rnn_persist_supported(d);
+// one launch per cell (k_rnn_step.hip) where its shape rules hold: 1 on (default), 0 off
+static std::atomic<int64_t> g_rnn_step{1};
+int64_t set_rnn_step(int64_t v) { return g_rnn_step.exchange(v); }
+static bool rnn_use_step(const RnnDims& d) {
+  return g_rnn_step.load(std::memory_order_relaxed) != 0 && rnn_step_supported(d);
 }
 
 // K slices of the per-step recurrent products (fixed per shape; the workspace holds them)
@@ -532,7 +651,7 @@ static int bwd_splits(const RnnDims& d, int* kc) { return sgemm_splits(d.B, d.H,
 
 struct RnnWs {
   float *xs, *X0, *G, *P[8], *bias7[8], *WX0, *ACT[8], *CN[8], *CL[8], *UH[8], *CI[8], *O, *Om, *E, *att, *ctx, *h1,
-      *y, *sync;
+      *y;
   int64_t floats;  // extent of the layout (rnn_work_floats)
 };
 // one layout function for both the size query (w = nullptr) and the pointers
@@ -555,7 +674,6 @@ static RnnWs rnn_ws(const RnnDims& d, float* w) {
   s.att = take(BT);
   s.ctx = take((int64_t)d.B * H); s.h1 = take((int64_t)d.B * H);
   s.y = take(d.B);
-  s.sync = take(64);  // grid-barrier counter + abort flag of the persistent recurrence
   s.floats = off;
   return s;
 }
@@ -587,18 +705,19 @@ int rnn_forward(hipStream_t s, const RnnDims& d, const RnnParams& P, const float
   int kc;
   const int sf = fwd_splits(d, &kc);
   const int eb = ew_blocks((int64_t)B * H);
-  if (rnn_use_persist(d)) {  // the whole recurrence as one launch (k_rnn_persist.hip)
-    RnnPersist a{};
+  const bool step = rnn_use_step(d);
+  if (step) {  // one launch per cell (k_rnn_step.hip)
+    RnnStep a{};
     a.B = B; a.T = T; a.H = H; a.L = d.L;
     for (int l = 0; l < d.L; ++l) {
       a.P[l] = w.P[l]; a.bias7[l] = w.bias7[l]; a.UH[l] = w.UH[l]; a.CI[l] = w.CI[l];
       a.ACT[l] = w.ACT[l]; a.CN[l] = w.CN[l]; a.CL[l] = w.CL[l];
     }
     a.X0 = w.X0; a.O = w.O; a.p = p; a.seed = seed;
-    a.bar = reinterpret_cast<unsigned*>(w.sync); a.abort = reinterpret_cast<int*>(w.sync) + 1;
-    DFD_TRY(launch_rnn_fwd_persist(s, d, a));
+    for (int t = 0; t < T; ++t)
+      for (int l = 0; l < d.L; ++l) DFD_TRY(launch_rnn_step_fwd(s, a, t, l));
   }
-  for (int t = 0; t < T && !rnn_use_persist(d); ++t) {
+  for (int t = 0; t < T && !step; ++t) {
     for (int l = 0; l < d.L; ++l) {
       // recurrent product h_in @ P_l^T in K slices (summed by the cell kernel)
       DFD_TRY(launch_sgemm_part(s, false, false, w.UH[l] + (int64_t)t * H, (int)ldr, w.P[l], H, w.G, B, 7 * H, H, sf,
@@ -662,8 +781,7 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   float* dhls = take((int64_t)sb * B * H);  // K slices: gradient into an inner layer's output
   float* dc = take((int64_t)B * H);         // gradient into the last layer's c'
   float* dcl = take((int64_t)B * H);        // gradient into an inner layer's c'
-  float* ppart = take(rnn_persist_scratch_floats(d));  // persistent path: product slices
-  float* psync = take(64);                              // persistent path: barrier counter + abort
+  float* spart = take((int64_t)rnn_step_slices() * B * H);  // per-cell path: product slices
   // classifier tail
   const dim3 gH((unsigned)cdiv(H, 256)), gH64((unsigned)cdiv(H, 64));
   hipLaunchKernelGGL(rnn_cls_bwd_kernel, gH64, dim3(1024), 0, s, dy, w.y, w.h1, P.cls_w2, B, H, p, seed, dh1,
@@ -684,18 +802,21 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   // cell kernel; the c gradients are updated in place (dc for the last layer, dcl inside).
   const int64_t ldr = (int64_t)T * H, slab = (int64_t)B * H;
   const int eb = ew_blocks((int64_t)B * H);
-  const bool persist = rnn_use_persist(d);
-  if (persist) {
-    RnnPersist a{};
-    a.B = B; a.T = T; a.H = H; a.L = d.L;
-    for (int l = 0; l < d.L; ++l) {
-      a.P[l] = w.P[l]; a.CI[l] = w.CI[l]; a.ACT[l] = w.ACT[l]; a.CN[l] = w.CN[l]; a.CL[l] = w.CL[l]; a.DZ[l] = DZ[l];
+  const bool step = rnn_use_step(d);
+  for (int t = T - 1; t >= 0 && step; --t) {  // k_rnn_step.hip's product, 8 slices
+    for (int l = d.L - 1; l >= 0; --l) {
+      const bool last = l == d.L - 1;
+      const bool first = t == T - 1;
+      hipLaunchKernelGGL(rnn_cell_bwd_kernel, dim3(eb), dim3(256), 0, s, last ? dOm + (int64_t)t * H : nullptr,
+                         (int)ldr, (last && first) ? nullptr : spart, rnn_step_slices(), slab, last ? 0 : 1, p, seed,
+                         (uint32_t)l, last ? (first ? nullptr : dc) : dcl, w.ACT[l], w.CN[l], w.CL[l],
+                         w.CI[l] + (int64_t)t * H, (int)ldr, B, T, t, H, DZ[l], l > 0 ? dcl : dc);
+      DFD_HIP_CHECK(hipGetLastError());
+      if (l > 0 || t > 0)
+        DFD_TRY(launch_rnn_dh(s, DZ[l] + (int64_t)t * 7 * H, (int64_t)T * 7 * H, w.P[l], B, H, spart));
     }
-    a.dOm = dOm; a.part = ppart; a.dc = dc; a.dcl = dcl; a.p = p; a.seed = seed;
-    a.bar = reinterpret_cast<unsigned*>(psync); a.abort = reinterpret_cast<int*>(psync) + 1;
-    DFD_TRY(launch_rnn_bwd_persist(s, d, a));
   }
-  for (int t = T - 1; t >= 0 && !persist; --t) {
+  for (int t = T - 1; t >= 0 && !step; --t) {
     for (int l = d.L - 1; l >= 0; --l) {
       const bool last = l == d.L - 1;
       const bool first = t == T - 1;  // nothing flows back from step T yet
@@ -789,7 +910,7 @@ int64_t rnn_scratch_floats(const RnnDims& d) {  // the takes of rnn_backward, pa
   int kc;
   const int64_t sb = bwd_splits(d, &kc);
   const int64_t sizes[] = {d.B * H, d.B * H, BT * H, BT * H, BT * H, BT, 7 * H * H, 6 * H * d.IN, 7 * H,
-                           sb * d.B * H, sb * d.B * H, d.B * H, d.B * H, rnn_persist_scratch_floats(d), 64};
+                           sb * d.B * H, sb * d.B * H, d.B * H, d.B * H, (int64_t)rnn_step_slices() * d.B * H};
   int64_t n = d.L * ((BT * 7 * H + 63) & ~int64_t(63));
   for (int64_t v : sizes) n += (v + 63) & ~int64_t(63);
   return n;

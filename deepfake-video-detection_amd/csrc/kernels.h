@@ -88,6 +88,7 @@ struct Mb7Args {
   float *sq, *rpre, *gate, *part;   // SE saved vectors; per-frame BN partial sums [F][2][C]
   unsigned* bar;                    // zeroed grid-barrier counter of this launch
   int* abort;                       // zeroed; set if the grid was not co-resident
+  unsigned long long* ts;           // development timing: per-workgroup phase timestamps (nullptr: off)
 };
 bool mbconv7_supported(int frames, int H, int W, int cin, int mid, int cout, int rd, int k, int s);
 int launch_mbconv7_fwd(hipStream_t s, const Mb7Args& a);

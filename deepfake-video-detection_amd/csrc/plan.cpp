@@ -331,8 +331,10 @@ inline bool probe_hit(const Plan& p, int kind, const Block* b) {
   } while (0)
 #define PROBED(KIND, BLK, EXPR) PROBED_ON(KIND, BLK, s, EXPR)
 
-// the fused 7x7-stage MBConv forward (k_mbconv7.hip) for the bf16 plan: 1 on (default), 0 off
-std::atomic<int64_t> g_mbconv7{1};
+// the fused 7x7-stage MBConv forward (k_mbconv7.hip) for the bf16 plan: 0 off (default), 1 on.
+// Off by default: measured 394 us per block (training) against ~135 us for the unfused launches
+// (six grid barriers at ~14 us each, per-frame weight re-reads from L2).
+std::atomic<int64_t> g_mbconv7{0};
 // blocks of the 7x7 stages that run as one fused launch (k_mbconv7.hip) in the bf16 forward
 static bool block_fused7(const Plan& p, const Block& b) {
   return !b.ds && b.o_s2 >= 0 && tune_or(TK_MBCONV7, g_mbconv7.load(std::memory_order_relaxed)) != 0 &&

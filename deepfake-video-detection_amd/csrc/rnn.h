@@ -42,9 +42,9 @@ int attn_backward(hipStream_t s, const float* O, const float* E, const float* at
                   const float* w2, int B, int T, int H, float* scratch, float* dO, float* gw1, float* gb1, float* gw2,
                   float* gb2);
 int colsum(hipStream_t s, const float* X, int M, int N, int ld, float* out);
-// persistent recurrence (k_rnn_persist.hip): the forward's T x L cells and the backward-through-time
-// each as one launch with grid-wide barriers
-struct RnnPersist {  // arguments of both persistent launches
+// one launch per recurrent cell (k_rnn_step.hip): the forward cell with its own gate products, and
+// the backward's product into the next cell's hidden gradient as KSL = rnn_step_slices() K slices
+struct RnnStep {
   int B, T, H, L;
   const float* P[8];      // packed recurrent weights [7H][H]
   const float* bias7[8];  // [7H]
@@ -55,21 +55,14 @@ struct RnnPersist {  // arguments of both persistent launches
   float* CN[8];
   float* CL[8];
   float* O;               // last layer's h' [B*T][H]
-  float* DZ[8];           // backward: gate pre-activation gradients [B*T][7H]
-  const float* dOm;       // backward: gradient into O
-  float* part;            // backward: product slices [8][B][H]
-  float* dc;              // backward: gradient into the last layer's c' [B][H]
-  float* dcl;             // backward: gradient into an inner layer's c'
   float p;
   uint64_t seed;
-  unsigned* bar;
-  int* abort;
 };
-bool rnn_persist_supported(const RnnDims& d);
-int64_t rnn_persist_scratch_floats(const RnnDims& d);
-int launch_rnn_fwd_persist(hipStream_t s, const RnnDims& d, const RnnPersist& a);
-int launch_rnn_bwd_persist(hipStream_t s, const RnnDims& d, const RnnPersist& a);
-int64_t set_rnn_persist(int64_t v);  // 1 on (default), 0 off; returns the previous value
+bool rnn_step_supported(const RnnDims& d);
+int rnn_step_slices();
+int launch_rnn_step_fwd(hipStream_t s, const RnnStep& a, int t, int l);
+int launch_rnn_dh(hipStream_t s, const float* DZ, int64_t ldz, const float* P, int B, int H, float* part);
+int64_t set_rnn_step(int64_t v);  // 1 on (default), 0 = K-sliced products + cell kernels; returns the previous value
 // table of 14*L + 8 pointers in the reference's named_parameters() order -> RnnParams
 int rnn_params_from_table(float* const* t, int L, RnnParams& P);
 

@@ -221,6 +221,13 @@ DFD_API int dfd_pw_conv_wgrad(void* stream, int dtype, const void* dY, const voi
                               int pro_mode, const float* scale, const float* shift, const float* gate,
                               int rows_per_frame, float* slab, int64_t slab_floats, float* dW, int accumulate);
 
+/* fp32 GEMM of the recurrent models' plain products (test seam): C[m][n] = beta*C + sum_k A(m,k) B(n,k)
+ * (+ bias[n]); A(m,k) = ta ? A[k*lda+m] : A[m*lda+k], B(n,k) = tb ? B[k*ldb+n] : B[n*ldb+k].  The
+ * kernels behind nn.Linear / nn.LSTM input projections and weight gradients of LogicRNNLSTM,
+ * CNNLSTMHybrid and the GCN head (no reference counterpart: torch's own GEMMs there). */
+DFD_API int dfd_sgemm(void* stream, int ta, int tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc,
+                      int M, int N, int K, float beta, const float* bias);
+
 /* ---- LogicRNNLSTM (src/RNNModel.py:43-147), fp32 ----
  * Replaces LogicRNNLSTM.forward (RNNModel.py:81-133) and its autograd backward.
  * x: (B, T, IN) fp32 contiguous.  order: the reference's sort_idx of lengths.sort(0, descending=True)

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "../deepfake-video-detection_amd/csrc/kernels.h"
@@ -192,6 +193,69 @@ int main(int argc, char** argv) {
     b.run("pwl_wgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
       return launch_pw_wgrad<bf16>(b.s, A, B, Mo, k.cout, C1, PRO_BN_SILU_G, pg, slab, slab_cap, dW, false);
     });
+    if (!k.ds && k.hin == 7 && k.s == 1 && mbconv7_supported(F, 7, 7, k.cin, k.mid, k.cout, k.cin / 4, k.k, 1)) {
+      // the fused 7x7 MBConv forward (k_mbconv7.hip), training and eval, then its per-phase timing
+      static unsigned* bar = nullptr;
+      static unsigned long long* ts = nullptr;
+      static float* bnv = nullptr;
+      if (!bar) {
+        CK(hipMalloc(&bar, 256));
+        CK(hipMalloc(&ts, (size_t)F * 24 * 8));
+        CK(hipMalloc(&bnv, 24 * 2048 * 4));
+        CK(hipMemset(bnv, 0, 24 * 2048 * 4));
+      }
+      Mb7Args a{};
+      a.frames = F; a.cin = k.cin; a.mid = k.mid; a.cout = k.cout; a.rd = k.cin / 4; a.k = k.k;
+      a.skip = k.cin == k.cout; a.momentum = 0.1f; a.eps = 1e-5f;
+      a.x = A; a.w1 = D; a.wdw = W; a.wr = W; a.br = W; a.we = W; a.be = W; a.w3 = D + (1 << 20);
+      for (int q = 0; q < 3; ++q) {
+        float* o = bnv + q * 8 * 2048;
+        a.bn[q] = Mb7Bn{o, o + 2048, o + 2 * 2048, o + 3 * 2048, o + 4 * 2048, o + 5 * 2048, o + 6 * 2048,
+                        o + 7 * 2048};
+      }
+      a.y1 = B; a.y2 = C; a.s2 = C + (int64_t)F * 49 * 1152; a.y3 = B + (int64_t)F * 49 * 1152;
+      a.xo = C + 2 * (int64_t)F * 49 * 1152;
+      a.sq = gate; a.rpre = coef; a.gate = gate; a.part = stats;
+      a.bar = bar; a.abort = reinterpret_cast<int*>(bar) + 63;
+      const double mb = 2.0 * (Mo * k.cin + Mo * k.cout + 4.0 * Mo * k.mid);
+      for (int tr = 1; tr >= 0; --tr) {
+        a.training = tr;
+        a.ts = nullptr;
+        auto go = [&] {
+          CK(hipMemsetAsync(bar, 0, 256, b.s));
+          return launch_mbconv7_fwd(b.s, a);
+        };
+        snprintf(nm, sizeof nm, "b%zu %s k%d %d>%d>%d", i, tr ? "train" : "eval", k.k, k.cin, k.mid, k.cout);
+        b.run("mb7", nm, mb, go);
+        if (b.filter.empty() || std::string("mb7").find(b.filter) == std::string::npos) continue;
+        a.ts = ts;
+        CK(hipMemset(ts, 0, (size_t)F * 24 * 8));
+        go();
+        CK(hipStreamSynchronize(b.s));
+        std::vector<unsigned long long> h((size_t)F * 24);
+        CK(hipMemcpy(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost));
+        // per phase: mean over workgroups of (stamp[i] - stamp[prev recorded]); 100 MHz wall clock
+        printf("   phases (us, mean / max over %d WGs):", F);
+        int prev = 0;
+        for (int ph = 1; ph <= 20; ++ph) {
+          if (h[ph] == 0) continue;
+          double sum = 0, mx = 0;
+          for (int w = 0; w < F; ++w) {
+            const double d = (double)(h[(size_t)w * 24 + ph] - h[(size_t)w * 24 + prev]) * 0.01;
+            sum += d;
+            mx = d > mx ? d : mx;
+          }
+          printf(" %d:%.1f/%.1f", ph, sum / F, mx);
+          prev = ph;
+        }
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int w = 0; w < F; ++w) {
+          t0 = std::min(t0, h[(size_t)w * 24]);
+          t1 = std::max(t1, h[(size_t)w * 24 + 20]);
+        }
+        printf("  | first start -> last end %.1f us\n", (t1 - t0) * 0.01);
+      }
+    }
     BnBwdIn bo{};
     bo.dZ = A; bo.mean = mean; bo.invstd = invstd; bo.scale = sc; bo.shift = sh;
     snprintf(nm, sizeof nm, "b%zu bn3 %ldx%d", i, (long)Mo, k.cout);
