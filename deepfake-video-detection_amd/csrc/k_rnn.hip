@@ -116,38 +116,39 @@ __global__ __launch_bounds__(256) void sgemm_kernel(const float* __restrict__ A,
 }
 
 // Large-tile form for the big products (weight gradients over all B*T rows, input projections):
-// 128 x 64 tile per 256-thread block, BK = 16, LDS double-buffered (one barrier per k-step), k-major
+// 128 x 64 tile per 256-thread block, BK = 32, LDS double-buffered (one barrier per k-step), k-major
 // LDS rows padded by 16 floats (the four k rows of an MFMA operand read hit disjoint bank quarters);
 // wave w owns a 64 x 32 quarter = 4 x 2 MFMA blocks.  Needs M % 128 == 0, N % 64 == 0, K % 16 == 0
 // and 16-B aligned rows (sgemm_go checks; other shapes take sgemm_kernel).
-constexpr int SB_M = 128, SB_N = 64, SB_K = 16, SB_PM = SB_M + 16, SB_PN = SB_N + 16;
+constexpr int SB_M = 128, SB_N = 64, SB_K = 32, SB_PM = SB_M + 16, SB_PN = SB_N + 16;
 
-template <bool T_, int R>  // R rows (m or n) x SB_K of one operand -> registers (R*SB_K/4/256 float4 per thread)
-__device__ __forceinline__ void sb_load(const float* __restrict__ P, int ld, int r0, int k0, float4 (&v)[R / 64]) {
+template <int R> constexpr int sb_nv() { return R * SB_K / 4 / 256; }  // float4 per thread of an R x SB_K operand tile
+template <bool T_, int R>  // R rows (m or n) x SB_K of one operand -> registers
+__device__ __forceinline__ void sb_load(const float* __restrict__ P, int ld, int r0, int k0, float4 (&v)[sb_nv<R>()]) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < R / 64; ++i) {
+  for (int i = 0; i < sb_nv<R>(); ++i) {
     const int e = tid + 256 * i;
     if (T_) {  // contiguous along r: k row e / (R/4), r4 = (e % (R/4)) * 4
       const int k = e / (R / 4), r4 = (e % (R / 4)) * 4;
       v[i] = *reinterpret_cast<const float4*>(P + (int64_t)(k0 + k) * ld + r0 + r4);
-    } else {   // contiguous along k: r = e / 4, k4 = (e % 4) * 4
-      const int r = e >> 2, k4 = (e & 3) * 4;
+    } else {   // contiguous along k: r = e / (SB_K/4), k4 = (e % (SB_K/4)) * 4
+      const int r = e / (SB_K / 4), k4 = (e % (SB_K / 4)) * 4;
       v[i] = *reinterpret_cast<const float4*>(P + (int64_t)(r0 + r) * ld + k0 + k4);
     }
   }
 }
 template <bool T_, int R, int PR>
-__device__ __forceinline__ void sb_store(float* S, const float4 (&v)[R / 64]) {  // S: [SB_K][PR] k-major
+__device__ __forceinline__ void sb_store(float* S, const float4 (&v)[sb_nv<R>()]) {  // S: [SB_K][PR] k-major
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < R / 64; ++i) {
+  for (int i = 0; i < sb_nv<R>(); ++i) {
     const int e = tid + 256 * i;
     if (T_) {
       const int k = e / (R / 4), r4 = (e % (R / 4)) * 4;
       *reinterpret_cast<float4*>(S + k * PR + r4) = v[i];
     } else {
-      const int r = e >> 2, k4 = (e & 3) * 4;
+      const int r = e / (SB_K / 4), k4 = (e % (SB_K / 4)) * 4;
       S[(k4 + 0) * PR + r] = v[i].x;
       S[(k4 + 1) * PR + r] = v[i].y;
       S[(k4 + 2) * PR + r] = v[i].z;
@@ -159,7 +160,7 @@ __device__ __forceinline__ void sb_store(float* S, const float4 (&v)[R / 64]) { 
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void sgemm_big_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B,
                                                         int ldb, float* __restrict__ C, int ldc, int K, float beta,
-                                                        const float* __restrict__ bias) {
+                                                        const float* __restrict__ bias, int kc, int64_t zstride) {
   __shared__ __attribute__((aligned(16))) float As[2][SB_K * SB_PM];
   __shared__ __attribute__((aligned(16))) float Bs[2][SB_K * SB_PN];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -170,18 +171,20 @@ __global__ __launch_bounds__(256) void sgemm_big_kernel(const float* __restrict_
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float4 va[SB_M / 64], vb[SB_N / 64];
-  sb_load<TA, SB_M>(A, lda, m0, 0, va);
-  sb_load<TB, SB_N>(B, ldb, n0, 0, vb);
+  // K slice of this z (split-K partials: slice z writes C + z * zstride; kc % SB_K == 0)
+  const int kb = blockIdx.z * kc, nk = (min(K, kb + kc) - kb) / SB_K;
+  C += (int64_t)blockIdx.z * zstride;
+  float4 va[sb_nv<SB_M>()], vb[sb_nv<SB_N>()];
+  sb_load<TA, SB_M>(A, lda, m0, kb, va);
+  sb_load<TB, SB_N>(B, ldb, n0, kb, vb);
   sb_store<TA, SB_M, SB_PM>(As[0], va);
   sb_store<TB, SB_N, SB_PN>(Bs[0], vb);
   __syncthreads();
-  const int nk = K / SB_K;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      sb_load<TA, SB_M>(A, lda, m0, (kt + 1) * SB_K, va);
-      sb_load<TB, SB_N>(B, ldb, n0, (kt + 1) * SB_K, vb);
+      sb_load<TA, SB_M>(A, lda, m0, kb + (kt + 1) * SB_K, va);
+      sb_load<TB, SB_N>(B, ldb, n0, kb + (kt + 1) * SB_K, vb);
     }
     const float* as = As[cur] + (lane >> 4) * SB_PM + wm + (lane & 15);
     const float* bs = Bs[cur] + (lane >> 4) * SB_PN + wn + (lane & 15);
@@ -217,17 +220,19 @@ __global__ __launch_bounds__(256) void sgemm_big_kernel(const float* __restrict_
       }
 }
 
-static bool sgemm_big_ok(const float* A, int lda, const float* B, int ldb, int M, int N, int K) {
-  return M % SB_M == 0 && N % SB_N == 0 && K % SB_K == 0 && K > 0 && lda % 4 == 0 && ldb % 4 == 0 &&
-         (reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0;
+static bool sgemm_big_ok(const float* A, int lda, const float* B, int ldb, int M, int N, int K, int kc) {
+  return M % SB_M == 0 && N % SB_N == 0 && K % SB_K == 0 && kc % SB_K == 0 && K > 0 && lda % 4 == 0 &&
+         ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0;
 }
 
 static int sgemm_go(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* C,
                     int ldc, int M, int N, int K, float beta, const float* bias, int splits, int kc, int64_t zs) {
-  if (splits == 1 && sgemm_big_ok(A, lda, B, ldb, M, N, K)) {
-    const dim3 g((unsigned)(N / SB_N), (unsigned)(M / SB_M));
-#define DFD_SB(a_, b_) \
-  hipLaunchKernelGGL((sgemm_big_kernel<a_, b_>), g, dim3(256), 0, s, A, lda, B, ldb, C, ldc, K, beta, bias)
+  if (sgemm_big_ok(A, lda, B, ldb, M, N, K, splits == 1 ? K : kc)) {
+    const dim3 g((unsigned)(N / SB_N), (unsigned)(M / SB_M), (unsigned)splits);
+    const int kcb = splits == 1 ? K : kc;
+#define DFD_SB(a_, b_)                                                                                           \
+  hipLaunchKernelGGL((sgemm_big_kernel<a_, b_>), g, dim3(256), 0, s, A, lda, B, ldb, C, ldc, K, beta, bias, kcb, \
+                     zs)
     if (!ta && !tb) DFD_SB(false, false);
     else if (!ta && tb) DFD_SB(false, true);
     else if (ta && !tb) DFD_SB(true, false);
@@ -252,6 +257,15 @@ int launch_sgemm(hipStream_t s, bool ta, bool tb, const float* A, int lda, const
                  int M, int N, int K, float beta, const float* bias) {
   if (M <= 0 || N <= 0) return 0;
   return sgemm_go(s, ta, tb, A, lda, B, ldb, C, ldc, M, N, K, beta, bias, 1, std::max(K, 1), 0);
+}
+
+// K slices of the big-tile weight-gradient products (M x N outputs over K = B*T rows): enough
+// 128 x 64 tiles x slices for ~2 workgroups per CU, slices of >= 256 k, at most 8
+int sgemm_wsplits(int M, int N, int K, int* kc) {
+  const int tiles = std::max(1, (M / SB_M) * (N / SB_N));
+  int sp = std::min(std::min(8, std::max(1, K / 256)), std::max(1, (512 + tiles - 1) / tiles));
+  *kc = cdiv(cdiv(std::max(K, 1), sp), SB_K) * SB_K;
+  return cdiv(std::max(K, 1), *kc);
 }
 
 // K slices for a product of few output tiles: aim at ~256 workgroups, at least 64 k per slice;
@@ -431,8 +445,10 @@ __global__ void rnn_cell_bwd_kernel(const float* __restrict__ dh_a, int dh_a_ld,
 }
 
 // scatter packed gradients back into the per-gate weight gradients of layer l (accumulating)
-__global__ void rnn_scatter_kernel(RnnLayerW gw, int in, int H, int layer, const float* __restrict__ dP,
-                                   const float* __restrict__ dWX0, const float* __restrict__ dbias7) {
+// dP / dWX0 arrive as np / nx K slices (split-K partials, slice stride = the matrix size), added in order
+__global__ void rnn_scatter_kernel(RnnLayerW gw, int in, int H, int layer, const float* __restrict__ dP, int np,
+                                   const float* __restrict__ dWX0, int nx, const float* __restrict__ dbias7) {
+  const int64_t pst = (int64_t)7 * H * H, xst = (int64_t)6 * H * in;
   const int ld = in + H;
   const int64_t nU = (int64_t)6 * H * ld, nN = (int64_t)H * H;
   const int64_t n = nU + nN + 7 * H;
@@ -441,12 +457,13 @@ __global__ void rnn_scatter_kernel(RnnLayerW gw, int in, int H, int layer, const
       const int grow = (int)(i / ld), k = (int)(i - (int64_t)grow * ld);
       const int g = grow / H, r = grow - g * H;
       float v;
-      if (layer == 0) v = k < in ? dWX0[(int64_t)(g * H + r) * in + k] : dP[(int64_t)(g * H + r) * H + (k - in)];
-      else v = dP[(int64_t)(g * H + r) * H + (k < in ? k : k - in)];
+      if (layer == 0) v = k < in ? slice_sum(dWX0 + (int64_t)(g * H + r) * in + k, nx, xst)
+                                 : slice_sum(dP + (int64_t)(g * H + r) * H + (k - in), np, pst);
+      else v = slice_sum(dP + (int64_t)(g * H + r) * H + (k < in ? k : k - in), np, pst);
       gw.wu[g][(int64_t)r * ld + k] = v;
     } else if (i < nU + nN) {
       const int64_t j = i - nU;
-      gw.wn[j] = dP[(int64_t)6 * H * H + j];
+      gw.wn[j] = slice_sum(dP + (int64_t)6 * H * H + j, np, pst);
     } else {
       const int j = (int)(i - nU - nN), g = j / H, r = j - g * H;
       if (g == 6) gw.bn[r] = dbias7[j];
@@ -774,8 +791,9 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   float* ds = take(BT);
   float* DZ[8];
   for (int l = 0; l < d.L; ++l) DZ[l] = take(BT * 7 * H);
-  float* dP = take((int64_t)7 * H * H);
-  float* dWX0 = take((int64_t)6 * H * IN);
+  int kq;
+  float* dP = take((int64_t)sgemm_wsplits(7 * H, H, (int)BT, &kq) * 7 * H * H);      // split-K partials
+  float* dWX0 = take((int64_t)sgemm_wsplits(6 * H, IN, (int)BT, &kq) * 6 * H * IN);  // split-K partials
   float* dbias = take(7 * H);
   float* dhs = take((int64_t)sb * B * H);   // K slices: gradient into the last layer's h' of step t-1
   float* dhls = take((int64_t)sb * B * H);  // K slices: gradient into an inner layer's output
@@ -836,13 +854,18 @@ int rnn_backward(hipStream_t s, const RnnDims& d, const RnnParams& P, const floa
   // weight gradients, one GEMM per layer over all B*T rows
   for (int l = 0; l < d.L; ++l) {
     // dP[7H][H] = DZ^T UH ; dWX0[6H][IN] = DZ[:, :6H]^T X   (sums over all B*T rows)
-    DFD_TRY(launch_sgemm(s, true, true, DZ[l], 7 * H, w.UH[l], H, dP, H, 7 * H, H, (int)BT, 0.f, nullptr));
-    if (l == 0)
-      DFD_TRY(launch_sgemm(s, true, true, DZ[0], 7 * H, order ? w.xs : x, IN, dWX0, IN, 6 * H, IN, (int)BT, 0.f,
-                           nullptr));
+    // as split-K partials (sgemm_wsplits slices, added in order by the scatter)
+    int kp, kx = 0;
+    const int np = sgemm_wsplits(7 * H, H, (int)BT, &kp);
+    DFD_TRY(launch_sgemm_part(s, true, true, DZ[l], 7 * H, w.UH[l], H, dP, 7 * H, H, (int)BT, np, kp));
+    int nx = 1;
+    if (l == 0) {
+      nx = sgemm_wsplits(6 * H, IN, (int)BT, &kx);
+      DFD_TRY(launch_sgemm_part(s, true, true, DZ[0], 7 * H, order ? w.xs : x, IN, dWX0, 6 * H, IN, (int)BT, nx, kx));
+    }
     DFD_TRY(launch_reduce_slabs(s, DZ[l], (int)BT, 7 * H, dbias, false));
     hipLaunchKernelGGL(rnn_scatter_kernel, dim3(ew_blocks((int64_t)6 * H * (IN + H) + (int64_t)H * H + 7 * H)),
-                       dim3(256), 0, s, Gr.layer[l], l == 0 ? IN : H, H, l, dP, dWX0, dbias);
+                       dim3(256), 0, s, Gr.layer[l], l == 0 ? IN : H, H, l, dP, np, dWX0, nx, dbias);
     DFD_HIP_CHECK(hipGetLastError());
   }
   return 0;
@@ -909,7 +932,9 @@ int64_t rnn_scratch_floats(const RnnDims& d) {  // the takes of rnn_backward, pa
   const int64_t BT = (int64_t)d.B * d.T, H = d.H;
   int kc;
   const int64_t sb = bwd_splits(d, &kc);
-  const int64_t sizes[] = {d.B * H, d.B * H, BT * H, BT * H, BT * H, BT, 7 * H * H, 6 * H * d.IN, 7 * H,
+  int kq;
+  const int64_t np = sgemm_wsplits(7 * (int)H, (int)H, (int)BT, &kq), nx = sgemm_wsplits(6 * (int)H, d.IN, (int)BT, &kq);
+  const int64_t sizes[] = {d.B * H, d.B * H, BT * H, BT * H, BT * H, BT, np * 7 * H * H, nx * 6 * H * d.IN, 7 * H,
                            sb * d.B * H, sb * d.B * H, d.B * H, d.B * H, (int64_t)rnn_step_slices() * d.B * H};
   int64_t n = d.L * ((BT * 7 * H + 63) & ~int64_t(63));
   for (int64_t v : sizes) n += (v + 63) & ~int64_t(63);

@@ -74,8 +74,12 @@ __device__ __forceinline__ f32x4_t mma_rows(const float4 (&av)[NS], const float*
 
 }  // namespace
 
+#define RS_TS(i) \
+  if (a.ts && threadIdx.x == 0) a.ts[blockIdx.x * 8 + (i)] = wall_clock64()
+
 template <int NS>  // NS = H / 16
 __global__ __launch_bounds__(256) void rnn_step_fwd_kernel(RnnStep a, int t, int l) {
+  RS_TS(0);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int H = 16 * NS, PS = H + 4;  // weight row stride: 16-B skew, conflict-free 16-B reads
   float* wl = lds;                        // [16][PS]
@@ -91,6 +95,22 @@ __global__ __launch_bounds__(256) void rnn_step_fwd_kernel(RnnStep a, int t, int
     const int b = wave * 16 + (lane & 15);
     load_a<NS>(av, b < B ? hin + (int64_t)b * ldr : nullptr);
   }
+  // the cell operands that do not depend on the product (bias, x projection, c), loaded per chunk
+  // ahead of the product: thread idx < 64*UJ owns (row b0 + idx/UJ, unit j0 + idx%UJ)
+  float cz[7], cc = 0.f;
+  auto cell_loads = [&](int b0) {
+    const int bl = tid / UJ, u = tid - bl * UJ, b = b0 + bl, j = j0 + u;
+    if (tid >= 64 * UJ || b >= B) return;
+    const int64_t row = (int64_t)b * T + t;
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+      float v = a.bias7[l][g * H + j];
+      if (l == 0 && g < 6) v += a.X0[row * 6 * H + g * H + j];
+      cz[g] = v;
+    }
+    cc = a.CI[l][(int64_t)b * ldr + (int64_t)t * H + j];
+  };
+  cell_loads(0);
   // weight rows: column c = g * UJ + u  <-  P_l row g*H + j0 + u ; columns 14, 15 zero.  All of the
   // thread's loads are issued before the first LDS store (one round trip, not one per float4).
   constexpr int WV = 16 * (H / 4) / 256;  // float4 per thread
@@ -108,30 +128,30 @@ __global__ __launch_bounds__(256) void rnn_step_fwd_kernel(RnnStep a, int t, int
     *reinterpret_cast<float4*>(wl + c * PS + k4) = wv[r];
   }
   __syncthreads();
+  RS_TS(1);
   for (int b0 = 0; b0 < B; b0 += 64) {
     if (b0 > 0) {
       const int b = b0 + wave * 16 + (lane & 15);
       load_a<NS>(av, b < B ? hin + (int64_t)b * ldr : nullptr);
+      cell_loads(b0);
     }
     const f32x4_t d = mma_rows<NS>(av, wl, PS);
 #pragma unroll
     for (int i = 0; i < 4; ++i) zt[(wave * 16 + 4 * (lane >> 4) + i) * 17 + (lane & 15)] = d[i];
     __syncthreads();
-    for (int idx = tid; idx < 64 * UJ; idx += 256) {
+    RS_TS(2);
+    {
+      const int idx = tid;
       const int bl = idx / UJ, u = idx - bl * UJ, b = b0 + bl;
-      if (b >= B) continue;
+      if (idx >= 64 * UJ || b >= B) goto cell_done;
       const int j = j0 + u;
       const int64_t row = (int64_t)b * T + t;
       float z[7];
 #pragma unroll
-      for (int g = 0; g < 7; ++g) {
-        float v = zt[bl * 17 + g * UJ + u] + a.bias7[l][g * H + j];
-        if (l == 0 && g < 6) v += a.X0[row * 6 * H + g * H + j];
-        z[g] = v;
-      }
+      for (int g = 0; g < 7; ++g) z[g] = zt[bl * 17 + g * UJ + u] + cz[g];
       const float ga = sig_s(z[0]), go = sig_s(z[1]), gf = sig_s(z[2]), gi = sig_s(z[3]), gg = tanhf(z[4]);
       const float gu = sig_s(z[5]), gn = tanhf(z[6]);
-      const float c = a.CI[l][(int64_t)b * ldr + (int64_t)t * H + j];
+      const float c = cc;
       const float cn = gf * c + gi * gg;
       const float cl = ga * cn + go * gn;
       const float h = gu * tanhf(cl);
@@ -151,7 +171,9 @@ __global__ __launch_bounds__(256) void rnn_step_fwd_kernel(RnnStep a, int t, int
         a.CI[l + 1][(int64_t)b * ldr + (int64_t)t * H + j] = cl;
       }
     }
+  cell_done:
     __syncthreads();  // zt is rewritten by the next chunk
+    RS_TS(3);
   }
 }
 

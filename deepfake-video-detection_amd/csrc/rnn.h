@@ -27,6 +27,8 @@ int launch_sgemm(hipStream_t s, bool ta, bool tb, const float* A, int lda, const
 // K-sliced form for products with few output tiles: sgemm_splits picks the slice count and
 // length (kc); launch_sgemm_part writes part[z][M][N], the consumer sums z = 0.. in order
 int sgemm_splits(int M, int N, int K, int* kc);
+// K slices of the large weight-gradient products (split-K partials for the big-tile kernel)
+int sgemm_wsplits(int M, int N, int K, int* kc);
 int launch_sgemm_part(hipStream_t s, bool ta, bool tb, const float* A, int lda, const float* B, int ldb, float* part,
                       int M, int N, int K, int splits, int kc);
 int64_t rnn_work_floats(const RnnDims& d);
@@ -57,6 +59,7 @@ struct RnnStep {
   float* O;               // last layer's h' [B*T][H]
   float p;
   uint64_t seed;
+  unsigned long long* ts;  // development timing: per-workgroup phase stamps [grid][8] (nullptr: off)
 };
 bool rnn_step_supported(const RnnDims& d);
 int rnn_step_slices();

@@ -15,6 +15,7 @@
 
 #include "../deepfake-video-detection_amd/csrc/kernels.h"
 #include "../include/dfd_hip.h"
+#include "../deepfake-video-detection_amd/csrc/rnn.h"
 
 using namespace dfd;
 
@@ -265,6 +266,59 @@ int main(int argc, char** argv) {
     b.run("bn_bwd_reduce", nm, 2.0 * 2 * Mo * k.cout, [&] {
       return launch_bn_bwd_reduce<bf16>(b.s, bo, B, Mo, k.cout, stats, &rows);
     });
+  }
+  if (b.filter == "rnn") {
+    // LogicRNNLSTM per-cell forward launch at the C4 shape (B 64, T 16, H 512, L 2) + phase stamps
+    const int RB = 64, RT = 16, RH = 512, RL = 2;
+    RnnStep a{};
+    a.B = RB; a.T = RT; a.H = RH; a.L = RL; a.p = 0.f; a.seed = 1;
+    float* base;
+    const int64_t bt = (int64_t)RB * RT;
+    const int64_t nfl = 2 * (7LL * RH * RH + 7 * RH) + bt * 6 * RH + 2 * bt * (2 * RH + 7 * RH + 3 * RH) + bt * RH;
+    CK(hipMalloc(&base, nfl * 4));
+    CK(hipMemset(base, 0, nfl * 4));
+    float* q = base;
+    for (int l = 0; l < RL; ++l) { a.P[l] = q; q += 7LL * RH * RH; a.bias7[l] = q; q += 7 * RH; }
+    a.X0 = q; q += bt * 6 * RH;
+    for (int l = 0; l < RL; ++l) {
+      a.UH[l] = q; q += bt * RH; a.CI[l] = q; q += bt * RH; a.ACT[l] = q; q += bt * 7 * RH;
+      a.CN[l] = q; q += bt * RH; a.CL[l] = q; q += bt * RH; q += bt * RH;
+    }
+    a.O = q;
+    unsigned long long* ts;
+    CK(hipMalloc(&ts, 256 * 8 * 8));
+    b.run("rnn", "step_fwd t3 l1", 4.0 * (RB * RH + 14.0 * RH * 256), [&] { return launch_rnn_step_fwd(b.s, a, 3, 1); });
+    b.run("rnn", "step_fwd t3 l0", 4.0 * (RB * RH + 14.0 * RH * 256), [&] { return launch_rnn_step_fwd(b.s, a, 3, 0); });
+    float* part;
+    CK(hipMalloc(&part, 8LL * RB * RH * 4));
+    b.run("rnn", "dh t3", 4.0 * (RB * 7 * RH + 7.0 * RH * RH), [&] {
+      return launch_rnn_dh(b.s, a.ACT[1] + 3 * 7 * RH, (int64_t)RT * 7 * RH, a.P[1], RB, RH, part);
+    });
+    for (int l = 0; l < 2; ++l) {
+      a.ts = ts;
+      CK(hipMemset(ts, 0, 256 * 8 * 8));
+      CK(launch_rnn_step_fwd(b.s, a, 3, l) == 0 ? hipSuccess : hipErrorUnknown);
+      CK(hipStreamSynchronize(b.s));
+      std::vector<unsigned long long> h(256 * 8);
+      CK(hipMemcpy(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long t0 = ~0ull, t1 = 0;
+      double d[4] = {0, 0, 0, 0}, mx[4] = {0, 0, 0, 0};
+      for (int w = 0; w < 256; ++w) {
+        t0 = std::min(t0, h[w * 8]);
+        t1 = std::max(t1, h[w * 8 + 3]);
+        for (int ph = 1; ph <= 3; ++ph) {
+          const double v = (double)(h[w * 8 + ph] - h[w * 8 + ph - 1]) * 0.01;
+          d[ph] += v / 256;
+          mx[ph] = std::max(mx[ph], v);
+        }
+      }
+      unsigned long long s0max = 0;
+      for (int w = 0; w < 256; ++w) s0max = std::max(s0max, h[w * 8]);
+      printf("   step_fwd l%d phases (us mean/max): weights+sync %.2f/%.2f  mfma %.2f/%.2f  cell %.2f/%.2f  | "
+             "WG starts spread %.2f us, first start -> last cell end %.2f us\n",
+             l, d[1], mx[1], d[2], mx[2], d[3], mx[3], (s0max - t0) * 0.01, (t1 - t0) * 0.01);
+      a.ts = nullptr;
+    }
   }
   printf("TOTAL %.1f us, floor %.1f us\n", b.total_us, b.total_floor);
   return 0;
