@@ -138,21 +138,26 @@ __device__ __forceinline__ void sb_load(const float* __restrict__ P, int ld, int
     }
   }
 }
+// LDS image [SB_K][PR] k-major; element (k, r) sits at column r ^ sb_swz(k): the XOR permutes
+// 4-column groups inside each 16-column block, so the MFMA reads (16 consecutive r of one k) stay
+// conflict-free while the transposing scalar stores of a k-contiguous operand (8 k x 4 r per 32
+// lanes) spread over 16 banks (2-way: free for ds_write_b32) instead of 4 (8-way)
+__device__ __forceinline__ int sb_swz(int k) { return ((k >> 2) & 3) << 2; }
 template <bool T_, int R, int PR>
-__device__ __forceinline__ void sb_store(float* S, const float4 (&v)[sb_nv<R>()]) {  // S: [SB_K][PR] k-major
+__device__ __forceinline__ void sb_store(float* S, const float4 (&v)[sb_nv<R>()]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < sb_nv<R>(); ++i) {
     const int e = tid + 256 * i;
     if (T_) {
       const int k = e / (R / 4), r4 = (e % (R / 4)) * 4;
-      *reinterpret_cast<float4*>(S + k * PR + r4) = v[i];
+      *reinterpret_cast<float4*>(S + k * PR + (r4 ^ sb_swz(k))) = v[i];
     } else {
-      const int r = e / (SB_K / 4), k4 = (e % (SB_K / 4)) * 4;
-      S[(k4 + 0) * PR + r] = v[i].x;
-      S[(k4 + 1) * PR + r] = v[i].y;
-      S[(k4 + 2) * PR + r] = v[i].z;
-      S[(k4 + 3) * PR + r] = v[i].w;
+      const int r = e / (SB_K / 4), k4 = (e % (SB_K / 4)) * 4, rs = r ^ sb_swz(k4);  // k4..k4+3 share sb_swz
+      S[(k4 + 0) * PR + rs] = v[i].x;
+      S[(k4 + 1) * PR + rs] = v[i].y;
+      S[(k4 + 2) * PR + rs] = v[i].z;
+      S[(k4 + 3) * PR + rs] = v[i].w;
     }
   }
 }
@@ -186,10 +191,12 @@ __global__ __launch_bounds__(256) void sgemm_big_kernel(const float* __restrict_
       sb_load<TA, SB_M>(A, lda, m0, kb + (kt + 1) * SB_K, va);
       sb_load<TB, SB_N>(B, ldb, n0, kb + (kt + 1) * SB_K, vb);
     }
-    const float* as = As[cur] + (lane >> 4) * SB_PM + wm + (lane & 15);
-    const float* bs = Bs[cur] + (lane >> 4) * SB_PN + wn + (lane & 15);
 #pragma unroll
     for (int s4 = 0; s4 < SB_K / 4; ++s4) {
+      // k = 4*s4 + (lane >> 4): sb_swz(k) = (s4 & 3) << 2 for every lane
+      const int rl = (lane & 15) ^ ((s4 & 3) << 2);
+      const float* as = As[cur] + (lane >> 4) * SB_PM + wm + rl;
+      const float* bs = Bs[cur] + (lane >> 4) * SB_PN + wn + rl;
       float af[4], bf[2];
 #pragma unroll
       for (int a = 0; a < 4; ++a) af[a] = as[s4 * 4 * SB_PM + a * 16];
