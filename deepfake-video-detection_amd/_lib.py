@@ -70,6 +70,8 @@ _SIGS = {
     "dfd_rn_avgpool": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_p]),
     "dfd_pw_conv": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p,
                           ctypes.POINTER(c_i)]),
+    "dfd_attention": (c_i, [c_p, c_i, c_i, c_i, c_i, c_f, c_p, c_i64, c_i, c_i, c_p, c_i64, c_p, c_p, c_i64, c_p,
+                            c_i64]),
     "dfd_sgemm": (c_i, [c_p, c_i, c_i, c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_f, c_p]),
     "dfd_pw_conv_wgrad": (c_i, [c_p, c_i, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i64, c_p,
                                 c_i]),

@@ -472,6 +472,23 @@ int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, 
   DFD_GUARD_END
 }
 
+int dfd_attention(void* stream, int backward, int images, int heads, int nt, float scale, const void* qkv, int64_t ldq,
+                  int koff, int voff, void* O, int64_t ldo, float* lse, const void* dO, int64_t lddo, void* dqkv,
+                  int64_t lddq) {
+  DFD_GUARD_BEGIN
+  if (!qkv || !O || !lse || images < 1 || heads < 1 || !dfd::attn_supported(nt, 64) || (backward && (!dO || !dqkv))) {
+    dfd::set_error("attention: bad arguments", __FILE__, __LINE__);
+    return -1;
+  }
+  dfd::AttnArgs a{};
+  a.images = images; a.heads = heads; a.nt = nt; a.scale = scale;
+  a.qkv = (const dfd::bf16*)qkv; a.ldq = ldq; a.koff = koff; a.voff = voff;
+  a.O = (dfd::bf16*)O; a.ldo = ldo; a.lse = lse;
+  a.dO = (const dfd::bf16*)dO; a.lddo = lddo; a.dqkv = (dfd::bf16*)dqkv; a.lddq = lddq;
+  return backward ? dfd::launch_attn_bwd((hipStream_t)stream, a) : dfd::launch_attn_fwd((hipStream_t)stream, a);
+  DFD_GUARD_END
+}
+
 int dfd_sgemm(void* stream, int ta, int tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc, int M,
               int N, int K, float beta, const float* bias) {
   DFD_GUARD_BEGIN

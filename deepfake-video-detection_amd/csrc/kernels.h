@@ -93,6 +93,27 @@ struct Mb7Args {
 bool mbconv7_supported(int frames, int H, int W, int cin, int mid, int cout, int rd, int k, int s);
 int launch_mbconv7_fwd(hipStream_t s, const Mb7Args& a);
 
+// Fused multi-head attention, bf16, head dim 64, <= 256 tokens (k_attn.hip): one workgroup per
+// (image, head).  qkv rows of `nt` tokens per image, q / k / v of head h at columns h*64, koff +
+// h*64, voff + h*64; O / dO [rows][ldo] with head h at h*64; lse [images*heads][nt] fp32.
+struct AttnArgs {
+  int images, heads, nt;
+  float scale;
+  const bf16* qkv;
+  int64_t ldq;
+  int koff, voff;
+  bf16* O;          // forward output (read by the backward for rowsum(dO * O))
+  int64_t ldo;
+  float* lse;       // forward output / backward input
+  const bf16* dO;   // backward input
+  int64_t lddo;
+  bf16* dqkv;       // backward output, qkv's layout
+  int64_t lddq;
+};
+bool attn_supported(int nt, int head_dim);
+int launch_attn_fwd(hipStream_t s, const AttnArgs& a);
+int launch_attn_bwd(hipStream_t s, const AttnArgs& a);
+
 // ResNet-50 convolutions as implicit-GEMM MFMA kernels (k_rnconv.hip): C = relu?(conv(X) + bias (+ R))
 struct RnConvGeom {
   int N, H, W, Cin, KH, KW, stride, pad, Ho, Wo, cin_log2;

@@ -158,6 +158,16 @@ int cast_weights(hipStream_t s, const VitDims& d, const VitLayout& L, const floa
 inline BgOp op_tok(int ld) { return BgOp{ld, HEADS, (int64_t)197 * ld, DH}; }
 inline BgOp op_score() { return BgOp{SLD, 1, (int64_t)197 * SLD, 0}; }
 
+// the fused attention's view of one layer's qkv / O / log-sum-exp buffers (bf16 path)
+template <typename T>
+inline AttnArgs attn_args(int images, int nt, const T* qkv, T* O, float* lse) {
+  AttnArgs a{};
+  a.images = images; a.heads = HEADS; a.nt = nt; a.scale = 0.125f;
+  a.qkv = reinterpret_cast<const bf16*>(qkv); a.ldq = D3; a.koff = D; a.voff = 2 * D;
+  a.O = reinterpret_cast<bf16*>(O); a.ldo = D; a.lse = lse;
+  return a;
+}
+
 // C[M][N] = A . B^T + bias (+ R): hipBLASLt in bf16 mode (plain GEMMs, blaslt.cpp), the k_gemm.hip
 // kernels in the fp32 parity mode
 template <typename T>
@@ -194,11 +204,15 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     DFD_TRY(lin<T>(s, w.at(b.h1), w.at(b.wqkv), w.at(b.qkv), nullptr, q[3], M, D3, D));
     T* qkv = w.at(b.qkv);
     // S = (q * 64^-0.5) k^T ; P = softmax(S) ; O = P v
-    DFD_TRY(launch_bgemm<T>(s, false, true, BH, nt, nt, DH, 0.125f, qkv, op_tok(D3), qkv + D, op_tok(D3), w.at(L.S),
-                            op_score()));
-    DFD_TRY(launch_softmax_fwd<T>(s, w.at(L.S), w.at(b.P), SR, nt, SLD));
-    DFD_TRY(launch_bgemm<T>(s, false, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), qkv + 2 * D, op_tok(D3),
-                            w.at(b.O), op_tok(D)));
+    if constexpr (sizeof(T) == 2) {  // fused (k_attn.hip): O and the row log-sum-exp (in b.P's space)
+      DFD_TRY(launch_attn_fwd(s, attn_args(I, nt, qkv, w.at(b.O), w.template at<float>(b.P))));
+    } else {
+      DFD_TRY(launch_bgemm<T>(s, false, true, BH, nt, nt, DH, 0.125f, qkv, op_tok(D3), qkv + D, op_tok(D3),
+                              w.at(L.S), op_score()));
+      DFD_TRY(launch_softmax_fwd<T>(s, w.at(L.S), w.at(b.P), SR, nt, SLD));
+      DFD_TRY(launch_bgemm<T>(s, false, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), qkv + 2 * D, op_tok(D3),
+                              w.at(b.O), op_tok(D)));
+    }
     // xm = x + proj(O) ; x' = xm + fc2(gelu(fc1(LN2(xm))))
     DFD_TRY(lin<T>(s, w.at(b.O), w.at(b.wp), w.at(b.xm), w.at(b.x), q[5], M, D, D));
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.xm), D, q[6], q[7], w.at(b.h2), D, w.template at<float>(b.mu2),
@@ -269,15 +283,24 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4]));
     DFD_TRY(launch_colsum<T>(s, dxm, M, D, part, L.part_cap, g[5], false));
     // ---- attention core: dP = dO v^T ; dS = scale P (dP - rowdot) ; dq = dS k ; dk = dS^T q ; dv = P^T dO
-    DFD_TRY(launch_bgemm<T>(s, false, true, BH, nt, nt, DH, 1.f, dO, op_tok(D), qkv + 2 * D, op_tok(D3), dS,
-                            op_score()));
-    DFD_TRY(launch_softmax_bwd<T>(s, w.at(b.P), dS, dS, SR, nt, SLD, 0.125f));
-    DFD_TRY(launch_bgemm<T>(s, false, false, BH, nt, DH, nt, 1.f, dS, op_score(), qkv + D, op_tok(D3), dqkv,
-                            op_tok(D3)));
-    DFD_TRY(launch_bgemm<T>(s, true, false, BH, nt, DH, nt, 1.f, dS, op_score(), qkv, op_tok(D3), dqkv + D,
-                            op_tok(D3)));
-    DFD_TRY(launch_bgemm<T>(s, true, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), dO, op_tok(D),
-                            dqkv + 2 * D, op_tok(D3)));
+    if constexpr (sizeof(T) == 2) {  // fused (k_attn.hip): recomputes P from the saved log-sum-exp
+      AttnArgs at = attn_args(I, nt, qkv, w.at(b.O), w.template at<float>(b.P));
+      at.dO = dO;
+      at.lddo = D;
+      at.dqkv = dqkv;
+      at.lddq = D3;
+      DFD_TRY(launch_attn_bwd(s, at));
+    } else {
+      DFD_TRY(launch_bgemm<T>(s, false, true, BH, nt, nt, DH, 1.f, dO, op_tok(D), qkv + 2 * D, op_tok(D3), dS,
+                              op_score()));
+      DFD_TRY(launch_softmax_bwd<T>(s, w.at(b.P), dS, dS, SR, nt, SLD, 0.125f));
+      DFD_TRY(launch_bgemm<T>(s, false, false, BH, nt, DH, nt, 1.f, dS, op_score(), qkv + D, op_tok(D3), dqkv,
+                              op_tok(D3)));
+      DFD_TRY(launch_bgemm<T>(s, true, false, BH, nt, DH, nt, 1.f, dS, op_score(), qkv, op_tok(D3), dqkv + D,
+                              op_tok(D3)));
+      DFD_TRY(launch_bgemm<T>(s, true, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), dO, op_tok(D),
+                              dqkv + 2 * D, op_tok(D3)));
+    }
     // ---- qkv projection and LN1: dx_l = dxm + LN1'(dqkv Wqkv) ----
     DFD_TRY(lin<T>(s, dqkv, w.at(b.wqkvT), dh, nullptr, nullptr, M, D, D3));
     DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2]));

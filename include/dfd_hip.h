@@ -221,6 +221,15 @@ DFD_API int dfd_pw_conv_wgrad(void* stream, int dtype, const void* dY, const voi
                               int pro_mode, const float* scale, const float* shift, const float* gate,
                               int rows_per_frame, float* slab, int64_t slab_floats, float* dW, int accumulate);
 
+/* Fused multi-head attention (bf16, head dim 64, nt <= 256; test seam of the ViT trunk's attention,
+ * timm Attention as run by ViTFeatureExtractor, src/models.py:88-107).  qkv: bf16 rows of nt tokens per
+ * image, head h's q / k / v at columns h*64 / koff + h*64 / voff + h*64 (row stride ldq); O [rows][ldo]
+ * bf16; lse [images*heads][nt] fp32.  backward = 0: O, lse from qkv.  backward = 1: dqkv (qkv's
+ * layout, row stride lddq) from qkv, O, lse and dO [rows][lddo]. */
+DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int nt, float scale, const void* qkv,
+                          int64_t ldq, int koff, int voff, void* O, int64_t ldo, float* lse, const void* dO,
+                          int64_t lddo, void* dqkv, int64_t lddq);
+
 /* fp32 GEMM of the recurrent models' plain products (test seam): C[m][n] = beta*C + sum_k A(m,k) B(n,k)
  * (+ bias[n]); A(m,k) = ta ? A[k*lda+m] : A[m*lda+k], B(n,k) = tb ? B[k*ldb+n] : B[n*ldb+k].  The
  * kernels behind nn.Linear / nn.LSTM input projections and weight gradients of LogicRNNLSTM,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # fused 7x7 phase timing (kbench mb7) + per-cell recurrent launches: tests, bench, trace
 R=$GRAFT_REPO_ROOT; TAG=${1:-e}; cd $R; mkdir -p gpurun_out
-timeout -k 10 120 tools/kbench rnn > gpurun_out/kb_rnn_$TAG.txt 2>&1; cat gpurun_out/kb_rnn_$TAG.txt
+# kbench rnn: tools/kbench rnn
 timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_rnn.py tests/test_sgemm_gpu.py -m gpu > gpurun_out/t_$TAG.log 2>&1; rc=$?
 grep -E "FAIL|Error|assert|passed|failed" gpurun_out/t_$TAG.log | cut -c1-300 | head -20
 [ $rc -eq 0 ] || exit $rc
