@@ -71,8 +71,10 @@ int handle_and_ws(hipStream_t s, int dev, hipblasLtHandle_t* h, void** ws) {
 
 // kind 0: C = A . B^T (+bias)(+R), D type = T; kind 1: dW (+)= dY^T . X, D fp32
 // epi: bit 0 bias, bit 1 ReLU (applied after bias and the residual: D = relu(A.B^T + R + bias))
+// batch > 1 (kind 1 only): `batch` independent products over consecutive k-ranges (A' and B' batch
+// strides k * rows), each into its own m x n slab of D (stride m * n) -- the split-M weight gradient
 int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k,
-          int epi_bits, Entry& e) {
+          int epi_bits, Entry& e, int batch = 1) {
   const bool bias = (epi_bits & 1) != 0, relu = (epi_bits & 2) != 0;
   LT_CHECK(hipblasLtMatmulDescCreate(&e.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
   const hipblasOperation_t opA = kind == 0 ? HIPBLAS_OP_T : HIPBLAS_OP_N;
@@ -97,6 +99,16 @@ int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t
   }
   LT_CHECK(hipblasLtMatrixLayoutCreate(&e.c, cd, m, n, m));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&e.d, cd, m, n, m));
+  if (batch > 1) {
+    const int32_t bc = batch;
+    const int64_t sa = k * m, sb = k * n, sc = m * n;
+    for (auto* l : {&e.a, &e.b, &e.c, &e.d})
+      LT_CHECK(hipblasLtMatrixLayoutSetAttribute(*l, HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc, sizeof(bc)));
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(e.a, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sa, sizeof(sa)));
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(e.b, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sb, sizeof(sb)));
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(e.c, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sc, sizeof(sc)));
+    LT_CHECK(hipblasLtMatrixLayoutSetAttribute(e.d, HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET, &sc, sizeof(sc)));
+  }
   hipblasLtMatmulPreference_t pref;
   LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
   const uint64_t wsb = kWorkspace;
@@ -114,7 +126,7 @@ int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t
 }
 
 int run(hipStream_t s, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k, const void* A,
-        const void* B, const void* C, void* D, const float* bias, float beta, bool relu = false) {
+        const void* B, const void* C, void* D, const float* bias, float beta, bool relu = false, int batch = 1) {
   int dev = 0;
   DFD_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_mu);
@@ -122,11 +134,11 @@ int run(hipStream_t s, int kind, hipDataType ab, hipDataType cd, int64_t m, int6
   void* ws;
   DFD_TRY(handle_and_ws(s, dev, &h, &ws));
   const int epi_bits = (bias ? 1 : 0) | (relu ? 2 : 0);
-  const Key key{dev, kind, m, n, k, (int)ab, (int)cd, epi_bits, 0};
+  const Key key{dev, kind, m, n, k, (int)ab, (int)cd, epi_bits, batch};
   auto it = g_cache.find(key);
   if (it == g_cache.end()) {
     Entry e;
-    DFD_TRY(build(h, kind, ab, cd, m, n, k, epi_bits, e));
+    DFD_TRY(build(h, kind, ab, cd, m, n, k, epi_bits, e, batch));
     it = g_cache.emplace(key, e).first;
   }
   Entry& e = it->second;
@@ -168,6 +180,18 @@ int blaslt_gemm(hipStream_t s, int dtype, const void* A, const void* B, void* C,
 int blaslt_wgrad(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, bool accumulate) {
   if (M <= 0) return 0;
   return run(s, 1, HIP_R_16BF, HIP_R_32F, K, N, M, X, dY, dW, dW, nullptr, accumulate ? 1.f : 0.f);
+}
+
+// The same over `splits` equal M-ranges as one batched library call into fp32 slabs [splits][N][K],
+// added in slab order by reduce_slabs (deterministic): the library's tile grid for a 768..3072 x 768
+// output is a few dozen workgroups, so the long (M = 25,216) reduction alone fills too little of the
+// chip.  M % splits != 0 or slab_floats < splits * N * K fall back to the single call.
+int blaslt_wgrad_split(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, int splits,
+                       float* slab, int64_t slab_floats) {
+  if (M <= 0) return 0;
+  if (splits <= 1 || M % splits || slab_floats < (int64_t)splits * N * K) return blaslt_wgrad(s, dY, X, dW, M, N, K, false);
+  DFD_TRY(run(s, 1, HIP_R_16BF, HIP_R_32F, K, N, M / splits, X, dY, slab, slab, nullptr, 0.f, false, splits));
+  return launch_reduce_slabs(s, slab, splits, (int64_t)N * K, dW, false);
 }
 
 }  // namespace dfd

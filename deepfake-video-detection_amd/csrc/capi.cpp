@@ -436,6 +436,8 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
   if (key && strcmp(key, "mbconv7") == 0) return dfd::set_mbconv7(value);
   if (key && strcmp(key, "rnn_step") == 0) return dfd::set_rnn_step(value);
+  if (key && strcmp(key, "vit_gemm") == 0) return dfd::set_vit_gemm(value);
+  if (key && strcmp(key, "vit_wsplit") == 0) return dfd::set_vit_wsplit(value);
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }

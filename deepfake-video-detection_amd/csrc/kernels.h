@@ -111,6 +111,9 @@ struct AttnArgs {
   int64_t lddq;
 };
 bool attn_supported(int nt, int head_dim);
+// ViT bf16 GEMM backend (vit.cpp): bit 0 own weight-gradient kernels, bit 1 own linears; previous value
+int64_t set_vit_gemm(int64_t v);
+int64_t set_vit_wsplit(int64_t v);  // M-splits of the ViT's library weight gradients (1 = single call)
 int launch_attn_fwd(hipStream_t s, const AttnArgs& a);
 int launch_attn_bwd(hipStream_t s, const AttnArgs& a);
 
@@ -125,6 +128,8 @@ int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, con
 int blaslt_linear(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
                   int N, int K);
 int blaslt_wgrad(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, bool accumulate);
+int blaslt_wgrad_split(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, int splits,
+                       float* slab, int64_t slab_floats);
 int blaslt_gemm(hipStream_t s, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
                 bool relu, int64_t M, int N, int K);
 

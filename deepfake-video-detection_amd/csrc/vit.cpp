@@ -14,6 +14,7 @@
 // split-M slab GEMMs reduced in a fixed order, so a step is bit-reproducible.
 #include "../../include/dfd_hip.h"
 
+#include <atomic>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -168,18 +169,31 @@ inline AttnArgs attn_args(int images, int nt, const T* qkv, T* O, float* lse) {
   return a;
 }
 
-// C[M][N] = A . B^T + bias (+ R): hipBLASLt in bf16 mode (plain GEMMs, blaslt.cpp), the k_gemm.hip
-// kernels in the fp32 parity mode
+// Which GEMMs of the bf16 mode run on the repo's own MFMA kernels (k_gemm.hip) instead of hipBLASLt:
+// bit 0 the weight gradients (launch_pw_wgrad: M-split, deterministic slabs), bit 1 the linears
+// (launch_tf_gemm, GELU fused as prologue / derivative epilogue).  The fp32 parity mode always uses
+// the k_gemm.hip kernels.
+std::atomic<int64_t> g_vit_gemm{0};
+// M-splits of the library weight gradients (batched call into slabs + ordered slab sum); 1 = one call
+std::atomic<int64_t> g_vit_wsplit{4};
+template <typename T> inline bool own_lin() { return sizeof(T) == 4 || (g_vit_gemm.load(std::memory_order_relaxed) & 2); }
+template <typename T> inline bool own_wgrad() { return sizeof(T) == 4 || (g_vit_gemm.load(std::memory_order_relaxed) & 1); }
+
+// C[M][N] = A . B^T + bias (+ R)
 template <typename T>
 int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N, int K) {
-  if constexpr (sizeof(T) == 2) return blaslt_linear(s, A, B, C, R, bias, M, N, K);
+  if constexpr (sizeof(T) == 2)
+    if (!own_lin<T>()) return blaslt_linear(s, A, B, C, R, bias, M, N, K);
   return launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE,
                            (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0));
 }
 // dW[N][K] = dY^T . X
 template <typename T>
 int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float* slab, int64_t slab_cap, float* dW) {
-  if constexpr (sizeof(T) == 2) return blaslt_wgrad(s, dY, X, dW, M, N, K, false);
+  if constexpr (sizeof(T) == 2)
+    if (!own_wgrad<T>())
+      return blaslt_wgrad_split(s, dY, X, dW, M, N, K, (int)g_vit_wsplit.load(std::memory_order_relaxed), slab,
+                                slab_cap);
   Pro none{};
   return launch_pw_wgrad<T>(s, dY, X, M, N, K, PRO_NONE, none, slab, slab_cap, dW, false);
 }
@@ -218,8 +232,8 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.xm), D, q[6], q[7], w.at(b.h2), D, w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), M, D, LN_EPS)));
     DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D));
-    if constexpr (sizeof(T) == 2) {  // gelu(Z) materialised once for the library GEMM
-      DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));
+    if (!own_lin<T>()) {  // gelu(Z) materialised once for the library GEMM (bf16 only)
+      if constexpr (sizeof(T) == 2) DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));
       DFD_TRY(lin<T>(s, w.at(L.G), w.at(b.w2), xnext, w.at(b.xm), q[11], M, D, FF));
     } else {
       DFD_TRY(launch_tf_gemm<T>(s, w.at(b.Z), w.at(b.w2), xnext, w.at(b.xm), q[11], nullptr, M, D, FF, PRO_GELU,
@@ -262,14 +276,17 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     T* dO = sc.at(L.dO);
     T* dS = sc.at(L.dS);
     // ---- MLP: dZ = (dx W2) * gelu'(Z); dW2 = dx^T gelu(Z); dh2 = dZ W1 ----
-    if constexpr (sizeof(T) == 2) {
-      DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D));
-      DFD_TRY(launch_gelu(s, w.at(b.Z), dZ, M * FF, true));   // dZ *= gelu'(Z)
-      DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));  // gelu(Z) for dW2
-      DFD_TRY(wgrad<T>(s, dx, w.at(L.G), M, D, FF, slab, L.slab_cap, g[10]));
-    } else {
+    if (own_lin<T>()) {
       DFD_TRY(launch_tf_gemm<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, w.at(b.Z), M, FF, D, PRO_NONE, EPI_DGELU));
+    } else {
+      DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D));
+      if constexpr (sizeof(T) == 2) DFD_TRY(launch_gelu(s, w.at(b.Z), dZ, M * FF, true));   // dZ *= gelu'(Z)
+    }
+    if (own_wgrad<T>()) {
       DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
+    } else {
+      if constexpr (sizeof(T) == 2) DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));  // gelu(Z) for dW2
+      DFD_TRY(wgrad<T>(s, dx, w.at(L.G), M, D, FF, slab, L.slab_cap, g[10]));
     }
     DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
     DFD_TRY(lin<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, M, D, FF));
@@ -442,6 +459,9 @@ int head_check(const HeadDims& h) {
 }
 
 }  // namespace
+
+int64_t set_vit_gemm(int64_t v) { return g_vit_gemm.exchange(v); }
+int64_t set_vit_wsplit(int64_t v) { return g_vit_wsplit.exchange(v); }
 }  // namespace dfd
 
 using dfd::VitDims;
