@@ -153,7 +153,7 @@ int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64
 int dfd_b0_plan_set_tuning(dfd_b0_plan* plan, const char* key, int64_t value) {
   if (!plan || !key) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
   static const char* names[dfd::TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile",
-                                             "dw_bwd1", "dw_fwd1", "wgrad_stream", "mbconv7"};
+                                             "dw_bwd1", "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused"};
   for (int k = 0; k < dfd::TK_COUNT; ++k)
     if (strcmp(key, names[k]) == 0) {
       std::lock_guard<std::mutex> lk(plan->mu);
@@ -435,6 +435,8 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
   if (key && strcmp(key, "dw_fwd1") == 0) return dfd::set_dw_fwd1(value);
   if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
   if (key && strcmp(key, "mbconv7") == 0) return dfd::set_mbconv7(value);
+  if (key && strcmp(key, "pwl_fused") == 0) return dfd::set_pwl_fused(value);
+  if (key && strcmp(key, "fold_fused") == 0) return dfd::set_fold_fused(value);
   if (key && strcmp(key, "rnn_step") == 0) return dfd::set_rnn_step(value);
   if (key && strcmp(key, "vit_gemm") == 0) return dfd::set_vit_gemm(value);
   if (key && strcmp(key, "vit_wsplit") == 0) return dfd::set_vit_wsplit(value);

@@ -380,89 +380,141 @@ int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const floa
 }
 
 // ------------------------------------------------------------------ per-frame channel sums
-// part[h][f][c] = sum over pixel chunk h of frame f of val(p, c), where
-//   SQUEEZE: val = silu(y*scale+shift);   SEBWD: val = dZ * silu(y*scale+shift)
-// SQUEEZE with s_out also stores silu(y*scale+shift) (rounded to T): the materialised activation
-// the late-stage conv_pwl forward and weight gradient read instead of recomputing it per N tile.
-// grid (frames*hsplit, groups); threads: vec = tid % vpg, pl = tid / vpg
-template <typename T, bool SEBWD>
-__global__ __launch_bounds__(256) void frame_sum_kernel(const T* __restrict__ dZ, const T* __restrict__ Y, Pro pro,
-                                                        int frames, int HW, int C, int hsplit, int vpg,
-                                                        float* __restrict__ part, T* __restrict__ s_out) {
-  __shared__ float sh[256][8];
+// part[q][h][f][c] = sum over pixel chunk h of frame f of val_q(p, c), for the per-frame reductions
+// of the SE module (one kernel, OP selects the values):
+//   FR_SQUEEZE (Q = 1): silu(y*scale+shift); with s_out the activation is also stored (rounded to
+//                       T): the late-stage conv_pwl forward and weight gradient read it instead of
+//                       recomputing it per N tile
+//   FR_SEBWD   (Q = 1): dZ * silu(y*scale+shift)
+//   FR_SEBN    (Q = 5): the one-pass SE + BN backward sums D, P1..P4 (below)
+// Work split: vpg 8-channel vectors x npl = 256/vpg pixel lanes per workgroup, the lanes being fpb
+// frames x pl lanes per frame.  Small maps (7x7: 49 pixels) put several frames in one workgroup so a
+// lane still walks ~8 pixels (one frame per workgroup left 3 pixels per lane and a workgroup's
+// launch and reduction dominated); large maps split a frame into hsplit chunks.  A lane's pixels go
+// in groups of FR_U (4; 2 for the register-heavy FR_SEBN) with every load of a group issued first; the pl lanes of a frame are added in
+// lane order through LDS (fixed summation order: bit-reproducible).
+enum { FR_SQUEEZE = 0, FR_SEBWD = 1, FR_SEBN = 2 };
+struct FrGeom {
+  int frames, HW, C, hsplit, vpg, pl, fpb;
+};
+struct FrCoef {
+  const float *scale, *shift, *mean, *invstd;
+};
+
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void frame_reduce_kernel(const T* __restrict__ dZ, const T* __restrict__ Y, FrCoef cf,
+                                                           FrGeom g, float* __restrict__ part, T* __restrict__ s_out) {
+  constexpr int Q = OP == FR_SEBN ? 5 : 1;
+  constexpr int FR_U = OP == FR_SEBN ? 2 : 4;  // the five FR_SEBN sums: 2 pixels in flight (occupancy)
+  __shared__ float sh[Q][256][8];
   const int tid = threadIdx.x;
-  const int vec = tid % vpg, pl = tid / vpg, npl = 256 / vpg;
-  const int f = blockIdx.x / hsplit, h = blockIdx.x % hsplit;
-  const int c = (blockIdx.y * vpg + vec) * 8;
-  const int chunk = (HW + hsplit - 1) / hsplit;
-  const int p0 = h * chunk, p1 = min(HW, p0 + chunk);
-  float acc[8];
+  const int vec = tid % g.vpg, l = tid / g.vpg;
+  const int fi = l / g.pl, li = l - fi * g.pl;
+  const int f = (blockIdx.x / g.hsplit) * g.fpb + fi, h = blockIdx.x % g.hsplit;
+  const int c = (blockIdx.y * g.vpg + vec) * 8;
+  const bool act = fi < g.fpb && f < g.frames && c < g.C;
+  const int chunk = (g.HW + g.hsplit - 1) / g.hsplit;
+  const int p0 = h * chunk, p1 = min(g.HW, p0 + chunk);
+  float acc[Q][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  if (pl < npl && c < C) {
-    float sc[8], shf[8];
-    ld8f(pro.scale + c, sc);
-    ld8f(pro.shift + c, shf);
-    // pixels in groups of FS_U with every load of a group issued first (same summation order)
-    auto one = [&](int64_t row, float (&y)[8], const float (&d)[8]) {
+  for (int q = 0; q < Q; ++q)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y[j] = siluf_(y[j] * sc[j] + shf[j]);
-      if (!SEBWD && s_out) st8(s_out + row * C + c, y);
-      if constexpr (SEBWD) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[j] *= d[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += y[j];
-    };
-    constexpr int FS_U = 4;
-    int p = p0 + pl;
-    for (; p + (FS_U - 1) * npl < p1; p += FS_U * npl) {
-      float y[FS_U][8], d[FS_U][8];
-#pragma unroll
-      for (int u = 0; u < FS_U; ++u) {
-        const int64_t row = (int64_t)f * HW + p + u * npl;
-        ld8(Y + row * C + c, y[u]);
-        if constexpr (SEBWD) ld8(dZ + row * C + c, d[u]);
-      }
-#pragma unroll
-      for (int u = 0; u < FS_U; ++u) one((int64_t)f * HW + p + u * npl, y[u], d[u]);
+    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
+  if (act) {
+    float sc[8], shf[8], mu[8], is[8];
+    ld8f(cf.scale + c, sc);
+    ld8f(cf.shift + c, shf);
+    if constexpr (OP == FR_SEBN) {
+      ld8f(cf.mean + c, mu);
+      ld8f(cf.invstd + c, is);
     }
-    for (; p < p1; p += npl) {
-      const int64_t row = (int64_t)f * HW + p;
+    const int64_t fbase = (int64_t)f * g.HW;
+    auto one = [&](int64_t row, float (&y)[8], const float (&d)[8]) {
+      if constexpr (OP == FR_SEBN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = y[j] * sc[j] + shf[j];
+          const float sg = sigmoidf_(z);
+          const float sp = sg * (1.0f + z * (1.0f - sg));
+          const float xh = (y[j] - mu[j]) * is[j];
+          const float dsp = d[j] * sp;
+          acc[0][j] += d[j] * (z * sg);
+          acc[1][j] += dsp;
+          acc[2 % Q][j] += sp;
+          acc[3 % Q][j] += dsp * xh;
+          acc[4 % Q][j] += sp * xh;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[j] = siluf_(y[j] * sc[j] + shf[j]);
+        if (OP == FR_SQUEEZE && s_out) st8(s_out + row * g.C + c, y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[0][j] += OP == FR_SEBWD ? y[j] * d[j] : y[j];
+      }
+    };
+    int p = p0 + li;
+    for (; p + (FR_U - 1) * g.pl < p1; p += FR_U * g.pl) {
+      float y[FR_U][8], d[FR_U][8];
+#pragma unroll
+      for (int u = 0; u < FR_U; ++u) {
+        const int64_t row = fbase + p + u * g.pl;
+        ld8(Y + row * g.C + c, y[u]);
+        if constexpr (OP != FR_SQUEEZE) ld8(dZ + row * g.C + c, d[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < FR_U; ++u) one(fbase + p + u * g.pl, y[u], d[u]);
+    }
+    for (; p < p1; p += g.pl) {
+      const int64_t row = fbase + p;
       float y[8], d[8];
-      ld8(Y + row * C + c, y);
-      if constexpr (SEBWD) ld8(dZ + row * C + c, d);
+      ld8(Y + row * g.C + c, y);
+      if constexpr (OP != FR_SQUEEZE) ld8(dZ + row * g.C + c, d);
       one(row, y, d);
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sh[tid][j] = acc[j];
+  for (int q = 0; q < Q; ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sh[q][tid][j] = acc[q][j];
   __syncthreads();
-  if (tid < vpg && c < C) {
-    for (int r = 1; r < npl; ++r)
+  if (act && li == 0) {
+    for (int r = 1; r < g.pl; ++r) {
+      const int idx = (l + r) * g.vpg + vec;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += sh[r * vpg + tid][j];
-    float* o = part + ((int64_t)h * frames + f) * C + c;
+      for (int q = 0; q < Q; ++q)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = acc[j];
+        for (int j = 0; j < 8; ++j) acc[q][j] += sh[q][idx][j];
+    }
+    const int64_t n = (int64_t)g.frames * g.C;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      float* o = part + ((int64_t)q * g.hsplit + h) * n + (int64_t)f * g.C + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = acc[q][j];
+    }
   }
 }
 
-template <typename T, bool SEBWD>
-static int launch_frame_sum(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
-                            float* part, int64_t part_cap, int* hsplit_out, T* s_out = nullptr) {
-  int vpg, groups;
-  bn_vpg_groups(C, vpg, groups);
-  const int npl = 256 / vpg;
-  int hsplit = 1;
-  while ((int64_t)frames * groups * hsplit < 1024 && HW / (hsplit * 2) >= npl * 2 &&
-         (int64_t)(hsplit * 2) * frames * C <= part_cap)
-    hsplit *= 2;
-  hipLaunchKernelGGL((frame_sum_kernel<T, SEBWD>), dim3(frames * hsplit, groups), dim3(256), 0, s, dZ, Y, pro, frames,
-                     HW, C, hsplit, vpg, part, s_out);
+template <typename T, int OP>
+static int launch_frame_reduce(hipStream_t s, const T* dZ, const T* Y, const FrCoef& cf, int frames, int HW, int C,
+                               float* part, int64_t part_cap, int* hsplit_out, T* s_out = nullptr) {
+  constexpr int Q = OP == FR_SEBN ? 5 : 1;
+  if (frames <= 0 || HW <= 0) { set_error("frame reduce: empty input", __FILE__, __LINE__); return -1; }
+  if ((int64_t)Q * frames * C > part_cap) { set_error("frame reduce: partial buffer too small", __FILE__, __LINE__); return -1; }
+  FrGeom g{frames, HW, C, 1, 0, 0, 1};
+  int groups;
+  bn_vpg_groups(C, g.vpg, groups);
+  const int npl = 256 / g.vpg;
+  g.fpb = std::max(1, std::min(npl, npl * 8 / HW));  // frames per workgroup: >= ~8 pixels per lane
+  g.pl = npl / g.fpb;
+  const int fgroups = cdiv(frames, g.fpb);
+  while ((int64_t)fgroups * groups * g.hsplit < 1024 && HW / (g.hsplit * 2) >= g.pl * 8 &&
+         (int64_t)Q * (g.hsplit * 2) * frames * C <= part_cap)
+    g.hsplit *= 2;
+  hipLaunchKernelGGL((frame_reduce_kernel<T, OP>), dim3(fgroups * g.hsplit, groups), dim3(256), 0, s, dZ, Y, cf, g,
+                     part, s_out);
   DFD_HIP_CHECK(hipGetLastError());
-  *hsplit_out = hsplit;
+  *hsplit_out = g.hsplit;
   return 0;
 }
 
@@ -489,14 +541,16 @@ __global__ void sum_parts_kernel(const float* __restrict__ part, int hsplit, int
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
                       int64_t part_cap, int* hsplit, T* s_out) {
-  return launch_frame_sum<T, false>(s, nullptr, Y, pro, frames, HW, C, part, part_cap, hsplit, s_out);
+  const FrCoef cf{pro.scale, pro.shift, nullptr, nullptr};
+  return launch_frame_reduce<T, FR_SQUEEZE>(s, nullptr, Y, cf, frames, HW, C, part, part_cap, hsplit, s_out);
 }
 
 template <typename T>
 int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
                          float* part, int64_t part_cap, float* dgate) {
   int hs;
-  if (launch_frame_sum<T, true>(s, dZ, Y, pro, frames, HW, C, part, part_cap, &hs)) return -1;
+  const FrCoef cf{pro.scale, pro.shift, nullptr, nullptr};
+  if (launch_frame_reduce<T, FR_SEBWD>(s, dZ, Y, cf, frames, HW, C, part, part_cap, &hs)) return -1;
   const int64_t n = (int64_t)frames * C;
   hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, part, hs, n, 1.0f, dgate);
   DFD_HIP_CHECK(hipGetLastError());
@@ -508,99 +562,22 @@ int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro,
 // stats), sq = mean_hw silu(z) (SE squeeze).  With ge = dL/dout and bc[f][c] = dL/dsq / HW the
 // BN's input gradient is g = (ge*gate + bc) * silu'(z); since gate and bc are constant per
 // (frame, channel), every reduction the backward needs decomposes into per-frame sums that one
-// pass over (ge, y) produces before bc is known:
+// pass over (ge, y) produces before bc is known (frame_reduce_kernel<FR_SEBN>):
 //   D  = sum ge*silu(z)      (-> dgate, the SE branch)
 //   P1 = sum ge*silu'(z)     P2 = sum silu'(z)     P3 = sum ge*silu'(z)*xhat     P4 = sum silu'(z)*xhat
 // so that  sum g = sum_f gate*P1 + bc*P2  and  sum g*xhat = sum_f gate*P3 + bc*P4.  This replaces
 // the separate SE-backward reduction and BN-backward reduction (two full passes over ge and y).
 template <typename T>
-__global__ __launch_bounds__(256) void se_bn_bwd_kernel(const T* __restrict__ dZ, const T* __restrict__ Y,
-                                                        const float* __restrict__ scale,
-                                                        const float* __restrict__ shift,
-                                                        const float* __restrict__ mean,
-                                                        const float* __restrict__ invstd, int frames, int HW, int C,
-                                                        int hsplit, int vpg, float* __restrict__ part) {
-  __shared__ float sh[5][256][8];
-  const int tid = threadIdx.x;
-  const int vec = tid % vpg, pl = tid / vpg, npl = 256 / vpg;
-  const int f = blockIdx.x / hsplit, h = blockIdx.x % hsplit;
-  const int c = (blockIdx.y * vpg + vec) * 8;
-  const int chunk = (HW + hsplit - 1) / hsplit;
-  const int p0 = h * chunk, p1 = min(HW, p0 + chunk);
-  float acc[5][8];
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
-  if (pl < npl && c < C) {
-    float sc[8], shf[8], mu[8], is[8];
-    ld8f(scale + c, sc);
-    ld8f(shift + c, shf);
-    ld8f(mean + c, mu);
-    ld8f(invstd + c, is);
-    for (int p = p0 + pl; p < p1; p += npl) {
-      const int64_t row = (int64_t)f * HW + p;
-      float y[8], d[8];
-      ld8(Y + row * C + c, y);
-      ld8(dZ + row * C + c, d);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float z = y[j] * sc[j] + shf[j];
-        const float sg = sigmoidf_(z);
-        const float sp = sg * (1.0f + z * (1.0f - sg));
-        const float xh = (y[j] - mu[j]) * is[j];
-        const float dsp = d[j] * sp;
-        acc[0][j] += d[j] * (z * sg);
-        acc[1][j] += dsp;
-        acc[2][j] += sp;
-        acc[3][j] += dsp * xh;
-        acc[4][j] += sp * xh;
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sh[q][tid][j] = acc[q][j];
-  __syncthreads();
-  if (tid < vpg && c < C) {
-    for (int r = 1; r < npl; ++r)
-#pragma unroll
-      for (int q = 0; q < 5; ++q)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[q][j] += sh[q][r * vpg + tid][j];
-    const int64_t n = (int64_t)frames * C;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      float* o = part + ((int64_t)q * hsplit + h) * n + (int64_t)f * C + c;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = acc[q][j];
-    }
-  }
-}
-
-template <typename T>
 int launch_se_bn_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const float* scale, const float* shift,
                             const float* mean, const float* invstd, int frames, int HW, int C, float* part,
                             int64_t part_cap, int* hsplit_out) {
-  int vpg, groups;
-  bn_vpg_groups(C, vpg, groups);
-  const int npl = 256 / vpg;
-  if (5 * (int64_t)frames * C > part_cap) { set_error("se/bn bwd: partial buffer too small", __FILE__, __LINE__); return -1; }
-  int hsplit = 1;
-  while ((int64_t)frames * groups * hsplit < 1024 && HW / (hsplit * 2) >= npl * 2 &&
-         5 * (int64_t)(hsplit * 2) * frames * C <= part_cap)
-    hsplit *= 2;
-  hipLaunchKernelGGL((se_bn_bwd_kernel<T>), dim3(frames * hsplit, groups), dim3(256), 0, s, dZ, Y, scale, shift, mean,
-                     invstd, frames, HW, C, hsplit, vpg, part);
-  DFD_HIP_CHECK(hipGetLastError());
-  *hsplit_out = hsplit;
-  return 0;
+  const FrCoef cf{scale, shift, mean, invstd};
+  return launch_frame_reduce<T, FR_SEBN>(s, dZ, Y, cf, frames, HW, C, part, part_cap, hsplit_out);
 }
 
-// BN backward finalize from the per-frame sums of se_bn_bwd_kernel once bc is known:
+// BN backward finalize from the per-frame sums of frame_reduce_kernel<FR_SEBN> once bc is known:
 // dbeta = sum g, dgamma = sum g*xhat, coefficients k1..k3 of dy = k1*g + k2*y + k3 (fp64).
-// The sums P1..P4 are the partials part[1..4][h][f][c] of se_bn_bwd_kernel, added over h in order.
+// The sums P1..P4 are the partials part[1..4][h][f][c] of that kernel, added over h in order.
 // Block = 64 channels x 16 frame slices (the slices' frames unrolled by 4, all loads issued
 // up front); slices added in order.
 constexpr int FF_SL = 16;
@@ -837,12 +814,11 @@ int launch_col_sums(hipStream_t s, const T* X, int64_t M, int C, float* part, in
 
 template <typename T>
 int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat) {
-  // HW is tiny (7x7 at 224^2): one partial per frame, write means directly
-  int vpg, groups;
-  bn_vpg_groups(C, vpg, groups);
-  hipLaunchKernelGGL((frame_sum_kernel<T, false>), dim3(frames, groups), dim3(256), 0, s, (const T*)nullptr, Y, pro,
-                     frames, HW, C, 1, vpg, feat, (T*)nullptr);
-  DFD_HIP_CHECK(hipGetLastError());
+  // HW is tiny (7x7 at 224^2): one partial per frame (the partial buffer is feat itself, so
+  // hsplit = 1), then the means in place
+  const FrCoef cf{pro.scale, pro.shift, nullptr, nullptr};
+  int hs = 1;
+  if (launch_frame_reduce<T, FR_SQUEEZE>(s, nullptr, Y, cf, frames, HW, C, feat, (int64_t)frames * C, &hs)) return -1;
   const int64_t n = (int64_t)frames * C;
   hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, feat, 1, n, 1.0f / (float)HW, feat);
   DFD_HIP_CHECK(hipGetLastError());

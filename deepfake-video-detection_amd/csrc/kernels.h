@@ -21,13 +21,27 @@ int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const
                      int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows);
 int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
+// Fused projection backward (k_pwl_bwd.hip, bf16): ge2 = gs . W (wt = W^T [K][N]), the weight gradient
+// dW[N][K] (+)= gs^T . (silu(y2*sc+sh) * gate) through the slab, and the per-frame SE + BN2 backward
+// sums part[5][*hsplit][frames][K] of launch_se_bn_bwd_reduce.  0 launched, 2 launched without the weight
+// gradient (the caller runs it), 1 not covered, -1 error.
+int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* wt, const bf16* y2, const float* sc, const float* sh,
+                   const float* mean, const float* invstd, const float* gate, int frames, int HW, int N, int K,
+                   bf16* ge2, float* slab, int64_t slab_cap, float* dW, bool accumulate, float* part, int64_t part_cap,
+                   int* hsplit);
+// Fused conv_pw backward through its BN on the fold path (k_pw_fold_bwd.hip, bf16): dx = g . w1t^T +
+// x . q^T + bv (+ r), and the partial products T = g^T x, G = x^T x, cs = 1^T x summed into T / G / cs
+// (launch_reduce_slabs) for pw_wgrad_bn_combine.  0 launched, 1 not covered, -1 error.
+int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* r, const bf16* w1t, const bf16* q,
+                       const float* bv, bf16* dx, int64_t M, int mid, int cin, float* slab, int64_t slab_cap, float* T,
+                       float* G, float* cs);
 // rows threshold of the streaming kernels (returns the previous value)
 // Kernel-selection knobs.  Process-wide defaults (set_* below, dfd_set_tuning), overridden per plan:
 // a plan's forward/backward installs its own Tuning for the enqueuing thread (TuningScope), so
 // concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_MBCONV7, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];

@@ -461,6 +461,12 @@ std::atomic<int64_t> g_fold_min_rows{100000};
 // SLOWER at every threshold (in-process A/B, tools/ab_bench.py) -- the persistent, occupancy-sized
 // depthwise kernels of the main chain lose resident workgroup slots to the concurrent gradients
 std::atomic<int64_t> g_wgrad_stream{0};
+// the projection backward of the bf16 plan as one fused launch (k_pwl_bwd.hip: data gradient, weight
+// gradient and the SE + BN2 backward sums; dfd_set_tuning("pwl_fused", 0) runs the three unfused ones)
+std::atomic<int64_t> g_pwl_fused{1};
+// the fold path's conv_pw backward of the bf16 plan as one fused launch (k_pw_fold_bwd.hip: x . Q,
+// the data gradient and the three weight-gradient products; dfd_set_tuning("fold_fused", 0): unfused)
+std::atomic<int64_t> g_fold_fused{1};
 
 template <typename T>
 int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& ifmt, const float* dfeat,
@@ -580,21 +586,38 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
         DFD_TRY(join(p.ev[1], gs_busy));  // the previous conv_pwl weight gradient is done with o_gs
         DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
-        PROBED(PK_PWL_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout,
-                                                    b.mid, b.cout, PRO_NONE, Pro{}, nullptr, nullptr)));
-        const bool mat = b.o_s2 >= 0;
-        DFD_TRY(fork(p.ev[0]));
-        PROBED_ON(PK_PWL_WGRAD, &b, w,
-                  (launch_pw_wgrad<T>(w, r.a(p.o_gs), mat ? r.a(b.o_s2) : r.a(b.o_y2), Mout, b.cout, b.mid,
-                                      mat ? PRO_GATE : PRO_BN_SILU_G, r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), slab(),
-                                      p.slab_cap, grad(b.pwl.t_w), acc != 0)));
-        DFD_TRY(mark(p.ev[1], gs_busy));
-        // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE
-        // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
-        int hs = 1;
-        DFD_TRY(launch_se_bn_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
-                                           r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), p.frames, hwo, b.mid,
-                                           r.f(p.o_part), p.part_cap, &hs));
+        int hs = 1, pf = 1;
+        if (sizeof(T) == 2 && tune_or(TK_PWL_FUSED, g_pwl_fused.load(std::memory_order_relaxed)) != 0) {
+          // data gradient, weight gradient and the SE + BN2 sums in one pass (k_pwl_bwd.hip)
+          if constexpr (sizeof(T) == 2) {
+            PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(b.o_y2),
+                                                           r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(bn_dw.o_mean),
+                                                           r.f(bn_dw.o_invstd), r.f(b.o_gate), p.frames, hwo,
+                                                           b.cout, b.mid, r.a(p.o_ge2), slab(), p.slab_cap,
+                                                           grad(b.pwl.t_w), acc != 0, r.f(p.o_part), p.part_cap,
+                                                           &hs)) < 0 ? -1 : 0));
+          }
+        }
+        if (pf == 1) {
+          PROBED(PK_PWL_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(p.o_ge2), nullptr, Mout,
+                                                      b.mid, b.cout, PRO_NONE, Pro{}, nullptr, nullptr)));
+        }
+        if (pf != 0) {  // the weight gradient as its own launch (unfused, or the fused kernel without it)
+          const bool mat = b.o_s2 >= 0;
+          DFD_TRY(fork(p.ev[0]));
+          PROBED_ON(PK_PWL_WGRAD, &b, w,
+                    (launch_pw_wgrad<T>(w, r.a(p.o_gs), mat ? r.a(b.o_s2) : r.a(b.o_y2), Mout, b.cout, b.mid,
+                                        mat ? PRO_GATE : PRO_BN_SILU_G, r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), slab(),
+                                        p.slab_cap, grad(b.pwl.t_w), acc != 0)));
+          DFD_TRY(mark(p.ev[1], gs_busy));
+        }
+        if (pf == 1) {
+          // squeeze-excite + the BN+SiLU after the depthwise conv: one pass over (ge2, y2) gives the SE
+          // gate gradient and the per-frame sums of the BN backward (input grad = gated + squeeze path)
+          DFD_TRY(launch_se_bn_bwd_reduce<T>(s, r.a(p.o_ge2), r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
+                                             r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), p.frames, hwo, b.mid,
+                                             r.f(p.o_part), p.part_cap, &hs));
+        }
         // the SE weight gradients (two small products per block, off the critical chain) are
         // batched into one launch per segment: de / dz stay in per-block buffers until then
         if (n_se + 2 > (int)(sizeof(se_jobs) / sizeof(se_jobs[0]))) DFD_TRY(flush_se());
@@ -675,6 +698,34 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
           DFD_TRY(launch_bn_fold_pw<T>(s, r.prm(b.pw.t_w), r.f(p.o_coef1), b.mid, b.cin, r.a(p.o_w1t), r.a(p.o_q),
                                        r.f(p.o_bv)));
           DFD_TRY(join(p.ev[1], gs_busy));  // the conv_pwl weight gradient is done with o_gs
+          int ff = 1;
+          if (sizeof(T) == 2 && tune_or(TK_FOLD_FUSED, g_fold_fused.load(std::memory_order_relaxed)) != 0) {
+            // x . Q, the data gradient and the partial products g^T x, x^T x, 1^T x in one pass
+            // (k_pw_fold_bwd.hip); their three slab reductions as ONE batched launch
+            if constexpr (sizeof(T) == 2) {
+              float* const parts[3] = {r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs)};
+              const int64_t extent[3] = {(int64_t)b.mid * b.cin, (int64_t)b.cin * b.cin, (int64_t)b.cin};
+              SlabDefer loc{};
+              loc.stream = s;
+              loc.lo = parts[0];
+              loc.hi = parts[0] + extent[0];
+              for (int q = 1; q < 3; ++q) {
+                loc.lo = std::min<const float*>(loc.lo, parts[q]);
+                loc.hi = std::max<const float*>(loc.hi, parts[q] + extent[q]);
+              }
+              const DeferScope inner{set_slab_defer(&loc)};
+              PROBED(PK_PW_DGRAD, &b, ((ff = launch_pw_fold_bwd(s, r.a(p.o_ge1), xin, b.skip ? gout : nullptr,
+                                                                r.a(p.o_w1t), r.a(p.o_q), r.f(p.o_bv), gxo, Min,
+                                                                b.mid, b.cin, slab(), p.slab_cap, parts[0], parts[1],
+                                                                parts[2])) < 0 ? -1 : 0));
+              if (ff == 0) DFD_TRY(loc.flush());
+            }
+          }
+          if (ff == 0) {
+            DFD_TRY(launch_pw_wgrad_bn_combine(s, r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs), r.prm(b.pw.t_w),
+                                               r.f(p.o_coef1), b.mid, b.cin, grad(b.pw.t_w), acc != 0));
+            continue;
+          }
           DFD_TRY(launch_tf_gemm<T>(s, xin, r.a(p.o_q), r.a(p.o_gs), b.skip ? gout : nullptr, r.f(p.o_bv), nullptr,
                                     Min, b.cin, b.cin, PRO_NONE, EPI_BIAS | (b.skip ? EPI_RESID : 0)));
           PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(p.o_w1t), gxo, r.a(p.o_gs), Min, b.cin,
@@ -731,6 +782,8 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
 int64_t set_fold_min_rows(int64_t v) { return g_fold_min_rows.exchange(v); }
 int64_t set_wgrad_stream(int64_t v) { return g_wgrad_stream.exchange(v); }
 int64_t set_mbconv7(int64_t v) { return g_mbconv7.exchange(v); }
+int64_t set_pwl_fused(int64_t v) { return g_pwl_fused.exchange(v); }
+int64_t set_fold_fused(int64_t v) { return g_fold_fused.exchange(v); }
 int plan_fused7_blocks(const Plan& p) {
   if (p.dtype != 1) return 0;  // bf16 plans only
   const TuningScope ts(&p.tune);

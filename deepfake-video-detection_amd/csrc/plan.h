@@ -108,6 +108,8 @@ int64_t set_fold_min_rows(int64_t v);
 // default --, 1 every block, N > 1 blocks with >= N gradient rows)
 int64_t set_wgrad_stream(int64_t v);
 int64_t set_mbconv7(int64_t v);
+int64_t set_pwl_fused(int64_t v);
+int64_t set_fold_fused(int64_t v);
 // number of blocks the bf16 forward runs through the fused 7x7 MBConv kernel (0: none)
 int plan_fused7_blocks(const Plan& p);
 // static topology (shape-independent)

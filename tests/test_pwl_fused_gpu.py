@@ -1,0 +1,126 @@
+"""The fused projection backward (``k_pwl_bwd.hip``: conv_pwl data gradient + weight gradient + the
+SE / BN2 backward sums in one pass over the expanded tensor) against the three unfused launches it
+replaces (dgrad GEMM -> weight-gradient GEMM -> ``frame_reduce_kernel<FR_SEBN>``), bf16, on the same
+forward (one forward, two backwards through the same saved tensors).
+
+Both paths round the data gradient to bf16 at the same point and accumulate in fp32; they differ only
+in summation order (the weight gradient's row partition, the per-frame sums' lane order), so the
+first backward segment's outputs agree to fp32-reassociation level and the rest of the backward
+sees one-ulp bf16 flips that grow slowly through the later blocks.  One rounding differs on purpose:
+on the 7x7 blocks the unfused weight gradient reads the forward's materialised bf16 silu(z) and
+rounds its product with the gate again, the fused kernel rounds silu(z)*gate once -- measured 2.3e-3
+relative on blocks.6.0's conv_pwl weight gradient (sums with cancellation), hence ``PWL_TOL``.
+Bounds: the last block's SE / bn2 gradients (identical inputs, same roundings; measured 1e-7..4e-7)
+relative L2 <= ``FIRST_TOL``, its conv_pwl weight gradient <= ``PWL_TOL``; every gradient cosine
+>= 0.998 and norm within 3 % (structurally ~zero tensors skipped; the bounds of
+``test_mbconv7_gpu.py``).  The fused path's own fp32 parity is the per-stage backward check of
+``test_b0_bench_config_gpu.py`` (it runs the default, fused path).  Shapes: the bench's 256 x 224^2 (frame-chunk parts on the 112^2 / 56^2
+maps, whole-frame parts below) and odd batches (5 frames: partial parts; 64^2 input: 2x2 last
+maps, a single 64-row step per frame)."""
+import pytest
+import torch
+
+from deepfake_amd.pretrained_detector import PretrainedBackboneDetector
+from deepfake_amd.weights import deterministic_init_
+
+pytestmark = pytest.mark.gpu
+
+SEED = 43
+FIRST_TOL = 1e-5
+PWL_TOL = 1e-2
+FOLD_TOL = 1e-4
+
+
+def _struct_zero(name):
+    """Biases of the BNs that feed a training-mode BN (through the next conv_pw, and the skip path
+    into the next one): their gradient is zero in exact arithmetic, rounding residue here (the
+    bench-config test excludes the same set)."""
+    return name.endswith("bn3.bias") or name == "backbone.2.0.0.bn2.bias"
+
+
+def _run(cuda, frames, hw, fused_list, knob="pwl_fused"):
+    det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
+                                     compute_dtype="bf16")
+    deterministic_init_(det, seed=SEED)
+    det = det.to(cuda).train()
+    det.ensure_flat()
+    rt = det.backbone.runtime()
+    rt.set_input_norm("imagenet")
+    g = torch.Generator().manual_seed(frames * 7 + hw)
+    x = torch.randint(0, 256, (frames, 3, hw, hw), generator=g, dtype=torch.uint8).to(cuda)
+    with torch.no_grad():
+        feats, (h, ws) = rt.forward(x, det, 1, True)
+    gd = torch.Generator(device=cuda).manual_seed(5)
+    dfeat = torch.randn(frames, 1280, device=cuda, generator=gd) * 1e-3
+    po = det.param_offsets()
+    out = {}
+    for fused in fused_list:
+        rt.set_tuning(knob, 1 if fused else 0)
+        grads = torch.zeros_like(det._flat_p)
+        with torch.no_grad():
+            rt.backward(h, ws, x, dfeat, det, grads, True, 0, 9)
+        torch.cuda.synchronize()
+        out[fused] = {n: grads[po[n]:po[n] + p.numel()].double().clone() for n, p in det.named_parameters()}
+    return out
+
+
+@pytest.mark.parametrize("frames,hw", [(256, 224), (5, 224), (6, 64)])
+def test_fused_projection_backward_matches_unfused(cuda, frames, hw):
+    out = _run(cuda, frames, hw, (False, True))
+    ref, got = out[False], out[True]
+    scale = max(float(v.norm()) for v in ref.values())
+    last = "backbone.2.6.0."
+    first_bad, bad, worst = [], [], []
+    for n, rg in ref.items():
+        gg = got[n]
+        rn = float(rg.norm())
+        assert torch.isfinite(gg).all(), n
+        if n.startswith(last) and any(k in n for k in ("conv_pwl", "se.", "bn2.")):
+            e = float((gg - rg).norm()) / (rn + 1e-30)
+            worst.append((n, e))
+            if e > (PWL_TOL if "conv_pwl" in n else FIRST_TOL):
+                first_bad.append((n, e))
+        if rn <= 1e-3 * scale or _struct_zero(n):
+            continue  # structurally ~zero (bn3 biases): rounding residue on both sides
+        cos = float(gg @ rg) / (float(gg.norm()) * rn + 1e-30)
+        if cos < 0.998 or abs(float(gg.norm()) - rn) > 3e-2 * rn:
+            bad.append((n, round(cos, 6), round(float(gg.norm()) / rn, 5)))
+    print(f"{frames}x{hw}^2: last block rel errors {worst}; outside bound {bad}")
+    assert not first_bad, first_bad
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("frames", [256, 9])  # 9 frames: only blocks.1.0 reaches the fold rows (100,352)
+def test_fused_fold_backward_matches_unfused(cuda, frames):
+    """The fold path's fused conv_pw backward (``k_pw_fold_bwd.hip``: x . Q + data gradient + the g^T x,
+    x^T x, 1^T x products in one pass; the fold blocks whose shapes it takes at 224^2) against its five
+    unfused launches.  The first fused block of the backward sees identical inputs: its conv_pw weight
+    gradient differs only by the fp32 summation order of the partial products (<= ``FOLD_TOL``).  The
+    data gradient skips one bf16 rounding (the unfused x . Q + bv + skip intermediate), so the
+    earlier blocks see one-ulp flips that accumulate through the remaining BN backward reductions
+    (measured at blocks.0.0's SE weights: cosine 0.9988, norm +3.4 %): cosine >= 0.995, norm within
+    5 % downstream (the end-to-end fp32-oracle bounds of the bf16 step are cosine 0.98 / 10 %)."""
+    out = _run(cuda, frames, 224, (False, True), knob="fold_fused")
+    ref, got = out[False], out[True]
+    scale = max(float(v.norm()) for v in ref.values())
+    first = None
+    for blk in ("3.0", "2.1", "2.0", "1.1", "1.0"):  # backward order
+        n = f"backbone.2.{blk}.conv_pw.weight"
+        e = float((got[n] - ref[n]).norm() / ref[n].norm())
+        if e > 0:
+            first = (n, e)
+            break
+    assert first is not None, "no fold block took the fused kernel"
+    bad = []
+    for n, rg in ref.items():
+        gg = got[n]
+        assert torch.isfinite(gg).all(), n
+        rn = float(rg.norm())
+        if rn <= 1e-3 * scale or _struct_zero(n):
+            continue
+        cos = float(gg @ rg) / (float(gg.norm()) * rn + 1e-30)
+        if cos < 0.995 or abs(float(gg.norm()) - rn) > 5e-2 * rn:
+            bad.append((n, round(cos, 6), round(float(gg.norm()) / rn, 5)))
+    print(f"fold fused vs unfused, {frames} frames: first fused block {first}; outside bound {bad}")
+    assert first[1] <= FOLD_TOL, first
+    assert not bad, bad

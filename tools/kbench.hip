@@ -257,15 +257,64 @@ int main(int argc, char** argv) {
         printf("  | first start -> last end %.1f us\n", (t1 - t0) * 0.01);
       }
     }
+    {
+      // the SE squeeze (per-frame sums of silu(bn2(y2)), the 7x7 stages also store the activation)
+      // and the one-pass SE + BN2 backward reduction, on the output-resolution expanded tensor
+      const int hwo = k.hout * k.hout;
+      const int64_t pcap = 4 << 20;
+      int hs = 1;
+      snprintf(nm, sizeof nm, "b%zu %dx%d c%d", i, k.hout, k.hout, C1);
+      const bool mat = Mo < 20000;
+      b.run("se_sq", nm, 2.0 * Mo * C1 * (mat ? 2 : 1), [&] {
+        return launch_se_squeeze<bf16>(b.s, A, pg, F, hwo, C1, stats, pcap, &hs, mat ? C : nullptr);
+      });
+      b.run("se_bn_bwd", nm, 2.0 * 2 * Mo * C1, [&] {
+        return launch_se_bn_bwd_reduce<bf16>(b.s, D, A, sc, sh, mean, invstd, F, hwo, C1, stats, pcap, &hs);
+      });
+    }
+    snprintf(nm, sizeof nm, "b%zu bn3 %ldx%d", i, (long)Mo, k.cout);
+    b.run("bn_apply", nm, 2.0 * (k.s == 1 && k.cin == k.cout ? 3 : 2) * Mo * k.cout, [&] {
+      return launch_bn_apply<bf16>(b.s, B, sc, sh, k.s == 1 && k.cin == k.cout ? D : nullptr, C, Mo, k.cout);
+    });
     BnBwdIn bo{};
     bo.dZ = A; bo.mean = mean; bo.invstd = invstd; bo.scale = sc; bo.shift = sh;
-    snprintf(nm, sizeof nm, "b%zu bn3 %ldx%d", i, (long)Mo, k.cout);
     b.run("bn_bwd_apply", nm, 2.0 * 3 * Mo * k.cout, [&] {
       return launch_bn_bwd_apply<bf16>(b.s, bo, B, coef, C, Mo, k.cout);
     });
     b.run("bn_bwd_reduce", nm, 2.0 * 2 * Mo * k.cout, [&] {
       return launch_bn_bwd_reduce<bf16>(b.s, bo, B, Mo, k.cout, stats, &rows);
     });
+  }
+  if (b.filter == "fused") {
+    // the fused backward kernels at their 256-frame shapes
+    // (k_pwl_bwd.hip: blocks.0.0 / 1.0 / 1.1 projections; k_pw_fold_bwd.hip: blocks.1.0 / 1.1 / 2.0)
+    float* part;
+    CK(hipMalloc(&part, 5ll * F * 1152 * 4 * 4));
+    const int64_t pcap = 5ll * F * 1152 * 4;
+    struct PwlS { int hw, N, K; } pws[3] = {{112, 16, 32}, {56, 24, 96}, {56, 24, 144}};
+    struct FoldS { int hw, cin, mid, skip; } fds[3] = {{112, 16, 96, 0}, {56, 24, 144, 1}, {56, 24, 144, 0}};
+    {
+      const int rows = 64;
+      for (auto& q : pws) {
+        const int64_t M = (int64_t)F * q.hw * q.hw;
+        int hs = 1;
+        snprintf(nm, sizeof nm, "r%d %dx%d %d>%d", rows, q.hw, q.hw, q.K, q.N);
+        b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + M * q.N), [&] {
+          const int rc = launch_pwl_bwd(b.s, A, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw, q.N, q.K, D, slab,
+                                        slab_cap, dW, false, part, pcap, &hs);
+          return rc == 1 ? -1 : rc;
+        });
+      }
+      for (auto& q : fds) {
+        const int64_t M = (int64_t)F * q.hw * q.hw;
+        snprintf(nm, sizeof nm, "r%d %dx%d %d>%d%s", rows, q.hw, q.hw, q.cin, q.mid, q.skip ? " skip" : "");
+        b.run("fused_fold", nm, 2.0 * (M * q.mid + (2 + q.skip) * M * q.cin), [&] {
+          const int rc = launch_pw_fold_bwd(b.s, A, B, q.skip ? C : nullptr, D, D, sc, C + (int64_t)M * 64, M, q.mid,
+                                            q.cin, slab, slab_cap, dW, dW + (1 << 17), dW + (1 << 18));
+          return rc == 1 ? -1 : rc;
+        });
+      }
+    }
   }
   if (b.filter == "rnn") {
     // LogicRNNLSTM per-cell forward launch at the C4 shape (B 64, T 16, H 512, L 2) + phase stamps

@@ -1,6 +1,6 @@
 """Per-training-step summary of a rocprofv3 kernel trace of bench.py.
 
-usage: python tools/step_summary.py <run_kernel_trace.csv> [probe-name-substring]
+usage: python tools/step_summary.py <run_kernel_trace.csv> [probe-name-substring] [--order]
 
 A step is the span between two launches of the stem forward kernel (the first kernel of every
 B0 step).  Prints, for the median step: GPU-busy time, launches, time per kernel class and the
@@ -11,9 +11,10 @@ import re
 import statistics
 import sys
 
-CLASSES = [("fused 7x7 MBConv fwd", r"mbconv7"), ("depthwise fwd", r"dw_fwd"), ("depthwise bwd", r"dw_bwd|dw_dgrad|dw_wgrad"),
+CLASSES = [("fused 7x7 MBConv fwd", r"mbconv7"), ("fused 1x1 backward", r"pwl_bwd|pw_fold_bwd"), ("depthwise fwd", r"dw_fwd"), ("depthwise bwd", r"dw_bwd|dw_dgrad|dw_wgrad"),
            ("1x1 conv fwd/dgrad", r"pw_gemm|pw_stream_kernel"), ("1x1 conv wgrad", r"pw_wgrad|col_sums"),
-           ("stem", r"stem_"), ("BN glue", r"bn_"), ("SE", r"se_|frame_sum|mfma_small|sum_parts"),
+           ("stem", r"stem_"), ("BN glue", r"bn_|frame_reduce_kernel<[^,]+, 2>"),
+           ("SE", r"se_|frame_sum|frame_reduce|mfma_small|sum_parts"),
            ("slab reductions", r"slabs"), ("head / loss", r"linear_|ce_|attn|relu_drop|pool"),
            ("optimizer", r"adam|sumsq|norm_fin|cast_params"), ("other", r".")]
 
@@ -28,7 +29,8 @@ def klass(name):
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
-    probe = sys.argv[2] if len(sys.argv) > 2 else None
+    args = [a for a in sys.argv[2:] if not a.startswith("--")]
+    probe = args[0] if args else None
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     starts = [i for i, r in enumerate(rows) if "stem_fwd" in r["Kernel_Name"]]
@@ -53,6 +55,10 @@ def main():
     print("\nlargest kernels (us/step, launches, avg us)")
     for k, (t, n) in sorted(per.items(), key=lambda x: -x[1][0])[:40]:
         print(f"{t:8.1f} {n:4d} {t / n:8.1f}  {k[:110]}")
+    if "--order" in sys.argv:  # every launch of the median step in issue order
+        print("\nlaunch order (us)")
+        for i, r in enumerate(med):
+            print(f"{i:4d} {dur(r):8.1f}  {r['Kernel_Name'].split('(')[0][:110]}")
     if probe:
         v = [dur(r) for r in rows if probe in r["Kernel_Name"]]
         if v:
