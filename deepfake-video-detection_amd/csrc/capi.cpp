@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "cnnlstm.h"
 #include "head.h"
 #include "plan.h"
 #include "rnn.h"
@@ -423,6 +424,113 @@ int dfd_rn_avgpool(void* stream, int dtype, const void* x, int N, int HW, int C,
   if (!x || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
   if (dtype == 1) return dfd::launch_rn_avgpool((hipStream_t)stream, (const dfd::bf16*)x, N, HW, C, out);
   return dfd::launch_rn_avgpool((hipStream_t)stream, (const float*)x, N, HW, C, out);
+  DFD_GUARD_END
+}
+
+// ---- ResNet-50 training (fp32)
+static dfd::ConvGeom rn_geom(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad) {
+  return dfd::ConvGeom{N, H, W, Cin, Cout, kh, kw, stride, pad, (H + 2 * pad - kh) / stride + 1,
+                       (W + 2 * pad - kw) / stride + 1};
+}
+
+int64_t dfd_rn_conv_stat_rows(int N, int Ho, int Wo) { return ((int64_t)N * Ho * Wo + 63) / 64; }
+
+int dfd_rn_train_conv_fwd(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin,
+                          const float* w, int Cout, int kh, int kw, int stride, int pad, float* wpack, float* y,
+                          float* stats) {
+  DFD_GUARD_BEGIN
+  if (!x || !xs4 || !w || !wpack || !y || !stats) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  const dfd::ConvGeom g = rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad);
+  if ((int64_t)N * g.Ho * g.Wo >= (1ll << 31)) { dfd::set_error("rn conv: too many rows", __FILE__, __LINE__); return -1; }
+  const int64_t xs[4] = {xs4[0], xs4[1], xs4[2], xs4[3]};
+  int rows = 0;
+  return dfd::conv_forward((hipStream_t)stream, g, x, xs, w, nullptr, wpack, y, stats, &rows);
+  DFD_GUARD_END
+}
+
+int dfd_rn_bn_train_finalize(void* stream, const float* stats, int rows, int64_t count, int C, const float* gamma,
+                             const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                             float* mean, float* invstd, float* scale, float* shift) {
+  DFD_GUARD_BEGIN
+  if (!stats || !gamma || !beta || !mean || !invstd || !scale || !shift) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::launch_bn_finalize((hipStream_t)stream, stats, rows, count, C, gamma, beta, running_mean, running_var,
+                                 momentum, eps, true, mean, invstd, scale, shift);
+  DFD_GUARD_END
+}
+
+int dfd_rn_bn_act(void* stream, const float* y, const float* scale, const float* shift, const float* res, int relu,
+                  int64_t M, int C, float* out) {
+  DFD_GUARD_BEGIN
+  if (!y || !scale || !shift || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn_bn_act((hipStream_t)stream, y, scale, shift, res, relu, M, C, out);
+  DFD_GUARD_END
+}
+
+int dfd_rn_pool_train_fwd(void* stream, const float* y, const float* scale, const float* shift, int N, int H, int W,
+                          int C, float* out, uint8_t* argmax) {
+  DFD_GUARD_BEGIN
+  if (!y || !scale || !shift || !out || !argmax) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::bn_relu_pool_fwd((hipStream_t)stream, y, scale, shift, N, H, W, C, (H + 2 - 3) / 2 + 1,
+                               (W + 2 - 3) / 2 + 1, out, argmax);
+  DFD_GUARD_END
+}
+
+int dfd_rn_pool_train_bwd(void* stream, const float* dout, const uint8_t* argmax, const float* y, const float* scale,
+                          const float* shift, int N, int H, int W, int C, float* g) {
+  DFD_GUARD_BEGIN
+  if (!dout || !argmax || !y || !scale || !shift || !g) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::bn_relu_pool_bwd((hipStream_t)stream, dout, argmax, y, scale, shift, N, H, W, C, (H + 2 - 3) / 2 + 1,
+                               (W + 2 - 3) / 2 + 1, g);
+  DFD_GUARD_END
+}
+
+int dfd_rn_relu_bwd(void* stream, const float* dout, const float* out, int64_t n, float* g) {
+  DFD_GUARD_BEGIN
+  if (!dout || !out || !g) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn_relu_bwd((hipStream_t)stream, dout, out, n, g);
+  DFD_GUARD_END
+}
+
+int dfd_rn_gap_bwd(void* stream, const float* dfeat, const float* out, int N, int HW, int C, float* g) {
+  DFD_GUARD_BEGIN
+  if (!dfeat || !out || !g) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn_gap_bwd((hipStream_t)stream, dfeat, out, N, HW, C, g);
+  DFD_GUARD_END
+}
+
+int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, int64_t M, int C, const float* mean,
+                        const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
+                        float* dbeta, float* stats, float* coef, float* dy) {
+  DFD_GUARD_BEGIN
+  if (!g || !y || !mean || !invstd || !scale || !shift || !gamma || !dgamma || !dbeta || !stats || !coef || !dy) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::rn_bn_train_bwd((hipStream_t)stream, g, y, M, C, mean, invstd, scale, shift, gamma, dgamma, dbeta,
+                              stats, coef, dy);
+  DFD_GUARD_END
+}
+
+int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout, int kh,
+                      int kw, int stride, int pad, float* wpack, float* wpack_t, float* dx) {
+  DFD_GUARD_BEGIN
+  if (!dy || !w || !wpack || !wpack_t || !dx) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  const dfd::ConvGeom g = rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad);
+  return dfd::conv_dgrad((hipStream_t)stream, g, dy, w, wpack, wpack_t, dx);
+  DFD_GUARD_END
+}
+
+int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin, const float* dy,
+                      int Cout, int kh, int kw, int stride, int pad, float* slab, int64_t slab_floats, float* dw) {
+  DFD_GUARD_BEGIN
+  if (!x || !xs4 || !dy || !slab || !dw) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  const dfd::ConvGeom g = rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad);
+  if ((int64_t)Cout * Cin * kh * kw > slab_floats) { dfd::set_error("rn wgrad: slab too small", __FILE__, __LINE__); return -1; }
+  const int64_t xs[4] = {xs4[0], xs4[1], xs4[2], xs4[3]};
+  return dfd::conv_wgrad((hipStream_t)stream, g, x, xs, dy, slab, slab_floats, dw);
   DFD_GUARD_END
 }
 

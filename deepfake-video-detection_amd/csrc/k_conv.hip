@@ -4,7 +4,8 @@
 // 64x64 output tile per 256-thread block, BK = 16, operands staged through LDS by "operand
 // policies" that gather on the fly (no im2col buffer):
 //   forward  Y[m][co]  = b[co] + sum_{ky,kx,ci} X[n, oy*s-p+ky, ox*s-p+kx, ci] * W[co][ky][kx][ci]
-//   dgrad    dX[m][ci] = sum_{ky,kx,co} dY[n, iy+p-ky, ix+p-kx, co] * W[co][ci][ky][kx]   (s = 1)
+//   dgrad    dX[m][ci] = sum_{ky,kx,co} dY[n, (iy+p-ky)/s, (ix+p-kx)/s, co] * W[co][ci][ky][kx]
+//            over the taps whose output position is integral (s = 1 or 2)
 //   wgrad    dW[co][(ky,kx,ci)] = sum_m dY[m][co] * X(m, ky, kx, ci)     (split over m, slabs)
 // NHWC activations (the input frames are read through their strides, channels-last per
 // SURVEY F10); the forward epilogue writes per-tile BatchNorm partial rows (sum, sum of squares).
@@ -101,12 +102,14 @@ struct OpConvA {
     }
   }
 };
-// dgrad gather (stride 1): rows = input pixels (n, iy, ix); k = (ky, kx, co), co fastest;
-// source dY [N][Ho][Wo][Co] at (iy + p - ky, ix + p - kx)
+// dgrad gather: rows = input pixels (n, iy, ix); k = (ky, kx, co), co fastest; source dY
+// [N][Ho][Wo][Co] at ((iy + p - ky) / S, (ix + p - kx) / S) where both divide (S = 1 or 2; the
+// other taps of a stride-2 conv never touched this pixel and read as zero)
 struct OpConvDgradA {
   const float* dy;
   int Ho, Wo, Co, KW, P, H, W, R, K;
   FDiv fCo, fKW, fHW, fW;  // set by the launcher (fdiv_make)
+  int S;                   // 1 or 2, set by the launcher
   int iy[4], ix[4];
   int64_t base[4];
   static constexpr bool kR = false;
@@ -128,8 +131,9 @@ struct OpConvDgradA {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + (tid + 256 * i) / CG_K;
-      const int oy = iy[i] - ky, ox = ix[i] - kx;
-      ok[i] = r < R && k < K && oy >= 0 && oy < Ho && ox >= 0 && ox < Wo;
+      const int ty = iy[i] - ky, tx = ix[i] - kx;  // = oy * S, ox * S
+      const int oy = S == 1 ? ty : ty >> 1, ox = S == 1 ? tx : tx >> 1;
+      ok[i] = r < R && k < K && ty >= 0 && tx >= 0 && (S == 1 || ((ty | tx) & 1) == 0) && oy < Ho && ox < Wo;
       v[i] = *(ok[i] ? dy + base[i] + ((int64_t)oy * Wo + ox) * Co + co : dy);
     }
   }
@@ -438,13 +442,14 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
 }
 
 int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX) {
-  if (g.S != 1) { set_error("conv dgrad: stride 1 only", __FILE__, __LINE__); return -1; }
+  if (g.S != 1 && g.S != 2) { set_error("conv dgrad: stride 1 or 2", __FILE__, __LINE__); return -1; }
   const int KK = g.KH * g.KW;
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
                      wd);
   const int M = g.N * g.H * g.W, K = KK * g.Co;
   OpConvDgradA pa{dY, g.Ho, g.Wo, g.Co, g.KW, g.P, g.H, g.W, M, K};
   pa.fCo = fdiv_make(g.Co); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.H * g.W); pa.fW = fdiv_make(g.W);
+  pa.S = g.S;
   OpRows pb{wd, K, g.Ci, K};
   return conv_gemm<OpConvDgradA, OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr);
 }

@@ -636,6 +636,7 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
     if (N == 40 && K == 40) DFD_WGS(3, 3, 2, PRO_NONE);
     if (N == 144 && K == 24) DFD_WGS(5, 2, 2, PRO_NONE);   // N in 2 chunks of 80
     if (N == 240 && K == 40) DFD_WGS(5, 3, 1, PRO_NONE);   // N in 3 chunks of 80
+    if (N == 480 && K == 80) DFD_WGS(4, 5, 1, PRO_NONE);   // 14x14 stage: N in chunks of 64 (-1 us)
     return 1;
   }
   if (pro_mode == PRO_BN_SILU_G) {  // conv_pwl: N = cout, K = mid
@@ -643,6 +644,10 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
     if (N == 24 && K == 96) DFD_WGS(2, 6, 1, PRO_BN_SILU_G);
     if (N == 24 && K == 144) DFD_WGS(2, 5, 1, PRO_BN_SILU_G);  // K in 2 chunks of 80
     if (N == 40 && (K == 144 || K == 240)) DFD_WGS(3, 5, 1, PRO_BN_SILU_G);
+    // 14x14 stage (tools/kbench, against the tiled wgrad): 80x240 31 -> 29 us, 80x480 44 -> 37 us,
+    // 112x480 45 -> 38 us, 112x672 55 -> 44 us
+    if (N == 80 && (K == 240 || K == 480)) DFD_WGS(5, 4, 1, PRO_BN_SILU_G);   // K in chunks of 64
+    if (N == 112 && (K == 480 || K == 672)) DFD_WGS(7, 3, 1, PRO_BN_SILU_G);  // K in chunks of 48
     return 1;
   }
 #undef DFD_WGS

@@ -29,6 +29,8 @@
 // part's slab row (summed in order by launch_reduce_slabs).  Deterministic throughout.
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace dfd {
 
 
@@ -39,7 +41,9 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 
 struct PwlBwdArgs {
-  const bf16* gs;   // [M][N]
+  const bf16* gs;   // [M][N] (or, with coef3: the block's output gradient dZ, gs = k1*dZ + k2*y3 + k3)
+  const bf16* y3;   // [M][N] pre-BN3 projection output (with coef3)
+  const float* coef3;  // [3][N] BN3 backward coefficients k1, k2, k3, or nullptr (gs given)
   const bf16* wt;   // [K][N]: row k holds W[:, k] (the cast conv_pwl weight, transposed)
   const bf16* y2;   // [M][K]
   const float *sc, *sh, *mean, *invstd;  // BN2 (after the depthwise conv) [K]
@@ -66,7 +70,7 @@ struct PbTile {
   static constexpr int W_BYTES = KBC * NG * 1024;
   static constexpr int G_BYTES = PB_R * GS * 2;
   static constexpr int T_BYTES = PB_R * XS * 2;
-  static constexpr int SMEM = W_BYTES + G_BYTES + (WG ? 3 : 2) * T_BYTES + 4 * KC * 4;
+  static constexpr int SMEM = W_BYTES + G_BYTES + (WG ? 3 : 2) * T_BYTES + 4 * KC * 4 + 3 * NP * 4;
   static_assert(KBC >= 1 && KBC <= 4, "one k-block per wave");
 };
 
@@ -89,6 +93,7 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
   bf16* Ys = Xs + (WG ? PB_R * TL::XS : 0);                 // [R][XS] raw y2
   bf16* Cs = Ys + PB_R * TL::XS;                            // [R][XS] ge2
   float* co = reinterpret_cast<float*>(Cs + PB_R * TL::XS);  // [4][KC] sc sh mean invstd
+  float* c3 = co + 4 * TL::KC;                                // [3][NP] BN3 k1 k2 k3 (coef3)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // the k-chunks of one part (same gs rows) are dealt to one XCD: gs is fetched once per L2
@@ -113,6 +118,11 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
       co[2 * TL::KC + i] = ok ? a.mean[k0 + i] : 0.f;
       co[3 * TL::KC + i] = ok ? a.invstd[k0 + i] : 0.f;
     }
+    if (a.coef3)
+      for (int i = tid; i < 3 * TL::NP; i += 256) {
+        const int q = i / TL::NP, n = i - q * TL::NP;
+        c3[i] = n < N ? a.coef3[q * N + n] : 0.f;
+      }
   }
 
   // the part's rows
@@ -134,19 +144,24 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
   const int spf = (pc1 - pc0 + PB_R - 1) / PB_R;
   const int nsteps = nf > 0 && pc1 > pc0 ? nf * spf : 0;
 
-  Raw8<bf16> rg[TL::NLG], ry[TL::NLK];
-  auto load = [&](int st) {
+  // two register sets: the rows of step st + 2 are loaded while step st is staged and computed
+  Raw8<bf16> rg[2][TL::NLG], r3[2][TL::NLG], ry[2][TL::NLK];
+  const bool bn3 = a.coef3 != nullptr;
+  auto load = [&](auto setc, int st) {
+    constexpr int S = decltype(setc)::value;
     const int f = fA + st / spf, pb = pc0 + (st % spf) * PB_R, pe = min(pc1, pb + PB_R);
     const int64_t rb = (int64_t)f * HW + pb;
 #pragma unroll
     for (int i = 0; i < TL::NLG; ++i) {
       const int v = tid + 256 * i, rr = v / TL::VG, cv = (v - rr * TL::VG) * 8;
-      raw_ld(rg[i], a.gs + (rb + rr) * N + cv, a.gs, rr < PB_R && pb + rr < pe && cv < N);
+      const bool ok = rr < PB_R && pb + rr < pe && cv < N;
+      raw_ld(rg[S][i], a.gs + (rb + rr) * N + cv, a.gs, ok);
+      if (bn3) raw_ld(r3[S][i], a.y3 + (rb + rr) * N + cv, a.y3, ok);
     }
 #pragma unroll
     for (int i = 0; i < TL::NLK; ++i) {
       const int v = tid + 256 * i, rr = v / TL::VK, cv = (v - rr * TL::VK) * 8;
-      raw_ld(ry[i], a.y2 + (rb + rr) * K + k0 + cv, a.y2, rr < PB_R && pb + rr < pe && k0 + cv < K);
+      raw_ld(ry[S][i], a.y2 + (rb + rr) * K + k0 + cv, a.y2, rr < PB_R && pb + rr < pe && k0 + cv < K);
     }
   };
 
@@ -163,7 +178,8 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) se[q][r] = 0.f;
 
-  if (nsteps > 0) load(0);
+  if (nsteps > 0) load(std::integral_constant<int, 0>{}, 0);
+  if (nsteps > 1) load(std::integral_constant<int, 1>{}, 1);
   __syncthreads();  // fragments and coefficients staged
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -175,27 +191,45 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
     cval[r] = cw && k0 + kl + r < K ? 1.f : 0.f;
   }
 
-  for (int st = 0; st < nsteps; ++st) {
+  auto step = [&](auto setc, int st) {
+    constexpr int S = decltype(setc)::value;
     const int f = fA + st / spf, pb = pc0 + (st % spf) * PB_R, pe = min(pc1, pb + PB_R);
     const int64_t rb = (int64_t)f * HW + pb;
     // ---- staging: gs, raw y2 and act into LDS ----
 #pragma unroll
     for (int i = 0; i < TL::NLG; ++i) {
       const int v = tid + 256 * i, rr = v / TL::VG, cv = (v - rr * TL::VG) * 8;
-      if (rr < PB_R) raw_st(Gs + rr * TL::GS + cv, rg[i]);
+      if (rr < PB_R) {
+        if (bn3) {  // the BN3 backward apply (bn_bwd_apply's arithmetic), rounded to bf16 like its store
+          float z[8], y[8], k1[8], k2[8], k3[8];
+          raw_to_f(rg[S][i], z);
+          raw_to_f(r3[S][i], y);
+          ld8(c3 + cv, k1);
+          ld8(c3 + TL::NP + cv, k2);
+          ld8(c3 + 2 * TL::NP + cv, k3);
+          const uint32_t msk = rg[S][i].ok ? 0xffffffffu : 0u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) z[j] = k1[j] * z[j] + k2[j] * y[j] + k3[j];
+          *reinterpret_cast<uint4*>(Gs + rr * TL::GS + cv) =
+              make_uint4(pack2bf(z[0], z[1]) & msk, pack2bf(z[2], z[3]) & msk, pack2bf(z[4], z[5]) & msk,
+                         pack2bf(z[6], z[7]) & msk);
+        } else {
+          raw_st(Gs + rr * TL::GS + cv, rg[S][i]);
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < TL::NLK; ++i) {
       const int v = tid + 256 * i, rr = v / TL::VK, cv = (v - rr * TL::VK) * 8;
       if (rr < PB_R) {
-        raw_st(Ys + rr * TL::XS + cv, ry[i]);
+        raw_st(Ys + rr * TL::XS + cv, ry[S][i]);
         if constexpr (!WG) continue;
         float x[8], sc[8], sh[8], gv[8];
-        raw_to_f(ry[i], x);
+        raw_to_f(ry[S][i], x);
         ld8(co + cv, sc);
         ld8(co + TL::KC + cv, sh);
         ld8f(a.gate + (int64_t)f * K + (k0 + cv < K ? k0 + cv : 0), gv);
-        const uint32_t msk = ry[i].ok ? 0xffffffffu : 0u;
+        const uint32_t msk = ry[S][i].ok ? 0xffffffffu : 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * gv[j];
         *reinterpret_cast<uint4*>(Xs + rr * TL::XS + cv) =
@@ -204,7 +238,7 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
       }
     }
     lds_barrier();
-    if (st + 1 < nsteps) load(st + 1);  // next step's rows in flight during this step's math
+    if (st + 2 < nsteps) load(setc, st + 2);  // rows two steps ahead in flight during this step's math
 
     if (cw) {
       // ---- data gradient: D[k][m] = W^T[k][:] . gs[m][:]^T, 4 row blocks ----
@@ -304,6 +338,10 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
         *reinterpret_cast<uint4*>(a.ge2 + (rb + rr) * K + k0 + cv) =
             *reinterpret_cast<const uint4*>(Cs + rr * TL::XS + cv);
     }
+  };
+  for (int st = 0; st < nsteps; st += 2) {
+    step(std::integral_constant<int, 0>{}, st);
+    if (st + 1 < nsteps) step(std::integral_constant<int, 1>{}, st + 1);
   }
 
   // ---- this part's weight-gradient rows: dW[n][k] of the wave's k-block ----
@@ -355,13 +393,16 @@ static int pb_launch(hipStream_t s, PwlBwdArgs& a, int64_t slab_cap, float* dW, 
 
 // 0: launched (all three outputs); 2: launched without the weight gradient (the caller runs it);
 // 1: shape not covered (the caller runs the three unfused launches); -1: error
-int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* wt, const bf16* y2, const float* sc, const float* sh,
-                   const float* mean, const float* invstd, const float* gate, int frames, int HW, int N, int K,
-                   bf16* ge2, float* slab, int64_t slab_cap, float* dW, bool accumulate, float* part, int64_t part_cap,
-                   int* hsplit) {
-  if (frames <= 0 || HW <= 0 || (N & 7) || (K & 15) || N > 24) return 1;
-  if ((int64_t)frames * HW * std::max(N, K) >= (1ll << 31)) return 1;
-  PwlBwdArgs a{gs, wt, y2, sc, sh, mean, invstd, gate, ge2, slab, part, frames, HW, N, K, 1, 1, 1};
+bool pwl_bwd_covers(int frames, int HW, int N, int K) {
+  return frames > 0 && HW > 0 && !(N & 7) && !(K & 15) && N <= 24 && (int64_t)frames * HW * std::max(N, K) < (1ll << 31);
+}
+
+int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* y3, const float* coef3, const bf16* wt, const bf16* y2,
+                   const float* sc, const float* sh, const float* mean, const float* invstd, const float* gate,
+                   int frames, int HW, int N, int K, bf16* ge2, float* slab, int64_t slab_cap, float* dW,
+                   bool accumulate, float* part, int64_t part_cap, int* hsplit) {
+  if (!pwl_bwd_covers(frames, HW, N, K) || (coef3 && !y3)) return 1;
+  PwlBwdArgs a{gs, y3, coef3, wt, y2, sc, sh, mean, invstd, gate, ge2, slab, part, frames, HW, N, K, 1, 1, 1};
   const int ng = cdiv(N, 32);
   const int kbc = K <= 32 ? 2 : 3;
   // 64-row steps: 128-row steps doubled the staging registers to one wave per SIMD and measured

@@ -23,12 +23,14 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
 // Fused projection backward (k_pwl_bwd.hip, bf16): ge2 = gs . W (wt = W^T [K][N]), the weight gradient
 // dW[N][K] (+)= gs^T . (silu(y2*sc+sh) * gate) through the slab, and the per-frame SE + BN2 backward
-// sums part[5][*hsplit][frames][K] of launch_se_bn_bwd_reduce.  0 launched, 2 launched without the weight
-// gradient (the caller runs it), 1 not covered, -1 error.
-int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* wt, const bf16* y2, const float* sc, const float* sh,
-                   const float* mean, const float* invstd, const float* gate, int frames, int HW, int N, int K,
-                   bf16* ge2, float* slab, int64_t slab_cap, float* dW, bool accumulate, float* part, int64_t part_cap,
-                   int* hsplit);
+// sums part[5][*hsplit][frames][K] of launch_se_bn_bwd_reduce.  With coef3 (the BN3 backward
+// coefficients [3][N]) gs is the block's output gradient dZ and the kernel applies the BN3 backward
+// gs = k1*dZ + k2*y3 + k3 while staging (no separate apply pass).  0 launched, 1 not covered, -1 error.
+bool pwl_bwd_covers(int frames, int HW, int N, int K);
+int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* y3, const float* coef3, const bf16* wt, const bf16* y2,
+                   const float* sc, const float* sh, const float* mean, const float* invstd, const float* gate,
+                   int frames, int HW, int N, int K, bf16* ge2, float* slab, int64_t slab_cap, float* dW,
+                   bool accumulate, float* part, int64_t part_cap, int* hsplit);
 // Fused conv_pw backward through its BN on the fold path (k_pw_fold_bwd.hip, bf16): dx = g . w1t^T +
 // x . q^T + bv (+ r), and the partial products T = g^T x, G = x^T x, cs = 1^T x summed into T / G / cs
 // (launch_reduce_slabs) for pw_wgrad_bn_combine.  0 launched, 1 not covered, -1 error.
@@ -74,6 +76,14 @@ template <typename T>
 int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* out);
 template <typename T>
 int launch_rn_avgpool(hipStream_t s, const T* x, int N, int HW, int C, float* out);
+// ResNet-50 training pieces (k_rntrain.hip, fp32)
+int rn_bn_act(hipStream_t s, const float* y, const float* sc, const float* sh, const float* r, int relu, int64_t M,
+              int C, float* out);
+int rn_relu_bwd(hipStream_t s, const float* dout, const float* out, int64_t n, float* g);
+int rn_gap_bwd(hipStream_t s, const float* dfeat, const float* out, int N, int HW, int C, float* g);
+int rn_bn_train_bwd(hipStream_t s, const float* g, const float* y, int64_t M, int C, const float* mean,
+                    const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
+                    float* dbeta, float* stats, float* coef, float* dy);
 
 // Fused 7x7-stage MBConv forward (k_mbconv7.hip): one workgroup per frame, the expanded tensor in LDS
 struct Mb7Bn {

@@ -585,17 +585,41 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         BnBwdIn i3{};
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
         DFD_TRY(join(p.ev[1], gs_busy));  // the previous conv_pwl weight gradient is done with o_gs
-        DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
         int hs = 1, pf = 1;
-        if (sizeof(T) == 2 && tune_or(TK_PWL_FUSED, g_pwl_fused.load(std::memory_order_relaxed)) != 0) {
-          // data gradient, weight gradient and the SE + BN2 sums in one pass (k_pwl_bwd.hip)
+        const bool fpwl = sizeof(T) == 2 && tune_or(TK_PWL_FUSED, g_pwl_fused.load(std::memory_order_relaxed)) != 0 &&
+                          pwl_bwd_covers(p.frames, hwo, b.cout, b.mid);
+        // the BN3 backward applied in the fused kernel's staging pays where the projection is 16 wide
+        // (blocks.0.0: +12 us in the kernel against a 49 us apply pass); at 24 wide the kernel's
+        // extra time exceeds the pass (+29 / +36 us against 18 us, tools/kbench fused)
+        if (fpwl && b.cout <= 16) {
+          // data gradient, weight gradient and the SE + BN2 sums in one pass (k_pwl_bwd.hip), the BN3
+          // backward applied in its staging: only the BN3 reduction + finalize run here
+          i3.mean = r.f(b.bn3.o_mean); i3.invstd = r.f(b.bn3.o_invstd);
+          i3.scale = r.f(b.bn3.o_scale); i3.shift = r.f(b.bn3.o_shift);
+          DFD_TRY(launch_bn_bwd_reduce<T>(s, i3, r.a(b.o_y3), Mout, b.cout, r.f(p.o_stats), &rows));
+          DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), rows, Mout, b.cout, r.prm(b.bn3.t_w), r.f(b.bn3.o_mean),
+                                         r.f(b.bn3.o_invstd), tr != 0, grad(b.bn3.t_w), grad(b.bn3.t_b), acc != 0,
+                                         r.f(p.o_coef)));
           if constexpr (sizeof(T) == 2) {
-            PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, r.a(p.o_gs), r.a(b.pwl.o_wt), r.a(b.o_y2),
-                                                           r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(bn_dw.o_mean),
-                                                           r.f(bn_dw.o_invstd), r.f(b.o_gate), p.frames, hwo,
-                                                           b.cout, b.mid, r.a(p.o_ge2), slab(), p.slab_cap,
-                                                           grad(b.pwl.t_w), acc != 0, r.f(p.o_part), p.part_cap,
-                                                           &hs)) < 0 ? -1 : 0));
+            PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, gout, r.a(b.o_y3), r.f(p.o_coef), r.a(b.pwl.o_wt),
+                                                           r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
+                                                           r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), r.f(b.o_gate),
+                                                           p.frames, hwo, b.cout, b.mid, r.a(p.o_ge2), slab(),
+                                                           p.slab_cap, grad(b.pwl.t_w), acc != 0, r.f(p.o_part),
+                                                           p.part_cap, &hs)) < 0 ? -1 : 0));
+          }
+          if (pf != 0) { set_error("pwl_bwd: covered shape not launched", __FILE__, __LINE__); return -1; }
+        } else {
+          DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
+          if (fpwl) {
+            if constexpr (sizeof(T) == 2) {
+              PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, r.a(p.o_gs), nullptr, nullptr, r.a(b.pwl.o_wt),
+                                                             r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
+                                                             r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), r.f(b.o_gate),
+                                                             p.frames, hwo, b.cout, b.mid, r.a(p.o_ge2), slab(),
+                                                             p.slab_cap, grad(b.pwl.t_w), acc != 0, r.f(p.o_part),
+                                                             p.part_cap, &hs)) < 0 ? -1 : 0));
+            }
           }
         }
         if (pf == 1) {

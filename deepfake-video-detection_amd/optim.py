@@ -1,4 +1,4 @@
-"""Fused global-norm clipping + Adam/AdamW over one flat fp32 buffer (K8).
+"""Fused global-norm clipping + Adam/AdamW over flat fp32 buffers (K8).
 
 Replaces the reference step ``torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)`` +
 ``optimizer.step()`` with ``optim.AdamW(params, lr, weight_decay)``
@@ -6,13 +6,35 @@ Replaces the reference step ``torch.nn.utils.clip_grad_norm_(model.parameters(),
 Update arithmetic and scalar rounding follow ``torch.optim`` (single-tensor path) so the
 result matches the reference step to fp32 rounding; clipping semantics match
 ``clip_grad_norm_`` (coefficient ``min(1, max_norm / (norm + 1e-6))``; the gradients are left
-clipped in ``.grad``).  Everything stays on the device: no ``.item()`` per step.
+clipped in ``.grad``).  Everything stays on the device: no ``.item()`` per step.  The parameters
+are one ``FlatModule``'s (one buffer) or several (``EnsembleDetector``: one buffer per member, the
+clipping norm taken over all of them, like ``clip_grad_norm_(ensemble.parameters())``).
 """
 from __future__ import annotations
 
 import torch
 
 from . import _lib, ops  # noqa: F401  (registers torch.ops.dfd.*)
+
+
+def _runs(tensors):
+    """Split ``tensors`` into maximal runs of consecutive views of one storage:
+    [(flat view, first index, end index)], or None if some tensor is not contiguous."""
+    out, i0 = [], 0
+    for i in range(1, len(tensors) + 1):
+        if i < len(tensors):
+            a, b = tensors[i - 1], tensors[i]
+            if not b.is_contiguous():
+                return None
+            if (b.untyped_storage().data_ptr() == a.untyped_storage().data_ptr()
+                    and b.storage_offset() == a.storage_offset() + a.numel()):
+                continue
+        fl = _flat_view(tensors[i0:i])
+        if fl is None:
+            return None
+        out.append((fl, i0, i))
+        i0 = i
+    return out
 
 
 def _flat_view(tensors):
@@ -41,11 +63,20 @@ class _FusedAdamBase(torch.optim.Optimizer):
         self.max_grad_norm = max_grad_norm
         self.grad_scale = grad_scale
         ps = self.param_groups[0]["params"]
-        self._flat_p = _flat_view(ps)
-        if self._flat_p is None:
-            raise ValueError("fused Adam(W) needs the parameters of one FlatModule (consecutive views of one buffer)")
-        dev = self._flat_p.device
-        n = self._flat_p.numel()
+        self._runs = _runs(ps)
+        if self._runs is None or len(self._runs) > 8:
+            raise ValueError("fused Adam(W) needs the parameters of FlatModules (consecutive views of flat buffers)")
+        dev = self._runs[0][0].device
+        n = sum(r[0].numel() for r in self._runs)
+        # run of each parameter and the moment-buffer offset of each run
+        self._run_of = [0] * len(ps)
+        self._run_off = []
+        o = 0
+        for k, (fl, i0, i1) in enumerate(self._runs):
+            for i in range(i0, i1):
+                self._run_of[i] = k
+            self._run_off.append(o)
+            o += fl.numel()
         self._m = torch.zeros(n, dtype=torch.float32, device=dev)
         self._v = torch.zeros(n, dtype=torch.float32, device=dev)
         # per-parameter step counts, as torch.optim keeps them (a parameter without a gradient is
@@ -80,7 +111,8 @@ class _FusedAdamBase(torch.optim.Optimizer):
             if p.grad is None or not p.requires_grad:
                 continue
             lo, hi = self._offs[i], self._offs[i] + p.numel()
-            if out and out[-1][1] == lo and self._steps[out[-1][2]] == self._steps[i]:
+            if (out and out[-1][1] == lo and self._steps[out[-1][2]] == self._steps[i] and
+                    self._run_of[out[-1][2]] == self._run_of[i]):
                 out[-1] = (out[-1][0], hi, out[-1][2], i + 1)
             else:
                 out.append((lo, hi, i, i + 1))
@@ -116,7 +148,10 @@ class _FusedAdamBase(torch.optim.Optimizer):
             step = self._steps[i0] + 1
             for i in range(i0, i1):
                 self._steps[i] = step
-            torch.ops.dfd.adam_step(self._flat_p[lo:hi], flat_g, self._m[lo:hi], self._v[lo:hi], float(g["lr"]),
+            k = self._run_of[i0]
+            ro = self._run_off[k]
+            torch.ops.dfd.adam_step(self._runs[k][0][lo - ro:hi - ro], flat_g, self._m[lo:hi], self._v[lo:hi],
+                                    float(g["lr"]),
                                     float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]), step,
                                     float(self.grad_scale), bool(self.decoupled), clip)
             if scatter is not None:  # gradients were gathered: leave the clipped values in .grad

@@ -23,8 +23,9 @@ atol 1e-5 on logits and loss) or ``"bf16"`` (the training/serving performance mo
 tests/test_b0_224_gpu.py and tests/test_serving.py).
 
 Backbones: ``efficientnet_b0`` (the hot path: training and inference) and ``resnet50`` (the app's
-default ensemble member, ``app.py:661,1597``: inference only -- ``resnet.ResNet50Trunk``, torchvision
-key names, eval BatchNorm folded into hipBLASLt GEMMs).  ``pretrained=True`` would download timm /
+default ensemble member, ``app.py:661,1597`` -- ``resnet.ResNet50Trunk``, torchvision key names;
+inference on implicit-GEMM MFMA kernels with the eval BatchNorm folded in, training in fp32 with
+train-mode BatchNorm on the implicit-GEMM forward / data-gradient / weight-gradient kernels).  ``pretrained=True`` would download timm /
 torchvision weights in the reference and is refused here (offline; load a checkpoint instead).
 """
 from __future__ import annotations
@@ -54,7 +55,7 @@ class PretrainedBackboneDetector(FlatModule):
         super().__init__()
         if backbone_name not in ("efficientnet_b0", "resnet50"):
             raise ValueError(f"Unsupported backbone: {backbone_name} (the MI355X path implements "
-                             f"efficientnet_b0 and, for inference, resnet50)")
+                             f"efficientnet_b0 and resnet50)")
         if pretrained:
             raise RuntimeError("pretrained=True fetches timm ImageNet weights, which is unavailable offline; "
                                "construct with pretrained=False and load a checkpoint (app.py:1691 does)")
@@ -135,7 +136,7 @@ class PretrainedBackboneDetector(FlatModule):
         x_flat = x.reshape(batch_size * num_frames, c, h, w)
         sink = GradSink(self)
         if isinstance(self.backbone, ResNet50Trunk):
-            feats = self.backbone(x_flat)  # (B*T, 2048), inference only
+            feats = self.backbone(x_flat)  # (B*T, 2048); train mode: fp32 autograd node (resnet._RnTrainFn)
         else:
             feats = self.backbone(x_flat, grad_sink=sink)  # (B*T, 1280)
         p = float(self.dropout.p) if self.training else 0.0
@@ -211,7 +212,8 @@ class _HeadFn(torch.autograd.Function):
 class EnsembleDetector(nn.Module):
     """``src/pretrained_detector.py:146-218``: efficientnet_b0 and resnet50 members (the app's
     default ``['efficientnet_b0', 'resnet50']``) run on the HIP path; the ensemble combination is a
-    few ops on (M, B, C) logits.  A resnet50 member is inference-only (``.eval()``)."""
+    few ops on (M, B, C) logits.  Both members train (``EnsembleTrainer.train_epoch``,
+    src/ensemble_trainer.py:158-229); the resnet50 member trains in fp32."""
 
     accepts_uint8_frames = True
 

@@ -17,8 +17,15 @@ INFERENCE forward on HIP, NHWC:
   uint8 with the input normalisation inside, like the B0 stem) and runs on the same MFMA kernel
   (``dfd_rn_gemm``); maxpool and the global average pool are HIP kernels (``csrc/k_resnet.hip``).
 
-Training mode is not provided for this member (the hot path trains EfficientNet-B0): calling it
-with gradients enabled, or in ``.train()`` mode, raises instead of silently using batch statistics.
+TRAINING (``.train()``: ``EnsembleTrainer.train_epoch`` trains every member of the ensemble,
+``src/ensemble_trainer.py:158-229``) runs in fp32 with torchvision's train-mode semantics -- batch
+statistics (biased variance) normalise, the running buffers update with momentum 0.1 and the
+unbiased variance, ``num_batches_tracked`` counts -- as one autograd node over the trunk
+(``_RnTrainFn``): every convolution's forward, data gradient (stride 1 and 2) and weight gradient
+are exact-fp32 implicit-GEMM MFMA kernels (``csrc/k_conv.hip``), the BatchNorm backward is the B0
+path's reduce / finalize / apply (``csrc/k_bn.hip``), the ReLU / residual / pooling pieces are
+``csrc/k_rntrain.hip`` and ``k_conv.hip`` kernels.  bf16 training of this member is refused
+(``compute_dtype='fp32'`` for training; bf16 remains the serving dtype).
 """
 from __future__ import annotations
 
@@ -142,20 +149,256 @@ class ResNet50Trunk(nn.Sequential):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """(N, 3, H, W) frames (fp32, or uint8 normalised in the conv1 gather) -> (N, 2048) fp32."""
-        if self.training:
-            raise NotImplementedError("the ResNet-50 ensemble member runs inference only on the MI355X path "
-                                      "(call .eval(); training is provided for efficientnet_b0)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("no backward for the ResNet-50 member: run it under torch.no_grad() or "
-                                      "freeze its parameters")
         _lib.require_hip(x, "frames")
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected (N, 3, H, W) frames, got {tuple(x.shape)}")
+        grads = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        if self.training:
+            if self.compute_dtype != "fp32":
+                raise NotImplementedError("training the ResNet-50 member runs in fp32: build it with "
+                                          "compute_dtype='fp32' (bf16 is its serving dtype)")
+            if x.dtype == torch.uint8:  # the serving feed's uint8 crops: normalise like the conv1 gather
+                from .backbone import NORMALIZATIONS
+
+                spec = self.input_normalization
+                mean, std = NORMALIZATIONS[spec] if isinstance(spec, str) else spec
+                x = (x.float() / 255.0 - torch.tensor(mean, device=x.device).view(1, 3, 1, 1)) / \
+                    torch.tensor(std, device=x.device).view(1, 3, 1, 1)
+            x = x.float()
+            params = self.train_parameters()
+            if grads:
+                return _RnTrainFn.apply(x, self, *params)
+            with torch.no_grad():
+                return _train_forward(self, x, save=False)[0]
+        if grads:
+            raise NotImplementedError("no eval-mode backward for the ResNet-50 member (eval BatchNorm is folded "
+                                      "into the inference kernels): train it in .train() mode or freeze it")
         if x.dtype not in (torch.float32, torch.uint8):
             x = x.float()
         dt = DTYPES[self.compute_dtype]
         with torch.no_grad():
             return _forward(self._fold(dt), x, dt, self.input_normalization)
+
+    def train_units(self):
+        """(conv, bn) pairs in forward order: stem, then per bottleneck conv1, conv2, conv3 (+ downsample)."""
+        units = [(self[0], self[1])]
+        for li in range(4):
+            for blk in self[4 + li]:
+                units += [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2), (blk.conv3, blk.bn3)]
+                if blk.downsample is not None:
+                    units.append((blk.downsample[0], blk.downsample[1]))
+        return units
+
+    def train_parameters(self):
+        out = []
+        for conv, bn in self.train_units():
+            out += [conv.weight, bn.weight, bn.bias]
+        return out
+
+
+# ------------------------------------------------------------------ training (fp32)
+class _Unit:
+    """One conv + train-mode BN of the trunk: the forward's saved tensors for the backward."""
+
+    __slots__ = ("conv", "bn", "x", "hw", "y", "ohw", "mean", "invstd", "scale", "shift")
+
+
+def _nhwc_strides(t, hw, c):
+    return (ctypes.c_int64 * 4)(hw[0] * hw[1] * c, hw[1] * c, c, 1)
+
+
+def _conv_bn_fwd(lib, st, u, x, xs, n, hw, save):
+    """y = conv(x) (no bias), the BN batch statistics (running buffers updated) -> unit with scale/shift."""
+    conv, bn = u.conv, u.bn
+    k, s, p, cin, cout = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.in_channels, conv.out_channels
+    ho, wo = (hw[0] + 2 * p - k) // s + 1, (hw[1] + 2 * p - k) // s + 1
+    dev = x.device
+    rows = lib.dfd_rn_conv_stat_rows(n, ho, wo)
+    stats = torch.empty(rows * 2 * cout, dtype=torch.float32, device=dev)
+    wpack = torch.empty(conv.weight.numel(), dtype=torch.float32, device=dev)
+    y = torch.empty(n * ho * wo, cout, dtype=torch.float32, device=dev)
+    w = conv.weight.detach().float().contiguous()
+    _lib.check(lib.dfd_rn_train_conv_fwd(st, x.data_ptr(), xs, n, hw[0], hw[1], cin, w.data_ptr(), cout, k, k, s, p,
+                                         wpack.data_ptr(), y.data_ptr(), stats.data_ptr()))
+    vecs = torch.empty(4, cout, dtype=torch.float32, device=dev)
+    with torch.no_grad():
+        bn.num_batches_tracked.add_(1)
+    _lib.check(lib.dfd_rn_bn_train_finalize(st, stats.data_ptr(), rows, n * ho * wo, cout, bn.weight.data_ptr(),
+                                            bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+                                            bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps),
+                                            vecs[0].data_ptr(), vecs[1].data_ptr(), vecs[2].data_ptr(),
+                                            vecs[3].data_ptr()))
+    if save:
+        u.x, u.hw, u.y, u.ohw = x, hw, y, (ho, wo)
+        u.mean, u.invstd, u.scale, u.shift = vecs[0], vecs[1], vecs[2], vecs[3]
+    return y, (ho, wo), vecs
+
+
+def _bn_act(lib, st, y, vecs, res, relu):
+    out = torch.empty_like(y)
+    _lib.check(lib.dfd_rn_bn_act(st, y.data_ptr(), vecs[2].data_ptr(), vecs[3].data_ptr(), _lib.ptr(res),
+                                 1 if relu else 0, y.shape[0], y.shape[1], out.data_ptr()))
+    return out
+
+
+def _train_forward(trunk, x, save):
+    """Train-mode forward of the trunk -> (features (N, 2048), saved state for the backward)."""
+    lib = _lib.load()
+    dev = x.device
+    st = _lib.stream_of(dev)
+    n, _, H, W = x.shape
+    units, blocks = [], []
+
+    def unit(conv, bn):
+        u = _Unit()
+        u.conv, u.bn = conv, bn
+        units.append(u)
+        return u
+
+    # conv1 7x7/2 reads the (N,3,H,W) frames through their strides; bn1 + relu + maxpool fused
+    us = unit(trunk[0], trunk[1])
+    xs = (ctypes.c_int64 * 4)(x.stride(0), x.stride(2), x.stride(3), x.stride(1))
+    y0, hw0, v0 = _conv_bn_fwd(lib, st, us, x, xs, n, (H, W), save)
+    hp, wp = (hw0[0] + 2 - 3) // 2 + 1, (hw0[1] + 2 - 3) // 2 + 1
+    h = torch.empty(n * hp * wp, 64, dtype=torch.float32, device=dev)
+    arg = torch.empty(n * hp * wp * 64, dtype=torch.uint8, device=dev)
+    _lib.check(lib.dfd_rn_pool_train_fwd(st, y0.data_ptr(), v0[2].data_ptr(), v0[3].data_ptr(), n, hw0[0], hw0[1], 64,
+                                         h.data_ptr(), arg.data_ptr()))
+    hw = (hp, wp)
+    for li in range(4):
+        for blk in trunk[4 + li]:
+            b = {"in": h, "hw": hw}
+            u1, u2, u3 = unit(blk.conv1, blk.bn1), unit(blk.conv2, blk.bn2), unit(blk.conv3, blk.bn3)
+            y1, hw1, v1 = _conv_bn_fwd(lib, st, u1, h, _nhwc_strides(h, hw, blk.conv1.in_channels), n, hw, save)
+            a1 = _bn_act(lib, st, y1, v1, None, True)
+            y2, hw2, v2 = _conv_bn_fwd(lib, st, u2, a1, _nhwc_strides(a1, hw1, blk.conv2.in_channels), n, hw1, save)
+            a2 = _bn_act(lib, st, y2, v2, None, True)
+            y3, _, v3 = _conv_bn_fwd(lib, st, u3, a2, _nhwc_strides(a2, hw2, blk.conv3.in_channels), n, hw2, save)
+            if blk.downsample is not None:
+                ud = unit(blk.downsample[0], blk.downsample[1])
+                yd, _, vd = _conv_bn_fwd(lib, st, ud, h, _nhwc_strides(h, hw, blk.conv1.in_channels), n, hw, save)
+                idn = _bn_act(lib, st, yd, vd, None, False)
+                b["ds"] = ud
+            else:
+                idn = h
+            h = _bn_act(lib, st, y3, v3, idn, True)
+            hw = hw2
+            b.update(u=(u1, u2, u3), a1=a1, a2=a2, out=h)
+            blocks.append(b)
+    feats = torch.empty(n, FEATURE_DIM, dtype=torch.float32, device=dev)
+    _lib.check(lib.dfd_rn_avgpool(st, 0, h.data_ptr(), n, hw[0] * hw[1], FEATURE_DIM, feats.data_ptr()))
+    saved = dict(units=units, blocks=blocks, stem_arg=arg, stem_pool_hw=(hp, wp), final_hw=hw, n=n) if save else None
+    return feats, saved
+
+
+def _bn_bwd(lib, st, u, g, grads):
+    """train-mode BN backward of unit u from its output gradient g -> dy; dgamma / dbeta into grads."""
+    C = u.y.shape[1]
+    dev = g.device
+    stats = torch.empty(2048 * 2 * C, dtype=torch.float32, device=dev)
+    coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+    dg, db = torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev)
+    dy = torch.empty_like(u.y)
+    _lib.check(lib.dfd_rn_bn_train_bwd(st, g.data_ptr(), u.y.data_ptr(), u.y.shape[0], C, u.mean.data_ptr(),
+                                       u.invstd.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
+                                       u.bn.weight.data_ptr(), dg.data_ptr(), db.data_ptr(), stats.data_ptr(),
+                                       coef.data_ptr(), dy.data_ptr()))
+    grads[id(u.bn.weight)] = dg
+    grads[id(u.bn.bias)] = db
+    return dy
+
+
+def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
+    """data gradient (if needed) and weight gradient of unit u's convolution from dy = dL/dy."""
+    conv = u.conv
+    k, s, p, cin, cout = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.in_channels, conv.out_channels
+    dev = dy.device
+    w = conv.weight.detach().float().contiguous()
+    nw = w.numel()
+    dx = None
+    if need_dx:
+        wp = torch.empty(2 * nw, dtype=torch.float32, device=dev)
+        dx = torch.empty(n * u.hw[0] * u.hw[1], cin, dtype=torch.float32, device=dev)
+        _lib.check(lib.dfd_rn_conv_dgrad(st, dy.data_ptr(), n, u.hw[0], u.hw[1], cin, w.data_ptr(), cout, k, k, s, p,
+                                         wp.data_ptr(), wp[nw:].data_ptr(), dx.data_ptr()))
+    slab = torch.empty(64 * nw, dtype=torch.float32, device=dev)
+    dw = torch.empty_like(w)
+    x = u.x
+    if x.dim() == 4:  # the stem reads the frames through their strides
+        xs = (ctypes.c_int64 * 4)(x.stride(0), x.stride(2), x.stride(3), x.stride(1))
+    else:
+        xs = _nhwc_strides(x, u.hw, cin)
+    _lib.check(lib.dfd_rn_conv_wgrad(st, x.data_ptr(), xs, n, u.hw[0], u.hw[1], cin, dy.data_ptr(), cout, k, k, s, p,
+                                     slab.data_ptr(), slab.numel(), dw.data_ptr()))
+    grads[id(conv.weight)] = dw
+    return dx
+
+
+def _train_backward(trunk, saved, dfeat):
+    lib = _lib.load()
+    dev = dfeat.device
+    st = _lib.stream_of(dev)
+    n = saved["n"]
+    grads = {}
+    blocks = saved["blocks"]
+    hw = saved["final_hw"]
+    # AdaptiveAvgPool2d + the last block's ReLU
+    last = blocks[-1]["out"]
+    g = torch.empty_like(last)
+    _lib.check(lib.dfd_rn_gap_bwd(st, dfeat.contiguous().data_ptr(), last.data_ptr(), n, hw[0] * hw[1], FEATURE_DIM,
+                                  g.data_ptr()))
+    masked = True
+    for b in reversed(blocks):
+        u1, u2, u3 = b["u"]
+        if not masked:  # the block's output ReLU
+            gm = torch.empty_like(g)
+            _lib.check(lib.dfd_rn_relu_bwd(st, g.data_ptr(), b["out"].data_ptr(), g.numel(), gm.data_ptr()))
+            g = gm
+        masked = False
+        dy3 = _bn_bwd(lib, st, u3, g, grads)
+        if "ds" in b:
+            dyd = _bn_bwd(lib, st, b["ds"], g, grads)
+            dx = _conv_bwd(lib, st, b["ds"], dyd, n, grads)
+        else:
+            dx = g.clone()
+        da2 = _conv_bwd(lib, st, u3, dy3, n, grads)
+        g2 = torch.empty_like(da2)
+        _lib.check(lib.dfd_rn_relu_bwd(st, da2.data_ptr(), b["a2"].data_ptr(), da2.numel(), g2.data_ptr()))
+        dy2 = _bn_bwd(lib, st, u2, g2, grads)
+        da1 = _conv_bwd(lib, st, u2, dy2, n, grads)
+        g1 = torch.empty_like(da1)
+        _lib.check(lib.dfd_rn_relu_bwd(st, da1.data_ptr(), b["a1"].data_ptr(), da1.numel(), g1.data_ptr()))
+        dy1 = _bn_bwd(lib, st, u1, g1, grads)
+        dx.add_(_conv_bwd(lib, st, u1, dy1, n, grads))
+        g = dx
+    # maxpool + stem relu/bn + conv1 weight gradient (no gradient to the frames)
+    us = saved["units"][0]
+    gs = torch.empty_like(us.y)
+    _lib.check(lib.dfd_rn_pool_train_bwd(st, g.data_ptr(), saved["stem_arg"].data_ptr(), us.y.data_ptr(),
+                                         us.scale.data_ptr(), us.shift.data_ptr(), n, us.ohw[0], us.ohw[1], 64,
+                                         gs.data_ptr()))
+    dy0 = _bn_bwd(lib, st, us, gs, grads)
+    _conv_bwd(lib, st, us, dy0, n, grads, need_dx=False)
+    return grads
+
+
+class _RnTrainFn(torch.autograd.Function):
+    """The whole train-mode trunk as one autograd node: forward saves every unit's input, pre-BN
+    output and batch statistics; backward returns the conv / BN parameter gradients (the frames get
+    none: they are data)."""
+
+    @staticmethod
+    def forward(ctx, x, trunk, *params):
+        feats, saved = _train_forward(trunk, x, save=True)
+        ctx.trunk, ctx.saved, ctx.nparams = trunk, saved, len(params)
+        return feats
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        grads = _train_backward(ctx.trunk, ctx.saved, dfeat.float())
+        ctx.saved = None
+        params = ctx.trunk.train_parameters()
+        return (None, None) + tuple(grads.get(id(p)) for p in params)
 
 
 def _norm6(spec) -> ctypes.Array:

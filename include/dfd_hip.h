@@ -181,6 +181,49 @@ DFD_API int dfd_rn_maxpool(void* stream, int dtype, const void* x, int N, int H,
 /* global average pooling (N, HW, C) -> (N, C) fp32 */
 DFD_API int dfd_rn_avgpool(void* stream, int dtype, const void* x, int N, int HW, int C, float* out);
 
+/* ---- ResNet-50 ensemble member, TRAINING, fp32 (EnsembleTrainer.train_epoch trains every member:
+ * src/ensemble_trainer.py:158-229; torchvision train-mode BatchNorm2d semantics).  NHWC fp32; the
+ * convolutions are exact-fp32 implicit-GEMM MFMA kernels (no im2col buffer, no library GEMM). ---- */
+/* BN-stat partial rows a training conv forward writes: stats needs rows * 2 * Cout floats */
+DFD_API int64_t dfd_rn_conv_stat_rows(int N, int Ho, int Wo);
+/* y (N,Ho,Wo,Cout) = conv(x, w) without bias, and the BN-stat partials of y's channels; x read
+ * through element strides xs4 = (n, y, x, c); w OIHW [Cout][Cin][kh][kw]; wpack >= Cout*Cin*kh*kw */
+DFD_API int dfd_rn_train_conv_fwd(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin,
+                                  const float* w, int Cout, int kh, int kw, int stride, int pad, float* wpack,
+                                  float* y, float* stats);
+/* batch mean / invstd / scale / shift of a train-mode BN from the partials; updates running_mean /
+ * running_var with momentum (unbiased variance), like torch */
+DFD_API int dfd_rn_bn_train_finalize(void* stream, const float* stats, int rows, int64_t count, int C,
+                                     const float* gamma, const float* beta, float* running_mean,
+                                     float* running_var, float momentum, float eps, float* mean, float* invstd,
+                                     float* scale, float* shift);
+/* out = relu?(y * scale + shift (+ res)), (M, C), C % 4 == 0 */
+DFD_API int dfd_rn_bn_act(void* stream, const float* y, const float* scale, const float* shift, const float* res,
+                          int relu, int64_t M, int C, float* out);
+/* stem: out = maxpool3x3/2(relu(y * scale + shift)) with the argmax tap kept; and its backward to
+ * the BN output gradient g (relu' included) */
+DFD_API int dfd_rn_pool_train_fwd(void* stream, const float* y, const float* scale, const float* shift, int N, int H,
+                                  int W, int C, float* out, uint8_t* argmax);
+DFD_API int dfd_rn_pool_train_bwd(void* stream, const float* dout, const uint8_t* argmax, const float* y,
+                                  const float* scale, const float* shift, int N, int H, int W, int C, float* g);
+/* g = out > 0 ? dout : 0 (n % 4 == 0);  global-average-pool backward through the last ReLU:
+ * g[n][p][c] = out > 0 ? dfeat[n][c] / HW : 0 */
+DFD_API int dfd_rn_relu_bwd(void* stream, const float* dout, const float* out, int64_t n, float* g);
+DFD_API int dfd_rn_gap_bwd(void* stream, const float* dfeat, const float* out, int N, int HW, int C, float* g);
+/* train-mode BN backward from its output gradient g: dgamma, dbeta (written) and dy;
+ * stats >= 2048*2*C floats, coef >= 3*C floats (scratch) */
+DFD_API int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, int64_t M, int C, const float* mean,
+                                const float* invstd, const float* scale, const float* shift, const float* gamma,
+                                float* dgamma, float* dbeta, float* stats, float* coef, float* dy);
+/* dx (N,H,W,Cin) = conv data gradient of dy (N,Ho,Wo,Cout), stride 1 or 2; wpack, wpack_t scratch of
+ * Cout*Cin*kh*kw floats each */
+DFD_API int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout,
+                              int kh, int kw, int stride, int pad, float* wpack, float* wpack_t, float* dx);
+/* dw OIHW (written) = weight gradient from x (strides xs4) and dy; slab: scratch of slab_floats */
+DFD_API int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin,
+                              const float* dy, int Cout, int kh, int kw, int stride, int pad, float* slab,
+                              int64_t slab_floats, float* dw);
+
 /* ---- optimizer ----------------------------------------------------------------------------
  * Replaces torch.nn.utils.clip_grad_norm_(params, max_norm) (src/ensemble_trainer.py:199) and
  * optim.AdamW / optim.Adam .step() (src/ensemble_trainer.py:146,200; src/train.py:323,126)

@@ -6,7 +6,7 @@ CPU: torchvision's key names / shapes / parameter count through the oracle resta
 (oracle/resnet_cpu.py; parity against torchvision itself is unpinned: not importable here), and
 the detector's state_dict layout.  GPU: eval features and logits against the fp32 oracle (rtol 1e-3,
 atol 1e-5 in fp32 mode; a bf16 bound), the uint8 frame feed bit-identical to the normalised fp32
-feed, the ensemble against the oracle ensemble, and the refusal of training mode."""
+feed, the ensemble against the oracle ensemble (training: tests/test_resnet_train_gpu.py)."""
 import numpy as np
 import pytest
 import torch
@@ -98,7 +98,7 @@ def test_features_bf16_bound_and_uint8_feed():
 
 
 @pytest.mark.gpu
-def test_ensemble_matches_oracle_and_refuses_training():
+def test_ensemble_matches_oracle():
     torch.manual_seed(0)
     ens = EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False)
     _randomize_bn_(ens.models[1].backbone, 3)
@@ -123,9 +123,6 @@ def test_ensemble_matches_oracle_and_refuses_training():
         z = torch.relu(g @ cpu["fc1.weight"].T + cpu["fc1.bias"]) @ cpu["fc2.weight"].T + cpu["fc2.bias"]
     torch.testing.assert_close(per[1][0].cpu(), z, rtol=1e-3, atol=1e-5)
     torch.testing.assert_close(per[1][1].cpu(), a, rtol=1e-3, atol=1e-5)
-    ens.train()
-    with pytest.raises(NotImplementedError):
-        ens(x.cuda())
 
 
 # every distinct convolution of the ResNet-50 trunk at 224x224 (torchvision v1.5 Bottleneck):

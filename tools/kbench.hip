@@ -292,7 +292,8 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&part, 5ll * F * 1152 * 4 * 4));
     const int64_t pcap = 5ll * F * 1152 * 4;
     struct PwlS { int hw, N, K; } pws[3] = {{112, 16, 32}, {56, 24, 96}, {56, 24, 144}};
-    struct FoldS { int hw, cin, mid, skip; } fds[3] = {{112, 16, 96, 0}, {56, 24, 144, 1}, {56, 24, 144, 0}};
+    struct FoldS { int hw, cin, mid, skip; } fds[5] = {{112, 16, 96, 0}, {56, 24, 144, 1}, {56, 24, 144, 0},
+                                                      {28, 40, 240, 1}, {28, 40, 240, 0}};
     {
       const int rows = 64;
       for (auto& q : pws) {
@@ -300,8 +301,14 @@ int main(int argc, char** argv) {
         int hs = 1;
         snprintf(nm, sizeof nm, "r%d %dx%d %d>%d", rows, q.hw, q.hw, q.K, q.N);
         b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + M * q.N), [&] {
-          const int rc = launch_pwl_bwd(b.s, A, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw, q.N, q.K, D, slab,
-                                        slab_cap, dW, false, part, pcap, &hs);
+          const int rc = launch_pwl_bwd(b.s, A, nullptr, nullptr, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw,
+                                        q.N, q.K, D, slab, slab_cap, dW, false, part, pcap, &hs);
+          return rc == 1 ? -1 : rc;
+        });
+        snprintf(nm, sizeof nm, "bn3 %dx%d %d>%d", q.hw, q.hw, q.K, q.N);
+        b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + 2 * M * q.N), [&] {  // + the BN3 backward apply in staging
+          const int rc = launch_pwl_bwd(b.s, A, A + (int64_t)M * 32, coef, B, C, sc, sh, mean, invstd, gate, F,
+                                        q.hw * q.hw, q.N, q.K, D, slab, slab_cap, dW, false, part, pcap, &hs);
           return rc == 1 ? -1 : rc;
         });
       }
