@@ -17,6 +17,9 @@ bounded sample (the reference itself does not travel to the GPU box).
   bf16 on 128 images (16 graphs x 8 nodes); unit: images/s, plus the MFMA fraction.
 * ``EnsembleDetector(['efficientnet_b0', 'resnet50'])`` serving forward (eval, bf16) on 32 clips x 8
   uint8 crops; unit: frames/s (SURVEY §8(f)1,4).
+* the same ensemble TRAINED (``--model ensemble_train``; ``EnsembleTrainer.train_epoch``'s step,
+  src/ensemble_trainer.py:182-200: forward, weighted CE, backward, clip 1.0 + AdamW over both
+  members) on 8 clips x 8 frames, fp32 (the ResNet-50 member trains in fp32); unit: frames/s.
 
     python bench_temporal.py [--model cnnlstm|rnn|vit|both|all] [--clips 64] [--image 224] [--steps K] [--warmup W]
 """
@@ -237,9 +240,33 @@ def bench_ensemble(args, dev):
             "b0_only": {"value": round(B * T / res["b0"], 2), "ms_per_step": round(res["b0"] * 1e3, 3)}}
 
 
+def bench_ensemble_train(args, dev):
+    """SURVEY §8(f)4 training: the default ensemble's train step (both members, fp32)."""
+    from deepfake_amd.pretrained_detector import EnsembleDetector
+    from deepfake_amd.trainer import TrainStep
+
+    B, T, S = args.clips, 8, 224
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    x = torch.rand(B, T, 3, S, S, generator=g, device=dev)
+    y = torch.randint(0, 2, (B,), generator=g, device=dev)
+    ens = EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False, compute_dtype="fp32").to(dev).train()
+    ts = TrainStep(ens, lr=1e-4, weight_decay=1e-5, class_weights=torch.tensor([0.7, 1.3]), max_grad_norm=1.0)
+
+    def step():
+        ts(x, y)
+
+    dt = _time(step, args.steps, args.warmup)
+    return {"metric": "frames/sec training EnsembleDetector(efficientnet_b0 + resnet50)", "value": round(B * T / dt, 2),
+            "unit": "frames/s", "n_gpus": 1, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
+            "dtype": "f32", "data": "synthetic U(0,1) frames (seeded, on device), random-init weights",
+            "config": {"workload": "EnsembleDetector train step (both members; weighted CE, clip 1.0 + AdamW)",
+                       "clips": B, "frames_per_clip": T, "image": [S, S, 3]}}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "vit", "ensemble", "both", "all"])
+    ap.add_argument("--model", default="both", choices=["cnnlstm", "rnn", "vit", "ensemble", "ensemble_train", "both", "all"])
     ap.add_argument("--graphs", type=int, default=16)
     ap.add_argument("--nodes", type=int, default=8)
     ap.add_argument("--clips", type=int, default=64)
@@ -260,6 +287,9 @@ def main():
     if args.model in ("ensemble", "all"):
         args.clips = min(args.clips, 32)
         print(json.dumps(bench_ensemble(args, dev)), flush=True)
+    if args.model in ("ensemble_train", "all"):
+        args.clips = min(args.clips, 8)
+        print(json.dumps(bench_ensemble_train(args, dev)), flush=True)
 
 
 if __name__ == "__main__":

@@ -47,7 +47,7 @@ struct PwFoldArgs {
 
 template <int MB, int CB, int R>
 struct PfTile {
-  static_assert(R == 32 || R == 64 || R == 128, "row steps of 32, 64 or 128");
+  static_assert(R == 64 || R == 128, "row steps of 64 or 128");
   static constexpr int MP = 32 * MB;                   // mid padded to the contraction
   static constexpr int CP = CB * 16 + 1 <= 32 ? 32 : 64;  // cin + the ones column, padded
   static constexpr int CX = CP / 32;
@@ -178,22 +178,6 @@ __global__ __launch_bounds__(256) void pw_fold_bwd_kernel(PwFoldArgs a) {
       }
       *reinterpret_cast<uint2*>(Rt + m * TL::RS + c) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
     };
-    if constexpr (R == 32) {
-      // 2 row blocks x CB channel blocks dealt to the 4 waves, one accumulator per unit
-      for (int u = wave; u < 2 * CB; u += 4) {
-        const int mb = u & 1, cb = u >> 1, m = mb * 16 + (lane & 15);
-        f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ch = 0; ch < TL::NC; ++ch) {
-          const bf16x8_t bf = ch < MB ? *reinterpret_cast<const bf16x8_t*>(Gs + m * TL::GS + ch * 32 + 8 * (lane >> 4))
-                                      : *reinterpret_cast<const bf16x8_t*>(Xs + m * TL::XS + (ch - MB) * 32 +
-                                                                            8 * (lane >> 4));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, Wf[(cb * TL::NC + ch) * 64 + lane]),
-                                                        bf, acc, 0, 0, 0);
-        }
-        dgrad_epi(acc, m, cb);
-      }
-    }
 #pragma unroll
     for (int mj = 0; mj < R / 64; ++mj) {
       f32x4_t ad[CB];
@@ -318,17 +302,17 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
                        float* G, float* cs) {
   // measured (rocprof, 256 frames, against the five unfused launches): blocks.1.0 430 -> 179 us,
   // blocks.1.1 / 2.0 194 / 183 -> 112 us
-  if (M <= 0 || (mid & 7) || (cin & 7) || mid > 256 || cin > 48 || M * std::max(mid, cin) >= (1ll << 31)) return 1;
+  if (M <= 0 || (mid & 7) || (cin & 7) || mid > 160 || cin > 48 || M * std::max(mid, cin) >= (1ll << 31)) return 1;
   PwFoldArgs a{g, x, r, w1t, q, bv, dx, nullptr, nullptr, nullptr, M, 0, mid, cin};
   const int mb = cdiv(mid, 32), cb = cdiv(cin, 16);
   // 64-row steps (128: 1.1-1.8x slower, one wave per SIMD on the 144-wide shapes; tools/kbench fused);
-  // the 240-wide shapes in 32-row steps (64-row steps: 319 registers, one wave per SIMD, 125 -> 199 us
-  // on blocks.2.1 against the unfused launches)
+  // the 240-wide shapes (blocks.2.1, 3.0: 40 -> 240) stay on the unfused launches: in 64-row steps
+  // 319 registers, one wave per SIMD, 125 -> 199 us on blocks.2.1; in 32-row steps (one accumulator
+  // per 16x16 unit) 125 -> 220 us with the skip, 119 -> 133 us without (tools/kbench fused)
 #define DFD_PF(MB_, CB_, R_) \
   if (mb == MB_ && cb == CB_) return pf_launch<MB_, CB_, R_>(s, a, slab, slab_cap, T, G, cs)
   DFD_PF(3, 1, 64);  // blocks.1.0: 16 -> 96
   DFD_PF(5, 2, 64);  // blocks.1.1, 2.0: 24 -> 144
-  DFD_PF(8, 3, 32);  // blocks.2.1, 3.0: 40 -> 240
 #undef DFD_PF
   return 1;
 }
