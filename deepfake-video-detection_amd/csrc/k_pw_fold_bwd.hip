@@ -63,8 +63,12 @@ struct PfTile {
   static constexpr int SMEM = W_BYTES + R * (GS + XS + RS) * 2 + CB * 16 * 4;
 };
 
+// waves per SIMD the register allocation must allow (A/B builds: -DPF_WPE=n)
+#ifndef PF_WPE
+#define PF_WPE 3  // 144-wide: 2 -> 3 waves, 141 -> 135 us without the skip (tools/kbench fused)
+#endif
 template <int MB, int CB, bool RES, int R>
-__global__ __launch_bounds__(256) void pw_fold_bwd_kernel(PwFoldArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) void pw_fold_bwd_kernel(PwFoldArgs a) {
   using TL = PfTile<MB, CB, R>;
   __shared__ __attribute__((aligned(16))) char smem[TL::SMEM];
   const uint4* Wf = reinterpret_cast<const uint4*>(smem);  // [CB][NC][64] fragments of [W1t | Q]

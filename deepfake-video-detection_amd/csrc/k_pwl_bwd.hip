@@ -70,7 +70,7 @@ struct PbTile {
   static constexpr int W_BYTES = KBC * NG * 1024;
   static constexpr int G_BYTES = PB_R * GS * 2;
   static constexpr int T_BYTES = PB_R * XS * 2;
-  static constexpr int SMEM = W_BYTES + G_BYTES + (WG ? 3 : 2) * T_BYTES + 4 * KC * 4 + 3 * NP * 4;
+  static constexpr int SMEM = W_BYTES + G_BYTES + (WG ? 3 : 2) * T_BYTES + 5 * KC * 4 + 3 * NP * 4;
   static_assert(KBC >= 1 && KBC <= 4, "one k-block per wave");
 };
 
@@ -83,8 +83,12 @@ __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
 
 // WG = false: the data gradient and the SE/BN sums only (no act tile, no weight-gradient
 // accumulators, any number of parts); the caller runs the weight gradient separately
+// waves per SIMD the register allocation must allow (A/B builds: -DPWL_WPE=n)
+#ifndef PWL_WPE
+#define PWL_WPE 1  // 3 spills (84-176 B/lane): 1.3-2.1x slower in tools/kbench fused
+#endif
 template <int NG, int KBC, bool WG, int PB_R>
-__global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) void pwl_bwd_kernel(PwlBwdArgs a) {
   using TL = PbTile<NG, KBC, WG, PB_R>;
   __shared__ __attribute__((aligned(16))) char smem[TL::SMEM];
   const uint4* Ws = reinterpret_cast<const uint4*>(smem);  // [KBC][NG][64] W^T fragments
@@ -94,6 +98,7 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
   bf16* Cs = Ys + PB_R * TL::XS;                            // [R][XS] ge2
   float* co = reinterpret_cast<float*>(Cs + PB_R * TL::XS);  // [4][KC] sc sh mean invstd
   float* c3 = co + 4 * TL::KC;                                // [3][NP] BN3 k1 k2 k3 (coef3)
+  float* gl = c3 + 3 * TL::NP;                                // [KC] SE gate of a one-frame part
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // the k-chunks of one part (same gs rows) are dealt to one XCD: gs is fetched once per L2
@@ -141,6 +146,10 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
     pc0 = 0;
     pc1 = HW;
   }
+  // a part of one frame (every dispatched shape: HW >= 2048 splits frames) reads its gate from LDS
+  const bool gate_lds = nf == 1;
+  if (gate_lds)
+    for (int i = tid; i < TL::KC; i += 256) gl[i] = k0 + i < K ? a.gate[(int64_t)fA * K + k0 + i] : 0.f;
   const int spf = (pc1 - pc0 + PB_R - 1) / PB_R;
   const int nsteps = nf > 0 && pc1 > pc0 ? nf * spf : 0;
 
@@ -228,7 +237,8 @@ __global__ __launch_bounds__(256) void pwl_bwd_kernel(PwlBwdArgs a) {
         raw_to_f(ry[S][i], x);
         ld8(co + cv, sc);
         ld8(co + TL::KC + cv, sh);
-        ld8f(a.gate + (int64_t)f * K + (k0 + cv < K ? k0 + cv : 0), gv);
+        if (gate_lds) ld8(gl + cv, gv);
+        else ld8f(a.gate + (int64_t)f * K + (k0 + cv < K ? k0 + cv : 0), gv);
         const uint32_t msk = ry[S][i].ok ? 0xffffffffu : 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * gv[j];
