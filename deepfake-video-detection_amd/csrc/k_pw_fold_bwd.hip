@@ -282,8 +282,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
 template <int MB, int CB, int R>
 static int pf_launch(hipStream_t s, PwFoldArgs& a, float* slab, int64_t slab_cap, float* T, float* G, float* cs) {
   const int64_t per = (int64_t)a.mid * a.cin + (int64_t)a.cin * a.cin + a.cin;
-  // ~1024 parts of whole 64-row steps, as many as the slab holds
-  int64_t parts = std::min<int64_t>(1024, std::max<int64_t>(1, slab_cap / per));
+  // one dispatch wave: as many parts as workgroups are co-resident (no partial second round), at
+  // most what the slab holds
+  static const int resident = [] {
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pw_fold_bwd_kernel<MB, CB, true, R>, 256, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    return std::max(1, cus * per_cu);
+  }();
+  int64_t parts = std::min<int64_t>(resident, std::max<int64_t>(1, slab_cap / per));
   parts = std::min<int64_t>(parts, cdiv64(a.M, R));
   a.rows_per_part = cdiv64(cdiv64(a.M, parts), R) * R;
   parts = cdiv64(a.M, a.rows_per_part);
