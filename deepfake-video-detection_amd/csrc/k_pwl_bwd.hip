@@ -84,6 +84,9 @@ __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
 // WG = false: the data gradient and the SE/BN sums only (no act tile, no weight-gradient
 // accumulators, any number of parts); the caller runs the weight gradient separately
 // waves per SIMD the register allocation must allow (A/B builds: -DPWL_WPE=n)
+#ifndef PWL_RING
+#define PWL_RING 2
+#endif
 #ifndef PWL_WPE
 #define PWL_WPE 1  // 3 spills (84-176 B/lane): 1.3-2.1x slower in tools/kbench fused
 #endif
@@ -153,8 +156,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
   const int spf = (pc1 - pc0 + PB_R - 1) / PB_R;
   const int nsteps = nf > 0 && pc1 > pc0 ? nf * spf : 0;
 
-  // two register sets: the rows of step st + 2 are loaded while step st is staged and computed
-  Raw8<bf16> rg[2][TL::NLG], r3[2][TL::NLG], ry[2][TL::NLK];
+  // NS register sets: the rows of step st + NS are loaded while step st is staged and computed
+  constexpr int NS = PWL_RING;
+  Raw8<bf16> rg[NS][TL::NLG], r3[NS][TL::NLG], ry[NS][TL::NLK];
   const bool bn3 = a.coef3 != nullptr;
   auto load = [&](auto setc, int st) {
     constexpr int S = decltype(setc)::value;
@@ -188,7 +192,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
     for (int r = 0; r < 4; ++r) se[q][r] = 0.f;
 
   if (nsteps > 0) load(std::integral_constant<int, 0>{}, 0);
-  if (nsteps > 1) load(std::integral_constant<int, 1>{}, 1);
+  if constexpr (NS == 2)
+    if (nsteps > 1) load(std::integral_constant<int, NS - 1>{}, 1);
   __syncthreads();  // fragments and coefficients staged
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
       }
     }
     lds_barrier();
-    if (st + 2 < nsteps) load(setc, st + 2);  // rows two steps ahead in flight during this step's math
+    if (st + NS < nsteps) load(setc, st + NS);  // rows NS steps ahead in flight during this step's math
 
     if (cw) {
       // ---- data gradient: D[k][m] = W^T[k][:] . gs[m][:]^T, 4 row blocks ----
@@ -349,9 +354,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
             *reinterpret_cast<const uint4*>(Cs + rr * TL::XS + cv);
     }
   };
-  for (int st = 0; st < nsteps; st += 2) {
+  for (int st = 0; st < nsteps; st += NS) {
     step(std::integral_constant<int, 0>{}, st);
-    if (st + 1 < nsteps) step(std::integral_constant<int, 1>{}, st + 1);
+    if constexpr (NS == 2)
+      if (st + 1 < nsteps) step(std::integral_constant<int, NS - 1>{}, st + 1);
   }
 
   // ---- this part's weight-gradient rows: dW[n][k] of the wave's k-block ----
