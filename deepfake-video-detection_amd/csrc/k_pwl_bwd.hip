@@ -85,10 +85,10 @@ __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
 // accumulators, any number of parts); the caller runs the weight gradient separately
 // waves per SIMD the register allocation must allow (A/B builds: -DPWL_WPE=n)
 #ifndef PWL_RING
-#define PWL_RING 2
+#define PWL_RING 1  // 2 sets: neutral at 2 waves per SIMD, and 3 waves do not fit with it
 #endif
 #ifndef PWL_WPE
-#define PWL_WPE 1  // 3 spills (84-176 B/lane): 1.3-2.1x slower in tools/kbench fused
+#define PWL_WPE 3  // with one prefetch set: 2 -> 3 waves, -13..-16 % (tools/kbench fused)
 #endif
 template <int NG, int KBC, bool WG, int PB_R>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) void pwl_bwd_kernel(PwlBwdArgs a) {
@@ -383,11 +383,26 @@ static int pb_launch(hipStream_t s, PwlBwdArgs& a, int64_t slab_cap, float* dW, 
   const int64_t per = WG ? (int64_t)a.N * a.K : 0;  // slab floats per part
   int64_t parts;
   if (a.HW >= 2048) {
-    // large maps: chunks of a frame (>= 8 steps each) until ~1024 workgroups
+    // large maps: chunks of a frame (>= 8 steps each); the chunk count minimising dispatch rounds x
+    // steps per workgroup (rounds of the co-resident grid): blocks.0.0 (nkc 1) in 3 chunks = one
+    // round of 66 steps instead of 4 chunks = 1.3 rounds of 49
+    static const int resident = [] {
+      int dev = 0, cus = 256, per_cu = 1;
+      if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pwl_bwd_kernel<NG, KBC, WG, PB_R>, 256, 0) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      return std::max(1, cus * per_cu);
+    }();
     a.hsplit = 1;
-    while ((int64_t)a.F * a.hsplit * a.nkc < 1024 && a.HW / (a.hsplit * 2) >= 8 * PB_R &&
-           (int64_t)a.F * a.hsplit * 2 * per <= slab_cap && 5 * (int64_t)(a.hsplit * 2) * a.F * a.K <= part_cap)
-      a.hsplit *= 2;
+    int64_t best = -1;
+    for (int hs = 1; a.HW / hs >= 8 * PB_R; ++hs) {
+      if ((int64_t)a.F * hs * per > slab_cap || 5 * (int64_t)hs * a.F * a.K > part_cap) break;
+      if (cdiv(a.HW, hs) * (hs - 1) >= a.HW) continue;  // every chunk non-empty (each writes its sums)
+      const int64_t wgs = (int64_t)a.F * hs * a.nkc;
+      const int64_t cost = cdiv64(wgs, resident) * cdiv(cdiv(a.HW, hs), PB_R);
+      if (best < 0 || cost < best) { best = cost; a.hsplit = hs; }
+    }
     a.fpp = 1;
     parts = (int64_t)a.F * a.hsplit;
   } else {
