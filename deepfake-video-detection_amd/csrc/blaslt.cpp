@@ -1,7 +1,6 @@
 // Plain library GEMMs through hipBLASLt (bf16 in, fp32 accumulate) for the large, compute-bound
 // transformer GEMMs of the ViT-B/16 branch (src/models.py:88-107, 280-291 -> timm
-// vit_base_patch16_224) and the dense convolutions of the ResNet-50 ensemble member
-// (src/pretrained_detector.py:37-40): there the fused prologues of k_gemm.hip buy nothing and
+// vit_base_patch16_224; the ResNet-50 member runs on k_rnconv.hip): there the fused prologues of k_gemm.hip buy nothing and
 // hipBLASLt's MFMA kernels run 2-5x faster (tools/torch_gemm_vit.py).  The EfficientNet-B0 hot
 // path keeps its own kernels (BN/SiLU prologues, BN-stat epilogues, skinny shapes where the library
 // is slower: tools/torch_gemm_ref.py).
@@ -10,8 +9,9 @@
 //   C[M][N] = A[M][K] . B[N][K]^T (+ bias[N]) (+ R[M][N])  ==  C^T = B^T' . A'  (m = N, n = M)
 //   dW[N][K] (+)= dY[M][N]^T . X[M][K]                     ==  dW^T = X' . dY'^T (m = K, n = N)
 // Algorithms come from the library heuristic (no split-K with atomics requested; deterministic).
-// One handle per device and one workspace per stream, created on first use under a lock; the
-// descriptor/algorithm cache is keyed by shape and guarded by the same lock.
+// One handle per device and one workspace per stream (at most kMaxWs per device, least recently
+// used evicted), created on first use under a lock; the descriptor/algorithm cache is keyed by shape
+// and guarded by the same lock.
 #include <hipblaslt/hipblaslt.h>
 
 #include <map>
@@ -37,7 +37,13 @@ using Key = std::tuple<int, int, int64_t, int64_t, int64_t, int, int, int, int>;
 
 std::mutex g_mu;
 std::map<int, hipblasLtHandle_t> g_handles;
-std::map<std::pair<int, hipStream_t>, void*> g_ws;
+struct Ws {
+  void* p;
+  uint64_t tick;  // last use (LRU)
+};
+std::map<std::pair<int, hipStream_t>, Ws> g_ws;
+uint64_t g_tick = 0;
+constexpr int kMaxWs = 8;  // workspaces per device; past it the least recently used one is freed
 std::map<Key, Entry> g_cache;
 
 #define LT_CHECK(x)                                                                         \
@@ -61,11 +67,27 @@ int handle_and_ws(hipStream_t s, int dev, hipblasLtHandle_t* h, void** ws) {
   auto wk = std::make_pair(dev, s);
   auto wi = g_ws.find(wk);
   if (wi == g_ws.end()) {
+    // bounded: serving from many threads, each on its own stream, must not grow HBM use per stream
+    // ever seen.  The evicted workspace may still be read by its stream's queued GEMMs (or that
+    // stream may be gone): a device synchronisation orders the free after all of them (rare).
+    int held = 0;
+    auto lru = g_ws.end();
+    for (auto e = g_ws.begin(); e != g_ws.end(); ++e)
+      if (e->first.first == dev) {
+        ++held;
+        if (lru == g_ws.end() || e->second.tick < lru->second.tick) lru = e;
+      }
+    if (held >= kMaxWs && lru != g_ws.end()) {
+      DFD_HIP_CHECK(hipDeviceSynchronize());
+      DFD_HIP_CHECK(hipFree(lru->second.p));
+      g_ws.erase(lru);
+    }
     void* p = nullptr;
     DFD_HIP_CHECK(hipMalloc(&p, kWorkspace));
-    wi = g_ws.emplace(wk, p).first;
+    wi = g_ws.emplace(wk, Ws{p, 0}).first;
   }
-  *ws = wi->second;
+  wi->second.tick = ++g_tick;
+  *ws = wi->second.p;
   return 0;
 }
 

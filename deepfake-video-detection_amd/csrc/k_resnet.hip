@@ -1,8 +1,9 @@
 // ResNet-50 member of EnsembleDetector (src/pretrained_detector.py:37-40: torchvision resnet50
 // minus fc, the app's default ensemble ENSEMBLE_BACKBONES, app.py:661,1597), inference path.
-// Layout NHWC.  Every convolution is a GEMM through hipBLASLt (blaslt.cpp) with the eval-mode
-// BatchNorm folded into its weights and bias, the ReLU and the bottleneck's identity add in the
-// library epilogue; what is not a plain GEMM lives here:
+// Layout NHWC.  Every convolution is the implicit-GEMM MFMA kernel of k_rnconv.hip (dfd_rn_conv;
+// conv1 on its im2col rows through dfd_rn_gemm, the same kernel as a 1x1 GEMM) with the eval-mode
+// BatchNorm folded into its weights and bias, the ReLU and the bottleneck's identity add in its
+// epilogue; no library GEMM.  What is not a convolution lives here:
 //   im2col      NHWC T -> [N*Ho*Wo][Kp] T, column (ky*kw + kx)*C + c, zero padding (k > 1 or stride 2)
 //   stem im2col the (N,3,H,W) frames (any strides; fp32, or uint8 normalised like the B0 stem) for
 //               conv1 7x7/2 -> [N*112*112][152] (147 taps zero padded to 16-B rows)
