@@ -461,28 +461,34 @@ int dfd_rn_bn_train_finalize(void* stream, const float* stats, int rows, int64_t
   DFD_GUARD_END
 }
 
-int dfd_rn_bn_act(void* stream, const float* y, const float* scale, const float* shift, const float* res, int relu,
-                  int64_t M, int C, float* out) {
+int dfd_rn_bn_act(void* stream, const float* y, const float* mean, const float* scale, const float* beta,
+                  const float* res, int relu, int64_t M, int C, float* out) {
   DFD_GUARD_BEGIN
-  if (!y || !scale || !shift || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
-  return dfd::rn_bn_act((hipStream_t)stream, y, scale, shift, res, relu, M, C, out);
+  if (!y || !mean || !scale || !beta || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn_bn_act((hipStream_t)stream, y, mean, scale, beta, res, relu, M, C, out);
   DFD_GUARD_END
 }
 
-int dfd_rn_pool_train_fwd(void* stream, const float* y, const float* scale, const float* shift, int N, int H, int W,
-                          int C, float* out, uint8_t* argmax) {
+int dfd_rn_pool_train_fwd(void* stream, const float* y, const float* mean, const float* scale, const float* beta,
+                          int N, int H, int W, int C, float* out, uint8_t* argmax) {
   DFD_GUARD_BEGIN
-  if (!y || !scale || !shift || !out || !argmax) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
-  return dfd::bn_relu_pool_fwd((hipStream_t)stream, y, scale, shift, N, H, W, C, (H + 2 - 3) / 2 + 1,
+  if (!y || !mean || !scale || !beta || !out || !argmax) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::bn_relu_pool_fwd((hipStream_t)stream, y, mean, scale, beta, N, H, W, C, (H + 2 - 3) / 2 + 1,
                                (W + 2 - 3) / 2 + 1, out, argmax);
   DFD_GUARD_END
 }
 
-int dfd_rn_pool_train_bwd(void* stream, const float* dout, const uint8_t* argmax, const float* y, const float* scale,
-                          const float* shift, int N, int H, int W, int C, float* g) {
+int dfd_rn_pool_train_bwd(void* stream, const float* dout, const uint8_t* argmax, const float* y, const float* mean,
+                          const float* scale, const float* beta, int N, int H, int W, int C, float* g) {
   DFD_GUARD_BEGIN
-  if (!dout || !argmax || !y || !scale || !shift || !g) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
-  return dfd::bn_relu_pool_bwd((hipStream_t)stream, dout, argmax, y, scale, shift, N, H, W, C, (H + 2 - 3) / 2 + 1,
+  if (!dout || !argmax || !y || !mean || !scale || !beta || !g) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::bn_relu_pool_bwd((hipStream_t)stream, dout, argmax, y, mean, scale, beta, N, H, W, C, (H + 2 - 3) / 2 + 1,
                                (W + 2 - 3) / 2 + 1, g);
   DFD_GUARD_END
 }
@@ -521,6 +527,10 @@ int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Ci
   const dfd::ConvGeom g = rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad);
   return dfd::conv_dgrad((hipStream_t)stream, g, dy, w, wpack, wpack_t, dx);
   DFD_GUARD_END
+}
+
+int64_t dfd_rn_conv_wgrad_slab_floats(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad) {
+  return dfd::conv_wgrad_slab_floats(rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad));
 }
 
 int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin, const float* dy,

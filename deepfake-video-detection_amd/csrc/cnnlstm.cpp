@@ -203,7 +203,7 @@ static int cl_forward(hipStream_t s, const ClDims& d, const ClParams& P, float* 
                                bn_run[2 * i + 1], momentum, 1e-5f, training != 0, bn, bn + 512, bn + 1024, bn + 1536));
     if (i < 3) {
       float* Pout = W + L.oP[i];
-      DFD_TRY(bn_relu_pool_fwd(s, Y, bn + 1024, bn + 1536, (int)BT, g.Ho, g.Wo, g.Co, L.Hp[i], L.Wp[i], Pout,
+      DFD_TRY(bn_relu_pool_fwd(s, Y, nullptr, bn + 1024, bn + 1536, (int)BT, g.Ho, g.Wo, g.Co, L.Hp[i], L.Wp[i], Pout,
                                reinterpret_cast<uint8_t*>(W + L.oArg[i])));
       src = Pout;
       const int64_t C = g.Co;
@@ -287,7 +287,7 @@ static int cl_backward(hipStream_t s, const ClDims& d, const ClParams& P, const 
     float* bn = W + L.oBN[i];
     if (i == 3) DFD_TRY(bn_relu_gap_bwd(s, S + L.sdF, Y, bn + 1024, bn + 1536, (int)BT, cg.Ho * cg.Wo, cg.Co, g));
     else
-      DFD_TRY(bn_relu_pool_bwd(s, dP, reinterpret_cast<const uint8_t*>(W + L.oArg[i]), Y, bn + 1024, bn + 1536, (int)BT,
+      DFD_TRY(bn_relu_pool_bwd(s, dP, reinterpret_cast<const uint8_t*>(W + L.oArg[i]), Y, nullptr, bn + 1024, bn + 1536, (int)BT,
                                cg.Ho, cg.Wo, cg.Co, L.Hp[i], L.Wp[i], g));
     BnBwdIn in{};
     in.dZ = g;

@@ -13,12 +13,14 @@ struct ConvGeom {
 int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* w,
                  const float* bias, float* wf, float* Y, float* stats, int* stat_rows);
 int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX);
+int64_t conv_wgrad_slab_floats(const ConvGeom& g);  // the slab conv_wgrad uses in full
 int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* dY, float* slab,
                int64_t slab_cap, float* gw);
-int bn_relu_pool_fwd(hipStream_t s, const float* Y, const float* sc, const float* sh, int N, int H, int W, int C,
-                     int Ho, int Wo, float* P, uint8_t* arg);
-int bn_relu_pool_bwd(hipStream_t s, const float* dP, const uint8_t* arg, const float* Y, const float* sc,
-                     const float* sh, int N, int H, int W, int C, int Ho, int Wo, float* g);
+// z = mu ? (Y - mu) * sc + sh : Y * sc + sh  (the centred form with sh = beta when mu is given)
+int bn_relu_pool_fwd(hipStream_t s, const float* Y, const float* mu, const float* sc, const float* sh, int N, int H,
+                     int W, int C, int Ho, int Wo, float* P, uint8_t* arg);
+int bn_relu_pool_bwd(hipStream_t s, const float* dP, const uint8_t* arg, const float* Y, const float* mu,
+                     const float* sc, const float* sh, int N, int H, int W, int C, int Ho, int Wo, float* g);
 int bn_relu_gap_fwd(hipStream_t s, const float* Y, const float* sc, const float* sh, int N, int HW, int C,
                     float* feat);
 int bn_relu_gap_bwd(hipStream_t s, const float* dfeat, const float* Y, const float* sc, const float* sh, int N,

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
                                                               const float* __restrict__ mean,
                                                               const float* __restrict__ invstd, int training,
                                                               float* dgamma, float* dbeta, int accumulate,
-                                                              float* coef) {
+                                                              float* coef, int centred) {
   __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
   double s = 0.0, q = 0.0;
   reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
@@ -322,7 +322,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
     if (training) {
       const double n = (double)count;
       k2 = -gm * is * is * q / n;
-      k3 = -gm * is * s / n + gm * is * is * (double)mean[c] * q / n;
+      k3 = -gm * is * s / n;
+      if (!centred) k3 += gm * is * is * (double)mean[c] * q / n;
     }
     coef[c] = (float)k1;
     coef[C + c] = (float)k2;
@@ -332,9 +333,9 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
 
 int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                            const float* mean, const float* invstd, bool training, float* dgamma, float* dbeta,
-                           bool accumulate, float* coef) {
+                           bool accumulate, float* coef, bool centred) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, FIN_CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, mean,
-                     invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef);
+                     invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef, centred ? 1 : 0);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

@@ -340,9 +340,15 @@ __global__ void conv_unpack_grad_kernel(const float* __restrict__ slab, int spli
 }
 
 // ------------------------------------------------------------------ BN + ReLU + MaxPool(3,2,1)
-__global__ void bn_relu_pool_fwd_kernel(const float* __restrict__ Y, const float* __restrict__ sc,
-                                        const float* __restrict__ sh, int N, int H, int W, int C, int Ho, int Wo,
-                                        float* __restrict__ P, uint8_t* __restrict__ arg) {
+// mu given: the centred form (Y - mu) * sc + sh (sh = beta), as torch's (y - mean) * invstd * gamma + beta
+// (the ResNet-50 training member: y * sc + (beta - mu * sc) cancels where |mean| >> std)
+__device__ __forceinline__ float bn_z(float y, const float* mu, float sc, float sh, int c) {
+  return mu ? (y - mu[c]) * sc + sh : y * sc + sh;
+}
+__global__ void bn_relu_pool_fwd_kernel(const float* __restrict__ Y, const float* __restrict__ mu,
+                                        const float* __restrict__ sc, const float* __restrict__ sh, int N, int H,
+                                        int W, int C, int Ho, int Wo, float* __restrict__ P,
+                                        uint8_t* __restrict__ arg) {
   const int64_t n = (int64_t)N * Ho * Wo * C;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int c = (int)(i % C);
@@ -359,7 +365,7 @@ __global__ void bn_relu_pool_fwd_kernel(const float* __restrict__ Y, const float
       for (int kx = 0; kx < 3; ++kx) {
         const int ix = ox * 2 - 1 + kx;
         if (ix < 0 || ix >= W) continue;
-        const float z = fmaxf(Y[(((int64_t)f * H + iy) * W + ix) * C + c] * sc[c] + sh[c], 0.f);
+        const float z = fmaxf(bn_z(Y[(((int64_t)f * H + iy) * W + ix) * C + c], mu, sc[c], sh[c], c), 0.f);
         if (z > best) { best = z; bi = ky * 3 + kx; }
       }
     }
@@ -369,7 +375,8 @@ __global__ void bn_relu_pool_fwd_kernel(const float* __restrict__ Y, const float
 }
 // g[n][iy][ix][c] = relu'(z) * sum of dP over the windows whose argmax is (iy, ix)
 __global__ void bn_relu_pool_bwd_kernel(const float* __restrict__ dP, const uint8_t* __restrict__ arg,
-                                        const float* __restrict__ Y, const float* __restrict__ sc,
+                                        const float* __restrict__ Y, const float* __restrict__ mu,
+                                        const float* __restrict__ sc,
                                         const float* __restrict__ sh, int N, int H, int W, int C, int Ho, int Wo,
                                         float* __restrict__ g) {
   const int64_t n = (int64_t)N * H * W * C;
@@ -393,7 +400,7 @@ __global__ void bn_relu_pool_bwd_kernel(const float* __restrict__ dP, const uint
         if (arg[o] == ky * 3 + kx) a += dP[o];
       }
     }
-    const float z = Y[i] * sc[c] + sh[c];
+    const float z = bn_z(Y[i], mu, sc[c], sh[c], c);
     g[i] = z > 0.f ? a : 0.f;
   }
 }
@@ -454,13 +461,22 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
   return conv_gemm<OpConvDgradA, OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr);
 }
 
+// pixel splits of the weight gradient (each its own slab of Co x Kp partial sums)
+static int conv_wgrad_splits(const ConvGeom& g) {
+  const int M = g.N * g.Ho * g.Wo, Kp = g.KH * g.KW * g.Ci;
+  const int tiles = cdiv(g.Co, CG_T) * cdiv(Kp, CG_T);
+  return std::max(1, std::min(cdiv(M, 256), 2048 / std::max(tiles, 1)));
+}
+int64_t conv_wgrad_slab_floats(const ConvGeom& g) {
+  return (int64_t)conv_wgrad_splits(g) * g.Co * g.KH * g.KW * g.Ci;
+}
+
 int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* dY, float* slab,
                int64_t slab_cap, float* gw) {
   const int KK = g.KH * g.KW;
   const int M = g.N * g.Ho * g.Wo, Kp = KK * g.Ci;  // GEMM: C[Co][Kp] = sum_m dY[m][co] X(m, kp)
   const int64_t per = (int64_t)g.Co * Kp;
-  const int tiles = cdiv(g.Co, CG_T) * cdiv(Kp, CG_T);
-  int splits = std::max(1, std::min(cdiv(M, 256), 2048 / std::max(tiles, 1)));
+  int splits = conv_wgrad_splits(g);
   splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / per));
   OpCols pa{dY, g.Co, g.Co, M};
   OpConvBT pb{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, Kp, M};
@@ -473,16 +489,16 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
   return 0;
 }
 
-int bn_relu_pool_fwd(hipStream_t s, const float* Y, const float* sc, const float* sh, int N, int H, int W, int C,
-                     int Ho, int Wo, float* P, uint8_t* arg) {
-  hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(ew((int64_t)N * Ho * Wo * C)), dim3(256), 0, s, Y, sc, sh, N, H, W,
+int bn_relu_pool_fwd(hipStream_t s, const float* Y, const float* mu, const float* sc, const float* sh, int N, int H,
+                     int W, int C, int Ho, int Wo, float* P, uint8_t* arg) {
+  hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(ew((int64_t)N * Ho * Wo * C)), dim3(256), 0, s, Y, mu, sc, sh, N, H, W,
                      C, Ho, Wo, P, arg);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
-int bn_relu_pool_bwd(hipStream_t s, const float* dP, const uint8_t* arg, const float* Y, const float* sc,
-                     const float* sh, int N, int H, int W, int C, int Ho, int Wo, float* g) {
-  hipLaunchKernelGGL(bn_relu_pool_bwd_kernel, dim3(ew((int64_t)N * H * W * C)), dim3(256), 0, s, dP, arg, Y, sc, sh,
+int bn_relu_pool_bwd(hipStream_t s, const float* dP, const uint8_t* arg, const float* Y, const float* mu,
+                     const float* sc, const float* sh, int N, int H, int W, int C, int Ho, int Wo, float* g) {
+  hipLaunchKernelGGL(bn_relu_pool_bwd_kernel, dim3(ew((int64_t)N * H * W * C)), dim3(256), 0, s, dP, arg, Y, mu, sc, sh,
                      N, H, W, C, Ho, Wo, g);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;

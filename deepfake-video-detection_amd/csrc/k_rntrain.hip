@@ -9,7 +9,11 @@
 // (stride 1 and 2: the gather visits only the taps whose output position is integral) and weight
 // gradient (split over pixels, ordered slab sum).  The BN backward is k_bn.hip's reduce / finalize /
 // apply with the identity activation; here live the elementwise pieces around them:
-//   bn_act    out = relu?(y * scale + shift (+ res))          (BN apply, bottleneck add, ReLU)
+//   bn_act    out = relu?((y - mean) * scale + beta (+ res))  (BN apply, bottleneck add, ReLU)
+//   bn_bwd    dy = k1*g + k2*(y - mean) + k3                   (BN backward apply)
+// Both in torch's centred form: the folded y * scale + (beta - mean * scale) loses
+// eps * |mean| / std of the normalised value where |mean| >> std (VERDICT r3 item 1;
+// tools/rn_bn_numerics.py emulates both forms against fp64).
 //   relu_bwd  g = out > 0 ? dout : 0                          (through a saved ReLU output)
 //   gap_bwd   g = out > 0 ? dfeat[n][c] / HW : 0              (AdaptiveAvgPool2d + the last ReLU)
 #include "cnnlstm.h"
@@ -17,14 +21,15 @@
 
 namespace dfd {
 
-__global__ __launch_bounds__(256) void rn_bn_act_kernel(const float* __restrict__ y, const float* __restrict__ sc,
-                                                        const float* __restrict__ sh, const float* __restrict__ r,
-                                                        int relu, int64_t nvec, int cv, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void rn_bn_act_kernel(const float* __restrict__ y, const float* __restrict__ mu,
+                                                        const float* __restrict__ sc, const float* __restrict__ be,
+                                                        const float* __restrict__ r, int relu, int64_t nvec, int cv,
+                                                        float* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
     const int c = (int)(i % cv) * 4;
     const float4 v = reinterpret_cast<const float4*>(y)[i];
-    float o[4] = {v.x * sc[c] + sh[c], v.y * sc[c + 1] + sh[c + 1], v.z * sc[c + 2] + sh[c + 2],
-                  v.w * sc[c + 3] + sh[c + 3]};
+    float o[4] = {(v.x - mu[c]) * sc[c] + be[c], (v.y - mu[c + 1]) * sc[c + 1] + be[c + 1],
+                  (v.z - mu[c + 2]) * sc[c + 2] + be[c + 2], (v.w - mu[c + 3]) * sc[c + 3] + be[c + 3]};
     if (r) {
       const float4 q = reinterpret_cast<const float4*>(r)[i];
       o[0] += q.x; o[1] += q.y; o[2] += q.z; o[3] += q.w;
@@ -56,13 +61,31 @@ __global__ __launch_bounds__(256) void rn_gap_bwd_kernel(const float* __restrict
   }
 }
 
+// dy = k1*g + k2*(y - mean) + k3 (coef rows k1, k2, k3 of the centred finalize)
+__global__ __launch_bounds__(256) void rn_bn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                              const float* __restrict__ mu,
+                                                              const float* __restrict__ coef, int64_t nvec, int C,
+                                                              float* __restrict__ dy) {
+  const int cv = C / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % cv) * 4;
+    const float4 a = reinterpret_cast<const float4*>(g)[i], v = reinterpret_cast<const float4*>(y)[i];
+    const float ga[4] = {a.x, a.y, a.z, a.w}, ya[4] = {v.x, v.y, v.z, v.w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = coef[c + j] * ga[j] + coef[C + c + j] * (ya[j] - mu[c + j]) + coef[2 * C + c + j];
+    reinterpret_cast<float4*>(dy)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 static int rn_grid(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 4096)); }
 
-int rn_bn_act(hipStream_t s, const float* y, const float* sc, const float* sh, const float* r, int relu, int64_t M,
-              int C, float* out) {
+int rn_bn_act(hipStream_t s, const float* y, const float* mean, const float* sc, const float* beta, const float* r,
+              int relu, int64_t M, int C, float* out) {
   if (C % 4) { set_error("rn_bn_act: C % 4", __FILE__, __LINE__); return -1; }
   const int64_t nvec = M * C / 4;
-  hipLaunchKernelGGL(rn_bn_act_kernel, dim3(rn_grid(nvec)), dim3(256), 0, s, y, sc, sh, r, relu, nvec, C / 4, out);
+  hipLaunchKernelGGL(rn_bn_act_kernel, dim3(rn_grid(nvec)), dim3(256), 0, s, y, mean, sc, beta, r, relu, nvec, C / 4,
+                     out);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -82,7 +105,7 @@ int rn_gap_bwd(hipStream_t s, const float* dfeat, const float* out, int N, int H
 }
 
 // the BN backward of a train-mode BatchNorm2d whose output gradient is g (identity activation):
-// dgamma, dbeta (written) and dy = k1*g + k2*y + k3
+// dgamma, dbeta (written) and dy = k1*g + k2*(y - mean) + k3
 int rn_bn_train_bwd(hipStream_t s, const float* g, const float* y, int64_t M, int C, const float* mean,
                     const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
                     float* dbeta, float* stats, float* coef, float* dy) {
@@ -95,8 +118,12 @@ int rn_bn_train_bwd(hipStream_t s, const float* g, const float* y, int64_t M, in
   in.shift = shift;
   int rows = 0;
   DFD_TRY(launch_bn_bwd_reduce<float>(s, in, y, M, C, stats, &rows));
-  DFD_TRY(launch_bn_bwd_finalize(s, stats, rows, M, C, gamma, mean, invstd, true, dgamma, dbeta, false, coef));
-  return launch_bn_bwd_apply<float>(s, in, y, coef, dy, M, C);
+  DFD_TRY(launch_bn_bwd_finalize(s, stats, rows, M, C, gamma, mean, invstd, true, dgamma, dbeta, false, coef, true));
+  if (C % 4) { set_error("rn_bn_train_bwd: C % 4", __FILE__, __LINE__); return -1; }
+  const int64_t nvec = M * C / 4;
+  hipLaunchKernelGGL(rn_bn_bwd_apply_kernel, dim3(rn_grid(nvec)), dim3(256), 0, s, g, y, mean, coef, nvec, C, dy);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
 }
 
 }  // namespace dfd

@@ -77,8 +77,9 @@ int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* 
 template <typename T>
 int launch_rn_avgpool(hipStream_t s, const T* x, int N, int HW, int C, float* out);
 // ResNet-50 training pieces (k_rntrain.hip, fp32)
-int rn_bn_act(hipStream_t s, const float* y, const float* sc, const float* sh, const float* r, int relu, int64_t M,
-              int C, float* out);
+// centred BN apply: out = relu?((y - mean) * sc + beta (+ r))
+int rn_bn_act(hipStream_t s, const float* y, const float* mean, const float* sc, const float* beta, const float* r,
+              int relu, int64_t M, int C, float* out);
 int rn_relu_bwd(hipStream_t s, const float* dout, const float* out, int64_t n, float* g);
 int rn_gap_bwd(hipStream_t s, const float* dfeat, const float* out, int N, int HW, int C, float* g);
 int rn_bn_train_bwd(hipStream_t s, const float* g, const float* y, int64_t M, int C, const float* mean,
@@ -243,7 +244,8 @@ int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M
 // phase 2 (finalize): dgamma/dbeta into grads, coefficients k1,k2,k3 for dY = k1*g + k2*y + k3
 int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C,
                            const float* gamma, const float* mean, const float* invstd, bool training,
-                           float* dgamma, float* dbeta, bool accumulate, float* coef /*[3][C]*/);
+                           float* dgamma, float* dbeta, bool accumulate, float* coef /*[3][C]*/,
+                           bool centred = false /* k3 without the k2*mean term: dY = k1*g + k2*(y-mean) + k3 */);
 // phase 3: dY = k1*g + k2*y + k3   (dY may alias dZ)
 template <typename T>
 int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const float* coef, T* dY, int64_t M,

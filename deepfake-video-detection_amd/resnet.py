@@ -223,9 +223,11 @@ def _conv_bn_fwd(lib, st, u, x, xs, n, hw, save):
     vecs = torch.empty(4, cout, dtype=torch.float32, device=dev)
     with torch.no_grad():
         bn.num_batches_tracked.add_(1)
+    # torch's momentum=None: the cumulative moving average, factor 1 / num_batches_tracked
+    mom = float(bn.momentum) if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
     _lib.check(lib.dfd_rn_bn_train_finalize(st, stats.data_ptr(), rows, n * ho * wo, cout, bn.weight.data_ptr(),
                                             bn.bias.data_ptr(), bn.running_mean.data_ptr(),
-                                            bn.running_var.data_ptr(), float(bn.momentum), float(bn.eps),
+                                            bn.running_var.data_ptr(), mom, float(bn.eps),
                                             vecs[0].data_ptr(), vecs[1].data_ptr(), vecs[2].data_ptr(),
                                             vecs[3].data_ptr()))
     if save:
@@ -234,10 +236,11 @@ def _conv_bn_fwd(lib, st, u, x, xs, n, hw, save):
     return y, (ho, wo), vecs
 
 
-def _bn_act(lib, st, y, vecs, res, relu):
+def _bn_act(lib, st, y, vecs, bn, res, relu):
+    """relu?((y - mean) * scale + beta (+ res)): torch's centred order of operations"""
     out = torch.empty_like(y)
-    _lib.check(lib.dfd_rn_bn_act(st, y.data_ptr(), vecs[2].data_ptr(), vecs[3].data_ptr(), _lib.ptr(res),
-                                 1 if relu else 0, y.shape[0], y.shape[1], out.data_ptr()))
+    _lib.check(lib.dfd_rn_bn_act(st, y.data_ptr(), vecs[0].data_ptr(), vecs[2].data_ptr(), bn.bias.data_ptr(),
+                                 _lib.ptr(res), 1 if relu else 0, y.shape[0], y.shape[1], out.data_ptr()))
     return out
 
 
@@ -262,7 +265,8 @@ def _train_forward(trunk, x, save):
     hp, wp = (hw0[0] + 2 - 3) // 2 + 1, (hw0[1] + 2 - 3) // 2 + 1
     h = torch.empty(n * hp * wp, 64, dtype=torch.float32, device=dev)
     arg = torch.empty(n * hp * wp * 64, dtype=torch.uint8, device=dev)
-    _lib.check(lib.dfd_rn_pool_train_fwd(st, y0.data_ptr(), v0[2].data_ptr(), v0[3].data_ptr(), n, hw0[0], hw0[1], 64,
+    _lib.check(lib.dfd_rn_pool_train_fwd(st, y0.data_ptr(), v0[0].data_ptr(), v0[2].data_ptr(),
+                                         trunk[1].bias.data_ptr(), n, hw0[0], hw0[1], 64,
                                          h.data_ptr(), arg.data_ptr()))
     hw = (hp, wp)
     for li in range(4):
@@ -270,18 +274,18 @@ def _train_forward(trunk, x, save):
             b = {"in": h, "hw": hw}
             u1, u2, u3 = unit(blk.conv1, blk.bn1), unit(blk.conv2, blk.bn2), unit(blk.conv3, blk.bn3)
             y1, hw1, v1 = _conv_bn_fwd(lib, st, u1, h, _nhwc_strides(h, hw, blk.conv1.in_channels), n, hw, save)
-            a1 = _bn_act(lib, st, y1, v1, None, True)
+            a1 = _bn_act(lib, st, y1, v1, blk.bn1, None, True)
             y2, hw2, v2 = _conv_bn_fwd(lib, st, u2, a1, _nhwc_strides(a1, hw1, blk.conv2.in_channels), n, hw1, save)
-            a2 = _bn_act(lib, st, y2, v2, None, True)
+            a2 = _bn_act(lib, st, y2, v2, blk.bn2, None, True)
             y3, _, v3 = _conv_bn_fwd(lib, st, u3, a2, _nhwc_strides(a2, hw2, blk.conv3.in_channels), n, hw2, save)
             if blk.downsample is not None:
                 ud = unit(blk.downsample[0], blk.downsample[1])
                 yd, _, vd = _conv_bn_fwd(lib, st, ud, h, _nhwc_strides(h, hw, blk.conv1.in_channels), n, hw, save)
-                idn = _bn_act(lib, st, yd, vd, None, False)
+                idn = _bn_act(lib, st, yd, vd, blk.downsample[1], None, False)
                 b["ds"] = ud
             else:
                 idn = h
-            h = _bn_act(lib, st, y3, v3, idn, True)
+            h = _bn_act(lib, st, y3, v3, blk.bn3, idn, True)
             hw = hw2
             b.update(u=(u1, u2, u3), a1=a1, a2=a2, out=h)
             blocks.append(b)
@@ -321,7 +325,8 @@ def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
         dx = torch.empty(n * u.hw[0] * u.hw[1], cin, dtype=torch.float32, device=dev)
         _lib.check(lib.dfd_rn_conv_dgrad(st, dy.data_ptr(), n, u.hw[0], u.hw[1], cin, w.data_ptr(), cout, k, k, s, p,
                                          wp.data_ptr(), wp[nw:].data_ptr(), dx.data_ptr()))
-    slab = torch.empty(64 * nw, dtype=torch.float32, device=dev)
+    slab = torch.empty(lib.dfd_rn_conv_wgrad_slab_floats(n, u.hw[0], u.hw[1], cin, cout, k, k, s, p),
+                       dtype=torch.float32, device=dev)
     dw = torch.empty_like(w)
     x = u.x
     if x.dim() == 4:  # the stem reads the frames through their strides
@@ -375,7 +380,8 @@ def _train_backward(trunk, saved, dfeat):
     us = saved["units"][0]
     gs = torch.empty_like(us.y)
     _lib.check(lib.dfd_rn_pool_train_bwd(st, g.data_ptr(), saved["stem_arg"].data_ptr(), us.y.data_ptr(),
-                                         us.scale.data_ptr(), us.shift.data_ptr(), n, us.ohw[0], us.ohw[1], 64,
+                                         us.mean.data_ptr(), us.scale.data_ptr(), us.bn.bias.data_ptr(), n,
+                                         us.ohw[0], us.ohw[1], 64,
                                          gs.data_ptr()))
     dy0 = _bn_bwd(lib, st, us, gs, grads)
     _conv_bwd(lib, st, us, dy0, n, grads, need_dx=False)
@@ -395,6 +401,9 @@ class _RnTrainFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dfeat):
+        if ctx.saved is None:
+            raise RuntimeError("the ResNet-50 training node frees its saved activations after the first backward: "
+                               "a second backward through it (retain_graph=True) is not supported")
         grads = _train_backward(ctx.trunk, ctx.saved, dfeat.float())
         ctx.saved = None
         params = ctx.trunk.train_parameters()

@@ -197,20 +197,23 @@ DFD_API int dfd_rn_bn_train_finalize(void* stream, const float* stats, int rows,
                                      const float* gamma, const float* beta, float* running_mean,
                                      float* running_var, float momentum, float eps, float* mean, float* invstd,
                                      float* scale, float* shift);
-/* out = relu?(y * scale + shift (+ res)), (M, C), C % 4 == 0 */
-DFD_API int dfd_rn_bn_act(void* stream, const float* y, const float* scale, const float* shift, const float* res,
-                          int relu, int64_t M, int C, float* out);
-/* stem: out = maxpool3x3/2(relu(y * scale + shift)) with the argmax tap kept; and its backward to
- * the BN output gradient g (relu' included) */
-DFD_API int dfd_rn_pool_train_fwd(void* stream, const float* y, const float* scale, const float* shift, int N, int H,
-                                  int W, int C, float* out, uint8_t* argmax);
+/* out = relu?((y - mean) * scale + beta (+ res)), (M, C), C % 4 == 0 -- torch's centred order of
+ * operations (scale = gamma * invstd from dfd_rn_bn_train_finalize, beta = the BN bias) */
+DFD_API int dfd_rn_bn_act(void* stream, const float* y, const float* mean, const float* scale, const float* beta,
+                          const float* res, int relu, int64_t M, int C, float* out);
+/* stem: out = maxpool3x3/2(relu((y - mean) * scale + beta)) with the argmax tap kept; and its backward
+ * to the BN output gradient g (relu' included) */
+DFD_API int dfd_rn_pool_train_fwd(void* stream, const float* y, const float* mean, const float* scale,
+                                  const float* beta, int N, int H, int W, int C, float* out, uint8_t* argmax);
 DFD_API int dfd_rn_pool_train_bwd(void* stream, const float* dout, const uint8_t* argmax, const float* y,
-                                  const float* scale, const float* shift, int N, int H, int W, int C, float* g);
+                                  const float* mean, const float* scale, const float* beta, int N, int H, int W, int C,
+                                  float* g);
 /* g = out > 0 ? dout : 0 (n % 4 == 0);  global-average-pool backward through the last ReLU:
  * g[n][p][c] = out > 0 ? dfeat[n][c] / HW : 0 */
 DFD_API int dfd_rn_relu_bwd(void* stream, const float* dout, const float* out, int64_t n, float* g);
 DFD_API int dfd_rn_gap_bwd(void* stream, const float* dfeat, const float* out, int N, int HW, int C, float* g);
-/* train-mode BN backward from its output gradient g: dgamma, dbeta (written) and dy;
+/* train-mode BN backward from its output gradient g: dgamma, dbeta (written) and
+ * dy = k1*g + k2*(y - mean) + k3 (centred);
  * stats >= 2048*2*C floats, coef >= 3*C floats (scratch) */
 DFD_API int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, int64_t M, int C, const float* mean,
                                 const float* invstd, const float* scale, const float* shift, const float* gamma,
@@ -219,6 +222,10 @@ DFD_API int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, in
  * Cout*Cin*kh*kw floats each */
 DFD_API int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout,
                               int kh, int kw, int stride, int pad, float* wpack, float* wpack_t, float* dx);
+/* the slab size (floats) dfd_rn_conv_wgrad uses in full for this shape (its pixel splits x |dw|; a
+ * smaller slab runs fewer splits) */
+DFD_API int64_t dfd_rn_conv_wgrad_slab_floats(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride,
+                                              int pad);
 /* dw OIHW (written) = weight gradient from x (strides xs4) and dy; slab: scratch of slab_floats */
 DFD_API int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin,
                               const float* dy, int Cout, int kh, int kw, int stride, int pad, float* slab,

@@ -14,7 +14,10 @@ infrastructure only).
    features relative L2 <= ``FEAT_TOL`` and elementwise rtol 1e-3 / atol 1e-4; every gradient
    against the fp64 restatement within ``GRAD_MULT`` x the fp32 oracle's own distance to it (the
    train-mode BatchNorm chain amplifies fp32 rounding to ~1-2 % on the early layers for ANY fp32
-   implementation); running buffers rtol 1e-4 / atol 1e-5.
+   implementation); running buffers rtol 1e-4 / atol 1e-5.  The BatchNorm apply and its backward
+   run in torch's centred order, (y - mean) * scale + beta and k1*g + k2*(y - mean) + k3: the folded
+   y * scale + shift put layer4's last-block gradients 3-4x further from fp64 than torch fp32 on
+   the ensemble step (tools/rn_bn_numerics.py emulates both forms on the CPU: 0.023 -> 0.008).
 3. The ensemble step: ``EnsembleDetector`` in train mode, weighted CE, backward -- both members
    receive every gradient, the resnet member's logits and gradients match the oracle trunk + the
    reference head math.
@@ -36,9 +39,6 @@ pytestmark = pytest.mark.gpu
 
 FEAT_TOL = 1e-4
 GRAD_MULT, GRAD_FLOOR = 3.0, 1e-4  # HIP vs fp64 <= max(3 x (torch fp32 vs fp64), 1e-4)
-# the ensemble step's dfeat comes through the head and CE: on layer4's last block torch's own fp32
-# gradients already sit 0.6 % from fp64 there (cancellation), and the HIP ones 2-3 % at 2 x 2 clips
-ENS_MULT = 4.0
 
 # (Cin, H, Cout, k, stride) of every distinct convolution (torchvision v1.5 Bottleneck) + conv1
 SHAPES = [(3, 32, 64, 7, 2), (64, 16, 64, 1, 1), (64, 16, 64, 3, 1), (64, 16, 256, 1, 1), (256, 16, 128, 1, 1),
@@ -169,8 +169,8 @@ def test_ensemble_training_step(cuda):
     resnet member matches the oracle trunk + the reference head math."""
     torch.manual_seed(0)
     ens = EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False, dropout_rate=0.0).to(cuda).train()
-    x = torch.randn(4, 2, 3, 128, 128).cuda()
-    y = torch.tensor([0, 1, 1, 0]).cuda()
+    x = torch.randn(2, 2, 3, 128, 128).cuda()
+    y = torch.tensor([0, 1]).cuda()
     w = torch.tensor([0.7, 1.3]).cuda()
     m = ens.models[1]
     refs = {}
@@ -187,7 +187,7 @@ def test_ensemble_training_step(cuda):
     for dt, ref in refs.items():
         sd = {k: v.detach().to(dt) if v.is_floating_point() else v for k, v in m.state_dict().items()}
         with torch.backends.cudnn.flags(enabled=False):
-            f = resnet_features(ref, x.reshape(8, 3, 128, 128).to(dt)).view(4, 2, -1)
+            f = resnet_features(ref, x.reshape(4, 3, 128, 128).to(dt)).view(2, 2, -1)
             hh = torch.relu(f @ sd["temporal_attention.0.weight"].T + sd["temporal_attention.0.bias"])
             a = torch.sigmoid(hh @ sd["temporal_attention.2.weight"].T + sd["temporal_attention.2.bias"]).squeeze(-1)
             a = torch.softmax(a, dim=1)
@@ -202,8 +202,11 @@ def test_ensemble_training_step(cuda):
     r32, r64 = dict(refs[torch.float32].named_parameters()), dict(refs[torch.float64].named_parameters())
     for n, p in m.backbone.named_parameters():
         e, e32 = _rel(p.grad, r64[n].grad), _rel(r32[n].grad, r64[n].grad)
-        if e > max(ENS_MULT * e32, GRAD_FLOOR):
+        if e > max(GRAD_MULT * e32, GRAD_FLOOR):
             bad.append((n, e, e32))
+    worst = sorted(((_rel(p.grad, r64[n].grad), _rel(r32[n].grad, r64[n].grad), n)
+                    for n, p in m.backbone.named_parameters()), reverse=True)
+    print(f"ensemble step: worst gradient rel errors vs fp64 (HIP, torch fp32): {worst[:6]}")
     assert not bad, bad
 
 
@@ -235,3 +238,31 @@ def test_ensemble_train_step_fused_adamw(cuda):
         torch.testing.assert_close(p.detach(), rp.detach(), rtol=1e-5, atol=1e-7)
         changed += int(not torch.equal(p.detach(), b))
     assert changed >= 0.95 * len(params), (changed, len(params))
+
+
+def test_second_backward_refused_and_cumulative_momentum(cuda):
+    """a second backward through the training node (retain_graph=True) raises a clear
+    RuntimeError; BatchNorm2d(momentum=None) updates the running buffers as torch's cumulative
+    moving average (factor 1 / num_batches_tracked)."""
+    t, ref = _pair(7, cuda)
+    x = torch.randn(2, 3, 64, 64).cuda()
+    f = t(x)
+    f.sum().backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="second backward"):
+        f.sum().backward()
+    t, ref = _pair(8, cuda)
+    for m in list(t.modules()) + list(ref.modules()):
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = None
+    for step in range(2):
+        xs = torch.randn(2, 3, 64, 64).cuda()
+        with torch.no_grad():
+            t(xs)
+            with torch.backends.cudnn.flags(enabled=False):
+                resnet_features(ref, xs)
+    rb = dict(ref.named_buffers())
+    for name, b in t.named_buffers():
+        if name.endswith("num_batches_tracked"):
+            assert int(b) == int(rb[name]) == 2, name
+        else:
+            torch.testing.assert_close(b, rb[name], rtol=1e-4, atol=1e-5, msg=lambda m: f"{name}: {m}")
