@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher/rendezvous self-test on CPU (gloo): ranks report and exit, no GPU use")
     ap.add_argument("--tune", action="append", default=[], metavar="KEY=VALUE",
-                    help="kernel-selection knob for A/B runs (dfd_set_tuning), e.g. dw_bwd_pre=2")
+                    help="kernel-selection knob of the model's plans for A/B runs (dfd_b0_plan_set_tuning), "
+                         "e.g. pwl_fused=0")
     return ap.parse_args()
 
 
@@ -210,15 +211,12 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    if args.tune:
-        from deepfake_amd import _lib
-        lib = _lib.load()
-        for kv in args.tune:
-            k, v = kv.split("=", 1)
-            lib.dfd_set_tuning(k.encode(), int(v))
     torch.manual_seed(0)
     model = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.5,
                                        compute_dtype=args.dtype)
+    for kv in args.tune or []:
+        k, v = kv.split("=", 1)
+        model.backbone.runtime().set_tuning(k, int(v))
     deterministic_init_(model, seed=0)
     model = model.to(dev).train()
     step = DataParallelTrainer(model, lr=1e-4, weight_decay=1e-5, max_grad_norm=1.0,

@@ -86,6 +86,9 @@ _SIGS = {
                           ctypes.POINTER(c_i)]),
     "dfd_attention": (c_i, [c_p, c_i, c_i, c_i, c_i, c_f, c_p, c_i64, c_i, c_i, c_p, c_i64, c_p, c_p, c_i64, c_p,
                             c_i64]),
+    "dfd_vgemm": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_i64]),
+    "dfd_vgemm_tn_slab_floats": (c_i64, [c_i64, c_i, c_i]),
+    "dfd_blaslt_calls": (c_i64, []),
     "dfd_sgemm": (c_i, [c_p, c_i, c_i, c_p, c_i, c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_f, c_p]),
     "dfd_pw_conv_wgrad": (c_i, [c_p, c_i, c_p, c_p, c_i64, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_p, c_i64, c_p,
                                 c_i]),

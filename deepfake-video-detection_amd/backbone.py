@@ -208,6 +208,13 @@ class EfficientNetB0Trunk(FlatModule):
         return s
 
 
+# Kernel-selection overrides every NEW B0Runtime starts from (Python-side configuration, read once at
+# runtime construction; the native plans hold their own copies, nothing process-wide is consulted on
+# the enqueue path).  Tests and A/B tools set it before building a model, or call set_tuning on a
+# model's runtime.
+DEFAULT_TUNING: dict = {}
+
+
 class B0Runtime:
     """Per-model plan cache: one native plan per (frames, H, W, dtype, device).
 
@@ -222,7 +229,7 @@ class B0Runtime:
         self.lib = _lib.load()
         self.offsets = list(offsets)
         self.plans: dict = {}
-        self.tuning: dict = {}
+        self.tuning: dict = dict(DEFAULT_TUNING)
         self._lock = threading.Lock()
         self._norm = [*NORMALIZATIONS["imagenet"][0], *NORMALIZATIONS["imagenet"][1]]
 
@@ -233,7 +240,7 @@ class B0Runtime:
         self._norm = [*[float(v) for v in mean], *[float(v) for v in std]]
 
     def set_tuning(self, key: str, value: int) -> None:
-        """Per-runtime kernel-selection override (same keys as dfd_set_tuning)."""
+        """Per-runtime kernel-selection override (keys of dfd_b0_plan_set_tuning)."""
         with self._lock:
             self.tuning[key] = int(value)
             for h in self.plans.values():

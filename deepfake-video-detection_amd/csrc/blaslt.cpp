@@ -1,9 +1,8 @@
-// Plain library GEMMs through hipBLASLt (bf16 in, fp32 accumulate) for the large, compute-bound
-// transformer GEMMs of the ViT-B/16 branch (src/models.py:88-107, 280-291 -> timm
-// vit_base_patch16_224; the ResNet-50 member runs on k_rnconv.hip): there the fused prologues of k_gemm.hip buy nothing and
-// hipBLASLt's MFMA kernels run 2-5x faster (tools/torch_gemm_vit.py).  The EfficientNet-B0 hot
-// path keeps its own kernels (BN/SiLU prologues, BN-stat epilogues, skinny shapes where the library
-// is slower: tools/torch_gemm_ref.py).
+// Plain library GEMMs through hipBLASLt (bf16 in, fp32 accumulate): the MEASUREMENT comparison for
+// the ViT-B/16 trunk's own GEMMs (k_vgemm.hip), reachable only through the dfd_vgemm seam (ops 2 / 3,
+// tools/vgemm_bench.py).  No model path calls it: the ViT trunk runs k_vgemm.hip / k_gemm.hip, the
+// ResNet-50 member k_rnconv.hip / k_conv.hip, EfficientNet-B0 its own kernels.  dfd_blaslt_calls()
+// counts the library calls so tests can assert that.
 //
 // Row-major operands are passed to the column-major library as their transposes:
 //   C[M][N] = A[M][K] . B[N][K]^T (+ bias[N]) (+ R[M][N])  ==  C^T = B^T' . A'  (m = N, n = M)
@@ -14,6 +13,7 @@
 // and guarded by the same lock.
 #include <hipblaslt/hipblaslt.h>
 
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -147,8 +147,11 @@ int build(hipblasLtHandle_t h, int kind, hipDataType ab, hipDataType cd, int64_t
   return 0;
 }
 
+std::atomic<int64_t> g_calls{0};
+
 int run(hipStream_t s, int kind, hipDataType ab, hipDataType cd, int64_t m, int64_t n, int64_t k, const void* A,
         const void* B, const void* C, void* D, const float* bias, float beta, bool relu = false, int batch = 1) {
+  g_calls.fetch_add(1, std::memory_order_relaxed);
   int dev = 0;
   DFD_HIP_CHECK(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(g_mu);
@@ -215,5 +218,7 @@ int blaslt_wgrad_split(hipStream_t s, const bf16* dY, const bf16* X, float* dW, 
   DFD_TRY(run(s, 1, HIP_R_16BF, HIP_R_32F, K, N, M / splits, X, dY, slab, slab, nullptr, 0.f, false, splits));
   return launch_reduce_slabs(s, slab, splits, (int64_t)N * K, dW, false);
 }
+
+int64_t blaslt_calls() { return g_calls.load(std::memory_order_relaxed); }
 
 }  // namespace dfd

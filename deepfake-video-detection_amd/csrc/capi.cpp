@@ -13,6 +13,7 @@
 #include "head.h"
 #include "plan.h"
 #include "rnn.h"
+#include "vit.h"
 
 namespace dfd {
 static thread_local std::string g_err;
@@ -153,10 +154,8 @@ int dfd_b0_backward(dfd_b0_plan* plan, void* stream, const float* x, const int64
 
 int dfd_b0_plan_set_tuning(dfd_b0_plan* plan, const char* key, int64_t value) {
   if (!plan || !key) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
-  static const char* names[dfd::TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile",
-                                             "dw_bwd1", "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused"};
   for (int k = 0; k < dfd::TK_COUNT; ++k)
-    if (strcmp(key, names[k]) == 0) {
+    if (strcmp(key, dfd::kTuneNames[k]) == 0) {
       std::lock_guard<std::mutex> lk(plan->mu);
       plan->p.tune.v[k] = value;
       return 0;
@@ -544,20 +543,24 @@ int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, i
   DFD_GUARD_END
 }
 
+// the kernel test seams' overrides (dfd_set_tuning): read only by dfd_pw_conv / dfd_pw_conv_wgrad,
+// which install a snapshot for their own launch; plans never see them (dfd_b0_plan_set_tuning)
+static std::mutex g_seam_mu;
+static dfd::Tuning g_seam;
+static dfd::Tuning seam_snapshot() {
+  std::lock_guard<std::mutex> lk(g_seam_mu);
+  return g_seam;
+}
+
 int64_t dfd_set_tuning(const char* key, int64_t value) {
-  if (key && strcmp(key, "stream_min_rows") == 0) return dfd::set_stream_min_rows(value);
-  if (key && strcmp(key, "fold_min_rows") == 0) return dfd::set_fold_min_rows(value);
-  if (key && strcmp(key, "dw_bwd_fused") == 0) return dfd::set_dw_bwd_fused(value);
-  if (key && strcmp(key, "gemm_tile") == 0) return dfd::set_gemm_tile((int)value);
-  if (key && strcmp(key, "dw_bwd1") == 0) return dfd::set_dw_bwd1(value);
-  if (key && strcmp(key, "dw_fwd1") == 0) return dfd::set_dw_fwd1(value);
-  if (key && strcmp(key, "wgrad_stream") == 0) return dfd::set_wgrad_stream(value);
-  if (key && strcmp(key, "mbconv7") == 0) return dfd::set_mbconv7(value);
-  if (key && strcmp(key, "pwl_fused") == 0) return dfd::set_pwl_fused(value);
-  if (key && strcmp(key, "fold_fused") == 0) return dfd::set_fold_fused(value);
   if (key && strcmp(key, "rnn_step") == 0) return dfd::set_rnn_step(value);
-  if (key && strcmp(key, "vit_gemm") == 0) return dfd::set_vit_gemm(value);
-  if (key && strcmp(key, "vit_wsplit") == 0) return dfd::set_vit_wsplit(value);
+  for (int k = 0; key && k < dfd::TK_COUNT; ++k)
+    if (strcmp(key, dfd::kTuneNames[k]) == 0) {
+      std::lock_guard<std::mutex> lk(g_seam_mu);
+      const int64_t prev = g_seam.v[k] == dfd::kTuneUnset ? dfd::kTuneDefault[k] : g_seam.v[k];
+      g_seam.v[k] = value;
+      return prev;
+    }
   dfd::set_error("set_tuning: unknown key", __FILE__, __LINE__);
   return -1;
 }
@@ -583,6 +586,8 @@ int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, 
                 int pro_mode, const float* scale, const float* shift, const float* gate, int rows_per_frame,
                 float* stats, int* stat_rows) {
   DFD_GUARD_BEGIN
+  const dfd::Tuning tn = seam_snapshot();
+  const dfd::TuningScope ts(&tn);
   if (!pw_args_ok(dtype, M, N, K, pro_mode, scale, shift, gate, rows_per_frame)) return -1;
   const dfd::Pro pro{scale, shift, gate, rows_per_frame, K};
   hipStream_t s = (hipStream_t)stream;
@@ -611,6 +616,47 @@ int dfd_attention(void* stream, int backward, int images, int heads, int nt, flo
   DFD_GUARD_END
 }
 
+int64_t dfd_blaslt_calls(void) { return dfd::blaslt_calls(); }
+
+int64_t dfd_vgemm_tn_slab_floats(int64_t M, int N, int K) {
+  return (int64_t)dfd::vgemm_tn_splits(M, N, K, INT64_MAX) * N * K;
+}
+
+int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const void* R, const float* bias,
+              const void* Z, void* G, int64_t M, int N, int K, int epi, float* slab, int64_t slab_floats) {
+  DFD_GUARD_BEGIN
+  hipStream_t s = (hipStream_t)stream;
+  if (!A || !B || !C) { dfd::set_error("vgemm: null argument", __FILE__, __LINE__); return -1; }
+  if (op == 0 || op == 2) {  // NT: own kernel (0) or the hipBLASLt comparison (2)
+    if (((epi & dfd::VG_BIAS) && !bias) || ((epi & dfd::VG_RESID) && !R) || ((epi & dfd::VG_DGELU) && !Z) ||
+        ((epi & dfd::VG_GELU2) && !G)) {
+      dfd::set_error("vgemm: epilogue operand missing", __FILE__, __LINE__);
+      return -1;
+    }
+    if (op == 2) {
+      if (epi & ~(dfd::VG_BIAS | dfd::VG_RESID)) { dfd::set_error("vgemm: library path takes bias/resid", __FILE__, __LINE__); return -1; }
+      return dfd::blaslt_linear(s, (const dfd::bf16*)A, (const dfd::bf16*)B, (dfd::bf16*)C, (const dfd::bf16*)R,
+                                bias, M, N, K);
+    }
+    dfd::VgemmArgs a{};
+    a.A = (const dfd::bf16*)A; a.B = (const dfd::bf16*)B; a.C = (dfd::bf16*)C; a.R = (const dfd::bf16*)R;
+    a.bias = bias; a.Z = (const dfd::bf16*)Z; a.G = (dfd::bf16*)G;
+    a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
+    return dfd::launch_vgemm_nt(s, a, epi);
+  }
+  if (op == 1 || op == 3) {  // TN: C (fp32 [N][K]) = A^T . B with A [M][N], B [M][K]
+    if (!slab) { dfd::set_error("vgemm: slab missing", __FILE__, __LINE__); return -1; }
+    if (op == 3)
+      return dfd::blaslt_wgrad_split(s, (const dfd::bf16*)A, (const dfd::bf16*)B, (float*)C, M, N, K, 4, slab,
+                                     slab_floats);
+    return dfd::launch_vgemm_tn(s, (const dfd::bf16*)A, N, (const dfd::bf16*)B, K, M, N, K, slab, slab_floats,
+                                (float*)C, false);
+  }
+  dfd::set_error("vgemm: op must be 0..3", __FILE__, __LINE__);
+  return -1;
+  DFD_GUARD_END
+}
+
 int dfd_sgemm(void* stream, int ta, int tb, const float* A, int lda, const float* B, int ldb, float* C, int ldc, int M,
               int N, int K, float beta, const float* bias) {
   DFD_GUARD_BEGIN
@@ -623,6 +669,8 @@ int dfd_pw_conv_wgrad(void* stream, int dtype, const void* dY, const void* X, in
                       const float* scale, const float* shift, const float* gate, int rows_per_frame, float* slab,
                       int64_t slab_floats, float* dW, int accumulate) {
   DFD_GUARD_BEGIN
+  const dfd::Tuning tn = seam_snapshot();
+  const dfd::TuningScope ts(&tn);
   if (!pw_args_ok(dtype, M, N, K, pro_mode, scale, shift, gate, rows_per_frame)) return -1;
   if (!slab || slab_floats < (int64_t)N * K) { dfd::set_error("pw wgrad: slab smaller than N*K", __FILE__, __LINE__); return -1; }
   const dfd::Pro pro{scale, shift, gate, rows_per_frame, K};

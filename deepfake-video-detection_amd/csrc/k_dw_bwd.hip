@@ -32,19 +32,14 @@
 namespace dfd {
 
 // 1: fused (default); 0: the two kernels (dgrad, wgrad)
-static std::atomic<int64_t> g_dw_bwd_fused{1};
-int64_t set_dw_bwd_fused(int64_t v) { return g_dw_bwd_fused.exchange(v); }
-bool dw_bwd_fused_enabled() { return tune_or(TK_DW_BWD_FUSED, g_dw_bwd_fused.load(std::memory_order_relaxed)) != 0; }
+bool dw_bwd_fused_enabled() { return tune(TK_DW_BWD_FUSED) != 0; }
 // 1: the stride-1 blocks take dw_bwd1_kernel (k_dw_bwd1.hip) with both BN backward passes fused
-static std::atomic<int64_t> g_dw_bwd1{1};
-int64_t set_dw_bwd1(int64_t v) { return g_dw_bwd1.exchange(v); }
+
 bool dw_bwd1_enabled() {
-  return dw_bwd_fused_enabled() && tune_or(TK_DW_BWD1, g_dw_bwd1.load(std::memory_order_relaxed)) != 0;
+  return dw_bwd_fused_enabled() && tune(TK_DW_BWD1) != 0;
 }
 // 1: the stride-1 forward takes dw_fwd1_kernel (k_dw_fwd1.hip, channel pairs)
-static std::atomic<int64_t> g_dw_fwd1{1};
-int64_t set_dw_fwd1(int64_t v) { return g_dw_fwd1.exchange(v); }
-bool dw_fwd1_enabled() { return tune_or(TK_DW_FWD1, g_dw_fwd1.load(std::memory_order_relaxed)) != 0; }
+bool dw_fwd1_enabled() { return tune(TK_DW_FWD1) != 0; }
 
 template <int TH, int TW, int K, int S, int VW>
 struct DwB {

@@ -305,9 +305,7 @@ __global__ __launch_bounds__(256, OCC) void pw_gemm_kernel(const T* __restrict__
   }
 }
 
-// tile configurations (BM, BN, WN, D, OCC); g_gemm_tile forces one for experiments (-1 = auto)
-static std::atomic<int> g_gemm_tile{-1};
-int set_gemm_tile(int v) { return g_gemm_tile.exchange(v); }
+// tile configurations (BM, BN, WN, D, OCC); the gemm_tile knob forces one for experiments (-1 = auto)
 
 template <typename T, int MODE, bool ST, int EP, int BM, int BN, int WN, int D, int BK, int OCC>
 static void gemm_go(hipStream_t s, int gx_m, int ntn, size_t dyn, const T* A, const T* B, T* C, const T* R,
@@ -324,7 +322,7 @@ static int gemm_tiles(hipStream_t s, const T* A, const T* B, T* C, const T* R, c
   // Chosen per shape from tools/kbench on MI355X (tools/gemm_tiles.sh): one 128-wide N tile while
   // N <= 128 (the A prologue then runs once per row tile); 128x64 for narrow N; the 14x14 / 7x7
   // stages (few row tiles) want the small tiles for enough workgroups in flight.
-  int cfg = (int)tune_or(TK_GEMM_TILE, g_gemm_tile.load());
+  int cfg = (int)tune(TK_GEMM_TILE);
   if (cfg < 0 || cfg > 12) {
     if (N <= 64) cfg = 1;
     else if (N <= 128) cfg = 0;

@@ -39,8 +39,6 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 // Row threshold above which the streaming kernel takes a layer (below it the tiled kernel's
 // weight reuse wins); settable through dfd_set_tuning("stream_min_rows", v).
-static std::atomic<int64_t> g_stream_min_rows{40000};
-int64_t set_stream_min_rows(int64_t v) { return g_stream_min_rows.exchange(v); }
 
 template <int NB, int U>
 struct StreamTile {
@@ -334,7 +332,7 @@ static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, c
 // the caller uses the tiled kernel); -1: launch error
 int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
                      int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
-  if (M <= 0 || M < tune_or(TK_STREAM_MIN_ROWS, g_stream_min_rows.load(std::memory_order_relaxed)) || K > 256 || (N & 7) || (K & 7)) return 1;
+  if (M <= 0 || M < tune(TK_STREAM_MIN_ROWS) || K > 256 || (N & 7) || (K & 7)) return 1;
   const int nchunks = cdiv(N, 128);
   const int NB = cdiv(cdiv(N, nchunks), 16), KB = cdiv(K, 32);
   const bool st = stats != nullptr, rs = R != nullptr, bs = bias != nullptr;
@@ -626,7 +624,7 @@ static int wgs_launch(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, i
 // 0: launched; 1: not covered (the caller uses the tiled wgrad kernel); -1: launch error
 int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate) {
-  if (M <= 0 || M < tune_or(TK_STREAM_MIN_ROWS, g_stream_min_rows.load(std::memory_order_relaxed)) || (N & 7) || (K & 7)) return 1;
+  if (M <= 0 || M < tune(TK_STREAM_MIN_ROWS) || (N & 7) || (K & 7)) return 1;
 #define DFD_WGS(NBW_, KBW_, S_, MODE_) \
   return wgs_launch<NBW_, KBW_, S_, MODE_>(s, dY, X, M, N, K, pro, slab, slab_cap, dW, accumulate)
   if (pro_mode == PRO_NONE) {  // conv_pw (expansion): N = mid, K = cin;  Gram x^T x: N = K = cin

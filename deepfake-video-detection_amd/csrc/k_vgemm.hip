@@ -1,0 +1,306 @@
+// Large bf16 GEMMs of the ViT-B/16 trunk (DeepfakeModel, src/models.py:88-107, 222-291; timm
+// vit_base_patch16_224 restated in oracle/vit_cpu.py): every linear layer's forward and data
+// gradient, C[M][N] = A[M][K] . B[N][K]^T, and every weight gradient, W[P][Q] = sum_m X1[m][p] X2[m][q],
+// at M = images * 197 token rows (25,216 at the C5 batch of 128) and N, K, P, Q in {768, 2304, 3072}.
+//
+// gfx950 design (cdna_hip_programming.md section 5: the 256^2 LDS-DMA template):
+//   * 256 x 256 output tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 each),
+//     v_mfma_f32_16x16x32_bf16, fp32 accumulators (128 per lane), one workgroup per CU;
+//   * operands move HBM -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR
+//     staging), 64-deep K-steps double-buffered (2 x 64 KiB): the next K-step's DMA is in flight
+//     while the current one's fragments are read and multiplied;
+//   * bank-conflict-free fragment reads through XOR swizzles applied on the DMA SOURCE address
+//     (the LDS image of an LDS-DMA is lane-linear): NT operands are [rows][64 k] images (128-B rows)
+//     read with ds_read_b128, chunk ^ ((row >> 1) & 7); the weight-gradient operands are [64 m][256]
+//     images (512-B rows) read TRANSPOSED with ds_read_b64_tr_b16, chunk ^ (2 (m & 3) + 8 ((m >> 3) & 1));
+//   * XCD-aware tile order (tiles that share an A row panel run on one XCD's L2);
+//   * epilogue through LDS in two 128-row passes: row-contiguous 16-B stores, with the bias, the
+//     residual add, GELU (fc1 stores both Z and gelu(Z)) or the GELU derivative (fc2's data
+//     gradient) applied in fp32 and rounded once;
+//   * weight gradients split over M into fp32 slabs (one dispatch wave of workgroups), summed in a
+//     fixed order (launch_reduce_slabs): the step stays bit-reproducible.
+#include "kernels.h"
+#include "vit.h"
+
+namespace dfd {
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef __attribute__((address_space(3))) s16x4* lds_s4p;
+
+constexpr int VT = 256;                       // output tile edge
+constexpr int VK = 64;                        // K-step (NT) / m-step (TN)
+constexpr int VTILE = VT * VK * 2;            // 32 KiB: one operand's K-step image
+constexpr int EPS = VT + 4;                   // fp32 epilogue row stride (floats): conflict-free ds_write_b32
+constexpr int EPI_BYTES = 128 * EPS * 4;      // one 128-row pass
+constexpr int VLDS = 4 * VTILE > EPI_BYTES ? 4 * VTILE : EPI_BYTES;
+
+__device__ const uint4 g_vzero[32] = {};      // 512 B of zeros: the DMA source of rows past the end (TN)
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---------------------------------------------------------------- NT: C = A . B^T
+// One K-step image of an operand: [256 rows][64 k] bf16, 128-B rows, chunk (16 B) c of row r at
+// slot c ^ ((r >> 1) & 7).  Wave w fills rows 32w .. 32w+31 with 4 DMA instructions of 8 rows.
+__device__ __forceinline__ void stage_nt(const bf16* __restrict__ G, int64_t ld, int row0, int rows, int k0, char* img,
+                                         int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = w * 4 + i;
+    const int r = 8 * q + (lane >> 3);
+    const int gc = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(row0 + r, rows - 1);  // rows past the end: any valid row (their outputs are not stored)
+    const bf16* src = G + (int64_t)gr * ld + k0 + gc * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_vp)(img + q * 1024), 16, 0, 0);
+  }
+}
+
+// fragment of rows base .. base+15 (base % 16 == 0) at k-chunk 4s + (lane >> 4)
+__device__ __forceinline__ s16x8 frag_nt(const char* img, int base, int s, int lane) {
+  const int r = base + (lane & 15);
+  const int c = (4 * s + (lane >> 4)) ^ ((lane & 15) >> 1);
+  return *reinterpret_cast<const s16x8*>(img + r * 128 + (c << 4));
+}
+
+// ---------------------------------------------------------------- TN: W = X1^T . X2
+// One m-step image of an operand: [64 m][256 cols] bf16, 512-B rows, chunk c of row m at slot
+// c ^ (2 (m & 3) + 8 ((m >> 3) & 1)).  Wave w fills rows 8w .. 8w+7 (4 DMA instructions of 2 rows).
+__device__ __forceinline__ int tn_swz(int m) { return 2 * (m & 3) + 8 * ((m >> 3) & 1); }
+
+__device__ __forceinline__ void stage_tn(const bf16* __restrict__ G, int64_t ld, int m0, int m_end, int c0, char* img,
+                                         int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = w * 4 + i;
+    const int m = 2 * q + (lane >> 5);
+    const int gc = (lane & 31) ^ tn_swz(m);
+    const bf16* src = m0 + m < m_end ? G + (int64_t)(m0 + m) * ld + c0 + gc * 8
+                                     : reinterpret_cast<const bf16*>(g_vzero) + gc * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_vp)(img + q * 1024), 16, 0, 0);
+  }
+}
+
+// MFMA operand of output rows base .. base+15 (the image's columns) at k = 32 s + 8 (lane >> 4) + j:
+// two transposed reads of 4 m-rows x 16 columns each (ds_read_b64_tr_b16)
+__device__ __forceinline__ s16x8 frag_tn(const char* img, int base, int s, int lane) {
+  const int h = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int n = base + 4 * pp;
+  const int c = n >> 3, half = (n >> 2) & 1;
+  const int m1 = 32 * s + 8 * h + qq, m2 = m1 + 4;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4p)(img + m1 * 512 + ((c ^ tn_swz(m1)) << 4) + half * 8));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4p)(img + m2 * 512 + ((c ^ tn_swz(m2)) << 4) + half * 8));
+  return s16x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+}
+
+// ---------------------------------------------------------------- shared pieces
+struct Acc {
+  f32x4 v[8][4];
+};
+
+template <bool TN>
+__device__ __forceinline__ void mma_step(const char* Ai, const char* Bi, int wm, int wn, int lane, Acc& acc) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    s16x8 af[8], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = TN ? frag_tn(Ai, wm * 128 + 16 * i, s, lane) : frag_nt(Ai, wm * 128 + 16 * i, s, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = TN ? frag_tn(Bi, wn * 64 + 16 * j, s, lane) : frag_nt(Bi, wn * 64 + 16 * j, s, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc.v[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc.v[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// the accumulators of waves with wm == pass into the [128][EPS] fp32 staging image
+__device__ __forceinline__ void epi_put(float* E, const Acc& acc, int wn, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) E[(16 * i + 4 * (lane >> 4) + e) * EPS + wn * 64 + 16 * j + (lane & 15)] = acc.v[i][j][e];
+}
+
+__device__ __forceinline__ void st8bf(bf16* p, const float (&v)[8]) { st8(p, v); }
+
+// ---------------------------------------------------------------- kernels
+template <int EP>
+__global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[VLDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = uni(tid >> 6), wm = w >> 2, wn = w & 3;
+  const int L = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+  const int tm = L / a.tiles_n, tn = L - tm * a.tiles_n;
+  const int row0 = tm * VT, col0 = tn * VT;
+  Acc acc;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc.v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = a.K / VK;
+  stage_nt(a.A, a.lda, row0, a.M, 0, smem, w, lane);
+  stage_nt(a.B, a.ldb, col0, a.N, 0, smem + VTILE, w, lane);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * 2 * VTILE;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * 2 * VTILE;
+      stage_nt(a.A, a.lda, row0, a.M, (kt + 1) * VK, nxt, w, lane);
+      stage_nt(a.B, a.ldb, col0, a.N, (kt + 1) * VK, nxt + VTILE, w, lane);
+    }
+    mma_step<false>(cur, cur + VTILE, wm, wn, lane, acc);
+    __syncthreads();  // this K-step's reads done everywhere; the next one's DMA landed (vmcnt(0))
+  }
+  // epilogue: two passes of 128 rows through LDS
+  float* E = reinterpret_cast<float*>(smem);
+  const int v = tid & 31, rsub = tid >> 5;  // 8-column vector, row within a 16-row sweep
+  const int c = col0 + 8 * v;
+  float bias[8];
+  if constexpr ((EP & VG_BIAS) != 0) ld8f(a.bias + c, bias);
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) epi_put(E, acc, wn, lane);
+    __syncthreads();
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int rl = it * 16 + rsub;
+      const int row = row0 + pass * 128 + rl;
+      if (row < a.M) {
+        float o[8];
+        const float4 x0 = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v);
+        const float4 x1 = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v + 4);
+        o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w; o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
+        if constexpr ((EP & VG_BIAS) != 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += bias[j];
+        }
+        if constexpr ((EP & VG_RESID) != 0) {
+          float r[8];
+          ld8(a.R + (int64_t)row * a.ldc + c, r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        }
+        if constexpr ((EP & VG_DGELU) != 0) {
+          float z[8];
+          ld8(a.Z + (int64_t)row * a.ldc + c, z);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] *= dgeluf_(z[j]);
+        }
+        st8bf(a.C + (int64_t)row * a.ldc + c, o);
+        if constexpr ((EP & VG_GELU2) != 0) {  // gelu of the stored (rounded) pre-activation
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = geluf_(Tr<bf16>::round(o[j]));
+          st8bf(a.G + (int64_t)row * a.ldc + c, o);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[VLDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = uni(tid >> 6), wm = w >> 2, wn = w & 3;
+  const int tiles = a.tiles_p * a.tiles_q;
+  const int L = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
+  const int split = L / tiles, t = L - split * tiles;
+  const int tp = t / a.tiles_q, tq = t - tp * a.tiles_q;
+  const int p0 = tp * VT, q0 = tq * VT;
+  const int m_begin = split * a.mchunk, m_end = min(a.M, m_begin + a.mchunk);
+  Acc acc;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc.v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = m_end > m_begin ? (m_end - m_begin + VK - 1) / VK : 0;
+  if (nk > 0) {
+    stage_tn(a.X1, a.ld1, m_begin, m_end, p0, smem, w, lane);
+    stage_tn(a.X2, a.ld2, m_begin, m_end, q0, smem + VTILE, w, lane);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * 2 * VTILE;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * 2 * VTILE;
+      stage_tn(a.X1, a.ld1, m_begin + (kt + 1) * VK, m_end, p0, nxt, w, lane);
+      stage_tn(a.X2, a.ld2, m_begin + (kt + 1) * VK, m_end, q0, nxt + VTILE, w, lane);
+    }
+    mma_step<true>(cur, cur + VTILE, wm, wn, lane, acc);
+    __syncthreads();
+  }
+  float* E = reinterpret_cast<float*>(smem);
+  const int v = tid & 31, rsub = tid >> 5;
+  float* out = a.slab + (int64_t)split * a.P * a.Q;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wm == pass) epi_put(E, acc, wn, lane);
+    __syncthreads();
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int rl = it * 16 + rsub;
+      const int p = p0 + pass * 128 + rl;
+      float* dst = out + (int64_t)p * a.Q + q0 + 8 * v;
+      *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v);
+      *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v + 4);
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+bool vgemm_nt_covers(int64_t M, int N, int K) {
+  return M > 0 && M < (1ll << 31) && N % VT == 0 && K % VK == 0 && K > 0;
+}
+bool vgemm_tn_covers(int64_t M, int P, int Q) { return M > 0 && M < (1ll << 31) && P % VT == 0 && Q % VT == 0; }
+
+int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
+  if (!vgemm_nt_covers(a0.M, a0.N, a0.K)) { set_error("vgemm: shape not covered", __FILE__, __LINE__); return -1; }
+  VgemmArgs a = a0;
+  a.tiles_n = a.N / VT;
+  const int tiles = cdiv(a.M, VT) * a.tiles_n;
+  switch (ep) {
+#define DFD_VG(E) case E: hipLaunchKernelGGL((vgemm_nt_kernel<E>), dim3(tiles), dim3(512), 0, s, a); break;
+    DFD_VG(0) DFD_VG(VG_BIAS) DFD_VG(VG_BIAS | VG_RESID) DFD_VG(VG_BIAS | VG_GELU2) DFD_VG(VG_DGELU)
+#undef DFD_VG
+    default: set_error("vgemm: epilogue not instantiated", __FILE__, __LINE__); return -1;
+  }
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap) {
+  const int tiles = (P / VT) * (Q / VT);
+  int splits = std::max(1, 256 / std::max(1, tiles));  // one dispatch wave of workgroups
+  splits = (int)std::min<int64_t>(splits, cdiv64(M, 4 * VK));  // at least 4 m-steps per split
+  splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / ((int64_t)P * Q)));
+  return splits;
+}
+
+int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, int64_t ld2, int64_t M, int P, int Q,
+                    float* slab, int64_t slab_cap, float* W, bool accumulate) {
+  if (!vgemm_tn_covers(M, P, Q)) { set_error("vgemm_tn: shape not covered", __FILE__, __LINE__); return -1; }
+  if ((int64_t)P * Q > slab_cap) { set_error("vgemm_tn: slab too small", __FILE__, __LINE__); return -1; }
+  VgemmTnArgs a{};
+  a.X1 = X1; a.ld1 = ld1; a.X2 = X2; a.ld2 = ld2; a.M = (int)M; a.P = P; a.Q = Q;
+  a.tiles_p = P / VT; a.tiles_q = Q / VT;
+  int splits = vgemm_tn_splits(M, P, Q, slab_cap);
+  a.mchunk = (int)(cdiv64(cdiv64(M, splits), VK) * VK);
+  splits = (int)cdiv64(M, a.mchunk);
+  a.slab = slab;
+  hipLaunchKernelGGL(vgemm_tn_kernel, dim3(splits * a.tiles_p * a.tiles_q), dim3(512), 0, s, a);
+  DFD_HIP_CHECK(hipGetLastError());
+  return launch_reduce_slabs(s, slab, splits, (int64_t)P * Q, W, accumulate);
+}
+
+}  // namespace dfd

@@ -37,11 +37,12 @@ int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* y3, const float* c
 int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* r, const bf16* w1t, const bf16* q,
                        const float* bv, bf16* dx, int64_t M, int mid, int cin, float* slab, int64_t slab_cap, float* T,
                        float* G, float* cs);
-// rows threshold of the streaming kernels (returns the previous value)
-// Kernel-selection knobs.  Process-wide defaults (set_* below, dfd_set_tuning), overridden per plan:
-// a plan's forward/backward installs its own Tuning for the enqueuing thread (TuningScope), so
-// concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
-// training step -- never read each other's knobs.
+// Kernel-selection knobs.  No process-wide mutable state is consulted on a model path: every knob
+// has a compile-time default (tune_default), a plan's forward/backward installs the plan's own
+// overrides (dfd_b0_plan_set_tuning) for the enqueuing thread (TuningScope), and the kernel test
+// seams (dfd_pw_conv, dfd_pw_conv_wgrad) install a snapshot of the seam overrides of dfd_set_tuning.
+// Concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
+// training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
                TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
@@ -49,18 +50,21 @@ struct Tuning {
   int64_t v[TK_COUNT];
   Tuning() { for (auto& x : v) x = kTuneUnset; }
 };
-int64_t tune_override(TuneKey k);  // the calling thread's plan override, or kTuneUnset
-inline int64_t tune_or(TuneKey k, int64_t dflt) {
+// defaults: streaming 1x1 kernels from 40,000 rows; BN-folded conv_pw backward from 100,000 rows;
+// fused depthwise backward / channel-pair kernels on; tiled-GEMM config automatic (-1); weight
+// gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1};
+extern const char* const kTuneNames[TK_COUNT];
+int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
+inline int64_t tune(TuneKey k) {
   const int64_t o = tune_override(k);
-  return o == kTuneUnset ? dflt : o;
+  return o == kTuneUnset ? kTuneDefault[k] : o;
 }
 struct TuningScope {
   const Tuning* prev;
   explicit TuningScope(const Tuning* t);
   ~TuningScope();
 };
-int64_t set_stream_min_rows(int64_t v);
-int set_gemm_tile(int v);  // tiled pw GEMM: force tile config 0/1/2, -1 = auto (returns previous)
 // Transformer form of the same kernel: C = pro(A) * B^T  (+bias[n]) (+R) (* gelu'(Z) elementwise),
 // pro_mode PRO_NONE or PRO_GELU; epi a mask of GemmEpi.
 enum GemmEpi { EPI_RESID = 1, EPI_BIAS = 2, EPI_DGELU = 4 };
@@ -137,8 +141,6 @@ struct AttnArgs {
 };
 bool attn_supported(int nt, int head_dim);
 // ViT bf16 GEMM backend (vit.cpp): bit 0 own weight-gradient kernels, bit 1 own linears; previous value
-int64_t set_vit_gemm(int64_t v);
-int64_t set_vit_wsplit(int64_t v);  // M-splits of the ViT's library weight gradients (1 = single call)
 int launch_attn_fwd(hipStream_t s, const AttnArgs& a);
 int launch_attn_bwd(hipStream_t s, const AttnArgs& a);
 
@@ -150,6 +152,7 @@ template <typename T>
 int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, const float* bias, int relu,
                    const RnConvGeom& g, int64_t M, int N, int K);
 // plain library GEMMs through hipBLASLt (blaslt.cpp): C = A . B^T + bias (+ R); dW (+)= dY^T . X
+int64_t blaslt_calls();  // library GEMM calls so far (the measurement seam only)
 int blaslt_linear(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
                   int N, int K);
 int blaslt_wgrad(hipStream_t s, const bf16* dY, const bf16* X, float* dW, int64_t M, int N, int K, bool accumulate);
@@ -189,7 +192,6 @@ template <typename T>
 int launch_dw_bwd(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T* out, const T* Yp,
                   const BnBwdIn* bn, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
                   bool accumulate);
-int64_t set_dw_bwd_fused(int64_t v);
 bool dw_bwd_fused_enabled();
 // stride-1 depthwise backward with the BN2 (after the conv) and BN1 (before it) backward fused,
 // k_dw_bwd1.hip: 0 launched, 1 not covered (BN2 apply + launch_dw_bwd instead)
@@ -198,7 +200,6 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
                    const float* sc2, const float* sh2, const float* coef2, const float* w, const T* Y1,
                    const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab, int64_t slab_cap, float* dW,
                    bool accumulate);
-int64_t set_dw_bwd1(int64_t v);
 bool dw_bwd1_enabled();
 bool dw_bwd1_covers(const DwGeom& g);  // a tile configuration exists and the knob is on
 // the stride-2 counterpart, k_dw_bwd2.hip (same contract; rides the dw_bwd1 knob)
@@ -212,7 +213,6 @@ bool dw_bwd2_covers(const DwGeom& g);
 template <typename T>
 int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                 int* stat_rows);
-int64_t set_dw_fwd1(int64_t v);
 bool dw_fwd1_enabled();
 
 // ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------

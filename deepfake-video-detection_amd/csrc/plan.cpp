@@ -331,13 +331,12 @@ inline bool probe_hit(const Plan& p, int kind, const Block* b) {
   } while (0)
 #define PROBED(KIND, BLK, EXPR) PROBED_ON(KIND, BLK, s, EXPR)
 
-// the fused 7x7-stage MBConv forward (k_mbconv7.hip) for the bf16 plan: 0 off (default), 1 on.
-// Off by default: measured 394 us per block (training) against ~135 us for the unfused launches
+// the fused 7x7-stage MBConv forward (k_mbconv7.hip) for the bf16 plan: knob mbconv7, 0 off (default),
+// 1 on.  Off by default: measured 394 us per block (training) against ~135 us for the unfused launches
 // (six grid barriers at ~14 us each, per-frame weight re-reads from L2).
-std::atomic<int64_t> g_mbconv7{0};
 // blocks of the 7x7 stages that run as one fused launch (k_mbconv7.hip) in the bf16 forward
 static bool block_fused7(const Plan& p, const Block& b) {
-  return !b.ds && b.o_s2 >= 0 && tune_or(TK_MBCONV7, g_mbconv7.load(std::memory_order_relaxed)) != 0 &&
+  return !b.ds && b.o_s2 >= 0 && tune(TK_MBCONV7) != 0 &&
          mbconv7_supported(p.frames, b.hin, b.win, b.cin, b.mid, b.cout, b.rd, b.k, b.s);
 }
 
@@ -452,21 +451,18 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   return 0;
 }
 
-// blocks with at least this many conv_pw rows take the BN-folded backward (bn_fold_pw); below it
-// the extra small passes over x cost more than the expanded-tensor passes they save
-// (dfd_set_tuning("fold_min_rows", v); tests force both paths)
-std::atomic<int64_t> g_fold_min_rows{100000};
-// 1x1-conv weight gradients on the plan's second stream (dfd_set_tuning("wgrad_stream", v): 0 off,
-// 1 every block, N > 1 blocks with >= N gradient rows).  Off by default: measured 0.17-0.26 ms/step
-// SLOWER at every threshold (in-process A/B, tools/ab_bench.py) -- the persistent, occupancy-sized
-// depthwise kernels of the main chain lose resident workgroup slots to the concurrent gradients
-std::atomic<int64_t> g_wgrad_stream{0};
-// the projection backward of the bf16 plan as one fused launch (k_pwl_bwd.hip: data gradient, weight
-// gradient and the SE + BN2 backward sums; dfd_set_tuning("pwl_fused", 0) runs the three unfused ones)
-std::atomic<int64_t> g_pwl_fused{1};
-// the fold path's conv_pw backward of the bf16 plan as one fused launch (k_pw_fold_bwd.hip: x . Q,
-// the data gradient and the three weight-gradient products; dfd_set_tuning("fold_fused", 0): unfused)
-std::atomic<int64_t> g_fold_fused{1};
+// Plan knobs (per plan, dfd_b0_plan_set_tuning; defaults in kTuneDefault):
+// fold_min_rows: blocks with at least this many conv_pw rows take the BN-folded backward
+//   (bn_fold_pw); below it the extra small passes over x cost more than the expanded-tensor passes
+//   they save (tests force both paths);
+// wgrad_stream: 1x1-conv weight gradients on the plan's second stream (0 off, 1 every block, N > 1
+//   blocks with >= N gradient rows).  Off by default: measured 0.17-0.26 ms/step SLOWER at every
+//   threshold (in-process A/B, tools/ab_bench.py) -- the persistent, occupancy-sized depthwise kernels
+//   of the main chain lose resident workgroup slots to the concurrent gradients;
+// pwl_fused: the projection backward of the bf16 plan as one fused launch (k_pwl_bwd.hip: data
+//   gradient, weight gradient and the SE + BN2 backward sums; 0 runs the three unfused ones);
+// fold_fused: the fold path's conv_pw backward of the bf16 plan as one fused launch
+//   (k_pw_fold_bwd.hip: x . Q, the data gradient and the three weight-gradient products; 0: unfused).
 
 template <typename T>
 int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& ifmt, const float* dfeat,
@@ -516,7 +512,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
   // reductions from both streams are batched on s (SlabDefer joins both ways at every flush).
   // knob: 0 off; 1 every block; N > 1 only blocks whose gradient rows reach N (the cross-stream
   // waits cost a few us each: small late-stage gradients are not worth them)
-  const int64_t ws_min = tune_or(TK_WGRAD_STREAM, g_wgrad_stream.load(std::memory_order_relaxed));
+  const int64_t ws_min = tune(TK_WGRAD_STREAM);
   hipStream_t w_aux = s;
   if (ws_min != 0) {
     DFD_TRY(aux_init(p, s));
@@ -586,7 +582,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
         DFD_TRY(join(p.ev[1], gs_busy));  // the previous conv_pwl weight gradient is done with o_gs
         int hs = 1, pf = 1;
-        const bool fpwl = sizeof(T) == 2 && tune_or(TK_PWL_FUSED, g_pwl_fused.load(std::memory_order_relaxed)) != 0 &&
+        const bool fpwl = sizeof(T) == 2 && tune(TK_PWL_FUSED) != 0 &&
                           pwl_bwd_covers(p.frames, hwo, b.cout, b.mid);
         // the BN3 backward applied in the fused kernel's staging pays where the projection is 16 wide
         // (blocks.0.0: +12 us in the kernel against a 49 us apply pass); at 24 wide the kernel's
@@ -697,7 +693,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                                       acc != 0)));
         }
         p.pending_rows = rows;
-        if (!b.ds && Min < tune_or(TK_FOLD_MIN_ROWS, g_fold_min_rows.load(std::memory_order_relaxed))) {
+        if (!b.ds && Min < tune(TK_FOLD_MIN_ROWS)) {
           BnBwdIn i1{};
           i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = false;
           DFD_TRY(bwd_bn_from_stats(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1), p.pending_rows));
@@ -723,7 +719,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                        r.f(p.o_bv)));
           DFD_TRY(join(p.ev[1], gs_busy));  // the conv_pwl weight gradient is done with o_gs
           int ff = 1;
-          if (sizeof(T) == 2 && tune_or(TK_FOLD_FUSED, g_fold_fused.load(std::memory_order_relaxed)) != 0) {
+          if (sizeof(T) == 2 && tune(TK_FOLD_FUSED) != 0) {
             // x . Q, the data gradient and the partial products g^T x, x^T x, 1^T x in one pass
             // (k_pw_fold_bwd.hip); their three slab reductions as ONE batched launch
             if constexpr (sizeof(T) == 2) {
@@ -803,11 +799,6 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
 
 }  // namespace
 
-int64_t set_fold_min_rows(int64_t v) { return g_fold_min_rows.exchange(v); }
-int64_t set_wgrad_stream(int64_t v) { return g_wgrad_stream.exchange(v); }
-int64_t set_mbconv7(int64_t v) { return g_mbconv7.exchange(v); }
-int64_t set_pwl_fused(int64_t v) { return g_pwl_fused.exchange(v); }
-int64_t set_fold_fused(int64_t v) { return g_fold_fused.exchange(v); }
 int plan_fused7_blocks(const Plan& p) {
   if (p.dtype != 1) return 0;  // bf16 plans only
   const TuningScope ts(&p.tune);
@@ -817,6 +808,8 @@ int plan_fused7_blocks(const Plan& p) {
 }
 
 
+const char* const kTuneNames[TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile", "dw_bwd1",
+                                          "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused"};
 static thread_local const Tuning* t_tune = nullptr;
 int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tune) { t_tune = t; }

@@ -102,14 +102,6 @@ int plan_backward_x(Plan& p, hipStream_t s, const void* x, const int64_t* xs, co
 // gradients are final once the segment has run.
 void plan_segment_range(const Plan& p, int seg, int* lo, int* hi);
 constexpr int kNumSegments = 9;
-// rows threshold of the BN-folded conv_pw backward (returns the previous value)
-int64_t set_fold_min_rows(int64_t v);
-// 1x1-conv weight gradients on a second stream, overlapping the backward's main chain (0 off -- the
-// default --, 1 every block, N > 1 blocks with >= N gradient rows)
-int64_t set_wgrad_stream(int64_t v);
-int64_t set_mbconv7(int64_t v);
-int64_t set_pwl_fused(int64_t v);
-int64_t set_fold_fused(int64_t v);
 // number of blocks the bf16 forward runs through the fused 7x7 MBConv kernel (0: none)
 int plan_fused7_blocks(const Plan& p);
 // static topology (shape-independent)

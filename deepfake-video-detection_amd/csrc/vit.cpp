@@ -7,11 +7,13 @@
 // (bf16 or fp32), fp32 accumulation everywhere.  Per block the forward keeps what the backward
 // reads: block input x, LN1 output h1, qkv [rows][2304], softmax probabilities P
 // [images*12*197][200] (rows padded to 200 for 16-B vector reads), attention output O, the
-// post-attention stream xm, LN2 output h2 and the fc1 pre-activation Z [rows][3072] (GELU is
-// re-applied by fc2's operand prologue and differentiated in the dgrad epilogue).  The linear
-// layers are MFMA GEMMs (launch_tf_gemm: bias / residual / GELU fused), weights cast per step
-// to T in both [out][in] (forward) and [in][out] (dgrad) layouts; weight gradients are
-// split-M slab GEMMs reduced in a fixed order, so a step is bit-reproducible.
+// post-attention stream xm, LN2 output h2 and the fc1 pre-activation Z [rows][3072] (bf16: fc1's
+// epilogue also stores G = gelu(Z), read by fc2 and by its weight gradient; fp32: GELU is re-applied
+// by fc2's operand prologue).  The bf16 linear layers are the LDS-DMA 256 x 256 MFMA GEMMs of
+// k_vgemm.hip (bias / residual / GELU / GELU-derivative epilogues), the fp32 parity mode and the
+// shapes they do not cover run launch_tf_gemm (k_gemm.hip); weights are cast per step to T in both
+// [out][in] (forward) and [in][out] (dgrad) layouts; weight gradients are split-M slab GEMMs
+// reduced in a fixed order, so a step is bit-reproducible.  No library GEMM.
 #include "../../include/dfd_hip.h"
 
 #include <atomic>
@@ -48,11 +50,11 @@ int vit_check(const VitDims& d) {
 // byte layout of the trunk workspace (kept forward -> backward) and backward scratch
 struct VitLayout {
   struct Blk {
-    int64_t x, h1, mu1, rs1, qkv, P, O, xm, h2, mu2, rs2, Z;
+    int64_t x, h1, mu1, rs1, qkv, P, O, xm, h2, mu2, rs2, Z, G;
     int64_t wqkv, wqkvT, wp, wpT, w1, w1T, w2, w2T;
   };
   std::vector<Blk> blk;
-  int64_t wpe, ape, pe, xfin, mu_f, rs_f, S, G, total;
+  int64_t wpe, ape, pe, xfin, mu_f, rs_f, S, total;
   // scratch
   int64_t dx, dxm, dh, dZ, dqkv, dO, dS, part, slab, dpe, stotal;
   int64_t part_cap, slab_cap;
@@ -96,12 +98,12 @@ VitLayout vit_layout(const VitDims& d) {
     b.mu2 = take(4 * M);
     b.rs2 = take(4 * M);
     b.Z = take(es * M * FF);
+    b.G = d.dtype == 1 ? take(es * M * FF) : 0;  // gelu(Z), written by fc1's epilogue (bf16)
   }
   L.xfin = take(es * M * D);
   L.mu_f = take(4LL * d.images);
   L.rs_f = take(4LL * d.images);
   L.S = take(es * SR * SLD);
-  L.G = d.dtype == 1 ? take(es * M * FF) : 0;  // gelu(Z) of one block (bf16 library-GEMM path)
   L.total = off;
   // scratch
   off = 0;
@@ -169,31 +171,32 @@ inline AttnArgs attn_args(int images, int nt, const T* qkv, T* O, float* lse) {
   return a;
 }
 
-// Which GEMMs of the bf16 mode run on the repo's own MFMA kernels (k_gemm.hip) instead of hipBLASLt:
-// bit 0 the weight gradients (launch_pw_wgrad: M-split, deterministic slabs), bit 1 the linears
-// (launch_tf_gemm, GELU fused as prologue / derivative epilogue).  The fp32 parity mode always uses
-// the k_gemm.hip kernels.
-std::atomic<int64_t> g_vit_gemm{0};
-// M-splits of the library weight gradients (batched call into slabs + ordered slab sum); 1 = one call
-std::atomic<int64_t> g_vit_wsplit{4};
-template <typename T> inline bool own_lin() { return sizeof(T) == 4 || (g_vit_gemm.load(std::memory_order_relaxed) & 2); }
-template <typename T> inline bool own_wgrad() { return sizeof(T) == 4 || (g_vit_gemm.load(std::memory_order_relaxed) & 1); }
-
-// C[M][N] = A . B^T + bias (+ R)
+// C[M][N] = A . B^T (+ bias) (+ R), epi a mask of VgEpi (G: gelu(C) for VG_GELU2; Z: VG_DGELU)
 template <typename T>
-int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N, int K) {
-  if constexpr (sizeof(T) == 2)
-    if (!own_lin<T>()) return blaslt_linear(s, A, B, C, R, bias, M, N, K);
-  return launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE,
-                           (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0));
+int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N, int K,
+        int epi_extra = 0, const T* Z = nullptr, T* G = nullptr) {
+  const int epi = (bias ? VG_BIAS : 0) | (R ? VG_RESID : 0) | epi_extra;
+  if constexpr (sizeof(T) == 2) {
+    if (vgemm_nt_covers(M, N, K)) {
+      VgemmArgs a{};
+      a.A = A; a.B = B; a.C = C; a.R = R; a.bias = bias; a.Z = Z; a.G = G;
+      a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
+      return launch_vgemm_nt(s, a, epi);
+    }
+    if (epi_extra & VG_GELU2) {  // uncovered shape: Z, then G = gelu(Z) as its own pass
+      DFD_TRY(launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE,
+                                (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0)));
+      return launch_gelu(s, C, G, M * N, false);
+    }
+  }
+  return launch_tf_gemm<T>(s, A, B, C, R, bias, Z, M, N, K, PRO_NONE,
+                           (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0) | ((epi_extra & VG_DGELU) ? EPI_DGELU : 0));
 }
 // dW[N][K] = dY^T . X
 template <typename T>
 int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float* slab, int64_t slab_cap, float* dW) {
   if constexpr (sizeof(T) == 2)
-    if (!own_wgrad<T>())
-      return blaslt_wgrad_split(s, dY, X, dW, M, N, K, (int)g_vit_wsplit.load(std::memory_order_relaxed), slab,
-                                slab_cap);
+    if (vgemm_tn_covers(M, N, K)) return launch_vgemm_tn(s, dY, N, X, K, M, N, K, slab, slab_cap, dW, false);
   Pro none{};
   return launch_pw_wgrad<T>(s, dY, X, M, N, K, PRO_NONE, none, slab, slab_cap, dW, false);
 }
@@ -231,11 +234,11 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     DFD_TRY(lin<T>(s, w.at(b.O), w.at(b.wp), w.at(b.xm), w.at(b.x), q[5], M, D, D));
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.xm), D, q[6], q[7], w.at(b.h2), D, w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), M, D, LN_EPS)));
-    DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D));
-    if (!own_lin<T>()) {  // gelu(Z) materialised once for the library GEMM (bf16 only)
-      if constexpr (sizeof(T) == 2) DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));
-      DFD_TRY(lin<T>(s, w.at(L.G), w.at(b.w2), xnext, w.at(b.xm), q[11], M, D, FF));
-    } else {
+    if constexpr (sizeof(T) == 2) {  // fc1 stores Z and G = gelu(Z); fc2 reads G
+      DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D, VG_GELU2, nullptr, w.at(b.G)));
+      DFD_TRY(lin<T>(s, w.at(b.G), w.at(b.w2), xnext, w.at(b.xm), q[11], M, D, FF));
+    } else {  // fp32: GELU re-applied in fc2's operand prologue
+      DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D));
       DFD_TRY(launch_tf_gemm<T>(s, w.at(b.Z), w.at(b.w2), xnext, w.at(b.xm), q[11], nullptr, M, D, FF, PRO_GELU,
                                 EPI_BIAS | EPI_RESID));
     }
@@ -276,17 +279,11 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     T* dO = sc.at(L.dO);
     T* dS = sc.at(L.dS);
     // ---- MLP: dZ = (dx W2) * gelu'(Z); dW2 = dx^T gelu(Z); dh2 = dZ W1 ----
-    if (own_lin<T>()) {
-      DFD_TRY(launch_tf_gemm<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, w.at(b.Z), M, FF, D, PRO_NONE, EPI_DGELU));
+    DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D, VG_DGELU, w.at(b.Z)));
+    if constexpr (sizeof(T) == 2) {  // G = gelu(Z) kept by the forward
+      DFD_TRY(wgrad<T>(s, dx, w.at(b.G), M, D, FF, slab, L.slab_cap, g[10]));
     } else {
-      DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D));
-      if constexpr (sizeof(T) == 2) DFD_TRY(launch_gelu(s, w.at(b.Z), dZ, M * FF, true));   // dZ *= gelu'(Z)
-    }
-    if (own_wgrad<T>()) {
       DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
-    } else {
-      if constexpr (sizeof(T) == 2) DFD_TRY(launch_gelu(s, w.at(b.Z), w.at(L.G), M * FF, false));  // gelu(Z) for dW2
-      DFD_TRY(wgrad<T>(s, dx, w.at(L.G), M, D, FF, slab, L.slab_cap, g[10]));
     }
     DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
     DFD_TRY(lin<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, M, D, FF));
@@ -460,8 +457,6 @@ int head_check(const HeadDims& h) {
 
 }  // namespace
 
-int64_t set_vit_gemm(int64_t v) { return g_vit_gemm.exchange(v); }
-int64_t set_vit_wsplit(int64_t v) { return g_vit_wsplit.exchange(v); }
 }  // namespace dfd
 
 using dfd::VitDims;

@@ -70,6 +70,35 @@ int launch_node_mean_bwd(hipStream_t s, const float* dG, int B, int N, int D, fl
 
 int launch_gelu(hipStream_t s, const bf16* Z, bf16* out, int64_t n, bool backward);
 
+// The large bf16 GEMMs of the trunk (k_vgemm.hip): 256 x 256 tiles, LDS-DMA double buffering.
+// NT: C[M][N] = A[M][K] . B[N][K]^T with the epilogue flags below (fp32, rounded once);
+// TN: W[P][Q] = sum_m X1[m][p] X2[m][q] (fp32, split over m into slabs summed in a fixed order).
+enum VgEpi { VG_BIAS = 1, VG_RESID = 2, VG_GELU2 = 4 /* C = Z, G = gelu(Z) */, VG_DGELU = 8 /* C *= gelu'(Z) */ };
+struct VgemmArgs {
+  const bf16* A;
+  const bf16* B;
+  bf16* C;
+  const bf16* R;      // residual [M][ldc] (VG_RESID)
+  const float* bias;  // [N] (VG_BIAS)
+  const bf16* Z;      // pre-activation [M][ldc] (VG_DGELU)
+  bf16* G;            // gelu(C) [M][ldc] (VG_GELU2)
+  int64_t lda, ldb, ldc;
+  int M, N, K, tiles_n;
+};
+struct VgemmTnArgs {
+  const bf16* X1;
+  const bf16* X2;
+  float* slab;
+  int64_t ld1, ld2;
+  int M, P, Q, tiles_p, tiles_q, mchunk;
+};
+bool vgemm_nt_covers(int64_t M, int N, int K);
+bool vgemm_tn_covers(int64_t M, int P, int Q);
+int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a, int ep);
+int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap);
+int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, int64_t ld2, int64_t M, int P, int Q,
+                    float* slab, int64_t slab_cap, float* W, bool accumulate);
+
 template <typename T>
 __device__ __forceinline__ void lds_st8v(T* p, const float (&v)[8]) { st8(p, v); }
 

@@ -280,6 +280,18 @@ DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int
                           int64_t ldq, int koff, int voff, void* O, int64_t ldo, float* lse, const void* dO,
                           int64_t lddo, void* dqkv, int64_t lddq);
 
+/* The ViT trunk's large bf16 GEMMs (k_vgemm.hip; test / measurement seam): op 0 (NT):
+ * C[M][N] (bf16) = A[M][K] . B[N][K]^T with the epilogue mask epi: 1 + bias[N] (fp32), 2 + R[M][N],
+ * 4 also G = gelu(C) (C keeps the pre-activation), 8 C *= gelu'(Z[M][N]); N % 256 == 0, K % 64 == 0.
+ * op 1 (TN): C (fp32 [N][K]) = A^T . B for A [M][N], B [M][K] (bf16), split over M into slab
+ * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0.  ops 2 / 3: the same
+ * products through hipBLASLt (measurement comparison only; op 2 takes epi 0..3). */
+DFD_API int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const void* R, const float* bias,
+                      const void* Z, void* G, int64_t M, int N, int K, int epi, float* slab, int64_t slab_floats);
+DFD_API int64_t dfd_vgemm_tn_slab_floats(int64_t M, int N, int K);
+/* hipBLASLt calls made so far in this process (only dfd_vgemm ops 2 / 3 make any) */
+DFD_API int64_t dfd_blaslt_calls(void);
+
 /* fp32 GEMM of the recurrent models' plain products (test seam): C[m][n] = beta*C + sum_k A(m,k) B(n,k)
  * (+ bias[n]); A(m,k) = ta ? A[k*lda+m] : A[m*lda+k], B(n,k) = tb ? B[k*ldb+n] : B[n*ldb+k].  The
  * kernels behind nn.Linear / nn.LSTM input projections and weight gradients of LogicRNNLSTM,

@@ -46,13 +46,13 @@ def kernel_paths(request):
     BN-folded conv_pw backward only on >= 100K-row layers, fused depthwise backward), with the first
     two forced onto every covered layer ("forced", so the small parity shapes exercise the
     high-resolution code paths too), and with the depthwise backward as two kernels ("split_dw")."""
-    from deepfake_amd import _lib
-    lib = _lib.load()
-    knobs = {"default": {}, "forced": {b"stream_min_rows": 0, b"fold_min_rows": 0},
-             "split_dw": {b"dw_bwd_fused": 0}}[request.param]
-    prev = {k: lib.dfd_set_tuning(k, v) for k, v in knobs.items()}
+    from deepfake_amd import backbone
+    knobs = {"default": {}, "forced": {"stream_min_rows": 0, "fold_min_rows": 0},
+             "split_dw": {"dw_bwd_fused": 0}}[request.param]
+    prev = dict(backbone.DEFAULT_TUNING)  # the plans of runtimes built inside the test take these
+    backbone.DEFAULT_TUNING.update(knobs)
     try:
         yield request.param
     finally:
-        for k, v in prev.items():
-            lib.dfd_set_tuning(k, v)
+        backbone.DEFAULT_TUNING.clear()
+        backbone.DEFAULT_TUNING.update(prev)

@@ -157,18 +157,19 @@ def test_train_step_224_bf16(cuda, case, kernel_paths):
 
 
 def test_wgrad_stream_bit_identical(cuda):
-    """The 1x1 weight gradients on the plan's second stream (dfd_set_tuning("wgrad_stream", 1); off by
-    default) give bit-identical results to the single-stream schedule: same kernels, same fixed-order reductions; only the overlap changes
-    (a missing event would show up as a race here)."""
-    from deepfake_amd import _lib
-    lib = _lib.load()
-    prev = lib.dfd_set_tuning(b"wgrad_stream", 1)
+    """The 1x1 weight gradients on the plan's second stream (plan knob wgrad_stream = 1; off by default)
+    give bit-identical results to the single-stream schedule: same kernels, same fixed-order
+    reductions; only the overlap changes (a missing event would show up as a race here)."""
+    from deepfake_amd import backbone
+    prev = dict(backbone.DEFAULT_TUNING)
     try:
+        backbone.DEFAULT_TUNING["wgrad_stream"] = 1
         _, _, loss_a, grads_a, bufs_a = hip_step("b4t8", "bf16", cuda)
-        lib.dfd_set_tuning(b"wgrad_stream", 0)
+        backbone.DEFAULT_TUNING["wgrad_stream"] = 0
         _, _, loss_b, grads_b, bufs_b = hip_step("b4t8", "bf16", cuda)
     finally:
-        lib.dfd_set_tuning(b"wgrad_stream", prev)
+        backbone.DEFAULT_TUNING.clear()
+        backbone.DEFAULT_TUNING.update(prev)
     assert loss_a == loss_b
     diff = [n for n in grads_a if not torch.equal(grads_a[n], grads_b[n])]
     assert not diff, diff[:10]

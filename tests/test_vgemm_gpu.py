@@ -1,0 +1,98 @@
+"""The ViT trunk's large bf16 GEMMs (``k_vgemm.hip``, the ``dfd_vgemm`` seam) against plain-PyTorch
+fp32 products of the same bf16 operands (the C5 config's linears, ``src/models.py:88-107`` via timm
+``vit_base_patch16_224``: qkv / proj / fc1 / fc2 forward, their data gradients and weight gradients).
+
+Bounds: NT outputs are bf16, so each element is compared with the fp32 reference rounded to bf16
+within 2 bf16 ulps (rtol 8e-3) plus an absolute term of 1e-3 x the reference's RMS (fp32 summation
+order); TN weight gradients are fp32: relative L2 error <= 1e-5.  Shapes cover ragged row counts
+(M not a multiple of the 256-row tile, and for TN not a multiple of the 64-row m-step, whose rows
+past the end must contribute zero), every epilogue, and the C5 token-row count at 8 images."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deepfake_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+
+def _nt(cuda, M, N, K, epi, seed):
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    A = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) if epi & 1 else None
+    R = torch.randn(M, N, device=cuda, generator=g).bfloat16() if epi & 2 else None
+    Z = torch.randn(M, N, device=cuda, generator=g).bfloat16() if epi & 8 else None
+    G = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16) if epi & 4 else None
+    C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+    lib = _lib.load()
+    _lib.check(lib.dfd_vgemm(None, 0, P(A), P(B), P(C), P(R), P(bias), P(Z), P(G), M, N, K, epi, None, 0))
+    torch.cuda.synchronize()
+    ref = A.float() @ B.float().T
+    if bias is not None:
+        ref = ref + bias
+    if R is not None:
+        ref = ref + R.float()
+    if Z is not None:
+        z = Z.float().requires_grad_(True)
+        dz = torch.autograd.grad(F.gelu(z).sum(), z)[0]
+        ref = ref * dz
+    return C, G, ref
+
+
+def _close(got, ref):
+    scale = float(ref.float().pow(2).mean().sqrt())
+    torch.testing.assert_close(got.float(), ref.bfloat16().float(), rtol=8e-3, atol=1e-3 * scale)
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(600, 256, 64, 0), (394, 768, 768, 1), (394, 2304, 768, 1),
+                                       (1000, 768, 3072, 3), (394, 3072, 768, 5), (777, 3072, 768, 8),
+                                       (8 * 197, 768, 2304, 0)])
+def test_vgemm_nt_vs_fp32(cuda, M, N, K, epi):
+    C, G, ref = _nt(cuda, M, N, K, epi, M + N + K + epi)
+    _close(C, ref)
+    if G is not None:  # gelu of the stored (rounded) pre-activation
+        torch.testing.assert_close(G.float(), F.gelu(C.float()).bfloat16().float(), rtol=8e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(394, 768, 256), (8 * 197, 768, 3072), (100, 256, 512), (4096, 2304, 768)])
+def test_vgemm_tn_vs_fp32(cuda, M, N, K):
+    g = torch.Generator(device=cuda).manual_seed(M * 7 + N)
+    A = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    B = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    lib = _lib.load()
+    slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(M, N, K), device=cuda)
+    W = torch.full((N, K), float("nan"), device=cuda)
+    _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, None, M, N, K, 0, P(slab), slab.numel()))
+    torch.cuda.synchronize()
+    ref = A.double().T @ B.double()
+    e = float((W.double() - ref).norm() / ref.norm())
+    assert e <= 1e-5, e
+
+
+def test_vgemm_deterministic(cuda):
+    """two runs of the same TN product and NT product are bit-identical (fixed-order slab sums)"""
+    M, N, K = 2 * 197, 768, 768
+    A = torch.randn(M, N, device=cuda).bfloat16()
+    B = torch.randn(M, K, device=cuda).bfloat16()
+    lib = _lib.load()
+    slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(M, N, K), device=cuda)
+    outs = []
+    for _ in range(2):
+        W = torch.empty(N, K, device=cuda)
+        _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, None, M, N, K, 0, P(slab), slab.numel()))
+        outs.append(W)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_vgemm_refuses_uncovered(cuda):
+    A = torch.zeros(64, 100, device=cuda).bfloat16()
+    B = torch.zeros(200, 100, device=cuda).bfloat16()
+    C = torch.zeros(64, 200, device=cuda).bfloat16()
+    lib = _lib.load()
+    assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 100, 0, None, 0) != 0

@@ -35,14 +35,15 @@ def main():
     x, labels = bench.synthetic_batch(0, dev)
     lib = _lib.load()
     res = {v: [] for v in a.values}
+    rt = model.backbone.runtime()  # the knob is per plan (dfd_b0_plan_set_tuning)
     for v in a.values:  # warm every variant
-        lib.dfd_set_tuning(a.key.encode(), v)
+        rt.set_tuning(a.key, v)
         for _ in range(2):
             step(x, labels)
     torch.cuda.synchronize()
     for r in range(a.rounds):
         for v in (a.values if r % 2 == 0 else a.values[::-1]):
-            lib.dfd_set_tuning(a.key.encode(), v)
+            rt.set_tuning(a.key, v)
             step(x, labels)
             torch.cuda.synchronize()
             t0 = time.perf_counter()

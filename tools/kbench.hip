@@ -82,8 +82,10 @@ int main(int argc, char** argv) {
   Bench b;
   b.filter = argc > 1 ? argv[1] : "";
   const int F = argc > 2 ? atoi(argv[2]) : 256;
-  if (argc > 3) set_stream_min_rows(atoll(argv[3]));  // e.g. 1e12: tiled GEMM kernels only
-  if (argc > 4) set_gemm_tile(atoi(argv[4]));            // tiled GEMM tile config (-1 auto)
+  static Tuning tn;  // this process's knobs, installed for the whole run
+  if (argc > 3) tn.v[TK_STREAM_MIN_ROWS] = atoll(argv[3]);  // e.g. 1e12: tiled GEMM kernels only
+  if (argc > 4) tn.v[TK_GEMM_TILE] = atoi(argv[4]);         // tiled GEMM tile config (-1 auto)
+  const TuningScope ts(&tn);
   const int H = 224;
   CK(hipStreamCreate(&b.s));
   CK(hipEventCreate(&b.e0));

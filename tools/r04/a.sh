@@ -1,10 +1,23 @@
 #!/bin/bash
-# round-4 call A: ResNet-50 training parity after the centred BatchNorm forms; counter list; bench.
+# round-4 call A: ResNet-50 training parity (centred BatchNorm forms); ViT GEMM kernels (k_vgemm.hip)
+# parity + timing against hipBLASLt, then the ViT model tests and its train-step line; counter list; bench.
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out/r04
 timeout -k 10 400 python -u -m pytest tests/test_resnet_train_gpu.py -x -v -s --timeout 300 --timeout-method thread \
   > gpurun_out/r04/a_rn.log 2>&1; rc=$?
 echo "rn tests rc=$rc"; tail -4 gpurun_out/r04/a_rn.log
 [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_vgemm_gpu.py -v -s --timeout 120 --timeout-method thread \
+  > gpurun_out/r04/a_vg.log 2>&1; rc=$?
+echo "vgemm tests rc=$rc"; tail -4 gpurun_out/r04/a_vg.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u tools/vgemm_bench.py 5 > gpurun_out/r04/a_vgb.jsonl 2> gpurun_out/r04/a_vgb.err || { echo VGB FAILED; tail -5 gpurun_out/r04/a_vgb.err; exit 1; }
+cat gpurun_out/r04/a_vgb.jsonl
+timeout -k 10 400 python -u -m pytest tests/test_vit_gcn.py tests/test_attention_gpu.py -v --timeout 200 --timeout-method thread \
+  > gpurun_out/r04/a_vit.log 2>&1; rc=$?
+echo "vit tests rc=$rc"; tail -4 gpurun_out/r04/a_vit.log
+[ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python bench_temporal.py --model vit --no-cpu-baseline > gpurun_out/r04/a_vitb.jsonl 2> gpurun_out/r04/a_vitb.err || { echo VITB FAILED; tail -5 gpurun_out/r04/a_vitb.err; exit 1; }
+cut -c1-300 gpurun_out/r04/a_vitb.jsonl
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/r04/counters.txt 2>&1; echo "list rc=$?"
 cd $R
