@@ -277,7 +277,20 @@ class B0Runtime:
         h = self.plan(N, H, W, dtype, x.device)
         feats, ws = torch.ops.dfd.b0_trunk_forward(x, h.value, owner._flat_p, owner._flat_b, self._norm, training,
                                                    BN_MOMENTUM)
+        if self.tuning.get("mbconv7"):
+            self._check_fused_abort(h, ws)
         return feats, (h, ws)
+
+    def _check_fused_abort(self, h, ws) -> None:
+        """The experimental fused 7x7 MBConv (knob mbconv7, off by default) synchronises its grid with
+        software barriers; one that times out (a grid that was not co-resident) sets an abort word and
+        leaves wrong statistics.  With the knob on, every forward reads that word (one device sync)
+        and raises instead of returning a silently wrong step."""
+        nb, off = ctypes.c_int(), ctypes.c_int64()
+        _lib.check(self.lib.dfd_b0_fused_info(h, ctypes.byref(nb), ctypes.byref(off)))
+        if nb.value and int(ws[off.value:off.value + 4].view(torch.int32).item()) != 0:
+            raise _lib.DFDError("fused 7x7 MBConv: a grid barrier timed out (grid not co-resident); "
+                                "this step's statistics are invalid -- turn the mbconv7 knob off")
 
     def backward(self, h, ws, x, dfeat, owner, grads, training, seg_begin, seg_end, accumulate=False):
         torch.ops.dfd.b0_trunk_backward(x, h.value, dfeat, owner._flat_p, ws, grads, self._norm, training, seg_begin,

@@ -604,7 +604,12 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                                            p.slab_cap, grad(b.pwl.t_w), acc != 0, r.f(p.o_part),
                                                            p.part_cap, &hs)) < 0 ? -1 : 0));
           }
-          if (pf != 0) { set_error("pwl_bwd: covered shape not launched", __FILE__, __LINE__); return -1; }
+          if (pf != 0) {
+            // declined (1: its partial-sum slab or part buffer would not hold this frame count)
+            // or launched without the weight gradient (2): materialise gs with the apply pass for the
+            // unfused launches below
+            DFD_TRY(launch_bn_bwd_apply<T>(s, i3, r.a(b.o_y3), r.f(p.o_coef), r.a(p.o_gs), Mout, b.cout));
+          }
         } else {
           DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
           if (fpwl) {

@@ -108,20 +108,35 @@ class KernelProbe:
             return None
         avg_s = sum(self.ms) / len(self.ms) / 1e3
         achieved = nbytes / avg_s / 1e9
-        traffic = None
-        tf = traffic_file or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                          "profiles", "traffic.json")
-        if os.path.exists(tf):
+        traffic, tsrc = None, None
+        tf = traffic_file or latest_traffic_file()
+        if tf and os.path.exists(tf):
             try:
                 d = json.load(open(tf))
                 ent = d.get(f"{self.kind}:{self.stage}.{self.block}")
                 traffic = ent.get("hbm_bytes_per_launch") if ent else None
+                tsrc = {"file": os.path.relpath(tf, _REPO), "commit": d.get("_commit")}
             except Exception:
                 traffic = None
         return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                "frac": round(achieved / (HBM_PEAK / 1e9), 4), "traffic": traffic,
+                "frac": round(achieved / (HBM_PEAK / 1e9), 4), "traffic": traffic, "traffic_source": tsrc,
                 "kernel": f"{self.kind} blocks.{self.stage}.{self.block}", "algorithmic_bytes": nbytes,
                 "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(self.ms)}
+
+
+_REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def latest_traffic_file():
+    """the newest round's PMC traffic table (profiles/rNN/traffic.json, written by
+    tools/pmc_traffic_r04.py from that round's rocprofv3 passes), else the round-2 profiles/traffic.json"""
+    import glob
+
+    cands = sorted(glob.glob(os.path.join(_REPO, "profiles", "r[0-9][0-9]", "traffic.json")))
+    if cands:
+        return cands[-1]
+    old = os.path.join(_REPO, "profiles", "traffic.json")
+    return old if os.path.exists(old) else None
 
 
 PW_KINDS = ("pw_fwd", "pw_dgrad", "pw_wgrad", "pwl_fwd", "pwl_dgrad", "pwl_wgrad")
