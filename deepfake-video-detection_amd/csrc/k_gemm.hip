@@ -406,6 +406,10 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
     return -1;
   }
   if constexpr (sizeof(T) == 2) {
+    if (pro_mode == PRO_NONE && tune(TK_PW_SK) != 0) {
+      const int rc = launch_pw_sk(s, A, B, C, R, M, N, K, stats, 1024, stat_rows);
+      if (rc <= 0) return rc;
+    }
     const int rc = launch_pw_stream(s, A, B, C, R, nullptr, M, N, K, pro_mode, pro, stats, stat_rows);
     if (rc <= 0) return rc;
   }

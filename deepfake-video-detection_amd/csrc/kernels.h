@@ -44,7 +44,7 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 // Concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -52,8 +52,9 @@ struct Tuning {
 };
 // defaults: streaming 1x1 kernels from 40,000 rows; BN-folded conv_pw backward from 100,000 rows;
 // fused depthwise backward / channel-pair kernels on; tiled-GEMM config automatic (-1); weight
-// gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1};
+// gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on; small-K
+// weight-panel GEMM (k_pw_sk.hip) off until measured
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 0};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {
@@ -161,6 +162,12 @@ int blaslt_wgrad_split(hipStream_t s, const bf16* dY, const bf16* X, float* dW, 
 int blaslt_gemm(hipStream_t s, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
                 bool relu, int64_t M, int N, int K);
 
+// small-K (80 / 112 / 192 / 320) bf16 1x1 GEMM with the weight panel resident in LDS and LDS-DMA row
+// tiles (k_pw_sk.hip): 0 launched, 1 not covered; stats as launch_pw_gemm (one partial row per
+// workgroup, at most max_rows rows), R (residual) or stats, not both
+bool pw_sk_covers(int64_t M, int N, int K);
+int launch_pw_sk(hipStream_t s, const bf16* A, const bf16* W, bf16* C, const bf16* R, int64_t M, int N, int K,
+                 float* stats, int max_rows, int* stat_rows);
 template <typename T>
 int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,
                    int N, int K, int pro_mode, int epi);

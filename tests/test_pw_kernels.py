@@ -48,7 +48,7 @@ def _inputs(M, N, K, mode, rpf, seed, dev):
     return a, w, scale, shift, gate
 
 
-def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, tile=-1):
+def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, tile=-1, sk=0):
     lib = _lib_()
     a, w, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed, dev)
     gr = torch.Generator(device=dev)
@@ -59,6 +59,7 @@ def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, ti
     rows = ctypes.c_int(0)
     prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
     prev_tile = lib.dfd_set_tuning(b"gemm_tile", tile)
+    prev_sk = lib.dfd_set_tuning(b"pw_sk", sk)
     try:
         _lib.check(lib.dfd_pw_conv(_lib.stream_of(dev), 1, a.data_ptr(), w.data_ptr(), c.data_ptr(), _lib.ptr(r), M,
                                    N, K, mode, scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf,
@@ -67,6 +68,7 @@ def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, ti
     finally:
         lib.dfd_set_tuning(b"stream_min_rows", prev)
         lib.dfd_set_tuning(b"gemm_tile", prev_tile)
+        lib.dfd_set_tuning(b"pw_sk", prev_sk)
     ap = _pro(a, mode, scale, shift, gate, rpf).to(torch.bfloat16).float()
     ref = ap @ w.float().t()
     mag = ref.abs()
@@ -129,6 +131,27 @@ def test_pw_conv_bf16(cuda, case, path):
 def test_pw_conv_bf16_late_layers(cuda, case, tile):
     M, N, K, mode, resid, stats = case
     _run(M, N, K, mode, resid, stats, 0, cuda, rpf=49, tile=tile)
+
+
+# the small-K weight-panel kernel (k_pw_sk.hip): every (K, panel width) instantiation the 14x14 / 7x7
+# stages and conv_head use, with the BN-stat epilogue, plain, and with the residual; rows past the
+# 64-row multiple fall back to the other kernels (last case)
+SK_CASES = [(12544, 1152, 192, 0, False, True),   # blocks.5.x / 6.0 conv_pw forward (K 192, BN 128)
+            (12544, 1152, 192, 0, False, False),  # blocks.5.x conv_pwl data gradient
+            (12544, 1280, 320, 0, False, True),   # conv_head forward (K 320, BN 64)
+            (12544, 1152, 320, 0, False, False),  # blocks.6.0 conv_pwl data gradient
+            (50176, 480, 80, 0, False, True),     # blocks.3.x / 4.0 conv_pw forward (K 80 -> 96, BN 96)
+            (50176, 480, 80, 0, False, False),    # blocks.3.x conv_pwl data gradient
+            (50176, 672, 112, 0, False, True),    # blocks.4.x / 5.0 conv_pw forward (K 112 -> 128, BN 96)
+            (50176, 672, 112, 0, True, False),    # residual epilogue
+            (640, 512, 192, 0, False, True),      # BN 128 with more workgroups than tiles
+            (12550, 1152, 192, 0, False, True)]   # ragged rows: not covered, the tiled kernel runs
+
+
+@pytest.mark.parametrize("case", SK_CASES, ids=lambda c: "x".join(map(str, c[:3])) + f"_r{int(c[4])}s{int(c[5])}")
+def test_pw_conv_small_k_panel(cuda, case):
+    M, N, K, mode, resid, stats = case
+    _run(M, N, K, mode, resid, stats, 1 << 60, cuda, rpf=49, sk=1)
 
 
 def test_pw_conv_rejects_bad_args(cuda):

@@ -12,6 +12,12 @@ echo "vgemm tests rc=$rc"; tail -4 gpurun_out/r04/a_vg.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python -u tools/vgemm_bench.py 5 > gpurun_out/r04/a_vgb.jsonl 2> gpurun_out/r04/a_vgb.err || { echo VGB FAILED; tail -5 gpurun_out/r04/a_vgb.err; exit 1; }
 cat gpurun_out/r04/a_vgb.jsonl
+timeout -k 10 300 python -u -m pytest tests/test_pw_kernels.py -k small_k -v --timeout 120 --timeout-method thread \
+  > gpurun_out/r04/a_sk.log 2>&1; rc=$?
+echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 200 python -u tools/pw_sk_bench.py 5 > gpurun_out/r04/a_skb.jsonl 2> gpurun_out/r04/a_skb.err || { echo SKB FAILED; tail -5 gpurun_out/r04/a_skb.err; exit 1; }
+cat gpurun_out/r04/a_skb.jsonl
 timeout -k 10 400 python -u -m pytest tests/test_vit_gcn.py tests/test_attention_gpu.py -v --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_vit.log 2>&1; rc=$?
 echo "vit tests rc=$rc"; tail -4 gpurun_out/r04/a_vit.log
@@ -23,3 +29,5 @@ timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/r04/counters.txt 2>&1; echo "list
 cd $R
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep > gpurun_out/r04/a_bench.json 2> gpurun_out/r04/a_bench.err || { echo BENCH FAILED; tail -5 gpurun_out/r04/a_bench.err; exit 1; }
 cut -c1-300 gpurun_out/r04/a_bench.json
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune pw_sk=1 > gpurun_out/r04/a_bench_sk.json 2> gpurun_out/r04/a_bench_sk.err || { echo BENCH SK FAILED; tail -5 gpurun_out/r04/a_bench_sk.err; exit 1; }
+cut -c1-300 gpurun_out/r04/a_bench_sk.json
