@@ -11,15 +11,17 @@
 namespace dfd {
 
 // ------------------------------------------------------------------ partial-row reduction
-// Sums rows of a [rows][2][C] slab for channels [blockIdx.x*16, +16) in fp64:
-// 1024 threads = 16 channels x 64 row lanes; the 4 row lanes of a wave are added by two shuffles,
-// the 16 waves by threads 0..15 in wave order (deterministic; one barrier instead of a 6-level
-// LDS tree).  Valid in threads 0..15 (channel tid).
-constexpr int FIN_CH = 16;
-constexpr int FIN_RL = 64;
-
+// Sums rows of a [rows][2][C] slab for channels [blockIdx.x*CH, +CH) in fp64: 1024 threads = CH
+// channels x (1024 / CH) row lanes; the row lanes of a wave are added by shuffles, the 16 waves by
+// threads 0..CH-1 in wave order (deterministic; one barrier instead of a 6-level LDS tree).  Valid
+// in threads 0..CH-1 (channel tid).  CH (16, 8 or 4) is chosen per launch so that each row lane
+// reads at most 8 rows (one batch of loads in flight): the producers of the high-resolution maps
+// write up to 1,024 partial rows of few channels, where 16 channels per workgroup left one or two
+// workgroups walking 16 rows per lane in two dependent batches (10-12 us finalizes).
+template <int CH>
 __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int C, double& s, double& q,
                                  double* sh_s, double* sh_q) {
+  constexpr int FIN_CH = CH, FIN_RL = 1024 / CH;
   const int tid = threadIdx.x, cl = tid % FIN_CH, rl = tid / FIN_CH;
   const int c = blockIdx.x * FIN_CH + cl;
   double a = 0.0, b = 0.0;
@@ -41,11 +43,12 @@ __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int 
       b += stats[((int64_t)r * 2 + 1) * C + c];
     }
   }
-  // lanes l, l^16, l^32, l^48 of a wave hold the same channel
-  a += __shfl_xor(a, 16, 64);
-  b += __shfl_xor(b, 16, 64);
-  a += __shfl_xor(a, 32, 64);
-  b += __shfl_xor(b, 32, 64);
+  // lanes l, l^CH, l^2CH, ... of a wave hold the same channel
+#pragma unroll
+  for (int o = CH; o < 64; o <<= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
   const int wave = tid >> 6;
   if ((tid & 63) < FIN_CH) {
     sh_s[wave * FIN_CH + cl] = a;
@@ -62,6 +65,10 @@ __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int 
   }
 }
 
+// channels per finalize workgroup: at most 8 rows per row lane (reduce_stat_rows)
+static int fin_ch(int rows) { return rows <= 8 * 64 ? 16 : (rows <= 8 * 128 ? 8 : 4); }
+
+template <int FIN_CH>
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
                                                            int C, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* run_mean,
@@ -69,7 +76,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
                                                            float* mean, float* invstd, float* scale, float* shift) {
   __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
   double s = 0.0, q = 0.0;
-  if (training) reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
+  if (training) reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
   const int c = blockIdx.x * FIN_CH + tid;
   if (tid < FIN_CH && c < C) {
@@ -100,8 +107,14 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps, bool training,
                        float* mean, float* invstd, float* scale, float* shift) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(C, FIN_CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, beta,
-                     run_mean, run_var, momentum, eps, training ? 1 : 0, mean, invstd, scale, shift);
+  const int ch = training ? fin_ch(rows) : 16;
+#define DFD_FIN(CH)                                                                                                 \
+  hipLaunchKernelGGL((bn_finalize_kernel<CH>), dim3(cdiv(C, CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, beta, \
+                     run_mean, run_var, momentum, eps, training ? 1 : 0, mean, invstd, scale, shift)
+  if (ch == 16) DFD_FIN(16);
+  else if (ch == 8) DFD_FIN(8);
+  else DFD_FIN(4);
+#undef DFD_FIN
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -301,6 +314,7 @@ int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M
   return 0;
 }
 
+template <int FIN_CH>
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
                                                               int C, const float* __restrict__ gamma,
                                                               const float* __restrict__ mean,
@@ -309,7 +323,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
                                                               float* coef, int centred) {
   __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
   double s = 0.0, q = 0.0;
-  reduce_stat_rows(stats, rows, C, s, q, sh_s, sh_q);
+  reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
   const int c = blockIdx.x * FIN_CH + tid;
   if (tid < FIN_CH && c < C) {
@@ -334,8 +348,14 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
 int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                            const float* mean, const float* invstd, bool training, float* dgamma, float* dbeta,
                            bool accumulate, float* coef, bool centred) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(C, FIN_CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, mean,
-                     invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef, centred ? 1 : 0);
+#define DFD_FIN(CH)                                                                                                \
+  hipLaunchKernelGGL((bn_bwd_finalize_kernel<CH>), dim3(cdiv(C, CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, \
+                     mean, invstd, training ? 1 : 0, dgamma, dbeta, accumulate ? 1 : 0, coef, centred ? 1 : 0)
+  const int ch = fin_ch(rows);
+  if (ch == 16) DFD_FIN(16);
+  else if (ch == 8) DFD_FIN(8);
+  else DFD_FIN(4);
+#undef DFD_FIN
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
