@@ -277,7 +277,7 @@ class B0Runtime:
         h = self.plan(N, H, W, dtype, x.device)
         feats, ws = torch.ops.dfd.b0_trunk_forward(x, h.value, owner._flat_p, owner._flat_b, self._norm, training,
                                                    BN_MOMENTUM)
-        if self.tuning.get("mbconv7"):
+        if training and self.tuning.get("mbconv7"):  # the eval-mode fused launch has no grid barrier
             self._check_fused_abort(h, ws)
         return feats, (h, ws)
 

@@ -45,8 +45,8 @@ struct Dw1 {
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
 
-template <typename T, int K, int TH, int TW, int RS, int FR>
-__global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bwd1_kernel(
+template <typename T, int K, int TH, int TW, int RS, int FR, bool PF>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF) ? 3 : 2) void dw_bwd1_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
     const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
     int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
@@ -89,6 +89,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
   const int cp = tid & 15, slot = tid >> 4;  // channel pair; strip slot
   const int ch = c0 + 2 * cp;
   const bool cokp = ch < C;
+  constexpr int NSI = (D::NSTRIP + 15) / 16;  // strips per slot and tile
 
   // ---- weight-gradient accumulators and BN1 sums, live for the whole launch ----
   v2f dw[K][K];
@@ -98,30 +99,65 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
     for (int b = 0; b < K; ++b) dw[a][b] = v2f{0.f, 0.f};
   v2f ss = {0.f, 0.f}, sq = {0.f, 0.f};
 
+  // staging loads of tile t: dZ, y2 + halo (this thread's 8 channels); frame base + 32-bit offsets.
+  // A tile past the end (the prefetch after a workgroup's last tile) loads nothing.
+  Raw8<T> rz[D::NLD], r2[D::NLD];
+  auto stage_ld = [&](int t) {
+    const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;
+    const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
+    const bool live = f < g.frames;
+    const T* zf = dZ + (int64_t)(live ? f : 0) * fstride;
+    const T* yf = Y2 + (int64_t)(live ? f : 0) * fstride;
+#pragma unroll
+    for (int i = 0; i < D::NLD; ++i) {
+      const int pixl = (tid >> 2) + 64 * i;
+      const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
+      const int oy = iy0 - D::PAD + pf / D::GW, ox = ix0 - D::PAD + pf % D::GW;
+      const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
+      const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
+      raw_ld(rz[i], zf + o, zf, in);
+      raw_ld(r2[i], yf + o, yf, in);
+    }
+  };
+  // PF: software pipeline -- the next tile's staging loads are in flight during this tile's strips
+  // (they reuse rz / r2, free once committed), and each strip's y1 is loaded before the commit
+  if (PF) stage_ld(bid / groups);
+
   for (int t = bid / groups; t < ntiles; t += tstep) {
     const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;  // first frame of the tile
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
-    // ---- staging loads: dZ, y2 + halo (this thread's 8 channels); frame base + 32-bit offsets ----
-    Raw8<T> rz[D::NLD], r2[D::NLD];
-    {
-      const T* zf = dZ + (int64_t)f * fstride;
-      const T* yf = Y2 + (int64_t)f * fstride;
-#pragma unroll
-      for (int i = 0; i < D::NLD; ++i) {
-        const int pixl = (tid >> 2) + 64 * i;
-        const int fi = FR > 1 ? pixl / (D::GH1 * D::GW) : 0, pf = pixl - fi * (D::GH1 * D::GW);
-        const int oy = iy0 - D::PAD + pf / D::GW, ox = ix0 - D::PAD + pf % D::GW;
-        const bool in = pixl < D::NG && cok8 && f + fi < g.frames && oy >= 0 && oy < g.H && ox >= 0 && ox < g.W;
-        const uint32_t o = in ? (uint32_t)(fi * fstride + (oy * g.W + ox) * C + c8) : 0u;
-        raw_ld(rz[i], zf + o, zf, in);
-        raw_ld(r2[i], yf + o, yf, in);
-      }
-    }
+    if (!PF) stage_ld(t);
     // the tile frames' SE gate and squeeze-path gradient (tiny, L2-resident) -> LDS
     for (int i = tid; i < FR * 2 * DCG; i += 256) {
       const int fi = i / (2 * DCG), w2 = (i / DCG) & 1, cl = i % DCG;
       const bool ok = c0 + cl < C && f + fi < g.frames;
       gbl[fi][w2][cl] = ok ? (w2 ? b2.bc : b2.gate)[(int64_t)(f + fi) * C + c0 + cl] : 0.f;
+    }
+    // strip geometry: tiles never cross the map (dw_bwd1_covers: exact tilings), so only the channel
+    // bound and, with stacked frames, a missing last frame mask anything: such lanes read pixel 0 of
+    // frame f (pixel stride 0; their zero dY gives zero dW terms) and skip the epilogue
+    const T* y1f = Y1 + (int64_t)f * fstride;
+    T* outf = out + (int64_t)f * fstride;
+    auto strip_at = [&](int s, int& fi, int& pr, int& xs, bool& rok, uint32_t& sb, uint32_t& pb) {
+      fi = FR > 1 ? s / D::SPF : 0;
+      const int sf = s - fi * D::SPF;
+      pr = sf % TH;
+      xs = (sf / TH) * RS;
+      rok = cokp && f + fi < g.frames && s < D::NSTRIP;
+      pb = rok ? (uint32_t)(C * sizeof(T)) : 0u;
+      sb = rok ? (uint32_t)((fi * fstride + ((iy0 + pr) * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
+    };
+    Raw2<T> ryp[PF ? NSI : 1][RS];
+    if (PF) {
+#pragma unroll
+      for (int si = 0; si < NSI; ++si) {
+        int fi, pr, xs;
+        bool rok;
+        uint32_t sb, pb;
+        strip_at(slot + 16 * si, fi, pr, xs, rok, sb, pb);
+#pragma unroll
+        for (int px = 0; px < RS; ++px) raw2_ld(ryp[PF ? si : 0][px], boff(y1f, sb + px * pb));
+      }
     }
     lds_barrier();  // the previous tile's strips are done with dys; gbl written
     // ---- commit: the fused BN2 backward into fp32 LDS (zero outside the map) ----
@@ -155,27 +191,26 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
         }
       }
     }
+    if (PF) stage_ld(t + tstep);
     lds_barrier();
 
     // ---- strips: data gradient + weight gradient from one read of each dY row ----
     const v2f sc1 = lds2(&cst[5][2 * cp]), sh1 = lds2(&cst[6][2 * cp]);
     const v2f is1 = lds2(&cst[8][2 * cp]), mi1 = -lds2(&cst[7][2 * cp]) * is1;  // xhat = y*is + mi
-#pragma unroll 1
-    for (int s = slot; s < D::NSTRIP; s += 16) {
-      const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
-      const int pr = sf % TH, xs = (sf / TH) * RS;
-      const int iy = iy0 + pr;
-      // tiles never cross the map (dw_bwd1_covers: exact tilings), so only the channel bound and,
-      // with stacked frames, a missing last frame mask anything: such lanes read pixel 0 of frame f
-      // (pixel stride 0; their zero dY gives zero dW terms) and skip the epilogue
-      const bool rok = cokp && f + fi < g.frames;
-      const T* y1f = Y1 + (int64_t)f * fstride;
-      T* outf = out + (int64_t)f * fstride;
-      const uint32_t pb = rok ? (uint32_t)(C * sizeof(T)) : 0u;
-      const uint32_t sb = rok ? (uint32_t)((fi * fstride + (iy * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
+#pragma unroll
+    for (int si = 0; si < NSI; ++si) {
+      const int s = slot + 16 * si;
+      if (NSI * 16 > D::NSTRIP && s >= D::NSTRIP) break;
+      int fi, pr, xs;
+      bool rok;
+      uint32_t sb, pb;
+      strip_at(s, fi, pr, xs, rok, sb, pb);
       Raw2<T> ry[RS];
 #pragma unroll
-      for (int px = 0; px < RS; ++px) raw2_ld(ry[px], boff(y1f, sb + px * pb));
+      for (int px = 0; px < RS; ++px) {
+        if (PF) ry[px] = ryp[PF ? si : 0][px];
+        else raw2_ld(ry[px], boff(y1f, sb + px * pb));
+      }
       // activations (weight-gradient operand) and sigmoids (for silu') of the strip
       v2f act[RS], sg[RS];
 #pragma unroll
@@ -266,7 +301,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3) ? 3 : 2) void dw_bw
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, bool PF = false>
 static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const Dw1Bn2& b2, const float* w,
                        const T* Y1, const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab,
                        int64_t slab_cap, float* dW, bool accumulate) {
@@ -275,8 +310,8 @@ static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
-  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS, FR>;
-  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS, FR>, 256>();
+  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS, FR, PF>;
+  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS, FR, PF>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
@@ -311,20 +346,24 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
   if (!dw_bwd1_covers(g)) return 1;
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   const int H = g.H, W = g.W;
+  // bf16: the software-pipelined form (knob dw_pf) where its registers fit the launch bounds
+  const bool pf = sizeof(T) == 2 && tune(TK_DW_PF) != 0;
+#define DFD_BWD1(K_, TH_, TW_, RS_, FR_)                                                                         \
+  return pf ? bwd1_launch<T, K_, TH_, TW_, RS_, FR_, sizeof(T) == 2>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows,  \
+                                                           slab, slab_cap, dW, accumulate)                       \
+            : bwd1_launch<T, K_, TH_, TW_, RS_, FR_, false>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, \
+                                                            slab, slab_cap, dW, accumulate)
   if (H == 7 && W == 7) {
-    if (g.k == 3)
-      return bwd1_launch<T, 3, 7, 7, 7, 2>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
-    return bwd1_launch<T, 5, 7, 7, 7, 2>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    if (g.k == 3) DFD_BWD1(3, 7, 7, 7, 2);
+    DFD_BWD1(5, 7, 7, 7, 2);
   }
   if (g.k == 3) {
-    if (H % 8 == 0 && W % 28 == 0)
-      return bwd1_launch<T, 3, 8, 28, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
-    if (H % 14 == 0 && W % 14 == 0)
-      return bwd1_launch<T, 3, 14, 14, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+    if (H % 8 == 0 && W % 28 == 0) DFD_BWD1(3, 8, 28, 7, 1);
+    if (H % 14 == 0 && W % 14 == 0) DFD_BWD1(3, 14, 14, 7, 1);
     return 1;
   }
-  if (H % 14 == 0 && W % 14 == 0)
-    return bwd1_launch<T, 5, 14, 14, 7>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate);
+  if (H % 14 == 0 && W % 14 == 0) DFD_BWD1(5, 14, 14, 7, 1);
+#undef DFD_BWD1
   return 1;
 }
 

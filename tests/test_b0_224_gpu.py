@@ -156,16 +156,19 @@ def test_train_step_224_bf16(cuda, case, kernel_paths):
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
 
 
-def test_wgrad_stream_bit_identical(cuda):
-    """The 1x1 weight gradients on the plan's second stream (plan knob wgrad_stream = 1; off by default)
-    give bit-identical results to the single-stream schedule: same kernels, same fixed-order
-    reductions; only the overlap changes (a missing event would show up as a race here)."""
+@pytest.mark.parametrize("knob", ["wgrad_stream", "dw_pf"])
+def test_schedule_knob_bit_identical(cuda, knob):
+    """Plan knobs that change only the schedule, not the arithmetic, give bit-identical steps:
+    wgrad_stream = 1 puts the 1x1 weight gradients on the plan's second stream (a missing event would
+    show up as a race here); dw_pf = 1 runs the software-pipelined stride-1 depthwise backward (the
+    next tile's staging loads in flight during the strips; same sums in the same order).  Both are
+    off by default."""
     from deepfake_amd import backbone
     prev = dict(backbone.DEFAULT_TUNING)
     try:
-        backbone.DEFAULT_TUNING["wgrad_stream"] = 1
+        backbone.DEFAULT_TUNING[knob] = 1
         _, _, loss_a, grads_a, bufs_a = hip_step("b4t8", "bf16", cuda)
-        backbone.DEFAULT_TUNING["wgrad_stream"] = 0
+        backbone.DEFAULT_TUNING[knob] = 0
         _, _, loss_b, grads_b, bufs_b = hip_step("b4t8", "bf16", cuda)
     finally:
         backbone.DEFAULT_TUNING.clear()

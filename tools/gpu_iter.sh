@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest tests/test_pw_kernels.py -x -q --timeout 1
 tail -3 gpurun_out/tk_$TAG.log
 [ $rc -ne 0 ] && { echo "KERNEL TESTS FAILED rc=$rc"; grep -E "Error|assert|FAILED" gpurun_out/tk_$TAG.log | head -30; exit $rc; }
 timeout -k 10 120 tools/kbench $FILTER > gpurun_out/kb_$TAG.txt 2>&1 || { echo KBENCH FAILED; tail gpurun_out/kb_$TAG.txt; exit 1; }
-timeout -k 10 120 tools/kbench $FILTER 256 1000000000000 > gpurun_out/kb_${TAG}_tiled.txt 2>&1 || { echo KBENCH2 FAILED; exit 1; }
+timeout -k 10 120 tools/kbench $FILTER 256 stream_min_rows=1000000000000 > gpurun_out/kb_${TAG}_tiled.txt 2>&1 || { echo KBENCH2 FAILED; exit 1; }
 tail -1 gpurun_out/kb_$TAG.txt; tail -1 gpurun_out/kb_${TAG}_tiled.txt
 timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1; rc=$?
 tail -3 gpurun_out/t_$TAG.log

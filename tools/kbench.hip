@@ -5,7 +5,7 @@
 // and prints the average duration next to the algorithmic HBM floor
 // (roofline.py / SURVEY.md §8(d) bytes ÷ 6.3 TB/s measured copy bandwidth).
 //
-// build: make -C tools kbench        run: tools/kbench [filter] [frames]
+// build: make -C tools kbench        run: tools/kbench [filter] [frames] [knob=value ...]
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -83,8 +83,14 @@ int main(int argc, char** argv) {
   b.filter = argc > 1 ? argv[1] : "";
   const int F = argc > 2 ? atoi(argv[2]) : 256;
   static Tuning tn;  // this process's knobs, installed for the whole run
-  if (argc > 3) tn.v[TK_STREAM_MIN_ROWS] = atoll(argv[3]);  // e.g. 1e12: tiled GEMM kernels only
-  if (argc > 4) tn.v[TK_GEMM_TILE] = atoi(argv[4]);         // tiled GEMM tile config (-1 auto)
+  // further arguments: name=value knobs (kTuneNames, e.g. dw_pf=1 stream_min_rows=1000000000000)
+  for (int i = 3; i < argc; ++i) {
+    const char* eq = strchr(argv[i], '=');
+    int k = 0;
+    while (eq && k < TK_COUNT && strncmp(argv[i], kTuneNames[k], eq - argv[i]) != 0) ++k;
+    if (!eq || k == TK_COUNT || kTuneNames[k][eq - argv[i]] != 0) { fprintf(stderr, "bad knob %s\n", argv[i]); return 2; }
+    tn.v[k] = atoll(eq + 1);
+  }
   const TuningScope ts(&tn);
   const int H = 224;
   CK(hipStreamCreate(&b.s));

@@ -18,6 +18,12 @@ echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 200 python -u tools/pw_sk_bench.py 5 > gpurun_out/r04/a_skb.jsonl 2> gpurun_out/r04/a_skb.err || { echo SKB FAILED; tail -5 gpurun_out/r04/a_skb.err; exit 1; }
 cat gpurun_out/r04/a_skb.jsonl
+timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k schedule_knob -v --timeout 200 --timeout-method thread \
+  > gpurun_out/r04/a_pf.log 2>&1; rc=$?
+echo "schedule-knob tests rc=$rc"; tail -3 gpurun_out/r04/a_pf.log
+[ $rc -eq 0 ] || exit 1
+for r in 1 2; do for v in 0 1; do echo "== dw_pf=$v round $r"; timeout -k 10 120 tools/kbench dw_bwd1 256 dw_pf=$v || exit 1; done; done > gpurun_out/r04/a_kbpf.txt 2>&1 || { echo KBPF FAILED; tail -5 gpurun_out/r04/a_kbpf.txt; exit 1; }
+cat gpurun_out/r04/a_kbpf.txt
 timeout -k 10 400 python -u -m pytest tests/test_vit_gcn.py tests/test_attention_gpu.py -v --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_vit.log 2>&1; rc=$?
 echo "vit tests rc=$rc"; tail -4 gpurun_out/r04/a_vit.log
@@ -31,3 +37,5 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep > gpurun_out/r
 cut -c1-300 gpurun_out/r04/a_bench.json
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune pw_sk=1 > gpurun_out/r04/a_bench_sk.json 2> gpurun_out/r04/a_bench_sk.err || { echo BENCH SK FAILED; tail -5 gpurun_out/r04/a_bench_sk.err; exit 1; }
 cut -c1-300 gpurun_out/r04/a_bench_sk.json
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune dw_pf=1 > gpurun_out/r04/a_bench_pf.json 2> gpurun_out/r04/a_bench_pf.err || { echo BENCH PF FAILED; tail -5 gpurun_out/r04/a_bench_pf.err; exit 1; }
+cut -c1-300 gpurun_out/r04/a_bench_pf.json
