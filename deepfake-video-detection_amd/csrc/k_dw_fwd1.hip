@@ -17,14 +17,17 @@
 
 namespace dfd {
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1, int RB = 1>
 struct Dwf1 {
   // TH x TW OUTPUT tile; the staged input window is ((TH-1)S+K) x ((TW-1)S+K) (+ FR stacked frames)
   static constexpr int PAD = K / 2;
   static constexpr int GH1 = (TH - 1) * S + K, GW = (TW - 1) * S + K;
   static constexpr int GH = FR * GH1, NG = GH * GW;
   static constexpr int NLD = (NG * 4 + 255) / 256;
-  static constexpr int SPR = TW / RS, SPF = TH * SPR, NSTRIP = FR * SPF;
+  // RB = 2: a thread's strip covers two adjacent output rows (stride 1): the K+1 input rows feed
+  // both rows' K kernel rows, so each staged row is read once per two outputs
+  static constexpr int SPR = TW / RS, SPF = (TH / RB) * SPR, NSTRIP = FR * SPF;
+  static_assert(TH % RB == 0 && (RB == 1 || S == 1), "row blocking: stride 1, whole row pairs");
   static constexpr int RW = (RS - 1) * S + K;
   static constexpr int NP = DCG / 2;
   // act row stride (float2 pairs): the four strips of a wave read rows S apart; stride 1: an odd
@@ -39,11 +42,11 @@ struct Dwf1 {
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
 
-template <typename T, int K, int TH, int TW, int RS, int FR, int S>
+template <typename T, int K, int TH, int TW, int RS, int FR, int S, int RB>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fwd1_kernel(
     DwGeom g, const T* __restrict__ Y1, const float* __restrict__ w, Pro bn1, T* __restrict__ out,
     float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
-  using D = Dwf1<T, K, TH, TW, RS, FR, S>;
+  using D = Dwf1<T, K, TH, TW, RS, FR, S, RB>;
   __shared__ __attribute__((aligned(16))) char araw[D::AB];        // staged activations; reduction scratch
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
   __shared__ __attribute__((aligned(16))) float cst[2][DCG];       // BN1 scale, shift
@@ -86,6 +89,15 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
       raw_ld(ry[i], yf + o, yf, in);
     }
   };
+  // RB = 2: the channel pair's K x K weights in registers for the whole launch
+  v2f wreg[RB == 2 ? K : 1][RB == 2 ? K : 1];
+  if constexpr (RB == 2) {
+    lds_barrier();  // wts written
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < K; ++kw) wreg[kh][kw] = lds2(wts + (kh * K + kw) * DCG + 2 * cp);
+  }
   Raw8<T> ry[D::NLD];
   if (DFD_FWD1_PF && bid / groups < ntiles) stage_load(bid / groups, ry);
   for (int t = bid / groups; t < ntiles; t += tstep) {
@@ -116,6 +128,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
     lds_barrier();
     // the next tile's window loads fly while this tile's strips run (issued before its stores)
     if (DFD_FWD1_PF && t + tstep < ntiles) stage_load(t + tstep, ry);
+    if constexpr (RB == 1) {
 #pragma unroll 1
     for (int s = slot; s < D::NSTRIP; s += 16) {
       const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
@@ -155,6 +168,62 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
         }
       }
     }
+    } else {
+    // two output rows per strip; the weights live in registers (loaded once per launch): per two
+    // rows K+1 staged-row reads instead of 2K row + 2K weight-row reads.  Same kh-then-kw FMA order
+    // per output as RB = 1 (bit-identical results)
+#pragma unroll 1
+    for (int s = slot; s < D::NSTRIP; s += 16) {
+      const int fi = FR > 1 ? s / D::SPF : 0, sf = s - fi * D::SPF;
+      const int pr = (sf % (TH / 2)) * 2, xs = (sf / (TH / 2)) * RS;
+      const int iy = iy0 + pr;
+      T* outf = out + (int64_t)f * ostride;
+      const uint32_t sb = (uint32_t)((fi * ostride + (iy * g.Wo + ix0 + xs) * C + ch) * sizeof(T));
+      const bool rok = cokp && f + fi < g.frames;
+      v2f acc0[RS], acc1[RS];
+#pragma unroll
+      for (int px = 0; px < RS; ++px) acc0[px] = acc1[px] = v2f{0.f, 0.f};
+#pragma unroll
+      for (int ih = 0; ih <= K; ++ih) {
+        asm volatile("" ::: "memory");
+        const float* rowp = acts + (fi * D::GH1 + pr + ih) * D::ARS * 2 + xs * DCG + 2 * cp;
+        v2f ar[D::RW];
+#pragma unroll
+        for (int j = 0; j < D::RW; ++j) ar[j] = lds2(rowp + j * DCG);
+        if (ih < K) {
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+            for (int px = 0; px < RS; ++px) acc0[px] = fma2(ar[px + kw], wreg[ih < K ? ih : 0][kw], acc0[px]);
+        }
+        if (ih > 0) {
+#pragma unroll
+          for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+            for (int px = 0; px < RS; ++px) acc1[px] = fma2(ar[px + kw], wreg[ih > 0 ? ih - 1 : 0][kw], acc1[px]);
+        }
+#pragma unroll
+        for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc0[px]), "+v"(acc1[px]));
+      }
+      if (rok) {
+        const uint32_t rowb = (uint32_t)(g.Wo * C * sizeof(T));
+#pragma unroll
+        for (int px = 0; px < RS; ++px) {
+          const v2f v = round2(acc0[px], (T*)nullptr);
+          ss += v;
+          sq = fma2(v, v, sq);
+          st2(boff(outf, sb + px * (uint32_t)(C * sizeof(T))), v);
+        }
+#pragma unroll
+        for (int px = 0; px < RS; ++px) {
+          const v2f v = round2(acc1[px], (T*)nullptr);
+          ss += v;
+          sq = fma2(v, v, sq);
+          st2(boff(outf, sb + rowb + px * (uint32_t)(C * sizeof(T))), v);
+        }
+      }
+    }
+    }
   }
   // ---- BN2 partial sums: lanes sharing a channel pair, then the 4 waves, in a fixed order ----
   lane_sum4(ss);
@@ -175,20 +244,20 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1, int RB = 1>
 static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                        int* stat_rows) {
   const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
   if (FR > 1 && (tiles_x != 1 || tiles_y != 1)) { set_error("dw_fwd1: frame stacking needs whole-map tiles", __FILE__, __LINE__); return -1; }
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
-  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR, S>, 256>();
+  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
   // XCD-aware order where it measured faster (kbench A/B: 56x56 s1 -16 %, 14x14 c480 -2..-6 %); the
   // 14x14 k5 c672 (+7 %), stacked 7x7 (+7..12 %) and single-group layers keep dispatch order
   const int xcd = DFD_DW_XCD >= 0 ? DFD_DW_XCD : (groups > 1 && (g.Ho >= 28 || (g.Ho == 14 && g.C <= 480)));
-  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
+  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
                      pro, Y, stats, ntiles, groups, tiles_x, tiles_y, xcd);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
@@ -206,6 +275,7 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
       !dw_fwd1_enabled())
     return 0;
   const int H = g.Ho, W = g.Wo;  // output map
+  const bool rb = tune(TK_DW_RB) != 0;  // two output rows per strip (knob dw_rb)
   int rc;
   if (g.s == 2) {
     // k3 stride 2 (112->56, 28->14): the 8x8 tile kernel is as fast or faster (kbench: 214 vs 246,
@@ -223,10 +293,15 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
     rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows)
                   : fwd1_launch<T, 5, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows);
   } else if (g.k == 3 && H % 8 == 0 && W % 28 == 0 && W >= 112) {  // 56x56: the 8-channel strip kernel is 6% faster
-    rc = fwd1_launch<T, 3, 8, 28, 7>(s, g, X, w, Y, pro, stats, stat_rows);
+    rc = rb ? fwd1_launch<T, 3, 8, 28, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+            : fwd1_launch<T, 3, 8, 28, 7>(s, g, X, w, Y, pro, stats, stat_rows);
   } else if (H % 14 == 0 && W % 14 == 0) {
-    rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows)
-                  : fwd1_launch<T, 5, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows);
+    if (rb)
+      rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+                    : fwd1_launch<T, 5, 14, 14, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+    else
+      rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows)
+                    : fwd1_launch<T, 5, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows);
   } else {
     return 0;
   }

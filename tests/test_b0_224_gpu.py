@@ -156,13 +156,14 @@ def test_train_step_224_bf16(cuda, case, kernel_paths):
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
 
 
-@pytest.mark.parametrize("knob", ["wgrad_stream", "dw_pf"])
+@pytest.mark.parametrize("knob", ["wgrad_stream", "dw_pf", "dw_rb"])
 def test_schedule_knob_bit_identical(cuda, knob):
     """Plan knobs that change only the schedule, not the arithmetic, give bit-identical steps:
     wgrad_stream = 1 puts the 1x1 weight gradients on the plan's second stream (a missing event would
     show up as a race here); dw_pf = 1 runs the software-pipelined stride-1 depthwise backward (the
-    next tile's staging loads in flight during the strips; same sums in the same order).  Both are
-    off by default."""
+    next tile's staging loads in flight during the strips; same sums in the same order); dw_rb = 1
+    runs the stride-1 depthwise forward with two output rows per strip (same per-output FMA order).
+    All three are off by default."""
     from deepfake_amd import backbone
     prev = dict(backbone.DEFAULT_TUNING)
     try:

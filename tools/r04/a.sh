@@ -24,6 +24,8 @@ echo "schedule-knob tests rc=$rc"; tail -3 gpurun_out/r04/a_pf.log
 [ $rc -eq 0 ] || exit 1
 for r in 1 2; do for v in 0 1; do echo "== dw_pf=$v round $r"; timeout -k 10 120 tools/kbench dw_bwd1 256 dw_pf=$v || exit 1; done; done > gpurun_out/r04/a_kbpf.txt 2>&1 || { echo KBPF FAILED; tail -5 gpurun_out/r04/a_kbpf.txt; exit 1; }
 cat gpurun_out/r04/a_kbpf.txt
+for r in 1 2; do for v in 0 1; do echo "== dw_rb=$v round $r"; timeout -k 10 120 tools/kbench dw_fwd 256 dw_rb=$v || exit 1; done; done > gpurun_out/r04/a_kbrb.txt 2>&1 || { echo KBRB FAILED; tail -5 gpurun_out/r04/a_kbrb.txt; exit 1; }
+cat gpurun_out/r04/a_kbrb.txt
 timeout -k 10 400 python -u -m pytest tests/test_vit_gcn.py tests/test_attention_gpu.py -v --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_vit.log 2>&1; rc=$?
 echo "vit tests rc=$rc"; tail -4 gpurun_out/r04/a_vit.log
