@@ -21,7 +21,7 @@
 
 namespace dfd {
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, int RB = 1>
 struct Dw1 {
   // FR > 1: the tile is FR whole frames (TH x TW = the map), stacked with their own halos -- fills
   // the 16 strip slots on 7x7 maps
@@ -30,7 +30,10 @@ struct Dw1 {
   static constexpr int GH = FR * GH1, NG = GH * GW;
   static constexpr int NLD = (NG * 4 + 255) / 256;  // 8-channel vector loads per thread per tensor
   static constexpr int SPR = TW / RS;               // strips per tile row
-  static constexpr int SPF = TH * SPR;              // strips per frame
+  // RB = 2: a strip covers two adjacent rows; the K+1 staged dY rows it reads feed both rows' K
+  // kernel rows (each staged row read once per two outputs)
+  static constexpr int SPF = (TH / RB) * SPR;       // strips per frame
+  static_assert(TH % RB == 0, "row blocking: whole row pairs");
   static constexpr int NSTRIP = FR * SPF;
   static constexpr int RW = RS + K - 1;             // dY pairs per strip row
   static_assert(TW % RS == 0, "strips tile the row");
@@ -45,12 +48,12 @@ struct Dw1 {
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
 
-template <typename T, int K, int TH, int TW, int RS, int FR, bool PF>
-__global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF) ? 3 : 2) void dw_bwd1_kernel(
+template <typename T, int K, int TH, int TW, int RS, int FR, bool PF, int RB>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF && RB == 1) ? 3 : 2) void dw_bwd1_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
     const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
     int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
-  using D = Dw1<T, K, TH, TW, RS, FR>;
+  using D = Dw1<T, K, TH, TW, RS, FR, RB>;
   __shared__ __attribute__((aligned(16))) char dyraw[D::DYB];  // staged dY (fp32 pairs); reduction scratch
   __shared__ __attribute__((aligned(16))) float gbl[FR][2][DCG];   // the tile frames' SE gate and bc
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
@@ -141,13 +144,14 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF) ? 3 : 2) voi
     auto strip_at = [&](int s, int& fi, int& pr, int& xs, bool& rok, uint32_t& sb, uint32_t& pb) {
       fi = FR > 1 ? s / D::SPF : 0;
       const int sf = s - fi * D::SPF;
-      pr = sf % TH;
-      xs = (sf / TH) * RS;
+      pr = (sf % (TH / RB)) * RB;
+      xs = (sf / (TH / RB)) * RS;
       rok = cokp && f + fi < g.frames && s < D::NSTRIP;
       pb = rok ? (uint32_t)(C * sizeof(T)) : 0u;
       sb = rok ? (uint32_t)((fi * fstride + ((iy0 + pr) * g.W + ix0 + xs) * C + ch) * sizeof(T)) : 0u;
     };
-    Raw2<T> ryp[PF ? NSI : 1][RS];
+    const uint32_t rowb = (uint32_t)(g.W * C * sizeof(T));  // next row of a strip (RB = 2)
+    Raw2<T> ryp[PF ? NSI : 1][RB][RS];
     if (PF) {
 #pragma unroll
       for (int si = 0; si < NSI; ++si) {
@@ -156,7 +160,9 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF) ? 3 : 2) voi
         uint32_t sb, pb;
         strip_at(slot + 16 * si, fi, pr, xs, rok, sb, pb);
 #pragma unroll
-        for (int px = 0; px < RS; ++px) raw2_ld(ryp[PF ? si : 0][px], boff(y1f, sb + px * pb));
+        for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+          for (int px = 0; px < RS; ++px) raw2_ld(ryp[PF ? si : 0][rr][px], boff(y1f, sb + (rok ? rr * rowb : 0u) + px * pb));
       }
     }
     lds_barrier();  // the previous tile's strips are done with dys; gbl written
@@ -205,59 +211,79 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF) ? 3 : 2) voi
       bool rok;
       uint32_t sb, pb;
       strip_at(s, fi, pr, xs, rok, sb, pb);
-      Raw2<T> ry[RS];
+      Raw2<T> ry[RB][RS];
 #pragma unroll
-      for (int px = 0; px < RS; ++px) {
-        if (PF) ry[px] = ryp[PF ? si : 0][px];
-        else raw2_ld(ry[px], boff(y1f, sb + px * pb));
-      }
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int px = 0; px < RS; ++px) {
+          if (PF) ry[rr][px] = ryp[PF ? si : 0][rr][px];
+          else raw2_ld(ry[rr][px], boff(y1f, sb + (rok ? rr * rowb : 0u) + px * pb));
+        }
       // activations (weight-gradient operand) and sigmoids (for silu') of the strip
-      v2f act[RS], sg[RS];
+      v2f act[RB][RS], sg[RB][RS];
 #pragma unroll
-      for (int px = 0; px < RS; ++px) {
-        const v2f z = fma2(raw2_f(ry[px]), sc1, sh1);
-        sg[px] = sigmoid2(z);
-        act[px] = z * sg[px];
-      }
-      v2f acc[RS];
+      for (int rr = 0; rr < RB; ++rr)
 #pragma unroll
-      for (int px = 0; px < RS; ++px) acc[px] = v2f{0.f, 0.f};
+        for (int px = 0; px < RS; ++px) {
+          const v2f z = fma2(raw2_f(ry[rr][px]), sc1, sh1);
+          sg[rr][px] = sigmoid2(z);
+          act[rr][px] = z * sg[rr][px];
+        }
+      v2f acc[RB][RS];
 #pragma unroll
-      for (int kh = 0; kh < K; ++kh) {
-        asm volatile("" ::: "memory");  // one kernel row's LDS operands live at a time
-        const float* rowp = dys + (fi * D::GH1 + pr + K - 1 - kh) * D::DRS * 2 + xs * DCG + 2 * cp;
-        v2f dr[D::RW], wr[K];
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int px = 0; px < RS; ++px) acc[rr][px] = v2f{0.f, 0.f};
+      // staged row pr + ih feeds row rr of the strip through kernel row kh = K - 1 - ih + rr; ih
+      // descending = kh ascending per output (RB = 1: the kernel-row order of the original loop)
+#pragma unroll
+      for (int ih = K + RB - 2; ih >= 0; --ih) {
+        asm volatile("" ::: "memory");  // one staged row's LDS operands live at a time
+        const float* rowp = dys + (fi * D::GH1 + pr + ih) * D::DRS * 2 + xs * DCG + 2 * cp;
+        v2f dr[D::RW];
 #pragma unroll
         for (int j = 0; j < D::RW; ++j) dr[j] = lds2(rowp + j * DCG);
 #pragma unroll
-        for (int kw = 0; kw < K; ++kw) wr[kw] = lds2(wts + (kh * K + kw) * DCG + 2 * cp);
+        for (int rr = 0; rr < RB; ++rr) {
+          const int kh = K - 1 - ih + rr;
+          if (kh < 0 || kh >= K) continue;
+          v2f wr[K];
 #pragma unroll
-        for (int kw = 0; kw < K; ++kw)
+          for (int kw = 0; kw < K; ++kw) wr[kw] = lds2(wts + (kh * K + kw) * DCG + 2 * cp);
 #pragma unroll
-          for (int px = 0; px < RS; ++px) {
-            acc[px] = fma2(dr[px + K - 1 - kw], wr[kw], acc[px]);
-            dw[kh][kw] = fma2(act[px], dr[px + K - 1 - kw], dw[kh][kw]);
-          }
-        // the row's FMAs complete here (otherwise they sink into the per-pixel epilogue and every
-        // row's operands stay live at once)
+          for (int kw = 0; kw < K; ++kw)
 #pragma unroll
-        for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc[px]));
+            for (int px = 0; px < RS; ++px) {
+              acc[rr][px] = fma2(dr[px + K - 1 - kw], wr[kw], acc[rr][px]);
+              dw[kh][kw] = fma2(act[rr][px], dr[px + K - 1 - kw], dw[kh][kw]);
+            }
+          // the row's FMAs complete here (otherwise they sink into the per-pixel epilogue and every
+          // row's operands stay live at once)
 #pragma unroll
-        for (int kw = 0; kw < K; ++kw) asm volatile("" : "+v"(dw[kh][kw]));
+          for (int kw = 0; kw < K; ++kw) asm volatile("" : "+v"(dw[kh][kw]));
+        }
+#pragma unroll
+        for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+          for (int px = 0; px < RS; ++px) asm volatile("" : "+v"(acc[rr][px]));
       }
       // ---- epilogue: g1 = dA * silu'(z1) -> out, BN1 backward sums ----
 #pragma unroll
-      for (int px = 0; px < RS; ++px) pin2(ry[px]);
+      for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+        for (int px = 0; px < RS; ++px) pin2(ry[rr][px]);
       if (rok) {
 #pragma unroll
-        for (int px = 0; px < RS; ++px) {
-          // silu'(z) = s (1 + z (1 - s)) = s + act (1 - s)
-          const v2f dsl = fma2(act[px], 1.0f - sg[px], sg[px]);
-          const v2f gg = round2(acc[px] * dsl, (T*)nullptr);
-          ss += gg;
-          sq = fma2(gg, fma2(raw2_f(ry[px]), is1, mi1), sq);
-          st2(boff(outf, sb + px * pb), gg);
-        }
+        for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+          for (int px = 0; px < RS; ++px) {
+            // silu'(z) = s (1 + z (1 - s)) = s + act (1 - s)
+            const v2f dsl = fma2(act[rr][px], 1.0f - sg[rr][px], sg[rr][px]);
+            const v2f gg = round2(acc[rr][px] * dsl, (T*)nullptr);
+            ss += gg;
+            sq = fma2(gg, fma2(raw2_f(ry[rr][px]), is1, mi1), sq);
+            st2(boff(outf, sb + rr * rowb + px * pb), gg);
+          }
       }
     }
   }
@@ -301,7 +327,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && K == 3 && !PF) ? 3 : 2) voi
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1, bool PF = false>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, bool PF = false, int RB = 1>
 static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const Dw1Bn2& b2, const float* w,
                        const T* Y1, const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab,
                        int64_t slab_cap, float* dW, bool accumulate) {
@@ -310,8 +336,8 @@ static int bwd1_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
-  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS, FR, PF>;
-  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS, FR, PF>, 256>();
+  auto kern = dw_bwd1_kernel<T, K, TH, TW, RS, FR, PF, RB>;
+  const int resident = resident_wgs<dw_bwd1_kernel<T, K, TH, TW, RS, FR, PF, RB>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
@@ -346,13 +372,22 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
   if (!dw_bwd1_covers(g)) return 1;
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   const int H = g.H, W = g.W;
-  // bf16: the software-pipelined form (knob dw_pf) where its registers fit the launch bounds
+  // bf16: the software-pipelined form (knob dw_pf) where its registers fit the launch bounds;
+  // two-row strips (knob dw_rb bit 1) on the even-height tiles
   const bool pf = sizeof(T) == 2 && tune(TK_DW_PF) != 0;
-#define DFD_BWD1(K_, TH_, TW_, RS_, FR_)                                                                         \
-  return pf ? bwd1_launch<T, K_, TH_, TW_, RS_, FR_, sizeof(T) == 2>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows,  \
-                                                           slab, slab_cap, dW, accumulate)                       \
-            : bwd1_launch<T, K_, TH_, TW_, RS_, FR_, false>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, \
-                                                            slab, slab_cap, dW, accumulate)
+  const bool rb = sizeof(T) == 2 && (tune(TK_DW_RB) & 2) != 0;
+#define DFD_BWD1_(K_, TH_, TW_, RS_, FR_, RB_, PFOK_)                                                           \
+  return pf && (PFOK_) ? bwd1_launch<T, K_, TH_, TW_, RS_, FR_, sizeof(T) == 2 && (PFOK_), RB_>(                  \
+                             s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate) \
+                       : bwd1_launch<T, K_, TH_, TW_, RS_, FR_, false, RB_>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, \
+                                                                            stat_rows, slab, slab_cap, dW, accumulate)
+  // (bf16 only; k5 two-row strips leave no registers for the prefetch)
+#define DFD_BWD1(K_, TH_, TW_, RS_, FR_)                                                                 \
+  do {                                                                                                   \
+    if (rb && (TH_) % 2 == 0)                                                                            \
+      DFD_BWD1_(K_, TH_, TW_, RS_, FR_, ((TH_) % 2 == 0 && sizeof(T) == 2 ? 2 : 1), (K_) == 3);         \
+    DFD_BWD1_(K_, TH_, TW_, RS_, FR_, 1, true);                                                          \
+  } while (0)
   if (H == 7 && W == 7) {
     if (g.k == 3) DFD_BWD1(3, 7, 7, 7, 2);
     DFD_BWD1(5, 7, 7, 7, 2);
@@ -363,6 +398,7 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
     return 1;
   }
   if (H % 14 == 0 && W % 14 == 0) DFD_BWD1(5, 14, 14, 7, 1);
+#undef DFD_BWD1_
 #undef DFD_BWD1
   return 1;
 }

@@ -18,11 +18,11 @@ echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 200 python -u tools/pw_sk_bench.py 5 > gpurun_out/r04/a_skb.jsonl 2> gpurun_out/r04/a_skb.err || { echo SKB FAILED; tail -5 gpurun_out/r04/a_skb.err; exit 1; }
 cat gpurun_out/r04/a_skb.jsonl
-timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k schedule_knob -v --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k 'schedule_knob or dw_rb_backward' -v --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_pf.log 2>&1; rc=$?
 echo "schedule-knob tests rc=$rc"; tail -3 gpurun_out/r04/a_pf.log
 [ $rc -eq 0 ] || exit 1
-for r in 1 2; do for v in 0 1; do echo "== dw_pf=$v round $r"; timeout -k 10 120 tools/kbench dw_bwd1 256 dw_pf=$v || exit 1; done; done > gpurun_out/r04/a_kbpf.txt 2>&1 || { echo KBPF FAILED; tail -5 gpurun_out/r04/a_kbpf.txt; exit 1; }
+for r in 1 2; do for v in "dw_pf=0" "dw_pf=1" "dw_rb=2" "dw_pf=1 dw_rb=2"; do echo "== $v round $r"; timeout -k 10 120 tools/kbench dw_bwd1 256 $v || exit 1; done; done > gpurun_out/r04/a_kbpf.txt 2>&1 || { echo KBPF FAILED; tail -5 gpurun_out/r04/a_kbpf.txt; exit 1; }
 cat gpurun_out/r04/a_kbpf.txt
 for r in 1 2; do for v in 0 1; do echo "== dw_rb=$v round $r"; timeout -k 10 120 tools/kbench dw_fwd 256 dw_rb=$v || exit 1; done; done > gpurun_out/r04/a_kbrb.txt 2>&1 || { echo KBRB FAILED; tail -5 gpurun_out/r04/a_kbrb.txt; exit 1; }
 cat gpurun_out/r04/a_kbrb.txt
