@@ -194,7 +194,7 @@ enum { CEPI_STORE = 0, CEPI_STATS = 1, CEPI_SLAB = 2 };
 // Main loop: 32-deep k-steps (two 16-deep halves per operand policy load) through two LDS stages --
 // the next step's gathers are in flight while this step's MFMAs run, and one barrier per step
 // (four per 32 k in the single-buffered form) hands the stages over.  The MFMA sequence over k is
-// unchanged (exact fp32 products, same order).
+// unchanged (exact fp32 products); each step's 32 products are summed into a fresh tile first.
 template <class PA, class PB, int EPI>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __restrict__ C, int ldc, int M, int N,
                                                         int K, int ksplit, const float* __restrict__ bias,
@@ -255,6 +255,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
   for (int k0 = kb; k0 < ke; k0 += 2 * CG_K) {
     const bool more = k0 + 2 * CG_K < ke;
     if (more) fetch(k0 + 2 * CG_K);
+    // two-level summation: each 32-deep step accumulates into a fresh tile, added to the running
+    // sum once per step -- the fp32 rounding error grows with ~32 + K/32 terms instead of K (the
+    // train-mode BatchNorm chain of the ResNet-50 member amplifies conv rounding into its gradients)
+    f32x4_t part[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -262,11 +270,15 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
         const int kk = 4 * s + (lane >> 4);
         const float a0 = As[cur][h][wm + (lane & 15)][kk], a1 = As[cur][h][wm + 16 + (lane & 15)][kk];
         const float b0 = Bs[cur][h][wn + (lane & 15)][kk], b1 = Bs[cur][h][wn + 16 + (lane & 15)][kk];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+        part[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, part[0][0], 0, 0, 0);
+        part[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, part[0][1], 0, 0, 0);
+        part[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, part[1][0], 0, 0, 0);
+        part[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, part[1][1], 0, 0, 0);
       }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] += part[a][b];
     if (more) commit(cur ^ 1, k0 + 2 * CG_K);
     lds_barrier();
     cur ^= 1;

@@ -406,7 +406,11 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
     return -1;
   }
   if constexpr (sizeof(T) == 2) {
-    if (pro_mode == PRO_NONE && tune(TK_PW_SK) != 0) {
+    // the small-K weight-panel kernel where it measured faster (tools/pw_sk_bench.py, round 4): the
+    // forward products with BN statistics (K 80 / 112 / 192: -22 / -14 / -7 %) and the sub-streaming
+    // row counts; the streaming kernel keeps the large stat-free data gradients (+31 / +22 % on sk)
+    // and K = 320 (+15..+24 %)
+    if (pro_mode == PRO_NONE && tune(TK_PW_SK) != 0 && K <= 192 && (stats || M < tune(TK_STREAM_MIN_ROWS))) {
       const int rc = launch_pw_sk(s, A, B, C, R, M, N, K, stats, 1024, stat_rows);
       if (rc <= 0) return rc;
     }

@@ -133,7 +133,8 @@ def test_pw_conv_bf16_late_layers(cuda, case, tile):
     _run(M, N, K, mode, resid, stats, 0, cuda, rpf=49, tile=tile)
 
 
-# the small-K weight-panel kernel (k_pw_sk.hip): every (K, panel width) instantiation the 14x14 / 7x7
+# the small-K weight-panel kernel (k_pw_sk.hip; dispatched for K <= 192 only, K = 320 measured slower):
+# every (K, panel width) instantiation the 14x14 / 7x7
 # stages and conv_head use, with the BN-stat epilogue, plain, and with the residual; rows past the
 # 64-row multiple fall back to the other kernels (last case)
 SK_CASES = [(12544, 1152, 192, 0, False, True),   # blocks.5.x / 6.0 conv_pw forward (K 192, BN 128)

@@ -18,7 +18,7 @@ echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 200 python -u tools/pw_sk_bench.py 5 > gpurun_out/r04/a_skb.jsonl 2> gpurun_out/r04/a_skb.err || { echo SKB FAILED; tail -5 gpurun_out/r04/a_skb.err; exit 1; }
 cat gpurun_out/r04/a_skb.jsonl
-timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k 'schedule_knob or dw_rb_backward' -v --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k 'depthwise_schedule or wgrad_stream' -v -s --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_pf.log 2>&1; rc=$?
 echo "schedule-knob tests rc=$rc"; tail -3 gpurun_out/r04/a_pf.log
 [ $rc -eq 0 ] || exit 1
@@ -37,7 +37,7 @@ timeout -k 10 120 rocprofv3 -L > $R/gpurun_out/r04/counters.txt 2>&1; echo "list
 cd $R
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep > gpurun_out/r04/a_bench.json 2> gpurun_out/r04/a_bench.err || { echo BENCH FAILED; tail -5 gpurun_out/r04/a_bench.err; exit 1; }
 cut -c1-300 gpurun_out/r04/a_bench.json
-timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune pw_sk=1 > gpurun_out/r04/a_bench_sk.json 2> gpurun_out/r04/a_bench_sk.err || { echo BENCH SK FAILED; tail -5 gpurun_out/r04/a_bench_sk.err; exit 1; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune pw_sk=0 > gpurun_out/r04/a_bench_sk.json 2> gpurun_out/r04/a_bench_sk.err || { echo BENCH SK FAILED; tail -5 gpurun_out/r04/a_bench_sk.err; exit 1; }
 cut -c1-300 gpurun_out/r04/a_bench_sk.json
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune dw_pf=1 > gpurun_out/r04/a_bench_pf.json 2> gpurun_out/r04/a_bench_pf.err || { echo BENCH PF FAILED; tail -5 gpurun_out/r04/a_bench_pf.err; exit 1; }
 cut -c1-300 gpurun_out/r04/a_bench_pf.json

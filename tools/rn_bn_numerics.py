@@ -17,7 +17,7 @@ autograd.Function that reproduces one arithmetic form in fp32:
   impl    round 4's kernels: one-pass statistics (conv epilogue), centred apply and backward
   c64     every conv in fp64 rounded to fp32 (the floor set by the BatchNorm arithmetic alone)
 
-usage: python tools/rn_bn_numerics.py [frames] [hw]
+usage: python tools/rn_bn_numerics.py [frames] [hw] | state.pt   (env MODES=impl,ex,...  WATCH=param name)
 """
 import re
 import sys
@@ -193,7 +193,10 @@ def main():
         sd = base.state_dict()
     w = torch.tensor([0.7, 1.3])
     grads = {}
-    for mode in ("f64", "torch", "hip", "fwd", "bwd", "cen", "st", "ap", "ex", "impl", "c64", "c64ap"):
+    import os
+    modes = os.environ.get("MODES", "hip,fwd,bwd,cen,st,ap,ex,impl,c64,c64ap").split(",")
+    watch = os.environ.get("WATCH", "")  # a parameter name to report per mode
+    for mode in ["f64", "torch"] + modes:
         t = ResNet50TrunkCPU().train()
         t.load_state_dict(sd)
         dt = torch.float64 if mode == "f64" else torch.float32
@@ -210,8 +213,10 @@ def main():
         loss.backward()
         grads[mode] = ({re.sub(r"\.(conv|bn)\.(weight|bias)$", r".\2", n): p.grad.detach().clone() for n, p in t.named_parameters()}, f.detach())
     g64, f64 = grads["f64"]
-    for mode in ("torch", "hip", "fwd", "bwd", "cen", "st", "ap", "ex", "impl", "c64", "c64ap"):
+    for mode in ["torch"] + modes:
         g, f = grads[mode]
+        if watch:
+            print(f"{mode:6s} {watch}: rel err {rel(g[watch], g64[watch]):.3e}")
         errs = sorted(((rel(g[n], g64[n]), n) for n in g64), reverse=True)
         l4 = [e for e, n in errs if n.startswith("7.2")]
         print(f"{mode:6s} feat {rel(f, f64):.2e}  worst {errs[0][0]:.4f} ({errs[0][1]})  median "
