@@ -10,14 +10,10 @@ timeout -k 10 300 python -u -m pytest tests/test_vgemm_gpu.py -v -s --timeout 12
   > gpurun_out/r04/a_vg.log 2>&1; rc=$?
 echo "vgemm tests rc=$rc"; tail -4 gpurun_out/r04/a_vg.log
 [ $rc -eq 0 ] || exit 1
-timeout -k 10 300 python -u tools/vgemm_bench.py 5 > gpurun_out/r04/a_vgb.jsonl 2> gpurun_out/r04/a_vgb.err || { echo VGB FAILED; tail -5 gpurun_out/r04/a_vgb.err; exit 1; }
-cat gpurun_out/r04/a_vgb.jsonl
 timeout -k 10 300 python -u -m pytest tests/test_pw_kernels.py -k small_k -v --timeout 120 --timeout-method thread \
   > gpurun_out/r04/a_sk.log 2>&1; rc=$?
 echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
 [ $rc -eq 0 ] || exit 1
-timeout -k 10 200 python -u tools/pw_sk_bench.py 5 > gpurun_out/r04/a_skb.jsonl 2> gpurun_out/r04/a_skb.err || { echo SKB FAILED; tail -5 gpurun_out/r04/a_skb.err; exit 1; }
-cat gpurun_out/r04/a_skb.jsonl
 timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k 'depthwise_schedule or wgrad_stream' -v -s --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_pf.log 2>&1; rc=$?
 echo "schedule-knob tests rc=$rc"; tail -3 gpurun_out/r04/a_pf.log
