@@ -183,9 +183,13 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
     so the grid -- and the fixed-order partial sums of dW and the BN1 statistics -- change); dw_rb
     bit 0 / bit 1, two-row strips in the stride-1 forward / backward (same per-output tap order, the
     BN2 / BN1 / dW partial sums in another pixel order).  None is bit-identical; each must agree with
-    the default step like two summation orders of the same bf16 chain: loss within 1e-2 relative,
-    every gradient tensor cosine >= 0.998 and norm within 3 % (the bounds of the fused-MBConv
-    comparison, test_mbconv7_gpu.py)."""
+    the default step like two summation orders of the same bf16 chain: loss within 1e-2 relative and
+    every gradient tensor cosine >= 0.998, norm within 3 % for the backward-only knobs (the bounds of
+    the fused-MBConv comparison, test_mbconv7_gpu.py); a forward knob perturbs every train-mode BN2
+    statistic of the step, whose rounding flips the early layers' gradients see through all 16
+    blocks: cosine >= 0.99, norm within 5 % (measured worst 0.9965 / 2.6 %; the bf16-vs-fp32 oracle
+    bound is 0.98 / 10 %).  The forward's arithmetic itself is held bit-identical in eval mode
+    (test_dw_rb_forward_eval_bit_identical)."""
     from deepfake_amd import backbone
     prev = dict(backbone.DEFAULT_TUNING)
     try:
@@ -206,7 +210,33 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
         if nb <= 1e-3 * scale:
             continue  # structurally ~zero: rounding residue on both sides
         cos = float(a @ b) / (float(a.norm()) * nb + 1e-30)
-        if cos < 0.998 or abs(float(a.norm()) - nb) > 3e-2 * nb:
+        cmin, ntol = (0.99, 5e-2) if knobs.get("dw_rb", 0) & 1 else (0.998, 3e-2)
+        if cos < cmin or abs(float(a.norm()) - nb) > ntol * nb:
             bad.append((n, round(cos, 6), round(float(a.norm()) / nb, 5)))
     print(f"{knobs} vs default: loss {loss_a:.6f} / {loss_b:.6f}, {len(grads_b)} gradients, outside {bad}")
     assert not bad
+
+
+def test_dw_rb_forward_eval_bit_identical(cuda):
+    """Eval mode (running statistics, no batch sums): the two-row forward strips (dw_rb bit 0)
+    compute every depthwise output from the same taps in the same order as the one-row strips, so
+    the logits are bit-identical."""
+    from deepfake_amd import backbone
+    x, _ = _inputs("b4t8")
+    outs = []
+    prev = dict(backbone.DEFAULT_TUNING)
+    try:
+        for v in (1, 0):
+            backbone.DEFAULT_TUNING["dw_rb"] = v
+            det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
+                                             compute_dtype="bf16")
+            deterministic_init_(det, seed=SEED)
+            det = det.to(cuda).eval()
+            with torch.no_grad():
+                logits, _ = det(x.to(cuda))
+            outs.append(logits.float().cpu())
+    finally:
+        backbone.DEFAULT_TUNING.clear()
+        backbone.DEFAULT_TUNING.update(prev)
+    assert torch.isfinite(outs[1]).all()
+    assert torch.equal(outs[0], outs[1])

@@ -14,7 +14,7 @@ timeout -k 10 300 python -u -m pytest tests/test_pw_kernels.py -k small_k -v --t
   > gpurun_out/r04/a_sk.log 2>&1; rc=$?
 echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
 [ $rc -eq 0 ] || exit 1
-timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k 'depthwise_schedule or wgrad_stream' -v -s --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_b0_224_gpu.py -k 'depthwise_schedule or wgrad_stream or dw_rb_forward' -v -s --timeout 200 --timeout-method thread \
   > gpurun_out/r04/a_pf.log 2>&1; rc=$?
 echo "schedule-knob tests rc=$rc"; tail -3 gpurun_out/r04/a_pf.log
 [ $rc -eq 0 ] || exit 1
