@@ -456,7 +456,7 @@ int dfd_rn_bn_train_finalize(void* stream, const float* stats, int rows, int64_t
     return -1;
   }
   return dfd::launch_bn_finalize((hipStream_t)stream, stats, rows, count, C, gamma, beta, running_mean, running_var,
-                                 momentum, eps, true, mean, invstd, scale, shift);
+                                 momentum, eps, true, mean, invstd, scale, shift, dfd::kConvStatRows);
   DFD_GUARD_END
 }
 
@@ -627,7 +627,7 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
   DFD_GUARD_BEGIN
   hipStream_t s = (hipStream_t)stream;
   if (!A || !B || !C) { dfd::set_error("vgemm: null argument", __FILE__, __LINE__); return -1; }
-  if (op == 0 || op == 2) {  // NT: own kernel (0) or the hipBLASLt comparison (2)
+  if (op == 0 || op == 2 || op == 4 || op == 5) {  // NT: own kernel (0; 4 / 5: 256- / 128-wide tiles) or hipBLASLt (2)
     if (((epi & dfd::VG_BIAS) && !bias) || ((epi & dfd::VG_RESID) && !R) || ((epi & dfd::VG_DGELU) && !Z) ||
         ((epi & dfd::VG_GELU2) && !G)) {
       dfd::set_error("vgemm: epilogue operand missing", __FILE__, __LINE__);
@@ -642,6 +642,7 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
     a.A = (const dfd::bf16*)A; a.B = (const dfd::bf16*)B; a.C = (dfd::bf16*)C; a.R = (const dfd::bf16*)R;
     a.bias = bias; a.Z = (const dfd::bf16*)Z; a.G = (dfd::bf16*)G;
     a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
+    a.bn = op == 4 ? 256 : op == 5 ? 128 : 0;
     return dfd::launch_vgemm_nt(s, a, epi);
   }
   if (op == 1 || op == 3) {  // TN: C (fp32 [N][K]) = A^T . B with A [M][N], B [M][K]
@@ -652,7 +653,7 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
     return dfd::launch_vgemm_tn(s, (const dfd::bf16*)A, N, (const dfd::bf16*)B, K, M, N, K, slab, slab_floats,
                                 (float*)C, false);
   }
-  dfd::set_error("vgemm: op must be 0..3", __FILE__, __LINE__);
+  dfd::set_error("vgemm: op must be 0..5", __FILE__, __LINE__);
   return -1;
   DFD_GUARD_END
 }

@@ -200,7 +200,8 @@ static int cl_forward(hipStream_t s, const ClDims& d, const ClParams& P, float* 
     DFD_TRY(conv_forward(s, g, src, ss, P.conv_w[i], P.conv_b[i], W + L.oWf, Y, W + L.oStats, &rows));
     float* bn = W + L.oBN[i];  // mean, invstd, scale, shift
     DFD_TRY(launch_bn_finalize(s, W + L.oStats, rows, BT * g.Ho * g.Wo, g.Co, P.bn_g[i], P.bn_b[i], bn_run[2 * i],
-                               bn_run[2 * i + 1], momentum, 1e-5f, training != 0, bn, bn + 512, bn + 1024, bn + 1536));
+                               bn_run[2 * i + 1], momentum, 1e-5f, training != 0, bn, bn + 512, bn + 1024, bn + 1536,
+                               kConvStatRows));
     if (i < 3) {
       float* Pout = W + L.oP[i];
       DFD_TRY(bn_relu_pool_fwd(s, Y, nullptr, bn + 1024, bn + 1536, (int)BT, g.Ho, g.Wo, g.Co, L.Hp[i], L.Wp[i], Pout,

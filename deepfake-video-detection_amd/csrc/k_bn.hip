@@ -68,22 +68,56 @@ __device__ void reduce_stat_rows(const float* __restrict__ stats, int rows, int 
 // channels per finalize workgroup: at most 8 rows per row lane (reduce_stat_rows)
 static int fin_ch(int rows) { return rows <= 8 * 64 ? 16 : (rows <= 8 * 128 ? 8 : 4); }
 
+// chan_rows > 0: the rows are centred tile partials (sum, M2 about the tile's own mean) of
+// consecutive chan_rows-row tiles (the conv epilogue, k_conv.hip): var = (sum M2 + sum_t n_t
+// (mean_t - mean)^2) / n, the second term from a pass over the tile sums once the mean is known
+template <int CH>
+__device__ void chan_between(const float* __restrict__ stats, int rows, int C, int64_t count, int chan_rows,
+                             double* sh_m, double& out, double* sh) {
+  constexpr int FIN_RL = 1024 / CH;
+  const int tid = threadIdx.x, cl = tid % CH, rl = tid / CH;
+  const int c = blockIdx.x * CH + cl;
+  double a = 0.0;
+  if (c < C) {
+    const double m = sh_m[cl];
+    for (int r = rl; r < rows; r += FIN_RL) {
+      const int64_t left = count - (int64_t)r * chan_rows, nt = left < chan_rows ? left : chan_rows;
+      const double d = (double)stats[((int64_t)r * 2 + 0) * C + c] / (double)nt - m;
+      a += (double)nt * d * d;
+    }
+  }
+#pragma unroll
+  for (int o = CH; o < 64; o <<= 1) a += __shfl_xor(a, o, 64);
+  const int wave = tid >> 6;
+  if ((tid & 63) < CH) sh[wave * CH + cl] = a;
+  __syncthreads();
+  out = 0.0;
+  if (tid < CH)
+    for (int w = 0; w < 1024 / 64; ++w) out += sh[w * CH + tid];
+}
+
 template <int FIN_CH>
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restrict__ stats, int rows, int64_t count,
                                                            int C, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float* run_mean,
                                                            float* run_var, float momentum, float eps, int training,
-                                                           float* mean, float* invstd, float* scale, float* shift) {
-  __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
-  double s = 0.0, q = 0.0;
+                                                           float* mean, float* invstd, float* scale, float* shift,
+                                                           int chan_rows) {
+  __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH], sh_m[FIN_CH];
+  double s = 0.0, q = 0.0, between = 0.0;
   if (training) reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
   const int c = blockIdx.x * FIN_CH + tid;
+  if (training && chan_rows > 0) {
+    if (tid < FIN_CH) sh_m[tid] = s / (double)count;
+    __syncthreads();
+    chan_between<FIN_CH>(stats, rows, C, count, chan_rows, sh_m, between, sh_s);
+  }
   if (tid < FIN_CH && c < C) {
     float mu, is;
     if (training) {
       const double m = s / (double)count;
-      double var = q / (double)count - m * m;
+      double var = chan_rows > 0 ? (q + between) / (double)count : q / (double)count - m * m;
       if (var < 0.0) var = 0.0;
       mu = (float)m;
       is = (float)(1.0 / sqrt(var + (double)eps));
@@ -106,11 +140,11 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
 
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps, bool training,
-                       float* mean, float* invstd, float* scale, float* shift) {
+                       float* mean, float* invstd, float* scale, float* shift, int chan_rows) {
   const int ch = training ? fin_ch(rows) : 16;
 #define DFD_FIN(CH)                                                                                                 \
   hipLaunchKernelGGL((bn_finalize_kernel<CH>), dim3(cdiv(C, CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, beta, \
-                     run_mean, run_var, momentum, eps, training ? 1 : 0, mean, invstd, scale, shift)
+                     run_mean, run_var, momentum, eps, training ? 1 : 0, mean, invstd, scale, shift, chan_rows)
   if (ch == 16) DFD_FIN(16);
   else if (ch == 8) DFD_FIN(8);
   else DFD_FIN(4);

@@ -18,6 +18,7 @@ namespace dfd {
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 constexpr int CG_T = 64, CG_K = 16;
+static_assert(CG_T == kConvStatRows, "BN partial rows of conv_forward");
 
 // Division by a launch-invariant divisor without the ~30-instruction integer division: q = x / d
 // for every 32-bit x as (mulhi(x, m) + x) >> l with l = ceil(log2 d), m = 2^32 (2^l - d) / d + 1
@@ -295,21 +296,39 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
         if (m < M && n < N) {
           float v = acc[a][b][r];
           if (bias) v += bias[n];
+          acc[a][b][r] = v;
           Cz[(int64_t)m * ldc + n] = v;
-          if (EPI == CEPI_STATS) { cs[b] += v; cq[b] += v * v; }
+          if (EPI == CEPI_STATS) cs[b] += v;
         }
       }
   if constexpr (EPI == CEPI_STATS) {
-    // per column: lanes with equal (lane & 15) hold its 4-row groups -> xor 16, 32; then the
-    // two row-halves of the tile (waves 0/1 and 2/3) in a fixed order through LDS
+    // BatchNorm partials of the 64-row tile, centred: (sum, M2 = sum (v - tile mean)^2) per column,
+    // merged over tiles in fp64 by the finalize (Chan) -- the one-pass sum of squares cancels when
+    // |mean| >> std.  Per column: lanes with equal (lane & 15) hold its 4-row groups -> xor 16, 32;
+    // then the two row-halves of the tile (waves 0/1 and 2/3) in a fixed order through LDS
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       cs[b] += __shfl_xor(cs[b], 16, 64); cs[b] += __shfl_xor(cs[b], 32, 64);
+      if (lane < 16) red[wave >> 1][0][wn + b * 16 + lane] = cs[b];
+    }
+    lds_barrier();
+    const float inv_n = 1.0f / (float)min(CG_T, M - m0);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int cl = wn + b * 16 + (lane & 15);
+      const float tmean = (red[0][0][cl] + red[1][0][cl]) * inv_n;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm + a * 16 + 4 * (lane >> 4) + r, n = n0 + cl;
+          if (m < M && n < N) {
+            const float d = acc[a][b][r] - tmean;
+            cq[b] += d * d;
+          }
+        }
       cq[b] += __shfl_xor(cq[b], 16, 64); cq[b] += __shfl_xor(cq[b], 32, 64);
-      if (lane < 16) {
-        red[wave >> 1][0][wn + b * 16 + lane] = cs[b];
-        red[wave >> 1][1][wn + b * 16 + lane] = cq[b];
-      }
+      if (lane < 16) red[wave >> 1][1][wn + b * 16 + lane] = cq[b];
     }
     lds_barrier();
     if (tid < 2 * CG_T) {

@@ -5,7 +5,9 @@
 //
 // gfx950 design (cdna_hip_programming.md section 5: the 256^2 LDS-DMA template):
 //   * 256 x 256 output tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N), 128 x 64 each),
-//     v_mfma_f32_16x16x32_bf16, fp32 accumulators (128 per lane), one workgroup per CU;
+//     v_mfma_f32_16x16x32_bf16, fp32 accumulators (128 per lane), one workgroup per CU; 256 x 128
+//     tiles (4 x 2 waves of 64 x 64) for the 768-wide products, whose 256-wide tiles fill only
+//     1.2 dispatch waves;
 //   * operands move HBM -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR
 //     staging), 64-deep K-steps double-buffered (2 x 64 KiB): the next K-step's DMA is in flight
 //     while the current one's fragments are read and multiplied;
@@ -43,13 +45,15 @@ __device__ const uint4 g_vzero[32] = {};      // 512 B of zeros: the DMA source 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ---------------------------------------------------------------- NT: C = A . B^T
-// One K-step image of an operand: [256 rows][64 k] bf16, 128-B rows, chunk (16 B) c of row r at
-// slot c ^ ((r >> 1) & 7).  Wave w fills rows 32w .. 32w+31 with 4 DMA instructions of 8 rows.
+// One K-step image of an operand: [ROWS rows][64 k] bf16, 128-B rows, chunk (16 B) c of row r at
+// slot c ^ ((r >> 1) & 7).  Wave w fills rows (ROWS/8) w .. with ROWS/64 DMA instructions of 8 rows.
+template <int ROWS = VT>
 __device__ __forceinline__ void stage_nt(const bf16* __restrict__ G, int64_t ld, int row0, int rows, int k0, char* img,
                                          int w, int lane) {
+  constexpr int IPW = ROWS / 64;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = w * 4 + i;
+  for (int i = 0; i < IPW; ++i) {
+    const int q = w * IPW + i;
     const int r = 8 * q + (lane >> 3);
     const int gc = (lane & 7) ^ ((r >> 1) & 7);
     const int gr = min(row0 + r, rows - 1);  // rows past the end: any valid row (their outputs are not stored)
@@ -98,86 +102,100 @@ __device__ __forceinline__ s16x8 frag_tn(const char* img, int base, int s, int l
 }
 
 // ---------------------------------------------------------------- shared pieces
+template <int MI = 8, int NJ = 4>
 struct Acc {
-  f32x4 v[8][4];
+  f32x4 v[MI][NJ];
 };
 
-template <bool TN>
-__device__ __forceinline__ void mma_step(const char* Ai, const char* Bi, int wm, int wn, int lane, Acc& acc) {
+// one 64-deep step of a wave's MI x NJ block of 16 x 16 MFMA tiles at (rbase, cbase) of the tile
+template <bool TN, int MI, int NJ>
+__device__ __forceinline__ void mma_step(const char* Ai, const char* Bi, int rbase, int cbase, int lane,
+                                         Acc<MI, NJ>& acc) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    s16x8 af[8], bfr[4];
+    s16x8 af[MI], bfr[NJ];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = TN ? frag_tn(Ai, wm * 128 + 16 * i, s, lane) : frag_nt(Ai, wm * 128 + 16 * i, s, lane);
+    for (int i = 0; i < MI; ++i) af[i] = TN ? frag_tn(Ai, rbase + 16 * i, s, lane) : frag_nt(Ai, rbase + 16 * i, s, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = TN ? frag_tn(Bi, wn * 64 + 16 * j, s, lane) : frag_nt(Bi, wn * 64 + 16 * j, s, lane);
+    for (int j = 0; j < NJ; ++j) bfr[j] = TN ? frag_tn(Bi, cbase + 16 * j, s, lane) : frag_nt(Bi, cbase + 16 * j, s, lane);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc.v[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc.v[i][j], 0, 0, 0);
+      for (int j = 0; j < NJ; ++j) acc.v[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc.v[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   }
 }
 
-// the accumulators of waves with wm == pass into the [128][EPS] fp32 staging image
-__device__ __forceinline__ void epi_put(float* E, const Acc& acc, int wn, int lane) {
+// a wave's accumulators into the fp32 staging image E (row stride eps) at (r0, c0)
+template <int MI, int NJ>
+__device__ __forceinline__ void epi_put(float* E, const Acc<MI, NJ>& acc, int r0, int c0, int eps, int lane) {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) E[(16 * i + 4 * (lane >> 4) + e) * EPS + wn * 64 + 16 * j + (lane & 15)] = acc.v[i][j][e];
+      for (int e = 0; e < 4; ++e) E[(r0 + 16 * i + 4 * (lane >> 4) + e) * eps + c0 + 16 * j + (lane & 15)] = acc.v[i][j][e];
 }
 
 __device__ __forceinline__ void st8bf(bf16* p, const float (&v)[8]) { st8(p, v); }
 
 // ---------------------------------------------------------------- kernels
-template <int EP>
+// BNT = 256: 8 waves as 2 (M) x 4 (N), 128 x 64 each; BNT = 128 (N = 768-wide products: 2.3 instead of
+// 1.2 dispatch waves of tiles, so the last wave idles less): 4 (M) x 2 (N) waves of 64 x 64
+template <int EP, int BNT>
 __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
+  constexpr int WMN = BNT == VT ? 2 : 4, WNN = 8 / WMN;  // waves along M / N
+  constexpr int MI = VT / WMN / 16, NJ = BNT / WNN / 16;
+  constexpr int BIMG = BNT * VK * 2;                    // B operand's K-step image
+  constexpr int STAGE = VTILE + BIMG;
+  constexpr int ES = BNT + 4;                           // epilogue row stride (floats)
+  static_assert(2 * STAGE <= VLDS && 128 * ES * 4 <= VLDS, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[VLDS];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int w = uni(tid >> 6), wm = w >> 2, wn = w & 3;
+  const int w = uni(tid >> 6), wm = w / WNN, wn = w % WNN;
   const int L = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
   const int tm = L / a.tiles_n, tn = L - tm * a.tiles_n;
-  const int row0 = tm * VT, col0 = tn * VT;
-  Acc acc;
+  const int row0 = tm * VT, col0 = tn * BNT;
+  Acc<MI, NJ> acc;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc.v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc.v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = a.K / VK;
-  stage_nt(a.A, a.lda, row0, a.M, 0, smem, w, lane);
-  stage_nt(a.B, a.ldb, col0, a.N, 0, smem + VTILE, w, lane);
+  stage_nt<VT>(a.A, a.lda, row0, a.M, 0, smem, w, lane);
+  stage_nt<BNT>(a.B, a.ldb, col0, a.N, 0, smem + VTILE, w, lane);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * 2 * VTILE;
+    char* cur = smem + (kt & 1) * STAGE;
     if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * 2 * VTILE;
-      stage_nt(a.A, a.lda, row0, a.M, (kt + 1) * VK, nxt, w, lane);
-      stage_nt(a.B, a.ldb, col0, a.N, (kt + 1) * VK, nxt + VTILE, w, lane);
+      char* nxt = smem + ((kt + 1) & 1) * STAGE;
+      stage_nt<VT>(a.A, a.lda, row0, a.M, (kt + 1) * VK, nxt, w, lane);
+      stage_nt<BNT>(a.B, a.ldb, col0, a.N, (kt + 1) * VK, nxt + VTILE, w, lane);
     }
-    mma_step<false>(cur, cur + VTILE, wm, wn, lane, acc);
+    mma_step<false>(cur, cur + VTILE, wm * (VT / WMN), wn * (BNT / WNN), lane, acc);
     __syncthreads();  // this K-step's reads done everywhere; the next one's DMA landed (vmcnt(0))
   }
   // epilogue: two passes of 128 rows through LDS
+  constexpr int VPR = BNT / 8, RPS = 512 / VPR;  // 8-column vectors per row, rows per sweep
   float* E = reinterpret_cast<float*>(smem);
-  const int v = tid & 31, rsub = tid >> 5;  // 8-column vector, row within a 16-row sweep
+  const int v = tid % VPR, rsub = tid / VPR;
   const int c = col0 + 8 * v;
   float bias[8];
   if constexpr ((EP & VG_BIAS) != 0) ld8f(a.bias + c, bias);
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) epi_put(E, acc, wn, lane);
+    const int wr0 = wm * (VT / WMN) - pass * 128;  // this wave's first row within the pass
+    if (wr0 >= 0 && wr0 < 128) epi_put(E, acc, wr0, wn * (BNT / WNN), ES, lane);
     __syncthreads();
 #pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
-      const int rl = it * 16 + rsub;
+    for (int it = 0; it < 128 / RPS; ++it) {
+      const int rl = it * RPS + rsub;
       const int row = row0 + pass * 128 + rl;
       if (row < a.M) {
         float o[8];
-        const float4 x0 = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v);
-        const float4 x1 = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v + 4);
+        const float4 x0 = *reinterpret_cast<const float4*>(E + rl * ES + 8 * v);
+        const float4 x1 = *reinterpret_cast<const float4*>(E + rl * ES + 8 * v + 4);
         o[0] = x0.x; o[1] = x0.y; o[2] = x0.z; o[3] = x0.w; o[4] = x1.x; o[5] = x1.y; o[6] = x1.z; o[7] = x1.w;
         if constexpr ((EP & VG_BIAS) != 0) {
 #pragma unroll
@@ -217,7 +235,7 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
   const int tp = t / a.tiles_q, tq = t - tp * a.tiles_q;
   const int p0 = tp * VT, q0 = tq * VT;
   const int m_begin = split * a.mchunk, m_end = min(a.M, m_begin + a.mchunk);
-  Acc acc;
+  Acc<8, 4> acc;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -235,7 +253,7 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
       stage_tn(a.X1, a.ld1, m_begin + (kt + 1) * VK, m_end, p0, nxt, w, lane);
       stage_tn(a.X2, a.ld2, m_begin + (kt + 1) * VK, m_end, q0, nxt + VTILE, w, lane);
     }
-    mma_step<true>(cur, cur + VTILE, wm, wn, lane, acc);
+    mma_step<true>(cur, cur + VTILE, wm * 128, wn * 64, lane, acc);
     __syncthreads();
   }
   float* E = reinterpret_cast<float*>(smem);
@@ -243,7 +261,7 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
   float* out = a.slab + (int64_t)split * a.P * a.Q;
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
-    if (wm == pass) epi_put(E, acc, wn, lane);
+    if (wm == pass) epi_put(E, acc, 0, wn * 64, EPS, lane);
     __syncthreads();
 #pragma unroll 2
     for (int it = 0; it < 8; ++it) {
@@ -260,17 +278,30 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
 }  // namespace
 
 bool vgemm_nt_covers(int64_t M, int N, int K) {
-  return M > 0 && M < (1ll << 31) && N % VT == 0 && K % VK == 0 && K > 0;
+  return M > 0 && M < (1ll << 31) && N % 128 == 0 && K % VK == 0 && K > 0;
 }
 bool vgemm_tn_covers(int64_t M, int P, int Q) { return M > 0 && M < (1ll << 31) && P % VT == 0 && Q % VT == 0; }
+
+// the 128-wide tile where 256-wide tiles would leave the last dispatch wave mostly idle: N % 256 != 0,
+// or fewer than ~2 waves of 256 x 256 tiles (ViT-B's 768-wide products at M = 25,216: 297 tiles on
+// 256 CUs)
+static int vgemm_nt_bn(int64_t M, int N) {
+  if (N % VT) return 128;
+  const int64_t t256 = cdiv64(M, VT) * (N / VT);
+  return t256 < 2 * 256 ? 128 : VT;
+}
 
 int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   if (!vgemm_nt_covers(a0.M, a0.N, a0.K)) { set_error("vgemm: shape not covered", __FILE__, __LINE__); return -1; }
   VgemmArgs a = a0;
-  a.tiles_n = a.N / VT;
+  const int bn = a0.bn ? a0.bn : vgemm_nt_bn(a.M, a.N);
+  if (bn != 128 && (bn != VT || a.N % VT)) { set_error("vgemm: tile width", __FILE__, __LINE__); return -1; }
+  a.tiles_n = a.N / bn;
   const int tiles = cdiv(a.M, VT) * a.tiles_n;
-  switch (ep) {
-#define DFD_VG(E) case E: hipLaunchKernelGGL((vgemm_nt_kernel<E>), dim3(tiles), dim3(512), 0, s, a); break;
+  switch (ep * 2 + (bn == 128)) {
+#define DFD_VG(E)                                                                                       \
+  case 2 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT>), dim3(tiles), dim3(512), 0, s, a); break; \
+  case 2 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128>), dim3(tiles), dim3(512), 0, s, a); break;
     DFD_VG(0) DFD_VG(VG_BIAS) DFD_VG(VG_BIAS | VG_RESID) DFD_VG(VG_BIAS | VG_GELU2) DFD_VG(VG_DGELU)
 #undef DFD_VG
     default: set_error("vgemm: epilogue not instantiated", __FILE__, __LINE__); return -1;

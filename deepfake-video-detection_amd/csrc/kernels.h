@@ -224,9 +224,12 @@ bool dw_fwd1_enabled();
 
 // ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------
 // finalize training stats: mean/invstd/scale/shift + running update (momentum); eval: from running
+// chan_rows > 0: stats rows are centred (sum, M2) partials of consecutive chan_rows-row tiles
+// (conv_forward's epilogue: kConvStatRows), merged in fp64 (Chan); 0: plain (sum, sum of squares)
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps,
-                       bool training, float* mean, float* invstd, float* scale, float* shift);
+                       bool training, float* mean, float* invstd, float* scale, float* shift, int chan_rows = 0);
+constexpr int kConvStatRows = 64;  // rows per BN partial of conv_forward (k_conv.hip CG_T)
 // X = Y*scale + shift (+ R)
 template <typename T>
 int launch_bn_apply(hipStream_t s, const T* Y, const float* scale, const float* shift, const T* R, T* X,

@@ -70,7 +70,7 @@ int launch_node_mean_bwd(hipStream_t s, const float* dG, int B, int N, int D, fl
 
 int launch_gelu(hipStream_t s, const bf16* Z, bf16* out, int64_t n, bool backward);
 
-// The large bf16 GEMMs of the trunk (k_vgemm.hip): 256 x 256 tiles, LDS-DMA double buffering.
+// The large bf16 GEMMs of the trunk (k_vgemm.hip): 256 x 256 / 256 x 128 tiles, LDS-DMA double buffering.
 // NT: C[M][N] = A[M][K] . B[N][K]^T with the epilogue flags below (fp32, rounded once);
 // TN: W[P][Q] = sum_m X1[m][p] X2[m][q] (fp32, split over m into slabs summed in a fixed order).
 enum VgEpi { VG_BIAS = 1, VG_RESID = 2, VG_GELU2 = 4 /* C = Z, G = gelu(Z) */, VG_DGELU = 8 /* C *= gelu'(Z) */ };
@@ -84,6 +84,7 @@ struct VgemmArgs {
   bf16* G;            // gelu(C) [M][ldc] (VG_GELU2)
   int64_t lda, ldb, ldc;
   int M, N, K, tiles_n;
+  int bn;             // tile width 256 / 128; 0: chosen by shape (launch_vgemm_nt)
 };
 struct VgemmTnArgs {
   const bf16* X1;

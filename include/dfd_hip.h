@@ -186,13 +186,16 @@ DFD_API int dfd_rn_avgpool(void* stream, int dtype, const void* x, int N, int HW
  * convolutions are exact-fp32 implicit-GEMM MFMA kernels (no im2col buffer, no library GEMM). ---- */
 /* BN-stat partial rows a training conv forward writes: stats needs rows * 2 * Cout floats */
 DFD_API int64_t dfd_rn_conv_stat_rows(int N, int Ho, int Wo);
-/* y (N,Ho,Wo,Cout) = conv(x, w) without bias, and the BN-stat partials of y's channels; x read
- * through element strides xs4 = (n, y, x, c); w OIHW [Cout][Cin][kh][kw]; wpack >= Cout*Cin*kh*kw */
+/* y (N,Ho,Wo,Cout) = conv(x, w) without bias, and the BN-stat partials of y's channels: per 64-row
+ * tile of y, [sum][Cout] then [M2][Cout] (M2 = sum of squared deviations from the tile's own mean;
+ * dfd_rn_bn_train_finalize merges the tiles in fp64); x read through element strides
+ * xs4 = (n, y, x, c); w OIHW [Cout][Cin][kh][kw]; wpack >= Cout*Cin*kh*kw */
 DFD_API int dfd_rn_train_conv_fwd(void* stream, const float* x, const int64_t* xs4, int N, int H, int W, int Cin,
                                   const float* w, int Cout, int kh, int kw, int stride, int pad, float* wpack,
                                   float* y, float* stats);
-/* batch mean / invstd / scale / shift of a train-mode BN from the partials; updates running_mean /
- * running_var with momentum (unbiased variance), like torch */
+/* batch mean / invstd / scale / shift of a train-mode BN from dfd_rn_train_conv_fwd's partials
+ * (Chan's merge of the tiles' (count, mean, M2)); updates running_mean / running_var with momentum
+ * (unbiased variance), like torch */
 DFD_API int dfd_rn_bn_train_finalize(void* stream, const float* stats, int rows, int64_t count, int C,
                                      const float* gamma, const float* beta, float* running_mean,
                                      float* running_var, float momentum, float eps, float* mean, float* invstd,
@@ -282,7 +285,8 @@ DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int
 
 /* The ViT trunk's large bf16 GEMMs (k_vgemm.hip; test / measurement seam): op 0 (NT):
  * C[M][N] (bf16) = A[M][K] . B[N][K]^T with the epilogue mask epi: 1 + bias[N] (fp32), 2 + R[M][N],
- * 4 also G = gelu(C) (C keeps the pre-activation), 8 C *= gelu'(Z[M][N]); N % 256 == 0, K % 64 == 0.
+ * 4 also G = gelu(C) (C keeps the pre-activation), 8 C *= gelu'(Z[M][N]); N % 128 == 0, K % 64 == 0;
+ * the tile width (256 or 128 columns) is chosen by shape; ops 4 / 5 force 256 (N % 256 == 0) / 128.
  * op 1 (TN): C (fp32 [N][K]) = A^T . B for A [M][N], B [M][K] (bf16), split over M into slab
  * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0.  ops 2 / 3: the same
  * products through hipBLASLt (measurement comparison only; op 2 takes epi 0..3). */

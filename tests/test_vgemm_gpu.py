@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 P = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())  # noqa: E731
 
 
-def _nt(cuda, M, N, K, epi, seed):
+def _nt(cuda, M, N, K, epi, seed, op=0):
     g = torch.Generator(device=cuda).manual_seed(seed)
     A = torch.randn(M, K, device=cuda, generator=g).bfloat16()
     B = (torch.randn(N, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
@@ -30,7 +30,7 @@ def _nt(cuda, M, N, K, epi, seed):
     G = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16) if epi & 4 else None
     C = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
     lib = _lib.load()
-    _lib.check(lib.dfd_vgemm(None, 0, P(A), P(B), P(C), P(R), P(bias), P(Z), P(G), M, N, K, epi, None, 0))
+    _lib.check(lib.dfd_vgemm(None, op, P(A), P(B), P(C), P(R), P(bias), P(Z), P(G), M, N, K, epi, None, 0))
     torch.cuda.synchronize()
     ref = A.float() @ B.float().T
     if bias is not None:
@@ -49,11 +49,12 @@ def _close(got, ref):
     torch.testing.assert_close(got.float(), ref.bfloat16().float(), rtol=8e-3, atol=1e-3 * scale)
 
 
+@pytest.mark.parametrize("op", [4, 5])  # 256- / 128-wide tiles (op 0 picks one by shape)
 @pytest.mark.parametrize("M,N,K,epi", [(600, 256, 64, 0), (394, 768, 768, 1), (394, 2304, 768, 1),
                                        (1000, 768, 3072, 3), (394, 3072, 768, 5), (777, 3072, 768, 8),
                                        (8 * 197, 768, 2304, 0)])
-def test_vgemm_nt_vs_fp32(cuda, M, N, K, epi):
-    C, G, ref = _nt(cuda, M, N, K, epi, M + N + K + epi)
+def test_vgemm_nt_vs_fp32(cuda, M, N, K, epi, op):
+    C, G, ref = _nt(cuda, M, N, K, epi, M + N + K + epi, op)
     _close(C, ref)
     if G is not None:  # gelu of the stored (rounded) pre-activation
         torch.testing.assert_close(G.float(), F.gelu(C.float()).bfloat16().float(), rtol=8e-3, atol=1e-3)
@@ -91,8 +92,22 @@ def test_vgemm_deterministic(cuda):
 
 
 def test_vgemm_refuses_uncovered(cuda):
-    A = torch.zeros(64, 100, device=cuda).bfloat16()
-    B = torch.zeros(200, 100, device=cuda).bfloat16()
+    A = torch.zeros(64, 128, device=cuda).bfloat16()
+    B = torch.zeros(200, 128, device=cuda).bfloat16()
     C = torch.zeros(64, 200, device=cuda).bfloat16()
     lib = _lib.load()
-    assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 100, 0, None, 0) != 0
+    assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 100, 0, None, 0) != 0  # K % 64
+    assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 128, 0, None, 0) != 0  # N % 128
+
+
+def test_vgemm_nt_tile_widths_agree(cuda):
+    """the two tile widths sum every output's K in the same order: bit-identical results (and op 0's
+    shape rule picks one of them), 128-wide-only N (N % 256 != 0) refused by the 256-wide op"""
+    outs = [_nt(cuda, 1000, 768, 768, 3, 5, op)[0] for op in (0, 4, 5)]
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    C, _, ref = _nt(cuda, 300, 640, 128, 1, 9, 0)  # N = 5 x 128
+    _close(C, ref)
+    A = torch.zeros(64, 128, device=cuda).bfloat16()
+    B = torch.zeros(640, 128, device=cuda).bfloat16()
+    C = torch.zeros(64, 640, device=cuda).bfloat16()
+    assert _lib.load().dfd_vgemm(None, 4, P(A), P(B), P(C), None, None, None, None, 64, 640, 128, 0, None, 0) != 0

@@ -10,6 +10,8 @@ timeout -k 10 300 python -u -m pytest tests/test_vgemm_gpu.py -v -s --timeout 12
   > gpurun_out/r04/a_vg.log 2>&1; rc=$?
 echo "vgemm tests rc=$rc"; tail -4 gpurun_out/r04/a_vg.log
 [ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python -u tools/vgemm_bench.py 5 > gpurun_out/r04/a_vgb.jsonl 2> gpurun_out/r04/a_vgb.err || { echo VGB FAILED; tail -5 gpurun_out/r04/a_vgb.err; exit 1; }
+cat gpurun_out/r04/a_vgb.jsonl
 timeout -k 10 300 python -u -m pytest tests/test_pw_kernels.py -k small_k -v --timeout 120 --timeout-method thread \
   > gpurun_out/r04/a_sk.log 2>&1; rc=$?
 echo "small-K tests rc=$rc"; tail -3 gpurun_out/r04/a_sk.log
