@@ -372,8 +372,9 @@ int launch_dw_bwd1(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
   if (!dw_bwd1_covers(g)) return 1;
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   const int H = g.H, W = g.W;
-  // bf16: the software-pipelined form (knob dw_pf) where its registers fit the launch bounds;
-  // two-row strips (knob dw_rb bit 1) on the even-height tiles
+  // bf16: the software-pipelined form (knob dw_pf, default on: kbench dw_bwd1 over the 12 stride-1
+  // layers 1,377-1,380 -> 1,350-1,357 us, round 4) where its registers fit the launch bounds;
+  // two-row strips (knob dw_rb bit 1, default off: 1,397 us) on the even-height tiles
   const bool pf = sizeof(T) == 2 && tune(TK_DW_PF) != 0;
   const bool rb = sizeof(T) == 2 && (tune(TK_DW_RB) & 2) != 0;
 #define DFD_BWD1_(K_, TH_, TW_, RS_, FR_, RB_, PFOK_)                                                           \

@@ -275,7 +275,9 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
       !dw_fwd1_enabled())
     return 0;
   const int H = g.Ho, W = g.Wo;  // output map
-  const bool rb = (tune(TK_DW_RB) & 1) != 0;  // two output rows per strip (knob dw_rb bit 0)
+  // two output rows per strip (knob dw_rb bit 0, default on: kbench dw_fwd over the 16 layers
+  // 1,037-1,042 -> 1,010-1,023 us, round 4)
+  const bool rb = (tune(TK_DW_RB) & 1) != 0;
   int rc;
   if (g.s == 2) {
     // k3 stride 2 (112->56, 28->14): the 8x8 tile kernel is as fast or faster (kbench: 214 vs 246,

@@ -54,7 +54,7 @@ struct Tuning {
 // fused depthwise backward / channel-pair kernels on; tiled-GEMM config automatic (-1); weight
 // gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on; small-K
 // weight-panel GEMM (k_pw_sk.hip) off until measured
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 0, 0};
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {

@@ -257,9 +257,10 @@ def test_second_backward_refused_and_cumulative_momentum(cuda):
     f.sum().backward(retain_graph=True)
     with pytest.raises(RuntimeError, match="second backward"):
         f.sum().backward()
-    # reference in fp64, atol 5e-5: at 2 frames of 64^2 the deepest layers normalise 8 rows, so any fp32
-    # implementation's rounding is the size of the bound (a wrong momentum rule -- the default 0.1
-    # instead of the cumulative 1/2 -- would be off by ~the batch means themselves)
+    # reference in fp64, each buffer within 1e-3 relative L2: at 2 frames of 64^2 the deepest layers
+    # normalise 8 rows of activations that carry the trunk's fp32 chain error (measured worst element
+    # 6e-5 absolute on 7.2.bn1.running_mean), while a wrong momentum rule -- the default 0.1 instead
+    # of the cumulative 1/2 -- would be off by ~the batch means themselves (tens of %)
     t, ref = _pair(8, cuda)
     ref = ref.double()
     for m in list(t.modules()) + list(ref.modules()):
@@ -276,4 +277,4 @@ def test_second_backward_refused_and_cumulative_momentum(cuda):
         if name.endswith("num_batches_tracked"):
             assert int(b) == int(rb[name]) == 2, name
         else:
-            torch.testing.assert_close(b.double(), rb[name], rtol=1e-4, atol=5e-5, msg=lambda m: f"{name}: {m}")
+            assert _rel(b, rb[name]) <= 1e-3, (name, _rel(b, rb[name]))
