@@ -651,7 +651,7 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
       return dfd::blaslt_wgrad_split(s, (const dfd::bf16*)A, (const dfd::bf16*)B, (float*)C, M, N, K, 4, slab,
                                      slab_floats);
     return dfd::launch_vgemm_tn(s, (const dfd::bf16*)A, N, (const dfd::bf16*)B, K, M, N, K, slab, slab_floats,
-                                (float*)C, false);
+                                (float*)C, false, (float*)G);
   }
   dfd::set_error("vgemm: op must be 0..5", __FILE__, __LINE__);
   return -1;

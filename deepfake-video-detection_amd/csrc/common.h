@@ -174,6 +174,12 @@ __device__ __forceinline__ float geluf_(float x) { return 0.5f * x * (1.0f + erf
 __device__ __forceinline__ float dgeluf_(float x) {
   return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
+// gelu(x) and gelu'(x) from one erf (the same expressions as geluf_ / dgeluf_: identical values)
+__device__ __forceinline__ void gelu_pair_(float x, float& g, float& d) {
+  const float e = 1.0f + erff(x * 0.70710678118654752f);
+  g = 0.5f * x * e;
+  d = 0.5f * e + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
 
 struct Pro {
   const float* scale;  // [C]

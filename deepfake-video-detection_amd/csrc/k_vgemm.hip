@@ -176,8 +176,10 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
     mma_step<false>(cur, cur + VTILE, wm * (VT / WMN), wn * (BNT / WNN), lane, acc);
     __syncthreads();  // this K-step's reads done everywhere; the next one's DMA landed (vmcnt(0))
   }
-  // epilogue: two passes of 128 rows through LDS
-  constexpr int VPR = BNT / 8, RPS = 512 / VPR;  // 8-column vectors per row, rows per sweep
+  // epilogue: two passes of 128 rows through LDS; a pass's residual / derivative rows are loaded
+  // before its staging barrier (their latency under the LDS round trip, not per row)
+  constexpr int VPR = BNT / 8, RPS = 512 / VPR, NIT = 128 / RPS;  // 8-column vectors per row, rows per sweep
+  constexpr bool LD = (EP & (VG_RESID | VG_DGELU)) != 0;
   float* E = reinterpret_cast<float*>(smem);
   const int v = tid % VPR, rsub = tid / VPR;
   const int c = col0 + 8 * v;
@@ -185,11 +187,20 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
   if constexpr ((EP & VG_BIAS) != 0) ld8f(a.bias + c, bias);
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
+    uint4 xr[LD ? NIT : 1];
+    if constexpr (LD) {
+      const bf16* src = (EP & VG_RESID) != 0 ? a.R : a.Z;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int row = min(row0 + pass * 128 + it * RPS + rsub, a.M - 1);
+        xr[it] = *reinterpret_cast<const uint4*>(src + (int64_t)row * a.ldc + c);
+      }
+    }
     const int wr0 = wm * (VT / WMN) - pass * 128;  // this wave's first row within the pass
     if (wr0 >= 0 && wr0 < 128) epi_put(E, acc, wr0, wn * (BNT / WNN), ES, lane);
     __syncthreads();
-#pragma unroll 2
-    for (int it = 0; it < 128 / RPS; ++it) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
       const int rl = it * RPS + rsub;
       const int row = row0 + pass * 128 + rl;
       if (row < a.M) {
@@ -201,24 +212,23 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] += bias[j];
         }
-        if constexpr ((EP & VG_RESID) != 0) {
-          float r[8];
-          ld8(a.R + (int64_t)row * a.ldc + c, r);
+        if constexpr (LD) {
+          const uint32_t wv[4] = {xr[it].x, xr[it].y, xr[it].z, xr[it].w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+          for (int j = 0; j < 8; ++j) {
+            const float xv = __uint_as_float((j & 1) ? (wv[j >> 1] & 0xffff0000u) : (wv[j >> 1] << 16));
+            if constexpr ((EP & VG_RESID) != 0) o[j] += xv;
+            else o[j] *= xv;  // VG_DGELU: the stored gelu'
+          }
         }
-        if constexpr ((EP & VG_DGELU) != 0) {
-          float z[8];
-          ld8(a.Z + (int64_t)row * a.ldc + c, z);
+        if constexpr ((EP & VG_GELU2) != 0) {
+          // C = gelu'(z), G = gelu(z) of the stored (rounded) pre-activation z
+          float g[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] *= dgeluf_(z[j]);
+          for (int j = 0; j < 8; ++j) gelu_pair_(Tr<bf16>::round(o[j]), g[j], o[j]);
+          st8bf(a.G + (int64_t)row * a.ldc + c, g);
         }
         st8bf(a.C + (int64_t)row * a.ldc + c, o);
-        if constexpr ((EP & VG_GELU2) != 0) {  // gelu of the stored (rounded) pre-activation
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = geluf_(Tr<bf16>::round(o[j]));
-          st8bf(a.G + (int64_t)row * a.ldc + c, o);
-        }
       }
     }
     __syncthreads();
@@ -246,6 +256,13 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
     stage_tn(a.X2, a.ld2, m_begin, m_end, q0, smem + VTILE, w, lane);
   }
   __syncthreads();
+  // the bias gradient of the linear whose output gradient is X1: colsum[p] = sum_m X1[m][p] as a
+  // product with a ones operand (exact products, fixed order) on the workgroups of tile column 0,
+  // each wave taking 2 of its half's 8 row blocks (+2 MFMAs and 4 transposed reads per 32-deep
+  // step; replaces a separate column-sum pass over X1)
+  const bool csum = a.colsum && tq == 0;
+  f32x4 cacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const s16x8 ones = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};  // bf16 1.0
   for (int kt = 0; kt < nk; ++kt) {
     char* cur = smem + (kt & 1) * 2 * VTILE;
     if (kt + 1 < nk) {
@@ -254,11 +271,27 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
       stage_tn(a.X2, a.ld2, m_begin + (kt + 1) * VK, m_end, q0, nxt + VTILE, w, lane);
     }
     mma_step<true>(cur, cur + VTILE, wm * 128, wn * 64, lane, acc);
+    if (csum) {
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+          cacc[ii] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tn(cur, wm * 128 + 16 * (2 * wn + ii), s2, lane), ones,
+                                                             cacc[ii], 0, 0, 0);
+    }
     __syncthreads();
+  }
+  const int64_t srow = (int64_t)a.P * a.Q + (a.colsum ? a.P : 0);  // slab row length
+  if (csum && (lane & 15) == 0) {
+    float* cs = a.slab + (int64_t)split * srow + (int64_t)a.P * a.Q + p0 + wm * 128;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[16 * (2 * wn + ii) + 4 * (lane >> 4) + e] = cacc[ii][e];
   }
   float* E = reinterpret_cast<float*>(smem);
   const int v = tid & 31, rsub = tid >> 5;
-  float* out = a.slab + (int64_t)split * a.P * a.Q;
+  float* out = a.slab + (int64_t)split * srow;
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
     if (wm == pass) epi_put(E, acc, 0, wn * 64, EPS, lane);
@@ -319,19 +352,24 @@ int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap) {
 }
 
 int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, int64_t ld2, int64_t M, int P, int Q,
-                    float* slab, int64_t slab_cap, float* W, bool accumulate) {
+                    float* slab, int64_t slab_cap, float* W, bool accumulate, float* colsum_out) {
   if (!vgemm_tn_covers(M, P, Q)) { set_error("vgemm_tn: shape not covered", __FILE__, __LINE__); return -1; }
-  if ((int64_t)P * Q > slab_cap) { set_error("vgemm_tn: slab too small", __FILE__, __LINE__); return -1; }
+  const int64_t srow = (int64_t)P * Q + (colsum_out ? P : 0);
+  if (srow > slab_cap) { set_error("vgemm_tn: slab too small", __FILE__, __LINE__); return -1; }
   VgemmTnArgs a{};
   a.X1 = X1; a.ld1 = ld1; a.X2 = X2; a.ld2 = ld2; a.M = (int)M; a.P = P; a.Q = Q;
   a.tiles_p = P / VT; a.tiles_q = Q / VT;
+  a.colsum = colsum_out != nullptr;
   int splits = vgemm_tn_splits(M, P, Q, slab_cap);
+  splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / srow));
   a.mchunk = (int)(cdiv64(cdiv64(M, splits), VK) * VK);
   splits = (int)cdiv64(M, a.mchunk);
   a.slab = slab;
   hipLaunchKernelGGL(vgemm_tn_kernel, dim3(splits * a.tiles_p * a.tiles_q), dim3(512), 0, s, a);
   DFD_HIP_CHECK(hipGetLastError());
-  return launch_reduce_slabs(s, slab, splits, (int64_t)P * Q, W, accumulate);
+  if (!colsum_out) return launch_reduce_slabs(s, slab, splits, (int64_t)P * Q, W, accumulate);
+  DFD_TRY(launch_reduce_slabs_strided(s, slab, splits, (int64_t)P * Q, srow, W, accumulate));
+  return launch_reduce_slabs_strided(s, slab + (int64_t)P * Q, splits, P, srow, colsum_out, accumulate);
 }
 
 }  // namespace dfd

@@ -621,34 +621,38 @@ int launch_node_mean_bwd(hipStream_t s, const float* dG, int B, int N, int D, fl
   return 0;
 }
 
-// ---- exact-erf GELU as separate passes for the hipBLASLt MLP (blaslt.cpp): G = gelu(Z) and, in
-// place, dZ *= gelu'(Z); bf16, 8 elements per lane ----
-__global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16* __restrict__ Z, bf16* __restrict__ G, int64_t n8) {
+// ---- exact-erf GELU passes of the bf16 MLP for shapes the vgemm kernels do not cover (k_vgemm.hip
+// applies the same in its epilogues), 8 elements per lane:
+//   GELU_PAIR  G = gelu(Z) and, in place, Z := gelu'(Z)  (the forward keeps the derivative, not Z)
+//   GELU_MULD  dZ *= D  (D = the derivative kept by the forward)
+__global__ __launch_bounds__(256) void gelu_pair_kernel(bf16* __restrict__ Z, bf16* __restrict__ G, int64_t n8) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
-    float z[8];
+    float z[8], g[8];
     ld8(Z + i * 8, z);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) z[j] = geluf_(z[j]);
-    st8(G + i * 8, z);
+    for (int j = 0; j < 8; ++j) gelu_pair_(z[j], g[j], z[j]);
+    st8(G + i * 8, g);
+    st8(Z + i * 8, z);
   }
 }
-__global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16* __restrict__ Z, bf16* __restrict__ dZ, int64_t n8) {
+__global__ __launch_bounds__(256) void gelu_muld_kernel(const bf16* __restrict__ D, bf16* __restrict__ dZ, int64_t n8) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
-    float z[8], d[8];
-    ld8(Z + i * 8, z);
+    float dd[8], d[8];
+    ld8(D + i * 8, dd);
     ld8(dZ + i * 8, d);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] *= dgeluf_(z[j]);
+    for (int j = 0; j < 8; ++j) d[j] *= dd[j];
     st8(dZ + i * 8, d);
   }
 }
-int launch_gelu(hipStream_t s, const bf16* Z, bf16* out, int64_t n, bool backward) {
+int launch_gelu(hipStream_t s, bf16* Z, bf16* out, int64_t n, int mode) {
   if (n <= 0) return 0;
   if (n % 8) { set_error("gelu: element count must be a multiple of 8", __FILE__, __LINE__); return -1; }
   const int64_t n8 = n / 8;
   const int g = (int)std::min<int64_t>(cdiv64(n8, 256), 4096);
-  if (backward) hipLaunchKernelGGL(gelu_bwd_kernel, dim3(g), dim3(256), 0, s, Z, out, n8);
-  else hipLaunchKernelGGL(gelu_fwd_kernel, dim3(g), dim3(256), 0, s, Z, out, n8);
+  if (mode == GELU_PAIR) hipLaunchKernelGGL(gelu_pair_kernel, dim3(g), dim3(256), 0, s, Z, out, n8);
+  else if (mode == GELU_MULD) hipLaunchKernelGGL(gelu_muld_kernel, dim3(g), dim3(256), 0, s, Z, out, n8);
+  else { set_error("gelu: mode", __FILE__, __LINE__); return -1; }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

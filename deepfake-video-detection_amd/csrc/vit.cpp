@@ -171,7 +171,9 @@ inline AttnArgs attn_args(int images, int nt, const T* qkv, T* O, float* lse) {
   return a;
 }
 
-// C[M][N] = A . B^T (+ bias) (+ R), epi a mask of VgEpi (G: gelu(C) for VG_GELU2; Z: VG_DGELU)
+// C[M][N] = A . B^T (+ bias) (+ R), epi a mask of VgEpi.  bf16 MLP: VG_GELU2 leaves G = gelu(pre) and
+// C = gelu'(pre); VG_DGELU multiplies by that stored derivative (Z).  fp32: C = pre-activation and
+// EPI_DGELU takes gelu' of Z itself (the fp32 forward keeps Z).
 template <typename T>
 int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N, int K,
         int epi_extra = 0, const T* Z = nullptr, T* G = nullptr) {
@@ -183,22 +185,30 @@ int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bi
       a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
       return launch_vgemm_nt(s, a, epi);
     }
-    if (epi_extra & VG_GELU2) {  // uncovered shape: Z, then G = gelu(Z) as its own pass
-      DFD_TRY(launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE,
-                                (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0)));
-      return launch_gelu(s, C, G, M * N, false);
+    // uncovered shapes: the GEMM, then the same GELU arithmetic as a pass
+    const int base = (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0);
+    if (epi_extra & VG_GELU2) {
+      DFD_TRY(launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE, base));
+      return launch_gelu(s, C, G, M * N, GELU_PAIR);
+    }
+    if (epi_extra & VG_DGELU) {
+      DFD_TRY(launch_tf_gemm<T>(s, A, B, C, R, bias, nullptr, M, N, K, PRO_NONE, base));
+      return launch_gelu(s, const_cast<T*>(Z), C, M * N, GELU_MULD);
     }
   }
   return launch_tf_gemm<T>(s, A, B, C, R, bias, Z, M, N, K, PRO_NONE,
                            (bias ? EPI_BIAS : 0) | (R ? EPI_RESID : 0) | ((epi_extra & VG_DGELU) ? EPI_DGELU : 0));
 }
-// dW[N][K] = dY^T . X
+// dW[N][K] = dY^T . X, and the bias gradient dB[N] = sum_m dY[m] (in the same launch on the own
+// bf16 kernel; a column-sum pass otherwise)
 template <typename T>
-int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float* slab, int64_t slab_cap, float* dW) {
+int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float* slab, int64_t slab_cap, float* dW,
+          float* dB, float* part, int64_t part_cap) {
   if constexpr (sizeof(T) == 2)
-    if (vgemm_tn_covers(M, N, K)) return launch_vgemm_tn(s, dY, N, X, K, M, N, K, slab, slab_cap, dW, false);
+    if (vgemm_tn_covers(M, N, K)) return launch_vgemm_tn(s, dY, N, X, K, M, N, K, slab, slab_cap, dW, false, dB);
   Pro none{};
-  return launch_pw_wgrad<T>(s, dY, X, M, N, K, PRO_NONE, none, slab, slab_cap, dW, false);
+  DFD_TRY(launch_pw_wgrad<T>(s, dY, X, M, N, K, PRO_NONE, none, slab, slab_cap, dW, false));
+  return launch_colsum<T>(s, dY, M, N, part, part_cap, dB, false);
 }
 
 template <typename T>
@@ -281,21 +291,19 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     // ---- MLP: dZ = (dx W2) * gelu'(Z); dW2 = dx^T gelu(Z); dh2 = dZ W1 ----
     DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D, VG_DGELU, w.at(b.Z)));
     if constexpr (sizeof(T) == 2) {  // G = gelu(Z) kept by the forward
-      DFD_TRY(wgrad<T>(s, dx, w.at(b.G), M, D, FF, slab, L.slab_cap, g[10]));
+      DFD_TRY(wgrad<T>(s, dx, w.at(b.G), M, D, FF, slab, L.slab_cap, g[10], g[11], part, L.part_cap));
     } else {
       DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
+      DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
     }
-    DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
     DFD_TRY(lin<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, M, D, FF));
-    DFD_TRY(wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, slab, L.slab_cap, g[8]));
-    DFD_TRY(launch_colsum<T>(s, dZ, M, FF, part, L.part_cap, g[9], false));
+    DFD_TRY(wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, slab, L.slab_cap, g[8], g[9], part, L.part_cap));
     // LN2: dxm = dx + LN2'(dh2)
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.xm), D, dh, D, q[6], w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), dx, dxm, M, D, part, L.part_cap, g[6], g[7], false)));
     // ---- attention projection ----
     DFD_TRY(lin<T>(s, dxm, w.at(b.wpT), dO, nullptr, nullptr, M, D, D));
-    DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4]));
-    DFD_TRY(launch_colsum<T>(s, dxm, M, D, part, L.part_cap, g[5], false));
+    DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4], g[5], part, L.part_cap));
     // ---- attention core: dP = dO v^T ; dS = scale P (dP - rowdot) ; dq = dS k ; dk = dS^T q ; dv = P^T dO
     if constexpr (sizeof(T) == 2) {  // fused (k_attn.hip): recomputes P from the saved log-sum-exp
       AttnArgs at = attn_args(I, nt, qkv, w.at(b.O), w.template at<float>(b.P));
@@ -317,16 +325,14 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     }
     // ---- qkv projection and LN1: dx_l = dxm + LN1'(dqkv Wqkv) ----
     DFD_TRY(lin<T>(s, dqkv, w.at(b.wqkvT), dh, nullptr, nullptr, M, D, D3));
-    DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2]));
-    DFD_TRY(launch_colsum<T>(s, dqkv, M, D3, part, L.part_cap, g[3], false));
+    DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2], g[3], part, L.part_cap));
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.x), D, dh, D, q[0], w.template at<float>(b.mu1), w.template at<float>(b.rs1),
                                 dxm, dx, M, D, part, L.part_cap, g[0], g[1], false)));
   }
   // tokens: dcls, dpos, patch rows -> patch-embedding weight / bias
   T* dpe = sc.at(L.dpe);
   DFD_TRY(launch_tokens_bwd<T>(s, dx, I, nt, D, dpe, G[1], G[0]));
-  DFD_TRY(wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, slab, L.slab_cap, G[2]));
-  return launch_colsum<T>(s, dpe, M0, D, part, L.part_cap, G[3], false);
+  return wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, slab, L.slab_cap, G[2], G[3], part, L.part_cap);
 }
 
 // ------------------------------------------------------------------------------------------

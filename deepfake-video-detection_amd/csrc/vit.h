@@ -68,20 +68,24 @@ int launch_relu_drop_bwd(hipStream_t s, const float* Y, const float* dD, float* 
 int launch_node_mean(hipStream_t s, const float* H, int B, int N, int D, float* G);
 int launch_node_mean_bwd(hipStream_t s, const float* dG, int B, int N, int D, float* dH);
 
-int launch_gelu(hipStream_t s, const bf16* Z, bf16* out, int64_t n, bool backward);
+enum GeluPass { GELU_PAIR = 0, GELU_MULD = 1 };
+int launch_gelu(hipStream_t s, bf16* Z, bf16* out, int64_t n, int mode);
 
 // The large bf16 GEMMs of the trunk (k_vgemm.hip): 256 x 256 / 256 x 128 tiles, LDS-DMA double buffering.
 // NT: C[M][N] = A[M][K] . B[N][K]^T with the epilogue flags below (fp32, rounded once);
 // TN: W[P][Q] = sum_m X1[m][p] X2[m][q] (fp32, split over m into slabs summed in a fixed order).
-enum VgEpi { VG_BIAS = 1, VG_RESID = 2, VG_GELU2 = 4 /* C = Z, G = gelu(Z) */, VG_DGELU = 8 /* C *= gelu'(Z) */ };
+// VG_GELU2: Z = the rounded pre-activation, G = gelu(Z) and C = gelu'(Z) (the MLP backward needs only
+// the derivative: computing it here, where erf(Z) is at hand, keeps the erf out of the backward);
+// VG_DGELU: C *= Z[m][n] with Z the derivative a VG_GELU2 launch stored
+enum VgEpi { VG_BIAS = 1, VG_RESID = 2, VG_GELU2 = 4, VG_DGELU = 8 };
 struct VgemmArgs {
   const bf16* A;
   const bf16* B;
   bf16* C;
   const bf16* R;      // residual [M][ldc] (VG_RESID)
   const float* bias;  // [N] (VG_BIAS)
-  const bf16* Z;      // pre-activation [M][ldc] (VG_DGELU)
-  bf16* G;            // gelu(C) [M][ldc] (VG_GELU2)
+  const bf16* Z;      // gelu'(pre-activation) [M][ldc] (VG_DGELU)
+  bf16* G;            // gelu(pre-activation) [M][ldc] (VG_GELU2)
   int64_t lda, ldb, ldc;
   int M, N, K, tiles_n;
   int bn;             // tile width 256 / 128; 0: chosen by shape (launch_vgemm_nt)
@@ -89,16 +93,19 @@ struct VgemmArgs {
 struct VgemmTnArgs {
   const bf16* X1;
   const bf16* X2;
-  float* slab;
+  float* slab;        // [split][P*Q (+ P when colsum)]
   int64_t ld1, ld2;
   int M, P, Q, tiles_p, tiles_q, mchunk;
+  int colsum;         // also sum X1's columns (a linear's bias gradient) into the slab rows' tail
 };
 bool vgemm_nt_covers(int64_t M, int N, int K);
 bool vgemm_tn_covers(int64_t M, int P, int Q);
 int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a, int ep);
 int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap);
+// colsum_out (optional): colsum_out[p] = sum_m X1[m][p] in the same launch (the slab then needs
+// splits x (P*Q + P) floats: vgemm_tn_splits(M, P, Q + 1, ...) x P x (Q + 1) is enough)
 int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, int64_t ld2, int64_t M, int P, int Q,
-                    float* slab, int64_t slab_cap, float* W, bool accumulate);
+                    float* slab, int64_t slab_cap, float* W, bool accumulate, float* colsum_out = nullptr);
 
 template <typename T>
 __device__ __forceinline__ void lds_st8v(T* p, const float (&v)[8]) { st8(p, v); }

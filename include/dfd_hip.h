@@ -288,7 +288,8 @@ DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int
  * 4 also G = gelu(C) (C keeps the pre-activation), 8 C *= gelu'(Z[M][N]); N % 128 == 0, K % 64 == 0;
  * the tile width (256 or 128 columns) is chosen by shape; ops 4 / 5 force 256 (N % 256 == 0) / 128.
  * op 1 (TN): C (fp32 [N][K]) = A^T . B for A [M][N], B [M][K] (bf16), split over M into slab
- * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0.  ops 2 / 3: the same
+ * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0; with G non-null also
+ * G (fp32 [N]) = the column sums of A (a linear's bias gradient) from the same launch.  ops 2 / 3: the same
  * products through hipBLASLt (measurement comparison only; op 2 takes epi 0..3). */
 DFD_API int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const void* R, const float* bias,
                       const void* Z, void* G, int64_t M, int N, int K, int epi, float* slab, int64_t slab_floats);

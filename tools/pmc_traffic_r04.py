@@ -5,11 +5,14 @@ usage: python tools/pmc_traffic_r04.py gpurun_out/r04/traffic [profiles/r04/traf
 Per kernel instance and launch site of the B0 training step (256 frames, 224^2, bf16):
   write_bytes = WRITE_SIZE (x 1024), divided by the write calibration factor of tools/fetch_calib
                 (16-B/lane stores: 1.0 in round 2; re-measured here);
-  fetch_bytes = when the request-size counters exist (TCC_EA0_RDREQ / _32B / TCC_BUBBLE):
-                  32 RDREQ_32B + 64 (RDREQ - BUBBLE - RDREQ_32B) + 128 BUBBLE,
+  fetch_bytes = when the request-size counters exist (TCC_EA0_RDREQ and _32B / _64B / _128B):
+                  32 RDREQ_32B + 64 RDREQ_64B + 128 RDREQ_128B (+ 64 per request in no class),
                 validated on the calibration kernels' known byte counts (contiguous 16-B/lane and
-                64-B channel-slice reads) -- the method that does not depend on the access pattern;
-                otherwise FETCH_SIZE (x 1024) divided by the calibration factor of the access pattern.
+                64-B channel-slice reads) -- the method that does not depend on the access pattern
+                (FETCH_SIZE's own expression, 128 TCC_BUBBLE + 64 (RDREQ - BUBBLE - 32B) + 32 32B,
+                tallies the 128-B requests of 16-B/lane streaming reads at 64 B on gfx950, round 4
+                calibration: 0.5 of the known bytes); otherwise FETCH_SIZE (x 1024) divided by the
+                calibration factor of the access pattern.
   algorithmic_bytes = SURVEY 8(d) / DESIGN.md section 4 per-launch figures (one read of every input,
                 one write of every output).
 Launch sites are assigned by the fixed backward order of the plan (blocks 6.0 -> 0.0).  The file
@@ -75,8 +78,9 @@ def read(d, sub):
 
 
 def raw_bytes(c):
-    rd, r32, bub = c["TCC_EA0_RDREQ_sum"], c["TCC_EA0_RDREQ_32B_sum"], c["TCC_BUBBLE_sum"]
-    return 32 * r32 + 64 * (rd - bub - r32) + 128 * bub
+    rd, r32 = c["TCC_EA0_RDREQ_sum"], c["TCC_EA0_RDREQ_32B_sum"]
+    r64, r128 = c["TCC_EA0_RDREQ_64B_sum"], c["TCC_EA0_RDREQ_128B_sum"]
+    return 32 * r32 + 64 * r64 + 128 * r128 + 64 * max(0.0, rd - r32 - r64 - r128)
 
 
 def calib(d, sub, fn):
@@ -106,7 +110,7 @@ def main():
     fetch, write = read(d, "fetch"), read(d, "write")
     raw = read(d, "raw") if raw_ok else None
     wf = cal["write_mode3"]
-    out = {"_method": ("fetch: request-size counters 32 RDREQ_32B + 64 (RDREQ - BUBBLE - RDREQ_32B) + 128 BUBBLE "
+    out = {"_method": ("fetch: request-size counters 32 RDREQ_32B + 64 RDREQ_64B + 128 RDREQ_128B "
                        "(validated on tools/fetch_calib's known bytes: raw_mode*)" if raw_ok else
                        "fetch: FETCH_SIZE / the 64-B channel-slice calibration factor (fetch_mode1)") +
                       "; write: WRITE_SIZE / write_mode3; separate rocprofv3 --pmc passes, kernel trace only",

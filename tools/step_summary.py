@@ -12,15 +12,20 @@ import statistics
 import sys
 
 CLASSES = [("fused 7x7 MBConv fwd", r"mbconv7"), ("fused 1x1 backward", r"pwl_bwd|pw_fold_bwd"), ("depthwise fwd", r"dw_fwd"), ("depthwise bwd", r"dw_bwd|dw_dgrad|dw_wgrad"),
-           ("1x1 conv fwd/dgrad", r"pw_gemm|pw_stream_kernel"), ("1x1 conv wgrad", r"pw_wgrad|col_sums"),
+           ("1x1 conv fwd/dgrad", r"pw_gemm|pw_stream_kernel|pw_sk_kernel"), ("1x1 conv wgrad", r"pw_wgrad|col_sums"),
            ("stem", r"stem_"), ("BN glue", r"bn_|frame_reduce_kernel<[^,]+, 2>"),
            ("SE", r"se_|frame_sum|frame_reduce|mfma_small|sum_parts"),
            ("slab reductions", r"slabs"), ("head / loss", r"linear_|ce_|attn|relu_drop|pool"),
            ("optimizer", r"adam|sumsq|norm_fin|cast_params"), ("other", r".")]
 
 
+def base(name):
+    """kernel name without its argument list (anonymous-namespace qualifiers dropped first)"""
+    return name.replace("(anonymous namespace)::", "").split("(")[0]
+
+
 def klass(name):
-    n = name.split("(")[0]
+    n = base(name)
     for k, pat in CLASSES:
         if re.search(pat, n):
             return k
@@ -49,7 +54,7 @@ def main():
         print(f"{k:20s} {t:9.1f} {n:9d}")
     per = {}
     for r in med:
-        p = per.setdefault(r["Kernel_Name"].split("(")[0], [0.0, 0])
+        p = per.setdefault(base(r["Kernel_Name"]), [0.0, 0])
         p[0] += dur(r)
         p[1] += 1
     print("\nlargest kernels (us/step, launches, avg us)")
@@ -58,7 +63,7 @@ def main():
     if "--order" in sys.argv:  # every launch of the median step in issue order
         print("\nlaunch order (us)")
         for i, r in enumerate(med):
-            print(f"{i:4d} {dur(r):8.1f}  {r['Kernel_Name'].split('(')[0][:110]}")
+            print(f"{i:4d} {dur(r):8.1f}  {base(r['Kernel_Name'])[:110]}")
     if probe:
         v = [dur(r) for r in rows if probe in r["Kernel_Name"]]
         if v:
