@@ -619,7 +619,7 @@ int dfd_attention(void* stream, int backward, int images, int heads, int nt, flo
 int64_t dfd_blaslt_calls(void) { return dfd::blaslt_calls(); }
 
 int64_t dfd_vgemm_tn_slab_floats(int64_t M, int N, int K) {
-  return (int64_t)dfd::vgemm_tn_splits(M, N, K, INT64_MAX) * N * K;
+  return (int64_t)dfd::vgemm_tn_splits(M, N, K, INT64_MAX) * ((int64_t)N * K + N);  // + the column sums
 }
 
 int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const void* R, const float* bias,

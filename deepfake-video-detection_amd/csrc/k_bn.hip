@@ -104,10 +104,18 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
                                                            float* mean, float* invstd, float* scale, float* shift,
                                                            int chan_rows) {
   __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH], sh_m[FIN_CH];
-  double s = 0.0, q = 0.0, between = 0.0;
-  if (training) reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
   const int c = blockIdx.x * FIN_CH + tid;
+  // the channel's parameters and running buffers, loaded before the reduction (their latency under
+  // the stat-row loads instead of after them: the kernel is a chain of dependent memory round trips)
+  float p_g = 0.f, p_b = 0.f, p_rm = 0.f, p_rv = 0.f;
+  if (tid < FIN_CH && c < C) {
+    p_g = gamma[c];
+    p_b = beta[c];
+    if (run_mean) { p_rm = run_mean[c]; p_rv = run_var[c]; }
+  }
+  double s = 0.0, q = 0.0, between = 0.0;
+  if (training) reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   if (training && chan_rows > 0) {
     if (tid < FIN_CH) sh_m[tid] = s / (double)count;
     __syncthreads();
@@ -123,18 +131,18 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
       is = (float)(1.0 / sqrt(var + (double)eps));
       if (run_mean) {
         const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
-        run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
-        run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+        run_mean[c] = (float)((1.0 - momentum) * p_rm + momentum * m);
+        run_var[c] = (float)((1.0 - momentum) * p_rv + momentum * unb);
       }
     } else {
-      mu = run_mean[c];
-      is = 1.0f / sqrtf(run_var[c] + eps);
+      mu = p_rm;
+      is = 1.0f / sqrtf(p_rv + eps);
     }
-    const float sc = gamma[c] * is;
+    const float sc = p_g * is;
     mean[c] = mu;
     invstd[c] = is;
     scale[c] = sc;
-    shift[c] = beta[c] - mu * sc;
+    shift[c] = p_b - mu * sc;
   }
 }
 
@@ -356,22 +364,30 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
                                                               float* dgamma, float* dbeta, int accumulate,
                                                               float* coef, int centred) {
   __shared__ double sh_s[1024 / 64 * FIN_CH], sh_q[1024 / 64 * FIN_CH];
-  double s = 0.0, q = 0.0;
-  reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   const int tid = threadIdx.x;
   const int c = blockIdx.x * FIN_CH + tid;
+  // per-channel operands loaded before the reduction (see bn_finalize_kernel)
+  float p_g = 0.f, p_is = 0.f, p_mu = 0.f, p_db = 0.f, p_dg = 0.f;
+  if (tid < FIN_CH && c < C) {
+    p_g = gamma[c];
+    p_is = invstd[c];
+    if (!centred) p_mu = mean[c];
+    if (accumulate) { p_db = dbeta[c]; p_dg = dgamma[c]; }
+  }
+  double s = 0.0, q = 0.0;
+  reduce_stat_rows<FIN_CH>(stats, rows, C, s, q, sh_s, sh_q);
   if (tid < FIN_CH && c < C) {
     const float db = (float)s, dg = (float)q;
-    if (accumulate) { dbeta[c] += db; dgamma[c] += dg; }
+    if (accumulate) { dbeta[c] = p_db + db; dgamma[c] = p_dg + dg; }
     else { dbeta[c] = db; dgamma[c] = dg; }
-    const double gm = gamma[c], is = invstd[c];
+    const double gm = p_g, is = p_is;
     const double k1 = gm * is;
     double k2 = 0.0, k3 = 0.0;
     if (training) {
       const double n = (double)count;
       k2 = -gm * is * is * q / n;
       k3 = -gm * is * s / n;
-      if (!centred) k3 += gm * is * is * (double)mean[c] * q / n;
+      if (!centred) k3 += gm * is * is * (double)p_mu * q / n;
     }
     coef[c] = (float)k1;
     coef[C + c] = (float)k2;
@@ -675,6 +691,14 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
   const int c = blockIdx.x * 64 + cl;
   const int64_t n = (int64_t)frames * C;
   const PartSum pf{part, hsplit, n};
+  // per-channel operands loaded before the reduction (see bn_finalize_kernel)
+  float p_g = 0.f, p_is = 0.f, p_mu = 0.f, p_db = 0.f, p_dg = 0.f;
+  if (sl == 0 && c < C) {
+    p_g = gamma[c];
+    p_is = invstd[c];
+    p_mu = mean[c];
+    if (accumulate) { p_db = dbeta[c]; p_dg = dgamma[c]; }
+  }
   double s = 0.0, q = 0.0;
   if (c < C) {
     const int per = (frames + FF_SL - 1) / FF_SL;
@@ -709,14 +733,14 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_frames_kernel(
     q = 0.0;
     for (int k = 0; k < FF_SL; ++k) { s += red[0][k][cl]; q += red[1][k][cl]; }
     const float db = (float)s, dg = (float)q;
-    if (accumulate) { dbeta[c] += db; dgamma[c] += dg; }
+    if (accumulate) { dbeta[c] = p_db + db; dgamma[c] = p_dg + dg; }
     else { dbeta[c] = db; dgamma[c] = dg; }
-    const double gm = gamma[c], is = invstd[c];
+    const double gm = p_g, is = p_is;
     double k2 = 0.0, k3 = 0.0;
     if (training) {
       const double cnt = (double)count;
       k2 = -gm * is * is * q / cnt;
-      k3 = -gm * is * s / cnt + gm * is * is * (double)mean[c] * q / cnt;
+      k3 = -gm * is * s / cnt + gm * is * is * (double)p_mu * q / cnt;
     }
     coef[c] = (float)(gm * is);
     coef[C + c] = (float)k2;
