@@ -17,3 +17,8 @@ for v in 100000 0 40000; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep --tune fold_min_rows=$v > $O/c_bench_fold$v.json 2> $O/c_bench_fold$v.err || { echo "BENCH fold $v FAILED"; tail -5 $O/c_bench_fold$v.err; exit 1; }
   echo "fold_min_rows=$v: $(cut -c1-260 $O/c_bench_fold$v.json | grep -o '"ms_per_step": [0-9.]*')"
 done
+timeout -k 10 400 python -u -m pytest tests/test_cnn_lstm.py tests/test_resnet_train_gpu.py -q --timeout 200 --timeout-method thread > $O/c_cnn.log 2>&1; rc=$?
+echo "cnn-lstm / resnet-train tests rc=$rc"; tail -2 $O/c_cnn.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench_temporal.py --model cnnlstm --no-cpu-baseline > $O/c_cnnb.jsonl 2> $O/c_cnnb.err || { echo CNNB FAILED; tail -5 $O/c_cnnb.err; exit 1; }
+cut -c1-200 $O/c_cnnb.jsonl
