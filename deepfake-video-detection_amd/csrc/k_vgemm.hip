@@ -368,6 +368,9 @@ int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, 
   hipLaunchKernelGGL(vgemm_tn_kernel, dim3(splits * a.tiles_p * a.tiles_q), dim3(512), 0, s, a);
   DFD_HIP_CHECK(hipGetLastError());
   if (!colsum_out) return launch_reduce_slabs(s, slab, splits, (int64_t)P * Q, W, accumulate);
+  // a linear's bias gradient stored right after its weight gradient (named_parameters order): one
+  // reduction over the whole slab row
+  if (colsum_out == W + (int64_t)P * Q) return launch_reduce_slabs(s, slab, splits, srow, W, accumulate);
   DFD_TRY(launch_reduce_slabs_strided(s, slab, splits, (int64_t)P * Q, srow, W, accumulate));
   return launch_reduce_slabs_strided(s, slab + (int64_t)P * Q, splits, P, srow, colsum_out, accumulate);
 }

@@ -69,18 +69,23 @@ def test_vgemm_nt_vs_fp32(cuda, M, N, K, epi, op):
         torch.testing.assert_close(C.float(), d.bfloat16().float(), rtol=8e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("colsum", [False, True])
+@pytest.mark.parametrize("colsum", [False, True, "adjacent"])
 @pytest.mark.parametrize("M,N,K", [(394, 768, 256), (8 * 197, 768, 3072), (100, 256, 512), (4096, 2304, 768)])
 def test_vgemm_tn_vs_fp32(cuda, M, N, K, colsum):
     """weight gradient; with colsum the bias gradient (column sums of A) from the same launch, rows past
-    the end of the last m-step contributing zero"""
+    the end of the last m-step contributing zero ("adjacent": the bias gradient stored right after the
+    weight gradient, as in the flat gradient buffer, reduced in one pass)"""
     g = torch.Generator(device=cuda).manual_seed(M * 7 + N)
     A = torch.randn(M, N, device=cuda, generator=g).bfloat16()
     B = torch.randn(M, K, device=cuda, generator=g).bfloat16()
     lib = _lib.load()
     slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(M, N, K), device=cuda)
-    W = torch.full((N, K), float("nan"), device=cuda)
-    cs = torch.full((N,), float("nan"), device=cuda) if colsum else None
+    if colsum == "adjacent":
+        flat = torch.full((N * K + N,), float("nan"), device=cuda)
+        W, cs = flat[:N * K].view(N, K), flat[N * K:]
+    else:
+        W = torch.full((N, K), float("nan"), device=cuda)
+        cs = torch.full((N,), float("nan"), device=cuda) if colsum else None
     _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, P(cs), M, N, K, 0, P(slab), slab.numel()))
     torch.cuda.synchronize()
     ref = A.double().T @ B.double()
