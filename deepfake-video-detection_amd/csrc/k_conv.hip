@@ -76,7 +76,6 @@ struct OpConvA {
   int64_t sn, sy, sx, sc;  // element strides of the source (n, y, x, c)
   int H, W, C, KW, S, P, Ho, Wo, R, K;
   FDiv fC, fKW, fHW, fWo;  // set by the launcher (fdiv_make)
-  int kuni;                // C % 16 == 0: the 16 k of a half-step share one tap (scalar index math)
   int iy0[4], ix0[4];
   int64_t base[4];
   static constexpr bool kR = false;
@@ -94,8 +93,7 @@ struct OpConvA {
   __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
     const int tid = threadIdx.x;
     const int k = k0 + (tid & 15);
-    const int tap = kuni ? fdiv(__builtin_amdgcn_readfirstlane(k0), fC) : fdiv(k, fC);
-    const int ci = k - tap * C, ky = fdiv(tap, fKW), kx = tap - ky * KW;
+    const int tap = fdiv(k, fC), ci = k - tap * C, ky = fdiv(tap, fKW), kx = tap - ky * KW;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + (tid + 256 * i) / CG_K;
@@ -115,7 +113,6 @@ struct OpConvDgradA {
   const float* dy;
   int Ho, Wo, Co, KW, P, H, W, R, K;
   FDiv fCo, fKW, fHW, fW;  // set by the launcher (fdiv_make)
-  int kuni;                // Co % 16 == 0: one tap per half-step (scalar index math)
   int iy[4], ix[4];
   int64_t base[4];
   static constexpr bool kR = false;
@@ -133,8 +130,7 @@ struct OpConvDgradA {
   __device__ void load(int r0, int k0, float (&v)[4], bool (&ok)[4]) const {
     const int tid = threadIdx.x;
     const int k = k0 + (tid & 15);
-    const int tap = kuni ? fdiv(__builtin_amdgcn_readfirstlane(k0), fCo) : fdiv(k, fCo);
-    const int co = k - tap * Co, ky = fdiv(tap, fKW), kx = tap - ky * KW;
+    const int tap = fdiv(k, fCo), co = k - tap * Co, ky = fdiv(tap, fKW), kx = tap - ky * KW;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = r0 + (tid + 256 * i) / CG_K;
@@ -173,8 +169,7 @@ struct OpConvBT {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      // one pixel per wave and element: its (n, oy, ox) on the scalar unit
-      const int m = __builtin_amdgcn_readfirstlane(m0 + (tid >> 6) + 4 * i);
+      const int m = m0 + (tid >> 6) + 4 * i;
       const int hw = Ho * Wo, n = fdiv(m, fHW), q = m - n * hw, oy = fdiv(q, fWo), ox = q - oy * Wo;
       const int iy = oy * S - P + ky, ix = ox * S - P + kx;
       ok[i] = jok && m < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
@@ -487,7 +482,6 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
   const int M = g.N * g.Ho * g.Wo, K = KK * g.Ci;
   OpConvA pa{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, M, K};
   pa.fC = fdiv_make(g.Ci); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.Ho * g.Wo); pa.fWo = fdiv_make(g.Wo);
-  pa.kuni = g.Ci % CG_K == 0;
   OpRows pb{wf, K, g.Co, K};
   if (stat_rows) *stat_rows = cdiv(M, CG_T);
   return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats);
@@ -504,7 +498,6 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
     pa.dy = dY; pa.Ho = g.Ho; pa.Wo = g.Wo; pa.Co = g.Co; pa.KW = g.KW; pa.P = g.P; pa.H = g.H; pa.W = g.W;
     pa.R = M; pa.K = K;
     pa.fCo = fdiv_make(g.Co); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.H * g.W); pa.fW = fdiv_make(g.W);
-    pa.kuni = g.Co % CG_K == 0;
     return conv_gemm<decltype(pa), OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr);
   };
   return g.S == 1 ? run(OpConvDgradA<1>{}) : run(OpConvDgradA<2>{});
