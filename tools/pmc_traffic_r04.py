@@ -106,12 +106,19 @@ def main():
     raw_ok = all(read(d, f"calib_r{m}") for m in range(3))
     if raw_ok:
         cal.update({f"raw_mode{m}": calib(d, f"calib_r{m}", raw_bytes) for m in range(3)})
-        raw_ok = all(abs(cal[f"raw_mode{m}"] - 1.0) < 0.05 for m in range(3))
+        # the request-size count is exact on the contiguous pattern (mode 0); on 64-B channel slices
+        # (modes 1, 2) it reads 2.0: each 64-B slice request is filled as a whole 128-B line, so it
+        # counts the bytes the L2s request from the fabric at line granularity (an upper bound of the
+        # HBM bytes: the other half of a line may be served by the Infinity Cache)
+        raw_ok = abs(cal["raw_mode0"] - 1.0) < 0.05
     fetch, write = read(d, "fetch"), read(d, "write")
     raw = read(d, "raw") if raw_ok else None
     wf = cal["write_mode3"]
-    out = {"_method": ("fetch: request-size counters 32 RDREQ_32B + 64 RDREQ_64B + 128 RDREQ_128B "
-                       "(validated on tools/fetch_calib's known bytes: raw_mode*)" if raw_ok else
+    out = {"_method": ("fetch: request-size counters 32 RDREQ_32B + 64 RDREQ_64B + 128 RDREQ_128B = the bytes "
+                       "the L2s request from the fabric at line granularity (exact on tools/fetch_calib's "
+                       "contiguous reads, raw_mode0; 2x the useful bytes of 64-B channel-slice reads, raw_mode1/2, "
+                       "whose 64-B requests are filled as 128-B lines); fetch_size_bytes = FETCH_SIZE x 1024 "
+                       "for comparison (1/2 of 128-B requests on gfx950)" if raw_ok else
                        "fetch: FETCH_SIZE / the 64-B channel-slice calibration factor (fetch_mode1)") +
                       "; write: WRITE_SIZE / write_mode3; separate rocprofv3 --pmc passes, kernel trace only",
            "_calibration": {k: (round(v, 4) if v is not None else None) for k, v in cal.items()},
@@ -121,12 +128,13 @@ def main():
     for cls, ss in st.items():
         fv, nst = per_site(raw if raw_ok else fetch, cls,
                            raw_bytes if raw_ok else (lambda c: c["FETCH_SIZE"] * 1024 / cal["fetch_mode1"]))
+        fz, _ = per_site(fetch, cls, lambda c: c["FETCH_SIZE"] * 1024)
         wv, _ = per_site(write, cls, lambda c: c["WRITE_SIZE"] * 1024 / wf)
-        for (site, alg), fb, wb in zip(ss, fv, wv):
+        for (site, alg), fb, fs, wb in zip(ss, fv, fz, wv):
             out[f"{cls.split('<')[0]}:{site}"] = {
-                "algorithmic_bytes": alg, "fetch_bytes": round(fb), "write_bytes": round(wb),
-                "hbm_bytes_per_launch": round(fb + wb), "traffic_over_algorithmic": round((fb + wb) / alg, 4),
-                "steps": nst}
+                "algorithmic_bytes": alg, "fetch_bytes": round(fb), "fetch_size_bytes": round(fs),
+                "write_bytes": round(wb), "hbm_bytes_per_launch": round(fb + wb),
+                "traffic_over_algorithmic": round((fb + wb) / alg, 4), "steps": nst}
         tot_alg = sum(a for _, a in ss)
         tot = sum(out[f"{cls.split('<')[0]}:{s}"]["hbm_bytes_per_launch"] for s, _ in ss)
         out[f"{cls.split('<')[0]}:total"] = {"algorithmic_bytes": tot_alg, "hbm_bytes_per_step": tot,
