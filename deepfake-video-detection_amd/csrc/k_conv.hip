@@ -195,7 +195,7 @@ enum { CEPI_STORE = 0, CEPI_STATS = 1, CEPI_SLAB = 2 };
 // Main loop: 32-deep k-steps (two 16-deep halves per operand policy load) through two LDS stages --
 // the next step's gathers are in flight while this step's MFMAs run, and one barrier per step
 // (four per 32 k in the single-buffered form) hands the stages over.  The MFMA sequence over k is
-// unchanged (exact fp32 products); each step's 32 products are summed into a fresh tile first.
+// unchanged (exact fp32 products); every 4 steps' 128 products are summed into a fresh tile first.
 template <class PA, class PB, int EPI>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __restrict__ C, int ldc, int M, int N,
                                                         int K, int ksplit, const float* __restrict__ bias,
@@ -252,18 +252,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
     commit(0, kb);
   }
   lds_barrier();
-  int cur = 0;
-  for (int k0 = kb; k0 < ke; k0 += 2 * CG_K) {
+  int cur = 0, step = 0;
+  // two-level summation: FOLD 32-deep steps accumulate into a fresh tile that is then added to the
+  // running sum -- the fp32 rounding error grows with ~128 + K/128 terms instead of K (the train-mode
+  // BatchNorm chain of the ResNet-50 member amplifies conv rounding into its gradients).  Folding
+  // every step cost 2-5 % (the VALU reads drain the MFMA chain); every 4th step ~1/4 of that
+  constexpr int FOLD = 4;
+  f32x4_t part[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = kb; k0 < ke; k0 += 2 * CG_K, ++step) {
     const bool more = k0 + 2 * CG_K < ke;
     if (more) fetch(k0 + 2 * CG_K);
-    // two-level summation: each 32-deep step accumulates into a fresh tile, added to the running
-    // sum once per step -- the fp32 rounding error grows with ~32 + K/32 terms instead of K (the
-    // train-mode BatchNorm chain of the ResNet-50 member amplifies conv rounding into its gradients)
-    f32x4_t part[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -276,10 +278,15 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
         part[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, part[1][0], 0, 0, 0);
         part[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, part[1][1], 0, 0, 0);
       }
+    if (step % FOLD == FOLD - 1 || !more) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] += part[a][b];
+        for (int b = 0; b < 2; ++b) {
+          acc[a][b] += part[a][b];
+          part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        }
+    }
     if (more) commit(cur ^ 1, k0 + 2 * CG_K);
     lds_barrier();
     cur ^= 1;
@@ -531,17 +538,103 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
   return 0;
 }
 
+// The same two passes on 4-channel vectors: one row of the output (forward) / input (backward) map
+// (a run of workgroups per row), 32-bit index math (the element-wise forms above divide 64-bit indices six times
+// per element).  Same window scan order, same first-maximum rule, same summation order: identical
+// results.  C % 4 == 0.
+__global__ __launch_bounds__(256) void bn_relu_pool_fwd4_kernel(const float* __restrict__ Y, const float* __restrict__ mu,
+                                                                const float* __restrict__ sc, const float* __restrict__ sh,
+                                                                int H, int W, int C, int Ho, int Wo,
+                                                                float* __restrict__ P, uint8_t* __restrict__ arg) {
+  const int C4 = C >> 2, xb = (Wo * C4 + 255) >> 8;  // blocks per output row
+  const int row = blockIdx.x / xb, e = (blockIdx.x - row * xb) * 256 + threadIdx.x;
+  if (e >= Wo * C4) return;
+  const int f = row / Ho, oy = row - f * Ho;
+  const int ox = e / C4, c = (e - ox * C4) * 4;
+  float scv[4], shv[4], best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int bi[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { scv[j] = sc[c + j]; shv[j] = sh[c + j]; }
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * 2 - 1 + ky;
+    if (iy < 0 || iy >= H) continue;
+    const float* yr = Y + ((int64_t)f * H + iy) * W * C + c;
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * 2 - 1 + kx;
+      if (ix < 0 || ix >= W) continue;
+      const float4 y4 = *reinterpret_cast<const float4*>(yr + (int64_t)ix * C);
+      const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float z = fmaxf(bn_z(yv[j], mu, scv[j], shv[j], c + j), 0.f);
+        if (z > best[j]) { best[j] = z; bi[j] = ky * 3 + kx; }
+      }
+    }
+  }
+  const int64_t o = ((int64_t)row * Wo + ox) * C + c;
+  *reinterpret_cast<float4*>(P + o) = make_float4(best[0], best[1], best[2], best[3]);
+  *reinterpret_cast<uchar4*>(arg + o) = make_uchar4((unsigned char)bi[0], (unsigned char)bi[1], (unsigned char)bi[2],
+                                                    (unsigned char)bi[3]);
+}
+
+__global__ __launch_bounds__(256) void bn_relu_pool_bwd4_kernel(const float* __restrict__ dP, const uint8_t* __restrict__ arg,
+                                                                const float* __restrict__ Y, const float* __restrict__ mu,
+                                                                const float* __restrict__ sc, const float* __restrict__ sh,
+                                                                int H, int W, int C, int Ho, int Wo, float* __restrict__ g) {
+  const int C4 = C >> 2, xb = (W * C4 + 255) >> 8;  // blocks per input row
+  const int row = blockIdx.x / xb, e = (blockIdx.x - row * xb) * 256 + threadIdx.x;
+  if (e >= W * C4) return;
+  const int f = row / H, iy = row - f * H;
+  const int ix = e / C4, c = (e - ix * C4) * 4;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  const int oy_lo = max(0, iy / 2), oy_hi = min(Ho - 1, (iy + 1) / 2);
+  const int ox_lo = max(0, ix / 2), ox_hi = min(Wo - 1, (ix + 1) / 2);
+  for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+    const int ky = iy - (oy * 2 - 1);
+    if (ky < 0 || ky > 2) continue;
+    for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+      const int kx = ix - (ox * 2 - 1);
+      if (kx < 0 || kx > 2) continue;
+      const int64_t o = (((int64_t)f * Ho + oy) * Wo + ox) * C + c;
+      const uchar4 a4 = *reinterpret_cast<const uchar4*>(arg + o);
+      const float4 d4 = *reinterpret_cast<const float4*>(dP + o);
+      const int tap = ky * 3 + kx;
+      if (a4.x == tap) a[0] += d4.x;
+      if (a4.y == tap) a[1] += d4.y;
+      if (a4.z == tap) a[2] += d4.z;
+      if (a4.w == tap) a[3] += d4.w;
+    }
+  }
+  const int64_t i = ((int64_t)row * W + ix) * C + c;
+  const float4 y4 = *reinterpret_cast<const float4*>(Y + i);
+  const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+  float out[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[j] = bn_z(yv[j], mu, sc[c + j], sh[c + j], c + j) > 0.f ? a[j] : 0.f;
+  *reinterpret_cast<float4*>(g + i) = make_float4(out[0], out[1], out[2], out[3]);
+}
+
 int bn_relu_pool_fwd(hipStream_t s, const float* Y, const float* mu, const float* sc, const float* sh, int N, int H,
                      int W, int C, int Ho, int Wo, float* P, uint8_t* arg) {
-  hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(ew((int64_t)N * Ho * Wo * C)), dim3(256), 0, s, Y, mu, sc, sh, N, H, W,
-                     C, Ho, Wo, P, arg);
+  if (C % 4 == 0 && (int64_t)N * Ho * cdiv(Wo * (C / 4), 256) < (1ll << 31)) {
+    hipLaunchKernelGGL(bn_relu_pool_fwd4_kernel, dim3((unsigned)((int64_t)N * Ho * cdiv(Wo * (C / 4), 256))), dim3(256), 0,
+                       s, Y, mu, sc, sh, H, W, C, Ho, Wo, P, arg);
+  } else {
+    hipLaunchKernelGGL(bn_relu_pool_fwd_kernel, dim3(ew((int64_t)N * Ho * Wo * C)), dim3(256), 0, s, Y, mu, sc, sh, N, H,
+                       W, C, Ho, Wo, P, arg);
+  }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
 int bn_relu_pool_bwd(hipStream_t s, const float* dP, const uint8_t* arg, const float* Y, const float* mu,
                      const float* sc, const float* sh, int N, int H, int W, int C, int Ho, int Wo, float* g) {
-  hipLaunchKernelGGL(bn_relu_pool_bwd_kernel, dim3(ew((int64_t)N * H * W * C)), dim3(256), 0, s, dP, arg, Y, mu, sc, sh,
-                     N, H, W, C, Ho, Wo, g);
+  if (C % 4 == 0 && (int64_t)N * H * cdiv(W * (C / 4), 256) < (1ll << 31)) {
+    hipLaunchKernelGGL(bn_relu_pool_bwd4_kernel, dim3((unsigned)((int64_t)N * H * cdiv(W * (C / 4), 256))), dim3(256), 0,
+                       s, dP, arg, Y, mu, sc, sh, H, W, C, Ho, Wo, g);
+  } else {
+    hipLaunchKernelGGL(bn_relu_pool_bwd_kernel, dim3(ew((int64_t)N * H * W * C)), dim3(256), 0, s, dP, arg, Y, mu, sc,
+                       sh, N, H, W, C, Ho, Wo, g);
+  }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
