@@ -43,7 +43,7 @@ struct Ws {
 };
 std::map<std::pair<int, hipStream_t>, Ws> g_ws;
 uint64_t g_tick = 0;
-constexpr int kMaxWs = 8;  // workspaces per device; past it the least recently used one is freed
+constexpr int kMaxWs = 32;  // workspaces per device; past it the least recently used one is freed
 std::map<Key, Entry> g_cache;
 
 #define LT_CHECK(x)                                                                         \
@@ -67,9 +67,10 @@ int handle_and_ws(hipStream_t s, int dev, hipblasLtHandle_t* h, void** ws) {
   auto wk = std::make_pair(dev, s);
   auto wi = g_ws.find(wk);
   if (wi == g_ws.end()) {
-    // bounded: serving from many threads, each on its own stream, must not grow HBM use per stream
-    // ever seen.  The evicted workspace may still be read by its stream's queued GEMMs (or that
-    // stream may be gone): a device synchronisation orders the free after all of them (rare).
+    // bounded: callers on many streams must not grow HBM use per stream ever seen.  The evicted
+    // workspace may still be read by its stream's queued GEMMs (or that stream may be gone): a device
+    // synchronisation orders the free after all of them.  Only the dfd_vgemm comparison ops reach
+    // this file (no model path, no serving thread: ADVICE r3), so evictions are rare by design.
     int held = 0;
     auto lru = g_ws.end();
     for (auto e = g_ws.begin(); e != g_ws.end(); ++e)
