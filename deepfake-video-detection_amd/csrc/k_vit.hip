@@ -273,22 +273,44 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
 #pragma unroll
     for (int j = 0; j < 8; ++j) { pg[i][j] = 0.f; pb[i][j] = 0.f; }
   const int64_t rbeg = (int64_t)blockIdx.x * rpb, rend = min(rows, rbeg + rpb);
+  // a row's x, dY and residual gradient are loaded together, one row ahead (raw registers), so the
+  // wave's loads for row r+4 are in flight while row r is reduced and written
+  Raw8<T> rx[VIT_LN_VEC], rr[VIT_LN_VEC];
+  Raw8<D> rd[VIT_LN_VEC];
+  auto row_ld = [&](int64_t r) {
+    const bool live = r < rend;
+#pragma unroll
+    for (int i = 0; i < VIT_LN_VEC; ++i) {
+      const int v = lane + 64 * i;
+      const bool ok = live && v < nv;
+      raw_ld(rx[i], X + r * ldx + v * 8, X, ok);
+      raw_ld(rd[i], dY + r * ldd + v * 8, dY, ok);
+      raw_ld(rr[i], dres ? dres + r * ldx + v * 8 : X, X, ok && dres != nullptr);
+    }
+  };
+  float gv[VIT_LN_VEC][8];
+#pragma unroll
+  for (int i = 0; i < VIT_LN_VEC; ++i) {
+    const int v = lane + 64 * i;
+    if (v < nv) ld8(g + v * 8, gv[i]);
+  }
+  row_ld(rbeg + wave);
   for (int64_t r = rbeg + wave; r < rend; r += 4) {
     const float mu = mean[r], rs = rstd[r];
-    float xh[VIT_LN_VEC][8], dxh[VIT_LN_VEC][8];
+    float xh[VIT_LN_VEC][8], dxh[VIT_LN_VEC][8], res[VIT_LN_VEC][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VIT_LN_VEC; ++i) {
       const int v = lane + 64 * i;
       if (v < nv) {
-        float x[8], dy[8], gg[8];
-        ld8(X + r * ldx + v * 8, x);
-        ld8(dY + r * ldd + v * 8, dy);
-        ld8(g + v * 8, gg);
+        float x[8], dy[8];
+        raw_to_f(rx[i], x);
+        raw_to_f(rd[i], dy);
+        raw_to_f(rr[i], res[i]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[i][j] = (x[j] - mu) * rs;
-          dxh[i][j] = dy[j] * gg[j];
+          dxh[i][j] = dy[j] * gv[i][j];
           s1 += dxh[i][j];
           s2 += dxh[i][j] * xh[i][j];
           pg[i][j] += dy[j] * xh[i][j];
@@ -296,6 +318,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
         }
       }
     }
+    row_ld(r + 4);
     s1 = wave_sum(s1) / C;
     s2 = wave_sum(s2) / C;
 #pragma unroll
@@ -303,14 +326,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
       const int v = lane + 64 * i;
       if (v < nv) {
         float o[8];
-        if (dres) {
-          ld8(dres + r * ldx + v * 8, o);
-        } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] += rs * (dxh[i][j] - s1 - xh[i][j] * s2);
+        for (int j = 0; j < 8; ++j) o[j] = (dres ? res[i][j] : 0.f) + rs * (dxh[i][j] - s1 - xh[i][j] * s2);
         st8(dX + r * ldx + v * 8, o);
       }
     }

@@ -12,3 +12,8 @@ cut -c1-200 $O/e_enst.jsonl
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/pf_cnn_e -o run -- python $R/bench_temporal.py --model cnnlstm --no-cpu-baseline --steps 3 --warmup 1 > $R/$O/pf_cnn_e.log 2>&1 || { echo CNN PROF FAILED; exit 1; }
 echo prof ok
+timeout -k 10 400 python -u -m pytest tests/test_vit_gcn.py tests/test_vgemm_gpu.py -q --timeout 200 --timeout-method thread > $O/e_vit.log 2>&1; rc=$?
+echo "vit tests rc=$rc"; tail -2 $O/e_vit.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench_temporal.py --model vit --no-cpu-baseline > $O/e_vitb.jsonl 2> $O/e_vitb.err || { echo VITB FAILED; tail -5 $O/e_vitb.err; exit 1; }
+cut -c1-200 $O/e_vitb.jsonl
