@@ -17,3 +17,6 @@ echo "vit tests rc=$rc"; tail -2 $O/e_vit.log
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python bench_temporal.py --model vit --no-cpu-baseline > $O/e_vitb.jsonl 2> $O/e_vitb.err || { echo VITB FAILED; tail -5 $O/e_vitb.err; exit 1; }
 cut -c1-200 $O/e_vitb.jsonl
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/pf_enst -o run -- python $R/bench_temporal.py --model ensemble_train --no-cpu-baseline --steps 3 --warmup 1 > $R/$O/pf_enst.log 2>&1 || { echo ENST PROF FAILED; exit 1; }
+echo enst prof ok
