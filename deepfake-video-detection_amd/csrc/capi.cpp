@@ -427,9 +427,11 @@ int dfd_rn_avgpool(void* stream, int dtype, const void* x, int N, int HW, int C,
 }
 
 // ---- ResNet-50 training (fp32)
+// the ResNet-50 training convolutions sum K in two levels (k_conv.hip FOLD): its train-mode BN
+// chain needs the accuracy (tests/test_resnet_train_gpu.py holds it to torch fp32's distance to fp64)
 static dfd::ConvGeom rn_geom(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad) {
   return dfd::ConvGeom{N, H, W, Cin, Cout, kh, kw, stride, pad, (H + 2 * pad - kh) / stride + 1,
-                       (W + 2 * pad - kw) / stride + 1};
+                       (W + 2 * pad - kw) / stride + 1, true};
 }
 
 int64_t dfd_rn_conv_stat_rows(int N, int Ho, int Wo) { return ((int64_t)N * Ho * Wo + 63) / 64; }

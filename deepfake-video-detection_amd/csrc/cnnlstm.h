@@ -8,6 +8,7 @@ namespace dfd {
 
 struct ConvGeom {
   int N, H, W, Ci, Co, KH, KW, S, P, Ho, Wo;
+  bool fold = false;  // two-level K summation (k_conv.hip): the ResNet-50 training convolutions
 };
 
 int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* w,

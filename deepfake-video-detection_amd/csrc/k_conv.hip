@@ -195,8 +195,8 @@ enum { CEPI_STORE = 0, CEPI_STATS = 1, CEPI_SLAB = 2 };
 // Main loop: 32-deep k-steps (two 16-deep halves per operand policy load) through two LDS stages --
 // the next step's gathers are in flight while this step's MFMAs run, and one barrier per step
 // (four per 32 k in the single-buffered form) hands the stages over.  The MFMA sequence over k is
-// unchanged (exact fp32 products); every 4 steps' 128 products are summed into a fresh tile first.
-template <class PA, class PB, int EPI>
+// unchanged (exact fp32 products); with FOLD each step's 32 products are summed into a fresh tile first.
+template <class PA, class PB, int EPI, bool FOLD>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __restrict__ C, int ldc, int M, int N,
                                                         int K, int ksplit, const float* __restrict__ bias,
                                                         float* __restrict__ stats) {
@@ -252,20 +252,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
     commit(0, kb);
   }
   lds_barrier();
-  int cur = 0, step = 0;
-  // two-level summation: FOLD 32-deep steps accumulate into a fresh tile that is then added to the
-  // running sum -- the fp32 rounding error grows with ~128 + K/128 terms instead of K (the train-mode
-  // BatchNorm chain of the ResNet-50 member amplifies conv rounding into its gradients).  Folding
-  // every step cost 2-5 % (the VALU reads drain the MFMA chain); every 4th step ~1/4 of that
-  constexpr int FOLD = 4;
-  f32x4_t part[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kb; k0 < ke; k0 += 2 * CG_K, ++step) {
-    const bool more = k0 + 2 * CG_K < ke;
-    if (more) fetch(k0 + 2 * CG_K);
+  int cur = 0;
+  // FOLD (the ResNet-50 training convolutions): two-level summation -- each 32-deep step accumulates
+  // into a fresh tile that is then added to the running sum, so the fp32 rounding error grows with
+  // ~32 + K/32 terms instead of K (the train-mode BatchNorm chain amplifies conv rounding into the
+  // gradients; folding only every 4th step measured 4x torch fp32's error on a BN gradient again).
+  // It costs 2-5 % (the VALU reads drain the MFMA chain each step), so the CNN-LSTM convolutions,
+  // whose parity bounds the plain K-order sum meets, keep FOLD = false
+  auto mma = [&](f32x4_t (&d)[2][2]) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -273,19 +267,28 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
         const int kk = 4 * s + (lane >> 4);
         const float a0 = As[cur][h][wm + (lane & 15)][kk], a1 = As[cur][h][wm + 16 + (lane & 15)][kk];
         const float b0 = Bs[cur][h][wn + (lane & 15)][kk], b1 = Bs[cur][h][wn + 16 + (lane & 15)][kk];
-        part[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, part[0][0], 0, 0, 0);
-        part[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, part[0][1], 0, 0, 0);
-        part[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, part[1][0], 0, 0, 0);
-        part[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, part[1][1], 0, 0, 0);
+        d[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, d[0][0], 0, 0, 0);
+        d[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, d[0][1], 0, 0, 0);
+        d[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, d[1][0], 0, 0, 0);
+        d[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, d[1][1], 0, 0, 0);
       }
-    if (step % FOLD == FOLD - 1 || !more) {
+  };
+  for (int k0 = kb; k0 < ke; k0 += 2 * CG_K) {
+    const bool more = k0 + 2 * CG_K < ke;
+    if (more) fetch(k0 + 2 * CG_K);
+    if constexpr (FOLD) {
+      f32x4_t part[2][2];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          acc[a][b] += part[a][b];
-          part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int b = 0; b < 2; ++b) part[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      mma(part);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] += part[a][b];
+    } else {
+      mma(acc);
     }
     if (more) commit(cur ^ 1, k0 + 2 * CG_K);
     lds_barrier();
@@ -347,13 +350,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(PA pa, PB pb, float* __r
 
 template <class PA, class PB, int EPI>
 static int conv_gemm(hipStream_t s, const PA& pa, const PB& pb, float* C, int ldc, int M, int N, int K, int splits,
-                     const float* bias, float* stats) {
+                     const float* bias, float* stats, bool fold) {
   const int64_t tiles = (int64_t)cdiv(N, CG_T) * cdiv(M, CG_T);
   if (tiles > 0x7fffffff) { set_error("conv: too many tiles", __FILE__, __LINE__); return -1; }
   const int ksplit = cdiv(cdiv(K, splits), CG_K) * CG_K;
   splits = cdiv(K, ksplit);
-  hipLaunchKernelGGL((conv_gemm_kernel<PA, PB, EPI>), dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, s, pa, pb,
-                     C, ldc, M, N, K, ksplit, bias, stats);
+  if (fold)
+    hipLaunchKernelGGL((conv_gemm_kernel<PA, PB, EPI, true>), dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, s,
+                       pa, pb, C, ldc, M, N, K, ksplit, bias, stats);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<PA, PB, EPI, false>), dim3((unsigned)tiles, (unsigned)splits), dim3(256), 0, s,
+                       pa, pb, C, ldc, M, N, K, ksplit, bias, stats);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -491,7 +498,7 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
   pa.fC = fdiv_make(g.Ci); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.Ho * g.Wo); pa.fWo = fdiv_make(g.Wo);
   OpRows pb{wf, K, g.Co, K};
   if (stat_rows) *stat_rows = cdiv(M, CG_T);
-  return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats);
+  return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats, g.fold);
 }
 
 int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX) {
@@ -505,7 +512,7 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
     pa.dy = dY; pa.Ho = g.Ho; pa.Wo = g.Wo; pa.Co = g.Co; pa.KW = g.KW; pa.P = g.P; pa.H = g.H; pa.W = g.W;
     pa.R = M; pa.K = K;
     pa.fCo = fdiv_make(g.Co); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.H * g.W); pa.fW = fdiv_make(g.W);
-    return conv_gemm<decltype(pa), OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr);
+    return conv_gemm<decltype(pa), OpRows, CEPI_STORE>(s, pa, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr, nullptr, g.fold);
   };
   return g.S == 1 ? run(OpConvDgradA<1>{}) : run(OpConvDgradA<2>{});
 }
@@ -532,7 +539,7 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
   pb.fHW = fdiv_make(g.Ho * g.Wo); pb.fWo = fdiv_make(g.Wo);
   const int ksplit = cdiv(cdiv(M, splits), CG_K) * CG_K;
   const int used = cdiv(M, ksplit);
-  DFD_TRY((conv_gemm<OpCols, OpConvBT, CEPI_SLAB>(s, pa, pb, slab, Kp, g.Co, Kp, M, splits, nullptr, nullptr)));
+  DFD_TRY((conv_gemm<OpCols, OpConvBT, CEPI_SLAB>(s, pa, pb, slab, Kp, g.Co, Kp, M, splits, nullptr, nullptr, g.fold)));
   hipLaunchKernelGGL(conv_unpack_grad_kernel, dim3(ew(per)), dim3(256), 0, s, slab, used, g.Co, g.Ci, KK, gw);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
