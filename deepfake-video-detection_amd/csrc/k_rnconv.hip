@@ -15,6 +15,7 @@
 // LDS through a D-deep register ring (XOR-swizzled 16-B chunks for bf16); epilogue: bias,
 // residual, ReLU, one rounding to the storage type, C tile restaged in LDS for 16-B stores.
 #include "kernels.h"
+#include "vit.h"
 
 namespace dfd {
 
@@ -239,6 +240,17 @@ int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, con
     if ((int64_t)g.N * g.H >= (1ll << 31)) { set_error("rn_conv: too many rows", __FILE__, __LINE__); return -1; }
     if (N <= 64) return rn_go<T, 128, 64, 1, 32, 2, true>(s, X, Wt, C, R, bias, relu, g, M, N, K);
     return rn_go<T, 128, 128, 2, 32, 2, true>(s, X, Wt, C, R, bias, relu, g, M, N, K);
+  }
+  if constexpr (sizeof(T) == 2) {
+    // bf16 1x1 stride-1 convolutions are plain NT GEMMs: the LDS-DMA 256-row-tile kernel of the ViT
+    // (k_vgemm.hip) where it covers the shape (Cout % 128, Cin % 64), with the same epilogue order
+    // (bias, identity, ReLU in fp32, one rounding)
+    if (vgemm_nt_covers(M, N, K)) {
+      VgemmArgs a{};
+      a.A = X; a.B = Wt; a.C = C; a.R = R; a.bias = bias;
+      a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
+      return launch_vgemm_nt(s, a, VG_BIAS | (R ? VG_RESID : 0) | (relu ? VG_RELU : 0));
+    }
   }
   if (N <= 64) return rn_go<T, 128, 64, 1, 32, 2, false>(s, X, Wt, C, R, bias, relu, g, M, N, K);
   return rn_go<T, 128, 128, 2, 32, 2, false>(s, X, Wt, C, R, bias, relu, g, M, N, K);

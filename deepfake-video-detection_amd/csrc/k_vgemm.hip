@@ -221,6 +221,10 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
             else o[j] *= xv;  // VG_DGELU: the stored gelu'
           }
         }
+        if constexpr ((EP & VG_RELU) != 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = fmaxf(o[j], 0.f);
+        }
         if constexpr ((EP & VG_GELU2) != 0) {
           // C = gelu'(z), G = gelu(z) of the stored (rounded) pre-activation z
           float g[8];
@@ -336,6 +340,7 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   case 2 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT>), dim3(tiles), dim3(512), 0, s, a); break; \
   case 2 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128>), dim3(tiles), dim3(512), 0, s, a); break;
     DFD_VG(0) DFD_VG(VG_BIAS) DFD_VG(VG_BIAS | VG_RESID) DFD_VG(VG_BIAS | VG_GELU2) DFD_VG(VG_DGELU)
+    DFD_VG(VG_BIAS | VG_RELU) DFD_VG(VG_BIAS | VG_RESID | VG_RELU)
 #undef DFD_VG
     default: set_error("vgemm: epilogue not instantiated", __FILE__, __LINE__); return -1;
   }
