@@ -488,16 +488,25 @@ __global__ void bn_relu_gap_bwd_kernel(const float* __restrict__ dfeat, const fl
 static int ew(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 4096)); }
 
 // ------------------------------------------------------------------ layer launchers
+// a 1x1 stride-1 unpadded convolution over a dense NHWC input is a plain GEMM on the activation rows
+static bool plain_1x1(const ConvGeom& g, const int64_t (&xs)[4]) {
+  return g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0 && xs[3] == 1 && xs[2] == g.Ci &&
+         xs[1] == (int64_t)g.W * g.Ci && xs[0] == (int64_t)g.H * g.W * g.Ci;
+}
+
 int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* w,
                  const float* bias, float* wf, float* Y, float* stats, int* stat_rows) {
   const int KK = g.KH * g.KW;
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
                      (float*)nullptr);
   const int M = g.N * g.Ho * g.Wo, K = KK * g.Ci;
-  OpConvA pa{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, M, K};
-  pa.fC = fdiv_make(g.Ci); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.Ho * g.Wo); pa.fWo = fdiv_make(g.Wo);
   OpRows pb{wf, K, g.Co, K};
   if (stat_rows) *stat_rows = cdiv(M, CG_T);
+  if (plain_1x1(g, xs))  // the activation rows themselves are the A operand (no gather index math)
+    return conv_gemm<OpRows, OpRows, CEPI_STATS>(s, OpRows{x, g.Ci, M, K}, pb, Y, g.Co, M, g.Co, K, 1, bias, stats,
+                                                 g.fold);
+  OpConvA pa{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, M, K};
+  pa.fC = fdiv_make(g.Ci); pa.fKW = fdiv_make(g.KW); pa.fHW = fdiv_make(g.Ho * g.Wo); pa.fWo = fdiv_make(g.Wo);
   return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats, g.fold);
 }
 
@@ -508,6 +517,9 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
                      wd);
   const int M = g.N * g.H * g.W, K = KK * g.Co;
   OpRows pb{wd, K, g.Ci, K};
+  if (g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0)  // dY rows are the A operand
+    return conv_gemm<OpRows, OpRows, CEPI_STORE>(s, OpRows{dY, g.Co, M, K}, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr,
+                                                 nullptr, g.fold);
   auto run = [&](auto pa) {
     pa.dy = dY; pa.Ho = g.Ho; pa.Wo = g.Wo; pa.Co = g.Co; pa.KW = g.KW; pa.P = g.P; pa.H = g.H; pa.W = g.W;
     pa.R = M; pa.K = K;
@@ -535,11 +547,17 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
   int splits = conv_wgrad_splits(g);
   splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / per));
   OpCols pa{dY, g.Co, g.Co, M};
-  OpConvBT pb{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, Kp, M};
-  pb.fHW = fdiv_make(g.Ho * g.Wo); pb.fWo = fdiv_make(g.Wo);
   const int ksplit = cdiv(cdiv(M, splits), CG_K) * CG_K;
   const int used = cdiv(M, ksplit);
-  DFD_TRY((conv_gemm<OpCols, OpConvBT, CEPI_SLAB>(s, pa, pb, slab, Kp, g.Co, Kp, M, splits, nullptr, nullptr, g.fold)));
+  if (plain_1x1(g, xs)) {  // b(j, m) = x[m][j]: the activation rows, read column-wise
+    DFD_TRY((conv_gemm<OpCols, OpCols, CEPI_SLAB>(s, pa, OpCols{x, g.Ci, Kp, M}, slab, Kp, g.Co, Kp, M, splits, nullptr,
+                                                  nullptr, g.fold)));
+  } else {
+    OpConvBT pb{x, xs[0], xs[1], xs[2], xs[3], g.H, g.W, g.Ci, g.KW, g.S, g.P, g.Ho, g.Wo, Kp, M};
+    pb.fHW = fdiv_make(g.Ho * g.Wo); pb.fWo = fdiv_make(g.Wo);
+    DFD_TRY((conv_gemm<OpCols, OpConvBT, CEPI_SLAB>(s, pa, pb, slab, Kp, g.Co, Kp, M, splits, nullptr, nullptr,
+                                                    g.fold)));
+  }
   hipLaunchKernelGGL(conv_unpack_grad_kernel, dim3(ew(per)), dim3(256), 0, s, slab, used, g.Co, g.Ci, KK, gw);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
