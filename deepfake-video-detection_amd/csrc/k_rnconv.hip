@@ -238,6 +238,18 @@ int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, con
       return -1;
     }
     if ((int64_t)g.N * g.H >= (1ll << 31)) { set_error("rn_conv: too many rows", __FILE__, __LINE__); return -1; }
+    if constexpr (sizeof(T) == 2) {
+      // bf16 3x3 and strided convolutions with Cin % 64 == 0 and Cout % 128 == 0: the same LDS-DMA NT
+      // kernel, its A tile gathered per tap from the NHWC input (implicit GEMM, K order tap-major as here)
+      if (vgemm_conv_covers(g.Cin, N, g.KH, g.KW) && vgemm_nt_covers(M, N, K)) {
+        VgemmArgs a{};
+        a.A = X; a.B = Wt; a.C = C; a.R = R; a.bias = bias;
+        a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
+        a.conv = 1; a.H = g.H; a.W = g.W; a.Ho = g.Ho; a.Wo = g.Wo; a.cin_log2 = g.cin_log2; a.KW = g.KW;
+        a.stride = g.stride; a.pad = g.pad;
+        return launch_vgemm_nt(s, a, VG_BIAS | (R ? VG_RESID : 0) | (relu ? VG_RELU : 0));
+      }
+    }
     if (N <= 64) return rn_go<T, 128, 64, 1, 32, 2, true>(s, X, Wt, C, R, bias, relu, g, M, N, K);
     return rn_go<T, 128, 128, 2, 32, 2, true>(s, X, Wt, C, R, bias, relu, g, M, N, K);
   }

@@ -62,6 +62,40 @@ __device__ __forceinline__ void stage_nt(const bf16* __restrict__ G, int64_t ld,
   }
 }
 
+// The A operand of an implicit convolution: row r of the tile = output pixel row0 + r; its 64-deep
+// K-step k0 is channels [c0, c0 + 64) of one tap (Cin % 64 == 0), read from the input pixel the tap
+// meets, or from the zero page outside the map (and past the last row).  The pixel decomposition
+// of the wave's rows (IPW per lane) is computed once per tile: ConvRows.
+struct ConvRows {
+  int nb[4], iy[4], ix[4];  // n * H, oy * stride - pad, ox * stride - pad (nb < 0: past the last row)
+};
+__device__ __forceinline__ void conv_rows(const VgemmArgs& a, int row0, int w, int lane, ConvRows& cr) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 8 * (w * 4 + i) + (lane >> 3);
+    const int m = row0 + r;
+    const int hw = a.Ho * a.Wo, n = m / hw, q = m - n * hw, oy = q / a.Wo, ox = q - oy * a.Wo;
+    cr.nb[i] = m < a.M ? n * a.H : -1;
+    cr.iy[i] = oy * a.stride - a.pad;
+    cr.ix[i] = ox * a.stride - a.pad;
+  }
+}
+__device__ __forceinline__ void stage_conv(const VgemmArgs& a, const ConvRows& cr, int k0, char* img, int w, int lane) {
+  const int tap = k0 >> a.cin_log2, c0 = k0 & ((1 << a.cin_log2) - 1);
+  const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = w * 4 + i;
+    const int r = 8 * q + (lane >> 3);
+    const int gc = (lane & 7) ^ ((r >> 1) & 7);
+    const int y = cr.iy[i] + kh, x = cr.ix[i] + kw;
+    const bool in = cr.nb[i] >= 0 && y >= 0 && y < a.H && x >= 0 && x < a.W;
+    const bf16* src = in ? a.A + ((((int64_t)(cr.nb[i] + y) * a.W + x) << a.cin_log2) + c0 + gc * 8)
+                         : reinterpret_cast<const bf16*>(g_vzero) + gc * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_vp)(img + q * 1024), 16, 0, 0);
+  }
+}
+
 // fragment of rows base .. base+15 (base % 16 == 0) at k-chunk 4s + (lane >> 4)
 __device__ __forceinline__ s16x8 frag_nt(const char* img, int base, int s, int lane) {
   const int r = base + (lane & 15);
@@ -143,7 +177,7 @@ __device__ __forceinline__ void st8bf(bf16* p, const float (&v)[8]) { st8(p, v);
 // ---------------------------------------------------------------- kernels
 // BNT = 256: 8 waves as 2 (M) x 4 (N), 128 x 64 each; BNT = 128 (N = 768-wide products: 2.3 instead of
 // 1.2 dispatch waves of tiles, so the last wave idles less): 4 (M) x 2 (N) waves of 64 x 64
-template <int EP, int BNT>
+template <int EP, int BNT, bool CONV = false>
 __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
   constexpr int WMN = BNT == VT ? 2 : 4, WNN = 8 / WMN;  // waves along M / N
   constexpr int MI = VT / WMN / 16, NJ = BNT / WNN / 16;
@@ -163,14 +197,20 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc.v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = a.K / VK;
-  stage_nt<VT>(a.A, a.lda, row0, a.M, 0, smem, w, lane);
+  ConvRows cr;
+  if constexpr (CONV) conv_rows(a, row0, w, lane, cr);
+  auto stage_a = [&](int k0, char* img) {
+    if constexpr (CONV) stage_conv(a, cr, k0, img, w, lane);
+    else stage_nt<VT>(a.A, a.lda, row0, a.M, k0, img, w, lane);
+  };
+  stage_a(0, smem);
   stage_nt<BNT>(a.B, a.ldb, col0, a.N, 0, smem + VTILE, w, lane);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     char* cur = smem + (kt & 1) * STAGE;
     if (kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * STAGE;
-      stage_nt<VT>(a.A, a.lda, row0, a.M, (kt + 1) * VK, nxt, w, lane);
+      stage_a((kt + 1) * VK, nxt);
       stage_nt<BNT>(a.B, a.ldb, col0, a.N, (kt + 1) * VK, nxt + VTILE, w, lane);
     }
     mma_step<false>(cur, cur + VTILE, wm * (VT / WMN), wn * (BNT / WNN), lane, acc);
@@ -317,6 +357,11 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
 bool vgemm_nt_covers(int64_t M, int N, int K) {
   return M > 0 && M < (1ll << 31) && N % 128 == 0 && K % VK == 0 && K > 0;
 }
+// implicit convolution: a 64-deep K-step is 64 channels of one tap (Cin a power of two >= 64), the
+// output width a multiple of the 128-wide tile, KW in {1, 3} (KH <= 3)
+bool vgemm_conv_covers(int Cin, int Cout, int KH, int KW) {
+  return Cin >= 64 && (Cin & (Cin - 1)) == 0 && Cout % 128 == 0 && (KW == 1 || KW == 3) && KH <= 3 && KH >= 1;
+}
 bool vgemm_tn_covers(int64_t M, int P, int Q) { return M > 0 && M < (1ll << 31) && P % VT == 0 && Q % VT == 0; }
 
 // the 128-wide tile where 256-wide tiles would leave the last dispatch wave mostly idle: N % 256 != 0,
@@ -335,6 +380,22 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   if (bn != 128 && (bn != VT || a.N % VT)) { set_error("vgemm: tile width", __FILE__, __LINE__); return -1; }
   a.tiles_n = a.N / bn;
   const int tiles = cdiv(a.M, VT) * a.tiles_n;
+  if (a.conv) {  // implicit convolutions (the ResNet-50 eval 3x3 / strided layers): bias, identity, ReLU
+    if (!vgemm_conv_covers(1 << a.cin_log2, a.N, 3, a.KW) || a.K % (1 << a.cin_log2)) {
+      set_error("vgemm: convolution shape not covered", __FILE__, __LINE__);
+      return -1;
+    }
+    switch (ep * 2 + (bn == 128)) {
+#define DFD_VGC(E)                                                                                            \
+  case 2 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT, true>), dim3(tiles), dim3(512), 0, s, a); break; \
+  case 2 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128, true>), dim3(tiles), dim3(512), 0, s, a); break;
+      DFD_VGC(VG_BIAS) DFD_VGC(VG_BIAS | VG_RELU) DFD_VGC(VG_BIAS | VG_RESID | VG_RELU)
+#undef DFD_VGC
+      default: set_error("vgemm: convolution epilogue not instantiated", __FILE__, __LINE__); return -1;
+    }
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   switch (ep * 2 + (bn == 128)) {
 #define DFD_VG(E)                                                                                       \
   case 2 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT>), dim3(tiles), dim3(512), 0, s, a); break; \

@@ -90,6 +90,9 @@ struct VgemmArgs {
   int64_t lda, ldb, ldc;
   int M, N, K, tiles_n;
   int bn;             // tile width 256 / 128; 0: chosen by shape (launch_vgemm_nt)
+  // implicit convolution (conv != 0): A is the NHWC input [N][H][W][Cin] (Cin = 2^cin_log2, a multiple of
+  // 64), row m = output pixel (n, oy, ox), column k = (kh * KW + kw) * Cin + ci; zero outside the map
+  int conv, H, W, Ho, Wo, cin_log2, KW, stride, pad;
 };
 struct VgemmTnArgs {
   const bf16* X1;
@@ -100,6 +103,7 @@ struct VgemmTnArgs {
   int colsum;         // also sum X1's columns (a linear's bias gradient) into the slab rows' tail
 };
 bool vgemm_nt_covers(int64_t M, int N, int K);
+bool vgemm_conv_covers(int Cin, int Cout, int KH, int KW);
 bool vgemm_tn_covers(int64_t M, int P, int Q);
 int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a, int ep);
 int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap);

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round-4 call G: ResNet-50 bf16 eval 3x3 / strided convolutions on the implicit-conv NT GEMM and the
+# SE excitation's batched loads -- tests, the B0 bench line, a kernel trace, the ensemble lines.
+R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/r04; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_resnet.py tests/test_b0_parity_gpu.py tests/test_b0_bench_config_gpu.py tests/test_serving.py -q -m gpu --timeout 200 --timeout-method thread > $O/g_tests.log 2>&1; rc=$?
+echo "resnet / b0 parity / serving tests rc=$rc"; tail -2 $O/g_tests.log; grep -E "^FAILED" $O/g_tests.log | head
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep > $O/g_bench.json 2> $O/g_bench.err || { echo BENCH FAILED; tail -5 $O/g_bench.err; exit 1; }
+cut -c1-300 $O/g_bench.json
+timeout -k 10 300 python bench_temporal.py --model ensemble --no-cpu-baseline > $O/g_ens.jsonl 2> $O/g_ens.err || { echo ENS FAILED; tail -5 $O/g_ens.err; exit 1; }
+cut -c1-300 $O/g_ens.jsonl
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/pf_g -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-pw-sweep > $R/$O/pf_g.log 2>&1 || { echo PROF FAILED; exit 1; }
+echo prof ok
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/pf_gens -o run -- python $R/bench_temporal.py --model ensemble --no-cpu-baseline > $R/$O/pf_gens.log 2>&1 || { echo ENS PROF FAILED; exit 1; }
+echo ens prof ok
