@@ -453,7 +453,9 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 // (thread = pixel), 8 MFMAs per wave, rounded tile through an LDS slab for 16-B row stores,
 // BN-stat partials from the rounded values (per lane, fixed-order reduction at the end).
 constexpr int SFC = SCO + 8;  // LDS row stride (bf16) of the output slab
-__global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const void* __restrict__ x,
+// OCC workgroups per CU (knob stem_occ: 2, or 3 at 168 VGPRs with some loop invariants spilled)
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void stem_fwd_mfma_kernel(StemGeom g, const void* __restrict__ x,
                                                             const float* __restrict__ w, bf16* __restrict__ Y,
                                                             float* __restrict__ stats, int64_t ntiles) {
   __shared__ float tin[SNIN];
@@ -461,7 +463,10 @@ __global__ __launch_bounds__(256, 2) void stem_fwd_mfma_kernel(StemGeom g, const
   __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
   stem_lut_init(g, lut);
   __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col [pix][tap]
-  __shared__ __attribute__((aligned(16))) bf16 ct[ST * ST * SFC];  // output slab [pix][co]
+  // the output slab [pix][co] shares xs: a wave writes the output rows of the 16-pixel blocks whose
+  // im2col rows it has just read (same pixels, same row stride), so no other wave's operand is hit
+  static_assert(SFC == SWL, "slab and im2col rows alias");
+  bf16* const ct = xs;
   __shared__ __attribute__((aligned(16))) bf16 wsb[SCO * SWL];     // weights [co][tap]
   __shared__ float red[2][4][SCO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -586,9 +591,13 @@ template <typename T>
 int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float* w, T* Y, float* stats,
                     int* stat_rows) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
-  const int gx = (int)std::min<int64_t>(ntiles, 1024);
+  const bool occ3 = sizeof(T) == 2 && tune(TK_STEM_OCC) == 3;
+  const int gx = (int)std::min<int64_t>(ntiles, occ3 ? 768 : 1024);  // whole rounds of co-resident workgroups
   if constexpr (sizeof(T) == 2) {
-    hipLaunchKernelGGL(stem_fwd_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+    if (occ3)
+      hipLaunchKernelGGL(stem_fwd_mfma_kernel<3>, dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+    else
+      hipLaunchKernelGGL(stem_fwd_mfma_kernel<2>, dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
   } else {  // fp32 parity mode: exact fp32 products
     if (stats)
       hipLaunchKernelGGL((stem_fwd_kernel<T, true>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);

@@ -176,13 +176,15 @@ def test_wgrad_stream_bit_identical(cuda):
     assert all(torch.equal(bufs_a[n], bufs_b[n]) for n in bufs_a)
 
 
-@pytest.mark.parametrize("knobs", [{"dw_pf": 1}, {"dw_rb": 1}, {"dw_rb": 2}, {"dw_pf": 1, "dw_rb": 3}])
+@pytest.mark.parametrize("knobs", [{"dw_pf": 1}, {"dw_rb": 1}, {"dw_rb": 2}, {"dw_pf": 1, "dw_rb": 3},
+                                   {"dw2_rs": 4}, {"dw2_rs": 5}])
 def test_depthwise_schedule_knobs_close(cuda, knobs):
     """Depthwise schedule knobs (all off by default) against the default schedule on the bf16 step:
     dw_pf = 1, the software-pipelined stride-1 backward (its k3 launches run at 2 workgroups per CU,
     so the grid -- and the fixed-order partial sums of dW and the BN1 statistics -- change); dw_rb
     bit 0 / bit 1, two-row strips in the stride-1 forward / backward (same per-output tap order, the
-    BN2 / BN1 / dW partial sums in another pixel order).  None is bit-identical; each must agree with
+    BN2 / BN1 / dW partial sums in another pixel order); dw2_rs = 4 / 5, 4-pixel strips in the 8 x 56-tile
+    stride-2 backward (3 / 4 workgroups per CU: other dW and BN1 partial-sum orders; off = 0 or 14).  None is bit-identical; each must agree with
     the default step like two summation orders of the same bf16 chain: loss within 1e-2 relative and
     every gradient tensor cosine >= 0.998, norm within 3 % for the backward-only knobs (the bounds of
     the fused-MBConv comparison, test_mbconv7_gpu.py); a forward knob perturbs every train-mode BN2
