@@ -44,6 +44,14 @@ __device__ const uint4 g_vzero[32] = {};      // 512 B of zeros: the DMA source 
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// wait for this wave's vector-memory operations except the youngest N (LDS counter untouched), and a
+// workgroup barrier that does not drain them (__syncthreads would wait for vmcnt(0))
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // ---------------------------------------------------------------- NT: C = A . B^T
 // One K-step image of an operand: [ROWS rows][64 k] bf16, 128-B rows, chunk (16 B) c of row r at
 // slot c ^ ((r >> 1) & 7).  Wave w fills rows (ROWS/8) w .. with ROWS/64 DMA instructions of 8 rows.
@@ -184,8 +192,13 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
   constexpr int BIMG = BNT * VK * 2;                    // B operand's K-step image
   constexpr int STAGE = VTILE + BIMG;
   constexpr int ES = BNT + 4;                           // epilogue row stride (floats)
-  static_assert(2 * STAGE <= VLDS && 128 * ES * 4 <= VLDS, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[VLDS];
+  // K-step images in flight: 3 for the 128-wide tile (144 KiB; a DMA has two K-steps to land), 2 for
+  // the 256-wide one (its K-step is twice as long)
+  constexpr int NST = BNT == VT ? 2 : 3;
+  constexpr int NPS = VT / 64 + BNT / 64;              // DMA instructions per thread per K-step
+  constexpr int SMEM = NST * STAGE > 128 * ES * 4 ? NST * STAGE : 128 * ES * 4;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = uni(tid >> 6), wm = w / WNN, wn = w % WNN;
   const int L = xcd_swizzle((int)blockIdx.x, (int)gridDim.x);
@@ -203,18 +216,29 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
     if constexpr (CONV) stage_conv(a, cr, k0, img, w, lane);
     else stage_nt<VT>(a.A, a.lda, row0, a.M, k0, img, w, lane);
   };
-  stage_a(0, smem);
-  stage_nt<BNT>(a.B, a.ldb, col0, a.N, 0, smem + VTILE, w, lane);
-  __syncthreads();
+  auto stage = [&](int kt, char* img) {
+    stage_a(kt * VK, img);
+    stage_nt<BNT>(a.B, a.ldb, col0, a.N, kt * VK, img + VTILE, w, lane);
+  };
+  // counted waits: a K-step's DMA must have landed before the barrier that precedes its reads; the
+  // younger K-steps' DMAs (NPS instructions each) stay in flight
+  stage(0, smem);
+  for (int p = 1; p < NST - 1; ++p)
+    if (p < nk) stage(p, smem + p * STAGE);
+  if (NST == 3 && nk > 1) vm_wait_n<NPS>();
+  else vm_wait_n<0>();
+  lds_bar();
+  int cb = 0, pb = NST - 1;  // buffers of K-steps kt and kt + NST - 1
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE;
-      stage_a((kt + 1) * VK, nxt);
-      stage_nt<BNT>(a.B, a.ldb, col0, a.N, (kt + 1) * VK, nxt + VTILE, w, lane);
-    }
+    char* cur = smem + cb * STAGE;
+    const bool pre = kt + NST - 1 < nk;
+    if (pre) stage(kt + NST - 1, smem + pb * STAGE);  // the buffer K-step kt - 1 read (barrier passed)
     mma_step<false>(cur, cur + VTILE, wm * (VT / WMN), wn * (BNT / WNN), lane, acc);
-    __syncthreads();  // this K-step's reads done everywhere; the next one's DMA landed (vmcnt(0))
+    if (NST == 3 && pre) vm_wait_n<NPS>();  // K-step kt + 1 landed; kt + 2 may still be in flight
+    else vm_wait_n<0>();
+    lds_bar();  // this K-step's reads done everywhere
+    cb = cb == NST - 1 ? 0 : cb + 1;
+    pb = pb == NST - 1 ? 0 : pb + 1;
   }
   // epilogue: two passes of 128 rows through LDS; a pass's residual / derivative rows are loaded
   // before its staging barrier (their latency under the LDS round trip, not per row)

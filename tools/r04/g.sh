@@ -2,7 +2,7 @@
 # round-4 call G: ResNet-50 bf16 eval 3x3 / strided convolutions on the implicit-conv NT GEMM and the
 # SE excitation's batched loads -- tests, the B0 bench line, a kernel trace, the ensemble lines.
 R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/r04; mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_resnet.py tests/test_b0_parity_gpu.py tests/test_b0_bench_config_gpu.py tests/test_serving.py -q -m gpu --timeout 200 --timeout-method thread > $O/g_tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_vgemm_gpu.py tests/test_vit_gcn.py tests/test_resnet.py tests/test_b0_parity_gpu.py tests/test_b0_bench_config_gpu.py tests/test_serving.py -q -m gpu --timeout 200 --timeout-method thread > $O/g_tests.log 2>&1; rc=$?
 echo "resnet / b0 parity / serving tests rc=$rc"; tail -2 $O/g_tests.log; grep -E "^FAILED" $O/g_tests.log | head
 [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep > $O/g_bench.json 2> $O/g_bench.err || { echo BENCH FAILED; tail -5 $O/g_bench.err; exit 1; }
@@ -22,3 +22,7 @@ for i in 1 2; do for kv in stem_occ=2 stem_occ=3 dw2_rs=14 dw2_rs=5; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --no-pw-sweep --steps 30 --warmup 5 --tune $kv > $O/g_ab_${kv}_$i.json 2>/dev/null || { echo "AB $kv FAILED"; exit 1; }
   echo "$kv $(python -c "import json,sys; d=json.load(open('$O/g_ab_${kv}_$i.json')); print(d['ms_per_step'])")"
 done; done
+timeout -k 10 300 python bench_temporal.py --model vit --no-cpu-baseline > $O/g_vit.jsonl 2> $O/g_vit.err || { echo VIT FAILED; tail -5 $O/g_vit.err; exit 1; }
+cut -c1-250 $O/g_vit.jsonl
+timeout -k 10 300 python tools/vgemm_bench.py 3 > $O/g_vgb.jsonl 2> $O/g_vgb.err || { echo VGB FAILED; tail -5 $O/g_vgb.err; exit 1; }
+tail -3 $O/g_vgb.jsonl | cut -c1-250
