@@ -38,11 +38,13 @@ constexpr int SRW = 26;                // dwords per staged row (99 B + alignmen
 constexpr int SNW = SIE * SRW;         // 858 dwords per tile
 constexpr int SNWL = (SNW + 255) / 256;
 static_assert(SNWL <= SNLD, "the dword path reuses the tile's load registers");
+// FMT: -1 = the input format read at run time; 2 = dense NHWC uint8 only (no strided-path registers)
+template <int FMT = -1>
 __device__ __forceinline__ void stem_load(const StemGeom& g, const void* __restrict__ x, int f, int iy0, int ix0,
                                           float (&r)[SNLD], uint32_t& okm) {
   okm = 0u;
   const int tid = threadIdx.x;
-  if (g.in.u8 == 2) {
+  if (FMT == 2 || (FMT < 0 && g.in.u8 == 2)) {
     const int xa = max(ix0, 0), xb = min(ix0 + SIE - 1, g.W - 1);
     const int off0 = (xa * 3) & ~3;
     const int nw = ((xb * 3 + 2) - off0) / 4 + 1;
@@ -57,6 +59,7 @@ __device__ __forceinline__ void stem_load(const StemGeom& g, const void* __restr
     }
     return;
   }
+  if constexpr (FMT == 2) return;
 #pragma unroll
   for (int i = 0; i < SNLD; ++i) {
     const int e = tid + 256 * i;
@@ -86,9 +89,10 @@ __device__ __forceinline__ void stem_lut_init(const StemGeom& g, float* lut) {
 }
 // tin[pix][ci] of the tile at input origin (iy0, ix0); the dword path stages its bytes in u8s
 // (an extra LDS barrier: every thread of the workgroup calls this uniformly).
+template <int FMT = -1>
 __device__ __forceinline__ void stem_store(const StemGeom& g, const float* lut, uint32_t* u8s, float* tin,
                                            const float (&r)[SNLD], uint32_t okm, int iy0, int ix0) {
-  if (g.in.u8 == 2) {
+  if (FMT == 2 || (FMT < 0 && g.in.u8 == 2)) {
 #pragma unroll
     for (int i = 0; i < SNWL; ++i) {
       const int w = threadIdx.x + 256 * i;
@@ -108,6 +112,7 @@ __device__ __forceinline__ void stem_store(const StemGeom& g, const float* lut, 
     }
     return;
   }
+  if constexpr (FMT == 2) return;
 #pragma unroll
   for (int i = 0; i < SNLD; ++i) {
     const int e = threadIdx.x + 256 * i;
@@ -454,7 +459,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 // BN-stat partials from the rounded values (per lane, fixed-order reduction at the end).
 constexpr int SFC = SCO + 8;  // LDS row stride (bf16) of the output slab
 // OCC workgroups per CU (knob stem_occ: 2, or 3 at 168 VGPRs with some loop invariants spilled)
-template <int OCC>
+template <int OCC, int FMT>
 __global__ __launch_bounds__(256, OCC) void stem_fwd_mfma_kernel(StemGeom g, const void* __restrict__ x,
                                                             const float* __restrict__ w, bf16* __restrict__ Y,
                                                             float* __restrict__ stats, int64_t ntiles) {
@@ -492,18 +497,18 @@ __global__ __launch_bounds__(256, OCC) void stem_fwd_mfma_kernel(StemGeom g, con
   if (t < ntiles) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
-    stem_load(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nxt, nok);
+    stem_load<FMT>(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nxt, nok);
   }
   for (; t < ntiles; t += gridDim.x) {
     int f, oy0, ox0;
     tl.coords(t, f, oy0, ox0);
     lds_barrier();
-    stem_store(g, lut, u8s, tin, nxt, nok, oy0 * 2 - 1, ox0 * 2 - 1);
+    stem_store<FMT>(g, lut, u8s, tin, nxt, nok, oy0 * 2 - 1, ox0 * 2 - 1);
     lds_barrier();
     if (t + gridDim.x < ntiles) {  // next tile in flight during this tile's math and stores
       int f2, oy2, ox2;
       tl.coords(t + gridDim.x, f2, oy2, ox2);
-      stem_load(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nxt, nok);
+      stem_load<FMT>(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nxt, nok);
     }
     {  // im2col: thread = output pixel, 27 taps + 5 zero pads as 4 x 16 B
       const int ly = tid / ST, lx = tid % ST;
@@ -594,10 +599,15 @@ int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float
   const bool occ3 = sizeof(T) == 2 && tune(TK_STEM_OCC) == 3;
   const int gx = (int)std::min<int64_t>(ntiles, occ3 ? 768 : 1024);  // whole rounds of co-resident workgroups
   if constexpr (sizeof(T) == 2) {
-    if (occ3)
-      hipLaunchKernelGGL(stem_fwd_mfma_kernel<3>, dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+    const bool dense = g.in.u8 == 2;
+    if (occ3 && dense)
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<3, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+    else if (occ3)
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<3, -1>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+    else if (dense)
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<2, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
     else
-      hipLaunchKernelGGL(stem_fwd_mfma_kernel<2>, dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<2, -1>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
   } else {  // fp32 parity mode: exact fp32 products
     if (stats)
       hipLaunchKernelGGL((stem_fwd_kernel<T, true>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
