@@ -177,21 +177,23 @@ def test_wgrad_stream_bit_identical(cuda):
 
 
 @pytest.mark.parametrize("knobs", [{"dw_pf": 1}, {"dw_rb": 1}, {"dw_rb": 2}, {"dw_pf": 1, "dw_rb": 3},
-                                   {"dw2_rs": 4}, {"dw2_rs": 5}])
+                                   {"dw2_rs": 4}, {"dw2_rs": 5}, {"stem_occ": 3}])
 def test_depthwise_schedule_knobs_close(cuda, knobs):
     """Depthwise schedule knobs (all off by default) against the default schedule on the bf16 step:
     dw_pf = 1, the software-pipelined stride-1 backward (its k3 launches run at 2 workgroups per CU,
     so the grid -- and the fixed-order partial sums of dW and the BN1 statistics -- change); dw_rb
     bit 0 / bit 1, two-row strips in the stride-1 forward / backward (same per-output tap order, the
     BN2 / BN1 / dW partial sums in another pixel order); dw2_rs = 4 / 5, 4-pixel strips in the 8 x 56-tile
-    stride-2 backward (3 / 4 workgroups per CU: other dW and BN1 partial-sum orders; off = 0 or 14).  None is bit-identical; each must agree with
+    stride-2 backward (3 / 4 workgroups per CU: other dW and BN1 partial-sum orders; off = 0 or 14);
+    stem_occ = 3, the stem forward at 3 workgroups per CU (768 instead of 1024 BN-stat rows: a forward
+    knob; off = 0 or 2).  None is bit-identical; each must agree with
     the default step like two summation orders of the same bf16 chain: loss within 1e-2 relative and
     every gradient tensor cosine >= 0.998, norm within 3 % for the backward-only knobs (the bounds of
     the fused-MBConv comparison, test_mbconv7_gpu.py); a forward knob perturbs every train-mode BN2
     statistic of the step, whose rounding flips reach every gradient through the 16 blocks' train-
     mode BatchNorms (measured worst: temporal_attention.0.bias cosine 0.988, a block-3.0 SE bias norm
     -5.9 %): the bf16-vs-fp32 bound of the oracle tests, cosine >= 0.98 and norm within 10 %.  The forward's arithmetic itself is held bit-identical in eval mode
-    (test_dw_rb_forward_eval_bit_identical)."""
+    (test_forward_knob_eval_bit_identical)."""
     from deepfake_amd import backbone
     prev = dict(backbone.DEFAULT_TUNING)
     try:
@@ -212,24 +214,27 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
         if nb <= 1e-3 * scale:
             continue  # structurally ~zero: rounding residue on both sides
         cos = float(a @ b) / (float(a.norm()) * nb + 1e-30)
-        cmin, ntol = (0.98, 0.10) if knobs.get("dw_rb", 0) & 1 else (0.998, 3e-2)
+        fwd = knobs.get("dw_rb", 0) & 1 or "stem_occ" in knobs
+        cmin, ntol = (0.98, 0.10) if fwd else (0.998, 3e-2)
         if cos < cmin or abs(float(a.norm()) - nb) > ntol * nb:
             bad.append((n, round(cos, 6), round(float(a.norm()) / nb, 5)))
     print(f"{knobs} vs default: loss {loss_a:.6f} / {loss_b:.6f}, {len(grads_b)} gradients, outside {bad}")
     assert not bad
 
 
-def test_dw_rb_forward_eval_bit_identical(cuda):
+@pytest.mark.parametrize("knob,on,off", [("dw_rb", 1, 0), ("stem_occ", 3, 2)])
+def test_forward_knob_eval_bit_identical(cuda, knob, on, off):
     """Eval mode (running statistics, no batch sums): the two-row forward strips (dw_rb bit 0)
-    compute every depthwise output from the same taps in the same order as the one-row strips, so
-    the logits are bit-identical."""
+    compute every depthwise output from the same taps in the same order as the one-row strips, and
+    the stem forward at 3 workgroups per CU (stem_occ) every output pixel with the same MFMA, so the
+    logits are bit-identical."""
     from deepfake_amd import backbone
     x, _ = _inputs("b4t8")
     outs = []
     prev = dict(backbone.DEFAULT_TUNING)
     try:
-        for v in (1, 0):
-            backbone.DEFAULT_TUNING["dw_rb"] = v
+        for v in (on, off):
+            backbone.DEFAULT_TUNING[knob] = v
             det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
                                              compute_dtype="bf16")
             deterministic_init_(det, seed=SEED)

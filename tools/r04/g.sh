@@ -15,7 +15,7 @@ echo prof ok
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/pf_gens -o run -- python $R/bench_temporal.py --model ensemble --no-cpu-baseline > $R/$O/pf_gens.log 2>&1 || { echo ENS PROF FAILED; exit 1; }
 echo ens prof ok
 cd $R
-timeout -k 10 300 python -u -m pytest tests/test_b0_224_gpu.py -q -k "knobs_close" --timeout 200 --timeout-method thread > $O/g_knobs.log 2>&1; echo "knob tests rc=$?"; tail -2 $O/g_knobs.log
+timeout -k 10 300 python -u -m pytest tests/test_b0_224_gpu.py -q -k "knobs_close or eval_bit_identical" --timeout 200 --timeout-method thread > $O/g_knobs.log 2>&1; echo "knob tests rc=$?"; tail -2 $O/g_knobs.log
 for i in 1 2; do for rs in 14 4 5; do echo "== dw2_rs=$rs"; timeout -k 10 120 tools/kbench dw_bwd2 256 dw2_rs=$rs || exit 1; done; done > $O/g_kb_dw2.log 2>&1
 grep -E "^==|dw_bwd2" $O/g_kb_dw2.log
 for i in 1 2; do for kv in stem_occ=2 stem_occ=3 dw2_rs=14 dw2_rs=5; do
