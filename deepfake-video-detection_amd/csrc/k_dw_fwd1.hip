@@ -282,7 +282,7 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
     // k3 stride 2 (112->56, 28->14): the 8x8 tile kernel is as fast or faster (kbench: 214 vs 246,
     // 42 vs 42 us); k5: 153 -> 126 and 43 -> 35 us
     if (g.k == 3) return 0;
-    const bool pf = tune(TK_DWF_PF) != 0;
+    const bool pf = (tune(TK_DWF_PF) & 1) != 0;  // knob dwf_pf bit 0
     if (H == 7 && W == 7)
       rc = pf ? fwd1_launch<T, 5, 7, 7, 7, 2, 2, 1, true>(s, g, X, w, Y, pro, stats, stat_rows)
               : fwd1_launch<T, 5, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows);

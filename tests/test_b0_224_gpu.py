@@ -178,7 +178,7 @@ def test_wgrad_stream_bit_identical(cuda):
 
 @pytest.mark.parametrize("knobs", [{"dw_pf": 1}, {"dw_rb": 1}, {"dw_rb": 2}, {"dw_pf": 1, "dw_rb": 3},
                                    {"dw2_rs": 4}, {"dw2_rs": 5}, {"stem_occ": 3},
-                                   {"dwf_pf": 1}])
+                                   {"dwf_pf": 3}])
 def test_depthwise_schedule_knobs_close(cuda, knobs):
     """Depthwise schedule knobs (all off by default) against the default schedule on the bf16 step:
     dw_pf = 1, the software-pipelined stride-1 backward (its k3 launches run at 2 workgroups per CU,
@@ -187,7 +187,7 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
     BN2 / BN1 / dW partial sums in another pixel order); dw2_rs = 4 / 5, 4-pixel strips in the 8 x 56-tile
     stride-2 backward (3 / 4 workgroups per CU: other dW and BN1 partial-sum orders; off = 0 or 14);
     stem_occ = 3, the stem forward at 3 workgroups per CU (768 instead of 1024 BN-stat rows: a forward
-    knob; off = 0 or 2); dwf_pf = 1, the stride-2 k5 forward's next-tile window prefetch.  None is bit-identical; each must agree with
+    knob; off = 0 or 2); dwf_pf = 3, the stride-2 forwards prefetching the next tile window (bit 0: k5, bit 1: k3 8x8 tiles).  None is bit-identical; each must agree with
     the default step like two summation orders of the same bf16 chain: loss within 1e-2 relative and
     every gradient tensor cosine >= 0.998, norm within 3 % for the backward-only knobs (the bounds of
     the fused-MBConv comparison, test_mbconv7_gpu.py); a forward knob perturbs every train-mode BN2
@@ -223,7 +223,7 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
     assert not bad
 
 
-@pytest.mark.parametrize("knob,on,off", [("dw_rb", 1, 0), ("stem_occ", 3, 2), ("dwf_pf", 1, 0)])
+@pytest.mark.parametrize("knob,on,off", [("dw_rb", 1, 0), ("stem_occ", 3, 2), ("dwf_pf", 3, 0)])
 def test_forward_knob_eval_bit_identical(cuda, knob, on, off):
     """Eval mode (running statistics, no batch sums): the two-row forward strips (dw_rb bit 0)
     compute every depthwise output from the same taps in the same order as the one-row strips, and
