@@ -9,6 +9,8 @@ timeout -k 10 300 python bench.py --no-cpu-baseline --no-pw-sweep > $O/g_bench.j
 cut -c1-300 $O/g_bench.json
 timeout -k 10 300 python bench_temporal.py --model ensemble --no-cpu-baseline > $O/g_ens.jsonl 2> $O/g_ens.err || { echo ENS FAILED; tail -5 $O/g_ens.err; exit 1; }
 cut -c1-300 $O/g_ens.jsonl
+timeout -k 10 300 python bench_temporal.py --model vit --no-cpu-baseline > $O/g_vit.jsonl 2> $O/g_vit.err || { echo VIT FAILED; tail -5 $O/g_vit.err; exit 1; }
+cut -c1-250 $O/g_vit.jsonl
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/pf_g -o run -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-pw-sweep > $R/$O/pf_g.log 2>&1 || { echo PROF FAILED; exit 1; }
 echo prof ok
@@ -23,7 +25,5 @@ for cfg in "stem_occ=3" "stem_occ=3 dw2_rs=5 dwf_pf=3" "stem_occ=2"; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --no-pw-sweep --steps 30 --warmup 5 $args > $O/g_ab_$tag.json 2>/dev/null || { echo "AB $cfg FAILED"; exit 1; }
   echo "$cfg $(python -c "import json; d=json.load(open('$O/g_ab_$tag.json')); print(d['ms_per_step'])")"
 done
-timeout -k 10 300 python bench_temporal.py --model vit --no-cpu-baseline > $O/g_vit.jsonl 2> $O/g_vit.err || { echo VIT FAILED; tail -5 $O/g_vit.err; exit 1; }
-cut -c1-250 $O/g_vit.jsonl
 timeout -k 10 300 python tools/vgemm_bench.py 3 > $O/g_vgb.jsonl 2> $O/g_vgb.err || { echo VGB FAILED; tail -5 $O/g_vgb.err; exit 1; }
 tail -3 $O/g_vgb.jsonl | cut -c1-250
