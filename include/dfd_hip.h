@@ -174,8 +174,8 @@ DFD_API int dfd_rn_gemm(void* stream, int dtype, const void* A, const void* B, v
  * out = relu?(conv(x, w) + bias (+ res)); w [Cout][kh*kw*Cin] (column (ky*kw + kx)*Cin + c);
  * Cin a power of two >= 8 unless kh = kw = stride = 1; kw 1 or 3.  bf16 with Cin % 64 == 0 and
  * Cout % 128 == 0 runs on the LDS-DMA NT GEMM of dfd_vgemm (1x1 stride 1: plain rows; 3x3 and strided:
- * per-tap implicit A gather); the epilogue order (fp32 acc + bias (+ res), ReLU, one rounding) is the
- * same on both kernels. */
+ * per-tap implicit A gather) and rounds once (fp32 acc + bias + res, ReLU); the implicit-GEMM kernel
+ * rounds acc + bias before adding res (bf16(bf16(acc + bias) + res)). */
 DFD_API int dfd_rn_conv(void* stream, int dtype, const void* x, int N, int H, int W, int Cin, int kh, int kw,
                         int stride, int pad, const void* w, const float* bias, const void* res, int relu, int Cout,
                         void* out);
