@@ -916,7 +916,6 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
 //          B2(j,c) = Wr[j][c], out = bc = inv_hw * .   (the squeeze path's input gradient)
 // The channel slices (gridDim.y) recompute the small first product instead of a second launch.
 constexpr int SE_RDMAX = 48, SE_TS = SE_RDMAX + 4, SE_CSL = 256, SE_W = 16;  // SE_W waves per workgroup
-constexpr int SE_KI = 5;  // first-product k iterations per load batch (forward; the backward's B1 loads are scalar: 3)
 typedef float se_f32x4 __attribute__((ext_vector_type(4)));
 
 // A is read from the squeeze / SE-backward partials A[h][f][c] (h < hsplit, added in order):
@@ -944,55 +943,48 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
   for (int t = 0; t < 3; ++t) acc1[t] = se_f32x4{0.f, 0.f, 0.f, 0.f};
   const bool fok = f0 + li < frames;
   // 16 k per iteration; lane group lk takes k = k0 + 4 lk + u in MFMA step u (the same
-  // permutation on both operands), so the row-major operands load as 16-B vectors (C % 8 == 0).
-  // SE_KI iterations' loads are issued before their MFMAs (C <= 1280: one batch; a wave's
-  // iterations were a chain of dependent round trips, ~3.5 us each at C = 1152)
-  constexpr int KI = FWD ? SE_KI : 3;
-  for (int kb = 16 * wave; kb < C; kb += 16 * SE_W * KI) {
-    float av[KI][4], bv[KI][4][3];
-#pragma unroll
-    for (int i = 0; i < KI; ++i) {
-      const int kq = kb + 16 * SE_W * i + 4 * lk;
-      const bool kok = kq < C;
-      if (fok && kok) {
-        const int64_t ai = (int64_t)(f0 + li) * C + kq, hn = (int64_t)frames * C;
-        float4 a4 = *reinterpret_cast<const float4*>(A + ai);
-        for (int h = 1; h < hsplit; ++h) {
-          const float4 v = *reinterpret_cast<const float4*>(A + h * hn + ai);
-          a4.x += v.x; a4.y += v.y; a4.z += v.z; a4.w += v.w;
-        }
-        if constexpr (FWD) {
-          a4.x *= a_scale; a4.y *= a_scale; a4.z *= a_scale; a4.w *= a_scale;
-        } else {
-          const float4 g = *reinterpret_cast<const float4*>(a_gate + ai);
-          a4.x = a4.x * g.x * (1.f - g.x); a4.y = a4.y * g.y * (1.f - g.y);
-          a4.z = a4.z * g.z * (1.f - g.z); a4.w = a4.w * g.w * (1.f - g.w);
-        }
-        if (blockIdx.y == 0) *reinterpret_cast<float4*>(a_out + ai) = a4;
-        av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
-      } else {
-        av[i][0] = av[i][1] = av[i][2] = av[i][3] = 0.f;
+  // permutation on both operands), so the row-major operands load as 16-B vectors (C % 8 == 0)
+  for (int k0 = 16 * wave; k0 < C; k0 += 16 * SE_W) {
+    const int kq = k0 + 4 * lk;
+    const bool kok = kq < C;
+    float av[4], bv[4][3];
+    if (fok && kok) {
+      const int64_t ai = (int64_t)(f0 + li) * C + kq, hn = (int64_t)frames * C;
+      float4 a4 = *reinterpret_cast<const float4*>(A + ai);
+      if (hsplit > 1)
+      for (int h = 1; h < hsplit; ++h) {
+        const float4 v = *reinterpret_cast<const float4*>(A + h * hn + ai);
+        a4.x += v.x; a4.y += v.y; a4.z += v.z; a4.w += v.w;
       }
+      if constexpr (FWD) {
+        a4.x *= a_scale; a4.y *= a_scale; a4.z *= a_scale; a4.w *= a_scale;
+      } else {
+        const float4 g = *reinterpret_cast<const float4*>(a_gate + ai);
+        a4.x = a4.x * g.x * (1.f - g.x); a4.y = a4.y * g.y * (1.f - g.y);
+        a4.z = a4.z * g.z * (1.f - g.z); a4.w = a4.w * g.w * (1.f - g.w);
+      }
+      if (blockIdx.y == 0) *reinterpret_cast<float4*>(a_out + ai) = a4;
+      av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
+    } else {
+      av[0] = av[1] = av[2] = av[3] = 0.f;
+    }
 #pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int n = 16 * t + li;
-        const bool ok = t < nt1 && n < rd && kok;
-        if constexpr (FWD) {
-          const float4 b4 = ok ? *reinterpret_cast<const float4*>(W1 + (int64_t)n * C + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
-          bv[i][0][t] = b4.x; bv[i][1][t] = b4.y; bv[i][2][t] = b4.z; bv[i][3][t] = b4.w;
-        } else {
+    for (int t = 0; t < 3; ++t) {
+      const int n = 16 * t + li;
+      const bool ok = t < nt1 && n < rd && kok;
+      if constexpr (FWD) {
+        const float4 b4 = ok ? *reinterpret_cast<const float4*>(W1 + (int64_t)n * C + kq) : make_float4(0.f, 0.f, 0.f, 0.f);
+        bv[0][t] = b4.x; bv[1][t] = b4.y; bv[2][t] = b4.z; bv[3][t] = b4.w;
+      } else {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) bv[i][u][t] = ok ? W1[(int64_t)(kq + u) * rd + n] : 0.f;
-        }
+        for (int u = 0; u < 4; ++u) bv[u][t] = ok ? W1[(int64_t)(kq + u) * rd + n] : 0.f;
       }
     }
 #pragma unroll
-    for (int i = 0; i < KI; ++i)
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-          if (t < nt1) acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][u], bv[i][u][t], acc1[t], 0, 0, 0);
+      for (int t = 0; t < 3; ++t)
+        if (t < nt1) acc1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u][t], acc1[t], 0, 0, 0);
   }
 #pragma unroll
   for (int t = 0; t < 3; ++t)

@@ -43,10 +43,8 @@ struct Dw2 {
   static_assert(GH * DRS * 8 + (K * K + 9 + 2 * FR) * DCG * 4 <= 80 * 1024, "two workgroups per CU");
 };
 
-// OCC workgroups per CU (launch bound): short strips hold fewer registers, so more waves per SIMD
-// cover the staging and y1 latency
-template <typename T, int K, int TH, int TW, int RS, int FR, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void dw_bwd2_kernel(
+template <typename T, int K, int TH, int TW, int RS, int FR>
+__global__ __launch_bounds__(256, 2) void dw_bwd2_kernel(
     DwGeom g, const T* __restrict__ dZ, const T* __restrict__ Y2, Dw1Bn2 b2, const float* __restrict__ w,
     const T* __restrict__ Y1, BnBwdIn bn1, T* __restrict__ out, float* __restrict__ stats, float* __restrict__ slab,
     int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
@@ -274,7 +272,7 @@ __global__ __launch_bounds__(256, OCC) void dw_bwd2_kernel(
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS, int FR, int OCC = 2>
+template <typename T, int K, int TH, int TW, int RS, int FR>
 static int bwd2_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, const Dw1Bn2& b2, const float* w,
                        const T* Y1, const BnBwdIn& bn1, T* out, float* stats, int* stat_rows, float* slab,
                        int64_t slab_cap, float* dW, bool accumulate) {
@@ -282,14 +280,14 @@ static int bwd2_launch(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2,
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
   const int64_t per = (int64_t)g.C * K * K;
-  const int resident = resident_wgs<dw_bwd2_kernel<T, K, TH, TW, RS, FR, OCC>, 256>();
+  const int resident = resident_wgs<dw_bwd2_kernel<T, K, TH, TW, RS, FR>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::max<int64_t>(1, std::min<int64_t>(rows, slab_cap / per));
   rows = std::min<int64_t>(rows, 1024);
   // XCD-aware order: faster on every stride-2 layer (kbench A/B, interleaved: blocks.1.0 -3 %,
   // 2.0 -11 %, 3.0 -20 %, 5.0 -3 %)
   const int xcd = DFD_DW_XCD >= 0 ? DFD_DW_XCD : (groups > 1);
-  hipLaunchKernelGGL((dw_bwd2_kernel<T, K, TH, TW, RS, FR, OCC>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, dZ,
+  hipLaunchKernelGGL((dw_bwd2_kernel<T, K, TH, TW, RS, FR>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, dZ,
                      Y2, b2, w, Y1, bn1, out, stats, slab, ntiles, groups, tiles_x, tiles_y, xcd);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
@@ -319,21 +317,12 @@ int launch_dw_bwd2(hipStream_t s, const DwGeom& g, const T* dZ, const T* Y2, con
   if (!dw_bwd2_covers(g)) return 1;
   const Dw1Bn2 b2{gate, bc, sc2, sh2, coef2};
   switch (dw2_config(g)) {
-    case 1: {
-      // strip length (knob dw2_rs): 14 input pixels (two balanced passes), or 4 (seven passes of
-      // 16 strips at lower register pressure: 3 workgroups per CU, or 4 with dw2_rs = 5)
-      const int rs = (int)tune(TK_DW2_RS);
-#define DFD_B2(KK, RSS, OCC) \
-  return bwd2_launch<T, KK, 8, 56, RSS, 1, OCC>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW, accumulate)
-      if (g.k == 3) {
-        if (rs == 4) DFD_B2(3, 4, 3);
-        if (rs == 5) DFD_B2(3, 4, 4);
-        DFD_B2(3, 14, 2);
-      }
-      if (rs == 4 || rs == 5) DFD_B2(5, 4, 3);
-      DFD_B2(5, 14, 2);
-#undef DFD_B2
-    }
+    case 1:
+      if (g.k == 3)
+        return bwd2_launch<T, 3, 8, 56, 14, 1>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
+                                               accumulate);
+      return bwd2_launch<T, 5, 8, 56, 14, 1>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
+                                             accumulate);
     case 2:
       return bwd2_launch<T, 3, 28, 28, 14, 1>(s, g, dZ, Y2, b2, w, Y1, bn1, out, stats, stat_rows, slab, slab_cap, dW,
                                               accumulate);

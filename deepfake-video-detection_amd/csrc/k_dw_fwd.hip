@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
   if constexpr (STATS) reduce_write_stats(st_s, st_q, reinterpret_cast<float*>(tin), stats + (int64_t)(blockIdx.x / groups) * 2 * C, C, c0);
 }
 
-template <typename T, int TH, int TW, int K, int S, bool PF = dwf_pf<TH, TW>()>
+template <typename T, int TH, int TW, int K, int S>
 static int fwd_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                       int* stat_rows) {
   if constexpr (!DwT<TH, TW, K, S>::fwd_ok) {
@@ -126,14 +126,14 @@ static int fwd_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w
     const int ntiles = g.frames * tiles_x * tiles_y;
     const int groups = cdiv(g.C, DCG);
     // persistent grid: the co-resident workgroups, at most 1024 (stat rows)
-    const int res = stats ? resident_wgs<dw_fwd_kernel<T, TH, TW, K, S, true, PF>, 256>()
-                          : resident_wgs<dw_fwd_kernel<T, TH, TW, K, S, false, PF>, 256>();
+    const int res = stats ? resident_wgs<dw_fwd_kernel<T, TH, TW, K, S, true>, 256>()
+                          : resident_wgs<dw_fwd_kernel<T, TH, TW, K, S, false>, 256>();
     const int gx = (int)(std::min<int64_t>(ntiles, std::max(1, std::min(res, 1024) / groups)) * groups);
     if (stats)
-      hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, true, PF>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
+      hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, true>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
                          ntiles, groups, tiles_x, tiles_y);
     else
-      hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, false, PF>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
+      hipLaunchKernelGGL((dw_fwd_kernel<T, TH, TW, K, S, false>), dim3(gx), dim3(256), 0, s, g, X, w, Y, pro, stats,
                          ntiles, groups, tiles_x, tiles_y);
     if (stat_rows) *stat_rows = gx / groups;
     DFD_HIP_CHECK(hipGetLastError());
@@ -158,10 +158,7 @@ static int fwd_ks(hipStream_t s, const DwGeom& g, const T* X, const float* w, T*
     case 1: return fwd_launch<T, 8, 28, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
     case 2: return fwd_launch<T, 14, 14, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
     case 3: return fwd_launch<T, 14, 7, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
-    case 4:
-      // knob dwf_pf bit 1: the stride-2 8x8 tiles prefetch the next tile's window
-      if (S == 2 && (tune(TK_DWF_PF) & 2)) return fwd_launch<T, 8, 8, K, S, true>(s, g, X, w, Y, pro, stats, stat_rows);
-      return fwd_launch<T, 8, 8, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
+    case 4: return fwd_launch<T, 8, 8, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
     default: return fwd_launch<T, 7, 7, K, S>(s, g, X, w, Y, pro, stats, stat_rows);
   }
 }

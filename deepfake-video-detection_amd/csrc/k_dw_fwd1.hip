@@ -11,6 +11,9 @@
 // strip / tile kernels on these shapes (VALU-issue bound: fewer instructions per output).
 #include "dw1_common.h"
 
+#ifndef DFD_FWD1_PF
+#define DFD_FWD1_PF 0  // next-tile register prefetch of the staged window (A/B knob)
+#endif
 
 namespace dfd {
 
@@ -39,9 +42,7 @@ struct Dwf1 {
   static_assert(LDS * OCC <= 160 * 1024, "LDS footprint sets the occupancy");
 };
 
-// PF: the next tile's window loads are issued right after this tile's commit and fly while its
-// strips run (knob dwf_pf, stride-2 tiles: their 17-row windows are 9 loads per lane)
-template <typename T, int K, int TH, int TW, int RS, int FR, int S, int RB, bool PF = false>
+template <typename T, int K, int TH, int TW, int RS, int FR, int S, int RB>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fwd1_kernel(
     DwGeom g, const T* __restrict__ Y1, const float* __restrict__ w, Pro bn1, T* __restrict__ out,
     float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
@@ -98,11 +99,11 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
       for (int kw = 0; kw < K; ++kw) wreg[kh][kw] = lds2(wts + (kh * K + kw) * DCG + 2 * cp);
   }
   Raw8<T> ry[D::NLD];
-  if (PF && bid / groups < ntiles) stage_load(bid / groups, ry);
+  if (DFD_FWD1_PF && bid / groups < ntiles) stage_load(bid / groups, ry);
   for (int t = bid / groups; t < ntiles; t += tstep) {
     const int f = (t / tpf) * FR, r = t - (t / tpf) * tpf, ty = r / tiles_x;
     const int iy0 = ty * TH, ix0 = (r - ty * tiles_x) * TW;
-    if (!PF) stage_load(t, ry);
+    if (!DFD_FWD1_PF) stage_load(t, ry);
     lds_barrier();  // the previous tile's strips are done with acts
 #pragma unroll
     for (int i = 0; i < D::NLD; ++i) {
@@ -126,7 +127,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
     }
     lds_barrier();
     // the next tile's window loads fly while this tile's strips run (issued before its stores)
-    if (PF && t + tstep < ntiles) stage_load(t + tstep, ry);
+    if (DFD_FWD1_PF && t + tstep < ntiles) stage_load(t + tstep, ry);
     if constexpr (RB == 1) {
 #pragma unroll 1
     for (int s = slot; s < D::NSTRIP; s += 16) {
@@ -243,20 +244,20 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
   }
 }
 
-template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1, int RB = 1, bool PF = false>
+template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1, int RB = 1>
 static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
                        int* stat_rows) {
   const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
   if (FR > 1 && (tiles_x != 1 || tiles_y != 1)) { set_error("dw_fwd1: frame stacking needs whole-map tiles", __FILE__, __LINE__); return -1; }
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
   const int groups = cdiv(g.C, DCG);
-  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB, PF>, 256>();
+  const int resident = resident_wgs<dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB>, 256>();
   int64_t rows = std::min<int64_t>(ntiles, std::max(1, resident / groups));
   rows = std::min<int64_t>(rows, 1024);  // the plan's BN-stat partial rows
   // XCD-aware order where it measured faster (kbench A/B: 56x56 s1 -16 %, 14x14 c480 -2..-6 %); the
   // 14x14 k5 c672 (+7 %), stacked 7x7 (+7..12 %) and single-group layers keep dispatch order
   const int xcd = DFD_DW_XCD >= 0 ? DFD_DW_XCD : (groups > 1 && (g.Ho >= 28 || (g.Ho == 14 && g.C <= 480)));
-  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB, PF>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
+  hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
                      pro, Y, stats, ntiles, groups, tiles_x, tiles_y, xcd);
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
@@ -282,13 +283,12 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
     // k3 stride 2 (112->56, 28->14): the 8x8 tile kernel is as fast or faster (kbench: 214 vs 246,
     // 42 vs 42 us); k5: 153 -> 126 and 43 -> 35 us
     if (g.k == 3) return 0;
-    const bool pf = (tune(TK_DWF_PF) & 1) != 0;  // knob dwf_pf bit 0
     if (H == 7 && W == 7)
-      rc = pf ? fwd1_launch<T, 5, 7, 7, 7, 2, 2, 1, true>(s, g, X, w, Y, pro, stats, stat_rows)
-              : fwd1_launch<T, 5, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+                    : fwd1_launch<T, 5, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows);
     else if (H % 7 == 0 && W % 14 == 0)
-      rc = pf ? fwd1_launch<T, 5, 7, 14, 7, 1, 2, 1, true>(s, g, X, w, Y, pro, stats, stat_rows)
-              : fwd1_launch<T, 5, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
+                    : fwd1_launch<T, 5, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows);
     else
       return 0;
   } else if (H == 7 && W == 7) {
