@@ -545,8 +545,8 @@ int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, i
   DFD_GUARD_END
 }
 
-// the kernel test seams' overrides (dfd_set_tuning): read only by dfd_pw_conv / dfd_pw_conv_wgrad,
-// which install a snapshot for their own launch; plans never see them (dfd_b0_plan_set_tuning)
+// the kernel test seams' overrides (dfd_set_tuning): read only by dfd_pw_conv / dfd_pw_conv_wgrad /
+// dfd_vgemm, which install a snapshot for their own launch; plans and models never see them
 static std::mutex g_seam_mu;
 static dfd::Tuning g_seam;
 static dfd::Tuning seam_snapshot() {
@@ -627,6 +627,8 @@ int64_t dfd_vgemm_tn_slab_floats(int64_t M, int N, int K) {
 int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const void* R, const float* bias,
               const void* Z, void* G, int64_t M, int N, int K, int epi, float* slab, int64_t slab_floats) {
   DFD_GUARD_BEGIN
+  const dfd::Tuning tn = seam_snapshot();  // a kernel test seam: the dfd_set_tuning overrides apply (vg_xp)
+  const dfd::TuningScope ts(&tn);
   hipStream_t s = (hipStream_t)stream;
   if (!A || !B || !C) { dfd::set_error("vgemm: null argument", __FILE__, __LINE__); return -1; }
   if (op == 0 || op == 2 || op == 4 || op == 5) {  // NT: own kernel (0; 4 / 5: 256- / 128-wide tiles) or hipBLASLt (2)

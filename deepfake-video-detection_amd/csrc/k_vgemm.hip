@@ -169,6 +169,32 @@ __device__ __forceinline__ void mma_step(const char* Ai, const char* Bi, int rba
   }
 }
 
+// XP schedule (NT): a sub-step's fragments are read while the previous sub-step's MFMAs run, across
+// the K-step barrier too (the next K-step's first fragments are read right after it, under the
+// second sub-step's MFMAs) -- the waves of a SIMD no longer all wait on LDS reads at once after each
+// barrier
+template <int MI, int NJ>
+struct Frags {
+  s16x8 a[MI], b[NJ];
+};
+template <int MI, int NJ>
+__device__ __forceinline__ void frags_nt(const char* Ai, const char* Bi, int rbase, int cbase, int s, int lane,
+                                         Frags<MI, NJ>& f) {
+#pragma unroll
+  for (int i = 0; i < MI; ++i) f.a[i] = frag_nt(Ai, rbase + 16 * i, s, lane);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) f.b[j] = frag_nt(Bi, cbase + 16 * j, s, lane);
+}
+template <int MI, int NJ>
+__device__ __forceinline__ void mma_frags(const Frags<MI, NJ>& f, Acc<MI, NJ>& acc) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc.v[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[i], f.b[j], acc.v[i][j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
 // a wave's accumulators into the fp32 staging image E (row stride eps) at (r0, c0)
 template <int MI, int NJ>
 __device__ __forceinline__ void epi_put(float* E, const Acc<MI, NJ>& acc, int r0, int c0, int eps, int lane) {
@@ -185,7 +211,7 @@ __device__ __forceinline__ void st8bf(bf16* p, const float (&v)[8]) { st8(p, v);
 // ---------------------------------------------------------------- kernels
 // BNT = 256: 8 waves as 2 (M) x 4 (N), 128 x 64 each; BNT = 128 (N = 768-wide products: 2.3 instead of
 // 1.2 dispatch waves of tiles, so the last wave idles less): 4 (M) x 2 (N) waves of 64 x 64
-template <int EP, int BNT, bool CONV = false>
+template <int EP, int BNT, bool CONV = false, bool XP = false>
 __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
   constexpr int WMN = BNT == VT ? 2 : 4, WNN = 8 / WMN;  // waves along M / N
   constexpr int MI = VT / WMN / 16, NJ = BNT / WNN / 16;
@@ -229,16 +255,41 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
   else vm_wait_n<0>();
   lds_bar();
   int cb = 0, pb = NST - 1;  // buffers of K-steps kt and kt + NST - 1
+  const int rb = wm * (VT / WMN), cbs = wn * (BNT / WNN);
+  if constexpr (XP) {
+    Frags<MI, NJ> f0, f1;
+    frags_nt(smem, smem + VTILE, rb, cbs, 0, lane, f0);
+    for (int kt = 0; kt < nk; ++kt) {
+      char* cur = smem + cb * STAGE;
+      const bool pre = kt + NST - 1 < nk;
+      if (pre) stage(kt + NST - 1, smem + pb * STAGE);
+      frags_nt(cur, cur + VTILE, rb, cbs, 1, lane, f1);
+      // f0's reads (issued before f1's) have landed once at most f1's MI + NJ reads are outstanding
+      __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | ((MI + NJ) << 8) | (3 << 14));
+      mma_frags(f0, acc);
+      if (NST == 3 && pre) vm_wait_n<NPS>();
+      else vm_wait_n<0>();
+      lds_bar();  // this K-step's reads done everywhere (f1 included); K-step kt + 1 landed
+      cb = cb == NST - 1 ? 0 : cb + 1;
+      pb = pb == NST - 1 ? 0 : pb + 1;
+      // unconditional (after the last K-step it reads a stale image, unused): no branch, so the
+      // compiler's LDS wait before f1's MFMAs stays counted
+      frags_nt(smem + cb * STAGE, smem + cb * STAGE + VTILE, rb, cbs, 0, lane, f0);
+      __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | ((MI + NJ) << 8) | (3 << 14));  // f1 landed before the barrier
+      mma_frags(f1, acc);
+    }
+  } else {
   for (int kt = 0; kt < nk; ++kt) {
     char* cur = smem + cb * STAGE;
     const bool pre = kt + NST - 1 < nk;
     if (pre) stage(kt + NST - 1, smem + pb * STAGE);  // the buffer K-step kt - 1 read (barrier passed)
-    mma_step<false>(cur, cur + VTILE, wm * (VT / WMN), wn * (BNT / WNN), lane, acc);
+    mma_step<false>(cur, cur + VTILE, rb, cbs, lane, acc);
     if (NST == 3 && pre) vm_wait_n<NPS>();  // K-step kt + 1 landed; kt + 2 may still be in flight
     else vm_wait_n<0>();
     lds_bar();  // this K-step's reads done everywhere
     cb = cb == NST - 1 ? 0 : cb + 1;
     pb = pb == NST - 1 ? 0 : pb + 1;
+  }
   }
   // epilogue: two passes of 128 rows through LDS; a pass's residual / derivative rows are loaded
   // before its staging barrier (their latency under the LDS round trip, not per row)
@@ -420,10 +471,15 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
     DFD_HIP_CHECK(hipGetLastError());
     return 0;
   }
-  switch (ep * 2 + (bn == 128)) {
-#define DFD_VG(E)                                                                                       \
-  case 2 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT>), dim3(tiles), dim3(512), 0, s, a); break; \
-  case 2 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128>), dim3(tiles), dim3(512), 0, s, a); break;
+  // knob vg_xp: the fragment-pipelined K loop (XP); bit 0 for the 128-wide tile, bit 1 for the 256-wide
+  const int64_t xpk = tune(TK_VG_XP);
+  const bool xp = (xpk & (bn == 128 ? 1 : 2)) != 0;
+  switch ((ep * 2 + (bn == 128)) * 2 + xp) {
+#define DFD_VG(E)                                                                                                   \
+  case 4 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT>), dim3(tiles), dim3(512), 0, s, a); break;             \
+  case 4 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, VT, false, true>), dim3(tiles), dim3(512), 0, s, a); break; \
+  case 4 * (E) + 2: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128>), dim3(tiles), dim3(512), 0, s, a); break;        \
+  case 4 * (E) + 3: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128, false, true>), dim3(tiles), dim3(512), 0, s, a); break;
     DFD_VG(0) DFD_VG(VG_BIAS) DFD_VG(VG_BIAS | VG_RESID) DFD_VG(VG_BIAS | VG_GELU2) DFD_VG(VG_DGELU)
     DFD_VG(VG_BIAS | VG_RELU) DFD_VG(VG_BIAS | VG_RESID | VG_RELU)
 #undef DFD_VG

@@ -40,11 +40,11 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 // Kernel-selection knobs.  No process-wide mutable state is consulted on a model path: every knob
 // has a compile-time default (tune_default), a plan's forward/backward installs the plan's own
 // overrides (dfd_b0_plan_set_tuning) for the enqueuing thread (TuningScope), and the kernel test
-// seams (dfd_pw_conv, dfd_pw_conv_wgrad) install a snapshot of the seam overrides of dfd_set_tuning.
+// seams (dfd_pw_conv, dfd_pw_conv_wgrad, dfd_vgemm) install a snapshot of the seam overrides of dfd_set_tuning.
 // Concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -54,7 +54,7 @@ struct Tuning {
 // fused depthwise backward / channel-pair kernels on; tiled-GEMM config automatic (-1); weight
 // gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on; small-K
 // weight-panel GEMM (k_pw_sk.hip) off until measured
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 2};
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 2, 0};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {

@@ -133,3 +133,22 @@ def test_vgemm_nt_tile_widths_agree(cuda):
     B = torch.zeros(640, 128, device=cuda).bfloat16()
     C = torch.zeros(64, 640, device=cuda).bfloat16()
     assert _lib.load().dfd_vgemm(None, 4, P(A), P(B), P(C), None, None, None, None, 64, 640, 128, 0, None, 0) != 0
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(1000, 768, 768, 3), (394, 3072, 768, 5), (777, 3072, 768, 8),
+                                       (300, 2304, 64, 1), (8 * 197, 768, 2304, 0)])
+def test_vgemm_nt_xp_bit_identical(cuda, M, N, K, epi):
+    """the fragment-pipelined K loop (knob vg_xp, through the dfd_set_tuning seam) issues the same
+    MFMAs in the same order per output: bit-identical to the default loop at both tile widths,
+    one-K-step products (K = 64) included"""
+    lib = _lib.load()
+    outs = {}
+    try:
+        for xp in (3, 0):
+            lib.dfd_set_tuning(b"vg_xp", xp)
+            outs[xp] = [_nt(cuda, M, N, K, epi, 17, op)[:2] for op in (4, 5) if N % 256 == 0 or op == 5]
+    finally:
+        lib.dfd_set_tuning(b"vg_xp", 0)
+    for (c3, g3), (c0, g0) in zip(outs[3], outs[0]):
+        assert torch.equal(c3, c0)
+        assert (g3 is None) == (g0 is None) and (g3 is None or torch.equal(g3, g0))

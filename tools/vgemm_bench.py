@@ -1,5 +1,6 @@
 """Time the ViT trunk's GEMM shapes (C5: 128 images x 197 tokens = 25,216 rows) on the own LDS-DMA
-kernels (k_vgemm.hip; NT products also with the 256- / 128-wide tile forced, "own256" / "own128")
+kernels (k_vgemm.hip; NT products also with the 256- / 128-wide tile forced, "own256" / "own128", and
+with the fragment-pipelined K loop, "xp")
 against hipBLASLt,
 HIP events on the current stream, interleaved rounds.
 
@@ -46,10 +47,11 @@ def main():
             C = torch.empty(N, K, device=dev)
             slab = torch.empty(max(lib.dfd_vgemm_tn_slab_floats(M, N, K), 4 * N * K), device=dev)
             args = lambda o: (st, o, P(A), P(B), P(C), None, None, None, None, M, N, K, 0, P(slab), slab.numel())  # noqa: E731
-        arms = (("own", op), ("blaslt", op + 2)) + ((("own256", 4), ("own128", 5)) if op == 0 else ())
+        arms = (("own", op), ("blaslt", op + 2)) + ((("own256", 4), ("own128", 5), ("xp", 0)) if op == 0 else ())
         times = {arm: [] for arm, _ in arms}
         for r in range(rounds + 1):
             for arm, o in arms:
+                lib.dfd_set_tuning(b"vg_xp", 3 if arm == "xp" else 0)  # the fragment-pipelined K loop
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 _lib.check(lib.dfd_vgemm(*args(o)))
                 e0.record()
