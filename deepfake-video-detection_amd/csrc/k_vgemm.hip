@@ -50,7 +50,10 @@ template <int N>
 __device__ __forceinline__ void vm_wait_n() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
-__device__ __forceinline__ void lds_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void lds_bar() {
+  __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0), visible to the compiler's wait tracking
+  __builtin_amdgcn_s_barrier();
+}
 
 // ---------------------------------------------------------------- NT: C = A . B^T
 // One K-step image of an operand: [ROWS rows][64 k] bf16, 128-B rows, chunk (16 B) c of row r at
@@ -472,6 +475,7 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
     return 0;
   }
   // knob vg_xp: the fragment-pipelined K loop (XP); bit 0 for the 128-wide tile, bit 1 for the 256-wide
+  // (the weight-gradient kernel's form of it needs 2 x 24 fragment registers and spills: not built)
   const int64_t xpk = tune(TK_VG_XP);
   const bool xp = (xpk & (bn == 128 ? 1 : 2)) != 0;
   switch ((ep * 2 + (bn == 128)) * 2 + xp) {
