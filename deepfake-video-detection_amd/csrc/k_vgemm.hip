@@ -51,8 +51,10 @@ __device__ __forceinline__ void vm_wait_n() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 __device__ __forceinline__ void lds_bar() {
+  asm volatile("" ::: "memory");  // no memory operation moves across (the builtins below touch no memory)
   __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0), visible to the compiler's wait tracking
   __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // ---------------------------------------------------------------- NT: C = A . B^T
