@@ -458,7 +458,8 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 // (thread = pixel), 8 MFMAs per wave, rounded tile through an LDS slab for 16-B row stores,
 // BN-stat partials from the rounded values (per lane, fixed-order reduction at the end).
 constexpr int SFC = SCO + 8;  // LDS row stride (bf16) of the output slab
-// OCC workgroups per CU (knob stem_occ: 2, or 3 at 168 VGPRs with some loop invariants spilled)
+// OCC workgroups per CU (knob stem_occ, default 3: the output slab aliases the im2col tile, 44 KB of
+// LDS, and the dense-uint8 instantiation fits 168 VGPRs; 2 is the previous occupancy)
 template <int OCC, int FMT>
 __global__ __launch_bounds__(256, OCC) void stem_fwd_mfma_kernel(StemGeom g, const void* __restrict__ x,
                                                             const float* __restrict__ w, bf16* __restrict__ Y,
@@ -596,14 +597,13 @@ template <typename T>
 int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float* w, T* Y, float* stats,
                     int* stat_rows) {
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
-  const bool occ3 = sizeof(T) == 2 && tune(TK_STEM_OCC) == 3;
+  // dense uint8 frames only: the strided-input instantiation spills at 168 VGPRs
+  const bool occ3 = sizeof(T) == 2 && tune(TK_STEM_OCC) == 3 && g.in.u8 == 2;
   const int gx = (int)std::min<int64_t>(ntiles, occ3 ? 768 : 1024);  // whole rounds of co-resident workgroups
   if constexpr (sizeof(T) == 2) {
     const bool dense = g.in.u8 == 2;
-    if (occ3 && dense)
+    if (occ3)
       hipLaunchKernelGGL((stem_fwd_mfma_kernel<3, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
-    else if (occ3)
-      hipLaunchKernelGGL((stem_fwd_mfma_kernel<3, -1>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
     else if (dense)
       hipLaunchKernelGGL((stem_fwd_mfma_kernel<2, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
     else

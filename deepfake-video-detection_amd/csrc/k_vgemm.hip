@@ -465,10 +465,13 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
       set_error("vgemm: convolution shape not covered", __FILE__, __LINE__);
       return -1;
     }
-    switch (ep * 2 + (bn == 128)) {
-#define DFD_VGC(E)                                                                                            \
-  case 2 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT, true>), dim3(tiles), dim3(512), 0, s, a); break; \
-  case 2 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128, true>), dim3(tiles), dim3(512), 0, s, a); break;
+    const bool xpc = (tune(TK_VG_XP) & (bn == 128 ? 1 : 2)) != 0;
+    switch ((ep * 2 + (bn == 128)) * 2 + xpc) {
+#define DFD_VGC(E)                                                                                                   \
+  case 4 * (E): hipLaunchKernelGGL((vgemm_nt_kernel<E, VT, true>), dim3(tiles), dim3(512), 0, s, a); break;        \
+  case 4 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, VT, true, true>), dim3(tiles), dim3(512), 0, s, a); break; \
+  case 4 * (E) + 2: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128, true>), dim3(tiles), dim3(512), 0, s, a); break;   \
+  case 4 * (E) + 3: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128, true, true>), dim3(tiles), dim3(512), 0, s, a); break;
       DFD_VGC(VG_BIAS) DFD_VGC(VG_BIAS | VG_RELU) DFD_VGC(VG_BIAS | VG_RESID | VG_RELU)
 #undef DFD_VGC
       default: set_error("vgemm: convolution epilogue not instantiated", __FILE__, __LINE__); return -1;

@@ -53,8 +53,10 @@ struct Tuning {
 // defaults: streaming 1x1 kernels from 40,000 rows; BN-folded conv_pw backward from 100,000 rows;
 // fused depthwise backward / channel-pair kernels on; tiled-GEMM config automatic (-1); weight
 // gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on; small-K
-// weight-panel GEMM (k_pw_sk.hip) off until measured
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 2, 0};
+// weight-panel GEMM (k_pw_sk.hip) on for K <= 192; depthwise prefetch / row blocking on; the stem
+// forward at 3 workgroups per CU (120 -> 91 us, profiles/r04 kernel_stats_r04h*); the vgemm NT
+// fragment-pipelined K loop at both tile widths (-7..-16 % per ViT shape, vgemm_vs_blaslt_r04h)
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, 3};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {

@@ -222,13 +222,16 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
 def test_forward_knob_eval_bit_identical(cuda, knob, on, off):
     """Eval mode (running statistics, no batch sums): the two-row forward strips (dw_rb bit 0)
     compute every depthwise output from the same taps in the same order as the one-row strips, and
-    the stem forward at 3 workgroups per CU (stem_occ = 3, off by default) every output pixel with the
-    same MFMA, so the logits are bit-identical.  (In training stem_occ = 3 changes the BN-stat row
-    partition -- 768 instead of 1024 rows -- and the b4t8 step's temporal_attention.0.bias gradient
-    then moves to cosine 0.964 against the default: that gradient is the chaotic one of the knob
-    test above; the knob is not in it.)"""
+    the stem forward at 3 workgroups per CU (stem_occ = 3, the default for dense uint8 frames; 2 is the
+    previous occupancy) every output pixel with the same MFMA, so the logits are bit-identical.  (In
+    training the occupancy changes the BN-stat row partition -- 768 instead of 1024 rows -- and the
+    b4t8 step's temporal_attention.0.bias gradient moves to cosine 0.964 between the two: that
+    gradient is the chaotic one of the knob test above; the knob is not in it.)"""
     from deepfake_amd import backbone
     x, _ = _inputs("b4t8")
+    if knob == "stem_occ":  # the dense-uint8 stem (the bench's feed): uint8 NHWC crops, permuted view
+        g = torch.Generator().manual_seed(5)
+        x = torch.randint(0, 256, (4, 8, 224, 224, 3), generator=g, dtype=torch.uint8).permute(0, 1, 4, 2, 3)
     outs = []
     prev = dict(backbone.DEFAULT_TUNING)
     try:
