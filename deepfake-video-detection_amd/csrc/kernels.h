@@ -44,7 +44,7 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 // Concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP, TK_STEM_WG, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -56,7 +56,7 @@ struct Tuning {
 // weight-panel GEMM (k_pw_sk.hip) on for K <= 192; depthwise prefetch / row blocking on; the stem
 // forward at 3 workgroups per CU (120 -> 91 us, profiles/r04 kernel_stats_r04h*); the vgemm NT
 // fragment-pipelined K loop at both tile widths (-7..-16 % per ViT shape, vgemm_vs_blaslt_r04h)
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, 3};
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, 3, 1};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {
