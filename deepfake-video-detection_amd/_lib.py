@@ -14,7 +14,8 @@ import threading
 import torch  # noqa: F401  (must be loaded first: provides the HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdfd_hip.so")
+# DFD_HIP_LIB: an alternate in-tree build of the same library (A/B measurements, tools/ab_lib.sh)
+LIB_PATH = os.environ.get("DFD_HIP_LIB") or os.path.join(_HERE, "libdfd_hip.so")
 
 _lock = threading.Lock()
 _lib = None

@@ -56,7 +56,10 @@ struct Tuning {
 // weight-panel GEMM (k_pw_sk.hip) on for K <= 192; depthwise prefetch / row blocking on; the stem
 // forward at 3 workgroups per CU (120 -> 91 us, profiles/r04 kernel_stats_r04h*); the vgemm NT
 // fragment-pipelined K loop at both tile widths (-7..-16 % per ViT shape, vgemm_vs_blaslt_r04h)
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, 3, 1};
+#ifndef DFD_VG_XP_DEFAULT  // A/B builds of k_vgemm.o only (tools/ab_lib.sh): the one reader of TK_VG_XP
+#define DFD_VG_XP_DEFAULT 3
+#endif
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, DFD_VG_XP_DEFAULT, 1};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {
