@@ -451,138 +451,6 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
   }
 }
 
-// The same weight gradient without the im2col image (knob stem_wg, default on): each lane builds its
-// B fragment -- patch[p][tap] for its tap column and the 8 pixels k = 8 (lane >> 4) + j of the
-// k-step, exactly the values and the k order the transposed reads of xs delivered -- straight from
-// the staged input tile (8 fp32 LDS reads, rounded to bf16 as the im2col store did).  No xs image
-// (61 -> 41 KB of LDS), no im2col barrier, 3 workgroups per CU for the dense-uint8 input; the grid
-// (and so the slab rows) is unchanged: bit-identical weight gradient.
-template <int FMT>
-__global__ __launch_bounds__(256, 3) void stem_wgrad_direct_kernel(StemGeom g, const void* __restrict__ x,
-                                                                 const bf16* __restrict__ dY, const bf16* __restrict__ Yb,
-                                                                 const float* __restrict__ coef,
-                                                                 float* __restrict__ slab, int64_t ntiles) {
-  __shared__ float tin[SNIN];
-  __shared__ float lut[SLUT];
-  __shared__ uint32_t u8s[SNW];
-  stem_lut_init(g, lut);
-  __shared__ __attribute__((aligned(16))) bf16 ys[ST * ST * SWL];  // dY tile [pix][co]; reused for the reduction
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
-  stw_f32x4_t acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = stw_f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float nx[SNLD];
-  uint32_t nxok = 0u;
-  Raw8<bf16> nd[4];
-  Raw8<bf16> ny[4];
-  __shared__ __attribute__((aligned(16))) float bnk[3][SCO];
-  stem_bn_coef(coef, bnk);
-  auto load_dy = [&](int64_t t) {
-    int f, oy0, ox0;
-    tl.coords(t, f, oy0, ox0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
-      const int oy = oy0 + pix / ST, ox = ox0 + pix % ST;
-      const int64_t o = (((int64_t)f * g.Ho + oy) * g.Wo + ox) * SCO + v * 8;
-      raw_ld(nd[i], dY + o, dY, oy < g.Ho && ox < g.Wo);
-      if (coef) raw_ld(ny[i], Yb + o, Yb, oy < g.Ho && ox < g.Wo);
-    }
-  };
-  const int gq = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3, ci16 = lane & 15;
-  // this lane's tap columns b * 16 + ci16 (b = 0, 1): offset of the tap within a pixel's input window
-  // (-1: a zero pad, tap >= 27)
-  int toff[2];
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const int tap = b * 16 + ci16;
-    toff[b] = tap < 27 ? (((tap % 9) / 3) * SIE + tap % 3) * 3 + tap / 9 : -1;
-  }
-  int64_t t = blockIdx.x;
-  if (t < ntiles) {
-    int f, oy0, ox0;
-    tl.coords(t, f, oy0, ox0);
-    stem_load<FMT>(g, x, f, oy0 * 2 - 1, ox0 * 2 - 1, nx, nxok);
-    load_dy(t);
-  }
-  for (; t < ntiles; t += gridDim.x) {
-    int f, oy0, ox0;
-    tl.coords(t, f, oy0, ox0);
-    lds_barrier();
-    stem_store<FMT>(g, lut, u8s, tin, nx, nxok, oy0 * 2 - 1, ox0 * 2 - 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + 256 * i, pix = e >> 2, v = e & 3;
-      if (coef) {
-        float d[8];
-        raw_to_f(nd[i], d);
-        stem_bn_apply(nd[i].ok, d, ny[i], bnk, v);
-        st8(ys + pix * SWL + v * 8, d);
-      } else {
-        raw_st(ys + pix * SWL + v * 8, nd[i]);
-      }
-    }
-    lds_barrier();
-    // the next tile's input bytes now (few registers); its dY / y loads after the MFMAs (their 32
-    // registers would otherwise be live across the fragment build)
-    if (t + gridDim.x < ntiles) {
-      int f2, oy2, ox2;
-      tl.coords(t + gridDim.x, f2, oy2, ox2);
-      stem_load<FMT>(g, x, f2, oy2 * 2 - 1, ox2 * 2 - 1, nx, nxok);
-    }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int p0 = (wave * 2 + ks) * 32;
-      // pixels p0 + 8 gq + j (j < 8) share one tile row: ly = (p0 >> 4) + (gq >> 1), lx = 8 (gq & 1) + j
-      const int pbase = (((p0 >> 4) + (gq >> 1)) * 2 * SIE + 16 * (gq & 1)) * 3;
-      stw_bf16x8_t bfr[2], afr[2];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = toff[b] >= 0 ? tin[pbase + toff[b] + 6 * j] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t pk = pack2bf(v[2 * j], v[2 * j + 1]);
-          bfr[b][2 * j] = (short)(pk & 0xffffu);
-          bfr[b][2 * j + 1] = (short)(pk >> 16);
-        }
-        const stw_s16x4_t alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (stw_lds_s16x4_t*)(ys + (p0 + 8 * gq + q) * SWL + b * 16 + 4 * pq));
-        const stw_s16x4_t ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (stw_lds_s16x4_t*)(ys + (p0 + 8 * gq + 4 + q) * SWL + b * 16 + 4 * pq));
-        afr[b] = stw_bf16x8_t{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[a], bfr[b], acc[a][b], 0, 0, 0);
-    }
-    if (t + gridDim.x < ntiles) load_dy(t + gridDim.x);
-  }
-  lds_barrier();
-  float* red = reinterpret_cast<float*>(ys);
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = a * 16 + 4 * (lane >> 4) + r, tap = b * 16 + (lane & 15);
-        red[(wave * 32 + co) * 32 + tap] = acc[a][b][r];
-      }
-  lds_barrier();
-  float* out = slab + (int64_t)blockIdx.x * 27 * SCO;
-  for (int i = tid; i < 27 * SCO; i += 256) {
-    const int co = i / 27, tap = i % 27;
-    out[i] = ((red[(0 * 32 + co) * 32 + tap] + red[(1 * 32 + co) * 32 + tap]) + red[(2 * 32 + co) * 32 + tap]) +
-             red[(3 * 32 + co) * 32 + tap];
-  }
-}
-
 // bf16 mode forward on v_mfma_f32_16x16x32_bf16: the 27 taps (+5 zero pads) are ONE 32-deep
 // k-step, so per 16-pixel block and 16 output channels a single MFMA computes the transposed
 // tile D[co][pix] = W[co][:] . patch[pix][:] (lanes then hold 4 consecutive channels of one
@@ -757,12 +625,8 @@ int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* 
   const int64_t ntiles = (int64_t)g.frames * cdiv(g.Ho, ST) * cdiv(g.Wo, ST);
   int gx = (int)std::min<int64_t>(ntiles, 1024);
   gx = (int)std::max<int64_t>(1, std::min<int64_t>(gx, slab_cap / (27 * SCO)));
-  if constexpr (sizeof(T) == 2) {
-    if (tune(TK_STEM_WG) != 0 && g.in.u8 == 2)  // dense uint8 frames (the strided form spills)
-      hipLaunchKernelGGL(stem_wgrad_direct_kernel<2>, dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
-    else
-      hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
-  }
+  if constexpr (sizeof(T) == 2)
+    hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
   else  // fp32 parity mode: exact fp32 products
     hipLaunchKernelGGL((stem_wgrad_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
   DFD_HIP_CHECK(hipGetLastError());

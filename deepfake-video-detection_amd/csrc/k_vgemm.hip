@@ -24,6 +24,12 @@
 #include "kernels.h"
 #include "vit.h"
 
+// 1: fc1's gelu / gelu' epilogue on the branch-free rational erf (common.h erf_rat_); 0: the library
+// erff (A/B builds, tools/ab_lib.sh)
+#ifndef DFD_GELU_RAT
+#define DFD_GELU_RAT 1
+#endif
+
 namespace dfd {
 namespace {
 
@@ -349,7 +355,10 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
           // C = gelu'(z), G = gelu(z) of the stored (rounded) pre-activation z
           float g[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) gelu_pair_(Tr<bf16>::round(o[j]), g[j], o[j]);
+          for (int j = 0; j < 8; ++j) {
+            if (DFD_GELU_RAT) gelu_pair_rat_(Tr<bf16>::round(o[j]), g[j], o[j]);
+            else gelu_pair_(Tr<bf16>::round(o[j]), g[j], o[j]);
+          }
           st8bf(a.G + (int64_t)row * a.ldc + c, g);
         }
         st8bf(a.C + (int64_t)row * a.ldc + c, o);

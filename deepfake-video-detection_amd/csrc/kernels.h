@@ -44,7 +44,7 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 // Concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP, TK_STEM_WG, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -55,11 +55,12 @@ struct Tuning {
 // gradients on the main stream; fused 7x7 MBConv off; fused projection / fold backward on; small-K
 // weight-panel GEMM (k_pw_sk.hip) on for K <= 192; depthwise prefetch / row blocking on; the stem
 // forward at 3 workgroups per CU (120 -> 91 us, profiles/r04 kernel_stats_r04h*); the vgemm NT
-// fragment-pipelined K loop at both tile widths (-7..-16 % per ViT shape, vgemm_vs_blaslt_r04h)
+// fragment-pipelined K loop for the 128-wide tile only (in-model A/B, profiles/r04 ab_vg_xp_r04l:
+// the 256-wide form is faster in the L2-warm microbenchmark but not in the ViT step)
 #ifndef DFD_VG_XP_DEFAULT  // A/B builds of k_vgemm.o only (tools/ab_lib.sh): the one reader of TK_VG_XP
-#define DFD_VG_XP_DEFAULT 3
+#define DFD_VG_XP_DEFAULT 1
 #endif
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, DFD_VG_XP_DEFAULT, 1};
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, DFD_VG_XP_DEFAULT};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {

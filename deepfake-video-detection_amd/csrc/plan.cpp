@@ -814,7 +814,7 @@ int plan_fused7_blocks(const Plan& p) {
 
 
 const char* const kTuneNames[TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile", "dw_bwd1",
-                                          "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused", "pw_sk", "dw_pf", "dw_rb", "stem_occ", "vg_xp", "stem_wg"};
+                                          "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused", "pw_sk", "dw_pf", "dw_rb", "stem_occ", "vg_xp"};
 static thread_local const Tuning* t_tune = nullptr;
 int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tune) { t_tune = t; }

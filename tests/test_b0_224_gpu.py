@@ -70,16 +70,8 @@ def oracle_step(case):
     return _ORACLE[case]
 
 
-def _u8_inputs(case):
-    """dense uint8 NHWC crops viewed as (B, T, 3, H, W): the bench's feed (the stem's dense-uint8 path)"""
-    b, t = CASES[case]
-    g = torch.Generator().manual_seed(SEED + 2)
-    x = torch.randint(0, 256, (b, t, 224, 224, 3), generator=g, dtype=torch.uint8).permute(0, 1, 4, 2, 3)
-    return x, _inputs(case)[1]
-
-
-def hip_step(case, dtype, cuda, u8=False):
-    x, labels = _u8_inputs(case) if u8 else _inputs(case)
+def hip_step(case, dtype, cuda):
+    x, labels = _inputs(case)
     torch.manual_seed(0)
     det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
                                      compute_dtype=dtype)
@@ -258,23 +250,3 @@ def test_forward_knob_eval_bit_identical(cuda, knob, on, off):
     assert torch.isfinite(outs[1]).all()
     assert torch.equal(outs[0], outs[1])
 
-
-def test_stem_wgrad_direct_bit_identical(cuda):
-    """the stem weight gradient without the im2col image (knob stem_wg, default on: B fragments
-    built from the staged input tile, 3 workgroups per CU, same grid) against the im2col kernel on
-    the dense-uint8 bf16 training step: every gradient and buffer bit-identical"""
-    from deepfake_amd import backbone
-    prev = dict(backbone.DEFAULT_TUNING)
-    try:
-        backbone.DEFAULT_TUNING["stem_wg"] = 1
-        _, _, loss_a, grads_a, bufs_a = hip_step("b4t8", "bf16", cuda, u8=True)
-        backbone.DEFAULT_TUNING["stem_wg"] = 0
-        _, _, loss_b, grads_b, bufs_b = hip_step("b4t8", "bf16", cuda, u8=True)
-    finally:
-        backbone.DEFAULT_TUNING.clear()
-        backbone.DEFAULT_TUNING.update(prev)
-    assert loss_a == loss_b
-    diff = [n for n in grads_a if not torch.equal(grads_a[n], grads_b[n])]
-    assert not diff, diff[:10]
-    assert all(torch.equal(bufs_a[n], bufs_b[n]) for n in bufs_a)
-    assert float(grads_a["backbone.0.weight"].abs().sum()) > 0
