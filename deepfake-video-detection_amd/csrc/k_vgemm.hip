@@ -127,11 +127,13 @@ __device__ __forceinline__ s16x8 frag_nt(const char* img, int base, int s, int l
 // c ^ (2 (m & 3) + 8 ((m >> 3) & 1)).  Wave w fills rows 8w .. 8w+7 (4 DMA instructions of 2 rows).
 __device__ __forceinline__ int tn_swz(int m) { return 2 * (m & 3) + 8 * ((m >> 3) & 1); }
 
+template <int ROWS = VK>
 __device__ __forceinline__ void stage_tn(const bf16* __restrict__ G, int64_t ld, int m0, int m_end, int c0, char* img,
                                          int w, int lane) {
+  constexpr int IPW = ROWS / 16;  // DMA instructions (2 rows each) per wave
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = w * 4 + i;
+  for (int i = 0; i < IPW; ++i) {
+    const int q = w * IPW + i;
     const int m = 2 * q + (lane >> 5);
     const int gc = (lane & 31) ^ tn_swz(m);
     const bf16* src = m0 + m < m_end ? G + (int64_t)(m0 + m) * ld + c0 + gc * 8
@@ -161,11 +163,11 @@ struct Acc {
 };
 
 // one 64-deep step of a wave's MI x NJ block of 16 x 16 MFMA tiles at (rbase, cbase) of the tile
-template <bool TN, int MI, int NJ>
+template <bool TN, int NS = 2, int MI, int NJ>
 __device__ __forceinline__ void mma_step(const char* Ai, const char* Bi, int rbase, int cbase, int lane,
                                          Acc<MI, NJ>& acc) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < NS; ++s) {
     s16x8 af[MI], bfr[NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i) af[i] = TN ? frag_tn(Ai, rbase + 16 * i, s, lane) : frag_nt(Ai, rbase + 16 * i, s, lane);
@@ -368,7 +370,17 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
   }
 }
 
+// TK = 64: two 64-deep m-step images (128 KiB); TK = 32: four 32-deep ones (a DMA has three steps to
+// land; one 32-deep MFMA sub-step per barrier) -- DFD_TN_DEPTH, an A/B build switch
+#ifndef DFD_TN_DEPTH
+#define DFD_TN_DEPTH 64
+#endif
+template <int TK>
 __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
+  constexpr int NST = TK == 64 ? 2 : 4;
+  constexpr int OPI = TK * VT * 2;        // one operand's m-step image
+  constexpr int NPS = 2 * (TK / 16);      // DMA instructions per thread per m-step (both operands)
+  static_assert(NST * 2 * OPI <= VLDS, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[VLDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = uni(tid >> 6), wm = w >> 2, wn = w & 3;
@@ -383,12 +395,18 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc.v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = m_end > m_begin ? (m_end - m_begin + VK - 1) / VK : 0;
-  if (nk > 0) {
-    stage_tn(a.X1, a.ld1, m_begin, m_end, p0, smem, w, lane);
-    stage_tn(a.X2, a.ld2, m_begin, m_end, q0, smem + VTILE, w, lane);
-  }
-  __syncthreads();
+  const int nk = m_end > m_begin ? (m_end - m_begin + TK - 1) / TK : 0;
+  auto stage = [&](int kt, char* img) {
+    stage_tn<TK>(a.X1, a.ld1, m_begin + kt * TK, m_end, p0, img, w, lane);
+    stage_tn<TK>(a.X2, a.ld2, m_begin + kt * TK, m_end, q0, img + OPI, w, lane);
+  };
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nk) stage(p, smem + p * 2 * OPI);
+  // m-step 0 landed: the younger prologue steps' DMAs stay in flight
+  if (NST == 4 && nk > 2) vm_wait_n<2 * NPS>();
+  else if (NST == 4 && nk > 1) vm_wait_n<NPS>();
+  else vm_wait_n<0>();
+  lds_bar();
   // the bias gradient of the linear whose output gradient is X1: colsum[p] = sum_m X1[m][p] as a
   // product with a ones operand (exact products, fixed order) on the workgroups of tile column 0,
   // each wave taking 2 of its half's 8 row blocks (+2 MFMAs and 4 transposed reads per 32-deep
@@ -396,23 +414,27 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
   const bool csum = a.colsum && tq == 0;
   f32x4 cacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const s16x8 ones = {0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80, 0x3f80};  // bf16 1.0
+  int cb = 0, pb = NST - 1;  // buffers of m-steps kt and kt + NST - 1
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * 2 * VTILE;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * 2 * VTILE;
-      stage_tn(a.X1, a.ld1, m_begin + (kt + 1) * VK, m_end, p0, nxt, w, lane);
-      stage_tn(a.X2, a.ld2, m_begin + (kt + 1) * VK, m_end, q0, nxt + VTILE, w, lane);
-    }
-    mma_step<true>(cur, cur + VTILE, wm * 128, wn * 64, lane, acc);
+    char* cur = smem + cb * 2 * OPI;
+    if (kt + NST - 1 < nk) stage(kt + NST - 1, smem + pb * 2 * OPI);  // the buffer m-step kt - 1 read
+    mma_step<true, TK / 32>(cur, cur + OPI, wm * 128, wn * 64, lane, acc);
     if (csum) {
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
+      for (int s2 = 0; s2 < TK / 32; ++s2)
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
           cacc[ii] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag_tn(cur, wm * 128 + 16 * (2 * wn + ii), s2, lane), ones,
                                                              cacc[ii], 0, 0, 0);
     }
-    __syncthreads();
+    // m-step kt + 1 landed; the younger ones (at most NST - 2) may still be in flight
+    const int younger = min(kt + NST - 1, nk - 1) - (kt + 1);
+    if (NST == 4 && younger >= 2) vm_wait_n<2 * NPS>();
+    else if (NST == 4 && younger == 1) vm_wait_n<NPS>();
+    else vm_wait_n<0>();
+    lds_bar();
+    cb = cb == NST - 1 ? 0 : cb + 1;
+    pb = pb == NST - 1 ? 0 : pb + 1;
   }
   const int64_t srow = (int64_t)a.P * a.Q + (a.colsum ? a.P : 0);  // slab row length
   if (csum && (lane & 15) == 0) {
@@ -529,7 +551,7 @@ int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, 
   a.mchunk = (int)(cdiv64(cdiv64(M, splits), VK) * VK);
   splits = (int)cdiv64(M, a.mchunk);
   a.slab = slab;
-  hipLaunchKernelGGL(vgemm_tn_kernel, dim3(splits * a.tiles_p * a.tiles_q), dim3(512), 0, s, a);
+  hipLaunchKernelGGL(vgemm_tn_kernel<DFD_TN_DEPTH>, dim3(splits * a.tiles_p * a.tiles_q), dim3(512), 0, s, a);
   DFD_HIP_CHECK(hipGetLastError());
   if (!colsum_out) return launch_reduce_slabs(s, slab, splits, (int64_t)P * Q, W, accumulate);
   // a linear's bias gradient stored right after its weight gradient (named_parameters order): one
