@@ -34,29 +34,49 @@ __global__ __launch_bounds__(256) void rn_im2col_vec_kernel(const T* __restrict_
 }
 
 // conv1 rows: Kp = 152 columns = 147 taps (ky, kx, c) + 5 zeros
-template <typename T>
-__global__ __launch_bounds__(256) void rn_stem_im2col_kernel(const void* __restrict__ x, int64_t sn, int64_t sc,
-                                                             int64_t sh, int64_t sw, InputFmt in, int H, int W,
-                                                             int Ho, int Wo, int64_t rows, T* __restrict__ out) {
+// conv1's im2col rows, one thread per output pixel: the 147 (ky, kx, c) column decompositions are
+// compile-time constants, the pixel's index math is done once, uint8 values are normalised through a
+// 3 x 256 LDS table built with the same operations in the same order (bit-identical values), and the
+// row goes out as 19 16-byte stores (an element-per-thread form did two 64-bit divisions and two
+// fp32 divisions per element: 1.35 ms for 256 frames).
+template <typename T, bool U8>
+__global__ __launch_bounds__(256) void rn_stem_rows_kernel(const void* __restrict__ x, int64_t sn, int64_t sc,
+                                                           int64_t sh, int64_t sw, InputFmt in, int H, int W, int Ho,
+                                                           int Wo, int64_t rows, T* __restrict__ out) {
   constexpr int KS = 7, KP = 152;
-  const int64_t total = rows * KP;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int64_t m = i / KP;
-    const int col = (int)(i - m * KP);
-    float v = 0.f;
-    if (col < KS * KS * 3) {
-      const int tap = col / 3, c = col - tap * 3, ky = tap / KS, kx = tap - ky * KS;
-      const int64_t n = m / ((int64_t)Ho * Wo);
-      const int rem = (int)(m - n * Ho * Wo), oy = rem / Wo, ox = rem - oy * Wo;
-      const int iy = oy * 2 - 3 + ky, ix = ox * 2 - 3 + kx;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        const int64_t o = n * sn + c * sc + iy * sh + ix * sw;
-        // uint8: the reference's `.float() / 255.0` then (v - mean) / std, same operations in order
-        if (in.u8) v = ((float)static_cast<const uint8_t*>(x)[o] / 255.0f - in.mean[c]) / in.stdv[c];
-        else v = static_cast<const float*>(x)[o];
-      }
+  __shared__ float lut[U8 ? 3 * 256 : 1];
+  if constexpr (U8) {
+    for (int i = threadIdx.x; i < 3 * 256; i += 256) {
+      const int c = i >> 8;
+      lut[i] = ((float)(i & 255) / 255.0f - in.mean[c]) / in.stdv[c];
     }
-    out[i] = Tr<T>::from_f(v);
+    __syncthreads();
+  }
+  const int64_t hw = (int64_t)Ho * Wo;
+  for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < rows; m += (int64_t)gridDim.x * 256) {
+    const int64_t n = m / hw;
+    const int rem = (int)(m - n * hw), oy = rem / Wo, ox = rem - oy * Wo;
+    const int iy0 = oy * 2 - 3, ix0 = ox * 2 - 3;
+    T* orow = out + m * KP;
+#pragma unroll
+    for (int v = 0; v < KP / 8; ++v) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = 8 * v + j;
+        o[j] = 0.f;
+        if (col < KS * KS * 3) {
+          const int tap = col / 3, c = col % 3, ky = tap / KS, kx = tap % KS;
+          const int iy = iy0 + ky, ix = ix0 + kx;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+            const int64_t e = n * sn + c * sc + iy * sh + ix * sw;
+            if constexpr (U8) o[j] = lut[c * 256 + static_cast<const uint8_t*>(x)[e]];
+            else o[j] = static_cast<const float*>(x)[e];
+          }
+        }
+      }
+      st8(orow + 8 * v, o);
+    }
   }
 }
 
@@ -119,8 +139,12 @@ int launch_rn_stem_im2col(hipStream_t s, const void* x, const InputFmt& in, cons
                           int W, T* out) {
   const int Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
   const int64_t rows = (int64_t)N * Ho * Wo;
-  hipLaunchKernelGGL(rn_stem_im2col_kernel<T>, dim3(ew_grid(rows * 152)), dim3(256), 0, s, x, strides[0], strides[1],
-                     strides[2], strides[3], in, H, W, Ho, Wo, rows, out);
+  if (in.u8)
+    hipLaunchKernelGGL((rn_stem_rows_kernel<T, true>), dim3(ew_grid(rows)), dim3(256), 0, s, x, strides[0], strides[1],
+                       strides[2], strides[3], in, H, W, Ho, Wo, rows, out);
+  else
+    hipLaunchKernelGGL((rn_stem_rows_kernel<T, false>), dim3(ew_grid(rows)), dim3(256), 0, s, x, strides[0],
+                       strides[1], strides[2], strides[3], in, H, W, Ho, Wo, rows, out);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
