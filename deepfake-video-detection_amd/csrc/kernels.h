@@ -232,6 +232,17 @@ bool dw_fwd1_enabled();
 // finalize training stats: mean/invstd/scale/shift + running update (momentum); eval: from running
 // chan_rows > 0: stats rows are centred (sum, M2) partials of consecutive chan_rows-row tiles
 // (conv_forward's epilogue: kConvStatRows), merged in fp64 (Chan); 0: plain (sum, sum of squares)
+// all of a plan's eval-mode BatchNorms in one launch (float offsets into params P, BN buffers bnb and
+// the fp32 view of the workspace)
+constexpr int kEvalBnMax = 64;
+struct EvalBnEntry {
+  int C, w, b, rm, rv, mean, invstd, scale, shift;
+};
+struct EvalBnTable {
+  int n;
+  EvalBnEntry e[kEvalBnMax];
+};
+int launch_bn_eval_all(hipStream_t s, const float* P, const float* bnb, float* wsf, const EvalBnTable& t, float eps);
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps,
                        bool training, float* mean, float* invstd, float* scale, float* shift, int chan_rows = 0);

@@ -372,7 +372,34 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   const float eps = 1e-5f;
   float* stats = tr ? r.f(p.o_stats) : nullptr;
   int rows = 0;
+  // eval mode: every BN's scale / shift from its running statistics in one launch up front (the
+  // per-layer finalize launches below are skipped), when the offsets fit the table's 32-bit fields
+  bool eval_all = false;
+  if (!tr) {
+    EvalBnTable t{};
+    bool ok = true;
+    auto add = [&](const BNL& b) {
+      const int64_t v[8] = {p.offs[b.t_w], p.offs[b.t_b], p.offs[b.t_rm], p.offs[b.t_rv],
+                            b.o_mean / 4, b.o_invstd / 4, b.o_scale / 4, b.o_shift / 4};
+      for (int64_t x : v) ok = ok && x >= 0 && x < INT32_MAX;
+      ok = ok && t.n < kEvalBnMax && (b.o_mean | b.o_invstd | b.o_scale | b.o_shift) % 4 == 0;
+      if (!ok) return;
+      t.e[t.n++] = EvalBnEntry{b.C, (int)v[0], (int)v[1], (int)v[2], (int)v[3], (int)v[4], (int)v[5], (int)v[6], (int)v[7]};
+    };
+    add(p.bn_stem);
+    for (const Block& b : p.blocks) {
+      if (!b.ds) add(b.bn1);
+      add(b.ds ? b.bn1 : b.bn2);
+      add(b.bn3);
+    }
+    add(p.bn_head);
+    if (ok) {
+      DFD_TRY(launch_bn_eval_all(s, P, bnb, reinterpret_cast<float*>(ws), t, eps));
+      eval_all = true;
+    }
+  }
   auto fin = [&](const BNL& b, int64_t count) {
+    if (eval_all) return 0;
     return launch_bn_finalize(s, r.f(p.o_stats), rows, count, b.C, r.prm(b.t_w), r.prm(b.t_b), bnb + p.offs[b.t_rm],
                               bnb + p.offs[b.t_rv], mom, eps, tr != 0, r.f(b.o_mean), r.f(b.o_invstd), r.f(b.o_scale),
                               r.f(b.o_shift));
