@@ -33,49 +33,71 @@ __global__ __launch_bounds__(256) void rn_im2col_vec_kernel(const T* __restrict_
   }
 }
 
-// conv1 rows: Kp = 152 columns = 147 taps (ky, kx, c) + 5 zeros
-// conv1's im2col rows, one thread per output pixel: the 147 (ky, kx, c) column decompositions are
-// compile-time constants, the pixel's index math is done once, uint8 values are normalised through a
-// 3 x 256 LDS table built with the same operations in the same order (bit-identical values), and the
-// row goes out as 19 16-byte stores (an element-per-thread form did two 64-bit divisions and two
-// fp32 divisions per element: 1.35 ms for 256 frames).
+// conv1 rows: Kp = 152 columns = 147 taps (ky, kx, c) + 5 zeros.  One thread per output pixel: the
+// 147 (ky, kx, c) column decompositions are compile-time constants, the pixel's index math is done
+// once, uint8 values are normalised through a 3 x 256 LDS table built with the same operations in
+// the same order (bit-identical values).  bf16 rows (304 B) are staged per wave in LDS and leave as
+// contiguous 1-KB wave stores (a thread's own row as 19 16-B stores 304 B apart measured 871 us for
+// 256 frames; an element per thread with two 64-bit and two fp32 divisions each, 1.35 ms).
 template <typename T, bool U8>
-__global__ __launch_bounds__(256) void rn_stem_rows_kernel(const void* __restrict__ x, int64_t sn, int64_t sc,
+__global__ __launch_bounds__(128) void rn_stem_rows_kernel(const void* __restrict__ x, int64_t sn, int64_t sc,
                                                            int64_t sh, int64_t sw, InputFmt in, int H, int W, int Ho,
                                                            int Wo, int64_t rows, T* __restrict__ out) {
-  constexpr int KS = 7, KP = 152;
+  constexpr int KS = 7, KP = 152, NV = KP / 8;
+  constexpr bool STG = sizeof(T) == 2;  // 16-B chunks of 8 bf16
   __shared__ float lut[U8 ? 3 * 256 : 1];
+  __shared__ uint4 stg[STG ? 2 * 64 * NV : 1];
   if constexpr (U8) {
-    for (int i = threadIdx.x; i < 3 * 256; i += 256) {
+    for (int i = threadIdx.x; i < 3 * 256; i += 128) {
       const int c = i >> 8;
       lut[i] = ((float)(i & 255) / 255.0f - in.mean[c]) / in.stdv[c];
     }
     __syncthreads();
   }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t hw = (int64_t)Ho * Wo;
-  for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < rows; m += (int64_t)gridDim.x * 256) {
-    const int64_t n = m / hw;
-    const int rem = (int)(m - n * hw), oy = rem / Wo, ox = rem - oy * Wo;
-    const int iy0 = oy * 2 - 3, ix0 = ox * 2 - 3;
-    T* orow = out + m * KP;
+  for (int64_t m0 = ((int64_t)blockIdx.x * 2 + wave) * 64, step = (int64_t)gridDim.x * 128; m0 - wave * 64 < rows;
+       m0 += step) {
+    const int64_t m = m0 + lane;
+    if (m < rows) {
+      const int64_t n = m / hw;
+      const int rem = (int)(m - n * hw), oy = rem / Wo, ox = rem - oy * Wo;
+      const int iy0 = oy * 2 - 3, ix0 = ox * 2 - 3;
 #pragma unroll
-    for (int v = 0; v < KP / 8; ++v) {
-      float o[8];
+      for (int v = 0; v < NV; ++v) {
+        float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = 8 * v + j;
-        o[j] = 0.f;
-        if (col < KS * KS * 3) {
-          const int tap = col / 3, c = col % 3, ky = tap / KS, kx = tap % KS;
-          const int iy = iy0 + ky, ix = ix0 + kx;
-          if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-            const int64_t e = n * sn + c * sc + iy * sh + ix * sw;
-            if constexpr (U8) o[j] = lut[c * 256 + static_cast<const uint8_t*>(x)[e]];
-            else o[j] = static_cast<const float*>(x)[e];
+        for (int j = 0; j < 8; ++j) {
+          const int col = 8 * v + j;
+          o[j] = 0.f;
+          if (col < KS * KS * 3) {
+            const int tap = col / 3, c = col % 3, ky = tap / KS, kx = tap % KS;
+            const int iy = iy0 + ky, ix = ix0 + kx;
+            if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+              const int64_t e = n * sn + c * sc + iy * sh + ix * sw;
+              if constexpr (U8) o[j] = lut[c * 256 + static_cast<const uint8_t*>(x)[e]];
+              else o[j] = static_cast<const float*>(x)[e];
+            }
           }
         }
+        if constexpr (STG) {
+          stg[(wave * 64 + lane) * NV + v] =
+              make_uint4(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]), pack2bf(o[4], o[5]), pack2bf(o[6], o[7]));
+        } else {
+          st8(out + m * KP + 8 * v, o);
+        }
       }
-      st8(orow + 8 * v, o);
+    }
+    if constexpr (STG) {
+      __syncthreads();
+      // the wave's 64 rows are 64 x 19 contiguous 16-B chunks of the output
+      uint4* dst = reinterpret_cast<uint4*>(out + m0 * KP);
+#pragma unroll
+      for (int it = 0; it < NV; ++it) {
+        const int q = it * 64 + lane;
+        if (m0 + q / NV < rows) dst[q] = stg[wave * 64 * NV + q];
+      }
+      __syncthreads();
     }
   }
 }
@@ -139,11 +161,12 @@ int launch_rn_stem_im2col(hipStream_t s, const void* x, const InputFmt& in, cons
                           int W, T* out) {
   const int Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
   const int64_t rows = (int64_t)N * Ho * Wo;
+  const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(rows, 128), 8192));
   if (in.u8)
-    hipLaunchKernelGGL((rn_stem_rows_kernel<T, true>), dim3(ew_grid(rows)), dim3(256), 0, s, x, strides[0], strides[1],
+    hipLaunchKernelGGL((rn_stem_rows_kernel<T, true>), dim3(gx), dim3(128), 0, s, x, strides[0], strides[1],
                        strides[2], strides[3], in, H, W, Ho, Wo, rows, out);
   else
-    hipLaunchKernelGGL((rn_stem_rows_kernel<T, false>), dim3(ew_grid(rows)), dim3(256), 0, s, x, strides[0],
+    hipLaunchKernelGGL((rn_stem_rows_kernel<T, false>), dim3(gx), dim3(128), 0, s, x, strides[0],
                        strides[1], strides[2], strides[3], in, H, W, Ho, Wo, rows, out);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
