@@ -66,6 +66,7 @@ _SIGS = {
     "dfd_rn_im2col": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p]),
     "dfd_rn_stem_im2col": (c_i, [c_p, c_i, c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_f), c_i, c_i, c_i, c_p]),
     "dfd_rn_gemm": (c_i, [c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_i, c_i64, c_i, c_i]),
+    "dfd_rn_stem_conv": (c_i, [c_p, c_i, c_p, c_i, ctypes.POINTER(c_i64), c_p, c_i, c_i, c_i, c_p, c_p, c_p]),
     "dfd_rn_conv": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_i, c_i, c_p]),
     "dfd_rn_maxpool": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_p]),
     "dfd_rn_avgpool": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_p]),

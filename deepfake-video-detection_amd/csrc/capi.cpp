@@ -358,6 +358,22 @@ int dfd_rn_im2col(void* stream, int dtype, const void* x, int N, int H, int W, i
   DFD_GUARD_END
 }
 
+int dfd_rn_stem_conv(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
+                     const float* norm6, int N, int H, int W, const void* w, const float* bias, void* out) {
+  DFD_GUARD_BEGIN
+  if (!x || !out || !strides4 || !w || !bias) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  if (dtype != 1) { dfd::set_error("rn stem conv: bf16 only (fp32: dfd_rn_stem_im2col + dfd_rn_gemm)", __FILE__, __LINE__); return -1; }
+  dfd::InputFmt in{};
+  in.u8 = input_fmt == DFD_INPUT_U8 ? 1 : 0;
+  for (int c = 0; c < 3; ++c) {
+    in.mean[c] = norm6 ? norm6[c] : 0.f;
+    in.stdv[c] = norm6 ? norm6[3 + c] : 1.f;
+  }
+  return dfd::launch_rn_stem_conv((hipStream_t)stream, x, in, strides4, N, H, W, (const dfd::bf16*)w, bias,
+                                  (dfd::bf16*)out);
+  DFD_GUARD_END
+}
+
 int dfd_rn_stem_im2col(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
                        const float* norm6, int N, int H, int W, void* out) {
   DFD_GUARD_BEGIN

@@ -102,6 +102,143 @@ __global__ __launch_bounds__(128) void rn_stem_rows_kernel(const void* __restric
   }
 }
 
+// conv1 (7x7/2 pad 3, 3 -> 64, folded BN + ReLU) as an implicit GEMM, bf16: no im2col rows in HBM.
+// Per 16 x 16 output tile: the 37 x 37 x 3 input window normalised into LDS (uint8 through the
+// 3 x 256 table, the same operations as the im2col rows), then 5 k-steps of 32 taps (147 + zeros):
+// each thread writes its pixel's 32 taps of the step (compile-time tap decomposition) into a
+// wave-local im2col slice, and each wave runs D[co][pix] += W[co][k] . patch[pix][k] on
+// v_mfma_f32_16x16x32_bf16 for its 64 pixels x 64 channels; bias + ReLU, one rounding, 16-B row
+// stores through an LDS slab.  Replaces 976 MB of im2col writes + reads per 256 frames.
+constexpr int RST = 16, RIE = (RST - 1) * 2 + 7, RNIN = RIE * RIE * 3;  // 37 x 37 x 3 window
+constexpr int RKS = 160, RXS = 40, RCS = 72;  // padded K; im2col / output slab row strides (bf16)
+constexpr int RTINB = (RNIN * 4 + 15) / 16 * 16, RXSB = 256 * RXS * 2, RCSB = 256 * RCS * 2;
+constexpr int RUNI = RTINB + RXSB > RCSB ? RTINB + RXSB : RCSB;  // tin + im2col, later the output slab
+typedef short rs_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool U8>
+__global__ __launch_bounds__(256, 2) void rn_stem_conv_kernel(const void* __restrict__ x, int64_t sn, int64_t sc,
+                                                              int64_t sh, int64_t sw, InputFmt in, int H, int W, int Ho,
+                                                              int Wo, const bf16* __restrict__ Wt,
+                                                              const float* __restrict__ bias, bf16* __restrict__ out,
+                                                              int64_t ntiles) {
+  __shared__ __attribute__((aligned(16))) char uni[RUNI];
+  __shared__ float lut[U8 ? 3 * 256 : 1];
+  __shared__ __attribute__((aligned(16))) bf16 wsb[64 * RKS];
+  float* tin = reinterpret_cast<float*>(uni);
+  bf16* xs = reinterpret_cast<bf16*>(uni + RTINB);
+  bf16* ct = reinterpret_cast<bf16*>(uni);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if constexpr (U8) {
+    for (int i = tid; i < 3 * 256; i += 256) {
+      const int c = i >> 8;
+      lut[i] = ((float)(i & 255) / 255.0f - in.mean[c]) / in.stdv[c];
+    }
+  }
+  for (int i = tid; i < 64 * RKS; i += 256) {  // W [64][152] -> [64][160], zero pad
+    const int co = i / RKS, k = i - co * RKS;
+    wsb[i] = k < 152 ? Wt[co * 152 + k] : bf16{0};
+  }
+  const int tpf = (Ho / RST) * (Wo / RST), tx = Wo / RST;
+  float bsv[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bsv[a][r] = bias[16 * a + 4 * (lane >> 4) + r];
+  const int ly = tid / RST, lx = tid % RST;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t n = t / tpf;
+    const int r = (int)(t - n * tpf), oy0 = (r / tx) * RST, ox0 = (r % tx) * RST;
+    const int iy0 = oy0 * 2 - 3, ix0 = ox0 * 2 - 3;
+    __syncthreads();  // the previous tile's output slab (aliases tin / xs) has been stored
+    for (int e = tid; e < RNIN; e += 256) {
+      const int pix = e / 3, c = e - pix * 3, ry = pix / RIE, rx = pix - ry * RIE;
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      float v = 0.f;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const int64_t o = n * sn + c * sc + iy * sh + ix * sw;
+        if constexpr (U8) v = lut[c * 256 + static_cast<const uint8_t*>(x)[o]];
+        else v = static_cast<const float*>(x)[o];
+      }
+      tin[e] = v;  // zero padding after normalisation, as conv2d pads
+    }
+    __syncthreads();
+    rs_f32x4 acc[4][4];
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) acc[pb][a] = rs_f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* tp = tin + (ly * 2 * RIE + lx * 2) * 3;  // this thread's pixel window origin
+#pragma unroll
+    for (int s = 0; s < RKS / 32; ++s) {
+      // this pixel's 32 taps of k-step s into its im2col row (rows of this wave only: wave-local)
+#pragma unroll
+      for (int c8 = 0; c8 < 4; ++c8) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = 32 * s + 8 * c8 + j;
+          if (k < 147) {
+            const int tap = k / 3, c = k % 3, ky = tap / 7, kx = tap % 7;
+            v[j] = tp[(ky * RIE + kx) * 3 + c];
+          } else {
+            v[j] = 0.f;
+          }
+        }
+        st8(xs + tid * RXS + 8 * c8, v);
+      }
+      rs_bf16x8 wf[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        wf[a] = *reinterpret_cast<const rs_bf16x8*>(wsb + (16 * a + (lane & 15)) * RKS + 32 * s + 8 * (lane >> 4));
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const int p0 = wave * 64 + 16 * pb;
+        const rs_bf16x8 pf = *reinterpret_cast<const rs_bf16x8*>(xs + (p0 + (lane & 15)) * RXS + 8 * (lane >> 4));
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[pb][a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], pf, acc[pb][a], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave is done with tin (the slab overwrites it)
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) {
+      const int pix = wave * 64 + 16 * pb + (lane & 15);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = fmaxf(Tr<bf16>::round(acc[pb][a][q] + bsv[a][q]), 0.f);
+        *reinterpret_cast<uint2*>(ct + pix * RCS + 16 * a + 4 * (lane >> 4)) =
+            make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // 256 pixels x 8 vectors of 8 channels
+      const int e = tid + 256 * i, pix = e >> 3, v = e & 7;
+      const int oy = oy0 + pix / RST, ox = ox0 + pix % RST;
+      *reinterpret_cast<uint4*>(out + (((int64_t)n * Ho + oy) * Wo + ox) * 64 + 8 * v) =
+          *reinterpret_cast<const uint4*>(ct + pix * RCS + 8 * v);
+    }
+  }
+}
+
+int launch_rn_stem_conv(hipStream_t s, const void* x, const InputFmt& in, const int64_t* strides, int N, int H, int W,
+                        const bf16* Wt, const float* bias, bf16* out) {
+  const int Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+  if (Ho % RST || Wo % RST) { set_error("resnet stem conv: output map not a multiple of 16", __FILE__, __LINE__); return -1; }
+  const int64_t ntiles = (int64_t)N * (Ho / RST) * (Wo / RST);
+  const int gx = (int)std::min<int64_t>(ntiles, 1024);
+  if (in.u8)
+    hipLaunchKernelGGL(rn_stem_conv_kernel<true>, dim3(gx), dim3(256), 0, s, x, strides[0], strides[1], strides[2],
+                       strides[3], in, H, W, Ho, Wo, Wt, bias, out, ntiles);
+  else
+    hipLaunchKernelGGL(rn_stem_conv_kernel<false>, dim3(gx), dim3(256), 0, s, x, strides[0], strides[1], strides[2],
+                       strides[3], in, H, W, Ho, Wo, Wt, bias, out, ntiles);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void rn_maxpool_kernel(const T* __restrict__ x, int N, int H, int W, int C, int Ho,
                                                          int Wo, T* __restrict__ out) {

@@ -83,6 +83,9 @@ int launch_rn_im2col(hipStream_t s, const T* x, int N, int H, int W, int C, int 
 template <typename T>
 int launch_rn_stem_im2col(hipStream_t s, const void* x, const InputFmt& in, const int64_t* strides, int N, int H,
                           int W, T* out);
+// conv1 7x7/2 + folded BN + ReLU as an implicit GEMM (bf16; Ho, Wo multiples of 16): Wt [64][152]
+int launch_rn_stem_conv(hipStream_t s, const void* x, const InputFmt& in, const int64_t* strides, int N, int H, int W,
+                        const bf16* Wt, const float* bias, bf16* out);
 template <typename T>
 int launch_rn_maxpool(hipStream_t s, const T* x, int N, int H, int W, int C, T* out);
 template <typename T>

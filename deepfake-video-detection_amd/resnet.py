@@ -443,11 +443,17 @@ def _forward(f, x, dt, norm):
     # conv1 7x7/2 + bn1 + relu (frames gathered straight from the caller's tensor)
     stem = f["stem"]
     ho, wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-    a = torch.empty(N * ho * wo, STEM_KP, dtype=tdt, device=dev)
     fmt = 1 if x.dtype == torch.uint8 else 0
-    _lib.check(lib.dfd_rn_stem_im2col(st, dt, x.data_ptr(), fmt, (ctypes.c_int64 * 4)(*x.stride()), _norm6(norm), N,
-                                      H, W, a.data_ptr()))
-    h = gemm(a, stem, N * ho * wo)
+    if dt == 1 and ho % 16 == 0 and wo % 16 == 0:
+        # bf16: one implicit-GEMM launch (k_resnet.hip rn_stem_conv_kernel), no im2col rows in HBM
+        h = torch.empty(N * ho * wo, stem.cout, dtype=tdt, device=dev)
+        _lib.check(lib.dfd_rn_stem_conv(st, dt, x.data_ptr(), fmt, (ctypes.c_int64 * 4)(*x.stride()), _norm6(norm),
+                                        N, H, W, stem.w.data_ptr(), stem.b.data_ptr(), h.data_ptr()))
+    else:
+        a = torch.empty(N * ho * wo, STEM_KP, dtype=tdt, device=dev)
+        _lib.check(lib.dfd_rn_stem_im2col(st, dt, x.data_ptr(), fmt, (ctypes.c_int64 * 4)(*x.stride()), _norm6(norm),
+                                          N, H, W, a.data_ptr()))
+        h = gemm(a, stem, N * ho * wo)
     # maxpool 3x3/2
     hp, wp = (ho + 2 - 3) // 2 + 1, (wo + 2 - 3) // 2 + 1
     p = torch.empty(N * hp * wp, 64, dtype=tdt, device=dev)

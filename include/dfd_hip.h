@@ -165,6 +165,11 @@ DFD_API int dfd_rn_im2col(void* stream, int dtype, const void* x, int N, int H, 
  * norm6 = mean[3], std[3]) -> [N*Ho*Wo][152] (147 taps + zero padding) */
 DFD_API int dfd_rn_stem_im2col(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
                                const float* norm6, int N, int H, int W, void* out);
+/* conv1 + its folded BN + ReLU in one implicit-GEMM launch (bf16 only; the output map's sides multiples
+ * of 16): the frames as for dfd_rn_stem_im2col, w [64][152] bf16 (the im2col column order), bias[64]
+ * fp32, out NHWC (N, Ho, Wo, 64) bf16 -- the rows of dfd_rn_stem_im2col never reach HBM. */
+DFD_API int dfd_rn_stem_conv(void* stream, int dtype, const void* x, int input_fmt, const int64_t* strides4,
+                             const float* norm6, int N, int H, int W, const void* w, const float* bias, void* out);
 /* C[M][N] = relu?(A[M][K] . B[N][K]^T + bias[N] (+ R[M][N])), fp32 accumulate (the MFMA kernel of
  * dfd_rn_conv on an explicit A; K % 8 == 0) */
 DFD_API int dfd_rn_gemm(void* stream, int dtype, const void* A, const void* B, void* C, const void* R,
