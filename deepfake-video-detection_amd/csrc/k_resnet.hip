@@ -114,6 +114,9 @@ constexpr int RKS = 160, RXS = 40, RCS = 72;  // padded K; im2col / output slab 
 constexpr int RTINB = (RNIN * 4 + 15) / 16 * 16, RXSB = 256 * RXS * 2, RCSB = 256 * RCS * 2;
 constexpr int RUNI = RTINB + RXSB > RCSB ? RTINB + RXSB : RCSB;  // tin + im2col, later the output slab
 typedef short rs_bf16x8 __attribute__((ext_vector_type(8)));
+#ifndef DFD_RSTEM_PF  // 1: the next tile's window loads fly during this tile's MFMAs (A/B build switch)
+#define DFD_RSTEM_PF 1
+#endif
 typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
 
 template <bool U8>
@@ -146,23 +149,48 @@ __global__ __launch_bounds__(256, 2) void rn_stem_conv_kernel(const void* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) bsv[a][r] = bias[16 * a + 4 * (lane >> 4) + r];
   const int ly = tid / RST, lx = tid % RST;
+  // the next tile's window in registers while this tile computes: raw bytes (U8) or fp32 bits, and
+  // 0xffffffff for positions outside the map
+  constexpr int NLD = (RNIN + 255) / 256;
+  uint32_t raw[NLD];
+  auto load = [&](int64_t t) {
+    const int64_t n = t / tpf;
+    const int r = (int)(t - n * tpf), iy0 = (r / tx) * RST * 2 - 3, ix0 = (r % tx) * RST * 2 - 3;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int e = tid + 256 * i;
+      const int pix = e / 3, c = e - pix * 3, ry = pix / RIE, rx = pix - ry * RIE;
+      const int iy = iy0 + ry, ix = ix0 + rx;
+      uint32_t v = 0xffffffffu;
+      if (e < RNIN && iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const int64_t o = n * sn + c * sc + iy * sh + ix * sw;
+        if constexpr (U8) v = static_cast<const uint8_t*>(x)[o];
+        else v = __float_as_uint(static_cast<const float*>(x)[o]);
+      }
+      raw[i] = v;
+    }
+  };
+  if (DFD_RSTEM_PF && blockIdx.x < ntiles) load(blockIdx.x);
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t n = t / tpf;
     const int r = (int)(t - n * tpf), oy0 = (r / tx) * RST, ox0 = (r % tx) * RST;
-    const int iy0 = oy0 * 2 - 3, ix0 = ox0 * 2 - 3;
+    if (!DFD_RSTEM_PF) load(t);
     __syncthreads();  // the previous tile's output slab (aliases tin / xs) has been stored
-    for (int e = tid; e < RNIN; e += 256) {
-      const int pix = e / 3, c = e - pix * 3, ry = pix / RIE, rx = pix - ry * RIE;
-      const int iy = iy0 + ry, ix = ix0 + rx;
-      float v = 0.f;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        const int64_t o = n * sn + c * sc + iy * sh + ix * sw;
-        if constexpr (U8) v = lut[c * 256 + static_cast<const uint8_t*>(x)[o]];
-        else v = static_cast<const float*>(x)[o];
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int e = tid + 256 * i;
+      if (e < RNIN) {
+        const int c = e % 3;
+        float v = 0.f;  // zero padding after normalisation, as conv2d pads
+        if (raw[i] != 0xffffffffu) {
+          if constexpr (U8) v = lut[c * 256 + raw[i]];
+          else v = __uint_as_float(raw[i]);
+        }
+        tin[e] = v;
       }
-      tin[e] = v;  // zero padding after normalisation, as conv2d pads
     }
     __syncthreads();
+    if (DFD_RSTEM_PF && t + gridDim.x < ntiles) load(t + gridDim.x);
     rs_f32x4 acc[4][4];
 #pragma unroll
     for (int pb = 0; pb < 4; ++pb)
