@@ -223,6 +223,11 @@ static int rn_go(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, const
   return 0;
 }
 
+// 1: the Cout = 64 convolutions (layer1) on the NT GEMM's 64-wide tile too (A/B build switch)
+#ifndef DFD_VG64
+#define DFD_VG64 1
+#endif
+
 template <typename T>
 int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, const float* bias, int relu,
                    const RnConvGeom& g, int64_t M, int N, int K) {
@@ -241,7 +246,7 @@ int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, con
     if constexpr (sizeof(T) == 2) {
       // bf16 3x3 and strided convolutions with Cin % 64 == 0 and Cout % 128 == 0: the same LDS-DMA NT
       // kernel, its A tile gathered per tap from the NHWC input (implicit GEMM, K order tap-major as here)
-      if (vgemm_conv_covers(g.Cin, N, g.KH, g.KW) && vgemm_nt_covers(M, N, K)) {
+      if (vgemm_conv_covers(g.Cin, N, g.KH, g.KW) && vgemm_nt_covers(M, N, K) && (DFD_VG64 || N % 128 == 0)) {
         VgemmArgs a{};
         a.A = X; a.B = Wt; a.C = C; a.R = R; a.bias = bias;
         a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
@@ -257,7 +262,7 @@ int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, con
     // bf16 1x1 stride-1 convolutions are plain NT GEMMs: the LDS-DMA 256-row-tile kernel of the ViT
     // (k_vgemm.hip) where it covers the shape (Cout % 128, Cin % 64), with the same epilogue order
     // (bias, identity, ReLU in fp32, one rounding)
-    if (vgemm_nt_covers(M, N, K)) {
+    if (vgemm_nt_covers(M, N, K) && (DFD_VG64 || N % 128 == 0)) {
       VgemmArgs a{};
       a.A = X; a.B = Wt; a.C = C; a.R = R; a.bias = bias;
       a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;

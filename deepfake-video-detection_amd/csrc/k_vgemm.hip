@@ -222,11 +222,12 @@ __device__ __forceinline__ void epi_put(float* E, const Acc<MI, NJ>& acc, int r0
 __device__ __forceinline__ void st8bf(bf16* p, const float (&v)[8]) { st8(p, v); }
 
 // ---------------------------------------------------------------- kernels
+// BNT = 64 (ResNet-50 layer1, Cout 64): 8 (M) x 1 (N) waves of 32 x 64.
 // BNT = 256: 8 waves as 2 (M) x 4 (N), 128 x 64 each; BNT = 128 (N = 768-wide products: 2.3 instead of
 // 1.2 dispatch waves of tiles, so the last wave idles less): 4 (M) x 2 (N) waves of 64 x 64
 template <int EP, int BNT, bool CONV = false, bool XP = false>
 __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
-  constexpr int WMN = BNT == VT ? 2 : 4, WNN = 8 / WMN;  // waves along M / N
+  constexpr int WMN = BNT == VT ? 2 : BNT == 128 ? 4 : 8, WNN = 8 / WMN;  // waves along M / N
   constexpr int MI = VT / WMN / 16, NJ = BNT / WNN / 16;
   constexpr int BIMG = BNT * VK * 2;                    // B operand's K-step image
   constexpr int STAGE = VTILE + BIMG;
@@ -466,12 +467,12 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
 }  // namespace
 
 bool vgemm_nt_covers(int64_t M, int N, int K) {
-  return M > 0 && M < (1ll << 31) && N % 128 == 0 && K % VK == 0 && K > 0;
+  return M > 0 && M < (1ll << 31) && N % 64 == 0 && K % VK == 0 && K > 0;
 }
 // implicit convolution: a 64-deep K-step is 64 channels of one tap (Cin a power of two >= 64), the
 // output width a multiple of the 128-wide tile, KW in {1, 3} (KH <= 3)
 bool vgemm_conv_covers(int Cin, int Cout, int KH, int KW) {
-  return Cin >= 64 && (Cin & (Cin - 1)) == 0 && Cout % 128 == 0 && (KW == 1 || KW == 3) && KH <= 3 && KH >= 1;
+  return Cin >= 64 && (Cin & (Cin - 1)) == 0 && Cout % 64 == 0 && (KW == 1 || KW == 3) && KH <= 3 && KH >= 1;
 }
 bool vgemm_tn_covers(int64_t M, int P, int Q) { return M > 0 && M < (1ll << 31) && P % VT == 0 && Q % VT == 0; }
 
@@ -479,6 +480,7 @@ bool vgemm_tn_covers(int64_t M, int P, int Q) { return M > 0 && M < (1ll << 31) 
 // or fewer than ~2 waves of 256 x 256 tiles (ViT-B's 768-wide products at M = 25,216: 297 tiles on
 // 256 CUs)
 static int vgemm_nt_bn(int64_t M, int N) {
+  if (N % 128) return 64;
   if (N % VT) return 128;
   const int64_t t256 = cdiv64(M, VT) * (N / VT);
   return t256 < 2 * 256 ? 128 : VT;
@@ -488,13 +490,26 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   if (!vgemm_nt_covers(a0.M, a0.N, a0.K)) { set_error("vgemm: shape not covered", __FILE__, __LINE__); return -1; }
   VgemmArgs a = a0;
   const int bn = a0.bn ? a0.bn : vgemm_nt_bn(a.M, a.N);
-  if (bn != 128 && (bn != VT || a.N % VT)) { set_error("vgemm: tile width", __FILE__, __LINE__); return -1; }
+  if (a.N % bn || (bn != 64 && bn != 128 && bn != VT)) { set_error("vgemm: tile width", __FILE__, __LINE__); return -1; }
   a.tiles_n = a.N / bn;
   const int tiles = cdiv(a.M, VT) * a.tiles_n;
   if (a.conv) {  // implicit convolutions (the ResNet-50 eval 3x3 / strided layers): bias, identity, ReLU
     if (!vgemm_conv_covers(1 << a.cin_log2, a.N, 3, a.KW) || a.K % (1 << a.cin_log2)) {
       set_error("vgemm: convolution shape not covered", __FILE__, __LINE__);
       return -1;
+    }
+    if (bn == 64) {  // Cout 64 (layer1): the plain K loop
+      switch (ep) {
+        case VG_BIAS: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS, 64, true>), dim3(tiles), dim3(512), 0, s, a); break;
+        case VG_BIAS | VG_RELU:
+          hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RELU, 64, true>), dim3(tiles), dim3(512), 0, s, a); break;
+        case VG_BIAS | VG_RESID | VG_RELU:
+          hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RESID | VG_RELU, 64, true>), dim3(tiles), dim3(512), 0, s, a);
+          break;
+        default: set_error("vgemm: convolution epilogue not instantiated", __FILE__, __LINE__); return -1;
+      }
+      DFD_HIP_CHECK(hipGetLastError());
+      return 0;
     }
     const bool xpc = (tune(TK_VG_XP) & (bn == 128 ? 1 : 2)) != 0;
     switch ((ep * 2 + (bn == 128)) * 2 + xpc) {
@@ -512,6 +527,18 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   }
   // knob vg_xp: the fragment-pipelined K loop (XP); bit 0 for the 128-wide tile, bit 1 for the 256-wide
   // (the weight-gradient kernel's form of it needs 2 x 24 fragment registers and spills: not built)
+  if (bn == 64) {  // 64-wide outputs (ResNet-50 layer1): bias / identity / ReLU epilogues, plain K loop
+    switch (ep) {
+      case VG_BIAS: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS, 64>), dim3(tiles), dim3(512), 0, s, a); break;
+      case VG_BIAS | VG_RESID: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RESID, 64>), dim3(tiles), dim3(512), 0, s, a); break;
+      case VG_BIAS | VG_RELU: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RELU, 64>), dim3(tiles), dim3(512), 0, s, a); break;
+      case VG_BIAS | VG_RESID | VG_RELU:
+        hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RESID | VG_RELU, 64>), dim3(tiles), dim3(512), 0, s, a); break;
+      default: set_error("vgemm: 64-wide epilogue not instantiated", __FILE__, __LINE__); return -1;
+    }
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   const int64_t xpk = tune(TK_VG_XP);
   const bool xp = (xpk & (bn == 128 ? 1 : 2)) != 0;
   switch ((ep * 2 + (bn == 128)) * 2 + xp) {

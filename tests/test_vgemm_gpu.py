@@ -119,7 +119,7 @@ def test_vgemm_refuses_uncovered(cuda):
     C = torch.zeros(64, 200, device=cuda).bfloat16()
     lib = _lib.load()
     assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 100, 0, None, 0) != 0  # K % 64
-    assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 128, 0, None, 0) != 0  # N % 128
+    assert lib.dfd_vgemm(None, 0, P(A), P(B), P(C), None, None, None, None, 64, 200, 128, 0, None, 0) != 0  # N % 64
 
 
 def test_vgemm_nt_tile_widths_agree(cuda):
@@ -152,3 +152,24 @@ def test_vgemm_nt_xp_bit_identical(cuda, M, N, K, epi):
     for (c3, g3), (c0, g0) in zip(outs[3], outs[0]):
         assert torch.equal(c3, c0)
         assert (g3 is None) == (g0 is None) and (g3 is None or torch.equal(g3, g0))
+
+
+@pytest.mark.parametrize("M,K,epi", [(1000, 64, 19), (777, 256, 17), (300, 576, 1), (64, 64, 3)])
+def test_vgemm_nt_64_wide(cuda, M, K, epi):
+    """the 64-wide tile (N % 128 != 0: ResNet-50 layer1's Cout 64) with the bias / identity / ReLU
+    epilogues, against the fp32 product"""
+    C, _, ref = _nt(cuda, M, 64, K, epi & 3, M + K + epi, 0)
+    if epi & 16:  # VG_RELU: rerun with ReLU (the helper's reference has none)
+        g = torch.Generator(device=cuda).manual_seed(M + K + epi)
+        A = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        B = (torch.randn(64, K, device=cuda, generator=g) / K ** 0.5).bfloat16()
+        bias = torch.randn(64, device=cuda, generator=g)
+        R = torch.randn(M, 64, device=cuda, generator=g).bfloat16() if epi & 2 else None
+        C = torch.full((M, 64), float("nan"), device=cuda, dtype=torch.bfloat16)
+        _lib.check(_lib.load().dfd_vgemm(None, 0, P(A), P(B), P(C), P(R), P(bias), None, None, M, 64, K, epi, None, 0))
+        torch.cuda.synchronize()
+        ref = A.float() @ B.float().T + bias
+        if R is not None:
+            ref = ref + R.float()
+        ref = torch.relu(ref)
+    _close(C, ref)
