@@ -223,9 +223,11 @@ static int rn_go(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, const
   return 0;
 }
 
-// 1: the Cout = 64 convolutions (layer1) on the NT GEMM's 64-wide tile too (A/B build switch)
+// 1: the Cout = 64 convolutions (layer1) on the NT GEMM's 64-wide tile too (A/B build switch; 0: the
+// serving line measured 7.92-7.95 ms with them on this kernel vs 8.00-8.13 on the 64-wide tile,
+// profiles/r04/ab_vg64_r04u.jsonl -- one 122 KB-LDS workgroup per CU loses to two here)
 #ifndef DFD_VG64
-#define DFD_VG64 1
+#define DFD_VG64 0
 #endif
 
 template <typename T>
