@@ -114,8 +114,9 @@ constexpr int RKS = 160, RXS = 40, RCS = 72;  // padded K; im2col / output slab 
 constexpr int RTINB = (RNIN * 4 + 15) / 16 * 16, RXSB = 256 * RXS * 2, RCSB = 256 * RCS * 2;
 constexpr int RUNI = RTINB + RXSB > RCSB ? RTINB + RXSB : RCSB;  // tin + im2col, later the output slab
 typedef short rs_bf16x8 __attribute__((ext_vector_type(8)));
-#ifndef DFD_RSTEM_PF  // 1: the next tile's window loads fly during this tile's MFMAs (A/B build switch)
-#define DFD_RSTEM_PF 1
+#ifndef DFD_RSTEM_PF  // 1: the next tile's window loads fly during this tile's MFMAs (A/B build switch;
+                      // measured neutral, ab_rstem_pf_r04t.jsonl, at 256 instead of 198 VGPRs: off)
+#define DFD_RSTEM_PF 0
 #endif
 typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
 
@@ -149,11 +150,13 @@ __global__ __launch_bounds__(256, 2) void rn_stem_conv_kernel(const void* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) bsv[a][r] = bias[16 * a + 4 * (lane >> 4) + r];
   const int ly = tid / RST, lx = tid % RST;
-  // the next tile's window in registers while this tile computes: raw bytes (U8) or fp32 bits, and
-  // 0xffffffff for positions outside the map
+  // the next tile's window in registers while this tile computes: raw bytes (U8) or fp32 bits, and a
+  // bit per load for the positions inside the map
   constexpr int NLD = (RNIN + 255) / 256;
-  uint32_t raw[NLD];
+  static_assert(NLD <= 32, "validity mask");
+  uint32_t raw[NLD], okm = 0u;
   auto load = [&](int64_t t) {
+    okm = 0u;
     const int64_t n = t / tpf;
     const int r = (int)(t - n * tpf), iy0 = (r / tx) * RST * 2 - 3, ix0 = (r % tx) * RST * 2 - 3;
 #pragma unroll
@@ -161,11 +164,12 @@ __global__ __launch_bounds__(256, 2) void rn_stem_conv_kernel(const void* __rest
       const int e = tid + 256 * i;
       const int pix = e / 3, c = e - pix * 3, ry = pix / RIE, rx = pix - ry * RIE;
       const int iy = iy0 + ry, ix = ix0 + rx;
-      uint32_t v = 0xffffffffu;
+      uint32_t v = 0u;
       if (e < RNIN && iy >= 0 && iy < H && ix >= 0 && ix < W) {
         const int64_t o = n * sn + c * sc + iy * sh + ix * sw;
         if constexpr (U8) v = static_cast<const uint8_t*>(x)[o];
         else v = __float_as_uint(static_cast<const float*>(x)[o]);
+        okm |= 1u << i;
       }
       raw[i] = v;
     }
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256, 2) void rn_stem_conv_kernel(const void* __rest
       if (e < RNIN) {
         const int c = e % 3;
         float v = 0.f;  // zero padding after normalisation, as conv2d pads
-        if (raw[i] != 0xffffffffu) {
+        if ((okm >> i) & 1u) {
           if constexpr (U8) v = lut[c * 256 + raw[i]];
           else v = __uint_as_float(raw[i]);
         }
