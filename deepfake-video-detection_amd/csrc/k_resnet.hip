@@ -115,7 +115,7 @@ constexpr int RTINB = (RNIN * 4 + 15) / 16 * 16, RXSB = 256 * RXS * 2, RCSB = 25
 constexpr int RUNI = RTINB + RXSB > RCSB ? RTINB + RXSB : RCSB;  // tin + im2col, later the output slab
 typedef short rs_bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef DFD_RSTEM_PF  // 1: the next tile's window loads fly during this tile's MFMAs (A/B build switch;
-                      // measured neutral, ab_rstem_pf_r04t.jsonl, at 256 instead of 198 VGPRs: off)
+                      // measured neutral, ab_rstem_pf_r04t.jsonl, at 256 instead of 244 VGPRs: off)
 #define DFD_RSTEM_PF 0
 #endif
 typedef float rs_f32x4 __attribute__((ext_vector_type(4)));
