@@ -179,7 +179,8 @@ int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bi
         int epi_extra = 0, const T* Z = nullptr, T* G = nullptr) {
   const int epi = (bias ? VG_BIAS : 0) | (R ? VG_RESID : 0) | epi_extra;
   if constexpr (sizeof(T) == 2) {
-    if (vgemm_nt_covers(M, N, K)) {
+    // the NT kernel's 64-wide tile carries only the bias / identity / ReLU epilogues: 128-multiples here
+    if (vgemm_nt_covers(M, N, K) && N % 128 == 0) {
       VgemmArgs a{};
       a.A = A; a.B = B; a.C = C; a.R = R; a.bias = bias; a.Z = Z; a.G = G;
       a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
