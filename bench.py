@@ -150,6 +150,10 @@ def cpu_baseline(steps: int):
     nproc = os.cpu_count() or 1
     share = int(os.environ.get("OMP_NUM_THREADS", "0")) or nproc
     threads = max(1, min(share, nproc))
+    try:  # the CPU affinity this process may use (the GPU lease's share of the host)
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     clips = 4
     torch.manual_seed(0)
     m = detector_cpu.DetectorCPU(dropout_rate=0.5)
@@ -175,7 +179,10 @@ def cpu_baseline(steps: int):
             "sample": f"{steps} timed steps x 32 frames (4 clips x 8) 224^2 fp32 on {threads} threads + 1 step on "
                       f"1 thread; oracle/detector_cpu.py train_step (weighted CE, clip 1.0, AdamW), torch "
                       f"{torch.__version__}",
-            "cpu_model": _cpu_model(), "nproc": nproc, "physical_cores": _physical_cores()}
+            "cpu_model": _cpu_model(), "nproc": nproc, "physical_cores": _physical_cores(),
+            "affinity_cpus": affinity, "omp_num_threads": share,
+            "threads_note": (f"{threads} threads = the GPU lease's CPU share (OMP_NUM_THREADS={share}, "
+                             f"affinity {affinity} CPUs) of a {nproc}-CPU host; not the whole host")}
 
 
 def main():
@@ -222,8 +229,9 @@ def main():
     step = DataParallelTrainer(model, lr=1e-4, weight_decay=1e-5, max_grad_norm=1.0,
                                class_weights=torch.tensor([1.0, 1.0]))
     x, labels = synthetic_batch(rank, dev, args.input)
-    # the dominant launch of the step: the fused depthwise backward of blocks.1.0
-    # (dw_bwd<16,16,3,2>, 112x112x96 <- 56x56x96, the largest single kernel in the rocprof trace)
+    # the dominant launch of the step: the fused stride-2 depthwise backward of blocks.1.0
+    # (dw_bwd2_kernel<bf16,3,8,56,14,1>, 112x112x96 <- 56x56x96, k_dw_bwd2.hip; the largest single
+    # kernel in the rocprof trace)
     probe = roofline.KernelProbe(model, "dw_bwd", stage=1, block=0)
 
     def timed(n, arm=False):

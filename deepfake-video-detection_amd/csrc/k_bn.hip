@@ -7,6 +7,7 @@
 // deterministic two-level reduction: producers write per-workgroup partial rows
 // [rows][2][C] and bn_finalize sums them in a fixed order (fp64) -- no float atomics in HBM.
 #include "kernels.h"
+#include "tail.h"
 
 namespace dfd {
 
@@ -945,7 +946,22 @@ typedef float se_f32x4 __attribute__((ext_vector_type(4)));
 // forward A = a_scale * sum (the squeeze mean), backward A = sum * g (1 - g) with g = a_gate[f][c]
 // (de = dgate * sigmoid'); the workgroups of channel slice 0 store A to a_out (sq / de), which the
 // backward's weight gradients read.
-template <bool FWD>
+// FIN (backward only): the BN2 backward finalize of bn_bwd_finalize_frames_kernel folded into the
+// same launch -- every workgroup adds its 16 frames' terms gate*P1 + bc*P2 / gate*P3 + bc*P4 (fp64)
+// for its channel slice into a partial row, and the last-arriving workgroup of the slice (tail.h)
+// sums the frame tiles' rows in order and writes dbeta, dgamma and the coefficients k1..k3.
+struct SeFin {
+  const float* part;  // frame_reduce<FR_SEBN> partials part[5][hsplit][frames][C] (q = 1..4 read)
+  int hsplit;
+  double* rows;       // [frame tiles][2][C] scratch
+  unsigned* ctr;      // one zeroed counter per channel slice
+  int64_t count;      // BN rows (frames x HW)
+  const float *gamma, *mean, *invstd;
+  int training, accumulate;
+  float *dgamma, *dbeta, *coef;
+};
+
+template <bool FWD, bool FIN = false>
 __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __restrict__ A, int hsplit, float a_scale,
                                                        const float* __restrict__ a_gate, float* __restrict__ a_out,
                                                        int frames, int C, int rd,
@@ -953,7 +969,7 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
                                                        const float* __restrict__ rpre_in,
                                                        const float* __restrict__ W2, const float* __restrict__ b2,
                                                        float scale2, float* __restrict__ t1_out,
-                                                       float* __restrict__ out) {
+                                                       float* __restrict__ out, SeFin fin) {
   __shared__ float red[SE_W][3][4][64];
   __shared__ float Ts[16][SE_TS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1057,13 +1073,66 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < SE_RDMAX / 4; ++i)
       if (4 * i < rd) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Ts[li][4 * i + lk], bw[i], acc, 0, 0, 0);
+    double fs = 0.0, fq = 0.0;  // FIN: this lane's frames' BN2-backward terms
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = f0 + 4 * lk + r;
       if (f < frames && nok) {
         const float v = FWD ? sigmoidf_(acc[r] + b2[n]) : acc[r] * scale2;
         out[(int64_t)f * C + n] = v;
+        if constexpr (FIN) {
+          const int64_t nfc = (int64_t)frames * C, i = (int64_t)f * C + n;
+          float p[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float* b = fin.part + (int64_t)(q + 1) * fin.hsplit * nfc + i;
+            float a = b[0];
+            for (int h = 1; h < fin.hsplit; ++h) a += b[(int64_t)h * nfc];
+            p[q] = a;
+          }
+          const double gt = a_gate[i];
+          fs += gt * (double)p[0] + (double)v * (double)p[1];
+          fq += gt * (double)p[2] + (double)v * (double)p[3];
+        }
       }
+    }
+    if constexpr (FIN) {
+      // the 4 frame groups of a column (lanes li, li+16, li+32, li+48) in a fixed order
+      fs += __shfl_xor(fs, 16, 64);
+      fq += __shfl_xor(fq, 16, 64);
+      fs += __shfl_xor(fs, 32, 64);
+      fq += __shfl_xor(fq, 32, 64);
+      if (lk == 0 && nok) {
+        fin.rows[((int64_t)blockIdx.x * 2 + 0) * C + n] = fs;
+        fin.rows[((int64_t)blockIdx.x * 2 + 1) * C + n] = fq;
+      }
+    }
+  }
+  if constexpr (FIN) {
+    if (!tail_arrive(fin.ctr + blockIdx.y, gridDim.x)) return;
+    // last workgroup of this channel slice: frame tiles in order, then bn_bwd_finalize_frames' arithmetic
+    const int c = cbeg + tid;
+    if (c < cend) {
+      const float p_g = fin.gamma[c], p_is = fin.invstd[c], p_mu = fin.mean[c];
+      const float p_db = fin.accumulate ? fin.dbeta[c] : 0.f, p_dg = fin.accumulate ? fin.dgamma[c] : 0.f;
+      double s = 0.0, q = 0.0;
+      for (int t = 0; t < (int)gridDim.x; ++t) {
+        s += fin.rows[((int64_t)t * 2 + 0) * C + c];
+        q += fin.rows[((int64_t)t * 2 + 1) * C + c];
+      }
+      const float db = (float)s, dg = (float)q;
+      fin.dbeta[c] = fin.accumulate ? p_db + db : db;
+      fin.dgamma[c] = fin.accumulate ? p_dg + dg : dg;
+      const double gm = p_g, is = p_is;
+      double k2 = 0.0, k3 = 0.0;
+      if (fin.training) {
+        const double cnt = (double)fin.count;
+        k2 = -gm * is * is * q / cnt;
+        k3 = -gm * is * s / cnt + gm * is * is * (double)p_mu * q / cnt;
+      }
+      fin.coef[c] = (float)(gm * is);
+      fin.coef[C + c] = (float)k2;
+      fin.coef[2 * C + c] = (float)k3;
     }
   }
 }
@@ -1074,7 +1143,7 @@ int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw,
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
   const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
   hipLaunchKernelGGL(se_chain_kernel<true>, grid, dim3(64 * SE_W), 0, s, part, hsplit, inv_hw, nullptr, sq, frames, C,
-                     rd, wr, br, nullptr, we, be, 1.f, rpre, gate);
+                     rd, wr, br, nullptr, we, be, 1.f, rpre, gate, SeFin{});
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1087,11 +1156,22 @@ int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw,
 int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
                      const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
                      float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate,
-                     MfmaGemm* defer2) {
+                     MfmaGemm* defer2, const BnFramesFin* bnf) {
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
   const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
-  hipLaunchKernelGGL(se_chain_kernel<false>, grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames, C, rd,
-                     we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out);
+  if (bnf) {
+    if ((int)grid.y > bnf->ctr_slots || (int64_t)grid.x * 2 * C * 2 > bnf->rows_cap) {
+      set_error("se: fused finalize scratch too small", __FILE__, __LINE__);
+      return -1;
+    }
+    const SeFin f{part, hsplit, bnf->rows, bnf->ctr, bnf->count, bnf->gamma, bnf->mean, bnf->invstd,
+                  bnf->training ? 1 : 0, bnf->accumulate ? 1 : 0, bnf->dgamma, bnf->dbeta, bnf->coef};
+    hipLaunchKernelGGL((se_chain_kernel<false, true>), grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames,
+                       C, rd, we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out, f);
+  } else {
+    hipLaunchKernelGGL((se_chain_kernel<false>), grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames, C,
+                       rd, we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out, SeFin{});
+  }
   DFD_HIP_CHECK(hipGetLastError());
   MfmaGemm ge{}, gr{};
   ge.A = de; ge.sam = 1; ge.sak = C; ge.B = rpre; ge.sbk = rd; ge.sbn = 1; ge.b_silu = 1; ge.C = gwe; ge.ldc = rd;

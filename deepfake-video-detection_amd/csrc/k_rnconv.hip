@@ -247,8 +247,11 @@ int launch_rn_conv(hipStream_t s, const T* X, const T* Wt, T* C, const T* R, con
     if ((int64_t)g.N * g.H >= (1ll << 31)) { set_error("rn_conv: too many rows", __FILE__, __LINE__); return -1; }
     if constexpr (sizeof(T) == 2) {
       // bf16 3x3 and strided convolutions with Cin % 64 == 0 and Cout % 128 == 0: the same LDS-DMA NT
-      // kernel, its A tile gathered per tap from the NHWC input (implicit GEMM, K order tap-major as here)
-      if (vgemm_conv_covers(g.Cin, N, g.KH, g.KW) && vgemm_nt_covers(M, N, K) && (DFD_VG64 || N % 128 == 0)) {
+      // kernel, its A tile gathered per tap from the NHWC input (implicit GEMM, K order tap-major as here).
+      // Its convolution instantiations carry ReLU (alone or after the identity) or the bias alone; a
+      // residual without ReLU (no ResNet-50 layer has one) stays on rn_go below
+      const bool ep_ok = relu || !R;
+      if (ep_ok && vgemm_conv_covers(g.Cin, N, g.KH, g.KW) && vgemm_nt_covers(M, N, K) && (DFD_VG64 || N % 128 == 0)) {
         VgemmArgs a{};
         a.A = X; a.B = Wt; a.C = C; a.R = R; a.bias = bias;
         a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;

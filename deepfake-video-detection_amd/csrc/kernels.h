@@ -44,7 +44,8 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 // Concurrent plans -- e.g. inference on a ThreadPoolExecutor worker (app.py:127-129) next to a
 // training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
-               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP, TK_COUNT };
+               TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP,
+               TK_TAIL_FIN, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -60,7 +61,13 @@ struct Tuning {
 #ifndef DFD_VG_XP_DEFAULT  // A/B builds of k_vgemm.o only (tools/ab_lib.sh): the one reader of TK_VG_XP
 #define DFD_VG_XP_DEFAULT 1
 #endif
-constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, DFD_VG_XP_DEFAULT};
+// tail_fin: BN finalizes in the producers' last-arriving workgroups (tail.h) instead of their own
+// launches (bit 0: the SE-backward chain's BN2 finalize)
+#ifndef DFD_TAIL_FIN_DEFAULT
+#define DFD_TAIL_FIN_DEFAULT 1
+#endif
+constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, DFD_VG_XP_DEFAULT,
+                                            DFD_TAIL_FIN_DEFAULT};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {
@@ -297,11 +304,24 @@ int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro,
 // (de = dgate g (1-g) from the q = 0 partials of launch_se_bn_bwd_reduce, stored to `de`)
 // defer2 != nullptr: the two weight-gradient products are returned there (MfmaGemm[2]) for a later
 // launch_mfma_small_gemm_batch instead of being launched (de and tmp_dz must then stay intact)
+// bnf != nullptr: the BN(+SiLU) backward finalize of launch_bn_bwd_finalize_frames (dbeta, dgamma, coef
+// from gate, bc and the partials part[1..4]) runs in the same launch, in each channel slice's
+// last-arriving workgroup (tail.h; ctr: >= cdiv(C, 256) zeroed counters, rows: frame-tile scratch)
 struct MfmaGemm;
+struct BnFramesFin {
+  double* rows;
+  int64_t rows_cap;  // floats
+  unsigned* ctr;
+  int ctr_slots;
+  int64_t count;
+  const float *gamma, *mean, *invstd;
+  bool training, accumulate;
+  float *dgamma, *dbeta, *coef;
+};
 int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
                      const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
                      float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate,
-                     MfmaGemm* defer2 = nullptr);
+                     MfmaGemm* defer2 = nullptr, const BnFramesFin* bnf = nullptr);
 // SE + BN(+SiLU) backward sums in one pass over (dZ, Y): per-frame partials part[5][hsplit][frames][C] -- q = 0
 // the SE gate gradient (added by launch_se_fc_bwd), q = 1..4 the sums bn_bwd_finalize_frames combines with the
 // gate and bc (k_bn.hip)

@@ -245,6 +245,10 @@ int plan_bind(Plan& p, const int64_t* offs, int n) {
   for (const Block& b : p.blocks) { if (!b.ds) seg(b.pw); seg(b.pwl); }
   seg(p.head);
   if (!p.cast_dev) DFD_HIP_CHECK(hipMalloc(&p.cast_dev, p.cast_host.size() * sizeof(CastSeg)));
+  if (!p.ctr_dev) {  // last-arrival counters (tail.h): zero at rest, every use resets its own
+    DFD_HIP_CHECK(hipMalloc(&p.ctr_dev, kCtrSlots * sizeof(unsigned)));
+    DFD_HIP_CHECK(hipMemset(p.ctr_dev, 0, kCtrSlots * sizeof(unsigned)));
+  }
   DFD_HIP_CHECK(hipMemcpy(p.cast_dev, p.cast_host.data(), p.cast_host.size() * sizeof(CastSeg), hipMemcpyHostToDevice));
   p.bound = true;
   return 0;
@@ -311,6 +315,7 @@ void plan_free(Plan& p) {
   probe_disarm(p);
   aux_free(p);
   if (p.cast_dev) { (void)hipFree(p.cast_dev); p.cast_dev = nullptr; }
+  if (p.ctr_dev) { (void)hipFree(p.ctr_dev); p.ctr_dev = nullptr; }
 }
 
 // ------------------------------------------------------------------ forward / backward
@@ -673,14 +678,21 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         // the SE weight gradients (two small products per block, off the critical chain) are
         // batched into one launch per segment: de / dz stay in per-block buffers until then
         if (n_se + 2 > (int)(sizeof(se_jobs) / sizeof(se_jobs[0]))) DFD_TRY(flush_se());
+        // the BN2 backward finalize (dbeta, dgamma, k1..k3 from gate, bc and the frame sums) in the
+        // excitation launch's last workgroups (knob tail_fin bit 0), o_stats free as row scratch here
+        const bool sefin = (tune(TK_TAIL_FIN) & 1) != 0;
+        const BnFramesFin bnf{reinterpret_cast<double*>(r.f(p.o_stats)), p.stats_cap, p.ctr_dev, kCtrSlots, Mout,
+                              r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), tr != 0, acc != 0,
+                              grad(bn_dw.t_w), grad(bn_dw.t_b), r.f(p.o_coef)};
         DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(b.o_de), r.f(b.o_sq), r.f(b.o_rpre),
                                  r.prm(b.t_se_wr), r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo,
                                  r.f(b.o_dz), r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we),
-                                 grad(b.t_se_be), acc != 0, se_jobs + n_se));
+                                 grad(b.t_se_be), acc != 0, se_jobs + n_se, sefin ? &bnf : nullptr));
         n_se += 2;
-        DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid,
-                                              Mout, r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd),
-                                              tr != 0, grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
+        if (!sefin)
+          DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid,
+                                                Mout, r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd),
+                                                tr != 0, grad(bn_dw.t_w), grad(bn_dw.t_b), acc != 0, r.f(p.o_coef)));
         // depthwise conv
         // depthwise dgrad fused with the backward reduction of the producer's BN+SiLU
         // (stem BN for the stage-0 block, bn1 otherwise): ge1 = g, stats = partials of g, g*xhat
@@ -841,7 +853,8 @@ int plan_fused7_blocks(const Plan& p) {
 
 
 const char* const kTuneNames[TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile", "dw_bwd1",
-                                          "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused", "pw_sk", "dw_pf", "dw_rb", "stem_occ", "vg_xp"};
+                                          "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused", "pw_sk", "dw_pf", "dw_rb", "stem_occ", "vg_xp",
+                                          "tail_fin"};
 static thread_local const Tuning* t_tune = nullptr;
 int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tune) { t_tune = t; }

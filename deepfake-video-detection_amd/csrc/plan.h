@@ -53,6 +53,8 @@ struct Probe {
   std::vector<hipEvent_t> b, e;
 };
 
+constexpr int kCtrSlots = 1024;
+
 struct Plan {
   int frames, H, W, dtype;
   int H1, W1, Hf, Wf;  // stem output, final feature map
@@ -74,6 +76,7 @@ struct Plan {
   // cast table (device copy)
   std::vector<CastSeg> cast_host;
   CastSeg* cast_dev = nullptr;
+  unsigned* ctr_dev = nullptr;  // last-arrival counters (tail.h), kCtrSlots, zero at rest
   int cast_max = 0;
   int device = 0;
   int pending_rows = 0;  // stat rows written by the stage-0 dw dgrad, consumed by the stem segment

@@ -1,0 +1,36 @@
+// Last-arriving-workgroup epilogues: a reduction that used to be its own (latency-bound, ~5 us)
+// launch after a producer kernel runs instead in the producer's last workgroup of a group.
+//
+// Protocol (the pattern of grid_sync.h, without the wait): every workgroup of the group writes its
+// partial row with plain stores, drains them, meets at the workgroup barrier; thread 0 publishes
+// with an agent-scope release (this XCD's L2 written back) and takes a ticket with an agent-scope
+// atomic.  The workgroup drawing the last ticket acquires (agent scope: stale lines of its CU and
+// L2 invalidated), resets the counter to zero for the next launch (counters are zero at rest: the
+// plan zeroes them once when it allocates them), and alone reads every partial row in a fixed order
+// -- so the result does not depend on which workgroup arrives last (bit-reproducible).  Nobody
+// waits: the other workgroups leave, so the grid need not be co-resident.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace dfd {
+
+// true in every thread of the last-arriving workgroup of the `expected` workgroups sharing `ctr`
+__device__ __forceinline__ bool tail_arrive(unsigned* ctr, unsigned expected) {
+  __shared__ int tail_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == expected - 1;
+    if (last) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    tail_last = last;
+  }
+  __syncthreads();
+  return tail_last != 0;
+}
+
+}  // namespace dfd

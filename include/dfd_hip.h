@@ -292,9 +292,14 @@ DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int
                           int64_t lddo, void* dqkv, int64_t lddq);
 
 /* The ViT trunk's large bf16 GEMMs (k_vgemm.hip; test / measurement seam): op 0 (NT):
- * C[M][N] (bf16) = A[M][K] . B[N][K]^T with the epilogue mask epi: 1 + bias[N] (fp32), 2 + R[M][N],
- * 4 also G = gelu(C) (C keeps the pre-activation), 8 C *= gelu'(Z[M][N]); N % 128 == 0, K % 64 == 0;
- * the tile width (256 or 128 columns) is chosen by shape; ops 4 / 5 force 256 (N % 256 == 0) / 128.
+ * C[M][N] (bf16) = A[M][K] . B[N][K]^T with the epilogue mask epi (applied in this order, fp32, one
+ * rounding): 1 + bias[N] (fp32), 2 + R[M][N], 16 ReLU; 4 (GELU pair, with 1): with z the bf16-rounded
+ * pre-activation, G = gelu(z) and C = gelu'(z) -- C does NOT keep the pre-activation; 8: C *= Z[M][N]
+ * elementwise, Z being the derivative an epi-4 launch stored in its C (the MLP backward's x gelu').
+ * Instantiated masks: 0, 1, 1|2, 1|4, 8, 1|16, 1|2|16.  K % 64 == 0 and N % 128 == 0, except that
+ * N % 64 == 0 (the 64-wide tile) is accepted with the bias / identity / ReLU masks 1, 1|2, 1|16,
+ * 1|2|16 only.  The tile width (256, 128 or 64 columns) is chosen by shape; ops 4 / 5 force 256
+ * (N % 256 == 0) / 128.
  * op 1 (TN): C (fp32 [N][K]) = A^T . B for A [M][N], B [M][K] (bf16), split over M into slab
  * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0; with G non-null also
  * G (fp32 [N]) = the column sums of A (a linear's bias gradient) from the same launch.  ops 2 / 3: the same

@@ -153,7 +153,8 @@ def test_rn_conv_kernel_every_shape(dt):
             ho = (h + 2 * p - k) // s + 1
             res = torch.randn(n, ho, ho, cout, generator=g).to(tdt).cuda()
             out = torch.empty(n, ho, ho, cout, dtype=tdt, device="cuda")
-            for use_res, relu in ((False, True), (True, True), (False, False)):
+            # (True, False): identity without ReLU -- no vgemm instantiation, the launcher's fallback
+            for use_res, relu in ((False, True), (True, True), (False, False), (True, False)):
                 st = _lib.stream_of(out.device)
                 _lib.check(lib.dfd_rn_conv(st, 0 if dt == "fp32" else 1, x.data_ptr(), n, h, h, cin, k, k, s, p,
                                            w.data_ptr(), b.data_ptr(), res.data_ptr() if use_res else None,

@@ -97,6 +97,41 @@ def test_vgemm_tn_vs_fp32(cuda, M, N, K, colsum):
         assert ec <= 1e-5, ec
 
 
+C5_M = 128 * 197  # the ViT line's token rows (128 images x 197 tokens)
+
+
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (3072, 768), (768, 3072), (768, 2304)])
+def test_vgemm_nt_c5_rows(cuda, N, K):
+    """the ViT-B/16 linears and data gradients (qkv / proj / fc1 / fc2 forward, fc2 / qkv data gradients)
+    at the C5 line's own M = 25,216: the tile width (256 vs 128 columns) and the dispatch-wave count
+    follow M (vgemm_nt_bn), so the configuration the 128-image step runs is checked here, not only at
+    <= 8 images"""
+    C, _, ref = _nt(cuda, C5_M, N, K, 1, N + K)
+    _close(C, ref)
+
+
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (3072, 768), (768, 3072)])
+def test_vgemm_tn_c5_rows(cuda, N, K):
+    """the four ViT weight gradients (dW = dY^T X, with the bias gradient from the same launch) at the
+    C5 M = 25,216, where vgemm_tn_splits picks its split count and slab layout from M (e.g. 28 splits
+    for 768 x 768 against 16 at M = 4,096): fp32 result against fp64, relative L2 <= 1e-5"""
+    g = torch.Generator(device=cuda).manual_seed(N * 3 + K)
+    A = torch.randn(C5_M, N, device=cuda, generator=g).bfloat16()
+    B = torch.randn(C5_M, K, device=cuda, generator=g).bfloat16()
+    lib = _lib.load()
+    slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(C5_M, N, K), device=cuda)
+    flat = torch.full((N * K + N,), float("nan"), device=cuda)
+    W, cs = flat[:N * K].view(N, K), flat[N * K:]
+    _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, P(cs), C5_M, N, K, 0, P(slab), slab.numel()))
+    torch.cuda.synchronize()
+    ref = A.double().T @ B.double()
+    e = float((W.double() - ref).norm() / ref.norm())
+    rc = A.double().sum(0)
+    ec = float((cs.double() - rc).norm() / rc.norm())
+    print(f"TN {N}x{K} at M={C5_M}: slab splits {slab.numel() // (N * K + N)}, rel err {e:.2e}, bias {ec:.2e}")
+    assert e <= 1e-5 and ec <= 1e-5, (e, ec)
+
+
 def test_vgemm_deterministic(cuda):
     """two runs of the same TN product and NT product are bit-identical (fixed-order slab sums)"""
     M, N, K = 2 * 197, 768, 768
@@ -143,12 +178,15 @@ def test_vgemm_nt_xp_bit_identical(cuda, M, N, K, epi):
     one-K-step products (K = 64) included"""
     lib = _lib.load()
     outs = {}
+    prev = None
     try:
         for xp in (3, 0):
-            lib.dfd_set_tuning(b"vg_xp", xp)
+            p = lib.dfd_set_tuning(b"vg_xp", xp)
+            prev = p if prev is None else prev
             outs[xp] = [_nt(cuda, M, N, K, epi, 17, op)[:2] for op in (4, 5) if N % 256 == 0 or op == 5]
     finally:
-        lib.dfd_set_tuning(b"vg_xp", 0)
+        if prev is not None:  # the seam's previous value (the default loop unless a test changed it)
+            lib.dfd_set_tuning(b"vg_xp", prev)
     for (c3, g3), (c0, g0) in zip(outs[3], outs[0]):
         assert torch.equal(c3, c0)
         assert (g3 is None) == (g0 is None) and (g3 is None or torch.equal(g3, g0))

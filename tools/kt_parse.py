@@ -1,4 +1,4 @@
-"""Parse tools/r03_tiles.sh output: per site, default time and best forced config."""
+"""Parse tools/r03/tiles.sh output: per site, default time and best forced config."""
 import re, sys
 cur = None
 data = {}

@@ -3,5 +3,5 @@
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
 bash tools/kb_var.sh pf dw_fwd p0 p1 > /dev/null || exit $?
 bash tools/kb_var.sh xcd dw_ x0 x1 > /dev/null || exit $?
-bash tools/r03_kt2.sh || exit $?
+bash tools/r03/kt2.sh || exit $?
 echo multi-done

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick check after a kernel change: selected GPU tests, kbench rows, bench line (no CPU baseline).
-# usage: tools/r03_quick.sh TAG "pytest targets" "kbench filter"
+# usage: tools/r03/quick.sh TAG "pytest targets" "kbench filter"
 R=$GRAFT_REPO_ROOT; TAG=${1:-q}; TESTS=${2:-"tests/test_b0_parity_gpu.py"}; KB=${3:-}
 cd $R; mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest $TESTS -x -q --timeout 300 --timeout-method thread > gpurun_out/t_$TAG.log 2>&1; rc=$?

@@ -5,5 +5,5 @@ grep -E "first fused|FAILED|passed|failed" gpurun_out/t_$TAG.log | tail -20
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 tools/kbench fused 256 > gpurun_out/kb_$TAG.txt 2>&1 || { echo KBENCH FAILED; exit 1; }
 cat gpurun_out/kb_$TAG.txt
-bash tools/r03_prof.sh $TAG
+bash tools/r03/prof.sh $TAG
 exit $rc

@@ -6,5 +6,5 @@ grep -E "first fused|FAILED|passed|failed" gpurun_out/t_$TAG.log | tail -20
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 400 python -u bench_temporal.py --model ensemble_train > gpurun_out/et_$TAG.jsonl 2> gpurun_out/et_$TAG.err || { echo ET FAILED; tail -20 gpurun_out/et_$TAG.err; exit 1; }
 cut -c1-600 gpurun_out/et_$TAG.jsonl
-bash tools/r03_prof.sh $TAG
+bash tools/r03/prof.sh $TAG
 exit $rc
