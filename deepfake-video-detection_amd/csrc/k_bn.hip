@@ -976,6 +976,31 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
   const int li = lane & 15, lk = lane >> 4;
   const int f0 = blockIdx.x * 16;
   const int nt1 = (rd + 15) / 16;
+  // FIN: this lane's second-product outputs are column cbeg + 16 wave + li, frames f0 + 4 lk + r; their
+  // gate and frame sums P1..P4 (added over the pixel chunks) are loaded up front, off the chain
+  float fgt[4], fp[4][4];
+  if constexpr (FIN) {
+    const int n = blockIdx.y * SE_CSL + 16 * wave + li;
+    const int64_t nfc = (int64_t)frames * C;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = f0 + 4 * lk + r;
+      const bool ok = f < frames && n < C;
+      const int64_t i = ok ? (int64_t)f * C + n : 0;
+      fgt[r] = ok ? a_gate[i] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fp[r][q] = ok ? fin.part[(int64_t)(q + 1) * fin.hsplit * nfc + i] : 0.f;
+    }
+    for (int h = 1; h < fin.hsplit; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = f0 + 4 * lk + r;
+        const bool ok = f < frames && n < C;
+        const int64_t i = ok ? (int64_t)f * C + n : 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) fp[r][q] += ok ? fin.part[((int64_t)(q + 1) * fin.hsplit + h) * nfc + i] : 0.f;
+      }
+  }
   // ---- T = A[16 frames][C] . B1[C][rd] ----
   se_f32x4 acc1[3];
 #pragma unroll
@@ -1081,18 +1106,8 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
         const float v = FWD ? sigmoidf_(acc[r] + b2[n]) : acc[r] * scale2;
         out[(int64_t)f * C + n] = v;
         if constexpr (FIN) {
-          const int64_t nfc = (int64_t)frames * C, i = (int64_t)f * C + n;
-          float p[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float* b = fin.part + (int64_t)(q + 1) * fin.hsplit * nfc + i;
-            float a = b[0];
-            for (int h = 1; h < fin.hsplit; ++h) a += b[(int64_t)h * nfc];
-            p[q] = a;
-          }
-          const double gt = a_gate[i];
-          fs += gt * (double)p[0] + (double)v * (double)p[1];
-          fq += gt * (double)p[2] + (double)v * (double)p[3];
+          fs += (double)fgt[r] * (double)fp[r][0] + (double)v * (double)fp[r][1];
+          fq += (double)fgt[r] * (double)fp[r][2] + (double)v * (double)fp[r][3];
         }
       }
     }
@@ -1103,8 +1118,8 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
       fs += __shfl_xor(fs, 32, 64);
       fq += __shfl_xor(fq, 32, 64);
       if (lk == 0 && nok) {
-        fin.rows[((int64_t)blockIdx.x * 2 + 0) * C + n] = fs;
-        fin.rows[((int64_t)blockIdx.x * 2 + 1) * C + n] = fq;
+        tail_store(fin.rows + ((int64_t)blockIdx.x * 2 + 0) * C + n, fs);
+        tail_store(fin.rows + ((int64_t)blockIdx.x * 2 + 1) * C + n, fq);
       }
     }
   }
@@ -1116,9 +1131,20 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
       const float p_g = fin.gamma[c], p_is = fin.invstd[c], p_mu = fin.mean[c];
       const float p_db = fin.accumulate ? fin.dbeta[c] : 0.f, p_dg = fin.accumulate ? fin.dgamma[c] : 0.f;
       double s = 0.0, q = 0.0;
-      for (int t = 0; t < (int)gridDim.x; ++t) {
-        s += fin.rows[((int64_t)t * 2 + 0) * C + c];
-        q += fin.rows[((int64_t)t * 2 + 1) * C + c];
+      int t = 0;
+      for (; t + 8 <= (int)gridDim.x; t += 8) {  // 16 loads in flight, added in tile order
+        double vs[8], vq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          vs[u] = tail_load(fin.rows + ((int64_t)(t + u) * 2 + 0) * C + c);
+          vq[u] = tail_load(fin.rows + ((int64_t)(t + u) * 2 + 1) * C + c);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { s += vs[u]; q += vq[u]; }
+      }
+      for (; t < (int)gridDim.x; ++t) {
+        s += tail_load(fin.rows + ((int64_t)t * 2 + 0) * C + c);
+        q += tail_load(fin.rows + ((int64_t)t * 2 + 1) * C + c);
       }
       const float db = (float)s, dg = (float)q;
       fin.dbeta[c] = fin.accumulate ? p_db + db : db;

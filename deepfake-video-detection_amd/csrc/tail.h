@@ -14,18 +14,36 @@
 
 namespace dfd {
 
+// DFD_TAIL_WT (A/B build switch, default 0): the partial rows are written and read with agent-scope
+// atomic stores / loads (coherent at the device level without an L2 write-back or invalidate) and the
+// arrival carries no release / acquire fence -- measures what the fences cost
+#ifndef DFD_TAIL_WT
+#define DFD_TAIL_WT 0
+#endif
+
+template <typename V>
+__device__ __forceinline__ void tail_store(V* p, V v) {
+  if constexpr (DFD_TAIL_WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <typename V>
+__device__ __forceinline__ V tail_load(const V* p) {
+  if constexpr (DFD_TAIL_WT) return __hip_atomic_load(const_cast<V*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+
 // true in every thread of the last-arriving workgroup of the `expected` workgroups sharing `ctr`
 __device__ __forceinline__ bool tail_arrive(unsigned* ctr, unsigned expected) {
   __shared__ int tail_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if constexpr (!DFD_TAIL_WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const unsigned t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = t == expected - 1;
     if (last) {
       __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if constexpr (!DFD_TAIL_WT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     tail_last = last;
   }
