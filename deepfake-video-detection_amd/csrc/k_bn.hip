@@ -362,13 +362,15 @@ static void bn_vpg_groups(int C, int& vpg, int& groups) {
 }
 
 template <typename T>
-int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, float* stats, int* stat_rows) {
+int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, float* stats, int* stat_rows,
+                         int max_rows) {
   if (M > (int64_t)UINT32_MAX) { set_error("bn: more than 2^32 rows", __FILE__, __LINE__); return -1; }
   int vpg, groups;
   bn_vpg_groups(C, vpg, groups);
   const int nrl = 256 / vpg;
   const int64_t rows_needed = cdiv64(M, nrl * 4);
-  const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(rows_needed, std::max(1, 1024 / groups)));
+  int gx = (int)std::max<int64_t>(1, std::min<int64_t>(rows_needed, std::max(1, 1024 / groups)));
+  if (max_rows > 0) gx = std::min(gx, max_rows);
   switch (bn_flags(in)) {
 #define DFD_BNR(F) case F: hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, F>), dim3(gx, groups), dim3(256), 0, s, in, Y, M, C, stats, vpg); break;
     DFD_BNR(0) DFD_BNR(1) DFD_BNR(2) DFD_BNR(3) DFD_BNR(4) DFD_BNR(5) DFD_BNR(6) DFD_BNR(7)
@@ -472,6 +474,145 @@ int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const floa
   }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
+}
+
+// ------------------------------------------------------------------ BN backward finalize + apply
+// The finalize (bn_bwd_finalize_kernel) and the apply pass in ONE launch where the producer wrote few
+// stat rows: every workgroup owns 64 channels and a chunk of rows; it first reduces the stat rows of
+// its channels (16 row lanes x 16 float4 columns, fp64, lanes added in a fixed order -- the same k1..k3
+// in every workgroup of the channel group), the row-chunk-0 workgroup also stores dbeta / dgamma /
+// coef, then it applies dY = k1*g + k2*y + k3 over its rows.  Saves the ~5 us finalize launch per BN
+// backward; the reduction costs each workgroup rows / 16 x 2 loads per thread (used for rows <= 256).
+constexpr int BAF_CH = 64, BAF_RL = 16, BAF_ROWS_MAX = 256;
+struct BnFinArgs {
+  int64_t count;
+  const float *gamma, *mean, *invstd;
+  int training, accumulate;
+  float *dgamma, *dbeta, *coef;
+};
+
+template <typename T, int FL>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(BnBwdIn in, const T* __restrict__ Y, int64_t M, int C,
+                                                               const float* __restrict__ stats, int rows, BnFinArgs fa,
+                                                               T* dY, int64_t rows_per_wg) {
+  __shared__ double sh[2][BAF_RL][BAF_CH];
+  __shared__ float kc[3][BAF_CH];
+  const int tid = threadIdx.x;
+  const int c0 = blockIdx.y * BAF_CH;
+  const int nch = min(BAF_CH, C - c0);
+  {
+    const int c4 = tid & 15, rl = tid >> 4;
+    const int c = c0 + 4 * c4;
+    double s[4] = {0.0, 0.0, 0.0, 0.0}, q[4] = {0.0, 0.0, 0.0, 0.0};
+    if (4 * c4 < nch) {
+      int r = rl;
+      for (; r + 7 * BAF_RL < rows; r += 8 * BAF_RL) {  // 16 loads in flight, added in row order
+        float4 vs[8], vq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          vs[u] = *reinterpret_cast<const float4*>(stats + ((int64_t)(r + u * BAF_RL) * 2 + 0) * C + c);
+          vq[u] = *reinterpret_cast<const float4*>(stats + ((int64_t)(r + u * BAF_RL) * 2 + 1) * C + c);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          s[0] += vs[u].x; s[1] += vs[u].y; s[2] += vs[u].z; s[3] += vs[u].w;
+          q[0] += vq[u].x; q[1] += vq[u].y; q[2] += vq[u].z; q[3] += vq[u].w;
+        }
+      }
+      for (; r < rows; r += BAF_RL) {
+        const float4 vs = *reinterpret_cast<const float4*>(stats + ((int64_t)r * 2 + 0) * C + c);
+        const float4 vq = *reinterpret_cast<const float4*>(stats + ((int64_t)r * 2 + 1) * C + c);
+        s[0] += vs.x; s[1] += vs.y; s[2] += vs.z; s[3] += vs.w;
+        q[0] += vq.x; q[1] += vq.y; q[2] += vq.z; q[3] += vq.w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sh[0][rl][4 * c4 + j] = s[j];
+      sh[1][rl][4 * c4 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  if (tid < nch) {
+    double s = 0.0, q = 0.0;
+#pragma unroll
+    for (int l = 0; l < BAF_RL; ++l) { s += sh[0][l][tid]; q += sh[1][l][tid]; }
+    const int c = c0 + tid;
+    const double gm = fa.gamma[c], is = fa.invstd[c];
+    const double k1 = gm * is;
+    double k2 = 0.0, k3 = 0.0;
+    if (fa.training) {
+      const double n = (double)fa.count;
+      k2 = -gm * is * is * q / n;
+      k3 = -gm * is * s / n + gm * is * is * (double)fa.mean[c] * q / n;
+    }
+    kc[0][tid] = (float)k1;
+    kc[1][tid] = (float)k2;
+    kc[2][tid] = (float)k3;
+    if (blockIdx.x == 0) {
+      const float db = (float)s, dg = (float)q;
+      fa.dbeta[c] = fa.accumulate ? fa.dbeta[c] + db : db;
+      fa.dgamma[c] = fa.accumulate ? fa.dgamma[c] + dg : dg;
+      if (fa.coef) {
+        fa.coef[c] = (float)k1;
+        fa.coef[C + c] = (float)k2;
+        fa.coef[2 * C + c] = (float)k3;
+      }
+    }
+  }
+  __syncthreads();
+  // apply: 8 channel vectors x 32 row lanes, two rows' loads in flight
+  const int v = tid & 7, rl = tid >> 3;
+  const int cl = 8 * v, c = c0 + cl;
+  if (cl >= nch) return;
+  float k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { k1[j] = kc[0][cl + j]; k2[j] = kc[1][cl + j]; k3[j] = kc[2][cl + j]; }
+  BnBwdCh ch;
+  bn_bwd_ch<FL>(in, c, ch);
+  const int64_t rb = (int64_t)blockIdx.x * rows_per_wg, re = min(M, rb + rows_per_wg);
+  int64_t row = rb + rl;
+  for (; row + 32 < re; row += 64) {
+    float g[2][8], y[2][8];
+    bn_bwd_g8<T, FL>(in, Y, row, bn_frame<FL>(in, row), c, C, ch, g[0], y[0]);
+    bn_bwd_g8<T, FL>(in, Y, row + 32, bn_frame<FL>(in, row + 32), c, C, ch, g[1], y[1]);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[u][j] = k1[j] * g[u][j] + k2[j] * y[u][j] + k3[j];
+      st8(dY + (row + 32 * u) * C + c, g[u]);
+    }
+  }
+  if (row < re) {
+    float g[8], y[8];
+    bn_bwd_g8<T, FL>(in, Y, row, bn_frame<FL>(in, row), c, C, ch, g, y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = k1[j] * g[j] + k2[j] * y[j] + k3[j];
+    st8(dY + row * C + c, g);
+  }
+}
+
+// 1: launched; 0: not covered (too many stat rows, or C % 8): the caller runs finalize + apply
+template <typename T>
+int launch_bn_bwd_apply_fin(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, const float* stats, int rows,
+                            int64_t count, const float* gamma, const float* mean, const float* invstd, bool training,
+                            float* dgamma, float* dbeta, bool accumulate, float* coef, T* dY) {
+  if (rows < 1 || rows > BAF_ROWS_MAX || (C & 7) || M <= 0) return 0;
+  if (M > (int64_t)UINT32_MAX) { set_error("bn: more than 2^32 rows", __FILE__, __LINE__); return -1; }
+  const int G = cdiv(C, BAF_CH);
+  // >= 128 rows per workgroup (4 per row lane), <= ~2048 workgroups
+  const int64_t rc = std::max<int64_t>(1, std::min<int64_t>(cdiv64(M, 128), std::max(1, 2048 / G)));
+  const int64_t rpw = cdiv64(M, rc);
+  const BnFinArgs fa{count, gamma, mean, invstd, training ? 1 : 0, accumulate ? 1 : 0, dgamma, dbeta, coef};
+  const dim3 grid((unsigned)cdiv64(M, rpw), (unsigned)G);
+  switch (bn_flags(in)) {
+#define DFD_BAF(F) case F: hipLaunchKernelGGL((bn_bwd_apply_fin_kernel<T, F>), grid, dim3(256), 0, s, in, Y, M, C, stats, rows, fa, dY, rpw); break;
+    DFD_BAF(0) DFD_BAF(1) DFD_BAF(2) DFD_BAF(3) DFD_BAF(4) DFD_BAF(5) DFD_BAF(6) DFD_BAF(7)
+    DFD_BAF(8) DFD_BAF(9) DFD_BAF(10) DFD_BAF(11) DFD_BAF(12) DFD_BAF(13) DFD_BAF(14) DFD_BAF(15)
+#undef DFD_BAF
+  }
+  DFD_HIP_CHECK(hipGetLastError());
+  return 1;
 }
 
 // ------------------------------------------------------------------ per-frame channel sums
@@ -961,6 +1102,40 @@ struct SeFin {
   float *dgamma, *dbeta, *coef;
 };
 
+// SPLIT (SeSplit.on): the first product is split over the channel slices too -- the workgroup of
+// slice s sums only k in its own slice (one 16-deep k step per wave instead of C / 256), writes its
+// partial T to scratch, the slices of a frame tile meet at a counter barrier (the grid is launched
+// slice-fastest and only when every workgroup is co-resident, so the spin cannot starve a sibling)
+// and each adds the slices' partials in slice order.  Used where C > 256 (several slices), whose
+// first product was a chain of C / 256 dependent load round trips per wave.
+struct SeSplit {
+  float* tp;      // [frame tiles][slices][16][SE_TS] partial first products
+  unsigned* bar;  // 2 zeroed counters (arrive, depart) per frame tile
+  int on;
+};
+
+// the workgroups sharing `arrive` / `depart` (n of them, all co-resident) wait for each other; the
+// last to leave zeroes both counters for the next launch.  Bounded poll: a grid that could not be
+// co-resident leaves after ~2^24 polls instead of hanging (its outputs are then invalid).
+__device__ __forceinline__ void se_group_sync(unsigned* arrive, unsigned* depart, unsigned n) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n && ++spins < (1u << 24))
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (__hip_atomic_fetch_add(depart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1) {
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(depart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+}
+
+// grid: x = channel slice (fastest), y = 16-frame tile
 template <bool FWD, bool FIN = false>
 __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __restrict__ A, int hsplit, float a_scale,
                                                        const float* __restrict__ a_gate, float* __restrict__ a_out,
@@ -969,18 +1144,20 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
                                                        const float* __restrict__ rpre_in,
                                                        const float* __restrict__ W2, const float* __restrict__ b2,
                                                        float scale2, float* __restrict__ t1_out,
-                                                       float* __restrict__ out, SeFin fin) {
+                                                       float* __restrict__ out, SeFin fin, SeSplit sp) {
   __shared__ float red[SE_W][3][4][64];
   __shared__ float Ts[16][SE_TS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int f0 = blockIdx.x * 16;
+  const int slc = blockIdx.x, nsl = gridDim.x, ftile = blockIdx.y, nft = gridDim.y;
+  const int f0 = ftile * 16;
   const int nt1 = (rd + 15) / 16;
+  const int cbeg = slc * SE_CSL, cend = min(C, cbeg + SE_CSL);
   // FIN: this lane's second-product outputs are column cbeg + 16 wave + li, frames f0 + 4 lk + r; their
   // gate and frame sums P1..P4 (added over the pixel chunks) are loaded up front, off the chain
   float fgt[4], fp[4][4];
   if constexpr (FIN) {
-    const int n = blockIdx.y * SE_CSL + 16 * wave + li;
+    const int n = cbeg + 16 * wave + li;
     const int64_t nfc = (int64_t)frames * C;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1006,11 +1183,14 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc1[t] = se_f32x4{0.f, 0.f, 0.f, 0.f};
   const bool fok = f0 + li < frames;
+  // k range of the first product: this slice's channels (split) or all of them
+  const int kbeg = sp.on ? cbeg : 0, kend = sp.on ? cend : C;
+  const bool store_a = sp.on || slc == 0;  // every A element stored once (sq / de for the weight gradients)
   // 16 k per iteration; lane group lk takes k = k0 + 4 lk + u in MFMA step u (the same
   // permutation on both operands), so the row-major operands load as 16-B vectors (C % 8 == 0)
-  for (int k0 = 16 * wave; k0 < C; k0 += 16 * SE_W) {
+  for (int k0 = kbeg + 16 * wave; k0 < kend; k0 += 16 * SE_W) {
     const int kq = k0 + 4 * lk;
-    const bool kok = kq < C;
+    const bool kok = kq < kend;
     float av[4], bv[4][3];
     if (fok && kok) {
       const int64_t ai = (int64_t)(f0 + li) * C + kq, hn = (int64_t)frames * C;
@@ -1027,7 +1207,7 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
         a4.x = a4.x * g.x * (1.f - g.x); a4.y = a4.y * g.y * (1.f - g.y);
         a4.z = a4.z * g.z * (1.f - g.z); a4.w = a4.w * g.w * (1.f - g.w);
       }
-      if (blockIdx.y == 0) *reinterpret_cast<float4*>(a_out + ai) = a4;
+      if (store_a) *reinterpret_cast<float4*>(a_out + ai) = a4;
       av[0] = a4.x; av[1] = a4.y; av[2] = a4.z; av[3] = a4.w;
     } else {
       av[0] = av[1] = av[2] = av[3] = 0.f;
@@ -1055,33 +1235,44 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wave][t][r][lane] = acc1[t][r];
   __syncthreads();
-  // element (fl, j): MFMA D layout lane = 16 * (fl / 4) + j % 16, register fl % 4, tile j / 16
-  for (int e = tid; e < 16 * SE_TS; e += 64 * SE_W) {
-    const int fl = e / SE_TS, j = e - fl * SE_TS;
-    float tv = 0.f;
-    if (j < rd) {
-      const int t = j >> 4, ln = 16 * (fl >> 2) + (j & 15), r = fl & 3;
-      float v = 0.f;
+  // element (fl, j): MFMA D layout lane = 16 * (fl / 4) + j % 16, register fl % 4, tile j / 16;
+  // 16 x SE_TS < 64 SE_W: one element per thread
+  static_assert(16 * SE_TS <= 64 * SE_W, "one first-product element per thread");
+  const int fl = tid / SE_TS, j = tid - fl * SE_TS;
+  const bool el = tid < 16 * SE_TS && j < rd;
+  float v = 0.f;
+  if (el) {
+    const int t = j >> 4, ln = 16 * (fl >> 2) + (j & 15), r = fl & 3;
 #pragma unroll
-      for (int w = 0; w < SE_W; ++w) v += red[w][t][r][ln];
-      const int f = f0 + fl;
-      if (f < frames) {
-        if constexpr (FWD) {
-          v += b1[j];
-          if (blockIdx.y == 0) t1_out[(int64_t)f * rd + j] = v;
-          tv = siluf_(v);
-        } else {
-          v *= dsiluf_(rpre_in[(int64_t)f * rd + j]);
-          if (blockIdx.y == 0) t1_out[(int64_t)f * rd + j] = v;
-          tv = v;
-        }
+    for (int w = 0; w < SE_W; ++w) v += red[w][t][r][ln];
+  }
+  if (sp.on) {  // the slices' partials of this frame tile, added in slice order
+    float* tp = sp.tp + (int64_t)ftile * nsl * 16 * SE_TS;
+    if (el) tp[slc * 16 * SE_TS + tid] = v;
+    se_group_sync(sp.bar + 2 * ftile, sp.bar + 2 * ftile + 1, (unsigned)nsl);
+    if (el) {
+      v = tp[tid];
+      for (int q = 1; q < nsl; ++q) v += tp[q * 16 * SE_TS + tid];
+    }
+  }
+  if (tid < 16 * SE_TS) {
+    float tv = 0.f;
+    const int f = f0 + fl;
+    if (el && f < frames) {
+      if constexpr (FWD) {
+        v += b1[j];
+        if (slc == 0) t1_out[(int64_t)f * rd + j] = v;
+        tv = siluf_(v);
+      } else {
+        v *= dsiluf_(rpre_in[(int64_t)f * rd + j]);
+        if (slc == 0) t1_out[(int64_t)f * rd + j] = v;
+        tv = v;
       }
     }
     Ts[fl][j] = tv;  // zero for j >= rd and for frames past the end
   }
   __syncthreads();
   // ---- out = T[16][rd] . B2[rd][C slice] ----
-  const int cbeg = blockIdx.y * SE_CSL, cend = min(C, cbeg + SE_CSL);
   for (int n0 = cbeg + 16 * wave; n0 < cend; n0 += 16 * SE_W) {
     const int n = n0 + li;
     const bool nok = n < cend;
@@ -1103,11 +1294,11 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
     for (int r = 0; r < 4; ++r) {
       const int f = f0 + 4 * lk + r;
       if (f < frames && nok) {
-        const float v = FWD ? sigmoidf_(acc[r] + b2[n]) : acc[r] * scale2;
-        out[(int64_t)f * C + n] = v;
+        const float o = FWD ? sigmoidf_(acc[r] + b2[n]) : acc[r] * scale2;
+        out[(int64_t)f * C + n] = o;
         if constexpr (FIN) {
-          fs += (double)fgt[r] * (double)fp[r][0] + (double)v * (double)fp[r][1];
-          fq += (double)fgt[r] * (double)fp[r][2] + (double)v * (double)fp[r][3];
+          fs += (double)fgt[r] * (double)fp[r][0] + (double)o * (double)fp[r][1];
+          fq += (double)fgt[r] * (double)fp[r][2] + (double)o * (double)fp[r][3];
         }
       }
     }
@@ -1118,13 +1309,13 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
       fs += __shfl_xor(fs, 32, 64);
       fq += __shfl_xor(fq, 32, 64);
       if (lk == 0 && nok) {
-        tail_store(fin.rows + ((int64_t)blockIdx.x * 2 + 0) * C + n, fs);
-        tail_store(fin.rows + ((int64_t)blockIdx.x * 2 + 1) * C + n, fq);
+        tail_store(fin.rows + ((int64_t)ftile * 2 + 0) * C + n, fs);
+        tail_store(fin.rows + ((int64_t)ftile * 2 + 1) * C + n, fq);
       }
     }
   }
   if constexpr (FIN) {
-    if (!tail_arrive(fin.ctr + blockIdx.y, gridDim.x)) return;
+    if (!tail_arrive(fin.ctr + slc, nft)) return;
     // last workgroup of this channel slice: frame tiles in order, then bn_bwd_finalize_frames' arithmetic
     const int c = cbeg + tid;
     if (c < cend) {
@@ -1132,7 +1323,7 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
       const float p_db = fin.accumulate ? fin.dbeta[c] : 0.f, p_dg = fin.accumulate ? fin.dgamma[c] : 0.f;
       double s = 0.0, q = 0.0;
       int t = 0;
-      for (; t + 8 <= (int)gridDim.x; t += 8) {  // 16 loads in flight, added in tile order
+      for (; t + 8 <= nft; t += 8) {  // 16 loads in flight, added in tile order
         double vs[8], vq[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -1142,7 +1333,7 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
 #pragma unroll
         for (int u = 0; u < 8; ++u) { s += vs[u]; q += vq[u]; }
       }
-      for (; t < (int)gridDim.x; ++t) {
+      for (; t < nft; ++t) {
         s += tail_load(fin.rows + ((int64_t)t * 2 + 0) * C + c);
         q += tail_load(fin.rows + ((int64_t)t * 2 + 1) * C + c);
       }
@@ -1163,13 +1354,39 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
   }
 }
 
+// CUs of the current device (co-residency bound of the split excitation's barrier)
+static int se_device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// the split form where it applies: several slices, one 1024-thread workgroup per CU fits the whole grid
+static SeSplit se_split(const SeScratch* sc, int frames, int C) {
+  SeSplit sp{};
+  if (!sc || !sc->bar || !sc->tp) return sp;
+  const int64_t nsl = cdiv(C, SE_CSL), nft = cdiv(frames, 16);
+  if (nsl < 2 || nsl * nft > se_device_cus() || 2 * nft > sc->bar_slots || nft * nsl * 16 * SE_TS > sc->tp_cap)
+    return sp;
+  sp.tp = sc->tp;
+  sp.bar = sc->bar;
+  sp.on = 1;
+  return sp;
+}
+
 int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw, float* sq, const float* wr,
                      const float* br, const float* we, const float* be, int frames, int C, int rd, float* rpre,
-                     float* gate) {
+                     float* gate, const SeScratch* sc) {
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
-  const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
+  const dim3 grid((unsigned)cdiv(C, SE_CSL), (unsigned)cdiv(frames, 16));
   hipLaunchKernelGGL(se_chain_kernel<true>, grid, dim3(64 * SE_W), 0, s, part, hsplit, inv_hw, nullptr, sq, frames, C,
-                     rd, wr, br, nullptr, we, be, 1.f, rpre, gate, SeFin{});
+                     rd, wr, br, nullptr, we, be, 1.f, rpre, gate, SeFin{}, se_split(sc, frames, C));
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }
@@ -1182,21 +1399,22 @@ int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw,
 int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
                      const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
                      float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate,
-                     MfmaGemm* defer2, const BnFramesFin* bnf) {
+                     MfmaGemm* defer2, const BnFramesFin* bnf, const SeScratch* sc) {
   if (rd < 1 || rd > SE_RDMAX) { set_error("se: reduce width out of range", __FILE__, __LINE__); return -1; }
-  const dim3 grid((unsigned)cdiv(frames, 16), (unsigned)cdiv(C, SE_CSL));
+  const dim3 grid((unsigned)cdiv(C, SE_CSL), (unsigned)cdiv(frames, 16));
+  const SeSplit sp = se_split(sc, frames, C);
   if (bnf) {
-    if ((int)grid.y > bnf->ctr_slots || (int64_t)grid.x * 2 * C * 2 > bnf->rows_cap) {
+    if ((int)grid.x > bnf->ctr_slots || (int64_t)grid.y * 2 * C * 2 > bnf->rows_cap) {
       set_error("se: fused finalize scratch too small", __FILE__, __LINE__);
       return -1;
     }
     const SeFin f{part, hsplit, bnf->rows, bnf->ctr, bnf->count, bnf->gamma, bnf->mean, bnf->invstd,
                   bnf->training ? 1 : 0, bnf->accumulate ? 1 : 0, bnf->dgamma, bnf->dbeta, bnf->coef};
     hipLaunchKernelGGL((se_chain_kernel<false, true>), grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames,
-                       C, rd, we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out, f);
+                       C, rd, we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out, f, sp);
   } else {
     hipLaunchKernelGGL((se_chain_kernel<false>), grid, dim3(64 * SE_W), 0, s, part, hsplit, 1.f, gate, de, frames, C,
-                       rd, we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out, SeFin{});
+                       rd, we, nullptr, rpre, wr, nullptr, inv_hw, tmp_dz, bc_out, SeFin{}, sp);
   }
   DFD_HIP_CHECK(hipGetLastError());
   MfmaGemm ge{}, gr{};
@@ -1326,8 +1544,11 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
 
 #define DFD_BN_INST(T)                                                                                               \
   template int launch_bn_apply<T>(hipStream_t, const T*, const float*, const float*, const T*, T*, int64_t, int);    \
-  template int launch_bn_bwd_reduce<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, float*, int*);          \
+  template int launch_bn_bwd_reduce<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, float*, int*, int);     \
   template int launch_bn_bwd_apply<T>(hipStream_t, const BnBwdIn&, const T*, const float*, T*, int64_t, int);       \
+  template int launch_bn_bwd_apply_fin<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, const float*, int,  \
+                                          int64_t, const float*, const float*, const float*, bool, float*, float*, \
+                                          bool, float*, T*);                                                        \
   template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, int*, T*); \
   template int launch_se_bwd_reduce<T>(hipStream_t, const T*, const T*, const Pro&, int, int, int, float*, int64_t, \
                                        float*);                                                                     \

@@ -451,8 +451,12 @@ template <typename T> struct WgCfg {
   static constexpr int SMEM = 4 * WAVE_BYTES > WT * WT * 4 ? 4 * WAVE_BYTES : WT * WT * 4;
 };
 
-template <typename T, int MODE>
-__global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 2) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
+// PF: m-steps of global loads in flight per wave (a register ring; the loop is unrolled by PF so
+// every set is a static register array).  PF = 1 issues step i+1's loads before step i's MFMAs;
+// the late-stage shapes (M = 12,544 / 50,176 rows, ~11 steps per workgroup) were ~1.5 us of load
+// latency per step with one step in flight, so PF = 2 keeps two.
+template <typename T, int MODE, int PF = 1>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE) && PF == 1) ? 3 : 2) void pw_wgrad_kernel(const T* __restrict__ dY, const T* __restrict__ X, int64_t M,
                                                        int N, int K, Pro pro, float* __restrict__ slab, int tnk,
                                                        int64_t m_per_split) {
   using G = WgCfg<T>;
@@ -479,18 +483,19 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 
     ld8f(pro.scale + kc, sc);
     ld8f(pro.shift + kc, sh);
   }
-  Raw8<T> ry[4], rx[4];
-  float rg[pro_is_gated(MODE) ? 4 : 1][8];
-  auto load = [&](int64_t ms) {
+  Raw8<T> ry[PF][4], rx[PF][4];
+  float rg[PF][pro_is_gated(MODE) ? 4 : 1][8];
+  auto load = [&](auto pc, int64_t ms) {
+    constexpr int P = decltype(pc)::value;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t gm = ms + rl + 8 * i;
       const bool ok = gm < mend;
-      raw_ld(ry[i], dY + gm * N + n0 + cv, dY, ok && yc);
-      raw_ld(rx[i], X + gm * K + k0 + cv, X, ok && xc);
+      raw_ld(ry[P][i], dY + gm * N + n0 + cv, dY, ok && yc);
+      raw_ld(rx[P][i], X + gm * K + k0 + cv, X, ok && xc);
       if constexpr (pro_is_gated(MODE)) {
         const uint32_t f = (uint32_t)(ok ? gm : mbeg) / (uint32_t)pro.rows_per_frame;
-        ld8f(pro.gate + (int64_t)f * pro.C + kc, rg[i]);
+        ld8f(pro.gate + (int64_t)f * pro.C + kc, rg[P][i]);
       }
     }
   };
@@ -501,24 +506,25 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  int64_t ms = mbeg + wave * WMS;
-  if (ms < mend) load(ms);
-  for (; ms < mend; ms += 4 * WMS) {
+  // one m-step: stage ring slot P (rows from ms) into this wave's LDS region, refill the slot with the
+  // step PF ahead, then the MFMAs of the staged step
+  auto step = [&](auto pc, int64_t ms) {
+    constexpr int P = decltype(pc)::value;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = rl + 8 * i;
-      raw_st(Ys + row * G::LS + cv, ry[i]);
+      raw_st(Ys + row * G::LS + cv, ry[P][i]);
       if constexpr (MODE == PRO_NONE) {
-        raw_st(Xs + row * G::LS + cv, rx[i]);
+        raw_st(Xs + row * G::LS + cv, rx[P][i]);
       } else {
         float x[8];
-        raw_to_f(rx[i], x);
+        raw_to_f(rx[P][i], x);
         if constexpr (MODE == PRO_BN_SILU_G) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * rg[i][j];
+          for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * rg[P][i][j];
         } else if constexpr (MODE == PRO_GATE) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] *= rg[i][j];
+          for (int j = 0; j < 8; ++j) x[j] *= rg[P][i][j];
         } else if constexpr (MODE == PRO_GELU) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] = geluf_(x[j]);
@@ -534,7 +540,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (ms + 4 * WMS < mend) load(ms + 4 * WMS);
+    if (ms + PF * 4 * WMS < mend) load(pc, ms + PF * 4 * WMS);
     if constexpr (sizeof(T) == 2) {
       const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
       bf16x8_t bfr[4];
@@ -574,6 +580,18 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && !pro_is_gated(MODE)) ? 3 : 
       }
     }
     __builtin_amdgcn_wave_barrier();
+  };
+
+  int64_t ms = mbeg + wave * WMS;
+  static_for<PF>([&](auto pc) {
+    constexpr int P = decltype(pc)::value;
+    if (ms + P * 4 * WMS < mend) load(pc, ms + P * 4 * WMS);
+  });
+  for (; ms < mend; ms += PF * 4 * WMS) {
+    static_for<PF>([&](auto pc) {
+      constexpr int P = decltype(pc)::value;
+      if (ms + P * 4 * WMS < mend) step(pc, ms + P * 4 * WMS);
+    });
   }
   // ---- cross-wave reduction of the 64x64 tile, waves added in a fixed order (deterministic) ----
   float* red = reinterpret_cast<float*>(smem);
@@ -621,16 +639,20 @@ int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, in
   int64_t mps = cdiv64(cdiv64(std::max<int64_t>(M, 1), splits), 4 * WMS) * (4 * WMS);
   splits = cdiv64(std::max<int64_t>(M, 1), mps);
   dim3 grid(tiles, (unsigned)splits), block(256);
-  if (pro_mode == PRO_NONE)
-    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_NONE>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
-  else if (pro_mode == PRO_BN_SILU)
-    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
-  else if (pro_mode == PRO_GELU)
-    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_GELU>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
-  else if (pro_mode == PRO_GATE)
-    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_GATE>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
-  else
-    hipLaunchKernelGGL((pw_wgrad_kernel<T, PRO_BN_SILU_G>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);
+  // two m-steps of loads in flight for bf16 (knob wg_pf: 1 or 2; DFD_WG_PF the build default)
+  // (the gated prologues keep one: their per-step gate rows double the ring and spill)
+  const int pf = sizeof(T) == 2 && tune(TK_WG_PF) >= 2 && !pro_is_gated(pro_mode) ? 2 : 1;
+#define DFD_WG_GO(MD)                                                                                           \
+  do {                                                                                                          \
+    if (pf == 2) hipLaunchKernelGGL((pw_wgrad_kernel<T, MD, 2>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps); \
+    else hipLaunchKernelGGL((pw_wgrad_kernel<T, MD, 1>), grid, block, 0, s, dY, X, M, N, K, pro, slab, tnk, mps);       \
+  } while (0)
+  if (pro_mode == PRO_NONE) DFD_WG_GO(PRO_NONE);
+  else if (pro_mode == PRO_BN_SILU) DFD_WG_GO(PRO_BN_SILU);
+  else if (pro_mode == PRO_GELU) DFD_WG_GO(PRO_GELU);
+  else if (pro_mode == PRO_GATE) DFD_WG_GO(PRO_GATE);
+  else DFD_WG_GO(PRO_BN_SILU_G);
+#undef DFD_WG_GO
   DFD_HIP_CHECK(hipGetLastError());
   return launch_reduce_slabs(s, slab, (int)splits, (int64_t)N * K, dW, accumulate);
 }

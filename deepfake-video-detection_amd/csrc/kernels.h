@@ -45,7 +45,7 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 // training step -- therefore never read each other's knobs.
 enum TuneKey { TK_STREAM_MIN_ROWS = 0, TK_FOLD_MIN_ROWS, TK_DW_BWD_FUSED, TK_GEMM_TILE, TK_DW_BWD1, TK_DW_FWD1,
                TK_WGRAD_STREAM, TK_MBCONV7, TK_PWL_FUSED, TK_FOLD_FUSED, TK_PW_SK, TK_DW_PF, TK_DW_RB, TK_STEM_OCC, TK_VG_XP,
-               TK_TAIL_FIN, TK_COUNT };
+               TK_TAIL_FIN, TK_WG_PF, TK_COUNT };
 constexpr int64_t kTuneUnset = INT64_MIN;
 struct Tuning {
   int64_t v[TK_COUNT];
@@ -62,12 +62,18 @@ struct Tuning {
 #define DFD_VG_XP_DEFAULT 1
 #endif
 // tail_fin: BN finalizes in the producers' last-arriving workgroups (tail.h) instead of their own
-// launches (bit 0: the SE-backward chain's BN2 finalize)
+// launches (bit 0: the SE-backward chain's BN2 finalize); bit 1: the SE excitation's first product
+// split over its channel slices (k_bn.hip SeSplit); bit 2: BN backward finalize inside the apply pass
+// (bn_bwd_apply_fin) where the producer wrote <= 256 stat rows
 #ifndef DFD_TAIL_FIN_DEFAULT
-#define DFD_TAIL_FIN_DEFAULT 1
+#define DFD_TAIL_FIN_DEFAULT 7
+#endif
+// wg_pf: m-steps of loads in flight in the tiled 1x1 weight gradient (pw_wgrad_kernel, bf16)
+#ifndef DFD_WG_PF
+#define DFD_WG_PF 1
 #endif
 constexpr int64_t kTuneDefault[TK_COUNT] = {40000, 100000, 1, -1, 1, 1, 0, 0, 1, 1, 1, 1, 1, 3, DFD_VG_XP_DEFAULT,
-                                            DFD_TAIL_FIN_DEFAULT};
+                                            DFD_TAIL_FIN_DEFAULT, DFD_WG_PF};
 extern const char* const kTuneNames[TK_COUNT];
 int64_t tune_override(TuneKey k);  // the calling thread's override, or kTuneUnset
 inline int64_t tune(TuneKey k) {
@@ -277,7 +283,7 @@ struct BnBwdIn {
 };
 template <typename T>
 int launch_bn_bwd_reduce(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, float* stats,
-                         int* stat_rows);
+                         int* stat_rows, int max_rows = 0);  // max_rows > 0: at most that many partial rows
 // phase 2 (finalize): dgamma/dbeta into grads, coefficients k1,k2,k3 for dY = k1*g + k2*y + k3
 int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C,
                            const float* gamma, const float* mean, const float* invstd, bool training,
@@ -287,14 +293,28 @@ int launch_bn_bwd_finalize(hipStream_t s, const float* stats, int rows, int64_t 
 template <typename T>
 int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const float* coef, T* dY, int64_t M,
                         int C);
+// phases 2 + 3 in one launch when the producer wrote <= 256 stat rows (k_bn.hip): dbeta / dgamma (and
+// coef, if non-null) and dY = k1*g + k2*y + k3; 1 launched, 0 not covered (finalize + apply instead)
+template <typename T>
+int launch_bn_bwd_apply_fin(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, const float* stats, int rows,
+                            int64_t count, const float* gamma, const float* mean, const float* invstd, bool training,
+                            float* dgamma, float* dbeta, bool accumulate, float* coef, T* dY);
 // SE squeeze partials: part[h][f][c] = sum over pixel chunk h of pro(Y)   (pro = BN+SiLU), h < *hsplit
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
                       int64_t part_cap, int* hsplit, T* s_out);  // s_out: optional materialised silu(bn(Y))
+// scratch of the split SE excitation (k_bn.hip se_chain_kernel SPLIT): zeroed counters (2 per 16-frame
+// tile) and partial first products; nullptr (or too small) runs the unsplit form
+struct SeScratch {
+  unsigned* bar;
+  int bar_slots;
+  float* tp;
+  int64_t tp_cap;  // floats
+};
 // SE excitation: sq = inv_hw * sum_h part (stored) ; r = silu(Wr sq + br) ; gate = sigmoid(We r + be) ; saves rpre
 int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw, float* sq, const float* wr,
                      const float* br, const float* we, const float* be, int frames, int C, int rd, float* rpre,
-                     float* gate);
+                     float* gate, const SeScratch* sc = nullptr);
 // SE backward reduce: dgate[f][c] = sum_hw dZ * pro(Y)   (pro = BN+SiLU, no gate)
 template <typename T>
 int launch_se_bwd_reduce(hipStream_t s, const T* dZ, const T* Y, const Pro& pro, int frames, int HW, int C,
@@ -321,7 +341,7 @@ struct BnFramesFin {
 int launch_se_fc_bwd(hipStream_t s, const float* part, int hsplit, const float* gate, float* de, const float* sq,
                      const float* rpre, const float* wr, const float* we, int frames, int C, int rd, float inv_hw,
                      float* tmp_dz, float* bc_out, float* gwr, float* gbr, float* gwe, float* gbe, bool accumulate,
-                     MfmaGemm* defer2 = nullptr, const BnFramesFin* bnf = nullptr);
+                     MfmaGemm* defer2 = nullptr, const BnFramesFin* bnf = nullptr, const SeScratch* sc = nullptr);
 // SE + BN(+SiLU) backward sums in one pass over (dZ, Y): per-frame partials part[5][hsplit][frames][C] -- q = 0
 // the SE gate gradient (added by launch_se_fc_bwd), q = 1..4 the sums bn_bwd_finalize_frames combines with the
 // gate and bc (k_bn.hip)

@@ -226,6 +226,10 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.o_gram = alloc(maxCin * maxCin * 4);
   p.o_cs = alloc(maxCin * 4);
   p.o_bar = alloc(kBarBytes);
+  // last-arrival / slice-barrier counters (tail.h, k_bn.hip se_chain): in the per-call workspace, so
+  // concurrent calls of one plan on different streams (the app's worker threads) never share them;
+  // zeroed at the start of every forward, and every use leaves them zero again
+  p.o_ctr = alloc(kCtrSlots * sizeof(unsigned));
   p.ws_bytes = cur;
   p.offs.assign(p.tensors.size(), -1);
   p.bound = false;
@@ -245,10 +249,7 @@ int plan_bind(Plan& p, const int64_t* offs, int n) {
   for (const Block& b : p.blocks) { if (!b.ds) seg(b.pw); seg(b.pwl); }
   seg(p.head);
   if (!p.cast_dev) DFD_HIP_CHECK(hipMalloc(&p.cast_dev, p.cast_host.size() * sizeof(CastSeg)));
-  if (!p.ctr_dev) {  // last-arrival counters (tail.h): zero at rest, every use resets its own
-    DFD_HIP_CHECK(hipMalloc(&p.ctr_dev, kCtrSlots * sizeof(unsigned)));
-    DFD_HIP_CHECK(hipMemset(p.ctr_dev, 0, kCtrSlots * sizeof(unsigned)));
-  }
+
   DFD_HIP_CHECK(hipMemcpy(p.cast_dev, p.cast_host.data(), p.cast_host.size() * sizeof(CastSeg), hipMemcpyHostToDevice));
   p.bound = true;
   return 0;
@@ -315,7 +316,7 @@ void plan_free(Plan& p) {
   probe_disarm(p);
   aux_free(p);
   if (p.cast_dev) { (void)hipFree(p.cast_dev); p.cast_dev = nullptr; }
-  if (p.ctr_dev) { (void)hipFree(p.ctr_dev); p.ctr_dev = nullptr; }
+
 }
 
 // ------------------------------------------------------------------ forward / backward
@@ -409,6 +410,8 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
                               bnb + p.offs[b.t_rv], mom, eps, tr != 0, r.f(b.o_mean), r.f(b.o_invstd), r.f(b.o_scale),
                               r.f(b.o_shift));
   };
+  DFD_HIP_CHECK(hipMemsetAsync(ws + p.o_ctr, 0, kCtrSlots * sizeof(unsigned), s));
+  unsigned* const ctr = reinterpret_cast<unsigned*>(ws + p.o_ctr);
   DFD_TRY(launch_cast_params<T>(s, P, reinterpret_cast<T*>(ws), p.cast_dev, (int)p.cast_host.size(), p.cast_max));
   const int64_t F = p.frames;
   StemGeom sg{p.frames, p.H, p.W, p.H1, p.W1, xs[0], xs[1], xs[2], xs[3], stem_fmt(in, x, xs)};
@@ -464,9 +467,12 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
     int hs = 1;
     PROBED(PK_SE_SQUEEZE, &b, (launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
                                                     r.f(p.o_part), p.part_cap, &hs, s2)));
+    // the excitation's first product split over its channel slices (knob tail_fin bit 1); o_stats is free
+    // between the BN2 finalize and the projection's BN3 statistics
+    const SeScratch sesc{ctr + kCtrSe, kCtrSlots - kCtrSe, r.f(p.o_stats), p.stats_cap};
     DFD_TRY(launch_se_fc_fwd(s, r.f(p.o_part), hs, 1.0f / (float)hwo, r.f(b.o_sq), r.prm(b.t_se_wr),
                              r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be), p.frames, b.mid, b.rd,
-                             r.f(b.o_rpre), r.f(b.o_gate)));
+                             r.f(b.o_rpre), r.f(b.o_gate), (tune(TK_TAIL_FIN) & 2) ? &sesc : nullptr));
     PROBED(PK_PWL_FWD, &b, (launch_pw_gemm<T>(s, s2 ? s2 : r.a(b.o_y2), r.a(b.pwl.o_w), r.a(b.o_y3), nullptr, Mout,
                                               b.cout, b.mid, s2 ? PRO_GATE : PRO_BN_SILU_G,
                                               r.pro_bn(bn_dw, hwo, r.f(b.o_gate)), stats, &rows)));
@@ -502,22 +508,35 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
   Run<T> r{p, s, ws, P, tr};
   int rows = 0;
   const int64_t F = p.frames;
+  unsigned* const ctr = reinterpret_cast<unsigned*>(ws + p.o_ctr);  // zeroed by the forward (see plan_build)
   auto grad = [&](int t) { return G + p.offs[t]; };
-  auto bwd_bn = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out) {
-    in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
-    DFD_TRY(launch_bn_bwd_reduce<T>(s, in, Y, M, b.C, r.f(p.o_stats), &rows));
-    DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), rows, M, b.C, r.prm(b.t_w), r.f(b.o_mean), r.f(b.o_invstd),
-                                   tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
-    DFD_TRY(launch_bn_bwd_apply<T>(s, in, Y, r.f(p.o_coef), out, M, b.C));
-    return 0;
-  };
-  // BN backward when the partials of g, g*xhat are already in o_stats (written by a fused producer)
-  auto bwd_bn_from_stats = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out, int nrows) {
-    in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
+  // BN backward finalize + apply: one launch (bn_bwd_apply_fin, knob tail_fin bit 2) when the stat rows are
+  // few enough for every apply workgroup to reduce its channels' rows itself, else the two launches
+  const bool apply_fin = (tune(TK_TAIL_FIN) & 4) != 0;
+  auto fin_apply = [&](const BnBwdIn& in, const BNL& b, const T* Y, int64_t M, T* out, int nrows) {
+    int rc = 0;
+    if (apply_fin)
+      rc = launch_bn_bwd_apply_fin<T>(s, in, Y, M, b.C, r.f(p.o_stats), nrows, M, r.prm(b.t_w), r.f(b.o_mean),
+                                      r.f(b.o_invstd), tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef), out);
+    if (rc < 0) return -1;
+    if (rc == 1) return 0;
     DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), nrows, M, b.C, r.prm(b.t_w), r.f(b.o_mean), r.f(b.o_invstd),
                                    tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
     DFD_TRY(launch_bn_bwd_apply<T>(s, in, Y, r.f(p.o_coef), out, M, b.C));
     return 0;
+  };
+  auto bwd_bn = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out) {
+    in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
+    // the fused finalize + apply reads <= 256 stat rows: the reduction takes that cap on the smaller
+    // (late-stage) tensors, where its workgroups still cover the rows in a few passes
+    const int cap = apply_fin && M * b.C <= ((int64_t)16 << 20) ? 256 : 0;
+    DFD_TRY(launch_bn_bwd_reduce<T>(s, in, Y, M, b.C, r.f(p.o_stats), &rows, cap));
+    return fin_apply(in, b, Y, M, out, rows);
+  };
+  // BN backward when the partials of g, g*xhat are already in o_stats (written by a fused producer)
+  auto bwd_bn_from_stats = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out, int nrows) {
+    in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
+    return fin_apply(in, b, Y, M, out, nrows);
   };
   const int nb = (int)p.blocks.size();
   // the gradient buffer's extent: slab reductions into it are deferred (one launch per segment)
@@ -681,13 +700,17 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         // the BN2 backward finalize (dbeta, dgamma, k1..k3 from gate, bc and the frame sums) in the
         // excitation launch's last workgroups (knob tail_fin bit 0), o_stats free as row scratch here
         const bool sefin = (tune(TK_TAIL_FIN) & 1) != 0;
-        const BnFramesFin bnf{reinterpret_cast<double*>(r.f(p.o_stats)), p.stats_cap, p.ctr_dev, kCtrSlots, Mout,
+        // the split excitation's partial products behind the finalize rows in o_stats
+        const SeScratch sesc{ctr + kCtrSe, kCtrSlots - kCtrSe, r.f(p.o_stats) + p.stats_cap / 2,
+                             p.stats_cap / 2};
+        const BnFramesFin bnf{reinterpret_cast<double*>(r.f(p.o_stats)), p.stats_cap, ctr, kCtrSe, Mout,
                               r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), tr != 0, acc != 0,
                               grad(bn_dw.t_w), grad(bn_dw.t_b), r.f(p.o_coef)};
         DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(b.o_de), r.f(b.o_sq), r.f(b.o_rpre),
                                  r.prm(b.t_se_wr), r.prm(b.t_se_we), p.frames, b.mid, b.rd, 1.0f / (float)hwo,
                                  r.f(b.o_dz), r.f(p.o_bc), grad(b.t_se_wr), grad(b.t_se_br), grad(b.t_se_we),
-                                 grad(b.t_se_be), acc != 0, se_jobs + n_se, sefin ? &bnf : nullptr));
+                                 grad(b.t_se_be), acc != 0, se_jobs + n_se, sefin ? &bnf : nullptr,
+                                 (tune(TK_TAIL_FIN) & 2) ? &sesc : nullptr));
         n_se += 2;
         if (!sefin)
           DFD_TRY(launch_bn_bwd_finalize_frames(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(p.o_bc), p.frames, b.mid,
@@ -854,7 +877,7 @@ int plan_fused7_blocks(const Plan& p) {
 
 const char* const kTuneNames[TK_COUNT] = {"stream_min_rows", "fold_min_rows", "dw_bwd_fused", "gemm_tile", "dw_bwd1",
                                           "dw_fwd1", "wgrad_stream", "mbconv7", "pwl_fused", "fold_fused", "pw_sk", "dw_pf", "dw_rb", "stem_occ", "vg_xp",
-                                          "tail_fin"};
+                                          "tail_fin", "wg_pf"};
 static thread_local const Tuning* t_tune = nullptr;
 int64_t tune_override(TuneKey k) { return t_tune ? t_tune->v[k] : kTuneUnset; }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tune) { t_tune = t; }

@@ -54,6 +54,7 @@ struct Probe {
 };
 
 constexpr int kCtrSlots = 1024;
+constexpr int kCtrSe = 64;  // counters [0, kCtrSe): last-arrival tails; [kCtrSe, kCtrSlots): SE slice barriers
 
 struct Plan {
   int frames, H, W, dtype;
@@ -72,11 +73,11 @@ struct Plan {
   int64_t o_w1t, o_q, o_bv, o_tg, o_gram, o_cs;  // conv_pw backward through its BN (bn_fold_pw)
   int64_t o_coef1, o_stats2;  // BN1 backward coefficients / col_sums partials read on the wgrad stream
   int64_t o_bar;  // grid-barrier counters + abort flag of the fused 7x7 MBConv launches (zeroed per forward)
+  int64_t o_ctr;  // kCtrSlots last-arrival / SE slice-barrier counters (zeroed per forward)
   int64_t stats_cap, slab_cap, part_cap;
   // cast table (device copy)
   std::vector<CastSeg> cast_host;
   CastSeg* cast_dev = nullptr;
-  unsigned* ctr_dev = nullptr;  // last-arrival counters (tail.h), kCtrSlots, zero at rest
   int cast_max = 0;
   int device = 0;
   int pending_rows = 0;  // stat rows written by the stage-0 dw dgrad, consumed by the stem segment

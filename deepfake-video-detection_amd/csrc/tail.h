@@ -5,8 +5,8 @@
 // partial row with plain stores, drains them, meets at the workgroup barrier; thread 0 publishes
 // with an agent-scope release (this XCD's L2 written back) and takes a ticket with an agent-scope
 // atomic.  The workgroup drawing the last ticket acquires (agent scope: stale lines of its CU and
-// L2 invalidated), resets the counter to zero for the next launch (counters are zero at rest: the
-// plan zeroes them once when it allocates them), and alone reads every partial row in a fixed order
+// L2 invalidated), resets the counter to zero for the next launch (counters are zero at rest: they live
+// in the per-call workspace, zeroed at the start of each forward), and alone reads every partial row in a fixed order
 // -- so the result does not depend on which workgroup arrives last (bit-reproducible).  Nobody
 // waits: the other workgroups leave, so the grid need not be co-resident.
 #pragma once

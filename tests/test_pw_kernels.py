@@ -165,7 +165,7 @@ def test_pw_conv_rejects_bad_args(cuda):
                            ctypes.byref(rows)) == -1
 
 
-def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate=False):
+def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate=False, wg_pf=None):
     """dW[N][K] = sum_m dY[m][n] * pro(X)[m][k] (conv_pw / conv_pwl weight gradient)."""
     lib = _lib_()
     g = torch.Generator(device=dev)
@@ -176,6 +176,7 @@ def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate
     dw0 = dw.clone()
     slab = torch.empty(8 << 20, device=dev)
     prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
+    prev_pf = lib.dfd_set_tuning(b"wg_pf", wg_pf) if wg_pf is not None else None
     try:
         _lib.check(lib.dfd_pw_conv_wgrad(_lib.stream_of(dev), 1, dy.data_ptr(), x.data_ptr(), M, N, K, mode,
                                          scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf, slab.data_ptr(),
@@ -183,6 +184,8 @@ def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate
         torch.cuda.synchronize()
     finally:
         lib.dfd_set_tuning(b"stream_min_rows", prev)
+        if prev_pf is not None:
+            lib.dfd_set_tuning(b"wg_pf", prev_pf)
     xp = _pro(x, mode, scale, shift, gate, rpf).to(torch.bfloat16).double()
     ref = dy.double().t() @ xp
     if accumulate:
@@ -220,3 +223,15 @@ def test_pw_conv_wgrad_gate_bf16(cuda, case):
 def test_pw_conv_wgrad_accumulate(cuda):
     _run_wgrad(50021, 24, 96, 2, 0, cuda, accumulate=True)
     _run_wgrad(12544, 192, 1152, 2, 0, cuda, rpf=49, accumulate=True)
+
+
+@pytest.mark.parametrize("case", [(12544, 1152, 192, 0), (50176, 672, 112, 0), (12544, 1152, 320, 0), (3001, 96, 40, 0),
+                                  (12544, 1152, 192, 1), (777, 64, 48, 0)],
+                         ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("wg_pf", [1, 2])
+def test_pw_conv_wgrad_tiled_ring(cuda, case, wg_pf):
+    """the tiled weight gradient with one / two m-steps of loads in flight (knob wg_pf): the late-stage
+    conv_pw shapes (12,544 / 50,176 rows), ragged row counts (the last ring slot of a split partly or
+    wholly past the end) and a split shorter than the ring"""
+    M, N, K, mode = case
+    _run_wgrad(M, N, K, mode, 1 << 60, cuda, rpf=49, wg_pf=wg_pf)
