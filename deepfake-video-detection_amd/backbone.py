@@ -322,11 +322,18 @@ class _TrunkFn(torch.autograd.Function):
         dfeat = dfeat.contiguous().float()
         rt = trunk.runtime()
         nseg = len(trunk._seg_ranges)
-        for s in range(nseg):
-            rt.backward(ctx.h, ctx.ws, x, dfeat, owner, grads, ctx.training, s, s + 1)
-            lo, hi = trunk._seg_ranges[s]
-            if hi > lo:
-                ctx.sink.ready(lo, hi)
+        if getattr(owner, "_grad_ready_hooks", ()):
+            # segment by segment: each segment's gradients are final when its call returns, so the
+            # hooks (the data-parallel all-reduce buckets) can start while the rest of backward runs
+            for s in range(nseg):
+                rt.backward(ctx.h, ctx.ws, x, dfeat, owner, grads, ctx.training, s, s + 1)
+                lo, hi = trunk._seg_ranges[s]
+                if hi > lo:
+                    ctx.sink.ready(lo, hi)
+        else:
+            # nobody waits for a segment: one call, the weight-gradient slab reductions and SE weight
+            # gradients batched across segments (fewer launches)
+            rt.backward(ctx.h, ctx.ws, x, dfeat, owner, grads, ctx.training, 0, nseg)
         ctx.ws = None
         views = ctx.sink.views(trunk._param_names)
         return (None, None, None, None, None, *views)

@@ -162,6 +162,11 @@ int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t coun
   return 0;
 }
 
+int launch_bn_finalize_fin(hipStream_t s, const BnFwdFin& f, int C) {
+  return launch_bn_finalize(s, f.stats, f.rows, f.count, C, f.gamma, f.beta, f.run_mean, f.run_var, f.momentum, f.eps,
+                            true, f.mean, f.invstd, f.scale, f.shift);
+}
+
 // Eval mode: every BatchNorm of a plan from its running statistics in ONE launch (workgroup = layer):
 // the same operations as bn_finalize_kernel's eval branch; one ~5 us launch instead of 49 per forward
 __global__ __launch_bounds__(256) void bn_eval_all_kernel(const float* __restrict__ P, const float* __restrict__ bnb,
@@ -484,6 +489,7 @@ int launch_bn_bwd_apply(hipStream_t s, const BnBwdIn& in, const T* Y, const floa
 // coef, then it applies dY = k1*g + k2*y + k3 over its rows.  Saves the ~5 us finalize launch per BN
 // backward; the reduction costs each workgroup rows / 16 x 2 loads per thread (used for rows <= 256).
 constexpr int BAF_CH = 64, BAF_RL = 16, BAF_ROWS_MAX = 256;
+constexpr int64_t BAF_M_MAX = 16384;
 struct BnFinArgs {
   int64_t count;
   const float *gamma, *mean, *invstd;
@@ -597,7 +603,10 @@ template <typename T>
 int launch_bn_bwd_apply_fin(hipStream_t s, const BnBwdIn& in, const T* Y, int64_t M, int C, const float* stats, int rows,
                             int64_t count, const float* gamma, const float* mean, const float* invstd, bool training,
                             float* dgamma, float* dbeta, bool accumulate, float* coef, T* dY) {
-  if (rows < 1 || rows > BAF_ROWS_MAX || (C & 7) || M <= 0) return 0;
+  // the small late-stage tensors only: at 50,176 rows x 480-672 channels the fused pass measured
+  // 45 us against 30 + 5 us for apply + finalize (trace r05 C) -- its channel-group-major grid streams
+  // worse than the channel-stationary apply, which the saved launch repays only on short passes
+  if (rows < 1 || rows > BAF_ROWS_MAX || (C & 7) || M <= 0 || M > BAF_M_MAX) return 0;
   if (M > (int64_t)UINT32_MAX) { set_error("bn: more than 2^32 rows", __FILE__, __LINE__); return -1; }
   const int G = cdiv(C, BAF_CH);
   // >= 128 rows per workgroup (4 per row lane), <= ~2048 workgroups
@@ -637,17 +646,28 @@ struct FrCoef {
   const float *scale, *shift, *mean, *invstd;
 };
 
-template <typename T, int OP>
+// FIN (squeeze only): the BN's train-mode finalize from its producer's stat rows inside the launch
+// (bnfin.h): every workgroup reduces the rows of its channel slice; blockIdx.x == 0 stores the
+// constants and the running statistics
+template <typename T, int OP, bool FIN = false>
 __global__ __launch_bounds__(256) void frame_reduce_kernel(const T* __restrict__ dZ, const T* __restrict__ Y, FrCoef cf,
-                                                           FrGeom g, float* __restrict__ part, T* __restrict__ s_out) {
+                                                           FrGeom g, float* __restrict__ part, T* __restrict__ s_out,
+                                                           BnFwdFin fin) {
   constexpr int Q = OP == FR_SEBN ? 5 : 1;
   constexpr int FR_U = OP == FR_SEBN ? 2 : 4;  // the five FR_SEBN sums: 2 pixels in flight (occupancy)
   __shared__ float sh[Q][256][8];
+  __shared__ double fscr[FIN ? kBnFinScratch : 1];
+  __shared__ float fss[2][FIN ? 128 : 1];
   const int tid = threadIdx.x;
   const int vec = tid % g.vpg, l = tid / g.vpg;
   const int fi = l / g.pl, li = l - fi * g.pl;
   const int f = (blockIdx.x / g.hsplit) * g.fpb + fi, h = blockIdx.x % g.hsplit;
   const int c = (blockIdx.y * g.vpg + vec) * 8;
+  const int cw0 = blockIdx.y * g.vpg * 8;  // this workgroup's channel slice
+  if constexpr (FIN) {
+    const int ncw = g.C - cw0 < g.vpg * 8 ? g.C - cw0 : g.vpg * 8;
+    bn_fin_wg(fin, g.C, cw0, ncw, blockIdx.x == 0, fss[0], fss[1], fscr);
+  }
   const bool act = fi < g.fpb && f < g.frames && c < g.C;
   const int chunk = (g.HW + g.hsplit - 1) / g.hsplit;
   const int p0 = h * chunk, p1 = min(g.HW, p0 + chunk);
@@ -658,8 +678,13 @@ __global__ __launch_bounds__(256) void frame_reduce_kernel(const T* __restrict__
     for (int j = 0; j < 8; ++j) acc[q][j] = 0.f;
   if (act) {
     float sc[8], shf[8], mu[8], is[8];
-    ld8f(cf.scale + c, sc);
-    ld8f(cf.shift + c, shf);
+    if constexpr (FIN) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sc[j] = fss[0][c - cw0 + j]; shf[j] = fss[1][c - cw0 + j]; }
+    } else {
+      ld8f(cf.scale + c, sc);
+      ld8f(cf.shift + c, shf);
+    }
     if constexpr (OP == FR_SEBN) {
       ld8f(cf.mean + c, mu);
       ld8f(cf.invstd + c, is);
@@ -733,7 +758,8 @@ __global__ __launch_bounds__(256) void frame_reduce_kernel(const T* __restrict__
 
 template <typename T, int OP>
 static int launch_frame_reduce(hipStream_t s, const T* dZ, const T* Y, const FrCoef& cf, int frames, int HW, int C,
-                               float* part, int64_t part_cap, int* hsplit_out, T* s_out = nullptr) {
+                               float* part, int64_t part_cap, int* hsplit_out, T* s_out = nullptr,
+                               const BnFwdFin* fin = nullptr) {
   constexpr int Q = OP == FR_SEBN ? 5 : 1;
   if (frames <= 0 || HW <= 0) { set_error("frame reduce: empty input", __FILE__, __LINE__); return -1; }
   if ((int64_t)Q * frames * C > part_cap) { set_error("frame reduce: partial buffer too small", __FILE__, __LINE__); return -1; }
@@ -747,8 +773,21 @@ static int launch_frame_reduce(hipStream_t s, const T* dZ, const T* Y, const FrC
   while ((int64_t)fgroups * groups * g.hsplit < 1024 && HW / (g.hsplit * 2) >= g.pl * 8 &&
          (int64_t)Q * (g.hsplit * 2) * frames * C <= part_cap)
     g.hsplit *= 2;
-  hipLaunchKernelGGL((frame_reduce_kernel<T, OP>), dim3(fgroups * g.hsplit, groups), dim3(256), 0, s, dZ, Y, cf, g,
-                     part, s_out);
+  // the input BN's finalize: inside the launch where its stat rows are few (squeeze; channel slices of
+  // <= 128), else its own launch first (cf.scale / cf.shift are that launch's outputs)
+  const bool embed = OP == FR_SQUEEZE && fin && fin->rows > 0 && fin->rows <= kBnFinRowsMax && g.vpg * 8 <= 128;
+  if (fin && fin->rows > 0 && !embed) DFD_TRY(launch_bn_finalize_fin(s, *fin, C));
+  if constexpr (OP == FR_SQUEEZE) {
+    if (embed) {
+      hipLaunchKernelGGL((frame_reduce_kernel<T, OP, true>), dim3(fgroups * g.hsplit, groups), dim3(256), 0, s, dZ, Y,
+                         cf, g, part, s_out, *fin);
+      DFD_HIP_CHECK(hipGetLastError());
+      *hsplit_out = g.hsplit;
+      return 0;
+    }
+  }
+    hipLaunchKernelGGL((frame_reduce_kernel<T, OP>), dim3(fgroups * g.hsplit, groups), dim3(256), 0, s, dZ, Y, cf, g,
+                       part, s_out, BnFwdFin{});
   DFD_HIP_CHECK(hipGetLastError());
   *hsplit_out = g.hsplit;
   return 0;
@@ -776,9 +815,9 @@ __global__ void sum_parts_kernel(const float* __restrict__ part, int hsplit, int
 // adds the partials and scales by 1/HW while loading them
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
-                      int64_t part_cap, int* hsplit, T* s_out) {
+                      int64_t part_cap, int* hsplit, T* s_out, const BnFwdFin* fin) {
   const FrCoef cf{pro.scale, pro.shift, nullptr, nullptr};
-  return launch_frame_reduce<T, FR_SQUEEZE>(s, nullptr, Y, cf, frames, HW, C, part, part_cap, hsplit, s_out);
+  return launch_frame_reduce<T, FR_SQUEEZE>(s, nullptr, Y, cf, frames, HW, C, part, part_cap, hsplit, s_out, fin);
 }
 
 template <typename T>
@@ -1057,12 +1096,14 @@ int launch_col_sums(hipStream_t s, const T* X, int64_t M, int C, float* part, in
 }
 
 template <typename T>
-int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat) {
+int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat, const BnFwdFin* fin) {
   // HW is tiny (7x7 at 224^2): one partial per frame (the partial buffer is feat itself, so
   // hsplit = 1), then the means in place
   const FrCoef cf{pro.scale, pro.shift, nullptr, nullptr};
   int hs = 1;
-  if (launch_frame_reduce<T, FR_SQUEEZE>(s, nullptr, Y, cf, frames, HW, C, feat, (int64_t)frames * C, &hs)) return -1;
+  if (launch_frame_reduce<T, FR_SQUEEZE>(s, nullptr, Y, cf, frames, HW, C, feat, (int64_t)frames * C, &hs, nullptr,
+                                         fin))
+    return -1;
   const int64_t n = (int64_t)frames * C;
   hipLaunchKernelGGL(sum_parts_kernel, dim3(ew_grid(n)), dim3(256), 0, s, feat, 1, n, 1.0f / (float)HW, feat);
   DFD_HIP_CHECK(hipGetLastError());
@@ -1372,7 +1413,10 @@ static SeSplit se_split(const SeScratch* sc, int frames, int C) {
   SeSplit sp{};
   if (!sc || !sc->bar || !sc->tp) return sp;
   const int64_t nsl = cdiv(C, SE_CSL), nft = cdiv(frames, 16);
-  if (nsl < 2 || nsl * nft > se_device_cus() || 2 * nft > sc->bar_slots || nft * nsl * 16 * SE_TS > sc->tp_cap)
+  // >= 4 slices (C > 768): the slice barrier costs ~3-4 us, which the split repays only where the
+  // unsplit first product walks >= 4 dependent k steps per wave (trace r05 C: 7x7 stage -2 us per
+  // launch, 14x14 stage +0.5..2 us)
+  if (nsl < 4 || nsl * nft > se_device_cus() || 2 * nft > sc->bar_slots || nft * nsl * 16 * SE_TS > sc->tp_cap)
     return sp;
   sp.tp = sc->tp;
   sp.bar = sc->bar;
@@ -1549,10 +1593,11 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
   template int launch_bn_bwd_apply_fin<T>(hipStream_t, const BnBwdIn&, const T*, int64_t, int, const float*, int,  \
                                           int64_t, const float*, const float*, const float*, bool, float*, float*, \
                                           bool, float*, T*);                                                        \
-  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, int*, T*); \
+  template int launch_se_squeeze<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, int64_t, int*, T*,   \
+                                    const BnFwdFin*);                                                               \
   template int launch_se_bwd_reduce<T>(hipStream_t, const T*, const T*, const Pro&, int, int, int, float*, int64_t, \
                                        float*);                                                                     \
-  template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*);                            \
+  template int launch_gap<T>(hipStream_t, const T*, const Pro&, int, int, int, float*, const BnFwdFin*);          \
   template int launch_se_bn_bwd_reduce<T>(hipStream_t, const T*, const T*, const float*, const float*, const float*, \
                                           const float*, int, int, int, float*, int64_t, int*);                 \
   template int launch_bn_fold_pw<T>(hipStream_t, const float*, const float*, int, int, T*, T*, float*);             \

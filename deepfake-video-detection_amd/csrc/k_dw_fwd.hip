@@ -165,13 +165,19 @@ static int fwd_ks(hipStream_t s, const DwGeom& g, const T* X, const float* w, T*
 
 template <typename T>
 int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, int pro_mode,
-                  float* stats, int* stat_rows) {
+                  float* stats, int* stat_rows, const BnFwdFin* fin) {
   if (g.C & 7) { set_error("dw: C must be a multiple of 8", __FILE__, __LINE__); return -1; }
   if (pro_mode != PRO_BN_SILU) { set_error("dw fwd: input must be a BN+SiLU producer", __FILE__, __LINE__); return -1; }
+  // the input BN's finalize inside the channel-pair kernel where it applies (few stat rows), else its
+  // own launch first (pro.scale / pro.shift are that launch's outputs)
+  const bool embed = fin && fin->rows > 0 && fin->rows <= kBnFinRowsMax;
+  if (fin && fin->rows > 0 && !embed) DFD_TRY(launch_bn_finalize_fin(s, *fin, g.C));
   {
-    const int rc = try_dw_fwd1<T>(s, g, X, w, Y, pro, stats, stat_rows);
-    if (rc != 0) return rc > 0 ? 0 : -1;
+    const int rc = try_dw_fwd1<T>(s, g, X, w, Y, pro, stats, stat_rows, embed ? fin : nullptr);
+    if (rc < 0) return -1;
+    if (rc > 0) return 0;
   }
+  if (embed) DFD_TRY(launch_bn_finalize_fin(s, *fin, g.C));  // the channel-pair kernel does not cover this shape
   if (g.s == 1 && dw_strip_enabled()) {
     const int rc = try_dw_fwd_strip<T>(s, g, X, w, Y, pro, stats, stat_rows);
     if (rc != 0) return rc > 0 ? 0 : -1;
@@ -185,8 +191,8 @@ int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T*
 }
 
 template int launch_dw_fwd<float>(hipStream_t, const DwGeom&, const float*, const float*, float*, const Pro&, int,
-                                  float*, int*);
+                                  float*, int*, const BnFwdFin*);
 template int launch_dw_fwd<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, int,
-                                 float*, int*);
+                                 float*, int*, const BnFwdFin*);
 
 }  // namespace dfd

@@ -10,6 +10,7 @@
 // 8x28 (k3, 112/56 maps), 14x14 (28/14 maps), two stacked 7x7 frames.  Replaces the 8-channel
 // strip / tile kernels on these shapes (VALU-issue bound: fewer instructions per output).
 #include "dw1_common.h"
+#include "bnfin.h"
 
 #ifndef DFD_FWD1_PF
 #define DFD_FWD1_PF 0  // next-tile register prefetch of the staged window (A/B knob)
@@ -45,8 +46,9 @@ struct Dwf1 {
 template <typename T, int K, int TH, int TW, int RS, int FR, int S, int RB>
 __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fwd1_kernel(
     DwGeom g, const T* __restrict__ Y1, const float* __restrict__ w, Pro bn1, T* __restrict__ out,
-    float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y, int xcd) {
+    float* __restrict__ stats, int ntiles, int groups, int tiles_x, int tiles_y, int xcd, BnFwdFin fin) {
   using D = Dwf1<T, K, TH, TW, RS, FR, S, RB>;
+  static_assert(D::AB >= kBnFinScratch * 8, "the staging area holds the BN1 finalize scratch");
   __shared__ __attribute__((aligned(16))) char araw[D::AB];        // staged activations; reduction scratch
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];  // [tap][ch]
   __shared__ __attribute__((aligned(16))) float cst[2][DCG];       // BN1 scale, shift
@@ -59,8 +61,13 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
     const int tap = i / DCG, cl = i - tap * DCG;
     wts[i] = (c0 + cl < C) ? w[(int64_t)(c0 + cl) * K * K + tap] : 0.f;
   }
+  // BN1 scale / shift: finalized here from the producer's stat rows (bnfin.h; the first workgroup of
+  // the channel group stores them and the running statistics), or read from the finalize launch's output
+  const int nc = C - c0 < DCG ? C - c0 : DCG;
+  if (fin.rows > 0) bn_fin_wg(fin, C, c0, nc, bid / groups == 0, cst[0], cst[1], reinterpret_cast<double*>(araw));
   for (int i = tid; i < 2 * DCG; i += 256) {
     const int k = i / DCG, cl = i - k * DCG, c = c0 + cl;
+    if (fin.rows > 0 && cl < nc) continue;
     cst[k][cl] = c < C ? (k ? bn1.shift[c] : bn1.scale[c]) : (k ? 0.f : 1.f);
   }
   const int tpf = tiles_x * tiles_y;
@@ -246,7 +253,7 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && S == 1) ? 3 : 2) void dw_fw
 
 template <typename T, int K, int TH, int TW, int RS, int FR = 1, int S = 1, int RB = 1>
 static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
-                       int* stat_rows) {
+                       int* stat_rows, const BnFwdFin* fin) {
   const int tiles_x = cdiv(g.Wo, TW), tiles_y = cdiv(g.Ho, TH);
   if (FR > 1 && (tiles_x != 1 || tiles_y != 1)) { set_error("dw_fwd1: frame stacking needs whole-map tiles", __FILE__, __LINE__); return -1; }
   const int ntiles = cdiv(g.frames, FR) * tiles_x * tiles_y;
@@ -258,7 +265,7 @@ static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* 
   // 14x14 k5 c672 (+7 %), stacked 7x7 (+7..12 %) and single-group layers keep dispatch order
   const int xcd = DFD_DW_XCD >= 0 ? DFD_DW_XCD : (groups > 1 && (g.Ho >= 28 || (g.Ho == 14 && g.C <= 480)));
   hipLaunchKernelGGL((dw_fwd1_kernel<T, K, TH, TW, RS, FR, S, RB>), dim3((unsigned)(rows * groups)), dim3(256), 0, s, g, X, w,
-                     pro, Y, stats, ntiles, groups, tiles_x, tiles_y, xcd);
+                     pro, Y, stats, ntiles, groups, tiles_x, tiles_y, xcd, fin ? *fin : BnFwdFin{});
   DFD_HIP_CHECK(hipGetLastError());
   if (stat_rows) *stat_rows = (int)rows;
   return 0;
@@ -267,7 +274,7 @@ static int fwd1_launch(hipStream_t s, const DwGeom& g, const T* X, const float* 
 // 1: launched, 0: shape not covered, -1: error
 template <typename T>
 int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
-                int* stat_rows) {
+                int* stat_rows, const BnFwdFin* fin) {
   if ((g.k != 3 && g.k != 5) || g.pad != g.k / 2 || (g.s != 1 && g.s != 2)) return 0;
   if (g.Ho != (g.H + 2 * g.pad - g.k) / g.s + 1 || g.Wo != (g.W + 2 * g.pad - g.k) / g.s + 1) return 0;
   // 32-bit element offsets into the input frames; 32-bit byte offsets within two output frames
@@ -284,26 +291,26 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
     // 42 vs 42 us); k5: 153 -> 126 and 43 -> 35 us
     if (g.k == 3) return 0;
     if (H == 7 && W == 7)
-      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows)
-                    : fwd1_launch<T, 5, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin)
+                    : fwd1_launch<T, 5, 7, 7, 7, 2, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin);
     else if (H % 7 == 0 && W % 14 == 0)
-      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
-                    : fwd1_launch<T, 5, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+      rc = g.k == 3 ? fwd1_launch<T, 3, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin)
+                    : fwd1_launch<T, 5, 7, 14, 7, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin);
     else
       return 0;
   } else if (H == 7 && W == 7) {
-    rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows)
-                  : fwd1_launch<T, 5, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+    rc = g.k == 3 ? fwd1_launch<T, 3, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin)
+                  : fwd1_launch<T, 5, 7, 7, 7, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin);
   } else if (g.k == 3 && H % 8 == 0 && W % 28 == 0 && W >= 112) {  // 56x56: the 8-channel strip kernel is 6% faster
-    rc = rb ? fwd1_launch<T, 3, 8, 28, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
-            : fwd1_launch<T, 3, 8, 28, 7>(s, g, X, w, Y, pro, stats, stat_rows);
+    rc = rb ? fwd1_launch<T, 3, 8, 28, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin)
+            : fwd1_launch<T, 3, 8, 28, 7>(s, g, X, w, Y, pro, stats, stat_rows, fin);
   } else if (H % 14 == 0 && W % 14 == 0) {
     if (rb)
-      rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows)
-                    : fwd1_launch<T, 5, 14, 14, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows);
+      rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin)
+                    : fwd1_launch<T, 5, 14, 14, 7, 1, 1, 2>(s, g, X, w, Y, pro, stats, stat_rows, fin);
     else
-      rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows)
-                    : fwd1_launch<T, 5, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows);
+      rc = g.k == 3 ? fwd1_launch<T, 3, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows, fin)
+                    : fwd1_launch<T, 5, 14, 14, 7>(s, g, X, w, Y, pro, stats, stat_rows, fin);
   } else {
     return 0;
   }
@@ -311,8 +318,8 @@ int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y
 }
 
 template int try_dw_fwd1<float>(hipStream_t, const DwGeom&, const float*, const float*, float*, const Pro&, float*,
-                                int*);
+                                int*, const BnFwdFin*);
 template int try_dw_fwd1<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, float*,
-                               int*);
+                               int*, const BnFwdFin*);
 
 }  // namespace dfd

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <climits>
 
+#include "bnfin.h"
 #include "common.h"
 
 namespace dfd {
@@ -64,9 +65,10 @@ struct Tuning {
 // tail_fin: BN finalizes in the producers' last-arriving workgroups (tail.h) instead of their own
 // launches (bit 0: the SE-backward chain's BN2 finalize); bit 1: the SE excitation's first product
 // split over its channel slices (k_bn.hip SeSplit); bit 2: BN backward finalize inside the apply pass
-// (bn_bwd_apply_fin) where the producer wrote <= 256 stat rows
+// (bn_bwd_apply_fin) where the producer wrote <= 256 stat rows; bit 3: forward BN finalize inside the
+// consumer (depthwise forward, SE squeeze, global average pool) where the producer wrote <= 64 rows
 #ifndef DFD_TAIL_FIN_DEFAULT
-#define DFD_TAIL_FIN_DEFAULT 7
+#define DFD_TAIL_FIN_DEFAULT 15
 #endif
 // wg_pf: m-steps of loads in flight in the tiled 1x1 weight gradient (pw_wgrad_kernel, bf16)
 #ifndef DFD_WG_PF
@@ -203,9 +205,11 @@ struct DwGeom {
   int frames, H, W, C, k, s, pad, Ho, Wo;
 };
 // Y[n,ho,wo,c] = sum_taps pro(X)[n, ho*s-pad+kh, wo*s-pad+kw, c] * w[c][kh][kw]
+// fin (optional): the input BN's train-mode finalize from its producer's stat rows -- inside the kernel
+// where the rows are few and the channel-pair kernel runs (bnfin.h), else as its own launch first
 template <typename T>
 int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro,
-                  int pro_mode, float* stats, int* stat_rows);
+                  int pro_mode, float* stats, int* stat_rows, const BnFwdFin* fin = nullptr);
 struct BnBwdIn;
 // dA = dgrad(dY).  With bn != null (fused backward of the producer's BN+SiLU): writes
 // g = dA * silu'(Yp*scale+shift) and per-channel partials of g, g*xhat into stats rows.
@@ -241,7 +245,7 @@ bool dw_bwd2_covers(const DwGeom& g);
 // k_dw_fwd1.hip: 1 launched, 0 not covered, -1 error
 template <typename T>
 int try_dw_fwd1(hipStream_t s, const DwGeom& g, const T* X, const float* w, T* Y, const Pro& pro, float* stats,
-                int* stat_rows);
+                int* stat_rows, const BnFwdFin* fin = nullptr);
 bool dw_fwd1_enabled();
 
 // ---------------- BatchNorm / SE / pooling: k_bn.hip ----------------
@@ -262,6 +266,8 @@ int launch_bn_eval_all(hipStream_t s, const float* P, const float* bnb, float* w
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps,
                        bool training, float* mean, float* invstd, float* scale, float* shift, int chan_rows = 0);
+// the same from a BnFwdFin descriptor (the consumer-side finalize's fallback)
+int launch_bn_finalize_fin(hipStream_t s, const BnFwdFin& f, int C);
 constexpr int kConvStatRows = 64;  // rows per BN partial of conv_forward (k_conv.hip CG_T)
 // X = Y*scale + shift (+ R)
 template <typename T>
@@ -300,9 +306,11 @@ int launch_bn_bwd_apply_fin(hipStream_t s, const BnBwdIn& in, const T* Y, int64_
                             int64_t count, const float* gamma, const float* mean, const float* invstd, bool training,
                             float* dgamma, float* dbeta, bool accumulate, float* coef, T* dY);
 // SE squeeze partials: part[h][f][c] = sum over pixel chunk h of pro(Y)   (pro = BN+SiLU), h < *hsplit
+// s_out: optional materialised silu(bn(Y)); fin: the BN's finalize (inside the launch where the stat rows
+// are few, else its own launch first)
 template <typename T>
 int launch_se_squeeze(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* part,
-                      int64_t part_cap, int* hsplit, T* s_out);  // s_out: optional materialised silu(bn(Y))
+                      int64_t part_cap, int* hsplit, T* s_out, const BnFwdFin* fin = nullptr);
 // scratch of the split SE excitation (k_bn.hip se_chain_kernel SPLIT): zeroed counters (2 per 16-frame
 // tile) and partial first products; nullptr (or too small) runs the unsplit form
 struct SeScratch {
@@ -389,7 +397,8 @@ int launch_mfma_small_gemm(hipStream_t s, const float* A, int64_t sam, int64_t s
                            float p, int64_t drop_ld);
 // head global average pool: feat[f][c] = mean_hw silu(Y*scale+shift)
 template <typename T>
-int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat);
+int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, int C, float* feat,
+               const BnFwdFin* fin = nullptr);
 // sum `splits` slabs of n floats into out (= or +=)
 // Deferred weight-gradient reductions: while a SlabDefer is active on the calling thread, slab
 // reductions on `stream` whose output lies inside [lo, hi) (the gradient buffer) are queued and

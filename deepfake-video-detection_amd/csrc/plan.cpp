@@ -410,6 +410,14 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
                               bnb + p.offs[b.t_rv], mom, eps, tr != 0, r.f(b.o_mean), r.f(b.o_invstd), r.f(b.o_scale),
                               r.f(b.o_shift));
   };
+  // training: the finalize handed to the BN's consumer (the depthwise forward, the SE squeeze, the
+  // global average pool), which runs it inside its own launch where the stat rows are few (bnfin.h;
+  // knob tail_fin bit 3) or launches it first; eval: nothing to finalize (fin() is a no-op too)
+  const bool cfin = tr && (tune(TK_TAIL_FIN) & 8) != 0;
+  auto fin_desc = [&](const BNL& b, int64_t count) {
+    return BnFwdFin{r.f(p.o_stats), rows, count, r.prm(b.t_w), r.prm(b.t_b), bnb + p.offs[b.t_rm],
+                    bnb + p.offs[b.t_rv], mom, eps, r.f(b.o_mean), r.f(b.o_invstd), r.f(b.o_scale), r.f(b.o_shift)};
+  };
   DFD_HIP_CHECK(hipMemsetAsync(ws + p.o_ctr, 0, kCtrSlots * sizeof(unsigned), s));
   unsigned* const ctr = reinterpret_cast<unsigned*>(ws + p.o_ctr);
   DFD_TRY(launch_cast_params<T>(s, P, reinterpret_cast<T*>(ws), p.cast_dev, (int)p.cast_host.size(), p.cast_max));
@@ -458,15 +466,18 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
     } else {
       PROBED(PK_PW_FWD, &b, (launch_pw_gemm<T>(s, xin, r.a(b.pw.o_w), r.a(b.o_y1), nullptr, Min, b.mid, b.cin,
                                                PRO_NONE, Pro{}, stats, &rows)));
-      DFD_TRY(fin(b.bn1, Min));
+      if (!cfin) DFD_TRY(fin(b.bn1, Min));
+      const BnFwdFin f1 = fin_desc(b.bn1, Min);
       PROBED(PK_DW_FWD, &b, (launch_dw_fwd<T>(s, g, r.a(b.o_y1), r.prm(b.t_dw), r.a(b.o_y2),
-                                              r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU, stats, &rows)));
+                                              r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU, stats, &rows,
+                                              cfin ? &f1 : nullptr)));
     }
-    DFD_TRY(fin(bn_dw, Mout));
+    if (!cfin) DFD_TRY(fin(bn_dw, Mout));
+    const BnFwdFin f2 = fin_desc(bn_dw, Mout);
     T* s2 = b.o_s2 >= 0 ? r.a(b.o_s2) : nullptr;
     int hs = 1;
     PROBED(PK_SE_SQUEEZE, &b, (launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
-                                                    r.f(p.o_part), p.part_cap, &hs, s2)));
+                                                    r.f(p.o_part), p.part_cap, &hs, s2, cfin ? &f2 : nullptr)));
     // the excitation's first product split over its channel slices (knob tail_fin bit 1); o_stats is free
     // between the BN2 finalize and the projection's BN3 statistics
     const SeScratch sesc{ctr + kCtrSe, kCtrSlots - kCtrSe, r.f(p.o_stats), p.stats_cap};
@@ -484,8 +495,10 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   const int64_t Mf = F * p.Hf * p.Wf;
   DFD_TRY(launch_pw_gemm<T>(s, xin, r.a(p.head.o_w), r.a(p.o_yh), nullptr, Mf, kHead, p.head.cin, PRO_NONE, Pro{},
                             stats, &rows));
-  DFD_TRY(fin(p.bn_head, Mf));
-  DFD_TRY(launch_gap<T>(s, r.a(p.o_yh), r.pro_bn(p.bn_head, p.Hf * p.Wf), p.frames, p.Hf * p.Wf, kHead, feat));
+  if (!cfin) DFD_TRY(fin(p.bn_head, Mf));
+  const BnFwdFin fh = fin_desc(p.bn_head, Mf);
+  DFD_TRY(launch_gap<T>(s, r.a(p.o_yh), r.pro_bn(p.bn_head, p.Hf * p.Wf), p.frames, p.Hf * p.Wf, kHead, feat,
+                        cfin ? &fh : nullptr));
   return 0;
 }
 
@@ -529,7 +542,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
     in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
     // the fused finalize + apply reads <= 256 stat rows: the reduction takes that cap on the smaller
     // (late-stage) tensors, where its workgroups still cover the rows in a few passes
-    const int cap = apply_fin && M * b.C <= ((int64_t)16 << 20) ? 256 : 0;
+    const int cap = apply_fin && M <= 16384 ? 256 : 0;
     DFD_TRY(launch_bn_bwd_reduce<T>(s, in, Y, M, b.C, r.f(p.o_stats), &rows, cap));
     return fin_apply(in, b, Y, M, out, rows);
   };
@@ -856,10 +869,15 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
       DFD_TRY(launch_stem_wgrad<T>(s, sg, x, r.a(p.o_ge1), r.a(p.o_ystem), r.f(p.o_coef), slab(), p.slab_cap,
                                    grad(p.t_stem), acc != 0));
     }
-    DFD_TRY(flush_se());
-    DFD_TRY(defer.flush());  // this segment's weight gradients are final
+    // this segment's weight gradients are final when the call returns: flushed here unless the call
+    // covers more segments (nobody waits for one; the batches then fill up across segments -- slab()
+    // and the SE batch flush themselves when full)
+    if (seg + 1 == seg_end) {
+      DFD_TRY(flush_se());
+      DFD_TRY(defer.flush());
+      region = 0;
+    }
     DFD_TRY(slab_err);
-    region = 0;
   }
   return 0;
 }
