@@ -8,7 +8,7 @@ resident in HBM.  N GPUs = N ranks (one process per GPU, torch.distributed over 
 sharded, bucketed gradient all-reduce overlapped with backward; value = frames of all ranks /
 max-over-ranks time.  Rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp32] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp16|fp32] [--no-cpu-baseline]
 
 ``--gpus N`` without a launcher: this process spawns ``torch.distributed.run`` with N ranks on
 127.0.0.1 BEFORE touching the GPU and exits with its status (the driver's own
@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    # fp16: IEEE half storage on v_mfma_f32_16x16x32_f16 with dynamic loss scaling (TrainStep's
+    # DynamicLossScaler: scale, unscale, skip-on-overflow and update all on the device, inside the step)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--input", default="uint8", choices=["uint8", "fp32"],
                     help="frames handed to the model: raw uint8 crops (normalised in the stem) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -260,6 +262,11 @@ def main():
     elapsed = timed(args.steps, arm=True)
     loss, _ = step.forward_backward(x, labels)
     finite = bool(torch.isfinite(loss).item())
+    # fp16: the dynamic loss scale after the warmup + timed steps, and how many of them were applied
+    # (an overflowing step is skipped on the device; skipped steps are still timed)
+    scaler_info = (None if step.loss_scaler is None else
+                   {"scale": step.loss_scaler.get_scale(), "applied_steps": step.loss_scaler.applied_steps(),
+                    "attempted_steps": args.warmup + args.steps})
     step.sync_grads()
 
     dp = None
@@ -280,7 +287,7 @@ def main():
     value = frames / elapsed
     if rank == 0:
         rl = probe.report()
-        es = 2 if args.dtype == "bf16" else 4
+        es = 2 if args.dtype in ("bf16", "fp16") else 4
         step_bytes = STEP_BYTES_256 * es / 2
         ms_step = 1000 * elapsed / args.steps
         if rl is not None:
@@ -306,6 +313,7 @@ def main():
                        "clips_per_gpu": CLIPS, "frames_per_clip": T, "frames_per_gpu": CLIPS * T,
                        "global_frames": CLIPS * T * world, "image": [H, W, 3], "parallelism": f"dp{world}"},
             "loss_finite": finite,
+            "loss_scaler": scaler_info,
             "roofline": rl,
             "pointwise": pw,
             "dp": dp,

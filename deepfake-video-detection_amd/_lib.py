@@ -62,6 +62,9 @@ _SIGS = {
     "dfd_grad_norm": (c_i, [c_p, c_p, c_i64, c_f, c_p, c_p]),
     "dfd_collate_frames": (c_i, [c_p, c_p, c_p, c_i64, c_i64, c_i, c_p]),
     "dfd_adam_step": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_i, c_d, c_i, c_p]),
+    "dfd_grad_norm_scaled": (c_i, [c_p, c_p, c_i64, c_f, c_p, c_p, c_p]),
+    "dfd_adam_step_scaled": (c_i, [c_p, c_p, c_p, c_p, c_p, c_i64, c_d, c_d, c_d, c_d, c_d, c_d, c_i, c_p, c_p]),
+    "dfd_loss_scale_update": (c_i, [c_p, c_p, c_d, c_d, c_i]),
     "dfd_set_tuning": (c_i64, [ctypes.c_char_p, c_i64]),
     "dfd_rn_im2col": (c_i, [c_p, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p]),
     "dfd_rn_stem_im2col": (c_i, [c_p, c_i, c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_f), c_i, c_i, c_i, c_p]),

@@ -26,7 +26,8 @@ from .flat import FlatModule, GradSink
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 FEATURE_DIM = 1280
-DTYPES = {"fp32": 0, "float32": 0, torch.float32: 0, "bf16": 1, "bfloat16": 1, torch.bfloat16: 1}
+DTYPES = {"fp32": 0, "float32": 0, torch.float32: 0, "bf16": 1, "bfloat16": 1, torch.bfloat16: 1,
+          "fp16": 2, "float16": 2, torch.float16: 2}
 INPUT_F32, INPUT_U8 = 0, 1
 # normalisation applied in the stem to uint8 frames: ((v / 255) - mean) / std
 NORMALIZATIONS = {
@@ -79,9 +80,11 @@ class EfficientNetB0Trunk(FlatModule):
 
     Args:
         compute_dtype: activation storage / MFMA dtype of the trunk: ``"fp32"`` (default: exact
-            fp32 MFMA, the reference's arithmetic within the north-star tolerance) or ``"bf16"``
+            fp32 MFMA, the reference's arithmetic within the north-star tolerance), ``"bf16"``
             (fp32 accumulation, fp32 master weights and BN statistics; the training/serving
-            performance mode, bound tested in tests/test_b0_224_gpu.py and tests/test_serving.py).
+            performance mode, bound tested in tests/test_b0_224_gpu.py and tests/test_serving.py) or
+            ``"fp16"`` (IEEE half storage on v_mfma_f32_16x16x32_f16, fp32 accumulation / master
+            weights / statistics; train it with loss scaling -- TrainStep does, DynamicLossScaler).
         input_normalization: how uint8 frames are normalised inside the stem (``"imagenet"``
             as app.py:2084-2085, ``"unit"`` = /255 only as src/train.py:59, or ``(mean3, std3)``).
             fp32 frames are used as given.

@@ -338,6 +338,45 @@ int dfd_adam_step(void* stream, float* params, float* grads, float* m, float* v,
   DFD_GUARD_END
 }
 
+int dfd_grad_norm_scaled(void* stream, const float* grads, int64_t n, float max_norm, float* scaler_state, void* scratch,
+                         float* out2) {
+  DFD_GUARD_BEGIN
+  if (!scaler_state) { dfd::set_error("grad_norm_scaled: scaler state missing", __FILE__, __LINE__); return -1; }
+  return dfd::grad_norm((hipStream_t)stream, grads, n, max_norm, (double*)scratch, 1024, out2, scaler_state);
+  DFD_GUARD_END
+}
+
+int dfd_adam_step_scaled(void* stream, float* params, float* grads, float* m, float* v, int64_t n, double lr,
+                         double beta1, double beta2, double eps, double weight_decay, double grad_scale, int decoupled,
+                         const float* clip_out2, const float* scaler_state) {
+  DFD_GUARD_BEGIN
+  if (!scaler_state) { dfd::set_error("adam_step_scaled: scaler state missing", __FILE__, __LINE__); return -1; }
+  dfd::AdamHyper h{};
+  h.omb1 = (float)(1.0 - beta1);
+  h.beta2 = (float)beta2;
+  h.omb2 = (float)(1.0 - beta2);
+  h.eps = (float)eps;
+  h.weight_decay = (float)weight_decay;
+  h.decay = (float)(1.0 - lr * weight_decay);
+  h.grad_scale = (float)grad_scale;
+  h.decoupled = decoupled;
+  h.scaler = scaler_state;
+  h.lr = lr;
+  h.beta1d = beta1;
+  h.beta2d = beta2;
+  return dfd::adam_step((hipStream_t)stream, params, grads, m, v, n, h, clip_out2);
+  DFD_GUARD_END
+}
+
+int dfd_loss_scale_update(void* stream, float* scaler_state, double growth_factor, double backoff_factor,
+                          int growth_interval) {
+  DFD_GUARD_BEGIN
+  if (!scaler_state || growth_interval < 1) { dfd::set_error("loss_scale_update: bad arguments", __FILE__, __LINE__); return -1; }
+  return dfd::loss_scale_update((hipStream_t)stream, scaler_state, (float)growth_factor, (float)backoff_factor,
+                                growth_interval);
+  DFD_GUARD_END
+}
+
 int dfd_collate_frames(void* stream, const uint8_t* src, const int64_t* sel, int64_t nsel, int64_t frame_bytes,
                        int out_f32, void* out) {
   DFD_GUARD_BEGIN
@@ -585,7 +624,10 @@ int64_t dfd_set_tuning(const char* key, int64_t value) {
 
 static bool pw_args_ok(int dtype, int64_t M, int N, int K, int pro_mode, const float* scale, const float* shift,
                        const float* gate, int rows_per_frame) {
-  if (dtype != DFD_DTYPE_F32 && dtype != DFD_DTYPE_BF16) { dfd::set_error("pw: bad dtype", __FILE__, __LINE__); return false; }
+  if (dtype != DFD_DTYPE_F32 && dtype != DFD_DTYPE_BF16 && dtype != DFD_DTYPE_F16) {
+    dfd::set_error("pw: bad dtype", __FILE__, __LINE__);
+    return false;
+  }
   if (M < 0 || N <= 0 || K <= 0) { dfd::set_error("pw: bad shape", __FILE__, __LINE__); return false; }
   if (pro_mode != dfd::PRO_NONE && pro_mode != dfd::PRO_BN_SILU && pro_mode != dfd::PRO_BN_SILU_G &&
       pro_mode != dfd::PRO_GATE) {
@@ -612,6 +654,9 @@ int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, 
   if (dtype == DFD_DTYPE_BF16)
     return dfd::launch_pw_gemm<dfd::bf16>(s, (const dfd::bf16*)A, (const dfd::bf16*)W, (dfd::bf16*)C,
                                           (const dfd::bf16*)R, M, N, K, pro_mode, pro, stats, stat_rows);
+  if (dtype == DFD_DTYPE_F16)
+    return dfd::launch_pw_gemm<dfd::f16>(s, (const dfd::f16*)A, (const dfd::f16*)W, (dfd::f16*)C, (const dfd::f16*)R,
+                                         M, N, K, pro_mode, pro, stats, stat_rows);
   return dfd::launch_pw_gemm<float>(s, (const float*)A, (const float*)W, (float*)C, (const float*)R, M, N, K, pro_mode,
                                     pro, stats, stat_rows);
   DFD_GUARD_END
@@ -699,6 +744,9 @@ int dfd_pw_conv_wgrad(void* stream, int dtype, const void* dY, const void* X, in
   if (dtype == DFD_DTYPE_BF16)
     return dfd::launch_pw_wgrad<dfd::bf16>(s, (const dfd::bf16*)dY, (const dfd::bf16*)X, M, N, K, pro_mode, pro, slab,
                                            slab_floats, dW, accumulate != 0);
+  if (dtype == DFD_DTYPE_F16)
+    return dfd::launch_pw_wgrad<dfd::f16>(s, (const dfd::f16*)dY, (const dfd::f16*)X, M, N, K, pro_mode, pro, slab,
+                                          slab_floats, dW, accumulate != 0);
   return dfd::launch_pw_wgrad<float>(s, (const float*)dY, (const float*)X, M, N, K, pro_mode, pro, slab, slab_floats,
                                      dW, accumulate != 0);
   DFD_GUARD_END

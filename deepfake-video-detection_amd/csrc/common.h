@@ -37,6 +37,23 @@ __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
 }
 __device__ __forceinline__ uint16_t f2bf(float f) { return (uint16_t)(pack2bf(f, 0.f) & 0xffffu); }
 
+// IEEE half (fp16 storage mode, v_mfma_f32_16x16x32_f16): conversions round to nearest even
+// (v_cvt_f16_f32; NaN stays NaN, overflow -> inf, which the loss scaler sees)
+struct f16 {
+  uint16_t x;
+};
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float h2f(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ uint32_t pack2h(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, f16x2_t{(_Float16)lo, (_Float16)hi});
+}
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+// the low / high 16-bit element of a packed word as fp32
+__device__ __forceinline__ float lo2f(uint32_t w, f16*) { return h2f((uint16_t)(w & 0xffffu)); }
+__device__ __forceinline__ float hi2f(uint32_t w, f16*) { return h2f((uint16_t)(w >> 16)); }
+__device__ __forceinline__ float lo2f(uint32_t w, struct bf16*) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi2f(uint32_t w, struct bf16*) { return __uint_as_float(w & 0xffff0000u); }
+
 template <typename T> struct Tr;
 template <> struct Tr<float> {
   static constexpr int kDtype = 0;
@@ -49,7 +66,32 @@ template <> struct Tr<bf16> {
   __device__ __forceinline__ static float to_f(bf16 v) { return bf2f(v.x); }
   __device__ __forceinline__ static bf16 from_f(float v) { return bf16{f2bf(v)}; }
   __device__ __forceinline__ static float round(float v) { return bf2f(f2bf(v)); }
+  __device__ __forceinline__ static uint32_t pack2(float lo, float hi) { return pack2bf(lo, hi); }
 };
+template <> struct Tr<f16> {
+  static constexpr int kDtype = 2;
+  __device__ __forceinline__ static float to_f(f16 v) { return h2f(v.x); }
+  __device__ __forceinline__ static f16 from_f(float v) { return f16{f2h(v)}; }
+  __device__ __forceinline__ static float round(float v) { return h2f(f2h(v)); }
+  __device__ __forceinline__ static uint32_t pack2(float lo, float hi) { return pack2h(lo, hi); }
+};
+// 16-bit storage types (bf16, f16): the MFMA operand paths; is_bf16: the kernels that exist for bf16 only
+template <typename T> constexpr bool is16 = sizeof(T) == 2;
+template <typename T> constexpr bool is_bf16 = std::is_same<T, bf16>::value;
+
+// 16 x 16 x 32 MFMA on 8 packed 16-bit operands per lane (bf16 or fp16 by storage type)
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4m_t __attribute__((ext_vector_type(4)));
+template <typename T>
+__device__ __forceinline__ f32x4m_t mfma16x16x32(s16x8_t a, s16x8_t b, f32x4m_t c) {
+  if constexpr (std::is_same<T, f16>::value) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+  } else {
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+  }
+}
 
 // ---- 8-element vector load/store (p must be 16-B aligned for bf16, 32-B for fp32) ----
 __device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
@@ -64,6 +106,19 @@ __device__ __forceinline__ void ld8(const bf16* p, float (&v)[8]) {
   v[2] = __uint_as_float(a.y << 16); v[3] = __uint_as_float(a.y & 0xffff0000u);
   v[4] = __uint_as_float(a.z << 16); v[5] = __uint_as_float(a.z & 0xffff0000u);
   v[6] = __uint_as_float(a.w << 16); v[7] = __uint_as_float(a.w & 0xffff0000u);
+}
+__device__ __forceinline__ void ld8(const f16* p, float (&v)[8]) {
+  const uint4 a = *reinterpret_cast<const uint4*>(p);
+  v[0] = lo2f(a.x, (f16*)nullptr); v[1] = hi2f(a.x, (f16*)nullptr);
+  v[2] = lo2f(a.y, (f16*)nullptr); v[3] = hi2f(a.y, (f16*)nullptr);
+  v[4] = lo2f(a.z, (f16*)nullptr); v[5] = hi2f(a.z, (f16*)nullptr);
+  v[6] = lo2f(a.w, (f16*)nullptr); v[7] = hi2f(a.w, (f16*)nullptr);
+}
+__device__ __forceinline__ void st8(f16* p, const float (&v)[8]) {
+  uint4 a;
+  a.x = pack2h(v[0], v[1]); a.y = pack2h(v[2], v[3]);
+  a.z = pack2h(v[4], v[5]); a.w = pack2h(v[6], v[7]);
+  *reinterpret_cast<uint4*>(p) = a;
 }
 __device__ __forceinline__ void st8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
@@ -86,6 +141,23 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) { ld8(p, v);
 template <typename T> struct Raw8;
 template <> struct Raw8<bf16> { uint4 a; bool ok; };
 template <> struct Raw8<float> { float4 a, b; bool ok; };
+template <> struct Raw8<f16> { uint4 a; bool ok; };
+__device__ __forceinline__ void raw_ld(Raw8<f16>& r, const f16* p, const f16* safe, bool ok) {
+  r.a = *reinterpret_cast<const uint4*>(ok ? p : safe);
+  r.ok = ok;
+}
+__device__ __forceinline__ void raw_to_f(const Raw8<f16>& r, float (&v)[8]) {
+  const uint32_t m = r.ok ? 0xffffffffu : 0u;
+  const uint32_t x = r.a.x & m, y = r.a.y & m, z = r.a.z & m, w = r.a.w & m;
+  v[0] = lo2f(x, (f16*)nullptr); v[1] = hi2f(x, (f16*)nullptr);
+  v[2] = lo2f(y, (f16*)nullptr); v[3] = hi2f(y, (f16*)nullptr);
+  v[4] = lo2f(z, (f16*)nullptr); v[5] = hi2f(z, (f16*)nullptr);
+  v[6] = lo2f(w, (f16*)nullptr); v[7] = hi2f(w, (f16*)nullptr);
+}
+__device__ __forceinline__ void raw_st(f16* p, const Raw8<f16>& r) {
+  const uint32_t m = r.ok ? 0xffffffffu : 0u;
+  *reinterpret_cast<uint4*>(p) = make_uint4(r.a.x & m, r.a.y & m, r.a.z & m, r.a.w & m);
+}
 
 __device__ __forceinline__ void raw_ld(Raw8<bf16>& r, const bf16* p, const bf16* safe, bool ok) {
   r.a = *reinterpret_cast<const uint4*>(ok ? p : safe);

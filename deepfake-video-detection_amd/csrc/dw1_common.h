@@ -51,6 +51,20 @@ __device__ __forceinline__ v2f round2(v2f v, bf16*) {
 __device__ __forceinline__ v2f round2(v2f v, float*) { return v; }
 __device__ __forceinline__ void st2(bf16* p, v2f v) { *reinterpret_cast<uint32_t*>(p) = pack2bf(v.x, v.y); }
 __device__ __forceinline__ void st2(float* p, v2f v) { *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y); }
+// fp16 storage (the half-precision mode): the same helpers with IEEE-half packing
+template <> struct Raw2<f16> { uint32_t v; };
+__device__ __forceinline__ void raw2_ld(Raw2<f16>& r, const f16* p) { r.v = *reinterpret_cast<const uint32_t*>(p); }
+__device__ __forceinline__ v2f raw2_f(const Raw2<f16>& r) { return v2f{lo2f(r.v, (f16*)nullptr), hi2f(r.v, (f16*)nullptr)}; }
+__device__ __forceinline__ void pin2(Raw2<f16>& r) { asm volatile("" : "+v"(r.v)); }
+__device__ __forceinline__ v2f raw8_pair(const Raw8<f16>& r, int q) {
+  const uint32_t w = q == 0 ? r.a.x : q == 1 ? r.a.y : q == 2 ? r.a.z : r.a.w;
+  return v2f{lo2f(w, (f16*)nullptr), hi2f(w, (f16*)nullptr)};
+}
+__device__ __forceinline__ v2f round2(v2f v, f16*) {
+  const uint32_t w = pack2h(v.x, v.y);
+  return v2f{lo2f(w, (f16*)nullptr), hi2f(w, (f16*)nullptr)};
+}
+__device__ __forceinline__ void st2(f16* p, v2f v) { *reinterpret_cast<uint32_t*>(p) = pack2h(v.x, v.y); }
 // base + a 32-bit BYTE offset: the uniform frame base stays in SGPRs and each access is one
 // global_load/store with a 32-bit VGPR offset (no per-lane 64-bit address arithmetic)
 template <typename T> __device__ __forceinline__ const T* boff(const T* base, uint32_t off) {

@@ -29,6 +29,11 @@ struct AdamHyper {
   float bc2_sqrt;   // sqrt(1 - beta2^step)
   float grad_scale; // multiplies the gradient first (e.g. 1/world_size)
   int decoupled;    // 1 = AdamW, 0 = Adam (L2 folded into the gradient)
+  // dynamic loss scaling (fp16 training): null, or the scaler state [scale, growth tracker, found_inf,
+  // applied steps].  With it the gradient is unscaled by 1/scale, a step whose gradient norm was
+  // non-finite is skipped, and the bias corrections use the applied-step count (lr, beta1, beta2).
+  const float* scaler;
+  double lr, beta1d, beta2d;
 };
 
 int head_forward(hipStream_t s, const HeadDims& d, const HeadParams& P, const float* F, HeadWork& w, uint64_t seed,
@@ -40,7 +45,9 @@ int ce_forward(hipStream_t s, const float* z, const int64_t* y, const float* w, 
                float* loss, float* wsum);
 int ce_backward(hipStream_t s, const float* z, const int64_t* y, const float* w, int B, int NC, int64_t ignore,
                 const float* wsum, const float* gout, float* dz);
-int grad_norm(hipStream_t s, const float* g, int64_t n, float max_norm, double* part, int nparts, float* out);
+int grad_norm(hipStream_t s, const float* g, int64_t n, float max_norm, double* part, int nparts, float* out,
+              float* scaler = nullptr);
+int loss_scale_update(hipStream_t s, float* scaler, float growth, float backoff, int interval);
 int adam_step(hipStream_t s, float* p, float* g, float* m, float* v, int64_t n, const AdamHyper& h, const float* coef);
 
 }  // namespace dfd

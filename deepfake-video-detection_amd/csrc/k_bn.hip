@@ -1604,6 +1604,7 @@ int launch_reduce_slabs_strided(hipStream_t s, const float* slab, int splits, in
   template int launch_col_sums<T>(hipStream_t, const T*, int64_t, int, float*, int64_t, float*);
 DFD_BN_INST(float)
 DFD_BN_INST(bf16)
+DFD_BN_INST(f16)
 #undef DFD_BN_INST
 
 }  // namespace dfd

@@ -64,17 +64,19 @@ template <typename T> struct RawV<T, 8> {
   __device__ __forceinline__ void ld(const T* p, const T* safe, bool ok) { raw_ld(r, p, safe, ok); }
   __device__ __forceinline__ void to_f(float (&v)[8]) const { raw_to_f(r, v); }
 };
-template <> struct RawV<bf16, 4> {
+template <typename T> struct RawV16x4 {  // 4 channels of a 16-bit type (bf16 / f16)
   uint2 a; bool ok;
-  __device__ __forceinline__ void ld(const bf16* p, const bf16* safe, bool o) {
+  __device__ __forceinline__ void ld(const T* p, const T* safe, bool o) {
     a = *reinterpret_cast<const uint2*>(o ? p : safe); ok = o;
   }
   __device__ __forceinline__ void to_f(float (&v)[4]) const {
     const uint32_t m = ok ? 0xffffffffu : 0u, x = a.x & m, y = a.y & m;
-    v[0] = __uint_as_float(x << 16); v[1] = __uint_as_float(x & 0xffff0000u);
-    v[2] = __uint_as_float(y << 16); v[3] = __uint_as_float(y & 0xffff0000u);
+    v[0] = lo2f(x, (T*)nullptr); v[1] = hi2f(x, (T*)nullptr);
+    v[2] = lo2f(y, (T*)nullptr); v[3] = hi2f(y, (T*)nullptr);
   }
 };
+template <> struct RawV<bf16, 4> : RawV16x4<bf16> {};
+template <> struct RawV<f16, 4> : RawV16x4<f16> {};
 template <> struct RawV<float, 4> {
   float4 a; bool ok;
   __device__ __forceinline__ void ld(const float* p, const float* safe, bool o) {
@@ -93,8 +95,12 @@ template <int VW> __device__ __forceinline__ void ldsv(const float* p, float (&v
 }
 __device__ __forceinline__ void stv(bf16* p, const float (&v)[8]) { st8(p, v); }
 __device__ __forceinline__ void stv(float* p, const float (&v)[8]) { st8(p, v); }
+__device__ __forceinline__ void stv(f16* p, const float (&v)[8]) { st8(p, v); }
 __device__ __forceinline__ void stv(bf16* p, const float (&v)[4]) {
   *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+}
+__device__ __forceinline__ void stv(f16* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack2h(v[0], v[1]), pack2h(v[2], v[3]));
 }
 __device__ __forceinline__ void stv(float* p, const float (&v)[4]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
@@ -424,6 +430,8 @@ int launch_dw_bwd(hipStream_t s, const DwGeom& g, const T* dY, const float* w, T
 template int launch_dw_bwd<float>(hipStream_t, const DwGeom&, const float*, const float*, float*, const float*,
                                   const BnBwdIn*, float*, int*, float*, int64_t, float*, bool);
 template int launch_dw_bwd<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const bf16*,
+                                 const BnBwdIn*, float*, int*, float*, int64_t, float*, bool);
+template int launch_dw_bwd<f16>(hipStream_t, const DwGeom&, const f16*, const float*, f16*, const f16*,
                                  const BnBwdIn*, float*, int*, float*, int64_t, float*, bool);
 
 }  // namespace dfd

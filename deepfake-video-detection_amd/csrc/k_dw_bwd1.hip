@@ -410,5 +410,8 @@ template int launch_dw_bwd1<float>(hipStream_t, const DwGeom&, const float*, con
 template int launch_dw_bwd1<bf16>(hipStream_t, const DwGeom&, const bf16*, const bf16*, const float*, const float*,
                                   const float*, const float*, const float*, const float*, const bf16*,
                                   const BnBwdIn&, bf16*, float*, int*, float*, int64_t, float*, bool);
+template int launch_dw_bwd1<f16>(hipStream_t, const DwGeom&, const f16*, const f16*, const float*, const float*,
+                                  const float*, const float*, const float*, const float*, const f16*,
+                                  const BnBwdIn&, f16*, float*, int*, float*, int64_t, float*, bool);
 
 }  // namespace dfd

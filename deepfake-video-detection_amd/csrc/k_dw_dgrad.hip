@@ -154,5 +154,7 @@ template int launch_dw_dgrad<float>(hipStream_t, const DwGeom&, const float*, co
                                     const BnBwdIn*, float*, int*);
 template int launch_dw_dgrad<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const bf16*,
                                    const BnBwdIn*, float*, int*);
+template int launch_dw_dgrad<f16>(hipStream_t, const DwGeom&, const f16*, const float*, f16*, const f16*,
+                                   const BnBwdIn*, float*, int*);
 
 }  // namespace dfd

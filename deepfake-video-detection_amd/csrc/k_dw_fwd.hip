@@ -26,7 +26,7 @@ __global__ __launch_bounds__(256, 2) void dw_fwd_kernel(DwGeom g, const T* __res
                                                      T* __restrict__ Y, Pro pro, float* __restrict__ stats, int ntiles,
                                                      int groups, int tiles_x, int tiles_y) {
   using D = DwT<TH, TW, K, S>;
-  using LT = std::conditional_t<(DFD_DWF_BF16LDS != 0 && S == 2 && sizeof(T) == 2), bf16, float>;
+  using LT = std::conditional_t<(DFD_DWF_BF16LDS != 0 && S == 2 && sizeof(T) == 2), T, float>;
   __shared__ __attribute__((aligned(16))) LT tin[D::NIN * DCG];
   __shared__ __attribute__((aligned(16))) float wts[K * K * DCG];
   const int tid = threadIdx.x, vec = tid & 3, tp = tid >> 2;
@@ -193,6 +193,8 @@ int launch_dw_fwd(hipStream_t s, const DwGeom& g, const T* X, const float* w, T*
 template int launch_dw_fwd<float>(hipStream_t, const DwGeom&, const float*, const float*, float*, const Pro&, int,
                                   float*, int*, const BnFwdFin*);
 template int launch_dw_fwd<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, int,
+                                 float*, int*, const BnFwdFin*);
+template int launch_dw_fwd<f16>(hipStream_t, const DwGeom&, const f16*, const float*, f16*, const Pro&, int,
                                  float*, int*, const BnFwdFin*);
 
 }  // namespace dfd

@@ -321,5 +321,7 @@ template int try_dw_fwd1<float>(hipStream_t, const DwGeom&, const float*, const 
                                 int*, const BnFwdFin*);
 template int try_dw_fwd1<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, float*,
                                int*, const BnFwdFin*);
+template int try_dw_fwd1<f16>(hipStream_t, const DwGeom&, const f16*, const float*, f16*, const Pro&, float*,
+                               int*, const BnFwdFin*);
 
 }  // namespace dfd

@@ -233,5 +233,7 @@ template int try_dw_fwd_strip<float>(hipStream_t, const DwGeom&, const float*, c
                                      int*);
 template int try_dw_fwd_strip<bf16>(hipStream_t, const DwGeom&, const bf16*, const float*, bf16*, const Pro&, float*,
                                     int*);
+template int try_dw_fwd_strip<f16>(hipStream_t, const DwGeom&, const f16*, const float*, f16*, const Pro&, float*,
+                                    int*);
 
 }  // namespace dfd

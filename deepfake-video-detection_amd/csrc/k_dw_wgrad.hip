@@ -133,5 +133,7 @@ template int launch_dw_wgrad<float>(hipStream_t, const DwGeom&, const float*, co
                                     int64_t, float*, bool);
 template int launch_dw_wgrad<bf16>(hipStream_t, const DwGeom&, const bf16*, const bf16*, const Pro&, int, float*,
                                    int64_t, float*, bool);
+template int launch_dw_wgrad<f16>(hipStream_t, const DwGeom&, const f16*, const f16*, const Pro&, int, float*,
+                                   int64_t, float*, bool);
 
 }  // namespace dfd

@@ -442,9 +442,11 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 }
 
 // out[0] = total norm, out[1] = clip coefficient min(1, max_norm/(norm+1e-6)) (1 if max_norm <= 0)
-// (256 threads: strided partial sums, then a fixed-order tree; deterministic)
+// (256 threads: strided partial sums, then a fixed-order tree; deterministic).  With a loss scaler
+// (fp16 training) the partials are of the SCALED gradient: the norm is unscaled by the fp32 inverse
+// scale (GradScaler.unscale_ then clip_grad_norm_), and scaler[2] = 1 when it is not finite.
 __global__ __launch_bounds__(256) void norm_finalize_kernel(const double* __restrict__ part, int nparts, float max_norm,
-                                                            float* out) {
+                                                            float* out, float* __restrict__ scaler) {
   __shared__ double sh[256];
   double v = 0.0;
   for (int i = threadIdx.x; i < nparts; i += 256) v += part[i];
@@ -456,7 +458,12 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const double* __rest
   }
   if (threadIdx.x != 0) return;
   const double a = sh[0];
-  const float nrm = (float)sqrt(a);
+  float nrm = (float)sqrt(a);
+  if (scaler) {
+    const bool bad = !isfinite(nrm);
+    scaler[2] = bad ? 1.f : 0.f;
+    nrm = bad ? nrm : (float)(sqrt(a) * (double)(1.f / scaler[0]));
+  }
   out[0] = nrm;
   float c = 1.f;
   if (max_norm > 0.f) {
@@ -470,8 +477,19 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
                                                    float* __restrict__ v, int64_t n, AdamHyper h,
                                                    const float* __restrict__ coef) {
   const float cf = coef ? coef[1] : 1.f;
+  float step_size = h.step_size, bc2_sqrt = h.bc2_sqrt, inv = 1.f;
+  if (h.scaler) {
+    if (h.scaler[2] != 0.f) return;  // non-finite scaled gradient: the step is skipped (GradScaler.step)
+    // bias corrections of the APPLIED step count (skipped steps do not count, as torch's optimizer
+    // step is not called for them), in double as torch.optim computes them
+    const double t = (double)h.scaler[3] + 1.0;
+    step_size = (float)(h.lr / (1.0 - pow(h.beta1d, t)));
+    bc2_sqrt = (float)sqrt(1.0 - pow(h.beta2d, t));
+    inv = 1.f / h.scaler[0];
+  }
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float gi = g[i] * h.grad_scale;
+    if (h.scaler) { gi = gi * inv; g[i] = gi; }  // unscale_ in place
     if (coef) { gi = gi * cf; g[i] = gi; }
     float pi = p[i];
     if (h.decoupled) {
@@ -482,11 +500,32 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
     float mi = m[i];
     mi = mi + h.omb1 * (gi - mi);
     float vi = v[i] * h.beta2 + h.omb2 * gi * gi;
-    const float denom = sqrtf(vi) / h.bc2_sqrt + h.eps;
-    pi = pi + (-h.step_size * mi) / denom;
+    const float denom = sqrtf(vi) / bc2_sqrt + h.eps;
+    pi = pi + (-step_size * mi) / denom;
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
+  }
+}
+
+// torch.amp.GradScaler's update (_amp_update_scale_): a non-finite step halves the scale (backoff) and
+// restarts the growth count; `interval` finite steps in a row multiply it by `growth`.  Also counts the
+// applied optimizer steps (scaler[3]) for the bias corrections.  One thread, after the Adam launches.
+__global__ void loss_scale_update_kernel(float* __restrict__ st, float growth, float backoff, int interval) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (st[2] != 0.f) {
+    st[0] = st[0] * backoff;
+    st[1] = 0.f;
+  } else {
+    st[3] = st[3] + 1.f;
+    const float t = st[1] + 1.f;
+    if (t >= (float)interval) {
+      const float ns = st[0] * growth;
+      if (isfinite(ns)) st[0] = ns;
+      st[1] = 0.f;
+    } else {
+      st[1] = t;
+    }
   }
 }
 
@@ -534,6 +573,7 @@ int launch_cast_params(hipStream_t s, const float* params, T* out, const CastSeg
 }
 template int launch_cast_params<float>(hipStream_t, const float*, float*, const CastSeg*, int, int);
 template int launch_cast_params<bf16>(hipStream_t, const float*, bf16*, const CastSeg*, int, int);
+template int launch_cast_params<f16>(hipStream_t, const float*, f16*, const CastSeg*, int, int);
 
 // ------------------------------------------------------------------ host launchers (head.h)
 static unsigned nblk(int64_t n) { return (unsigned)std::max<int64_t>(1, cdiv64(n, 256)); }
@@ -608,10 +648,17 @@ int ce_backward(hipStream_t s, const float* z, const int64_t* y, const float* w,
   return 0;
 }
 
-int grad_norm(hipStream_t s, const float* g, int64_t n, float max_norm, double* part, int nparts, float* out) {
+int grad_norm(hipStream_t s, const float* g, int64_t n, float max_norm, double* part, int nparts, float* out,
+              float* scaler) {
   const int gx = std::max(1, std::min<int>(nparts, (int)nblk(n)));
   hipLaunchKernelGGL(sumsq_kernel, dim3(gx), dim3(256), 0, s, g, n, part);
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, s, part, gx, max_norm, out);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, s, part, gx, max_norm, out, scaler);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+int loss_scale_update(hipStream_t s, float* scaler, float growth, float backoff, int interval) {
+  hipLaunchKernelGGL(loss_scale_update_kernel, dim3(1), dim3(64), 0, s, scaler, growth, backoff, interval);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
 }

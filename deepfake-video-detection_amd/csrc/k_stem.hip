@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void stem_wgrad_kernel(StemGeom g, const void*
   }
 }
 
-// bf16 mode: the same weight gradient as a GEMM on v_mfma_f32_16x16x32_bf16 --
+// 16-bit modes: the same weight gradient as a GEMM on v_mfma_f32_16x16x32_bf16 / _f16 --
 // dW[co][tap] = sum_p dY[p][co] * patch[p][tap], K = pixels.  Per 16x16-pixel tile the dY tile
 // ([pix][co], 16-B row writes) and the im2col tile ([pix][tap], 27 taps padded to 32, bf16 as the
 // bf16 conv consumes its input) are staged in LDS; each wave takes 32-pixel k-steps and reads both
@@ -327,16 +327,17 @@ typedef short stw_s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) stw_s16x4_t stw_lds_s16x4_t;
 typedef float stw_f32x4_t __attribute__((ext_vector_type(4)));
 
+template <typename T>
 __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, const void* __restrict__ x,
-                                                              const bf16* __restrict__ dY, const bf16* __restrict__ Yb,
+                                                              const T* __restrict__ dY, const T* __restrict__ Yb,
                                                               const float* __restrict__ coef,
                                                               float* __restrict__ slab, int64_t ntiles) {
   __shared__ float tin[SNIN];
   __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
   __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
   stem_lut_init(g, lut);
-  __shared__ __attribute__((aligned(16))) bf16 ys[ST * ST * SWL];  // dY tile [pix][co]; reused for the reduction
-  __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col tile [pix][tap]
+  __shared__ __attribute__((aligned(16))) T ys[ST * ST * SWL];  // dY tile [pix][co]; reused for the reduction
+  __shared__ __attribute__((aligned(16))) T xs[ST * ST * SWL];  // im2col tile [pix][tap]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const StemTiles tl{(g.Wo + ST - 1) / ST, (g.Ho + ST - 1) / ST};
   stw_f32x4_t acc[2][2];
@@ -346,8 +347,8 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
     for (int b = 0; b < 2; ++b) acc[a][b] = stw_f32x4_t{0.f, 0.f, 0.f, 0.f};
   float nx[SNLD];
   uint32_t nxok = 0u;
-  Raw8<bf16> nd[4];  // 256 px x 4 vectors / 256 threads
-  Raw8<bf16> ny[4];  // fused BN backward: the stem's pre-BN output at the same pixels
+  Raw8<T> nd[4];  // 256 px x 4 vectors / 256 threads
+  Raw8<T> ny[4];  // fused BN backward: the stem's pre-BN output at the same pixels
   __shared__ __attribute__((aligned(16))) float bnk[3][SCO];
   stem_bn_coef(coef, bnk);
   auto load = [&](int64_t t) {
@@ -427,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[a], bfr[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < 2; ++b) acc[a][b] = mfma16x16x32<T>(afr[a], bfr[b], acc[a][b]);
     }
   }
   // ---- the 4 waves' 32x32 partials in a fixed order into this workgroup's slab row ----
@@ -460,25 +461,25 @@ __global__ __launch_bounds__(256, 2) void stem_wgrad_mfma_kernel(StemGeom g, con
 constexpr int SFC = SCO + 8;  // LDS row stride (bf16) of the output slab
 // OCC workgroups per CU (knob stem_occ, default 3: the output slab aliases the im2col tile, 44 KB of
 // LDS, and the dense-uint8 instantiation fits 168 VGPRs; 2 is the previous occupancy)
-template <int OCC, int FMT>
+template <typename T, int OCC, int FMT>
 __global__ __launch_bounds__(256, OCC) void stem_fwd_mfma_kernel(StemGeom g, const void* __restrict__ x,
-                                                            const float* __restrict__ w, bf16* __restrict__ Y,
+                                                            const float* __restrict__ w, T* __restrict__ Y,
                                                             float* __restrict__ stats, int64_t ntiles) {
   __shared__ float tin[SNIN];
   __shared__ float lut[SLUT];  // uint8 input: normalised value per (channel, byte)
   __shared__ uint32_t u8s[SNW];  // dense uint8 input: the tile's rows as staged dwords
   stem_lut_init(g, lut);
-  __shared__ __attribute__((aligned(16))) bf16 xs[ST * ST * SWL];  // im2col [pix][tap]
+  __shared__ __attribute__((aligned(16))) T xs[ST * ST * SWL];  // im2col [pix][tap]
   // the output slab [pix][co] shares xs: a wave writes the output rows of the 16-pixel blocks whose
   // im2col rows it has just read (same pixels, same row stride), so no other wave's operand is hit
   static_assert(SFC == SWL, "slab and im2col rows alias");
-  bf16* const ct = xs;
-  __shared__ __attribute__((aligned(16))) bf16 wsb[SCO * SWL];     // weights [co][tap]
+  T* const ct = xs;
+  __shared__ __attribute__((aligned(16))) T wsb[SCO * SWL];     // weights [co][tap]
   __shared__ float red[2][4][SCO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < SCO * 32; i += 256) {
     const int co = i / 32, tap = i % 32;  // w[co][ci][kh][kw], tap = ci*9 + kh*3 + kw
-    wsb[co * SWL + tap] = Tr<bf16>::from_f(tap < 27 ? w[co * 27 + tap] : 0.f);
+    wsb[co * SWL + tap] = Tr<T>::from_f(tap < 27 ? w[co * 27 + tap] : 0.f);
   }
   lds_barrier();
   stw_bf16x8_t wf[2];
@@ -541,11 +542,11 @@ __global__ __launch_bounds__(256, OCC) void stem_fwd_mfma_kernel(StemGeom g, con
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         stw_f32x4_t d = {0.f, 0.f, 0.f, 0.f};
-        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[a], pf, d, 0, 0, 0);
-        const uint2 pk = make_uint2(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]));
+        d = mfma16x16x32<T>(wf[a], pf, d);
+        const uint2 pk = make_uint2(Tr<T>::pack2(d[0], d[1]), Tr<T>::pack2(d[2], d[3]));
         if (stats_on) {
-          const float v[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
-                              __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+          const float v[4] = {lo2f(pk.x, (T*)nullptr), hi2f(pk.x, (T*)nullptr), lo2f(pk.y, (T*)nullptr),
+                              hi2f(pk.y, (T*)nullptr)};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float vv = ok ? v[r] : 0.f;
@@ -603,11 +604,11 @@ int launch_stem_fwd(hipStream_t s, const StemGeom& g, const void* x, const float
   if constexpr (sizeof(T) == 2) {
     const bool dense = g.in.u8 == 2;
     if (occ3)
-      hipLaunchKernelGGL((stem_fwd_mfma_kernel<3, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<T, 3, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
     else if (dense)
-      hipLaunchKernelGGL((stem_fwd_mfma_kernel<2, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<T, 2, 2>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
     else
-      hipLaunchKernelGGL((stem_fwd_mfma_kernel<2, -1>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
+      hipLaunchKernelGGL((stem_fwd_mfma_kernel<T, 2, -1>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
   } else {  // fp32 parity mode: exact fp32 products
     if (stats)
       hipLaunchKernelGGL((stem_fwd_kernel<T, true>), dim3(gx), dim3(256), 0, s, g, x, w, Y, stats, ntiles);
@@ -626,7 +627,7 @@ int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* 
   int gx = (int)std::min<int64_t>(ntiles, 1024);
   gx = (int)std::max<int64_t>(1, std::min<int64_t>(gx, slab_cap / (27 * SCO)));
   if constexpr (sizeof(T) == 2)
-    hipLaunchKernelGGL(stem_wgrad_mfma_kernel, dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
+    hipLaunchKernelGGL((stem_wgrad_mfma_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
   else  // fp32 parity mode: exact fp32 products
     hipLaunchKernelGGL((stem_wgrad_kernel<T>), dim3(gx), dim3(256), 0, s, g, x, dY, Yb, coef, slab, ntiles);
   DFD_HIP_CHECK(hipGetLastError());
@@ -635,9 +636,12 @@ int launch_stem_wgrad(hipStream_t s, const StemGeom& g, const void* x, const T* 
 
 template int launch_stem_fwd<float>(hipStream_t, const StemGeom&, const void*, const float*, float*, float*, int*);
 template int launch_stem_fwd<bf16>(hipStream_t, const StemGeom&, const void*, const float*, bf16*, float*, int*);
+template int launch_stem_fwd<f16>(hipStream_t, const StemGeom&, const void*, const float*, f16*, float*, int*);
 template int launch_stem_wgrad<float>(hipStream_t, const StemGeom&, const void*, const float*, const float*,
                                       const float*, float*, int64_t, float*, bool);
 template int launch_stem_wgrad<bf16>(hipStream_t, const StemGeom&, const void*, const bf16*, const bf16*,
+                                     const float*, float*, int64_t, float*, bool);
+template int launch_stem_wgrad<f16>(hipStream_t, const StemGeom&, const void*, const f16*, const f16*,
                                      const float*, float*, int64_t, float*, bool);
 
 }  // namespace dfd

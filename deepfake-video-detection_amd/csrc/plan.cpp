@@ -132,7 +132,7 @@ void plan_segment_range(const Plan& p, int seg, int* lo, int* hi) {
 
 int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   if (frames <= 0 || H < 8 || W < 8) { set_error("plan: bad shape", __FILE__, __LINE__); return -1; }
-  if (dtype != 0 && dtype != 1) { set_error("plan: dtype must be 0 (fp32) or 1 (bf16)", __FILE__, __LINE__); return -1; }
+  if (dtype < 0 || dtype > 2) { set_error("plan: dtype must be 0 (fp32), 1 (bf16) or 2 (fp16)", __FILE__, __LINE__); return -1; }
   const Topo& tp = topo();
   p.frames = frames; p.H = H; p.W = W; p.dtype = dtype;
   p.tensors = tp.t;
@@ -427,8 +427,8 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   DFD_TRY(fin(p.bn_stem, F * p.H1 * p.W1));
   const T* xin = nullptr;
   // fused 7x7-stage blocks (bf16): which blocks take the one-launch path, and their barrier slots
-  auto fused7 = [&](const Block& b) { return sizeof(T) == 2 && block_fused7(p, b); };
-  const int nfused = sizeof(T) == 2 ? plan_fused7_blocks(p) : 0;
+  auto fused7 = [&](const Block& b) { return is_bf16<T> && block_fused7(p, b); };
+  const int nfused = is_bf16<T> ? plan_fused7_blocks(p) : 0;
   if (nfused && tr) DFD_HIP_CHECK(hipMemsetAsync(ws + p.o_bar, 0, kBarBytes, s));
   int slot = 0;
   for (size_t i = 0; i < p.blocks.size(); ++i) {
@@ -438,7 +438,7 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
     const BNL& bn_dw = b.ds ? b.bn1 : b.bn2;  // BN after the depthwise conv
     DwGeom g{p.frames, b.hin, b.win, b.mid, b.k, b.s, b.k / 2, b.hout, b.wout};
     if (nfused && fused7(b)) {
-      if constexpr (sizeof(T) == 2) {
+      if constexpr (is_bf16<T>) {
         auto bnp = [&](const BNL& q) {
           return Mb7Bn{r.prm(q.t_w), r.prm(q.t_b), bnb + p.offs[q.t_rm], bnb + p.offs[q.t_rv], r.f(q.o_mean),
                        r.f(q.o_invstd), r.f(q.o_scale), r.f(q.o_shift)};
@@ -646,7 +646,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
         DFD_TRY(join(p.ev[1], gs_busy));  // the previous conv_pwl weight gradient is done with o_gs
         int hs = 1, pf = 1;
-        const bool fpwl = sizeof(T) == 2 && tune(TK_PWL_FUSED) != 0 &&
+        const bool fpwl = is_bf16<T> && tune(TK_PWL_FUSED) != 0 &&
                           pwl_bwd_covers(p.frames, hwo, b.cout, b.mid);
         // the BN3 backward applied in the fused kernel's staging pays where the projection is 16 wide
         // (blocks.0.0: +12 us in the kernel against a 49 us apply pass); at 24 wide the kernel's
@@ -660,7 +660,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
           DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), rows, Mout, b.cout, r.prm(b.bn3.t_w), r.f(b.bn3.o_mean),
                                          r.f(b.bn3.o_invstd), tr != 0, grad(b.bn3.t_w), grad(b.bn3.t_b), acc != 0,
                                          r.f(p.o_coef)));
-          if constexpr (sizeof(T) == 2) {
+          if constexpr (is_bf16<T>) {
             PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, gout, r.a(b.o_y3), r.f(p.o_coef), r.a(b.pwl.o_wt),
                                                            r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                                            r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), r.f(b.o_gate),
@@ -677,7 +677,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         } else {
           DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
           if (fpwl) {
-            if constexpr (sizeof(T) == 2) {
+            if constexpr (is_bf16<T>) {
               PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, r.a(p.o_gs), nullptr, nullptr, r.a(b.pwl.o_wt),
                                                              r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                                              r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), r.f(b.o_gate),
@@ -799,10 +799,10 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                        r.f(p.o_bv)));
           DFD_TRY(join(p.ev[1], gs_busy));  // the conv_pwl weight gradient is done with o_gs
           int ff = 1;
-          if (sizeof(T) == 2 && tune(TK_FOLD_FUSED) != 0) {
+          if (is_bf16<T> && tune(TK_FOLD_FUSED) != 0) {
             // x . Q, the data gradient and the partial products g^T x, x^T x, 1^T x in one pass
             // (k_pw_fold_bwd.hip); their three slab reductions as ONE batched launch
-            if constexpr (sizeof(T) == 2) {
+            if constexpr (is_bf16<T>) {
               float* const parts[3] = {r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs)};
               const int64_t extent[3] = {(int64_t)b.mid * b.cin, (int64_t)b.cin * b.cin, (int64_t)b.cin};
               SlabDefer loc{};
@@ -906,6 +906,7 @@ int plan_forward(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
   const TuningScope ts(&p.tune);
   if (p.dtype == 1) return forward_impl<bf16>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
+  if (p.dtype == 2) return forward_impl<f16>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
   return forward_impl<float>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
 }
 
@@ -920,6 +921,8 @@ int plan_backward_x(Plan& p, hipStream_t s, const void* x, const int64_t* xs, co
   const TuningScope ts(&p.tune);
   if (p.dtype == 1)
     return backward_impl<bf16>(p, s, x, xs, in, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
+  if (p.dtype == 2)
+    return backward_impl<f16>(p, s, x, xs, in, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
   return backward_impl<float>(p, s, x, xs, in, dfeat, params, ws, grads, training, seg_begin, seg_end, accumulate);
 }
 

@@ -9,6 +9,8 @@ implementation for shape propagation, and autograd where the op is differentiabl
                                                    global_pool, src/pretrained_detector.py:116)
   dfd::weighted_cross_entropy (+ _backward)        nn.CrossEntropyLoss(weight) (ensemble_trainer.py:358)
   dfd::grad_norm, dfd::adam_step                   clip_grad_norm_(1.0) + AdamW (ensemble_trainer.py:196-200)
+  dfd::grad_norm_scaled, dfd::adam_step_scaled,    the same under dynamic loss scaling (fp16 training:
+  dfd::loss_scale_update                           GradScaler unscale_ / step / update, on the device)
   dfd::collate_frames                              the collate gather + /255 (train.py:38-61)
 
 Every operator runs on the caller's current HIP stream and raises ``RuntimeError`` (``DFDError``) on
@@ -173,6 +175,51 @@ def _(params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, s
     return None
 
 
+# dynamic loss scaling (fp16 training): `scaler` is the 4-float device state of optim.DynamicLossScaler
+@torch.library.custom_op("dfd::grad_norm_scaled", mutates_args=("scaler", "scratch", "out"), device_types="cuda")
+def grad_norm_scaled(grads: Tensor, max_norm: float, scaler: Tensor, scratch: Tensor, out: Tensor) -> None:
+    """dfd::grad_norm of the SCALED gradient: out[0] = the unscaled norm, scaler[2] = found_inf."""
+    _lib.check(_lib.load().dfd_grad_norm_scaled(_lib.stream_of(grads.device), grads.data_ptr(), grads.numel(),
+                                                float(max_norm), scaler.data_ptr(), scratch.data_ptr(),
+                                                out.data_ptr()))
+
+
+@grad_norm_scaled.register_fake
+def _(grads, max_norm, scaler, scratch, out):
+    return None
+
+
+@torch.library.custom_op("dfd::adam_step_scaled", mutates_args=("params", "grads", "exp_avg", "exp_avg_sq"),
+                         device_types="cuda")
+def adam_step_scaled(params: Tensor, grads: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, lr: float, beta1: float,
+                     beta2: float, eps: float, weight_decay: float, grad_scale: float, decoupled: bool,
+                     clip: Optional[Tensor], scaler: Tensor) -> None:
+    """dfd::adam_step on grads / scale, skipped on device when the scaler saw a non-finite norm; the
+    bias corrections count applied steps only (scaler[3])."""
+    _lib.check(_lib.load().dfd_adam_step_scaled(_lib.stream_of(params.device), params.data_ptr(), grads.data_ptr(),
+                                                exp_avg.data_ptr(), exp_avg_sq.data_ptr(), params.numel(), float(lr),
+                                                float(beta1), float(beta2), float(eps), float(weight_decay),
+                                                float(grad_scale), 1 if decoupled else 0,
+                                                None if clip is None else clip.data_ptr(), scaler.data_ptr()))
+
+
+@adam_step_scaled.register_fake
+def _(params, grads, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, grad_scale, decoupled, clip, scaler):
+    return None
+
+
+@torch.library.custom_op("dfd::loss_scale_update", mutates_args=("scaler",), device_types="cuda")
+def loss_scale_update(scaler: Tensor, growth_factor: float, backoff_factor: float, growth_interval: int) -> None:
+    """GradScaler.update on the device state (no host synchronisation)."""
+    _lib.check(_lib.load().dfd_loss_scale_update(_lib.stream_of(scaler.device), scaler.data_ptr(),
+                                                 float(growth_factor), float(backoff_factor), int(growth_interval)))
+
+
+@loss_scale_update.register_fake
+def _(scaler, growth_factor, backoff_factor, growth_interval):
+    return None
+
+
 # ---------------------------------------------------------------- input pipeline
 @torch.library.custom_op("dfd::collate_frames", mutates_args=(), device_types="cuda")
 def collate_frames(src: Tensor, sel: Tensor, frame_shape: List[int], to_float: bool) -> Tensor:
@@ -193,4 +240,4 @@ def _(src, sel, frame_shape, to_float):
 
 
 OPS = ("b0_trunk_forward", "b0_trunk_backward", "weighted_cross_entropy", "weighted_cross_entropy_backward",
-       "grad_norm", "adam_step", "collate_frames")
+       "grad_norm", "adam_step", "grad_norm_scaled", "adam_step_scaled", "loss_scale_update", "collate_frames")

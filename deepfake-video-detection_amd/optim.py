@@ -51,6 +51,54 @@ def _flat_view(tensors):
     return flat
 
 
+class DynamicLossScaler:
+    """Dynamic loss scaling for the fp16 trunk (``compute_dtype="fp16"``), the semantics of
+    ``torch.amp.GradScaler(init_scale=2**16, growth_factor=2, backoff_factor=0.5,
+    growth_interval=2000)`` kept entirely on the device: no ``found_inf.item()`` per step.
+
+    State: 4 device floats ``[scale, growth tracker, found_inf, applied steps]``.  ``scale(loss)``
+    multiplies the loss before backward; the fused optimizer (``FusedAdam(W).set_loss_scaler``)
+    takes the norm of the scaled gradient (``found_inf`` = not finite), unscales and clips the
+    gradient inside its step kernel, skips the whole step on the device when ``found_inf`` (torch
+    skips ``optimizer.step()``), and then updates the scale.  Bias corrections count applied steps."""
+
+    def __init__(self, device, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
+                 backoff_factor: float = 0.5, growth_interval: int = 2000):
+        self.state = torch.tensor([float(init_scale), 0.0, 0.0, 0.0], dtype=torch.float32, device=device)
+        self.growth_factor = float(growth_factor)
+        self.backoff_factor = float(backoff_factor)
+        self.growth_interval = int(growth_interval)
+
+    def scale(self, loss: torch.Tensor) -> torch.Tensor:
+        return loss * self.state[0]
+
+    def update(self) -> None:
+        torch.ops.dfd.loss_scale_update(self.state, self.growth_factor, self.backoff_factor, self.growth_interval)
+
+    # host reads (synchronise; for logging / checkpoints only)
+    def get_scale(self) -> float:
+        return float(self.state[0])
+
+    def applied_steps(self) -> int:
+        return int(self.state[3])
+
+    def found_inf(self) -> bool:
+        return bool(self.state[2] != 0)
+
+    def state_dict(self):
+        st = self.state.cpu()
+        return {"scale": float(st[0]), "_growth_tracker": int(st[1]), "growth_factor": self.growth_factor,
+                "backoff_factor": self.backoff_factor, "growth_interval": self.growth_interval,
+                "applied_steps": int(st[3])}
+
+    def load_state_dict(self, sd) -> None:
+        self.growth_factor = float(sd.get("growth_factor", self.growth_factor))
+        self.backoff_factor = float(sd.get("backoff_factor", self.backoff_factor))
+        self.growth_interval = int(sd.get("growth_interval", self.growth_interval))
+        self.state.copy_(torch.tensor([float(sd["scale"]), float(sd.get("_growth_tracker", 0)), 0.0,
+                                       float(sd.get("applied_steps", 0))]))
+
+
 class _FusedAdamBase(torch.optim.Optimizer):
     decoupled = True
 
@@ -89,7 +137,17 @@ class _FusedAdamBase(torch.optim.Optimizer):
             o += p.numel()
         self._norm = torch.zeros(2, dtype=torch.float32, device=dev)
         self._scratch = torch.empty(1024, dtype=torch.float64, device=dev)
+        self.loss_scaler = None
         self._bind_state()
+
+    def set_loss_scaler(self, scaler: "DynamicLossScaler | None") -> None:
+        """Step on scaled gradients (fp16 training): see DynamicLossScaler."""
+        if scaler is not None and scaler.state.device != self._m.device:
+            raise ValueError("loss scaler state and optimizer state on different devices")
+        self.loss_scaler = scaler
+        if scaler is not None:
+            with torch.no_grad():  # bias corrections continue from this optimizer's step count (resume)
+                scaler.state[3] = float(self._step_count)
 
     def _bind_state(self):
         """``self.state[p]`` holds views of the flat moment buffers (what the kernel updates)."""
@@ -138,6 +196,8 @@ class _FusedAdamBase(torch.optim.Optimizer):
         if not ranges:
             return loss
         grads = [self._grad_range(r[2], r[3]) for r in ranges]
+        if self.loss_scaler is not None:
+            return self._step_scaled(ranges, grads, loss)
         clip = None
         if self.max_grad_norm is not None:
             allg = grads[0][0] if len(grads) == 1 else torch.cat([fg for fg, _ in grads])
@@ -161,9 +221,38 @@ class _FusedAdamBase(torch.optim.Optimizer):
                     o += t.numel()
         return loss
 
+    def _step_scaled(self, ranges, grads, loss):
+        """Scaled-gradient step: norm (+ found_inf), device-skipped Adam(W), scale update."""
+        sc = self.loss_scaler
+        if len(ranges) != 1 or ranges[0][2] != 0 or ranges[0][3] != len(self.param_groups[0]["params"]):
+            raise RuntimeError("loss-scaled step: every parameter needs a gradient (one flat range)")
+        g = self.param_groups[0]
+        (lo, hi, i0, i1), (flat_g, scatter) = ranges[0], grads[0]
+        max_norm = float(self.max_grad_norm) if self.max_grad_norm is not None else 0.0
+        torch.ops.dfd.grad_norm_scaled(flat_g, max_norm, sc.state, self._scratch, self._norm)
+        clip = self._norm if self.max_grad_norm is not None else None
+        b1, b2 = g["betas"]
+        k = self._run_of[i0]
+        ro = self._run_off[k]
+        torch.ops.dfd.adam_step_scaled(self._runs[k][0][lo - ro:hi - ro], flat_g, self._m[lo:hi], self._v[lo:hi],
+                                       float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                       float(g["weight_decay"]), float(self.grad_scale), bool(self.decoupled), clip,
+                                       sc.state)
+        sc.update()
+        self._scaled_steps = True  # per-parameter step counts live on the device (scaler applied steps)
+        if scatter is not None:
+            o = 0
+            for t in scatter:
+                t.copy_(flat_g[o:o + t.numel()].view(t.shape))
+                o += t.numel()
+        return loss
+
     # -- checkpoints: torch.optim.Adam(W)-format state ({step, exp_avg, exp_avg_sq} per parameter), so
     # a resume (src/train.py:349-387,401) works across this optimizer and torch's in both directions
     def state_dict(self):
+        if getattr(self, "_scaled_steps", False) and self.loss_scaler is not None:
+            n = self.loss_scaler.applied_steps()  # skipped (non-finite) steps did not count
+            self._steps = [n] * len(self._steps)
         for i, p in enumerate(self.param_groups[0]["params"]):
             self.state[p]["step"] = torch.tensor(float(self._steps[i]))
         return super().state_dict()
@@ -184,6 +273,9 @@ class _FusedAdamBase(torch.optim.Optimizer):
                     self._v[o:o + k].zero_()
                     self._steps[i] = 0
         self._bind_state()
+        if self.loss_scaler is not None:
+            with torch.no_grad():
+                self.loss_scaler.state[3] = float(self._step_count)
 
     @property
     def last_grad_norm(self) -> torch.Tensor:

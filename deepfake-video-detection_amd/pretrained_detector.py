@@ -19,8 +19,9 @@ Mirrors ``src/pretrained_detector.py`` of the reference:
   reference (its Sequential trunk has no ``.blocks``).
 
 Arithmetic: ``compute_dtype="fp32"`` (default -- the drop-in meets the north-star rtol 1e-3 /
-atol 1e-5 on logits and loss) or ``"bf16"`` (the training/serving performance mode; bounds in
-tests/test_b0_224_gpu.py and tests/test_serving.py).
+atol 1e-5 on logits and loss), ``"bf16"`` (the training/serving performance mode; bounds in
+tests/test_b0_224_gpu.py and tests/test_serving.py) or ``"fp16"`` (EfficientNet-B0 only: IEEE half
+storage with fp32 accumulation, trained under dynamic loss scaling by ``trainer.TrainStep``).
 
 Backbones: ``efficientnet_b0`` (the hot path: training and inference) and ``resnet50`` (the app's
 default ensemble member, ``app.py:661,1597`` -- ``resnet.ResNet50Trunk``, torchvision key names;

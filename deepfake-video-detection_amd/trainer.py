@@ -13,6 +13,10 @@ launched from inside backward as soon as a segment's gradients are enqueued (rev
 order: head, conv_head, stage 6, 5, ...), so communication overlaps the remaining backward
 (RCCL runs on its own stream); the loss is pre-divided by the world size so the sum is the
 mean.  BatchNorm statistics stay local per rank (the reference has no SyncBN).
+
+With the fp16 trunk (``compute_dtype="fp16"``) the step scales the loss by a ``DynamicLossScaler``
+before backward (fp16 activation gradients would underflow) and the fused optimizer unscales, skips
+non-finite steps and updates the scale on the device (``torch.amp.GradScaler`` semantics, no sync).
 """
 from __future__ import annotations
 
@@ -20,12 +24,12 @@ import torch
 import torch.distributed as dist
 
 from .losses import WeightedCrossEntropyLoss
-from .optim import FusedAdam, FusedAdamW
+from .optim import DynamicLossScaler, FusedAdam, FusedAdamW
 
 
 class TrainStep:
     def __init__(self, model, lr=1e-4, weight_decay=1e-5, class_weights=None, max_grad_norm=1.0,
-                 optimizer="adamw", world_size: int = 1, criterion=None):
+                 optimizer="adamw", world_size: int = 1, criterion=None, loss_scale="auto"):
         self.model = model
         # the reference trainers hand the criterion in (ensemble_trainer.py:358 -> train_epoch); default:
         # the HIP weighted cross entropy
@@ -33,13 +37,21 @@ class TrainStep:
         cls = FusedAdamW if optimizer == "adamw" else FusedAdam
         self.optimizer = cls(model.parameters(), lr=lr, weight_decay=weight_decay, max_grad_norm=max_grad_norm)
         self.world_size = world_size
+        # fp16 trunk: dynamic loss scaling (torch.amp.GradScaler semantics, on the device).  "auto" =
+        # on for compute_dtype "fp16", off otherwise; or a DynamicLossScaler / None.
+        if loss_scale == "auto":
+            fp16 = getattr(model, "compute_dtype", None) == "fp16"
+            loss_scale = DynamicLossScaler(self.optimizer._m.device) if fp16 else None
+        self.loss_scaler = loss_scale
+        self.optimizer.set_loss_scaler(loss_scale)
 
     def forward_backward(self, images, labels):
         self.optimizer.zero_grad(set_to_none=True)
         out = self.model(images)
         logits = out[0] if isinstance(out, tuple) else out
         loss = self.criterion(logits, labels)
-        (loss / self.world_size if self.world_size > 1 else loss).backward()
+        l = loss / self.world_size if self.world_size > 1 else loss
+        (self.loss_scaler.scale(l) if self.loss_scaler is not None else l).backward()
         return loss, logits
 
     def __call__(self, images, labels):

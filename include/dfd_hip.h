@@ -26,6 +26,7 @@ extern "C" {
 /* dtype codes for the activation storage of the trunk */
 #define DFD_DTYPE_F32 0
 #define DFD_DTYPE_BF16 1
+#define DFD_DTYPE_F16 2 /* IEEE half storage, v_mfma_f32_16x16x32_f16 (train with dynamic loss scaling) */
 
 /* tensor kinds reported by dfd_b0_tensor_info */
 #define DFD_TENSOR_PARAM 0   /* trainable fp32 parameter (flat parameter buffer)      */
@@ -251,6 +252,21 @@ DFD_API int dfd_grad_norm(void* stream, const float* grads, int64_t n, float max
 DFD_API int dfd_adam_step(void* stream, float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                           double lr, double beta1, double beta2, double eps, double weight_decay, int step,
                           double grad_scale, int decoupled, const float* clip_out2);
+/* Dynamic loss scaling for fp16 training (replaces torch.cuda.amp.GradScaler's scale / unscale_ /
+ * step / update around the same step; no host synchronisation).  scaler_state: 4 device floats
+ * [scale, growth tracker, found_inf, applied steps].  The gradient is the SCALED one (the loss was
+ * multiplied by scale before backward).  dfd_grad_norm_scaled: as dfd_grad_norm, the norm unscaled
+ * and found_inf = (norm not finite).  dfd_adam_step_scaled: as dfd_adam_step on grads / scale (written
+ * back unscaled, and clipped with clip_out2), skipped entirely when found_inf; bias corrections from
+ * applied steps + 1.  dfd_loss_scale_update: scale *= backoff on found_inf, else *= growth after
+ * growth_interval finite steps in a row; counts the applied steps. */
+DFD_API int dfd_grad_norm_scaled(void* stream, const float* grads, int64_t n, float max_norm, float* scaler_state,
+                                 void* scratch, float* out2);
+DFD_API int dfd_adam_step_scaled(void* stream, float* params, float* grads, float* exp_avg, float* exp_avg_sq,
+                                 int64_t n, double lr, double beta1, double beta2, double eps, double weight_decay,
+                                 double grad_scale, int decoupled, const float* clip_out2, const float* scaler_state);
+DFD_API int dfd_loss_scale_update(void* stream, float* scaler_state, double growth_factor, double backoff_factor,
+                                  int growth_interval);
 
 /* Kernel-selection knobs (process-wide; returns the previous value, -1 for an unknown key).
  * "stream_min_rows": bf16 1x1 convs with at least this many rows use the streaming kernel
@@ -270,7 +286,7 @@ DFD_API int64_t dfd_set_tuning(const char* key, int64_t value);
  *   C[M][N] = pro(A)[M][K] . W[N][K]^T (+ R[M][N])
  *   pro_mode 0: a = x;  1: a = silu(x*scale[k] + shift[k]);  2: the same times gate[m / rows_per_frame][k];
  *   4: a = x * gate[m / rows_per_frame][k] (x already activated).
- * dtype DFD_DTYPE_F32 (fp32 storage) or DFD_DTYPE_BF16 (bf16 storage); fp32 accumulation; N, K
+ * dtype DFD_DTYPE_F32 (fp32 storage), DFD_DTYPE_BF16 or DFD_DTYPE_F16 (16-bit storage); fp32 accumulation; N, K
  * multiples of 8.  stats (optional, R must then be NULL): per-column partial sums of C and C^2 in
  * rows [*stat_rows][2][N] (room for 1024*2*N floats).  Used by the trunk and the kernel tests. */
 DFD_API int dfd_pw_conv(void* stream, int dtype, const void* A, const void* W, void* C, const void* R, int64_t M,

@@ -16,7 +16,8 @@ persistent grid.  Three checks:
    ``model(images)`` -> ``CrossEntropyLoss(weight)`` -> ``backward`` (``src/ensemble_trainer.py:188-198``).
    North-star tolerance: logits / frame scores / loss rtol 1e-3 atol 1e-5; every gradient norm
    within 1e-3 and its 64 leading elements within rtol 1e-3; BN running stats rtol 1e-4.
-2. **bf16 step** (the bench's dtype) against the same fp32 oracle: loss within 2 %, and the
+2. **bf16 step** (the bench's dtype) and the **fp16 step** (loss-scaled) against the same fp32
+   oracle: loss within 2 %, and the
    gradient bound of ``test_b0_224_gpu.py`` for the 32-frame batch (90 % of the tensors within 10 %
    in norm and cosine >= 0.98, every tensor cosine >= 0.85).
 3. **bf16, layer by layer** (what a fault confined to a few channels of one layer cannot escape):
@@ -108,7 +109,7 @@ def _gpu_oracle(cuda):
     return _CACHE["oracle"]
 
 
-def _hip_step(dtype, cuda):
+def _hip_step(dtype, cuda, loss_scale=1.0):
     torch.manual_seed(0)
     det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
                                      compute_dtype=dtype)
@@ -117,10 +118,10 @@ def _hip_step(dtype, cuda):
     x = _u8_frames().to(cuda).permute(0, 1, 4, 2, 3)  # the bench's feed: uint8, normalised in the stem
     logits, scores = det(x)
     loss = F.cross_entropy(logits, _labels().to(cuda), weight=CLASS_W.to(cuda))
-    loss.backward()
+    (loss * loss_scale if loss_scale != 1.0 else loss).backward()
     torch.cuda.synchronize()
     out = (logits.detach().cpu(), scores.detach().cpu(), float(loss),
-           {n: p.grad.detach().cpu() for n, p in det.named_parameters()},
+           {n: p.grad.detach().cpu() / loss_scale for n, p in det.named_parameters()},
            {n: b.detach().cpu() for n, b in det.named_buffers() if "running" in n})
     del det
     torch.cuda.empty_cache()
@@ -156,9 +157,12 @@ def test_bench_config_fp32_vs_oracle(cuda):
         torch.testing.assert_close(bufs[n], rb, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n}: {m}")
 
 
-def test_bench_config_bf16_vs_oracle(cuda):
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_bench_config_half_vs_oracle(cuda, dtype):
+    """bf16 (the bench's dtype) and fp16 (static loss scale 1024, the fp16 recipe; the bf16-only
+    fused kernels fall back to the generic 16-bit ones) against the fp32 oracle."""
     ref = _gpu_oracle(cuda)
-    logits, _, loss, grads, bufs = _hip_step("bf16", cuda)
+    logits, _, loss, grads, bufs = _hip_step(dtype, cuda, 1024.0 if dtype == "fp16" else 1.0)
     assert abs(loss - ref["loss"]) <= 2e-2 * abs(ref["loss"]), (loss, ref["loss"])
     torch.testing.assert_close(logits, ref["logits"], rtol=5e-2, atol=5e-2)
     scale = max(float(g.double().norm()) for g in ref["grads"].values())
@@ -176,7 +180,7 @@ def test_bench_config_bf16_vs_oracle(cuda):
             outside.append((n, round(float(g.norm()) / rn, 4), round(cos, 5)))
         if cos < 0.85:
             low.append((n, round(cos, 5)))
-    print(f"bf16 256 frames: {counted} gradients, min cos {min(cos_all):.5f}, median {np.median(cos_all):.5f}, "
+    print(f"{dtype} 256 frames: {counted} gradients, min cos {min(cos_all):.5f}, median {np.median(cos_all):.5f}, "
           f"{len(outside)} outside (10 %, cos 0.98): {outside}")
     assert counted >= 0.85 * len(ref["grads"])
     assert len(outside) <= 0.10 * counted, (len(outside), counted)

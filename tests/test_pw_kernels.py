@@ -36,11 +36,14 @@ def _pro(a, mode, scale, shift, gate, rpf):
     return x
 
 
-def _inputs(M, N, K, mode, rpf, seed, dev):
+TDT = {1: torch.bfloat16, 2: torch.float16}  # DFD_DTYPE_BF16 / DFD_DTYPE_F16 storage
+
+
+def _inputs(M, N, K, mode, rpf, seed, dev, dt=1):
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    a = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
-    w = (torch.randn(N, K, generator=g, device=dev) / K ** 0.5).to(torch.bfloat16)
+    a = torch.randn(M, K, generator=g, device=dev).to(TDT[dt])
+    w = (torch.randn(N, K, generator=g, device=dev) / K ** 0.5).to(TDT[dt])
     scale = torch.rand(K, generator=g, device=dev) + 0.5
     shift = torch.randn(K, generator=g, device=dev) * 0.1
     frames = (M + rpf - 1) // rpf
@@ -48,20 +51,20 @@ def _inputs(M, N, K, mode, rpf, seed, dev):
     return a, w, scale, shift, gate
 
 
-def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, tile=-1, sk=0):
+def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, tile=-1, sk=0, dt=1):
     lib = _lib_()
-    a, w, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed, dev)
+    a, w, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed, dev, dt)
     gr = torch.Generator(device=dev)
     gr.manual_seed(seed + 1)
-    r = torch.randn(M, N, generator=gr, device=dev).to(torch.bfloat16) if resid else None
-    c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    r = torch.randn(M, N, generator=gr, device=dev).to(TDT[dt]) if resid else None
+    c = torch.empty(M, N, device=dev, dtype=TDT[dt])
     st = torch.zeros(1024 * 2 * N, device=dev) if stats else None
     rows = ctypes.c_int(0)
     prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
     prev_tile = lib.dfd_set_tuning(b"gemm_tile", tile)
     prev_sk = lib.dfd_set_tuning(b"pw_sk", sk)
     try:
-        _lib.check(lib.dfd_pw_conv(_lib.stream_of(dev), 1, a.data_ptr(), w.data_ptr(), c.data_ptr(), _lib.ptr(r), M,
+        _lib.check(lib.dfd_pw_conv(_lib.stream_of(dev), dt, a.data_ptr(), w.data_ptr(), c.data_ptr(), _lib.ptr(r), M,
                                    N, K, mode, scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf,
                                    _lib.ptr(st), ctypes.byref(rows)))
         torch.cuda.synchronize()
@@ -69,17 +72,17 @@ def _run(M, N, K, mode, resid, stats, stream_min_rows, dev, rpf=3136, seed=0, ti
         lib.dfd_set_tuning(b"stream_min_rows", prev)
         lib.dfd_set_tuning(b"gemm_tile", prev_tile)
         lib.dfd_set_tuning(b"pw_sk", prev_sk)
-    ap = _pro(a, mode, scale, shift, gate, rpf).to(torch.bfloat16).float()
+    ap = _pro(a, mode, scale, shift, gate, rpf).to(TDT[dt]).float()
     ref = ap @ w.float().t()
     mag = ref.abs()
     if resid:
         # the kernel adds the residual to the fp32 accumulator and rounds once; a bf16 framework
         # rounds the conv output first, so near-cancelling sums may differ by one ulp of |conv|
         mag = mag + r.float().abs()
-        ref = ref.to(torch.bfloat16).float() + r.float()
+        ref = ref.to(TDT[dt]).float() + r.float()
     got = c.float()
     err = (got - ref).abs()
-    tol = 1e-2 * mag + 1e-2 * ref.abs().mean()
+    tol = (1e-2 if dt == 1 else 2e-3) * (mag + ref.abs().mean())
     assert bool((err <= tol).all()), f"max err {float(err.max())} (ref mean {float(ref.abs().mean())})"
     if stats:
         n = rows.value
@@ -165,20 +168,20 @@ def test_pw_conv_rejects_bad_args(cuda):
                            ctypes.byref(rows)) == -1
 
 
-def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate=False, wg_pf=None):
+def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate=False, wg_pf=None, dt=1):
     """dW[N][K] = sum_m dY[m][n] * pro(X)[m][k] (conv_pw / conv_pwl weight gradient)."""
     lib = _lib_()
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    dy = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16)
-    x, _, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed + 1, dev)
+    dy = torch.randn(M, N, generator=g, device=dev).to(TDT[dt])
+    x, _, scale, shift, gate = _inputs(M, N, K, mode, rpf, seed + 1, dev, dt)
     dw = torch.randn(N, K, device=dev) if accumulate else torch.empty(N, K, device=dev)
     dw0 = dw.clone()
     slab = torch.empty(8 << 20, device=dev)
     prev = lib.dfd_set_tuning(b"stream_min_rows", stream_min_rows)
     prev_pf = lib.dfd_set_tuning(b"wg_pf", wg_pf) if wg_pf is not None else None
     try:
-        _lib.check(lib.dfd_pw_conv_wgrad(_lib.stream_of(dev), 1, dy.data_ptr(), x.data_ptr(), M, N, K, mode,
+        _lib.check(lib.dfd_pw_conv_wgrad(_lib.stream_of(dev), dt, dy.data_ptr(), x.data_ptr(), M, N, K, mode,
                                          scale.data_ptr(), shift.data_ptr(), gate.data_ptr(), rpf, slab.data_ptr(),
                                          slab.numel(), dw.data_ptr(), 1 if accumulate else 0))
         torch.cuda.synchronize()
@@ -186,7 +189,7 @@ def _run_wgrad(M, N, K, mode, stream_min_rows, dev, rpf=3136, seed=1, accumulate
         lib.dfd_set_tuning(b"stream_min_rows", prev)
         if prev_pf is not None:
             lib.dfd_set_tuning(b"wg_pf", prev_pf)
-    xp = _pro(x, mode, scale, shift, gate, rpf).to(torch.bfloat16).double()
+    xp = _pro(x, mode, scale, shift, gate, rpf).to(TDT[dt]).double()
     ref = dy.double().t() @ xp
     if accumulate:
         ref = ref + dw0.double()
@@ -235,3 +238,23 @@ def test_pw_conv_wgrad_tiled_ring(cuda, case, wg_pf):
     wholly past the end) and a split shorter than the ring"""
     M, N, K, mode = case
     _run_wgrad(M, N, K, mode, 1 << 60, cuda, rpf=49, wg_pf=wg_pf)
+
+
+# fp16 storage (DFD_DTYPE_F16, v_mfma_f32_16x16x32_f16): the generic 16-bit tile kernels (the streaming
+# and weight-panel kernels are bf16-only); a forward / dgrad case of every prologue mode and tile, and
+# the weight gradient of every prologue mode; tolerance scaled to fp16's 2^-11 rounding
+@pytest.mark.parametrize("case", [STREAM_CASES[0], STREAM_CASES[5], STREAM_CASES[10], (12544, 192, 1152, 2, False, True),
+                                  (12544, 1280, 320, 0, False, True), (50176, 112, 672, 4, False, True),
+                                  (3001, 200, 104, 1, False, True)],
+                         ids=lambda c: "x".join(map(str, c[:3])) + f"_m{c[3]}r{int(c[4])}")
+@pytest.mark.parametrize("tile", [-1, 0, 2, 3])
+def test_pw_conv_fp16(cuda, case, tile):
+    M, N, K, mode, resid, stats = case
+    _run(M, N, K, mode, resid, stats, 0, cuda, rpf=49 if M < 20000 else 3136, tile=tile, dt=2)
+
+
+@pytest.mark.parametrize("case", [WGRAD_CASES[0], WGRAD_CASES[3], (12544, 192, 1152, 4), (12544, 1152, 192, 1),
+                                  (777, 64, 48, 0)], ids=lambda c: "x".join(map(str, c)))
+def test_pw_conv_wgrad_fp16(cuda, case):
+    M, N, K, mode = case
+    _run_wgrad(M, N, K, mode, 0, cuda, rpf=49 if M < 20000 else 3136, dt=2)

@@ -14,6 +14,8 @@ with ``criterion = nn.CrossEntropyLoss(weight=class_weights)`` (``:358``) and
 * ``FusedAdamW(max_grad_norm=1.0)`` / ``FusedAdam`` vs ``clip_grad_norm_`` + ``torch.optim.AdamW`` /
   ``Adam`` over several steps on identical gradients: parameters, clipped ``.grad``, moments, norm;
   a parameter without a gradient is skipped like torch does.
+* ``DynamicLossScaler`` + the fused optimizers (the fp16 step's device-side unscale / skip / update)
+  vs ``torch.amp.GradScaler`` around the same torch step, with injected inf / nan gradients.
 * ``TrainStep`` on ``EnsembleDetector(['efficientnet_b0'])`` in fp32 vs ``train_step_64.npz`` (the
   reference's ``EnsembleTrainer.train_epoch`` run on one batch, tests/golden/make_golden.py).
 * Optimizer checkpoints (CPU): the fused optimizers' ``state_dict`` loads into ``torch.optim.AdamW``
@@ -113,6 +115,66 @@ def test_fused_adam_vs_torch(cuda, kind, scale, freeze):
     tsd = topt.state_dict()
     for k in tsd["state"]:
         assert float(sd["state"][k]["step"]) == float(tsd["state"][k]["step"])
+
+
+# ------------------------------------------------------ dynamic loss scaling (the fp16 train step)
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["adamw", "adam"])
+def test_loss_scaled_adam_vs_torch_gradscaler(cuda, kind):
+    """DynamicLossScaler + FusedAdam(W) (device-side unscale / clip / skip / update) against
+    torch.amp.GradScaler around clip_grad_norm_ + torch.optim.AdamW / Adam, fed the same SCALED
+    gradients (the gradient of loss * scale): a non-finite step (step 2) is skipped and halves the
+    scale, growth_interval = 2 finite steps double it again; parameters, moments, clipped unscaled
+    .grad, scale and the step counts of the checkpoint match."""
+    import warnings
+
+    from deepfake_amd.optim import DynamicLossScaler
+    m = _Flat().to(cuda)
+    ref = _Flat()
+    params, rparams = list(m.parameters()), list(ref.parameters())
+    shapes = [p.shape for p in params]
+    Fused, Torch = (FusedAdamW, torch.optim.AdamW) if kind == "adamw" else (FusedAdam, torch.optim.Adam)
+    opt = Fused(params, lr=1e-3, weight_decay=1e-2, max_grad_norm=1.0)
+    topt = Torch(rparams, lr=1e-3, weight_decay=1e-2)
+    sc = DynamicLossScaler(cuda, init_scale=2.0 ** 10, growth_interval=2)
+    opt.set_loss_scaler(sc)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        tsc = torch.amp.GradScaler("cpu", init_scale=2.0 ** 10, growth_interval=2)
+    for step in range(7):
+        tsc.scale(torch.tensor(1.0))  # initialises the reference scaler's state
+        s = tsc.get_scale()
+        gs = [g * s for g in _grads(step, shapes, 10.0 if step % 3 else 1e-2)]
+        if step == 2:
+            gs[2][17] = float("inf")
+        if step == 4:
+            gs[0][0, 0] = float("nan")
+        flat = torch.cat([gg.flatten() for gg in gs]).to(cuda)
+        o = 0
+        for p, q, gg in zip(params, rparams, gs):
+            p.grad = flat[o:o + gg.numel()].view(gg.shape)
+            o += gg.numel()
+            q.grad = gg.clone()
+        tsc.unscale_(topt)
+        torch.nn.utils.clip_grad_norm_(rparams, max_norm=1.0)
+        tsc.step(topt)
+        tsc.update()
+        opt.step()
+        torch.cuda.synchronize()
+        assert sc.get_scale() == tsc.get_scale(), (step, sc.get_scale(), tsc.get_scale())
+        assert sc.found_inf() == (step in (2, 4))
+        for i, (p, q) in enumerate(zip(params, rparams)):
+            torch.testing.assert_close(p.detach().cpu(), q.detach(), rtol=1e-5, atol=1e-7,
+                                       msg=lambda t: f"step {step} param {i}: {t}")
+            if step not in (2, 4):  # torch leaves unscaled non-finite grads; the skipped step leaves them scaled
+                torch.testing.assert_close(p.grad.cpu(), q.grad, rtol=1e-5, atol=1e-8)
+            st, rst = opt.state[p], topt.state[q]
+            torch.testing.assert_close(st["exp_avg"].cpu(), rst["exp_avg"], rtol=1e-5, atol=1e-9)
+            torch.testing.assert_close(st["exp_avg_sq"].cpu(), rst["exp_avg_sq"], rtol=1e-5, atol=1e-12)
+    assert sc.applied_steps() == 5
+    sd, tsd = opt.state_dict(), topt.state_dict()
+    for k in tsd["state"]:
+        assert float(sd["state"][k]["step"]) == float(tsd["state"][k]["step"]) == 5.0
 
 
 # -------------------------------------------------------------- reference EnsembleTrainer step
