@@ -405,7 +405,7 @@ int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int6
     set_error("pw_gemm: residual only with plain input", __FILE__, __LINE__);
     return -1;
   }
-  if constexpr (is_bf16<T>) {
+  if constexpr (is16<T>) {
     // the small-K weight-panel kernel where it measured faster (tools/pw_sk_bench.py, round 4): the
     // forward products with BN statistics (K 80 / 112 / 192: -22 / -14 / -7 %) and the sub-streaming
     // row counts; the streaming kernel keeps the large stat-free data gradients (+31 / +22 % on sk)
@@ -425,7 +425,7 @@ template <typename T>
 int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,
                    int N, int K, int pro_mode, int epi) {
   Pro none{};
-  if constexpr (is_bf16<T>) {
+  if constexpr (is16<T>) {
     if (pro_mode == PRO_NONE && (epi & EPI_BIAS) && !(epi & EPI_DGELU) && bias && (R || !(epi & EPI_RESID))) {
       const int rc = launch_pw_stream(s, A, B, C, (epi & EPI_RESID) ? R : nullptr, bias, M, N, K, PRO_NONE, none,
                                       nullptr, nullptr);
@@ -623,7 +623,7 @@ int launch_pw_wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, in
                     float* slab, int64_t slab_cap, float* dW, bool accumulate) {
   if ((N & 7) || (K & 7)) { set_error("pw_wgrad: N and K must be multiples of 8", __FILE__, __LINE__); return -1; }
   if (M > (int64_t)UINT32_MAX) { set_error("pw_wgrad: M exceeds 2^32 rows", __FILE__, __LINE__); return -1; }
-  if constexpr (is_bf16<T>) {
+  if constexpr (is16<T>) {
     const int rc = launch_pw_wgrad_stream(s, dY, X, M, N, K, pro_mode, pro, slab, slab_cap, dW, accumulate);
     if (rc <= 0) return rc;
   }
@@ -669,8 +669,7 @@ template int launch_pw_wgrad<float>(hipStream_t, const float*, const float*, int
                                     float*, int64_t, float*, bool);
 template int launch_pw_wgrad<bf16>(hipStream_t, const bf16*, const bf16*, int64_t, int, int, int, const Pro&, float*,
                                    int64_t, float*, bool);
-// fp16 mode (v_mfma_f32_16x16x32_f16): the generic 16-bit tile kernels (the streaming / weight-panel
-// kernels exist for bf16 only)
+// fp16 mode (v_mfma_f32_16x16x32_f16): the same 16-bit kernels (tiled, streaming, weight panel)
 template int launch_pw_gemm<f16>(hipStream_t, const f16*, const f16*, f16*, const f16*, int64_t, int, int, int,
                                  const Pro&, float*, int*);
 template int launch_tf_gemm<f16>(hipStream_t, const f16*, const f16*, f16*, const f16*, const float*, const f16*,

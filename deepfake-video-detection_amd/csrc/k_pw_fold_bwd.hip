@@ -32,14 +32,15 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 
+template <typename T>
 struct PwFoldArgs {
-  const bf16* g;     // [M][mid]
-  const bf16* x;     // [M][cin]
-  const bf16* r;     // [M][cin] skip gradient or nullptr
-  const bf16* w1t;   // [cin][mid]
-  const bf16* q;     // [cin][cin]
+  const T* g;        // [M][mid]
+  const T* x;        // [M][cin]
+  const T* r;        // [M][cin] skip gradient or nullptr
+  const T* w1t;      // [cin][mid]
+  const T* q;        // [cin][cin]
   const float* bv;   // [cin]
-  bf16* dx;          // [M][cin]
+  T* dx;             // [M][cin]
   float *slabT, *slabG, *slabC;  // [parts][mid*cin], [parts][cin*cin], [parts][cin]
   int64_t M, rows_per_part;
   int mid, cin;
@@ -67,14 +68,14 @@ struct PfTile {
 #ifndef PF_WPE
 #define PF_WPE 3  // 144-wide: 2 -> 3 waves, 141 -> 135 us without the skip (tools/kbench fused)
 #endif
-template <int MB, int CB, bool RES, int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) void pw_fold_bwd_kernel(PwFoldArgs a) {
+template <typename T, int MB, int CB, bool RES, int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) void pw_fold_bwd_kernel(PwFoldArgs<T> a) {
   using TL = PfTile<MB, CB, R>;
   __shared__ __attribute__((aligned(16))) char smem[TL::SMEM];
   const uint4* Wf = reinterpret_cast<const uint4*>(smem);  // [CB][NC][64] fragments of [W1t | Q]
-  bf16* Gs = reinterpret_cast<bf16*>(smem + TL::W_BYTES);   // [R][GS]
-  bf16* Xs = Gs + R * TL::GS;                             // [R][XS] (+ ones column)
-  bf16* Rt = Xs + R * TL::XS;                             // [R][RS] skip gradient in, dX out
+  T* Gs = reinterpret_cast<T*>(smem + TL::W_BYTES);   // [R][GS]
+  T* Xs = Gs + R * TL::GS;                          // [R][XS] (+ ones column)
+  T* Rt = Xs + R * TL::XS;                          // [R][RS] skip gradient in, dX out
   float* bvl = reinterpret_cast<float*>(Rt + R * TL::RS);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
     for (int i = tid; i < CB * 16; i += 256) bvl[i] = i < cin ? a.bv[i] : 0.f;
   }
 
-  Raw8<bf16> rg[TL::NLG], rx[TL::NLX], rr8[RES ? TL::NLR : 1];
+  Raw8<T> rg[TL::NLG], rx[TL::NLX], rr8[RES ? TL::NLR : 1];
   auto load = [&](int64_t m0) {
 #pragma unroll
     for (int i = 0; i < TL::NLG; ++i) {
@@ -147,7 +148,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
         // the ones column (index cin) of the valid rows: G's row cin becomes the column sums
         if (cv <= cin && cin < cv + 8 && m0 + rr < mend) {
           const int j = cin - cv;
-          const uint32_t one = 0x3f80u << ((j & 1) * 16);
+          constexpr uint32_t kOne = std::is_same<T, f16>::value ? 0x3c00u : 0x3f80u;  // 1.0 in the storage type
+          const uint32_t one = kOne << ((j & 1) * 16);
           if ((j >> 1) == 0) o.x |= one;
           else if ((j >> 1) == 1) o.y |= one;
           else if ((j >> 1) == 2) o.z |= one;
@@ -175,12 +177,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
       for (int j = 0; j < 4; ++j) v[j] = acc[j] + bvl[c + j];
       if constexpr (RES) {
         const uint2 rv = *reinterpret_cast<const uint2*>(Rt + m * TL::RS + c);
-        v[0] += __uint_as_float(rv.x << 16);
-        v[1] += __uint_as_float(rv.x & 0xffff0000u);
-        v[2] += __uint_as_float(rv.y << 16);
-        v[3] += __uint_as_float(rv.y & 0xffff0000u);
+        v[0] += lo2f(rv.x, (T*)nullptr);
+        v[1] += hi2f(rv.x, (T*)nullptr);
+        v[2] += lo2f(rv.y, (T*)nullptr);
+        v[3] += hi2f(rv.y, (T*)nullptr);
       }
-      *reinterpret_cast<uint2*>(Rt + m * TL::RS + c) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      *reinterpret_cast<uint2*>(Rt + m * TL::RS + c) = make_uint2(Tr<T>::pack2(v[0], v[1]), Tr<T>::pack2(v[2], v[3]));
     };
 #pragma unroll
     for (int mj = 0; mj < R / 64; ++mj) {
@@ -196,8 +198,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
                                                                           8 * (lane >> 4));
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb)
-          ad[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, Wf[(cb * TL::NC + ch) * 64 + lane]),
-                                                           bf, ad[cb], 0, 0, 0);
+          ad[cb] = mfma16x16x32<T>(__builtin_bit_cast(bf16x8_t, Wf[(cb * TL::NC + ch) * 64 + lane]), bf, ad[cb]);
       }
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) dgrad_epi(ad[cb], m, cb);
@@ -208,9 +209,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
       const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
 #pragma unroll
       for (int sub = 0; sub < R / 32; ++sub) {
-        const bf16* Gb = Gs + sub * 32 * TL::GS;
-        const bf16* Xb = Xs + sub * 32 * TL::XS;
-        auto trx = [&](const bf16* base, int stride, int col) {
+        const T* Gb = Gs + sub * 32 * TL::GS;
+        const T* Xb = Xs + sub * 32 * TL::XS;
+        auto trx = [&](const T* base, int stride, int col) {
           const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + (8 * gq + q) * stride + col + 4 * p));
           const s16x4_t hi =
               __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(base + (8 * gq + 4 + q) * stride + col + 4 * p));
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
           if (kb < kbt) {  // uniform
             const bf16x8_t gk = trx(Gb, TL::GS, kb * 16);
 #pragma unroll
-            for (int cb = 0; cb < CB; ++cb) aT[i][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(gk, xc[cb], aT[i][cb], 0, 0, 0);
+            for (int cb = 0; cb < CB; ++cb) aT[i][cb] = mfma16x16x32<T>(gk, xc[cb], aT[i][cb]);
           }
         }
 #pragma unroll
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
           const int b = wave + 4 * i, gi = b / CB, gj = b - gi * CB;
           if (gi < gib) {  // uniform
             const bf16x8_t xr = trx(Xb, TL::XS, gi * 16);
-            aG[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xr, xc[gj], aG[i], 0, 0, 0);
+            aG[i] = mfma16x16x32<T>(xr, xc[gj], aG[i]);
           }
         }
       }
@@ -279,15 +280,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF_WPE))) v
   }
 }
 
-template <int MB, int CB, int R>
-static int pf_launch(hipStream_t s, PwFoldArgs& a, float* slab, int64_t slab_cap, float* T, float* G, float* cs) {
+template <int MB, int CB, int R, typename E>
+static int pf_launch(hipStream_t s, PwFoldArgs<E>& a, float* slab, int64_t slab_cap, float* T, float* G, float* cs) {
   const int64_t per = (int64_t)a.mid * a.cin + (int64_t)a.cin * a.cin + a.cin;
   // one dispatch wave: as many parts as workgroups are co-resident (no partial second round), at
   // most what the slab holds
   static const int resident = [] {
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pw_fold_bwd_kernel<MB, CB, true, R>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pw_fold_bwd_kernel<E, MB, CB, true, R>, 256, 0) != hipSuccess ||
         per_cu < 1)
       per_cu = 1;
     return std::max(1, cus * per_cu);
@@ -300,9 +301,9 @@ static int pf_launch(hipStream_t s, PwFoldArgs& a, float* slab, int64_t slab_cap
   a.slabG = slab + parts * a.mid * a.cin;
   a.slabC = a.slabG + parts * a.cin * a.cin;
   if (a.r)
-    hipLaunchKernelGGL((pw_fold_bwd_kernel<MB, CB, true, R>), dim3((unsigned)parts), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((pw_fold_bwd_kernel<E, MB, CB, true, R>), dim3((unsigned)parts), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((pw_fold_bwd_kernel<MB, CB, false, R>), dim3((unsigned)parts), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((pw_fold_bwd_kernel<E, MB, CB, false, R>), dim3((unsigned)parts), dim3(256), 0, s, a);
   DFD_HIP_CHECK(hipGetLastError());
   DFD_TRY(launch_reduce_slabs(s, a.slabT, (int)parts, (int64_t)a.mid * a.cin, T, false));
   DFD_TRY(launch_reduce_slabs(s, a.slabG, (int)parts, (int64_t)a.cin * a.cin, G, false));
@@ -310,13 +311,14 @@ static int pf_launch(hipStream_t s, PwFoldArgs& a, float* slab, int64_t slab_cap
 }
 
 // 0: launched; 1: shape not covered (the caller runs the unfused fold launches); -1: error
-int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* r, const bf16* w1t, const bf16* q,
-                       const float* bv, bf16* dx, int64_t M, int mid, int cin, float* slab, int64_t slab_cap, float* T,
-                       float* G, float* cs) {
+template <typename E>
+int launch_pw_fold_bwd(hipStream_t s, const E* g, const E* x, const E* r, const E* w1t, const E* q, const float* bv,
+                       E* dx, int64_t M, int mid, int cin, float* slab, int64_t slab_cap, float* T, float* G,
+                       float* cs) {
   // measured (rocprof, 256 frames, against the five unfused launches): blocks.1.0 430 -> 179 us,
   // blocks.1.1 / 2.0 194 / 183 -> 112 us
   if (M <= 0 || (mid & 7) || (cin & 7) || mid > 160 || cin > 48 || M * std::max(mid, cin) >= (1ll << 31)) return 1;
-  PwFoldArgs a{g, x, r, w1t, q, bv, dx, nullptr, nullptr, nullptr, M, 0, mid, cin};
+  PwFoldArgs<E> a{g, x, r, w1t, q, bv, dx, nullptr, nullptr, nullptr, M, 0, mid, cin};
   const int mb = cdiv(mid, 32), cb = cdiv(cin, 16);
   // 64-row steps (128: 1.1-1.8x slower, one wave per SIMD on the 144-wide shapes; tools/kbench fused);
   // the 240-wide shapes (blocks.2.1, 3.0: 40 -> 240) stay on the unfused launches: in 64-row steps
@@ -329,5 +331,9 @@ int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* 
 #undef DFD_PF
   return 1;
 }
+template int launch_pw_fold_bwd<bf16>(hipStream_t, const bf16*, const bf16*, const bf16*, const bf16*, const bf16*,
+                                      const float*, bf16*, int64_t, int, int, float*, int64_t, float*, float*, float*);
+template int launch_pw_fold_bwd<f16>(hipStream_t, const f16*, const f16*, const f16*, const f16*, const f16*,
+                                     const float*, f16*, int64_t, int, int, float*, int64_t, float*, float*, float*);
 
 }  // namespace dfd

@@ -45,8 +45,8 @@ __device__ __forceinline__ int sk_swz(int r) {
 // DMA `rows` rows x KC chunks of G (row stride ld elements, kval valid chunks) into img (lane-linear,
 // row-major [rows][KC]); rows past `valid_rows` read row valid_rows - 1.  Wave w of `waves` issues
 // instructions w, w + waves, ...
-template <int KC>
-__device__ __forceinline__ void sk_dma(const bf16* __restrict__ G, int64_t ld, int64_t row0, int64_t valid_rows,
+template <int KC, typename T>
+__device__ __forceinline__ void sk_dma(const T* __restrict__ G, int64_t ld, int64_t row0, int64_t valid_rows,
                                        int kval, int rows, char* img, int w, int waves, int lane) {
   const int ninst = rows * KC / 64;
   for (int q = w; q < ninst; q += waves) {
@@ -55,7 +55,7 @@ __device__ __forceinline__ void sk_dma(const bf16* __restrict__ G, int64_t ld, i
     const int sc = p ^ sk_swz<KC>(r);
     int64_t gr = row0 + r;
     gr = gr < valid_rows ? gr : valid_rows - 1;
-    const bf16* src = sc < kval ? G + gr * ld + sc * 8 : reinterpret_cast<const bf16*>(g_skzero) + 8 * (lane & 7);
+    const T* src = sc < kval ? G + gr * ld + sc * 8 : reinterpret_cast<const T*>(g_skzero) + 8 * (lane & 7);
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_vp)(img + q * 1024), 16, 0, 0);
   }
 }
@@ -66,9 +66,9 @@ __device__ __forceinline__ void vm_wait() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int KC, int BN, bool STATS, bool RESID>
-__global__ __launch_bounds__(256, 1) void pw_sk_kernel(const bf16* __restrict__ A, const bf16* __restrict__ W,
-                                                        bf16* __restrict__ C, const bf16* __restrict__ R,
+template <typename T, int KC, int BN, bool STATS, bool RESID>
+__global__ __launch_bounds__(256, 1) void pw_sk_kernel(const T* __restrict__ A, const T* __restrict__ W,
+                                                        T* __restrict__ C, const T* __restrict__ R,
                                                         float* __restrict__ stats, int64_t M, int N, int K,
                                                         int panels, int per_panel) {
   constexpr int ROWB = KC * 16;                   // bytes per LDS row
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256, 1) void pw_sk_kernel(const bf16* __restrict__ 
   __shared__ __attribute__((aligned(16))) char smem[BIMG + 2 * AIMG + SK_BM * CS * 2];
   char* Bi = smem;
   char* const Ai0 = smem + BIMG;  // row tile images: Ai0 + buf * AIMG
-  bf16* Cs = reinterpret_cast<bf16*>(smem + BIMG + 2 * AIMG);
+  T* Cs = reinterpret_cast<T*>(smem + BIMG + 2 * AIMG);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6), wm = w >> 1, wn = w & 1;
   const int panel = (int)blockIdx.x % panels, slot = (int)blockIdx.x / panels;
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256, 1) void pw_sk_kernel(const bf16* __restrict__ 
 #pragma unroll
       for (int i = 0; i < RB; ++i)
 #pragma unroll
-        for (int j = 0; j < CB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < CB; ++j) acc[i][j] = mfma16x16x32<T>(af[i], bfr[j], acc[i][j]);
     }
     // epilogue: round, BN-stat sums of the rounded values (valid rows), stage the tile
     const int64_t m0 = t * SK_BM;
@@ -137,8 +137,8 @@ __global__ __launch_bounds__(256, 1) void pw_sk_kernel(const bf16* __restrict__ 
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int row = wm * 32 + 16 * i + 4 * (lane >> 4) + e;
-          const float v = Tr<bf16>::round(acc[i][j][e]);
-          Cs[row * CS + col] = Tr<bf16>::from_f(v);
+          const float v = Tr<T>::round(acc[i][j][e]);
+          Cs[row * CS + col] = Tr<T>::from_f(v);
           if constexpr (STATS) { cs[j] += v; cq[j] += v * v; }
         }
     }
@@ -184,10 +184,10 @@ __global__ __launch_bounds__(256, 1) void pw_sk_kernel(const bf16* __restrict__ 
   }
 }
 
-template <int KC, int BN, bool STATS, bool RESID>
-int sk_go(hipStream_t s, const bf16* A, const bf16* W, bf16* C, const bf16* R, float* stats, int64_t M, int N, int K,
+template <int KC, int BN, bool STATS, bool RESID, typename T>
+int sk_go(hipStream_t s, const T* A, const T* W, T* C, const T* R, float* stats, int64_t M, int N, int K,
           int max_rows, int* stat_rows) {
-  auto kern = pw_sk_kernel<KC, BN, STATS, RESID>;
+  auto kern = pw_sk_kernel<T, KC, BN, STATS, RESID>;
   static const int resident = [&] {
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -219,8 +219,9 @@ bool pw_sk_covers(int64_t M, int N, int K) {
          sk_bn(N, K) != 0;
 }
 
-int launch_pw_sk(hipStream_t s, const bf16* A, const bf16* W, bf16* C, const bf16* R, int64_t M, int N, int K,
-                 float* stats, int max_rows, int* stat_rows) {
+template <typename T>
+int launch_pw_sk(hipStream_t s, const T* A, const T* W, T* C, const T* R, int64_t M, int N, int K, float* stats,
+                 int max_rows, int* stat_rows) {
   if (!pw_sk_covers(M, N, K) || (R && stats)) return 1;
   const bool st = stats != nullptr, rs = R != nullptr;
 #define DFD_SK(KC_, BN_)                                                                                          \
@@ -234,5 +235,9 @@ int launch_pw_sk(hipStream_t s, const bf16* A, const bf16* W, bf16* C, const bf1
   DFD_SK(40, 64);
 #undef DFD_SK
 }
+template int launch_pw_sk<bf16>(hipStream_t, const bf16*, const bf16*, bf16*, const bf16*, int64_t, int, int, float*,
+                                int, int*);
+template int launch_pw_sk<f16>(hipStream_t, const f16*, const f16*, f16*, const f16*, int64_t, int, int, float*, int,
+                               int*);
 
 }  // namespace dfd

@@ -1,4 +1,4 @@
-// Streaming pointwise (1x1 conv) GEMM for the tall-skinny layers of EfficientNet-B0 (bf16).
+// Streaming pointwise (1x1 conv) GEMM for the tall-skinny layers of EfficientNet-B0 (16-bit: bf16 / fp16).
 //
 // Same contract as pw_gemm_kernel (k_gemm.hip) -- C[M][N] = pro(A)[M][K] . B[N][K]^T with the
 // producer's BN+SiLU(+SE gate) prologue, BN-stat partials of C's columns and the residual add
@@ -49,15 +49,15 @@ struct StreamTile {
   static constexpr int SLAB = U * 16 * CS * 2;     // bytes per wave
 };
 
-template <int KB, int U, bool RESID, int NV>
+template <typename T, int KB, int U, bool RESID, int NV>
 struct StreamRegs {
-  Raw8<bf16> a[U][KB];
+  Raw8<T> a[U][KB];
   uint4 r[RESID ? NV : 1];
 };
 
-template <int NB, int KB, int U, int MODE, bool STATS, bool RESID, bool BIAS>
-__global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                           bf16* __restrict__ C, const bf16* __restrict__ R,
+template <typename T, int NB, int KB, int U, int MODE, bool STATS, bool RESID, bool BIAS>
+__global__ __launch_bounds__(256, 2) void pw_stream_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                           T* __restrict__ C, const T* __restrict__ R,
                                                            const float* __restrict__ bias,
                                                            int64_t M, int N, int K, Pro pro,
                                                            float* __restrict__ stats, int nchunks,
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
   float* bl = red + 8 * NC;                                      // [NC] bias
   float* gl = bl + NC;                                           // [gate_frames][KP] SE gates
   using TL = StreamTile<NB, U>;
-  bf16* ct = reinterpret_cast<bf16*>(gl + gate_frames * KP) + (threadIdx.x >> 6) * (TL::SLAB / 2);  // wave's C slab
+  T* ct = reinterpret_cast<T*>(gl + gate_frames * KP) + (threadIdx.x >> 6) * (TL::SLAB / 2);  // wave's C slab
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bid = DFD_XCD_SWZ_F ? xcd_swizzle(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
 
   const int lr = lane & 15, lk = 8 * (lane >> 4), ln4 = 4 * (lane >> 4);
 
-  StreamRegs<KB, U, RESID, TL::NV> rg;
+  StreamRegs<T, KB, U, RESID, TL::NV> rg;
   auto load = [&](int64_t g0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
     // keep the LDS operand/coefficient reads inside the loop (hoisted, they would pin up to
     // 2*KP + 4*NB*KB registers per lane and spill the gated variants)
     asm volatile("" ::: "memory");
-    // ---- prologue in registers: raw A -> bf16 MFMA operands ----
+    // ---- prologue in registers: raw A -> 16-bit MFMA operands ----
     bf16x8_t af[U][KB];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -183,8 +183,8 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
 #pragma unroll
             for (int j = 0; j < 8; ++j) x[j] *= gv[j];
           }
-          const uint4 v = make_uint4(pack2bf(x[0], x[1]) & m, pack2bf(x[2], x[3]) & m, pack2bf(x[4], x[5]) & m,
-                                     pack2bf(x[6], x[7]) & m);
+          const uint4 v = make_uint4(Tr<T>::pack2(x[0], x[1]) & m, Tr<T>::pack2(x[2], x[3]) & m,
+                                     Tr<T>::pack2(x[4], x[5]) & m, Tr<T>::pack2(x[6], x[7]) & m);
           af[u][kb] = __builtin_bit_cast(bf16x8_t, v);
           asm volatile("" ::: "memory");  // one k-block's coefficients live at a time
         }
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
         const bf16x8_t wf = __builtin_bit_cast(bf16x8_t, Bs[(nb * KB + kb) * 64 + lane]);
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          acc[u][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, af[u][kb], acc[u][nb], 0, 0, 0);
+          acc[u][nb] = mfma16x16x32<T>(wf, af[u][kb], acc[u][nb]);
       }
 
     // ---- epilogue: lane = row lr, channels n .. n+3: stats from registers, bf16 into the slab ----
@@ -225,11 +225,12 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[u][nb][r] += bl[nb * 16 + ln4 + r];
         }
-        const uint2 pk = make_uint2(pack2bf(acc[u][nb][0], acc[u][nb][1]), pack2bf(acc[u][nb][2], acc[u][nb][3]));
+        const uint2 pk =
+            make_uint2(Tr<T>::pack2(acc[u][nb][0], acc[u][nb][1]), Tr<T>::pack2(acc[u][nb][2], acc[u][nb][3]));
         if constexpr (STATS) {
           const bool ok = rok && n < N;
-          const float v[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
-                              __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+          const float v[4] = {lo2f(pk.x, (T*)nullptr), hi2f(pk.x, (T*)nullptr), lo2f(pk.y, (T*)nullptr),
+                              hi2f(pk.y, (T*)nullptr)};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float w = ok ? v[r] : 0.f;
@@ -252,11 +253,12 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
         uint4 o = *reinterpret_cast<const uint4*>(ct + rr * TL::CS + cv);
         if constexpr (RESID) {
           float x[8], y[8];
-          ld8(reinterpret_cast<const bf16*>(&o), x);
-          ld8(reinterpret_cast<const bf16*>(&rres[i]), y);
+          ld8(reinterpret_cast<const T*>(&o), x);
+          ld8(reinterpret_cast<const T*>(&rres[i]), y);
 #pragma unroll
           for (int j = 0; j < 8; ++j) x[j] += y[j];
-          o = make_uint4(pack2bf(x[0], x[1]), pack2bf(x[2], x[3]), pack2bf(x[4], x[5]), pack2bf(x[6], x[7]));
+          o = make_uint4(Tr<T>::pack2(x[0], x[1]), Tr<T>::pack2(x[2], x[3]), Tr<T>::pack2(x[4], x[5]),
+                         Tr<T>::pack2(x[6], x[7]));
         }
         *reinterpret_cast<uint4*>(C + row * N + n0 + cv) = o;
       }
@@ -293,12 +295,12 @@ __global__ __launch_bounds__(256, 2) void pw_stream_kernel(const bf16* __restric
   }
 }
 
-template <int NB, int KB, int MODE, bool STATS, bool RESID, bool BIAS = false>
-static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias,
+template <typename T, int NB, int KB, int MODE, bool STATS, bool RESID, bool BIAS = false>
+static int stream_launch(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias,
                          int64_t M, int N, int K, const Pro& pro, float* stats, int* stat_rows) {
   constexpr int U = KB <= 2 ? 2 : 1;
   using TL = StreamTile<NB, U>;
-  auto kern = pw_stream_kernel<NB, KB, U, MODE, STATS, RESID, BIAS>;
+  auto kern = pw_stream_kernel<T, NB, KB, U, MODE, STATS, RESID, BIAS>;
   const int nchunks = cdiv(N, NB * 16);
   const int64_t G = cdiv64(M, 16);
   const size_t lds_fixed = (size_t)NB * KB * 1024 + 2 * (size_t)KB * 32 * 4 + 9 * (size_t)NB * 16 * 4 + 4 * TL::SLAB;
@@ -330,8 +332,9 @@ static int stream_launch(hipStream_t s, const bf16* A, const bf16* B, bf16* C, c
 
 // 0: launched; 1: not covered (shape/mode without an instantiation, or M below the threshold;
 // the caller uses the tiled kernel); -1: launch error
-int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
-                     int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
+template <typename T>
+int launch_pw_stream(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N,
+                     int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows) {
   if (M <= 0 || M < tune(TK_STREAM_MIN_ROWS) || K > 256 || (N & 7) || (K & 7)) return 1;
   const int nchunks = cdiv(N, 128);
   const int NB = cdiv(cdiv(N, nchunks), 16), KB = cdiv(K, 32);
@@ -340,10 +343,10 @@ int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const
   const int key = NB * 16 + KB;
 #define DFD_STREAM_CASE(NB_, KB_, MODE_, ST_, RS_) \
   case NB_ * 16 + KB_:                             \
-    return stream_launch<NB_, KB_, MODE_, ST_, RS_>(s, A, B, C, R, bias, M, N, K, pro, stats, stat_rows);
+    return stream_launch<T, NB_, KB_, MODE_, ST_, RS_>(s, A, B, C, R, bias, M, N, K, pro, stats, stat_rows);
 #define DFD_STREAM_BIAS(NB_, KB_, RS_) \
   case NB_ * 16 + KB_:                 \
-    return stream_launch<NB_, KB_, PRO_NONE, false, RS_, true>(s, A, B, C, R, bias, M, N, K, pro, stats, stat_rows);
+    return stream_launch<T, NB_, KB_, PRO_NONE, false, RS_, true>(s, A, B, C, R, bias, M, N, K, pro, stats, stat_rows);
   if (bs) {  // x . Q + bv (+ skip gradient): the linear part of the conv_pw input gradient (bn_fold_pw)
     if (rs) {
       switch (key) {
@@ -433,9 +436,9 @@ struct WgsTile {
   static_assert((R * VY) % 64 == 0 && (R * VX) % 64 == 0, "step must be whole wave loads");
 };
 
-template <int NBW, int KBW, int S, int MODE>
-__global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __restrict__ dY,
-                                                                 const bf16* __restrict__ X, int64_t M, int N,
+template <typename T, int NBW, int KBW, int S, int MODE>
+__global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const T* __restrict__ dY,
+                                                                 const T* __restrict__ X, int64_t M, int N,
                                                                  int K, Pro pro, float* __restrict__ slab,
                                                                  int nch_n, int nch_k, int64_t rows_per_part,
                                                                  int gate_frames) {
@@ -454,8 +457,8 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
   const int cn = chunk / nch_k, ck = chunk - cn * nch_k;
   const int n0 = cn * TL::NW, k0 = ck * TL::KW;
   const int64_t mbeg = part * rows_per_part, mend = min(M, mbeg + rows_per_part);
-  bf16* Ys = reinterpret_cast<bf16*>(wave_base + wave * TL::WAVE_BYTES);
-  bf16* Xs = Ys + TL::R * TL::YS;
+  T* Ys = reinterpret_cast<T*>(wave_base + wave * TL::WAVE_BYTES);
+  T* Xs = Ys + TL::R * TL::YS;
 
   int f_first = 0;
   if constexpr (pro_is_bn(MODE)) {
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
   }
   __syncthreads();
 
-  Raw8<bf16> ry[TL::NVY], rx[TL::NVX];
+  Raw8<T> ry[TL::NVY], rx[TL::NVX];
   auto load = [&](int64_t ms) {
 #pragma unroll
     for (int i = 0; i < TL::NVY; ++i) {
@@ -531,8 +534,8 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
         }
         const uint32_t m = rx[i].ok ? 0xffffffffu : 0u;
         *reinterpret_cast<uint4*>(Xs + rr * TL::XS + cv) =
-            make_uint4(pack2bf(x[0], x[1]) & m, pack2bf(x[2], x[3]) & m, pack2bf(x[4], x[5]) & m,
-                       pack2bf(x[6], x[7]) & m);
+            make_uint4(Tr<T>::pack2(x[0], x[1]) & m, Tr<T>::pack2(x[2], x[3]) & m, Tr<T>::pack2(x[4], x[5]) & m,
+                       Tr<T>::pack2(x[6], x[7]) & m);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -541,8 +544,8 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
 #pragma unroll
     for (int sub = 0; sub < S; ++sub) {
-      const bf16* Yb = Ys + sub * 32 * TL::YS;
-      const bf16* Xb = Xs + sub * 32 * TL::XS;
+      const T* Yb = Ys + sub * 32 * TL::YS;
+      const T* Xb = Xs + sub * 32 * TL::XS;
       bf16x8_t bfr[KBW];
 #pragma unroll
       for (int kb = 0; kb < KBW; ++kb) {
@@ -558,7 +561,7 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Yb + (8 * g + 4 + q) * TL::YS + nb * 16 + 4 * p));
         const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int kb = 0; kb < KBW; ++kb) acc[nb][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[kb], acc[nb][kb], 0, 0, 0);
+        for (int kb = 0; kb < KBW; ++kb) acc[nb][kb] = mfma16x16x32<T>(af, bfr[kb], acc[nb][kb]);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -590,11 +593,11 @@ __global__ __launch_bounds__(256, 2) void pw_wgrad_stream_kernel(const bf16* __r
   }
 }
 
-template <int NBW, int KBW, int S, int MODE>
-static int wgs_launch(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, const Pro& pro,
+template <typename T, int NBW, int KBW, int S, int MODE>
+static int wgs_launch(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, const Pro& pro,
                       float* slab, int64_t slab_cap, float* dW, bool accumulate) {
   using TL = WgsTile<NBW, KBW, S>;
-  auto kern = pw_wgrad_stream_kernel<NBW, KBW, S, MODE>;
+  auto kern = pw_wgrad_stream_kernel<T, NBW, KBW, S, MODE>;
   const int nch_n = cdiv(N, TL::NW), nch_k = cdiv(K, TL::KW), chunks = nch_n * nch_k;
   const size_t lds_fixed = 2 * (size_t)TL::KW * 4 + 4 * (size_t)TL::WAVE_BYTES;
   static const int resident = [&] {
@@ -622,11 +625,12 @@ static int wgs_launch(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, i
 }
 
 // 0: launched; 1: not covered (the caller uses the tiled wgrad kernel); -1: launch error
-int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
+template <typename T>
+int launch_pw_wgrad_stream(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, int pro_mode,
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate) {
   if (M <= 0 || M < tune(TK_STREAM_MIN_ROWS) || (N & 7) || (K & 7)) return 1;
 #define DFD_WGS(NBW_, KBW_, S_, MODE_) \
-  return wgs_launch<NBW_, KBW_, S_, MODE_>(s, dY, X, M, N, K, pro, slab, slab_cap, dW, accumulate)
+  return wgs_launch<T, NBW_, KBW_, S_, MODE_>(s, dY, X, M, N, K, pro, slab, slab_cap, dW, accumulate)
   if (pro_mode == PRO_NONE) {  // conv_pw (expansion): N = mid, K = cin;  Gram x^T x: N = K = cin
     if (N == 96 && K == 16) DFD_WGS(6, 1, 2, PRO_NONE);
     if (N == 16 && K == 16) DFD_WGS(1, 1, 4, PRO_NONE);
@@ -651,5 +655,15 @@ int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t
 #undef DFD_WGS
   return 1;
 }
+
+// bf16 (the performance mode) and fp16 (v_mfma_f32_16x16x32_f16) storage
+#define DFD_STREAM_INST(T)                                                                                     \
+  template int launch_pw_stream<T>(hipStream_t, const T*, const T*, T*, const T*, const float*, int64_t, int, int, \
+                                   int, const Pro&, float*, int*);                                             \
+  template int launch_pw_wgrad_stream<T>(hipStream_t, const T*, const T*, int64_t, int, int, int, const Pro&,   \
+                                         float*, int64_t, float*, bool);
+DFD_STREAM_INST(bf16)
+DFD_STREAM_INST(f16)
+#undef DFD_STREAM_INST
 
 }  // namespace dfd

@@ -40,15 +40,16 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 
+template <typename T>
 struct PwlBwdArgs {
-  const bf16* gs;   // [M][N] (or, with coef3: the block's output gradient dZ, gs = k1*dZ + k2*y3 + k3)
-  const bf16* y3;   // [M][N] pre-BN3 projection output (with coef3)
+  const T* gs;   // [M][N] (or, with coef3: the block's output gradient dZ, gs = k1*dZ + k2*y3 + k3)
+  const T* y3;   // [M][N] pre-BN3 projection output (with coef3)
   const float* coef3;  // [3][N] BN3 backward coefficients k1, k2, k3, or nullptr (gs given)
-  const bf16* wt;   // [K][N]: row k holds W[:, k] (the cast conv_pwl weight, transposed)
-  const bf16* y2;   // [M][K]
+  const T* wt;   // [K][N]: row k holds W[:, k] (the cast conv_pwl weight, transposed)
+  const T* y2;   // [M][K]
   const float *sc, *sh, *mean, *invstd;  // BN2 (after the depthwise conv) [K]
   const float* gate;                     // SE gate [F][K]
-  bf16* ge2;                             // [M][K]
+  T* ge2;                                // [M][K]
   float* slab;                           // [parts][N][K]
   float* part;                           // [5][hsplit][F][K]
   int F, HW, N, K;
@@ -74,11 +75,12 @@ struct PbTile {
   static_assert(KBC >= 1 && KBC <= 4, "one k-block per wave");
 };
 
+template <typename T>
 __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
-  f[0] = __uint_as_float(v.x << 16);
-  f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16);
-  f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[0] = lo2f(v.x, (T*)nullptr);
+  f[1] = hi2f(v.x, (T*)nullptr);
+  f[2] = lo2f(v.y, (T*)nullptr);
+  f[3] = hi2f(v.y, (T*)nullptr);
 }
 
 // WG = false: the data gradient and the SE/BN sums only (no act tile, no weight-gradient
@@ -90,15 +92,15 @@ __device__ __forceinline__ void unpack4(uint2 v, float (&f)[4]) {
 #ifndef PWL_WPE
 #define PWL_WPE 3  // with one prefetch set: 2 -> 3 waves, -13..-16 % (tools/kbench fused)
 #endif
-template <int NG, int KBC, bool WG, int PB_R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) void pwl_bwd_kernel(PwlBwdArgs a) {
+template <typename T, int NG, int KBC, bool WG, int PB_R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) void pwl_bwd_kernel(PwlBwdArgs<T> a) {
   using TL = PbTile<NG, KBC, WG, PB_R>;
   __shared__ __attribute__((aligned(16))) char smem[TL::SMEM];
   const uint4* Ws = reinterpret_cast<const uint4*>(smem);  // [KBC][NG][64] W^T fragments
-  bf16* Gs = reinterpret_cast<bf16*>(smem + TL::W_BYTES);  // [R][GS]
-  bf16* Xs = Gs + PB_R * TL::GS;                            // [R][XS] act (WG)
-  bf16* Ys = Xs + (WG ? PB_R * TL::XS : 0);                 // [R][XS] raw y2
-  bf16* Cs = Ys + PB_R * TL::XS;                            // [R][XS] ge2
+  T* Gs = reinterpret_cast<T*>(smem + TL::W_BYTES);  // [R][GS]
+  T* Xs = Gs + PB_R * TL::GS;                         // [R][XS] act (WG)
+  T* Ys = Xs + (WG ? PB_R * TL::XS : 0);              // [R][XS] raw y2
+  T* Cs = Ys + PB_R * TL::XS;                         // [R][XS] ge2
   float* co = reinterpret_cast<float*>(Cs + PB_R * TL::XS);  // [4][KC] sc sh mean invstd
   float* c3 = co + 4 * TL::KC;                                // [3][NP] BN3 k1 k2 k3 (coef3)
   float* gl = c3 + 3 * TL::NP;                                // [KC] SE gate of a one-frame part
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
 
   // NS register sets: the rows of step st + NS are loaded while step st is staged and computed
   constexpr int NS = PWL_RING;
-  Raw8<bf16> rg[NS][TL::NLG], r3[NS][TL::NLG], ry[NS][TL::NLK];
+  Raw8<T> rg[NS][TL::NLG], r3[NS][TL::NLG], ry[NS][TL::NLK];
   const bool bn3 = a.coef3 != nullptr;
   auto load = [&](auto setc, int st) {
     constexpr int S = decltype(setc)::value;
@@ -225,8 +227,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
 #pragma unroll
           for (int j = 0; j < 8; ++j) z[j] = k1[j] * z[j] + k2[j] * y[j] + k3[j];
           *reinterpret_cast<uint4*>(Gs + rr * TL::GS + cv) =
-              make_uint4(pack2bf(z[0], z[1]) & msk, pack2bf(z[2], z[3]) & msk, pack2bf(z[4], z[5]) & msk,
-                         pack2bf(z[6], z[7]) & msk);
+              make_uint4(Tr<T>::pack2(z[0], z[1]) & msk, Tr<T>::pack2(z[2], z[3]) & msk, Tr<T>::pack2(z[4], z[5]) & msk,
+                         Tr<T>::pack2(z[6], z[7]) & msk);
         } else {
           raw_st(Gs + rr * TL::GS + cv, rg[S][i]);
         }
@@ -248,8 +250,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = siluf_(x[j] * sc[j] + sh[j]) * gv[j];
         *reinterpret_cast<uint4*>(Xs + rr * TL::XS + cv) =
-            make_uint4(pack2bf(x[0], x[1]) & msk, pack2bf(x[2], x[3]) & msk, pack2bf(x[4], x[5]) & msk,
-                       pack2bf(x[6], x[7]) & msk);
+            make_uint4(Tr<T>::pack2(x[0], x[1]) & msk, Tr<T>::pack2(x[2], x[3]) & msk, Tr<T>::pack2(x[4], x[5]) & msk,
+                       Tr<T>::pack2(x[6], x[7]) & msk);
       }
     }
     lds_barrier();
@@ -268,7 +270,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
         for (int mb = 0; mb < PB_R / 16; ++mb) {
           const bf16x8_t gf = *reinterpret_cast<const bf16x8_t*>(Gs + (mb * 16 + (lane & 15)) * TL::GS + ng * 32 +
                                                                  8 * (lane >> 4));
-          ad[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, gf, ad[mb], 0, 0, 0);
+          ad[mb] = mfma16x16x32<T>(wf, gf, ad[mb]);
         }
       }
       // ---- epilogue: bf16 ge2 into the C tile, SE/BN sums against y2 of the same 4 channels ----
@@ -276,11 +278,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
       for (int mb = 0; mb < PB_R / 16; ++mb) {
         const int m = mb * 16 + (lane & 15);
         const float rv = pb + m < pe ? 1.f : 0.f;
-        const uint2 pk = make_uint2(pack2bf(ad[mb][0], ad[mb][1]), pack2bf(ad[mb][2], ad[mb][3]));
+        const uint2 pk = make_uint2(Tr<T>::pack2(ad[mb][0], ad[mb][1]), Tr<T>::pack2(ad[mb][2], ad[mb][3]));
         *reinterpret_cast<uint2*>(Cs + m * TL::XS + kl) = pk;
         float d[4], y[4];
-        unpack4(pk, d);
-        unpack4(*reinterpret_cast<const uint2*>(Ys + m * TL::XS + kl), y);
+        unpack4<T>(pk, d);
+        unpack4<T>(*reinterpret_cast<const uint2*>(Ys + m * TL::XS + kl), y);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float z = y[r] * csc[r] + csh[r];
@@ -299,8 +301,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
       const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
 #pragma unroll
       for (int sub = 0; sub < (WG ? PB_R / 32 : 0); ++sub) {
-        const bf16* Gb = Gs + sub * 32 * TL::GS;
-        const bf16* Xb = Xs + sub * 32 * TL::XS;
+        const T* Gb = Gs + sub * 32 * TL::GS;
+        const T* Xb = Xs + sub * 32 * TL::XS;
         const s16x4_t xlo =
             __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(Xb + (8 * g + q) * TL::XS + wave * 16 + 4 * p));
         const s16x4_t xhi =
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
             const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (lds_s16x4_t*)(Gb + (8 * g + 4 + q) * TL::GS + nb * 16 + 4 * p));
             const bf16x8_t af = bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            aw[WG ? nb : 0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, aw[WG ? nb : 0], 0, 0, 0);
+            aw[WG ? nb : 0] = mfma16x16x32<T>(af, bfr, aw[WG ? nb : 0]);
           }
         }
       }
@@ -374,11 +376,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
   }
 }
 
-template <int NG, int KBC, bool WG, int PB_R>
-static int pb_launch(hipStream_t s, PwlBwdArgs& a, int64_t slab_cap, float* dW, bool accumulate, int64_t part_cap,
+template <int NG, int KBC, bool WG, int PB_R, typename T>
+static int pb_launch(hipStream_t s, PwlBwdArgs<T>& a, int64_t slab_cap, float* dW, bool accumulate, int64_t part_cap,
                      int* hsplit_out) {
   using TL = PbTile<NG, KBC, WG, PB_R>;
-  auto kern = pwl_bwd_kernel<NG, KBC, WG, PB_R>;
+  auto kern = pwl_bwd_kernel<T, NG, KBC, WG, PB_R>;
   a.nkc = cdiv(a.K, TL::KC);
   const int64_t per = WG ? (int64_t)a.N * a.K : 0;  // slab floats per part
   int64_t parts;
@@ -389,7 +391,7 @@ static int pb_launch(hipStream_t s, PwlBwdArgs& a, int64_t slab_cap, float* dW, 
     static const int resident = [] {
       int dev = 0, cus = 256, per_cu = 1;
       if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pwl_bwd_kernel<NG, KBC, WG, PB_R>, 256, 0) != hipSuccess ||
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pwl_bwd_kernel<T, NG, KBC, WG, PB_R>, 256, 0) != hipSuccess ||
           per_cu < 1)
         per_cu = 1;
       return std::max(1, cus * per_cu);
@@ -422,18 +424,21 @@ static int pb_launch(hipStream_t s, PwlBwdArgs& a, int64_t slab_cap, float* dW, 
   return launch_reduce_slabs(s, a.slab, (int)parts, per, dW, accumulate);
 }
 
+#ifndef DFD_PWL_F16_TU
 // 0: launched (all three outputs); 2: launched without the weight gradient (the caller runs it);
 // 1: shape not covered (the caller runs the three unfused launches); -1: error
 bool pwl_bwd_covers(int frames, int HW, int N, int K) {
   return frames > 0 && HW > 0 && !(N & 7) && !(K & 15) && N <= 24 && (int64_t)frames * HW * std::max(N, K) < (1ll << 31);
 }
+#endif
 
-int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* y3, const float* coef3, const bf16* wt, const bf16* y2,
+template <typename T>
+int launch_pwl_bwd(hipStream_t s, const T* gs, const T* y3, const float* coef3, const T* wt, const T* y2,
                    const float* sc, const float* sh, const float* mean, const float* invstd, const float* gate,
-                   int frames, int HW, int N, int K, bf16* ge2, float* slab, int64_t slab_cap, float* dW,
+                   int frames, int HW, int N, int K, T* ge2, float* slab, int64_t slab_cap, float* dW,
                    bool accumulate, float* part, int64_t part_cap, int* hsplit) {
   if (!pwl_bwd_covers(frames, HW, N, K) || (coef3 && !y3)) return 1;
-  PwlBwdArgs a{gs, y3, coef3, wt, y2, sc, sh, mean, invstd, gate, ge2, slab, part, frames, HW, N, K, 1, 1, 1};
+  PwlBwdArgs<T> a{gs, y3, coef3, wt, y2, sc, sh, mean, invstd, gate, ge2, slab, part, frames, HW, N, K, 1, 1, 1};
   const int ng = cdiv(N, 32);
   const int kbc = K <= 32 ? 2 : 3;
   // 64-row steps: 128-row steps doubled the staging registers to one wave per SIMD and measured
@@ -453,5 +458,20 @@ int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* y3, const float* c
 #undef DFD_PB
   return 1;
 }
+#define DFD_PWL_INST(T)                                                                                        \
+  template int launch_pwl_bwd<T>(hipStream_t, const T*, const T*, const float*, const T*, const T*, const float*, \
+                                 const float*, const float*, const float*, const float*, int, int, int, int, T*,   \
+                                 float*, int64_t, float*, bool, float*, int64_t, int*);
+// The fp16 instance is compiled in its own translation unit (k_pwl_bwd_f16.hip) without SLP
+// vectorisation: its SLP-packed (v_pk_*_f32) BN2 sums gave run-to-run different sum(d * silu') and
+// sum(d * silu' * xhat) partials on MI355X (tools/pwl_det: 16-185 of F x K entries differ between two
+// identical launches at 32 frames; the d-free sums and the data / weight gradients bit-identical),
+// the same source without SLP is bit-reproducible like the bf16 instance
+#ifdef DFD_PWL_F16_TU
+DFD_PWL_INST(f16)
+#else
+DFD_PWL_INST(bf16)
+#endif
+#undef DFD_PWL_INST
 
 }  // namespace dfd

@@ -16,27 +16,31 @@ namespace dfd {
 template <typename T>
 int launch_pw_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, int64_t M, int N, int K,
                    int pro_mode, const Pro& pro, float* stats, int* stat_rows);
-// Streaming variant for tall-skinny bf16 layers (k_pw_stream.hip): 0 launched, 1 not covered
-// (shape/mode without an instantiation, or M below the streaming threshold), -1 error.
-int launch_pw_stream(hipStream_t s, const bf16* A, const bf16* B, bf16* C, const bf16* R, const float* bias, int64_t M,
-                     int N, int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows);
-int launch_pw_wgrad_stream(hipStream_t s, const bf16* dY, const bf16* X, int64_t M, int N, int K, int pro_mode,
+// Streaming variant for tall-skinny 16-bit layers (k_pw_stream.hip; T = bf16 / f16): 0 launched, 1 not
+// covered (shape/mode without an instantiation, or M below the streaming threshold), -1 error.
+template <typename T>
+int launch_pw_stream(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, int64_t M, int N,
+                     int K, int pro_mode, const Pro& pro, float* stats, int* stat_rows);
+template <typename T>
+int launch_pw_wgrad_stream(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, int pro_mode,
                            const Pro& pro, float* slab, int64_t slab_cap, float* dW, bool accumulate);
-// Fused projection backward (k_pwl_bwd.hip, bf16): ge2 = gs . W (wt = W^T [K][N]), the weight gradient
+// Fused projection backward (k_pwl_bwd.hip, T = bf16 / f16): ge2 = gs . W (wt = W^T [K][N]), the weight gradient
 // dW[N][K] (+)= gs^T . (silu(y2*sc+sh) * gate) through the slab, and the per-frame SE + BN2 backward
 // sums part[5][*hsplit][frames][K] of launch_se_bn_bwd_reduce.  With coef3 (the BN3 backward
 // coefficients [3][N]) gs is the block's output gradient dZ and the kernel applies the BN3 backward
 // gs = k1*dZ + k2*y3 + k3 while staging (no separate apply pass).  0 launched, 1 not covered, -1 error.
 bool pwl_bwd_covers(int frames, int HW, int N, int K);
-int launch_pwl_bwd(hipStream_t s, const bf16* gs, const bf16* y3, const float* coef3, const bf16* wt, const bf16* y2,
+template <typename T>
+int launch_pwl_bwd(hipStream_t s, const T* gs, const T* y3, const float* coef3, const T* wt, const T* y2,
                    const float* sc, const float* sh, const float* mean, const float* invstd, const float* gate,
-                   int frames, int HW, int N, int K, bf16* ge2, float* slab, int64_t slab_cap, float* dW,
+                   int frames, int HW, int N, int K, T* ge2, float* slab, int64_t slab_cap, float* dW,
                    bool accumulate, float* part, int64_t part_cap, int* hsplit);
-// Fused conv_pw backward through its BN on the fold path (k_pw_fold_bwd.hip, bf16): dx = g . w1t^T +
+// Fused conv_pw backward through its BN on the fold path (k_pw_fold_bwd.hip, T = bf16 / f16): dx = g . w1t^T +
 // x . q^T + bv (+ r), and the partial products T = g^T x, G = x^T x, cs = 1^T x summed into T / G / cs
 // (launch_reduce_slabs) for pw_wgrad_bn_combine.  0 launched, 1 not covered, -1 error.
-int launch_pw_fold_bwd(hipStream_t s, const bf16* g, const bf16* x, const bf16* r, const bf16* w1t, const bf16* q,
-                       const float* bv, bf16* dx, int64_t M, int mid, int cin, float* slab, int64_t slab_cap, float* T,
+template <typename E>
+int launch_pw_fold_bwd(hipStream_t s, const E* g, const E* x, const E* r, const E* w1t, const E* q,
+                       const float* bv, E* dx, int64_t M, int mid, int cin, float* slab, int64_t slab_cap, float* T,
                        float* G, float* cs);
 // Kernel-selection knobs.  No process-wide mutable state is consulted on a model path: every knob
 // has a compile-time default (tune_default), a plan's forward/backward installs the plan's own
@@ -186,12 +190,13 @@ int blaslt_wgrad_split(hipStream_t s, const bf16* dY, const bf16* X, float* dW, 
 int blaslt_gemm(hipStream_t s, int dtype, const void* A, const void* B, void* C, const void* R, const float* bias,
                 bool relu, int64_t M, int N, int K);
 
-// small-K (80 / 112 / 192 / 320) bf16 1x1 GEMM with the weight panel resident in LDS and LDS-DMA row
-// tiles (k_pw_sk.hip): 0 launched, 1 not covered; stats as launch_pw_gemm (one partial row per
-// workgroup, at most max_rows rows), R (residual) or stats, not both
+// small-K (80 / 112 / 192 / 320) 16-bit 1x1 GEMM with the weight panel resident in LDS and LDS-DMA row
+// tiles (k_pw_sk.hip; T = bf16 / f16): 0 launched, 1 not covered; stats as launch_pw_gemm (one partial
+// row per workgroup, at most max_rows rows), R (residual) or stats, not both
 bool pw_sk_covers(int64_t M, int N, int K);
-int launch_pw_sk(hipStream_t s, const bf16* A, const bf16* W, bf16* C, const bf16* R, int64_t M, int N, int K,
-                 float* stats, int max_rows, int* stat_rows);
+template <typename T>
+int launch_pw_sk(hipStream_t s, const T* A, const T* W, T* C, const T* R, int64_t M, int N, int K, float* stats,
+                 int max_rows, int* stat_rows);
 template <typename T>
 int launch_tf_gemm(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bias, const T* Z, int64_t M,
                    int N, int K, int pro_mode, int epi);

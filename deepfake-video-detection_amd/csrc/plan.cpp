@@ -646,7 +646,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         i3.dZ = gout; i3.rows_per_frame = hwo; i3.silu = false;
         DFD_TRY(join(p.ev[1], gs_busy));  // the previous conv_pwl weight gradient is done with o_gs
         int hs = 1, pf = 1;
-        const bool fpwl = is_bf16<T> && tune(TK_PWL_FUSED) != 0 &&
+        const bool fpwl = is16<T> && tune(TK_PWL_FUSED) != 0 &&
                           pwl_bwd_covers(p.frames, hwo, b.cout, b.mid);
         // the BN3 backward applied in the fused kernel's staging pays where the projection is 16 wide
         // (blocks.0.0: +12 us in the kernel against a 49 us apply pass); at 24 wide the kernel's
@@ -660,8 +660,8 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
           DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), rows, Mout, b.cout, r.prm(b.bn3.t_w), r.f(b.bn3.o_mean),
                                          r.f(b.bn3.o_invstd), tr != 0, grad(b.bn3.t_w), grad(b.bn3.t_b), acc != 0,
                                          r.f(p.o_coef)));
-          if constexpr (is_bf16<T>) {
-            PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, gout, r.a(b.o_y3), r.f(p.o_coef), r.a(b.pwl.o_wt),
+          if constexpr (is16<T>) {
+            PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd<T>(s, gout, r.a(b.o_y3), r.f(p.o_coef), r.a(b.pwl.o_wt),
                                                            r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                                            r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), r.f(b.o_gate),
                                                            p.frames, hwo, b.cout, b.mid, r.a(p.o_ge2), slab(),
@@ -677,8 +677,8 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         } else {
           DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
           if (fpwl) {
-            if constexpr (is_bf16<T>) {
-              PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd(s, r.a(p.o_gs), nullptr, nullptr, r.a(b.pwl.o_wt),
+            if constexpr (is16<T>) {
+              PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd<T>(s, r.a(p.o_gs), nullptr, nullptr, r.a(b.pwl.o_wt),
                                                              r.a(b.o_y2), r.f(bn_dw.o_scale), r.f(bn_dw.o_shift),
                                                              r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), r.f(b.o_gate),
                                                              p.frames, hwo, b.cout, b.mid, r.a(p.o_ge2), slab(),
@@ -799,10 +799,10 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                        r.f(p.o_bv)));
           DFD_TRY(join(p.ev[1], gs_busy));  // the conv_pwl weight gradient is done with o_gs
           int ff = 1;
-          if (is_bf16<T> && tune(TK_FOLD_FUSED) != 0) {
+          if (is16<T> && tune(TK_FOLD_FUSED) != 0) {
             // x . Q, the data gradient and the partial products g^T x, x^T x, 1^T x in one pass
             // (k_pw_fold_bwd.hip); their three slab reductions as ONE batched launch
-            if constexpr (is_bf16<T>) {
+            if constexpr (is16<T>) {
               float* const parts[3] = {r.f(p.o_tg), r.f(p.o_gram), r.f(p.o_cs)};
               const int64_t extent[3] = {(int64_t)b.mid * b.cin, (int64_t)b.cin * b.cin, (int64_t)b.cin};
               SlabDefer loc{};

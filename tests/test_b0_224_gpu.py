@@ -127,8 +127,9 @@ def test_train_step_224_fp32(cuda, case, kernel_paths):
 # sums (round 5), hence 0.65.  For scale: torch's own bf16 autocast of the same oracle step on the CPU
 # (tools/r05/bf16_floor.py) leaves 191 / 202 (2 frames) and 47 / 202 (32 frames) outside.
 BF16_BOUND = {"b1t2": (0.65, 0.85), "b4t8": (0.90, 0.85)}
-# fp16 storage (10 mantissa bits against bf16's 7) under a static loss scale of 1024
-FP16_BOUND = {"b1t2": (0.65, 0.85), "b4t8": (0.90, 0.85)}
+# fp16 storage (10 mantissa bits against bf16's 7) under a static loss scale of 1024: measured 0 of 202
+# tensors outside on both batches (round 5, call E), every cosine >= 0.98
+FP16_BOUND = {"b1t2": (0.95, 0.97), "b4t8": (0.97, 0.98)}
 FP16_LOSS_SCALE = 1024.0
 
 
@@ -182,6 +183,22 @@ def test_train_step_224_fp16(cuda, case):
     _bf16_vs_oracle(case, loss, grads, "/fp16", bound=FP16_BOUND)
     for n, rb in ref["bufs"].items():
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+def test_step_224_bit_reproducible(cuda, dtype):
+    """Two identical 32-frame 224^2 training steps give bit-identical loss, gradients and BN running
+    statistics in both 16-bit modes.  This shape reaches the fused projection backward at its
+    dispatched hsplit: the first fp16 build of that kernel (SLP-packed BN2 sums) differed run to run
+    there while passing every tolerance test at 64^2 (tools/pwl_det)."""
+    a = hip_step("b4t8", dtype, cuda, loss_scale=FP16_LOSS_SCALE if dtype == "fp16" else 1.0)
+    b = hip_step("b4t8", dtype, cuda, loss_scale=FP16_LOSS_SCALE if dtype == "fp16" else 1.0)
+    assert a[2] == b[2]
+    assert torch.equal(a[0], b[0])
+    diff = [n for n in a[3] if not torch.equal(a[3][n], b[3][n])]
+    assert not diff, diff[:8]
+    for n in a[4]:
+        assert torch.equal(a[4][n], b[4][n]), n
 
 
 def test_wgrad_stream_bit_identical(cuda):

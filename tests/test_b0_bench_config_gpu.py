@@ -57,7 +57,7 @@ EPS = 1e-5
 
 # bf16 layer-by-layer bounds: per-channel relative L2 error of a conv output recomputed from the
 # kernel's own bf16 inputs (output rounding 2^-9 + the bf16 rounding of the 1x1 GEMMs' A operand)
-FWD_CH_TOL = 1e-2  # measured worst 3.2e-3 (conv_pwl of stages 5-6)
+FWD_CH_TOL = 1e-2  # measured worst 3.2e-3 (conv_pwl of stages 5-6); fp16: 3.9e-4, held to 0.2x
 # per-stage backward: relative L2 error of the stage-input gradient and of each parameter gradient
 # (the recompute keeps fp32 intermediates where the HIP step stores bf16 ones), and the minimum
 # cosine of every depthwise-weight-gradient channel
@@ -183,8 +183,11 @@ def test_bench_config_half_vs_oracle(cuda, dtype):
     print(f"{dtype} 256 frames: {counted} gradients, min cos {min(cos_all):.5f}, median {np.median(cos_all):.5f}, "
           f"{len(outside)} outside (10 %, cos 0.98): {outside}")
     assert counted >= 0.85 * len(ref["grads"])
-    assert len(outside) <= 0.10 * counted, (len(outside), counted)
+    # fp16: measured 0 outside, min cosine 0.9976 (round 5) -- held to 2 % and cosine 0.99
+    assert len(outside) <= (0.10 if dtype == "bf16" else 0.02) * counted, (len(outside), counted)
     assert not low, low
+    if dtype == "fp16":
+        assert min(cos_all) >= 0.99, min(cos_all)
     for n, rb in ref["bufs"].items():
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
 
@@ -221,33 +224,40 @@ def _bn_act(y, gamma, beta, act=True):
     return F.silu(z) if act else z
 
 
-def _view(ws, off, rows, cols):
+TDT = {"bf16": torch.bfloat16, "fp16": torch.float16}
+DTC = {"bf16": 1, "fp16": 2}
+
+
+def _view(ws, off, rows, cols, dt=torch.bfloat16):
     n = rows * cols
-    return ws[off:off + 2 * n].view(torch.bfloat16).view(rows, cols)
+    return ws[off:off + 2 * n].view(dt).view(rows, cols)
 
 
-def _saved(lib, h, ws):
+def _saved(lib, h, ws, dt=torch.bfloat16):
     off, rows, cols = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     out, i = [], 0
     while lib.dfd_b0_saved_tensor(h, i, ctypes.byref(off), ctypes.byref(rows), ctypes.byref(cols)) == 0:
-        out.append(_view(ws, off.value, rows.value, cols.value).float().clone())
+        out.append(_view(ws, off.value, rows.value, cols.value, dt).float().clone())
         i += 1
     return out
 
 
-def _grad_in(lib, h, ws, block):
+def _grad_in(lib, h, ws, block, dt=torch.bfloat16):
     off, rows, cols = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     _lib.check(lib.dfd_b0_grad_tensor(h, block, ctypes.byref(off), ctypes.byref(rows), ctypes.byref(cols)))
-    return _view(ws, off.value, rows.value, cols.value).float().clone()
+    return _view(ws, off.value, rows.value, cols.value, dt).float().clone()
 
 
-@pytest.fixture(scope="module")
-def bf16_run(cuda):
-    """One bf16 trunk forward + segment-by-segment backward at the bench shape, with every saved
-    activation and every stage-boundary gradient copied out."""
+@pytest.fixture(scope="module", params=["bf16", "fp16"])
+def bf16_run(cuda, request):
+    """One 16-bit trunk forward + segment-by-segment backward at the bench shape, with every saved
+    activation and every stage-boundary gradient copied out: bf16 (the bench's dtype) and fp16 (the
+    feature gradient carries a loss scale of 2^15; every check below is relative, so scale-free)."""
+    dtype = request.param
+    dt = TDT[dtype]
     lib = _lib.load()
     det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
-                                     compute_dtype="bf16")
+                                     compute_dtype=dtype)
     deterministic_init_(det, seed=SEED)
     det = det.to(cuda).train()
     trunk = det.backbone
@@ -256,11 +266,11 @@ def bf16_run(cuda):
     rt.set_input_norm("imagenet")
     x = _u8_frames().to(cuda).permute(0, 1, 4, 2, 3).reshape(N, 3, HW, HW)
     with torch.no_grad():
-        feats, (h, ws) = rt.forward(x, det, 1, True)
+        feats, (h, ws) = rt.forward(x, det, DTC[dtype], True)
         torch.cuda.synchronize()
-        saved = _saved(lib, h, ws)
+        saved = _saved(lib, h, ws, dt)
         g = torch.Generator(device=cuda).manual_seed(9)
-        dfeat = torch.randn(N, 1280, device=cuda, generator=g) * 1e-3
+        dfeat = torch.randn(N, 1280, device=cuda, generator=g) * (1e-3 if dtype == "bf16" else 1e-3 * 2.0 ** 15)
         grads = torch.zeros_like(det._flat_p)
         nb = 16
         # block index whose input gradient is final after segment s (0 = head ... 7 = stage 0)
@@ -274,21 +284,25 @@ def bf16_run(cuda):
             rt.backward(h, ws, x, dfeat, det, grads, True, s, s + 1)
             torch.cuda.synchronize()
             if s == 0:
-                gin[nb] = _grad_in(lib, h, ws, nb)
+                gin[nb] = _grad_in(lib, h, ws, nb, dt)
             elif s <= 7 and first[7 - s] > 0:
-                gin[first[7 - s]] = _grad_in(lib, h, ws, first[7 - s])
+                gin[first[7 - s]] = _grad_in(lib, h, ws, first[7 - s], dt)
+    for k_, v_ in sorted(gin.items()):
+        a_ = v_.abs()
+        print(f"{dtype} grad into block {k_}: max {float(a_.max()):.3g} median {float(a_.median()):.3g} "
+              f"below 2^-14 {float((a_ < 2.0 ** -14).float().mean()):.3f} zero {float((a_ == 0).float().mean()):.3f}")
     sd = {k: v.detach() for k, v in det.state_dict().items()}
     po = det.param_offsets()
     hip_grads = {n: grads[po[n]:po[n] + p.numel()].view_as(p).detach().clone() for n, p in det.named_parameters()}
     out = dict(x=x, feats=feats.detach().clone(), saved=saved, dfeat=dfeat, gin=gin, sd=sd, grads=hip_grads,
-               first=first)
+               first=first, dtype=dtype, dt=dt)
     yield out
     del det, ws
 
 
-def _pw_bf16(w):
-    """1x1 conv weights as the bf16 GEMMs see them (launch_cast_params rounds the fp32 masters)."""
-    return w.reshape(w.shape[0], w.shape[1]).bfloat16().float()
+def _pw_bf16(w, dt=torch.bfloat16):
+    """1x1 conv weights as the 16-bit GEMMs see them (launch_cast_params rounds the fp32 masters)."""
+    return w.reshape(w.shape[0], w.shape[1]).to(dt).float()
 
 
 def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
@@ -299,7 +313,7 @@ def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
     def check(name, got, ref):
         e = _ch_err(got, ref)
         worst.append((name, float(e.max())))
-        if float(e.max()) > FWD_CH_TOL:
+        if float(e.max()) > FWD_CH_TOL * (0.2 if r["dtype"] == "fp16" else 1.0):
             bad.append((name, float(e.max()), int(e.argmax())))
 
     with torch.backends.cudnn.flags(enabled=False):
@@ -315,7 +329,7 @@ def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
             pre = f"backbone.2.{si}.{bi}."
             if bt == "ir":
                 y1 = sv[k]; k += 1
-                check(pre + "conv_pw", y1, x_prev @ _pw_bf16(sd[pre + "conv_pw.weight"]).t())
+                check(pre + "conv_pw", y1, x_prev @ _pw_bf16(sd[pre + "conv_pw.weight"], r["dt"]).t())
                 a1 = _bn_act(y1, sd[pre + "bn1.weight"], sd[pre + "bn1.bias"])
                 bn_dw = "bn2"
             else:
@@ -335,7 +349,7 @@ def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
             y3 = sv[k]; k += 1
             pwl = "conv_pwl" if bt == "ir" else "conv_pw"
             bn3 = "bn3" if bt == "ir" else "bn2"
-            check(pre + pwl, y3, a2g @ _pw_bf16(sd[pre + pwl + ".weight"]).t())
+            check(pre + pwl, y3, a2g @ _pw_bf16(sd[pre + pwl + ".weight"], r["dt"]).t())
             xo = sv[k]; k += 1
             xo_ref = _bn_act(y3, sd[pre + bn3 + ".weight"], sd[pre + bn3 + ".bias"], act=False)
             if s == 1 and cin == cout:
@@ -343,7 +357,7 @@ def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
             check(pre + "out", xo, xo_ref)
             x_prev = xo
         yh = sv[k]
-        check("conv_head", yh, x_prev @ _pw_bf16(sd["backbone.3.weight"]).t())
+        check("conv_head", yh, x_prev @ _pw_bf16(sd["backbone.3.weight"], r["dt"]).t())
         ah = _bn_act(yh, sd["backbone.4.weight"], sd["backbone.4.bias"])
         feats_ref = ah.view(N, hw[0] * hw[1], -1).mean(1)
         fe = float((r["feats"] - feats_ref).norm() / feats_ref.norm())
@@ -351,13 +365,13 @@ def test_bench_config_bf16_forward_per_layer(bf16_run, cuda):
         if fe > 1e-2:
             bad.append(("features", fe))
     worst.sort(key=lambda t: -t[1])
-    print(f"per-layer forward, {len(worst)} tensors, worst per-channel rel errors: {worst[:8]}")
+    print(f"{r['dtype']} per-layer forward, {len(worst)} tensors, worst per-channel rel errors: {worst[:8]}")
     assert not bad, bad
 
 
-def _oracle_trunk(sd, cuda):
-    """The oracle trunk on the GPU with the detector's weights; 1x1 conv weights rounded to bf16 as the
-    HIP GEMMs use them (depthwise, stem and SE weights are fp32 in the HIP step)."""
+def _oracle_trunk(sd, cuda, dt=torch.bfloat16):
+    """The oracle trunk on the GPU with the detector's weights; 1x1 conv weights rounded to the storage
+    type as the HIP GEMMs use them (depthwise, stem and SE weights are fp32 in the HIP step)."""
     t = b0_cpu.trunk(b0_cpu.EfficientNetB0())
     tsd = {}
     for k, v in sd.items():
@@ -365,7 +379,7 @@ def _oracle_trunk(sd, cuda):
             continue
         name = k[len("backbone."):]
         if v.dim() == 4 and v.shape[2] == 1 and v.shape[3] == 1 and ".se." not in name:
-            v = v.bfloat16().float()
+            v = v.to(dt).float()
         tsd[name] = v
     t.load_state_dict(tsd)
     return t.to(cuda).train()
@@ -390,8 +404,10 @@ def _stage_io(r, si):
 def test_bench_config_bf16_backward_per_stage(bf16_run, cuda):
     r = bf16_run
     sd, gin, hg = r["sd"], r["gin"], r["grads"]
-    otr = _oracle_trunk(sd, cuda)
+    otr = _oracle_trunk(sd, cuda, r["dt"])
     report, bad = [], []
+    # fp16 (2^-11 storage rounding): measured worst 3.3e-3 (round 5), held to 1e-2
+    rel_tol = BWD_REL_TOL if r["dtype"] == "bf16" else 1e-2
     maps = {1: 112, 2: 56, 3: 28, 4: 14, 5: 14, 6: 7}
 
     def cmp_param(name, ref_grad, scale):
@@ -408,7 +424,7 @@ def test_bench_config_bf16_backward_per_stage(bf16_run, cuda):
             return
         rel = float((g - rr).norm()) / rn
         report.append((name, rel))
-        if rel > BWD_REL_TOL:
+        if rel > rel_tol:
             bad.append((name, "rel", rel))
         if name.endswith("conv_dw.weight"):
             gc = hg[name].double().flatten(1)
@@ -427,7 +443,7 @@ def test_bench_config_bf16_backward_per_stage(bf16_run, cuda):
         f.backward(r["dfeat"])
         e = float((_rows(x_last.grad) - gin[16]).norm() / _rows(x_last.grad).norm())
         report.append(("grad into conv_head", e))
-        if e > BWD_REL_TOL:
+        if e > rel_tol:
             bad.append(("grad into conv_head", e))
         scale = max(float(p.grad.norm()) for p in list(otr[3].parameters()) + list(otr[4].parameters()))
         for n, p in list(otr[3].named_parameters(prefix="backbone.3")) + list(otr[4].named_parameters(prefix="backbone.4")):
@@ -442,7 +458,7 @@ def test_bench_config_bf16_backward_per_stage(bf16_run, cuda):
             out.backward(dout)
             e = float((_rows(xi.grad) - gin[r["first"][si]]).norm() / _rows(xi.grad).norm())
             report.append((f"grad into stage {si}", e))
-            if e > BWD_REL_TOL:
+            if e > rel_tol:
                 bad.append((f"grad into stage {si}", e))
             ps = list(stage.named_parameters(prefix=f"backbone.2.{si}"))
             scale = max(float(p.grad.norm()) for _, p in ps)
@@ -460,5 +476,5 @@ def test_bench_config_bf16_backward_per_stage(bf16_run, cuda):
         for n, p in ps:
             cmp_param(n, p.grad, scale)
     report.sort(key=lambda t: -t[1])
-    print(f"per-stage backward: {len(report)} checks, worst: {report[:10]}")
+    print(f"{r['dtype']} per-stage backward: {len(report)} checks, worst: {report[:10]}")
     assert not bad, bad

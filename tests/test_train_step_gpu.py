@@ -146,9 +146,9 @@ def test_loss_scaled_adam_vs_torch_gradscaler(cuda, kind):
         s = tsc.get_scale()
         gs = [g * s for g in _grads(step, shapes, 10.0 if step % 3 else 1e-2)]
         if step == 2:
-            gs[2][17] = float("inf")
+            gs[2].view(-1)[17] = float("inf")
         if step == 4:
-            gs[0][0, 0] = float("nan")
+            gs[0].view(-1)[0] = float("nan")
         flat = torch.cat([gg.flatten() for gg in gs]).to(cuda)
         o = 0
         for p, q, gg in zip(params, rparams, gs):

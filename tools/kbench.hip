@@ -309,13 +309,13 @@ int main(int argc, char** argv) {
         int hs = 1;
         snprintf(nm, sizeof nm, "r%d %dx%d %d>%d", rows, q.hw, q.hw, q.K, q.N);
         b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + M * q.N), [&] {
-          const int rc = launch_pwl_bwd(b.s, A, nullptr, nullptr, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw,
+          const int rc = launch_pwl_bwd<bf16>(b.s, A, nullptr, nullptr, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw,
                                         q.N, q.K, D, slab, slab_cap, dW, false, part, pcap, &hs);
           return rc == 1 ? -1 : rc;
         });
         snprintf(nm, sizeof nm, "bn3 %dx%d %d>%d", q.hw, q.hw, q.K, q.N);
         b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + 2 * M * q.N), [&] {  // + the BN3 backward apply in staging
-          const int rc = launch_pwl_bwd(b.s, A, A + (int64_t)M * 32, coef, B, C, sc, sh, mean, invstd, gate, F,
+          const int rc = launch_pwl_bwd<bf16>(b.s, A, A + (int64_t)M * 32, coef, B, C, sc, sh, mean, invstd, gate, F,
                                         q.hw * q.hw, q.N, q.K, D, slab, slab_cap, dW, false, part, pcap, &hs);
           return rc == 1 ? -1 : rc;
         });
@@ -324,7 +324,7 @@ int main(int argc, char** argv) {
         const int64_t M = (int64_t)F * q.hw * q.hw;
         snprintf(nm, sizeof nm, "r%d %dx%d %d>%d%s", rows, q.hw, q.hw, q.cin, q.mid, q.skip ? " skip" : "");
         b.run("fused_fold", nm, 2.0 * (M * q.mid + (2 + q.skip) * M * q.cin), [&] {
-          const int rc = launch_pw_fold_bwd(b.s, A, B, q.skip ? C : nullptr, D, D, sc, C + (int64_t)M * 64, M, q.mid,
+          const int rc = launch_pw_fold_bwd<bf16>(b.s, A, B, q.skip ? C : nullptr, D, D, sc, C + (int64_t)M * 64, M, q.mid,
                                             q.cin, slab, slab_cap, dW, dW + (1 << 17), dW + (1 << 18));
           return rc == 1 ? -1 : rc;
         });
