@@ -710,15 +710,24 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
     a.bn = op == 4 ? 256 : op == 5 ? 128 : 0;
     return dfd::launch_vgemm_nt(s, a, epi);
   }
-  if (op == 1 || op == 3) {  // TN: C (fp32 [N][K]) = A^T . B with A [M][N], B [M][K]
+  if (op == 1 || op == 3 || op == 6) {  // TN: C (fp32 [N][K]) = A^T . B with A [M][N], B [M][K]
     if (!slab) { dfd::set_error("vgemm: slab missing", __FILE__, __LINE__); return -1; }
+    if (op == 6) {  // the cooperative split reduction (the ViT backward's form): counters from the slab's tail
+      const int nb = dfd::vgemm_tn_bar_count(N, K);
+      const int64_t cap = slab_floats - (nb + 64);
+      if (nb <= 0 || cap <= 0) { dfd::set_error("vgemm: slab too small", __FILE__, __LINE__); return -1; }
+      unsigned* bar = reinterpret_cast<unsigned*>(slab + cap);
+      DFD_HIP_CHECK(hipMemsetAsync(bar, 0, (size_t)nb * sizeof(unsigned), s));
+      return dfd::launch_vgemm_tn(s, (const dfd::bf16*)A, N, (const dfd::bf16*)B, K, M, N, K, slab, cap, (float*)C,
+                                  false, (float*)G, bar);
+    }
     if (op == 3)
       return dfd::blaslt_wgrad_split(s, (const dfd::bf16*)A, (const dfd::bf16*)B, (float*)C, M, N, K, 4, slab,
                                      slab_floats);
     return dfd::launch_vgemm_tn(s, (const dfd::bf16*)A, N, (const dfd::bf16*)B, K, M, N, K, slab, slab_floats,
                                 (float*)C, false, (float*)G);
   }
-  dfd::set_error("vgemm: op must be 0..5", __FILE__, __LINE__);
+  dfd::set_error("vgemm: op must be 0..6", __FILE__, __LINE__);
   return -1;
   DFD_GUARD_END
 }

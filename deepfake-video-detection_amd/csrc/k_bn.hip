@@ -1155,25 +1155,9 @@ struct SeSplit {
   int on;
 };
 
-// the workgroups sharing `arrive` / `depart` (n of them, all co-resident) wait for each other; the
-// last to leave zeroes both counters for the next launch.  Bounded poll: a grid that could not be
-// co-resident leaves after ~2^24 polls instead of hanging (its outputs are then invalid).
+// the slice barrier: group_sync (tail.h)
 __device__ __forceinline__ void se_group_sync(unsigned* arrive, unsigned* depart, unsigned n) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n && ++spins < (1u << 24))
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (__hip_atomic_fetch_add(depart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(depart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
+  group_sync(arrive, depart, n);
 }
 
 // grid: x = channel slice (fastest), y = 16-frame tile

@@ -22,6 +22,7 @@
 //   * weight gradients split over M into fp32 slabs (one dispatch wave of workgroups), summed in a
 //     fixed order (launch_reduce_slabs): the step stays bit-reproducible.
 #include "kernels.h"
+#include "tail.h"
 #include "vit.h"
 
 // 1: fc1's gelu / gelu' epilogue on the branch-free rational erf (common.h erf_rat_); 0: the library
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
 #ifndef DFD_TN_DEPTH
 #define DFD_TN_DEPTH 64
 #endif
-template <int TK>
+template <int TK, bool COOP = false>
 __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
   constexpr int NST = TK == 64 ? 2 : 4;
   constexpr int OPI = TK * VT * 2;        // one operand's m-step image
@@ -461,6 +462,48 @@ __global__ __launch_bounds__(512, 1) void vgemm_tn_kernel(VgemmTnArgs a) {
       *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(E + rl * EPS + 8 * v + 4);
     }
     __syncthreads();
+  }
+  if constexpr (COOP) {
+    // every split of this tile has written its slab rows; this split sums its share of the tile's
+    // rows over all splits in split order (bit-reproducible: independent of arrival order)
+    const int S = a.splits;
+    if (S > 1) group_sync(a.bar + 2 * t, a.bar + 2 * t + 1, (unsigned)S);
+    const int per = (VT + S - 1) / S;
+    const int r0 = min(VT, split * per), r1 = min(VT, r0 + per);
+    const int nv = (r1 - r0) * (VT / 4);
+    for (int i = tid; i < nv; i += 512) {
+      const int rr = r0 + i / (VT / 4), c4 = (i % (VT / 4)) * 4;
+      const int64_t off = (int64_t)(p0 + rr) * a.Q + q0 + c4;
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+      // 8 splits' loads in flight per round trip, added in split order
+      for (int sb = 0; sb < S; sb += 8) {
+        float4 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          x[u] = sb + u < S ? *reinterpret_cast<const float4*>(a.slab + (int64_t)(sb + u) * srow + off)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (sb + u < S) {
+            if (sb + u == 0) sum = x[u];
+            else { sum.x += x[u].x; sum.y += x[u].y; sum.z += x[u].z; sum.w += x[u].w; }
+          }
+      }
+      if (a.accumulate) {
+        const float4 w0 = *reinterpret_cast<const float4*>(a.W + off);
+        sum.x = w0.x + sum.x; sum.y = w0.y + sum.y; sum.z = w0.z + sum.z; sum.w = w0.w + sum.w;
+      }
+      *reinterpret_cast<float4*>(a.W + off) = sum;
+    }
+    if (csum) {  // the bias gradient entries p0 + [r0, r1) of this tile row
+      for (int i = tid; i < r1 - r0; i += 512) {
+        const int64_t off = (int64_t)a.P * a.Q + p0 + r0 + i;
+        float sum = a.slab[off];
+        for (int sp = 1; sp < S; ++sp) sum += a.slab[(int64_t)sp * srow + off];
+        const int64_t o = p0 + r0 + i;
+        a.colsum_out[o] = a.accumulate ? a.colsum_out[o] + sum : sum;
+      }
+    }
   }
 }
 
@@ -564,8 +607,20 @@ int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap) {
   return splits;
 }
 
+static int tn_device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, int64_t ld2, int64_t M, int P, int Q,
-                    float* slab, int64_t slab_cap, float* W, bool accumulate, float* colsum_out) {
+                    float* slab, int64_t slab_cap, float* W, bool accumulate, float* colsum_out, unsigned* bar) {
   if (!vgemm_tn_covers(M, P, Q)) { set_error("vgemm_tn: shape not covered", __FILE__, __LINE__); return -1; }
   const int64_t srow = (int64_t)P * Q + (colsum_out ? P : 0);
   if (srow > slab_cap) { set_error("vgemm_tn: slab too small", __FILE__, __LINE__); return -1; }
@@ -578,7 +633,16 @@ int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, 
   a.mchunk = (int)(cdiv64(cdiv64(M, splits), VK) * VK);
   splits = (int)cdiv64(M, a.mchunk);
   a.slab = slab;
-  hipLaunchKernelGGL(vgemm_tn_kernel<DFD_TN_DEPTH>, dim3(splits * a.tiles_p * a.tiles_q), dim3(512), 0, s, a);
+  const int grid = splits * a.tiles_p * a.tiles_q;
+  // cooperative split reduction: one 512-thread, ~128 KiB-LDS workgroup per CU, so the whole grid is
+  // co-resident when it has at most one workgroup per CU (vgemm_tn_splits sizes it to one dispatch wave)
+  if (bar && grid <= tn_device_cus()) {
+    a.bar = bar; a.W = W; a.colsum_out = colsum_out; a.splits = splits; a.accumulate = accumulate ? 1 : 0;
+    hipLaunchKernelGGL((vgemm_tn_kernel<DFD_TN_DEPTH, true>), dim3(grid), dim3(512), 0, s, a);
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
+  hipLaunchKernelGGL(vgemm_tn_kernel<DFD_TN_DEPTH>, dim3(grid), dim3(512), 0, s, a);
   DFD_HIP_CHECK(hipGetLastError());
   if (!colsum_out) return launch_reduce_slabs(s, slab, splits, (int64_t)P * Q, W, accumulate);
   // a linear's bias gradient stored right after its weight gradient (named_parameters order): one

@@ -56,9 +56,14 @@ struct VitLayout {
   std::vector<Blk> blk;
   int64_t wpe, ape, pe, xfin, mu_f, rs_f, S, total;
   // scratch
-  int64_t dx, dxm, dh, dZ, dqkv, dO, dS, part, slab, dpe, stotal;
+  int64_t dx, dxm, dh, dZ, dqkv, dO, dS, part, slab, dpe, bar, stotal;
   int64_t part_cap, slab_cap;
 };
+
+constexpr int kVitBars = 256;  // >= vgemm_tn_bar_count of every ViT-B weight gradient (3072 x 768: 72)
+#ifndef DFD_VIT_TN_COOP
+#define DFD_VIT_TN_COOP 0  // 1: the weight gradients' split partials reduced inside the GEMM launch (measured slower, DESIGN r5)
+#endif
 
 VitLayout vit_layout(const VitDims& d) {
   VitLayout L;
@@ -119,6 +124,7 @@ VitLayout vit_layout(const VitDims& d) {
   L.part = take(4 * L.part_cap);
   L.slab_cap = 16LL * FF * D;
   L.slab = take(4 * L.slab_cap);
+  L.bar = take(4 * kVitBars);  // the weight-gradient GEMMs' split-barrier counters (zeroed per backward)
   L.stotal = off;
   return L;
 }
@@ -204,9 +210,11 @@ int lin(hipStream_t s, const T* A, const T* B, T* C, const T* R, const float* bi
 // bf16 kernel; a column-sum pass otherwise)
 template <typename T>
 int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float* slab, int64_t slab_cap, float* dW,
-          float* dB, float* part, int64_t part_cap) {
+          float* dB, float* part, int64_t part_cap, unsigned* bar) {
   if constexpr (sizeof(T) == 2)
-    if (vgemm_tn_covers(M, N, K)) return launch_vgemm_tn(s, dY, N, X, K, M, N, K, slab, slab_cap, dW, false, dB);
+    if (vgemm_tn_covers(M, N, K))
+      return launch_vgemm_tn(s, dY, N, X, K, M, N, K, slab, slab_cap, dW, false, dB,
+                             DFD_VIT_TN_COOP && bar && vgemm_tn_bar_count(N, K) <= kVitBars ? bar : nullptr);
   Pro none{};
   DFD_TRY(launch_pw_wgrad<T>(s, dY, X, M, N, K, PRO_NONE, none, slab, slab_cap, dW, false));
   return launch_colsum<T>(s, dY, M, N, part, part_cap, dB, false);
@@ -269,6 +277,8 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
   const int64_t M = d.rows(), M0 = (int64_t)I * (nt - 1), SR = (int64_t)BH * nt;
   float* part = sc.template at<float>(L.part);
   float* slab = sc.template at<float>(L.slab);
+  unsigned* bar = sc.template at<unsigned>(L.bar);
+  DFD_HIP_CHECK(hipMemsetAsync(bar, 0, 4 * kVitBars, s));  // zero at rest from here on (group_sync)
   T* dx = sc.at(L.dx);
   T* dxm = sc.at(L.dxm);
   T* dh = sc.at(L.dh);
@@ -292,19 +302,19 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     // ---- MLP: dZ = (dx W2) * gelu'(Z); dW2 = dx^T gelu(Z); dh2 = dZ W1 ----
     DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D, VG_DGELU, w.at(b.Z)));
     if constexpr (sizeof(T) == 2) {  // G = gelu(Z) kept by the forward
-      DFD_TRY(wgrad<T>(s, dx, w.at(b.G), M, D, FF, slab, L.slab_cap, g[10], g[11], part, L.part_cap));
+      DFD_TRY(wgrad<T>(s, dx, w.at(b.G), M, D, FF, slab, L.slab_cap, g[10], g[11], part, L.part_cap, bar));
     } else {
       DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
       DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
     }
     DFD_TRY(lin<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, M, D, FF));
-    DFD_TRY(wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, slab, L.slab_cap, g[8], g[9], part, L.part_cap));
+    DFD_TRY(wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, slab, L.slab_cap, g[8], g[9], part, L.part_cap, bar));
     // LN2: dxm = dx + LN2'(dh2)
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.xm), D, dh, D, q[6], w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), dx, dxm, M, D, part, L.part_cap, g[6], g[7], false)));
     // ---- attention projection ----
     DFD_TRY(lin<T>(s, dxm, w.at(b.wpT), dO, nullptr, nullptr, M, D, D));
-    DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4], g[5], part, L.part_cap));
+    DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4], g[5], part, L.part_cap, bar));
     // ---- attention core: dP = dO v^T ; dS = scale P (dP - rowdot) ; dq = dS k ; dk = dS^T q ; dv = P^T dO
     if constexpr (sizeof(T) == 2) {  // fused (k_attn.hip): recomputes P from the saved log-sum-exp
       AttnArgs at = attn_args(I, nt, qkv, w.at(b.O), w.template at<float>(b.P));
@@ -326,14 +336,14 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
     }
     // ---- qkv projection and LN1: dx_l = dxm + LN1'(dqkv Wqkv) ----
     DFD_TRY(lin<T>(s, dqkv, w.at(b.wqkvT), dh, nullptr, nullptr, M, D, D3));
-    DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2], g[3], part, L.part_cap));
+    DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2], g[3], part, L.part_cap, bar));
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.x), D, dh, D, q[0], w.template at<float>(b.mu1), w.template at<float>(b.rs1),
                                 dxm, dx, M, D, part, L.part_cap, g[0], g[1], false)));
   }
   // tokens: dcls, dpos, patch rows -> patch-embedding weight / bias
   T* dpe = sc.at(L.dpe);
   DFD_TRY(launch_tokens_bwd<T>(s, dx, I, nt, D, dpe, G[1], G[0]));
-  return wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, slab, L.slab_cap, G[2], G[3], part, L.part_cap);
+  return wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, slab, L.slab_cap, G[2], G[3], part, L.part_cap, bar);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -101,6 +101,12 @@ struct VgemmTnArgs {
   int64_t ld1, ld2;
   int M, P, Q, tiles_p, tiles_q, mchunk;
   int colsum;         // also sum X1's columns (a linear's bias gradient) into the slab rows' tail
+  // cooperative split reduction (coop launches): the splits of a tile meet at a group barrier and each
+  // sums its share of the tile's rows over all splits (fixed order) into W (+ colsum_out)
+  unsigned* bar;      // 2 zeroed counters per tile
+  float* W;
+  float* colsum_out;
+  int splits, accumulate;
 };
 bool vgemm_nt_covers(int64_t M, int N, int K);
 bool vgemm_conv_covers(int Cin, int Cout, int KH, int KW);
@@ -109,8 +115,14 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a, int ep);
 int vgemm_tn_splits(int64_t M, int P, int Q, int64_t slab_cap);
 // colsum_out (optional): colsum_out[p] = sum_m X1[m][p] in the same launch (the slab then needs
 // splits x (P*Q + P) floats: vgemm_tn_splits(M, P, Q + 1, ...) x P x (Q + 1) is enough)
+// bar (optional): 2 x (P/256) x (Q/256) zeroed unsigned counters (zero again when the launch ends): the
+// split partial sums are then reduced inside the launch (cooperative, when the grid fits the device at
+// once) instead of by separate slab-reduction launches
 int launch_vgemm_tn(hipStream_t s, const bf16* X1, int64_t ld1, const bf16* X2, int64_t ld2, int64_t M, int P, int Q,
-                    float* slab, int64_t slab_cap, float* W, bool accumulate, float* colsum_out = nullptr);
+                    float* slab, int64_t slab_cap, float* W, bool accumulate, float* colsum_out = nullptr,
+                    unsigned* bar = nullptr);
+// counters launch_vgemm_tn's cooperative form needs for a P x Q product
+inline int vgemm_tn_bar_count(int P, int Q) { return 2 * (P / 256) * (Q / 256); }
 
 template <typename T>
 __device__ __forceinline__ void lds_st8v(T* p, const float (&v)[8]) { st8(p, v); }

@@ -318,8 +318,12 @@ DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int
  * (N % 256 == 0) / 128.
  * op 1 (TN): C (fp32 [N][K]) = A^T . B for A [M][N], B [M][K] (bf16), split over M into slab
  * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0; with G non-null also
- * G (fp32 [N]) = the column sums of A (a linear's bias gradient) from the same launch.  ops 2 / 3: the same
- * products through hipBLASLt (measurement comparison only; op 2 takes epi 0..3). */
+ * G (fp32 [N]) = the column sums of A (a linear's bias gradient) from the same launch.  op 6: op 1 with
+ * the split partials reduced inside the launch (the ViT backward's form: the splits of a 256 x 256 tile
+ * meet at a group barrier and each sums its share of the tile's rows over all splits in split order;
+ * used when the grid fits the device at once, else op 1's separate reductions); needs 2 x (N/256) x
+ * (K/256) + 64 floats of slab beyond op 1's, taken from the slab's end.  ops 2 / 3: the same products
+ * through hipBLASLt (measurement comparison only; op 2 takes epi 0..3). */
 DFD_API int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const void* R, const float* bias,
                       const void* Z, void* G, int64_t M, int N, int K, int epi, float* slab, int64_t slab_floats);
 DFD_API int64_t dfd_vgemm_tn_slab_floats(int64_t M, int N, int K);

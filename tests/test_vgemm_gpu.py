@@ -69,9 +69,16 @@ def test_vgemm_nt_vs_fp32(cuda, M, N, K, epi, op):
         torch.testing.assert_close(C.float(), d.bfloat16().float(), rtol=8e-3, atol=2e-3)
 
 
+def _tn_slab(lib, M, N, K, op, cuda):
+    """op 1's slab; op 6 also carves its tile counters from the slab's end"""
+    extra = 2 * (N // 256) * (K // 256) + 64 if op == 6 else 0
+    return torch.empty(lib.dfd_vgemm_tn_slab_floats(M, N, K) + extra, device=cuda)
+
+
+@pytest.mark.parametrize("op", [1, 6])  # 6: the splits reduced inside the launch (cooperative)
 @pytest.mark.parametrize("colsum", [False, True, "adjacent"])
 @pytest.mark.parametrize("M,N,K", [(394, 768, 256), (8 * 197, 768, 3072), (100, 256, 512), (4096, 2304, 768)])
-def test_vgemm_tn_vs_fp32(cuda, M, N, K, colsum):
+def test_vgemm_tn_vs_fp32(cuda, M, N, K, colsum, op):
     """weight gradient; with colsum the bias gradient (column sums of A) from the same launch, rows past
     the end of the last m-step contributing zero ("adjacent": the bias gradient stored right after the
     weight gradient, as in the flat gradient buffer, reduced in one pass)"""
@@ -79,14 +86,14 @@ def test_vgemm_tn_vs_fp32(cuda, M, N, K, colsum):
     A = torch.randn(M, N, device=cuda, generator=g).bfloat16()
     B = torch.randn(M, K, device=cuda, generator=g).bfloat16()
     lib = _lib.load()
-    slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(M, N, K), device=cuda)
+    slab = _tn_slab(lib, M, N, K, op, cuda)
     if colsum == "adjacent":
         flat = torch.full((N * K + N,), float("nan"), device=cuda)
         W, cs = flat[:N * K].view(N, K), flat[N * K:]
     else:
         W = torch.full((N, K), float("nan"), device=cuda)
         cs = torch.full((N,), float("nan"), device=cuda) if colsum else None
-    _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, P(cs), M, N, K, 0, P(slab), slab.numel()))
+    _lib.check(lib.dfd_vgemm(None, op, P(A), P(B), P(W), None, None, None, P(cs), M, N, K, 0, P(slab), slab.numel()))
     torch.cuda.synchronize()
     ref = A.double().T @ B.double()
     e = float((W.double() - ref).norm() / ref.norm())
@@ -110,8 +117,9 @@ def test_vgemm_nt_c5_rows(cuda, N, K):
     _close(C, ref)
 
 
+@pytest.mark.parametrize("op", [1, 6])
 @pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (3072, 768), (768, 3072)])
-def test_vgemm_tn_c5_rows(cuda, N, K):
+def test_vgemm_tn_c5_rows(cuda, N, K, op):
     """the four ViT weight gradients (dW = dY^T X, with the bias gradient from the same launch) at the
     C5 M = 25,216, where vgemm_tn_splits picks its split count and slab layout from M (e.g. 28 splits
     for 768 x 768 against 16 at M = 4,096): fp32 result against fp64, relative L2 <= 1e-5"""
@@ -119,33 +127,36 @@ def test_vgemm_tn_c5_rows(cuda, N, K):
     A = torch.randn(C5_M, N, device=cuda, generator=g).bfloat16()
     B = torch.randn(C5_M, K, device=cuda, generator=g).bfloat16()
     lib = _lib.load()
-    slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(C5_M, N, K), device=cuda)
+    slab = _tn_slab(lib, C5_M, N, K, op, cuda)
     flat = torch.full((N * K + N,), float("nan"), device=cuda)
     W, cs = flat[:N * K].view(N, K), flat[N * K:]
-    _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, P(cs), C5_M, N, K, 0, P(slab), slab.numel()))
+    _lib.check(lib.dfd_vgemm(None, op, P(A), P(B), P(W), None, None, None, P(cs), C5_M, N, K, 0, P(slab), slab.numel()))
     torch.cuda.synchronize()
     ref = A.double().T @ B.double()
     e = float((W.double() - ref).norm() / ref.norm())
     rc = A.double().sum(0)
     ec = float((cs.double() - rc).norm() / rc.norm())
-    print(f"TN {N}x{K} at M={C5_M}: slab splits {slab.numel() // (N * K + N)}, rel err {e:.2e}, bias {ec:.2e}")
+    print(f"TN op {op} {N}x{K} at M={C5_M}: slab splits {slab.numel() // (N * K + N)}, rel err {e:.2e}, bias {ec:.2e}")
     assert e <= 1e-5 and ec <= 1e-5, (e, ec)
 
 
-def test_vgemm_deterministic(cuda):
-    """two runs of the same TN product and NT product are bit-identical (fixed-order slab sums)"""
-    M, N, K = 2 * 197, 768, 768
+@pytest.mark.parametrize("op,M", [(1, 2 * 197), (6, 2 * 197), (6, C5_M)])
+def test_vgemm_deterministic(cuda, op, M):
+    """runs of the same TN product are bit-identical (fixed-order slab sums; op 6: each split sums its
+    rows over the splits in split order whatever the arrival order at the tile barrier), also across
+    back-to-back launches that reuse the same counters (zero at rest)"""
+    N, K = 768, 768
     A = torch.randn(M, N, device=cuda).bfloat16()
     B = torch.randn(M, K, device=cuda).bfloat16()
     lib = _lib.load()
-    slab = torch.empty(lib.dfd_vgemm_tn_slab_floats(M, N, K), device=cuda)
+    slab = _tn_slab(lib, M, N, K, op, cuda)
     outs = []
-    for _ in range(2):
+    for _ in range(3):
         W = torch.empty(N, K, device=cuda)
-        _lib.check(lib.dfd_vgemm(None, 1, P(A), P(B), P(W), None, None, None, None, M, N, K, 0, P(slab), slab.numel()))
+        _lib.check(lib.dfd_vgemm(None, op, P(A), P(B), P(W), None, None, None, None, M, N, K, 0, P(slab), slab.numel()))
         outs.append(W)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 def test_vgemm_refuses_uncovered(cuda):
