@@ -26,7 +26,10 @@ struct BnFwdFin {
 };
 
 // rows the consumer-side finalize is used for (larger row counts keep bn_finalize_kernel)
-constexpr int kBnFinRowsMax = 64;
+#ifndef DFD_BNFIN_ROWS
+#define DFD_BNFIN_ROWS 128  // 64 -> 128: 9.379-9.386 vs 9.384-9.405 ms/step (profiles/r05 ab_bnfin_rows_r05n.txt)
+#endif
+constexpr int kBnFinRowsMax = DFD_BNFIN_ROWS;
 // LDS scratch of bn_fin_wg in doubles (2 x 256 threads x 4 channels)
 constexpr int kBnFinScratch = 2 * 256 * 4;
 
