@@ -342,7 +342,10 @@ def test_forward_knob_training_close(cuda, knob, on, off):
     |b - fp64| each within TA_BIAS_TOL of the conditioning scale S = |sum_f |dpre_f|| (l2 over the 64
     units).  Measured (stem_occ, round 5): kappa 10.8, |3 - 2| / S = 1.4e-2, |each - fp64| / S = 4.0e-2
     (cosines 0.986 between the two, 0.90 of each to fp64: the bf16 step is equally far from fp64 under
-    both partitions)."""
+    both partitions).  The between-arm bound holds for the shipped summation orders, not for every valid
+    one: with another fp32 order of the SE excitation (measured and reverted, profiles/r05/ab_se_tail_r05w.txt)
+    blocks.2.1.0's se.conv_reduce gradient sits at 0.71-0.91 of the fp64 norm across the four variants and
+    the conv_head BN weight at cosine 0.959-0.986 to fp64 -- no variant systematically closer to fp64."""
     from deepfake_amd import backbone
     g = torch.Generator().manual_seed(5)
     u8 = torch.randint(0, 256, (4, 8, 224, 224, 3), generator=g, dtype=torch.uint8)
