@@ -1275,9 +1275,15 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
     float* tp = sp.tp + (int64_t)ftile * nsl * 16 * SE_TS;
     if (el) tp[slc * 16 * SE_TS + tid] = v;
     se_group_sync(sp.bar + 2 * ftile, sp.bar + 2 * ftile + 1, (unsigned)nsl);
-    if (el) {
-      v = tp[tid];
-      for (int q = 1; q < nsl; ++q) v += tp[q * 16 * SE_TS + tid];
+    if (el) {  // up to 8 slices' loads in flight, added in slice order
+      float pv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) pv[q] = q < nsl ? tp[q * 16 * SE_TS + tid] : 0.f;
+      v = pv[0];
+#pragma unroll
+      for (int q = 1; q < 8; ++q)
+        if (q < nsl) v += pv[q];
+      for (int q = 8; q < nsl; ++q) v += tp[q * 16 * SE_TS + tid];
     }
   }
   if (tid < 16 * SE_TS) {
