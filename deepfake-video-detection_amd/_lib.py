@@ -105,6 +105,8 @@ _SIGS = {
     "dfd_vit_work_bytes": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_vit_scratch_bytes": (c_i64, [c_i, c_i, c_i, c_i, c_i]),
     "dfd_vit_forward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, ctypes.POINTER(c_i64), c_fpp, c_p, c_p]),
+    "dfd_vit_forward_ex": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_p, ctypes.POINTER(c_i64), c_fpp, c_p, c_p,
+                                 c_i]),
     "dfd_vit_backward": (c_i, [c_p, c_i, c_i, c_i, c_i, c_i, c_fpp, c_p, c_p, c_p, c_fpp]),
     "dfd_gcn_head_work_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i]),
     "dfd_gcn_head_scratch_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i]),

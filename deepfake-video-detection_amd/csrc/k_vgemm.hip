@@ -365,6 +365,15 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
           }
           st8bf(a.G + (int64_t)row * a.ldc + c, g);
         }
+        if constexpr ((EP & VG_GELU) != 0) {
+          // inference fc1: C = gelu(z) alone, the same value VG_GELU2 leaves in G (no derivative store)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float gd;
+            if (DFD_GELU_RAT) gelu_pair_rat_(Tr<bf16>::round(o[j]), o[j], gd);
+            else gelu_pair_(Tr<bf16>::round(o[j]), o[j], gd);
+          }
+        }
         st8bf(a.C + (int64_t)row * a.ldc + c, o);
       }
     }
@@ -590,7 +599,8 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   case 4 * (E) + 1: hipLaunchKernelGGL((vgemm_nt_kernel<E, VT, false, true>), dim3(tiles), dim3(512), 0, s, a); break; \
   case 4 * (E) + 2: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128>), dim3(tiles), dim3(512), 0, s, a); break;        \
   case 4 * (E) + 3: hipLaunchKernelGGL((vgemm_nt_kernel<E, 128, false, true>), dim3(tiles), dim3(512), 0, s, a); break;
-    DFD_VG(0) DFD_VG(VG_BIAS) DFD_VG(VG_BIAS | VG_RESID) DFD_VG(VG_BIAS | VG_GELU2) DFD_VG(VG_DGELU)
+    DFD_VG(0) DFD_VG(VG_BIAS) DFD_VG(VG_BIAS | VG_RESID) DFD_VG(VG_BIAS | VG_GELU2) DFD_VG(VG_BIAS | VG_GELU)
+    DFD_VG(VG_DGELU)
     DFD_VG(VG_BIAS | VG_RELU) DFD_VG(VG_BIAS | VG_RESID | VG_RELU)
 #undef DFD_VG
     default: set_error("vgemm: epilogue not instantiated", __FILE__, __LINE__); return -1;

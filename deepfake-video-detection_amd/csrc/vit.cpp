@@ -220,9 +220,11 @@ int wgrad(hipStream_t s, const T* dY, const T* X, int64_t M, int N, int K, float
   return launch_colsum<T>(s, dY, M, N, part, part_cap, dB, false);
 }
 
+// keep_backward = 0 (inference): fc1 stores gelu(pre) alone where the own GEMM covers it (the
+// derivative the backward would read is not written); the outputs are the same bits either way
 template <typename T>
 int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, const float* x,
-                  const VitImg& im, char* work, float* feats) {
+                  const VitImg& im, char* work, float* feats, bool keep_backward = true) {
   const Ws<T> w{work};
   const int nt = d.ntok(), I = d.images, BH = I * HEADS;
   const int64_t M = d.rows(), M0 = (int64_t)I * (nt - 1), SR = (int64_t)BH * nt;
@@ -253,8 +255,11 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     DFD_TRY(lin<T>(s, w.at(b.O), w.at(b.wp), w.at(b.xm), w.at(b.x), q[5], M, D, D));
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.xm), D, q[6], q[7], w.at(b.h2), D, w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), M, D, LN_EPS)));
-    if constexpr (sizeof(T) == 2) {  // fc1 stores Z and G = gelu(Z); fc2 reads G
-      DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D, VG_GELU2, nullptr, w.at(b.G)));
+    if constexpr (sizeof(T) == 2) {  // fc1 stores Z and G = gelu(Z) (inference: G alone); fc2 reads G
+      if (!keep_backward && vgemm_nt_covers(M, FF, D) && FF % 128 == 0)
+        DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.G), nullptr, q[9], M, FF, D, VG_GELU));
+      else
+        DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D, VG_GELU2, nullptr, w.at(b.G)));
       DFD_TRY(lin<T>(s, w.at(b.G), w.at(b.w2), xnext, w.at(b.xm), q[11], M, D, FF));
     } else {  // fp32: GELU re-applied in fc2's operand prologue
       DFD_TRY(lin<T>(s, w.at(b.h2), w.at(b.w1), w.at(b.Z), nullptr, q[9], M, FF, D));
@@ -504,6 +509,12 @@ int64_t dfd_vit_scratch_bytes(int dtype, int depth, int images, int height, int 
 
 int dfd_vit_forward(void* stream, int dtype, int depth, int images, int nodes, int height, int width, const float* x,
                     const int64_t* x_strides5, const float* const* params, void* work, float* feats) {
+  return dfd_vit_forward_ex(stream, dtype, depth, images, nodes, height, width, x, x_strides5, params, work, feats, 1);
+}
+
+int dfd_vit_forward_ex(void* stream, int dtype, int depth, int images, int nodes, int height, int width, const float* x,
+                       const int64_t* x_strides5, const float* const* params, void* work, float* feats,
+                       int keep_backward) {
   VIT_GUARD_BEGIN
   const VitDims d{dtype, depth, images, height, width};
   if (dfd::vit_check(d)) return -1;
@@ -514,8 +525,9 @@ int dfd_vit_forward(void* stream, int dtype, int depth, int images, int nodes, i
   const dfd::VitImg im{nodes, height, width, x_strides5[0], x_strides5[1], x_strides5[2], x_strides5[3], x_strides5[4]};
   const auto L = dfd::vit_layout(d);
   if (dtype == 1)
-    return dfd::vit_forward_t<dfd::bf16>((hipStream_t)stream, d, L, params, x, im, (char*)work, feats);
-  return dfd::vit_forward_t<float>((hipStream_t)stream, d, L, params, x, im, (char*)work, feats);
+    return dfd::vit_forward_t<dfd::bf16>((hipStream_t)stream, d, L, params, x, im, (char*)work, feats,
+                                         keep_backward != 0);
+  return dfd::vit_forward_t<float>((hipStream_t)stream, d, L, params, x, im, (char*)work, feats, keep_backward != 0);
   VIT_GUARD_END
 }
 

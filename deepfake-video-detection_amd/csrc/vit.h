@@ -78,7 +78,7 @@ int launch_gelu(hipStream_t s, bf16* Z, bf16* out, int64_t n, int mode);
 // the derivative: computing it here, where erf(Z) is at hand, keeps the erf out of the backward);
 // VG_DGELU: C *= Z[m][n] with Z the derivative a VG_GELU2 launch stored
 // VG_RELU: relu after the bias and residual (the ResNet-50 eval 1x1 convolutions, k_rnconv.hip)
-enum VgEpi { VG_BIAS = 1, VG_RESID = 2, VG_GELU2 = 4, VG_DGELU = 8, VG_RELU = 16 };
+enum VgEpi { VG_BIAS = 1, VG_RESID = 2, VG_GELU2 = 4, VG_DGELU = 8, VG_RELU = 16, VG_GELU = 32 };
 struct VgemmArgs {
   const bf16* A;
   const bf16* B;

@@ -122,8 +122,9 @@ class _VitFn(torch.autograd.Function):
         work = torch.empty(int(lib.dfd_vit_work_bytes(dtype, depth, B * N, H, W)), dtype=torch.uint8, device=dev)
         feats = torch.empty(B * N, EMBED, dtype=torch.float32, device=dev)
         xs = (ctypes.c_int64 * 5)(*images.stride())
-        _lib.check(lib.dfd_vit_forward(_lib.stream_of(dev), dtype, depth, B * N, N, H, W, images.data_ptr(), xs,
-                                       _ptrs(params), work.data_ptr(), feats.data_ptr()))
+        # no gradient sink: an inference call (the fc1 epilogue skips the GELU derivative)
+        _lib.check(lib.dfd_vit_forward_ex(_lib.stream_of(dev), dtype, depth, B * N, N, H, W, images.data_ptr(), xs,
+                                          _ptrs(params), work.data_ptr(), feats.data_ptr(), 0 if sink is None else 1))
         ctx.owner, ctx.prefix, ctx.sink, ctx.dtype, ctx.depth = owner, prefix, sink, dtype, depth
         ctx.dims = (B * N, H, W)
         ctx.work = work

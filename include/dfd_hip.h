@@ -395,6 +395,13 @@ DFD_API int64_t dfd_vit_scratch_bytes(int dtype, int depth, int images, int heig
 DFD_API int dfd_vit_forward(void* stream, int dtype, int depth, int images, int nodes, int height, int width,
                             const float* x, const int64_t* x_strides5, const float* const* params, void* work,
                             float* feats);
+/* dfd_vit_forward with keep_backward = 0: an inference forward -- the bf16 fc1 epilogue stores
+ * gelu(pre) alone, not the GELU derivative the backward reads (12 x images*197 x 3072 bf16 fewer
+ * bytes written); feats are bit-identical to dfd_vit_forward's.  dfd_vit_backward must not follow it.
+ * keep_backward = 1 is dfd_vit_forward. */
+DFD_API int dfd_vit_forward_ex(void* stream, int dtype, int depth, int images, int nodes, int height, int width,
+                               const float* x, const int64_t* x_strides5, const float* const* params, void* work,
+                               float* feats, int keep_backward);
 DFD_API int dfd_vit_backward(void* stream, int dtype, int depth, int images, int height, int width,
                              const float* const* params, void* work, void* scratch, const float* dfeats,
                              float* const* grads);
