@@ -42,6 +42,18 @@ __device__ __forceinline__ bf16x8_t pack8(const float (&x)[2][4]) {  // RNE, as 
   return __builtin_bit_cast(bf16x8_t, make_uint4(pack2bf(x[0][0], x[0][1]), pack2bf(x[0][2], x[0][3]),
                                                  pack2bf(x[1][0], x[1][1]), pack2bf(x[1][2], x[1][3])));
 }
+// The MFMA operand of head-dimension rows col .. col+15 whose 8 contraction entries are the tokens
+// {rlo + 0..3, rhi + 0..3}, read as COLUMNS of a token-major image with ds_read_b64_tr_b16 (lane 4q + pq
+// of a 16-lane group supplies row r + q, columns col + 4pq .. +3; lane n receives column col + n of the
+// four rows) -- the transposed copy of the image is not needed
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
+__device__ __forceinline__ bf16x8_t tr8(const bf16* img, int rlo, int rhi, int col) {
+  const int lane = threadIdx.x & 63, q = (lane >> 2) & 3, pq = lane & 3;
+  const s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + (rlo + q) * RS + col + 4 * pq));
+  const s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4_t*)(img + (rhi + q) * RS + col + 4 * pq));
+  return bf16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
 __device__ __forceinline__ void st4(bf16* p, const f32x4_t& v, float s) {  // 4 consecutive bf16
   *reinterpret_cast<uint2*>(p) = make_uint2(pack2bf(v[0] * s, v[1] * s), pack2bf(v[2] * s, v[3] * s));
 }
@@ -90,13 +102,13 @@ template <int NB>
 __global__ __launch_bounds__(1024) void attn_fwd_kernel(AttnArgs a) {
   constexpr int NP = 16 * NB, TS = NP + 8;
   __shared__ __attribute__((aligned(16))) bf16 Ks[NP * RS];
-  __shared__ __attribute__((aligned(16))) bf16 Vt[AD * TS];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[NP * RS];
   const int bh = blockIdx.x, img = bh / a.heads, h = bh - img * a.heads;
   const int nt = a.nt, lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
   const int64_t row0 = (int64_t)img * nt;
   const bf16* base = a.qkv + row0 * a.ldq + h * AD;
   load_head<NP>(base + a.koff, a.ldq, nt, Ks, nullptr);
-  load_head<NP>(base + a.voff, a.ldq, nt, nullptr, Vt);
+  load_head<NP>(base + a.voff, a.ldq, nt, Vs, nullptr);
   __syncthreads();
   const int q = wave * 16 + (lane & 15);  // this lane's query (MFMA column)
   if (wave * 16 >= nt) return;
@@ -152,10 +164,7 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(AttnArgs a) {
     }
     const bf16x8_t pb = pack8(pv);
 #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      const bf16* vr = Vt + (db * 16 + (lane & 15)) * TS + 32 * c + 4 * g;
-      o[db] = mma(cat8(vr, vr + 16), pb, o[db]);
-    }
+    for (int db = 0; db < 4; ++db) o[db] = mma(tr8(Vs, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), pb, o[db]);
   }
   if (q < nt) {
     bf16* orow = a.O + (row0 + q) * a.ldo + h * AD;
@@ -170,16 +179,14 @@ __global__ __launch_bounds__(1024) void attn_bwd_kv_kernel(AttnArgs a) {
   constexpr int NP = 16 * NB, TS = NP + 8;
   __shared__ __attribute__((aligned(16))) bf16 Qs[NP * RS];
   __shared__ __attribute__((aligned(16))) bf16 dOs[NP * RS];
-  __shared__ __attribute__((aligned(16))) bf16 Qt[AD * TS];
-  __shared__ __attribute__((aligned(16))) bf16 dOt[AD * TS];
   __shared__ float Ls[NP], Dq[NP];
   const int bh = blockIdx.x, img = bh / a.heads, h = bh - img * a.heads;
   const int nt = a.nt, lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
   const int64_t row0 = (int64_t)img * nt;
   const bf16* base = a.qkv + row0 * a.ldq + h * AD;
   const bf16* dob = a.dO + row0 * a.lddo + h * AD;
-  load_head<NP>(base, a.ldq, nt, Qs, Qt);
-  load_head<NP>(dob, a.lddo, nt, dOs, dOt);
+  load_head<NP>(base, a.ldq, nt, Qs, nullptr);
+  load_head<NP>(dob, a.lddo, nt, dOs, nullptr);
   load_rowdot<NP>(dob, a.lddo, a.O + row0 * a.ldo + h * AD, a.ldo, nt, Dq);
   for (int t = threadIdx.x; t < NP; t += blockDim.x) Ls[t] = t < nt ? a.lse[(int64_t)bh * nt + t] : 0.f;
   __syncthreads();
@@ -217,9 +224,8 @@ __global__ __launch_bounds__(1024) void attn_bwd_kv_kernel(AttnArgs a) {
     const bf16x8_t pb = pack8(pv), sb = pack8(sv);
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
-      const int off = (db * 16 + (lane & 15)) * TS + 32 * c + 4 * g;
-      dv[db] = mma(cat8(dOt + off, dOt + off + 16), pb, dv[db]);
-      dk[db] = mma(cat8(Qt + off, Qt + off + 16), sb, dk[db]);
+      dv[db] = mma(tr8(dOs, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), pb, dv[db]);
+      dk[db] = mma(tr8(Qs, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), sb, dk[db]);
     }
   }
   if (key < nt) {
@@ -238,14 +244,13 @@ __global__ __launch_bounds__(1024) void attn_bwd_q_kernel(AttnArgs a) {
   constexpr int NP = 16 * NB, TS = NP + 8;
   __shared__ __attribute__((aligned(16))) bf16 Ks[NP * RS];
   __shared__ __attribute__((aligned(16))) bf16 Vs[NP * RS];
-  __shared__ __attribute__((aligned(16))) bf16 Kt[AD * TS];
   __shared__ float Dq[NP];
   const int bh = blockIdx.x, img = bh / a.heads, h = bh - img * a.heads;
   const int nt = a.nt, lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
   const int64_t row0 = (int64_t)img * nt;
   const bf16* base = a.qkv + row0 * a.ldq + h * AD;
   const bf16* dob = a.dO + row0 * a.lddo + h * AD;
-  load_head<NP>(base + a.koff, a.ldq, nt, Ks, Kt);
+  load_head<NP>(base + a.koff, a.ldq, nt, Ks, nullptr);
   load_head<NP>(base + a.voff, a.ldq, nt, Vs, nullptr);
   load_rowdot<NP>(dob, a.lddo, a.O + row0 * a.ldo + h * AD, a.ldo, nt, Dq);
   __syncthreads();
@@ -282,10 +287,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_q_kernel(AttnArgs a) {
     }
     const bf16x8_t sb = pack8(sv);
 #pragma unroll
-    for (int db = 0; db < 4; ++db) {
-      const bf16* kr = Kt + (db * 16 + (lane & 15)) * TS + 32 * c + 4 * g;
-      dq[db] = mma(cat8(kr, kr + 16), sb, dq[db]);
-    }
+    for (int db = 0; db < 4; ++db) dq[db] = mma(tr8(Ks, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), sb, dq[db]);
   }
   if (qok) {
     bf16* rowp = a.dqkv + (row0 + q) * a.lddq + h * AD;
