@@ -255,6 +255,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ X, in
   }
 }
 
+// rows of loads in flight per wave in the LayerNorm backward, and its grid (0: one round of co-resident
+// workgroups) -- A/B build switches
+#ifndef DFD_LN_PF
+#define DFD_LN_PF 2
+#endif
+#ifndef DFD_LN_GRID
+#define DFD_LN_GRID 0
+#endif
 // dX = dres + rstd * (dxh - mean(dxh) - xhat * mean(dxh * xhat)),  dxh = dY * gamma.
 // Workgroup w handles rows [w*rpb, (w+1)*rpb): per-column partials of dY*xhat (dgamma) and dY
 // (dbeta) go to part[w][2][C] in a fixed order (waves summed in order through LDS).
@@ -273,19 +281,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
 #pragma unroll
     for (int j = 0; j < 8; ++j) { pg[i][j] = 0.f; pb[i][j] = 0.f; }
   const int64_t rbeg = (int64_t)blockIdx.x * rpb, rend = min(rows, rbeg + rpb);
-  // a row's x, dY and residual gradient are loaded together, one row ahead (raw registers), so the
-  // wave's loads for row r+4 are in flight while row r is reduced and written
-  Raw8<T> rx[VIT_LN_VEC], rr[VIT_LN_VEC];
-  Raw8<D> rd[VIT_LN_VEC];
-  auto row_ld = [&](int64_t r) {
+  // a row's x, dY and residual gradient are loaded together into raw registers, DFD_LN_PF rows ahead
+  // (ring of register sets), so the wave's loads of the next rows are in flight while row r is reduced
+  // and written
+  struct RowRaw {
+    Raw8<T> x[VIT_LN_VEC], r[VIT_LN_VEC];
+    Raw8<D> d[VIT_LN_VEC];
+  };
+  auto row_ld = [&](RowRaw& w, int64_t r) {
     const bool live = r < rend;
 #pragma unroll
     for (int i = 0; i < VIT_LN_VEC; ++i) {
       const int v = lane + 64 * i;
       const bool ok = live && v < nv;
-      raw_ld(rx[i], X + r * ldx + v * 8, X, ok);
-      raw_ld(rd[i], dY + r * ldd + v * 8, dY, ok);
-      raw_ld(rr[i], dres ? dres + r * ldx + v * 8 : X, X, ok && dres != nullptr);
+      raw_ld(w.x[i], X + r * ldx + v * 8, X, ok);
+      raw_ld(w.d[i], dY + r * ldd + v * 8, dY, ok);
+      raw_ld(w.r[i], dres ? dres + r * ldx + v * 8 : X, X, ok && dres != nullptr);
     }
   };
   float gv[VIT_LN_VEC][8];
@@ -294,8 +305,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
     const int v = lane + 64 * i;
     if (v < nv) ld8(g + v * 8, gv[i]);
   }
-  row_ld(rbeg + wave);
-  for (int64_t r = rbeg + wave; r < rend; r += 4) {
+  // row r from its raw registers; the set is refilled with row r + 4 * DFD_LN_PF before the reductions
+  auto row_do = [&](RowRaw& w, int64_t r) {
     const float mu = mean[r], rs = rstd[r];
     float xh[VIT_LN_VEC][8], dxh[VIT_LN_VEC][8], res[VIT_LN_VEC][8];
     float s1 = 0.f, s2 = 0.f;
@@ -304,9 +315,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
       const int v = lane + 64 * i;
       if (v < nv) {
         float x[8], dy[8];
-        raw_to_f(rx[i], x);
-        raw_to_f(rd[i], dy);
-        raw_to_f(rr[i], res[i]);
+        raw_to_f(w.x[i], x);
+        raw_to_f(w.d[i], dy);
+        raw_to_f(w.r[i], res[i]);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           xh[i][j] = (x[j] - mu) * rs;
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
         }
       }
     }
-    row_ld(r + 4);
+    row_ld(w, r + 4 * DFD_LN_PF);
     s1 = wave_sum(s1) / C;
     s2 = wave_sum(s2) / C;
 #pragma unroll
@@ -331,6 +342,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ X, in
         st8(dX + r * ldx + v * 8, o);
       }
     }
+  };
+  RowRaw ring[DFD_LN_PF];
+#pragma unroll
+  for (int k = 0; k < DFD_LN_PF; ++k) row_ld(ring[k], rbeg + wave + 4 * k);
+  for (int64_t r = rbeg + wave; r < rend; r += 4 * DFD_LN_PF) {
+#pragma unroll
+    for (int k = 0; k < DFD_LN_PF; ++k)
+      if (r + 4 * k < rend) row_do(ring[k], r + 4 * k);
   }
 #pragma unroll
   for (int i = 0; i < VIT_LN_VEC; ++i) {
@@ -564,7 +583,15 @@ int launch_ln_bwd(hipStream_t s, const T* X, int64_t ldx, const D* dY, int64_t l
                   const float* rstd, const T* dres, T* dX, int64_t rows, int C, float* part, int64_t part_cap,
                   float* dgamma, float* dbeta, bool accumulate) {
   if ((C & 7) || C > VIT_LN_MAXC) { set_error("layernorm: unsupported width", __FILE__, __LINE__); return -1; }
-  int blocks = (int)std::min<int64_t>(1024, cdiv64(rows, 16));
+  // one round of co-resident workgroups (the rows of a wave then pipeline DFD_LN_PF deep)
+  static const int resident = [] {
+    int dev = 0, cus = 256, per_cu = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ln_bwd_kernel<T, D>, 256, 0) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    return std::max(1, cus * per_cu);
+  }();
+  int blocks = (int)std::min<int64_t>(DFD_LN_GRID ? DFD_LN_GRID : resident, cdiv64(rows, 16));
   blocks = (int)std::min<int64_t>(blocks, std::max<int64_t>(1, part_cap / (2LL * C)));
   const int rpb = (int)cdiv64(rows, blocks);
   blocks = (int)cdiv64(rows, rpb);
