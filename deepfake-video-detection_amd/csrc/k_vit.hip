@@ -433,39 +433,40 @@ __global__ __launch_bounds__(256) void tokens_bwd_kernel(const T* __restrict__ d
 }
 
 // ------------------------------------------------------------------------------------------
-// weight casts: out = cast(W) ([rows][cols]) or its transpose ([cols][rows]), 32x32 LDS tiles
+// weight casts: cast(W) ([rows][cols]) and / or its transpose ([cols][rows]) from ONE read of the fp32
+// source, 32x32 LDS tiles; blockIdx.x = the segment's tile (the grid spans the largest segment)
 template <typename T>
 __global__ __launch_bounds__(256) void wcast_kernel(VitCast cs) {
   const VitCastSeg sg = cs.seg[blockIdx.z];
   const int tr = (sg.cols + 31) / 32;
+  if ((int)blockIdx.x >= tr * ((sg.rows + 31) / 32)) return;
   const int ty = blockIdx.x / tr, tx = blockIdx.x - (blockIdx.x / tr) * tr;
-  if (ty * 32 >= sg.rows) return;
   __shared__ float tile[32][33];
   const int lx = threadIdx.x & 31, ly = threadIdx.x >> 5;
   T* out = reinterpret_cast<T*>(sg.dst);
+  T* out_t = reinterpret_cast<T*>(sg.dst_t);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = ty * 32 + ly + 8 * i, c = tx * 32 + lx;
     const float v = (r < sg.rows && c < sg.cols) ? sg.src[(int64_t)r * sg.cols + c] : 0.f;
-    if (!sg.transpose) {
-      if (r < sg.rows && c < sg.cols) out[(int64_t)r * sg.cols + c] = Tr<T>::from_f(v);
-    } else {
-      tile[ly + 8 * i][lx] = v;
-    }
+    if (out && r < sg.rows && c < sg.cols) out[(int64_t)r * sg.cols + c] = Tr<T>::from_f(v);
+    tile[ly + 8 * i][lx] = v;
   }
-  if (!sg.transpose) return;
+  if (!out_t) return;  // uniform per segment
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int c = tx * 32 + ly + 8 * i, r = ty * 32 + lx;  // out[c][r]
-    if (r < sg.rows && c < sg.cols) out[(int64_t)c * sg.rows + r] = Tr<T>::from_f(tile[lx][ly + 8 * i]);
+    const int c = tx * 32 + ly + 8 * i, r = ty * 32 + lx;  // out_t[c][r]
+    if (r < sg.rows && c < sg.cols) out_t[(int64_t)c * sg.rows + r] = Tr<T>::from_f(tile[lx][ly + 8 * i]);
   }
 }
 
 template <typename T>
-int launch_wcast(hipStream_t s, const VitCast& cs, int nseg, int max_rows, int max_cols) {
+int launch_wcast(hipStream_t s, const VitCast& cs, int nseg) {
   if (nseg <= 0) return 0;
-  const dim3 grid((unsigned)(cdiv(max_rows, 32) * cdiv(max_cols, 32)), 1, (unsigned)nseg);
+  int tiles = 0;
+  for (int i = 0; i < nseg; ++i) tiles = std::max(tiles, cdiv(cs.seg[i].rows, 32) * cdiv(cs.seg[i].cols, 32));
+  const dim3 grid((unsigned)tiles, 1, (unsigned)nseg);
   hipLaunchKernelGGL((wcast_kernel<T>), grid, dim3(256), 0, s, cs);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
@@ -714,7 +715,7 @@ int launch_gelu(hipStream_t s, bf16* Z, bf16* out, int64_t n, int mode) {
   template int launch_tokens_fwd<T>(hipStream_t, const T*, const float*, const float*, int, int, int, T*);           \
   template int launch_tokens_bwd<T>(hipStream_t, const T*, int, int, int, T*, float*, float*);                       \
   template int launch_colsum<T>(hipStream_t, const T*, int64_t, int, float*, int64_t, float*, bool);                 \
-  template int launch_wcast<T>(hipStream_t, const VitCast&, int, int, int);
+  template int launch_wcast<T>(hipStream_t, const VitCast&, int);
 DFD_VIT_INST(float)
 DFD_VIT_INST(bf16)
 template int launch_ln_fwd<bf16, float>(hipStream_t, const bf16*, int64_t, const float*, const float*, float*, int64_t,

@@ -143,21 +143,17 @@ struct Ws {
 template <typename T>
 int cast_weights(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, const Ws<T>& w) {
   VitCast pe{};
-  pe.seg[0] = {P[2], w.at(L.wpe), D, D, 0};
-  DFD_TRY(launch_wcast<T>(s, pe, 1, D, D));
+  pe.seg[0] = {P[2], w.at(L.wpe), nullptr, D, D};
+  DFD_TRY(launch_wcast<T>(s, pe, 1));
   for (int l = 0; l < d.depth; ++l) {
     const float* const* q = P + 4 + 12 * l;
     const auto& b = L.blk[l];
     VitCast c{};
-    c.seg[0] = {q[2], w.at(b.wqkv), D3, D, 0};
-    c.seg[1] = {q[2], w.at(b.wqkvT), D3, D, 1};
-    c.seg[2] = {q[4], w.at(b.wp), D, D, 0};
-    c.seg[3] = {q[4], w.at(b.wpT), D, D, 1};
-    c.seg[4] = {q[8], w.at(b.w1), FF, D, 0};
-    c.seg[5] = {q[8], w.at(b.w1T), FF, D, 1};
-    c.seg[6] = {q[10], w.at(b.w2), D, FF, 0};
-    c.seg[7] = {q[10], w.at(b.w2T), D, FF, 1};
-    DFD_TRY(launch_wcast<T>(s, c, 8, FF, FF));
+    c.seg[0] = {q[2], w.at(b.wqkv), w.at(b.wqkvT), D3, D};
+    c.seg[1] = {q[4], w.at(b.wp), w.at(b.wpT), D, D};
+    c.seg[2] = {q[8], w.at(b.w1), w.at(b.w1T), FF, D};
+    c.seg[3] = {q[10], w.at(b.w2), w.at(b.w2T), D, FF};
+    DFD_TRY(launch_wcast<T>(s, c, 4));
   }
   return 0;
 }

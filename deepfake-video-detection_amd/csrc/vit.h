@@ -28,9 +28,10 @@ struct VitImg {
 };
 
 struct VitCastSeg {
-  const float* src;  // [rows][cols] fp32
-  void* dst;         // T [rows][cols] or, transposed, [cols][rows]
-  int rows, cols, transpose;
+  const float* src;  // [rows][cols] fp32, read once
+  void* dst;         // T [rows][cols] (null: not wanted)
+  void* dst_t;       // T [cols][rows], the transpose (null: not wanted)
+  int rows, cols;
 };
 struct VitCast {
   VitCastSeg seg[8];
@@ -60,7 +61,7 @@ template <typename T>
 int launch_colsum(hipStream_t s, const T* X, int64_t M, int N, float* part, int64_t part_cap, float* out,
                   bool accumulate);
 template <typename T>
-int launch_wcast(hipStream_t s, const VitCast& cs, int nseg, int max_rows, int max_cols);
+int launch_wcast(hipStream_t s, const VitCast& cs, int nseg);
 int launch_gcn_mix(hipStream_t s, const float* A, const float* F, int B, int N, int D, bool transpose, float* H);
 int launch_relu_drop(hipStream_t s, float* Y, float* D, int64_t n, uint64_t seed, uint32_t st, float p);
 int launch_relu_drop_bwd(hipStream_t s, const float* Y, const float* dD, float* dY, int64_t n, uint64_t seed,
