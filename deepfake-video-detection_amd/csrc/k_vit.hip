@@ -599,7 +599,10 @@ int launch_ln_bwd(hipStream_t s, const T* X, int64_t ldx, const D* dY, int64_t l
   hipLaunchKernelGGL((ln_bwd_kernel<T, D>), dim3((unsigned)blocks), dim3(256), 0, s, X, ldx, dY, ldd, g, mean, rstd,
                      dres, dX, rows, C, rpb, part);
   DFD_HIP_CHECK(hipGetLastError());
-  // part rows alternate [dgamma; dbeta]: reduce each column set with a stride-2C view
+  // part rows alternate [dgamma; dbeta]: where the two gradients are adjacent (timm's weight, bias
+  // order in one flat gradient buffer) the whole rows reduce in one launch, else each column set
+  // with a stride-2C view
+  if (dbeta == dgamma + C) return launch_reduce_slabs(s, part, blocks, 2LL * C, dgamma, accumulate);
   DFD_TRY(launch_reduce_slabs_strided(s, part, blocks, C, 2LL * C, dgamma, accumulate));
   DFD_TRY(launch_reduce_slabs_strided(s, part + C, blocks, C, 2LL * C, dbeta, accumulate));
   return 0;
