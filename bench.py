@@ -8,7 +8,7 @@ resident in HBM.  N GPUs = N ranks (one process per GPU, torch.distributed over 
 sharded, bucketed gradient all-reduce overlapped with backward; value = frames of all ranks /
 max-over-ranks time.  Rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype bf16|fp16|fp32] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype fp16|bf16|fp32] [--no-cpu-baseline]
 
 ``--gpus N`` without a launcher: this process spawns ``torch.distributed.run`` with N ranks on
 127.0.0.1 BEFORE touching the GPU and exits with its status (the driver's own
@@ -40,9 +40,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=None, help="ranks (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    # fp16: IEEE half storage on v_mfma_f32_16x16x32_f16 with dynamic loss scaling (TrainStep's
-    # DynamicLossScaler: scale, unscale, skip-on-overflow and update all on the device, inside the step)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
+    # fp16 (the default: BASELINE.json configs[1] names "train loop bs=256 fp16"): IEEE half storage on
+    # v_mfma_f32_16x16x32_f16 with dynamic loss scaling (TrainStep's DynamicLossScaler: scale, unscale,
+    # skip-on-overflow and update all on the device, inside the step); bf16 the same kernels on bf16
+    ap.add_argument("--dtype", default="fp16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--input", default="uint8", choices=["uint8", "fp32"],
                     help="frames handed to the model: raw uint8 crops (normalised in the stem) or fp32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -232,7 +233,7 @@ def main():
                                class_weights=torch.tensor([1.0, 1.0]))
     x, labels = synthetic_batch(rank, dev, args.input)
     # the dominant launch of the step: the fused stride-2 depthwise backward of blocks.1.0
-    # (dw_bwd2_kernel<bf16,3,8,56,14,1>, 112x112x96 <- 56x56x96, k_dw_bwd2.hip; the largest single
+    # (dw_bwd2_kernel<f16,3,8,56,14,1> / <bf16,...>, 112x112x96 <- 56x56x96, k_dw_bwd2.hip; the largest single
     # kernel in the rocprof trace)
     probe = roofline.KernelProbe(model, "dw_bwd", stage=1, block=0)
 

@@ -49,6 +49,9 @@ _SIGS = {
     "dfd_b0_saved_tensor": (c_i, [c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "dfd_b0_grad_tensor": (c_i, [c_p, c_i, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]),
     "dfd_b0_fused_info": (c_i, [c_p, ctypes.POINTER(c_i), ctypes.POINTER(c_i64)]),
+    "dfd_b0_plan_status": (c_i, [c_p, ctypes.POINTER(c_i)]),
+    "dfd_b0_plan_clear_status": (c_i, [c_p]),
+    "dfd_test_occupy": (c_i, [c_p, c_i, c_i64]),
     "dfd_b0_probe_arm": (c_i, [c_p, c_i, c_i, c_i, c_i]),
     "dfd_b0_probe_read": (c_i, [c_p, ctypes.POINTER(c_f), c_i, ctypes.POINTER(c_i)]),
     "dfd_b0_probe_disarm": (c_i, [c_p]),

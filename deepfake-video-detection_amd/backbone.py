@@ -295,6 +295,27 @@ class B0Runtime:
             raise _lib.DFDError("fused 7x7 MBConv: a grid barrier timed out (grid not co-resident); "
                                 "this step's statistics are invalid -- turn the mbconv7 knob off")
 
+    def check_status(self, synchronize: bool = True) -> None:
+        """Raise if a device-side software barrier of any of this runtime's plans timed out (the split
+        SE excitation's slice sync, when another stream's kernels held the CUs its grid needed): that
+        call's outputs were invalid.  The plans also refuse every later call on their own (the status
+        is sticky, set by the device in pinned host memory); this is the definitive check after a
+        device synchronisation (trainers call it at epoch ends, tests after a step)."""
+        if synchronize:
+            torch.cuda.synchronize()
+        st = ctypes.c_int()
+        with self._lock:
+            for h in self.plans.values():
+                _lib.check(self.lib.dfd_b0_plan_status(h, ctypes.byref(st)))
+                if st.value:
+                    raise _lib.DFDError("b0 plan: a software barrier (SE slice sync) timed out -- that step's "
+                                        "outputs were invalid; call clear_status() to run the plan again")
+
+    def clear_status(self) -> None:
+        with self._lock:
+            for h in self.plans.values():
+                _lib.check(self.lib.dfd_b0_plan_clear_status(h))
+
     def backward(self, h, ws, x, dfeat, owner, grads, training, seg_begin, seg_end, accumulate=False):
         torch.ops.dfd.b0_trunk_backward(x, h.value, dfeat, owner._flat_p, ws, grads, self._norm, training, seg_begin,
                                         seg_end, accumulate)

@@ -230,6 +230,25 @@ int dfd_b0_fused_info(const dfd_b0_plan* plan, int* nblocks, int64_t* abort_offs
   return 0;
 }
 
+int dfd_b0_plan_status(const dfd_b0_plan* plan, int* status) {
+  if (!plan || !status) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  *status = dfd::plan_status(plan->p);
+  return 0;
+}
+
+int dfd_b0_plan_clear_status(dfd_b0_plan* plan) {
+  if (!plan) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  std::lock_guard<std::mutex> lk(plan->mu);
+  if (plan->p.err_host) *reinterpret_cast<volatile int*>(plan->p.err_host) = 0;
+  return 0;
+}
+
+int dfd_test_occupy(void* stream, int workgroups, int64_t microseconds) {
+  DFD_GUARD_BEGIN
+  return dfd::launch_occupy((hipStream_t)stream, workgroups, microseconds);
+  DFD_GUARD_END
+}
+
 int dfd_b0_segment_tensors(int seg, int* lo, int* hi) {
   if (seg < 0 || seg >= dfd::kNumSegments || !lo || !hi) {
     dfd::set_error("bad segment", __FILE__, __LINE__);

@@ -1153,11 +1153,12 @@ struct SeSplit {
   float* tp;      // [frame tiles][slices][16][SE_TS] partial first products
   unsigned* bar;  // 2 zeroed counters (arrive, depart) per frame tile
   int on;
+  SyncAbort ab;   // a timed-out slice barrier is reported here (the plan raises on its next call)
 };
 
-// the slice barrier: group_sync (tail.h)
-__device__ __forceinline__ void se_group_sync(unsigned* arrive, unsigned* depart, unsigned n) {
-  group_sync(arrive, depart, n);
+// the slice barrier: group_sync (tail.h); false when it timed out (the workgroup leaves)
+__device__ __forceinline__ bool se_group_sync(unsigned* arrive, unsigned* depart, unsigned n, const SyncAbort& ab) {
+  return group_sync(arrive, depart, n, ab);
 }
 
 // grid: x = channel slice (fastest), y = 16-frame tile
@@ -1274,7 +1275,7 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
   if (sp.on) {  // the slices' partials of this frame tile, added in slice order
     float* tp = sp.tp + (int64_t)ftile * nsl * 16 * SE_TS;
     if (el) tp[slc * 16 * SE_TS + tid] = v;
-    se_group_sync(sp.bar + 2 * ftile, sp.bar + 2 * ftile + 1, (unsigned)nsl);
+    if (!se_group_sync(sp.bar + 2 * ftile, sp.bar + 2 * ftile + 1, (unsigned)nsl, sp.ab)) return;
     if (el) {  // up to 8 slices' loads in flight, added in slice order
       float pv[8];
 #pragma unroll
@@ -1411,6 +1412,7 @@ static SeSplit se_split(const SeScratch* sc, int frames, int C) {
   sp.tp = sc->tp;
   sp.bar = sc->bar;
   sp.on = 1;
+  sp.ab = SyncAbort{sc->abort_dev, sc->abort_host};
   return sp;
 }
 

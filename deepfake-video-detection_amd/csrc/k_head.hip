@@ -460,7 +460,10 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(const double* __rest
   const double a = sh[0];
   float nrm = (float)sqrt(a);
   if (scaler) {
-    const bool bad = !isfinite(nrm);
+    // found_inf from the fp64 sum: it is not finite iff an element is (squares of finite floats cannot
+    // overflow it), whereas a finite-element norm above FLT_MAX would turn the fp32 narrowing inf
+    // and skip a step GradScaler's per-element check keeps
+    const bool bad = !isfinite(a);
     scaler[2] = bad ? 1.f : 0.f;
     nrm = bad ? nrm : (float)(sqrt(a) * (double)(1.f / scaler[0]));
   }

@@ -37,6 +37,10 @@ namespace dfd {
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+// two channels of a lane's four in natural lane order (x = channel 2h, y = channel 2h + 1): the BN2 /
+// SE sums are written on these pairs so that every packed f32 instruction reads both operands in the
+// same lane order (see the note at the epilogue)
+typedef float pv2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4_t;
 
 
@@ -183,29 +187,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
   // per-lane constants of the 4 channels this lane holds in the transposed dgrad tile
   const bool cw = wave < KBC;
   const int kl = wave * 16 + 4 * (lane >> 4);  // local channel of r = 0
-  float csc[4], csh[4], cmu[4], cis[4], cval[4];
+  pv2 csc[2], csh[2], cmu[2], cis[2];
+  float cval[4];
   f32x4_t aw[WG ? TL::NBW : 1];
 #pragma unroll
   for (int nb = 0; nb < (WG ? TL::NBW : 1); ++nb) aw[nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float se[5][4];
+  pv2 se[5][2];  // [q][channel pair]
 #pragma unroll
   for (int q = 0; q < 5; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) se[q][r] = 0.f;
+    for (int hp = 0; hp < 2; ++hp) se[q][hp] = pv2{0.f, 0.f};
 
   if (nsteps > 0) load(std::integral_constant<int, 0>{}, 0);
   if constexpr (NS == 2)
     if (nsteps > 1) load(std::integral_constant<int, NS - 1>{}, 1);
   __syncthreads();  // fragments and coefficients staged
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int c = cw ? kl + r : 0;
-    csc[r] = co[c];
-    csh[r] = co[TL::KC + c];
-    cmu[r] = co[2 * TL::KC + c];
-    cis[r] = co[3 * TL::KC + c];
-    cval[r] = cw && k0 + kl + r < K ? 1.f : 0.f;
+  for (int hp = 0; hp < 2; ++hp) {
+    const int c = cw ? kl + 2 * hp : 0, c1 = cw ? c + 1 : 0;
+    csc[hp] = pv2{co[c], co[c1]};
+    csh[hp] = pv2{co[TL::KC + c], co[TL::KC + c1]};
+    cmu[hp] = pv2{co[2 * TL::KC + c], co[2 * TL::KC + c1]};
+    cis[hp] = pv2{co[3 * TL::KC + c], co[3 * TL::KC + c1]};
   }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) cval[r] = cw && k0 + kl + r < K ? 1.f : 0.f;
 
   auto step = [&](auto setc, int st) {
     constexpr int S = decltype(setc)::value;
@@ -274,6 +280,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
         }
       }
       // ---- epilogue: bf16 ge2 into the C tile, SE/BN sums against y2 of the same 4 channels ----
+      // Written on channel pairs in natural lane order (pv2).  As four scalar channels, the SLP
+      // vectoriser of the fp16 instance paired y (hi, lo) against d (lo, hi) and reconciled them with
+      // SWAPPED packed-f32 operand selects (v_pk_mul/fma_f32 ... op_sel:[0,1] op_sel_hi:[1,0]: the low
+      // lane reads the pair's high register and the high lane its low one) -- exactly the instructions
+      // feeding sum(d * silu') and sum(d * silu' * xhat), the only outputs that differed between two
+      // identical launches on MI355X (16-185 entries, sign flips; profiles/r05 pwl_det_slp_r05j.txt).
+      // Packed operands in one lane order leave the compiler nothing to swap (tests/test_isa_scan.py
+      // checks every code object of the library for that form).
 #pragma unroll
       for (int mb = 0; mb < PB_R / 16; ++mb) {
         const int m = mb * 16 + (lane & 15);
@@ -283,18 +297,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
         float d[4], y[4];
         unpack4<T>(pk, d);
         unpack4<T>(*reinterpret_cast<const uint2*>(Ys + m * TL::XS + kl), y);
+        const pv2 rv2 = pv2{rv, rv};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float z = y[r] * csc[r] + csh[r];
-          const float sg = sigmoidf_(z);
-          const float sp = sg * (1.0f + z * (1.0f - sg)) * rv;
-          const float xh = (y[r] - cmu[r]) * cis[r];
-          const float dsp = d[r] * sp;
-          se[0][r] += d[r] * (z * sg);  // d = 0 on masked rows (gs rows are zero)
-          se[1][r] += dsp;
-          se[2][r] += sp;
-          se[3][r] += dsp * xh;
-          se[4][r] += sp * xh;
+        for (int hp = 0; hp < 2; ++hp) {
+          const pv2 dd = pv2{d[2 * hp], d[2 * hp + 1]}, yy = pv2{y[2 * hp], y[2 * hp + 1]};
+          const pv2 z = yy * csc[hp] + csh[hp];
+          const pv2 sg = pv2{sigmoidf_(z.x), sigmoidf_(z.y)};
+          const pv2 sp = sg * (1.0f + z * (1.0f - sg)) * rv2;
+          const pv2 xh = (yy - cmu[hp]) * cis[hp];
+          const pv2 dsp = dd * sp;
+          se[0][hp] += dd * (z * sg);  // d = 0 on masked rows (gs rows are zero)
+          se[1][hp] += dsp;
+          se[2][hp] += sp;
+          se[3][hp] += dsp * xh;
+          se[4][hp] += sp * xh;
         }
       }
       // ---- weight gradient: dW[n][k-block] += gs^T . act over the 64 rows ----
@@ -323,28 +339,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PWL_WPE))) 
       // ---- end of a frame: the SE/BN sums of its channels ----
       if (st % spf == spf - 1) {
         const int64_t n = (int64_t)a.F * K;
+        float sv[5][4];
 #pragma unroll
         for (int qq = 0; qq < 5; ++qq)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float v = se[qq][r];
+            float v = se[qq][r >> 1][r & 1];
             v += __shfl_xor(v, 1, 64);
             v += __shfl_xor(v, 2, 64);
             v += __shfl_xor(v, 4, 64);
             v += __shfl_xor(v, 8, 64);
-            se[qq][r] = v;
+            sv[qq][r] = v;
           }
         if ((lane & 15) == 0) {
 #pragma unroll
           for (int qq = 0; qq < 5; ++qq)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              if (cval[r] != 0.f) a.part[((int64_t)qq * a.hsplit + h) * n + (int64_t)f * K + k0 + kl + r] = se[qq][r];
+              if (cval[r] != 0.f) a.part[((int64_t)qq * a.hsplit + h) * n + (int64_t)f * K + k0 + kl + r] = sv[qq][r];
         }
 #pragma unroll
         for (int qq = 0; qq < 5; ++qq)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) se[qq][r] = 0.f;
+          for (int hp = 0; hp < 2; ++hp) se[qq][hp] = pv2{0.f, 0.f};
       }
     }
     lds_barrier();  // C tile complete; every read of this step's Gs / Xs / Ys done
@@ -424,13 +441,11 @@ static int pb_launch(hipStream_t s, PwlBwdArgs<T>& a, int64_t slab_cap, float* d
   return launch_reduce_slabs(s, a.slab, (int)parts, per, dW, accumulate);
 }
 
-#ifndef DFD_PWL_F16_TU
 // 0: launched (all three outputs); 2: launched without the weight gradient (the caller runs it);
 // 1: shape not covered (the caller runs the three unfused launches); -1: error
 bool pwl_bwd_covers(int frames, int HW, int N, int K) {
   return frames > 0 && HW > 0 && !(N & 7) && !(K & 15) && N <= 24 && (int64_t)frames * HW * std::max(N, K) < (1ll << 31);
 }
-#endif
 
 template <typename T>
 int launch_pwl_bwd(hipStream_t s, const T* gs, const T* y3, const float* coef3, const T* wt, const T* y2,
@@ -462,16 +477,8 @@ int launch_pwl_bwd(hipStream_t s, const T* gs, const T* y3, const float* coef3, 
   template int launch_pwl_bwd<T>(hipStream_t, const T*, const T*, const float*, const T*, const T*, const float*, \
                                  const float*, const float*, const float*, const float*, int, int, int, int, T*,   \
                                  float*, int64_t, float*, bool, float*, int64_t, int*);
-// The fp16 instance is compiled in its own translation unit (k_pwl_bwd_f16.hip) without SLP
-// vectorisation: its SLP-packed (v_pk_*_f32) BN2 sums gave run-to-run different sum(d * silu') and
-// sum(d * silu' * xhat) partials on MI355X (tools/pwl_det: 16-185 of F x K entries differ between two
-// identical launches at 32 frames; the d-free sums and the data / weight gradients bit-identical),
-// the same source without SLP is bit-reproducible like the bf16 instance
-#ifdef DFD_PWL_F16_TU
-DFD_PWL_INST(f16)
-#else
 DFD_PWL_INST(bf16)
-#endif
+DFD_PWL_INST(f16)
 #undef DFD_PWL_INST
 
 }  // namespace dfd

@@ -70,7 +70,8 @@ struct Tuning {
 // launches (bit 0: the SE-backward chain's BN2 finalize); bit 1: the SE excitation's first product
 // split over its channel slices (k_bn.hip SeSplit); bit 2: BN backward finalize inside the apply pass
 // (bn_bwd_apply_fin) where the producer wrote <= 256 stat rows; bit 3: forward BN finalize inside the
-// consumer (depthwise forward, SE squeeze, global average pool) where the producer wrote <= 64 rows
+// consumer (depthwise forward, SE squeeze, global average pool) where the producer wrote <= 128 rows
+// (kBnFinRowsMax)
 #ifndef DFD_TAIL_FIN_DEFAULT
 #define DFD_TAIL_FIN_DEFAULT 15
 #endif
@@ -323,6 +324,10 @@ struct SeScratch {
   int bar_slots;
   float* tp;
   int64_t tp_cap;  // floats
+  // a timed-out slice barrier raises these (tail.h SyncAbort): a zeroed device word the waiters poll
+  // and the plan's sticky host word, checked on every later call of the plan
+  int* abort_dev = nullptr;
+  int* abort_host = nullptr;
 };
 // SE excitation: sq = inv_hw * sum_h part (stored) ; r = silu(Wr sq + br) ; gate = sigmoid(We r + be) ; saves rpre
 int launch_se_fc_fwd(hipStream_t s, const float* part, int hsplit, float inv_hw, float* sq, const float* wr,
@@ -393,6 +398,8 @@ struct MfmaGemm {
 };
 int launch_mfma_small_gemm(hipStream_t s, const MfmaGemm& g);
 int launch_mfma_small_gemm2(hipStream_t s, const MfmaGemm& g0, const MfmaGemm& g1);  // one launch, same K
+// test seam: CU-holding workgroups spinning for a bounded time (k_test.hip, dfd_test_occupy)
+int launch_occupy(hipStream_t s, int workgroups, int64_t microseconds);
 // n independent products of equal K in one launch per kMaxBatch (workgroup ranges per product)
 constexpr int kMfmaBatch = 8;
 int launch_mfma_small_gemm_batch(hipStream_t s, const MfmaGemm* g, int n);

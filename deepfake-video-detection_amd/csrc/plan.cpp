@@ -234,7 +234,22 @@ int plan_build(Plan& p, int frames, int H, int W, int dtype) {
   p.offs.assign(p.tensors.size(), -1);
   p.bound = false;
   DFD_HIP_CHECK(hipGetDevice(&p.device));
+  if (!p.err_host) {
+    DFD_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.err_host), sizeof(int), hipHostMallocCoherent));
+    *reinterpret_cast<volatile int*>(p.err_host) = 0;
+  }
   return 0;
+}
+
+int plan_status(const Plan& p) { return p.err_host ? *reinterpret_cast<volatile const int*>(p.err_host) : 0; }
+
+// every plan entry refuses to run after a timed-out software barrier (plan_status)
+static int check_status(const Plan& p) {
+  if (plan_status(p) == 0) return 0;
+  set_error("b0 plan: a software barrier (SE slice sync) timed out in an earlier call -- that call's outputs "
+            "were invalid (another stream's kernels held the CUs the grid needed); clear the status "
+            "(dfd_b0_plan_clear_status) to use this plan again", __FILE__, __LINE__);
+  return -1;
 }
 
 int plan_bind(Plan& p, const int64_t* offs, int n) {
@@ -316,7 +331,7 @@ void plan_free(Plan& p) {
   probe_disarm(p);
   aux_free(p);
   if (p.cast_dev) { (void)hipFree(p.cast_dev); p.cast_dev = nullptr; }
-
+  if (p.err_host) { (void)hipHostFree(p.err_host); p.err_host = nullptr; }
 }
 
 // ------------------------------------------------------------------ forward / backward
@@ -414,10 +429,14 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   // global average pool), which runs it inside its own launch where the stat rows are few (bnfin.h;
   // knob tail_fin bit 3) or launches it first; eval: nothing to finalize (fin() is a no-op too)
   const bool cfin = tr && (tune(TK_TAIL_FIN) & 8) != 0;
-  auto fin_desc = [&](const BNL& b, int64_t count) {
-    return BnFwdFin{r.f(p.o_stats), rows, count, r.prm(b.t_w), r.prm(b.t_b), bnb + p.offs[b.t_rm],
+  auto fin_desc = [&](const BNL& b, int64_t count, float* rows_at) {
+    return BnFwdFin{rows_at, rows, count, r.prm(b.t_w), r.prm(b.t_b), bnb + p.offs[b.t_rm],
                     bnb + p.offs[b.t_rv], mom, eps, r.f(b.o_mean), r.f(b.o_invstd), r.f(b.o_scale), r.f(b.o_shift)};
   };
+  // the depthwise forward reduces BN1's stat rows (o_stats) in its prologue while its own workgroups
+  // store BN2's partial rows in their epilogue: with the finalize inside that launch the BN2 rows go to
+  // o_stats2, so no workgroup can overwrite a BN1 row another one has not read yet
+  float* const dstats = cfin ? r.f(p.o_stats2) : stats;
   DFD_HIP_CHECK(hipMemsetAsync(ws + p.o_ctr, 0, kCtrSlots * sizeof(unsigned), s));
   unsigned* const ctr = reinterpret_cast<unsigned*>(ws + p.o_ctr);
   DFD_TRY(launch_cast_params<T>(s, P, reinterpret_cast<T*>(ws), p.cast_dev, (int)p.cast_host.size(), p.cast_max));
@@ -462,25 +481,26 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
     }
     if (b.ds) {
       DFD_TRY(launch_dw_fwd<T>(s, g, r.a(p.o_ystem), r.prm(b.t_dw), r.a(b.o_y2), r.pro_bn(p.bn_stem, b.hin * b.win),
-                               PRO_BN_SILU, stats, &rows));
+                               PRO_BN_SILU, dstats, &rows));
     } else {
       PROBED(PK_PW_FWD, &b, (launch_pw_gemm<T>(s, xin, r.a(b.pw.o_w), r.a(b.o_y1), nullptr, Min, b.mid, b.cin,
                                                PRO_NONE, Pro{}, stats, &rows)));
       if (!cfin) DFD_TRY(fin(b.bn1, Min));
-      const BnFwdFin f1 = fin_desc(b.bn1, Min);
+      const BnFwdFin f1 = fin_desc(b.bn1, Min, stats);
       PROBED(PK_DW_FWD, &b, (launch_dw_fwd<T>(s, g, r.a(b.o_y1), r.prm(b.t_dw), r.a(b.o_y2),
-                                              r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU, stats, &rows,
+                                              r.pro_bn(b.bn1, b.hin * b.win), PRO_BN_SILU, dstats, &rows,
                                               cfin ? &f1 : nullptr)));
     }
     if (!cfin) DFD_TRY(fin(bn_dw, Mout));
-    const BnFwdFin f2 = fin_desc(bn_dw, Mout);
+    const BnFwdFin f2 = fin_desc(bn_dw, Mout, dstats);
     T* s2 = b.o_s2 >= 0 ? r.a(b.o_s2) : nullptr;
     int hs = 1;
     PROBED(PK_SE_SQUEEZE, &b, (launch_se_squeeze<T>(s, r.a(b.o_y2), r.pro_bn(bn_dw, hwo), p.frames, hwo, b.mid,
                                                     r.f(p.o_part), p.part_cap, &hs, s2, cfin ? &f2 : nullptr)));
     // the excitation's first product split over its channel slices (knob tail_fin bit 1); o_stats is free
     // between the BN2 finalize and the projection's BN3 statistics
-    const SeScratch sesc{ctr + kCtrSe, kCtrSlots - kCtrSe, r.f(p.o_stats), p.stats_cap};
+    const SeScratch sesc{ctr + kCtrSe, kCtrAbort - kCtrSe, r.f(p.o_stats), p.stats_cap,
+                         reinterpret_cast<int*>(ctr + kCtrAbort), p.err_host};
     DFD_TRY(launch_se_fc_fwd(s, r.f(p.o_part), hs, 1.0f / (float)hwo, r.f(b.o_sq), r.prm(b.t_se_wr),
                              r.prm(b.t_se_br), r.prm(b.t_se_we), r.prm(b.t_se_be), p.frames, b.mid, b.rd,
                              r.f(b.o_rpre), r.f(b.o_gate), (tune(TK_TAIL_FIN) & 2) ? &sesc : nullptr));
@@ -496,7 +516,7 @@ int forward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const
   DFD_TRY(launch_pw_gemm<T>(s, xin, r.a(p.head.o_w), r.a(p.o_yh), nullptr, Mf, kHead, p.head.cin, PRO_NONE, Pro{},
                             stats, &rows));
   if (!cfin) DFD_TRY(fin(p.bn_head, Mf));
-  const BnFwdFin fh = fin_desc(p.bn_head, Mf);
+  const BnFwdFin fh = fin_desc(p.bn_head, Mf, stats);
   DFD_TRY(launch_gap<T>(s, r.a(p.o_yh), r.pro_bn(p.bn_head, p.Hf * p.Wf), p.frames, p.Hf * p.Wf, kHead, feat,
                         cfin ? &fh : nullptr));
   return 0;
@@ -714,9 +734,10 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         // excitation launch's last workgroups (knob tail_fin bit 0), o_stats free as row scratch here
         const bool sefin = (tune(TK_TAIL_FIN) & 1) != 0;
         // the split excitation's partial products behind the finalize rows in o_stats
-        const SeScratch sesc{ctr + kCtrSe, kCtrSlots - kCtrSe, r.f(p.o_stats) + p.stats_cap / 2,
-                             p.stats_cap / 2};
-        const BnFramesFin bnf{reinterpret_cast<double*>(r.f(p.o_stats)), p.stats_cap, ctr, kCtrSe, Mout,
+        const SeScratch sesc{ctr + kCtrSe, kCtrAbort - kCtrSe, r.f(p.o_stats) + p.stats_cap / 2,
+                             p.stats_cap / 2, reinterpret_cast<int*>(ctr + kCtrAbort), p.err_host};
+        // (the finalize rows may use only the first half: the split's products sit in the second)
+        const BnFramesFin bnf{reinterpret_cast<double*>(r.f(p.o_stats)), p.stats_cap / 2, ctr, kCtrSe, Mout,
                               r.prm(bn_dw.t_w), r.f(bn_dw.o_mean), r.f(bn_dw.o_invstd), tr != 0, acc != 0,
                               grad(bn_dw.t_w), grad(bn_dw.t_b), r.f(p.o_coef)};
         DFD_TRY(launch_se_fc_bwd(s, r.f(p.o_part), hs, r.f(b.o_gate), r.f(b.o_de), r.f(b.o_sq), r.f(b.o_rpre),
@@ -904,6 +925,7 @@ TuningScope::~TuningScope() { t_tune = prev; }
 int plan_forward(Plan& p, hipStream_t s, const void* x, const int64_t* xs, const InputFmt& in, const float* params,
                  float* bnbuf, char* ws, float* feat, int training, float momentum) {
   if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
+  DFD_TRY(check_status(p));
   const TuningScope ts(&p.tune);
   if (p.dtype == 1) return forward_impl<bf16>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
   if (p.dtype == 2) return forward_impl<f16>(p, s, x, xs, in, params, bnbuf, ws, feat, training, momentum);
@@ -914,6 +936,7 @@ int plan_backward_x(Plan& p, hipStream_t s, const void* x, const int64_t* xs, co
                     const float* params, char* ws, float* grads, int training, int seg_begin, int seg_end,
                     int accumulate) {
   if (!p.bound) { set_error("plan not bound", __FILE__, __LINE__); return -1; }
+  DFD_TRY(check_status(p));
   if (seg_begin < 0 || seg_end > kNumSegments || seg_begin > seg_end) {
     set_error("backward: bad segment range", __FILE__, __LINE__);
     return -1;

@@ -54,7 +54,10 @@ struct Probe {
 };
 
 constexpr int kCtrSlots = 1024;
-constexpr int kCtrSe = 64;  // counters [0, kCtrSe): last-arrival tails; [kCtrSe, kCtrSlots): SE slice barriers
+// counters [0, kCtrSe): last-arrival tails; [kCtrSe, kCtrAbort): SE slice barriers; kCtrAbort: the
+// device abort word of the slice barriers (tail.h SyncAbort)
+constexpr int kCtrSe = 64;
+constexpr int kCtrAbort = kCtrSlots - 1;
 
 struct Plan {
   int frames, H, W, dtype;
@@ -88,7 +91,14 @@ struct Plan {
   hipStream_t aux = nullptr;
   int aux_dev = -1;
   hipEvent_t ev[6] = {};
+  // sticky error word in coherent pinned host memory: a device-side software barrier that timed out
+  // (its launch's outputs invalid) sets it; every later forward / backward of the plan then fails
+  // (dfd_last_error) until dfd_b0_plan_clear_status -- loud, with no host synchronisation per call
+  int* err_host = nullptr;
 };
+// the sticky status word (0: ok), read without synchronising (the caller synchronises first for a
+// definitive answer)
+int plan_status(const Plan& p);
 
 int probe_arm(Plan& p, int kind, int stage, int idx, int n);
 int probe_read(Plan& p, float* ms, int cap, int* count);

@@ -51,27 +51,60 @@ __device__ __forceinline__ bool tail_arrive(unsigned* ctr, unsigned expected) {
   return tail_last != 0;
 }
 
+// Where a timed-out barrier is reported.  `dev`: a device word every waiter polls, so one timeout
+// releases the whole grid at once; `host`: a word in coherent pinned host memory the plan checks on
+// every later call (sticky until the host clears it), so a launch whose outputs are invalid can never
+// go unnoticed -- no host synchronisation on the normal path.  Either may be null.
+struct SyncAbort {
+  int* dev;
+  int* host;
+};
+
+// wall-clock budget of a software barrier: 2 s of the 100 MHz constant clock.  A group that is not
+// co-resident within it (e.g. another stream's kernels hold the CUs) gives up instead of hanging.
+constexpr unsigned long long kSyncBudgetTicks = 200000000ull;
+
+__device__ __forceinline__ void sync_abort_raise(const SyncAbort& ab) {
+  if (ab.dev) __hip_atomic_store(ab.dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ab.host) __hip_atomic_store(ab.host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The n workgroups sharing `arrive` / `depart` (all co-resident) wait for each other: every one's
 // prior global writes are visible to all after the call (agent-scope release before arriving, acquire
 // after the wait).  The last to leave zeroes both counters for the next launch (zero at rest).
-// Bounded poll: a grid that could not be co-resident leaves after ~2^24 polls instead of hanging (its
-// outputs are then invalid; callers launch this form only when the grid fits the device at once).
-__device__ __forceinline__ void group_sync(unsigned* arrive, unsigned* depart, unsigned n) {
+// Bounded: a group that could not be co-resident raises the abort words after kSyncBudgetTicks and
+// every waiter that sees the device word leaves; the call returns false and the launch's outputs are
+// invalid (the host reports it: SyncAbort).  Callers launch this form only when the grid fits the
+// device at once.
+__device__ __forceinline__ bool group_sync(unsigned* arrive, unsigned* depart, unsigned n, SyncAbort ab = {}) {
+  __shared__ int group_sync_ok;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    const unsigned long long t0 = wall_clock64();
     unsigned spins = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n && ++spins < (1u << 24))
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
       __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255u) != 0) continue;  // the slow checks every 256 polls
+      if (ab.dev && __hip_atomic_load(ab.dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
+      if (wall_clock64() - t0 > kSyncBudgetTicks || spins > (1u << 27)) {  // (a poll count too, never unbounded)
+        sync_abort_raise(ab);
+        ok = 0;
+        break;
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (__hip_atomic_fetch_add(depart, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1) {
       __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(depart, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    group_sync_ok = ok;
   }
   __syncthreads();
+  return group_sync_ok != 0;
 }
 
 }  // namespace dfd

@@ -222,29 +222,32 @@ class _FusedAdamBase(torch.optim.Optimizer):
         return loss
 
     def _step_scaled(self, ranges, grads, loss):
-        """Scaled-gradient step: norm (+ found_inf), device-skipped Adam(W), scale update."""
+        """Scaled-gradient step: norm (+ found_inf) over every range, device-skipped Adam(W) per range,
+        one scale update.  Several ranges arise with several flat buffers (``EnsembleDetector``: one
+        per member) or frozen parameters (the reference's ``freeze_backbone``); the bias corrections
+        of every range use the scaler's applied-step count (torch's per-parameter count whenever the
+        trained parameters get a gradient every step, as they do in the reference's loops)."""
         sc = self.loss_scaler
-        if len(ranges) != 1 or ranges[0][2] != 0 or ranges[0][3] != len(self.param_groups[0]["params"]):
-            raise RuntimeError("loss-scaled step: every parameter needs a gradient (one flat range)")
         g = self.param_groups[0]
-        (lo, hi, i0, i1), (flat_g, scatter) = ranges[0], grads[0]
         max_norm = float(self.max_grad_norm) if self.max_grad_norm is not None else 0.0
-        torch.ops.dfd.grad_norm_scaled(flat_g, max_norm, sc.state, self._scratch, self._norm)
+        allg = grads[0][0] if len(grads) == 1 else torch.cat([fg for fg, _ in grads])
+        torch.ops.dfd.grad_norm_scaled(allg, max_norm, sc.state, self._scratch, self._norm)
         clip = self._norm if self.max_grad_norm is not None else None
         b1, b2 = g["betas"]
-        k = self._run_of[i0]
-        ro = self._run_off[k]
-        torch.ops.dfd.adam_step_scaled(self._runs[k][0][lo - ro:hi - ro], flat_g, self._m[lo:hi], self._v[lo:hi],
-                                       float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                       float(g["weight_decay"]), float(self.grad_scale), bool(self.decoupled), clip,
-                                       sc.state)
+        for (lo, hi, i0, i1), (flat_g, scatter) in zip(ranges, grads):
+            k = self._run_of[i0]
+            ro = self._run_off[k]
+            torch.ops.dfd.adam_step_scaled(self._runs[k][0][lo - ro:hi - ro], flat_g, self._m[lo:hi], self._v[lo:hi],
+                                           float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                           float(g["weight_decay"]), float(self.grad_scale), bool(self.decoupled),
+                                           clip, sc.state)
+            if scatter is not None:
+                o = 0
+                for t in scatter:
+                    t.copy_(flat_g[o:o + t.numel()].view(t.shape))
+                    o += t.numel()
         sc.update()
         self._scaled_steps = True  # per-parameter step counts live on the device (scaler applied steps)
-        if scatter is not None:
-            o = 0
-            for t in scatter:
-                t.copy_(flat_g[o:o + t.numel()].view(t.shape))
-                o += t.numel()
         return loss
 
     # -- checkpoints: torch.optim.Adam(W)-format state ({step, exp_avg, exp_avg_sq} per parameter), so

@@ -102,7 +102,7 @@ class KernelProbe:
 
     def report(self, traffic_file: str | None = None):
         frames, H, W, dtype, _dev = self.key
-        es = 2 if dtype == 1 else 4
+        es = 2 if dtype in (1, 2) else 4  # bf16 and fp16 store 2-byte elements, fp32 4
         nbytes, flops = algorithmic(self.kind, self.stage, self.block, frames, H, W, es)
         if not self.ms:
             return None

@@ -38,9 +38,10 @@ class TrainStep:
         self.optimizer = cls(model.parameters(), lr=lr, weight_decay=weight_decay, max_grad_norm=max_grad_norm)
         self.world_size = world_size
         # fp16 trunk: dynamic loss scaling (torch.amp.GradScaler semantics, on the device).  "auto" =
-        # on for compute_dtype "fp16", off otherwise; or a DynamicLossScaler / None.
+        # on when any submodule computes in fp16 (the detector, or a member of EnsembleDetector), off
+        # otherwise; or a DynamicLossScaler / None.
         if loss_scale == "auto":
-            fp16 = getattr(model, "compute_dtype", None) == "fp16"
+            fp16 = any(getattr(m, "compute_dtype", None) == "fp16" for m in model.modules())
             loss_scale = DynamicLossScaler(self.optimizer._m.device) if fp16 else None
         self.loss_scaler = loss_scale
         self.optimizer.set_loss_scaler(loss_scale)

@@ -111,6 +111,19 @@ DFD_API int dfd_b0_grad_tensor(const dfd_b0_plan* plan, int block, int64_t* byte
  * then invalid; the flag is cleared at the start of each training forward).  No reference
  * counterpart: the reference's forward is torch's eager timm module. */
 DFD_API int dfd_b0_fused_info(const dfd_b0_plan* plan, int* nblocks, int64_t* abort_offset);
+/* Sticky plan status (0 ok, 1 a device-side software barrier timed out -- the split SE excitation's
+ * slice barrier, when another stream's kernels held the CUs its grid needed -- and that call's
+ * outputs were invalid).  Set by the device in pinned host memory, so reading it needs no device
+ * call (synchronise the stream first for a definitive answer).  While it is set, every
+ * forward / backward call of the plan fails with dfd_last_error() explaining why; clear it to
+ * run again.  Error convention of the reference's callers: app.py:2320-2321 turns the raised error
+ * into an error dict. */
+DFD_API int dfd_b0_plan_status(const dfd_b0_plan* plan, int* status);
+DFD_API int dfd_b0_plan_clear_status(dfd_b0_plan* plan);
+/* Test seam: `workgroups` 1024-thread workgroups, each holding a whole CU's LDS, that spin for
+ * `microseconds` (wall clock, bounded) on `stream` -- occupies CUs so tests can run the plan next to
+ * a kernel that denies it the device (tests/test_se_sync_gpu.py). */
+DFD_API int dfd_test_occupy(void* stream, int workgroups, int64_t microseconds);
 /* Tensor index range [*lo, *hi) whose gradients are final after segment `seg`. */
 DFD_API int dfd_b0_segment_tensors(int seg, int* lo, int* hi);
 

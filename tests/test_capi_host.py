@@ -147,3 +147,17 @@ def test_hash_uniform_portable():
     assert a.dtype == np.float32 and a.min() >= -1.0 and a.max() < 1.0
     assert np.array_equal(a, hash_uniform(3, "x", 1000))
     assert not np.array_equal(a, hash_uniform(4, "x", 1000))
+
+
+def test_train_step_auto_loss_scaling_sees_ensemble_members():
+    """TrainStep(loss_scale="auto") turns dynamic loss scaling on when ANY submodule computes in fp16
+    -- EnsembleDetector has no compute_dtype of its own -- and leaves it off otherwise."""
+    from deepfake_amd.pretrained_detector import EnsembleDetector
+    from deepfake_amd.trainer import TrainStep
+
+    ens16 = EnsembleDetector(["efficientnet_b0", "efficientnet_b0"], pretrained=False, compute_dtype="fp16")
+    assert TrainStep(ens16).loss_scaler is not None
+    ens32 = EnsembleDetector(["efficientnet_b0"], pretrained=False)
+    assert TrainStep(ens32).loss_scaler is None
+    det16 = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, compute_dtype="fp16")
+    assert TrainStep(det16).loss_scaler is not None

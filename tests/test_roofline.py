@@ -74,3 +74,17 @@ def test_pointwise_sweep_sites_and_totals(monkeypatch):
     assert out["gpu_us_per_step"] == pytest.approx(930.0)
     assert out["mfma_frac"] == pytest.approx(fl / 930e-6 / R.MFMA_BF16_PEAK, rel=1e-3)
     assert out["arith_intensity"] < out["ridge_flop_per_byte"]  # HBM-bound shapes
+
+
+def test_probe_report_element_size_per_dtype():
+    """fp16 (plan dtype 2) stores 2-byte elements like bf16 (it was costed at 4 bytes and
+    reported frac ~0.95 at the bf16 kernel's duration); fp32 4."""
+    from deepfake_amd.roofline import KernelProbe, algorithmic
+
+    for dt, es in ((0, 4), (1, 2), (2, 2)):
+        p = KernelProbe(None, "dw_bwd", 1, 0)
+        p.key = (256, 224, 224, dt, 0)
+        p.ms = [0.4]
+        r = p.report(traffic_file="/nonexistent/traffic.json")
+        assert r["algorithmic_bytes"] == algorithmic("dw_bwd", 1, 0, 256, 224, 224, es)[0]
+        assert abs(r["frac"] - r["algorithmic_bytes"] / 0.4e-3 / 8e12) < 1e-4

@@ -1,0 +1,111 @@
+"""The split SE excitation's slice barrier under device contention.
+
+At 256 frames the SE excitation of the 1152-channel blocks splits its first product over 5 channel
+slices that meet at a software barrier (``k_bn.hip`` se_chain_kernel, ``tail.h`` group_sync).  The
+launcher turns the split on only when the grid fits the device at once, but another stream's kernels
+(the data-parallel trainer's RCCL all-reduce runs on a side stream during backward) can
+hold the CUs the grid needs.  The barrier is bounded (2 s of wall clock); a group that times out
+raises a device word every waiter polls AND a sticky word in the plan's pinned host memory, so:
+
+* either the step completes with results bit-identical to an uncontended step,
+* or the plan reports the failure -- ``B0Runtime.check_status()`` raises, every later call of the plan
+  raises (``dfd_last_error`` explains why), and after ``clear_status()`` the plan runs again and is
+  bit-identical to the uncontended step.
+
+Silent wrong output is the one outcome this test rejects.  The contention is ``dfd_test_occupy``:
+workgroups that each hold a whole CU's LDS and spin for a bounded time on another stream, leaving 2 of
+the device's CUs to the step (fewer than one frame tile's 5 slices).  Reference error convention:
+``app.py:2320-2321`` turns a raised error into an error dict.
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from deepfake_amd import _lib
+from deepfake_amd.pretrained_detector import PretrainedBackboneDetector
+from deepfake_amd.weights import deterministic_init_
+
+pytestmark = pytest.mark.gpu
+
+B, T, HW = 32, 8, 224  # 256 frames: nft = 16 frame tiles x 5 slices = 80 workgroups <= CUs -> split on
+SEED = 41
+OCCUPY_US = 3_000_000  # longer than the barrier's 2 s budget
+
+
+def _model(cuda):
+    det = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.0,
+                                     compute_dtype="bf16")
+    deterministic_init_(det, seed=SEED)
+    return det.to(cuda).train()
+
+
+def _inputs(cuda):
+    g = torch.Generator().manual_seed(9)
+    x = torch.randint(0, 256, (B, T, HW, HW, 3), generator=g, dtype=torch.uint8).to(cuda).permute(0, 1, 4, 2, 3)
+    y = torch.tensor([(i * 5 + 2) % 2 for i in range(B)], device=cuda)
+    return x, y
+
+
+def _step(det, x, y):
+    logits, _ = det(x)
+    loss = F.cross_entropy(logits, y)
+    loss.backward()
+    return logits
+
+
+def _result(det, logits):
+    torch.cuda.synchronize()
+    return logits.detach().cpu(), {n: p.grad.detach().cpu().clone() for n, p in det.named_parameters()}
+
+
+def _same(a, b):
+    la, ga = a
+    lb, gb = b
+    return torch.equal(la, lb) and all(torch.equal(ga[n], gb[n]) for n in ga)
+
+
+def test_se_split_under_contention(cuda):
+    lib = _lib.load()
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    x, y = _inputs(cuda)
+
+    ref_det = _model(cuda)
+    ref = _result(ref_det, _step(ref_det, x, y))
+    rt = ref_det.backbone.runtime()
+    rt.check_status()  # an uncontended step never trips the barrier
+    del ref_det
+
+    det = _model(cuda)
+    rt = det.backbone.runtime()
+    side = torch.cuda.Stream(cuda)
+    _lib.check(lib.dfd_test_occupy(ctypes.c_void_p(side.cuda_stream), cus - 2, OCCUPY_US))
+    logits = None
+    raised = None
+    try:
+        logits = _step(det, x, y)
+        torch.cuda.synchronize()
+        rt.check_status(synchronize=False)
+    except _lib.DFDError as e:  # the barrier timed out: reported, not silent
+        raised = str(e)
+    side.synchronize()
+    if raised is None:
+        got = _result(det, logits)
+        assert _same(got, ref), "contended step completed but differs from the uncontended one (silent corruption)"
+        print("contended step completed bit-identical")
+        return
+    assert "timed out" in raised
+    print("contended step reported:", raised)
+    # sticky: every later call of the plan refuses to run until cleared
+    det.zero_grad(set_to_none=True)
+    with pytest.raises(_lib.DFDError, match="timed out"):
+        _step(det, x, y)
+    rt.clear_status()
+    rt.check_status()
+    # the plan works again; a fresh model (the failed step moved BN running stats) matches the reference
+    del det
+    det = _model(cuda)
+    got = _result(det, _step(det, x, y))
+    det.backbone.runtime().check_status()
+    assert _same(got, ref)

@@ -120,18 +120,26 @@ def test_fused_adam_vs_torch(cuda, kind, scale, freeze):
 # ------------------------------------------------------ dynamic loss scaling (the fp16 train step)
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["adamw", "adam"])
-def test_loss_scaled_adam_vs_torch_gradscaler(cuda, kind):
+@pytest.mark.parametrize("layout", ["one", "two_runs", "frozen"])
+def test_loss_scaled_adam_vs_torch_gradscaler(cuda, kind, layout):
     """DynamicLossScaler + FusedAdam(W) (device-side unscale / clip / skip / update) against
     torch.amp.GradScaler around clip_grad_norm_ + torch.optim.AdamW / Adam, fed the same SCALED
     gradients (the gradient of loss * scale): a non-finite step (step 2) is skipped and halves the
     scale, growth_interval = 2 finite steps double it again; parameters, moments, clipped unscaled
-    .grad, scale and the step counts of the checkpoint match."""
+    .grad, scale and the step counts of the checkpoint match.  Layouts: one flat buffer; two
+    FlatModules (two runs: ``EnsembleDetector`` has one per member); a parameter that never
+    gets a gradient (the reference's ``freeze_backbone``)."""
     import warnings
 
     from deepfake_amd.optim import DynamicLossScaler
-    m = _Flat().to(cuda)
-    ref = _Flat()
-    params, rparams = list(m.parameters()), list(ref.parameters())
+    if layout == "two_runs":
+        m1, m2 = _Flat().to(cuda), _Flat().to(cuda)
+        params = list(m1.parameters()) + list(m2.parameters())
+        rparams = list(_Flat().parameters()) + list(_Flat().parameters())
+    else:
+        m = _Flat().to(cuda)
+        params, rparams = list(m.parameters()), list(_Flat().parameters())
+    frozen = {1} if layout == "frozen" else set()
     shapes = [p.shape for p in params]
     Fused, Torch = (FusedAdamW, torch.optim.AdamW) if kind == "adamw" else (FusedAdam, torch.optim.Adam)
     opt = Fused(params, lr=1e-3, weight_decay=1e-2, max_grad_norm=1.0)
@@ -151,12 +159,12 @@ def test_loss_scaled_adam_vs_torch_gradscaler(cuda, kind):
             gs[0].view(-1)[0] = float("nan")
         flat = torch.cat([gg.flatten() for gg in gs]).to(cuda)
         o = 0
-        for p, q, gg in zip(params, rparams, gs):
-            p.grad = flat[o:o + gg.numel()].view(gg.shape)
+        for i, (p, q, gg) in enumerate(zip(params, rparams, gs)):
+            p.grad = None if i in frozen else flat[o:o + gg.numel()].view(gg.shape)
             o += gg.numel()
-            q.grad = gg.clone()
+            q.grad = None if i in frozen else gg.clone()
         tsc.unscale_(topt)
-        torch.nn.utils.clip_grad_norm_(rparams, max_norm=1.0)
+        torch.nn.utils.clip_grad_norm_([q for q in rparams if q.grad is not None], max_norm=1.0)
         tsc.step(topt)
         tsc.update()
         opt.step()
@@ -166,6 +174,8 @@ def test_loss_scaled_adam_vs_torch_gradscaler(cuda, kind):
         for i, (p, q) in enumerate(zip(params, rparams)):
             torch.testing.assert_close(p.detach().cpu(), q.detach(), rtol=1e-5, atol=1e-7,
                                        msg=lambda t: f"step {step} param {i}: {t}")
+            if i in frozen:
+                continue
             if step not in (2, 4):  # torch leaves unscaled non-finite grads; the skipped step leaves them scaled
                 torch.testing.assert_close(p.grad.cpu(), q.grad, rtol=1e-5, atol=1e-8)
             st, rst = opt.state[p], topt.state[q]
