@@ -1,0 +1,34 @@
+// Test seam (dfd_test_occupy): workgroups that hold whole CUs for a bounded wall-clock time, so a GPU
+// test can run the B0 plan while another stream's kernel denies it most of the device (the split SE
+// excitation's slice barrier must then either complete or fail loudly, tail.h SyncAbort).
+#include "kernels.h"
+
+namespace dfd {
+
+constexpr int kOccupyLds = 160 * 1024 - 64;  // the whole CU's LDS: no other workgroup with LDS fits beside it
+
+__global__ __launch_bounds__(1024) void occupy_kernel(unsigned long long ticks, int* sink) {
+  __shared__ char hold[kOccupyLds];
+  volatile char* h = hold;
+  h[threadIdx.x * 64] = (char)threadIdx.x;  // the allocation is live (not optimised away)
+  __syncthreads();
+  const unsigned long long t0 = wall_clock64();
+  unsigned spins = 0;
+  // bounded twice: the wall clock, and a poll count in case the clock does not advance
+  while (wall_clock64() - t0 < ticks && ++spins < (1u << 26)) __builtin_amdgcn_s_sleep(32);
+  __syncthreads();
+  if (threadIdx.x == 0 && sink) sink[blockIdx.x] = h[64];
+}
+
+int launch_occupy(hipStream_t s, int workgroups, int64_t microseconds) {
+  if (workgroups < 1 || workgroups > 4096 || microseconds < 0 || microseconds > 10000000) {
+    set_error("occupy: 1..4096 workgroups for at most 10 s", __FILE__, __LINE__);
+    return -1;
+  }
+  const unsigned long long ticks = (unsigned long long)microseconds * 100ull;  // 100 MHz constant clock
+  hipLaunchKernelGGL(occupy_kernel, dim3((unsigned)workgroups), dim3(1024), 0, s, ticks, nullptr);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace dfd
