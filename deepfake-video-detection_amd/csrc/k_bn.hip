@@ -1412,7 +1412,8 @@ static SeSplit se_split(const SeScratch* sc, int frames, int C) {
   sp.tp = sc->tp;
   sp.bar = sc->bar;
   sp.on = 1;
-  sp.ab = SyncAbort{sc->abort_dev, sc->abort_host};
+  static const unsigned long long budget = sync_budget_ticks(2.0);
+  sp.ab = SyncAbort{sc->abort_dev, sc->abort_host, budget};
   return sp;
 }
 

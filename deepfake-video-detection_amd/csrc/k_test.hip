@@ -2,6 +2,7 @@
 // test can run the B0 plan while another stream's kernel denies it most of the device (the split SE
 // excitation's slice barrier must then either complete or fail loudly, tail.h SyncAbort).
 #include "kernels.h"
+#include "tail.h"
 
 namespace dfd {
 
@@ -15,7 +16,7 @@ __global__ __launch_bounds__(1024) void occupy_kernel(unsigned long long ticks, 
   const unsigned long long t0 = wall_clock64();
   unsigned spins = 0;
   // bounded twice: the wall clock, and a poll count in case the clock does not advance
-  while (wall_clock64() - t0 < ticks && ++spins < (1u << 26)) __builtin_amdgcn_s_sleep(32);
+  while (wall_clock64() - t0 < ticks && ++spins < (1u << 28)) __builtin_amdgcn_s_sleep(32);
   __syncthreads();
   if (threadIdx.x == 0 && sink) sink[blockIdx.x] = h[64];
 }
@@ -25,7 +26,7 @@ int launch_occupy(hipStream_t s, int workgroups, int64_t microseconds) {
     set_error("occupy: 1..4096 workgroups for at most 10 s", __FILE__, __LINE__);
     return -1;
   }
-  const unsigned long long ticks = (unsigned long long)microseconds * 100ull;  // 100 MHz constant clock
+  const unsigned long long ticks = sync_budget_ticks((double)microseconds * 1e-6);  // the device's wall-clock rate
   hipLaunchKernelGGL(occupy_kernel, dim3((unsigned)workgroups), dim3(1024), 0, s, ticks, nullptr);
   DFD_HIP_CHECK(hipGetLastError());
   return 0;

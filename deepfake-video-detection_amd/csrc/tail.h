@@ -55,14 +55,26 @@ __device__ __forceinline__ bool tail_arrive(unsigned* ctr, unsigned expected) {
 // releases the whole grid at once; `host`: a word in coherent pinned host memory the plan checks on
 // every later call (sticky until the host clears it), so a launch whose outputs are invalid can never
 // go unnoticed -- no host synchronisation on the normal path.  Either may be null.
+// `budget`: wall-clock ticks (wall_clock64) a waiter polls before it gives up -- the launcher sizes it
+// to ~2 s from the device's wall-clock rate (sync_budget_ticks); a group that is not co-resident within
+// it (e.g. another stream's kernels hold the CUs) gives up instead of hanging.
 struct SyncAbort {
   int* dev;
   int* host;
+  unsigned long long budget;
 };
 
-// wall-clock budget of a software barrier: 2 s of the 100 MHz constant clock.  A group that is not
-// co-resident within it (e.g. another stream's kernels hold the CUs) gives up instead of hanging.
+// fallback budget when the launcher passes none: 2 s at a 100 MHz wall clock
 constexpr unsigned long long kSyncBudgetTicks = 200000000ull;
+
+// host side: `seconds` of the current device's wall clock (hipDeviceAttributeWallClockRate, kHz)
+inline unsigned long long sync_budget_ticks(double seconds) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  return (unsigned long long)(seconds * 1e3 * (double)khz);
+}
 
 __device__ __forceinline__ void sync_abort_raise(const SyncAbort& ab) {
   if (ab.dev) __hip_atomic_store(ab.dev, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -84,13 +96,13 @@ __device__ __forceinline__ bool group_sync(unsigned* arrive, unsigned* depart, u
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
-    const unsigned long long t0 = wall_clock64();
+    const unsigned long long t0 = wall_clock64(), budget = ab.budget ? ab.budget : kSyncBudgetTicks;
     unsigned spins = 0;
     while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n) {
       __builtin_amdgcn_s_sleep(1);
       if ((++spins & 255u) != 0) continue;  // the slow checks every 256 polls
       if (ab.dev && __hip_atomic_load(ab.dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
-      if (wall_clock64() - t0 > kSyncBudgetTicks || spins > (1u << 27)) {  // (a poll count too, never unbounded)
+      if (wall_clock64() - t0 > budget || spins > (1u << 27)) {  // (a poll count too, never unbounded)
         sync_abort_raise(ab);
         ok = 0;
         break;

@@ -21,10 +21,12 @@ reference step: ``model(images)`` -> ``CrossEntropyLoss(weight)`` -> ``backward`
 
 Tolerances: fp32 -- logits and loss rtol 1e-3 / atol 1e-5 (north star); every parameter gradient's
 norm within 1e-3 relative and its 64 leading elements within rtol 1e-3 / atol 1e-5 + 1e-3 *
-max|leading|; BN running statistics rtol 1e-4.  bf16 (fp32 accumulation) against the same fp32
-oracle: loss within 2 %; among the tensors whose reference gradient is not structurally zero, at
-least 90 % (32 frames) / 70 % (2 frames) have their norm within 10 % and cosine >= 0.98, and every
-one has cosine >= 0.9 (``BF16_BOUND``).
+max|leading|; BN running statistics rtol 1e-4.  16-bit steps (bf16 / fp16 storage, fp32
+accumulation): loss within 2 % of the fp32 oracle, and a PER-TENSOR gradient bound anchored to fp64
+(``_vs_fp64``): every gradient's relative L2 error against the oracle run in float64 must stay within
+K x the error torch's own bf16 autocast of the same oracle step makes on that tensor (floor 1e-3) --
+the bound scales with how ill-conditioned each tensor is, measured, instead of a count of tensors
+allowed outside a fixed tolerance (K per dtype at ``K_VS_AUTOCAST``).
 """
 import numpy as np
 import pytest
@@ -115,48 +117,73 @@ def test_train_step_224_fp32(cuda, case, kernel_paths):
         torch.testing.assert_close(bufs[n], rb, rtol=1e-4, atol=1e-6, msg=lambda m: f"{n}: {m}")
 
 
-# bf16 bound per batch: (fraction of gradient tensors whose norm is within 10 % AND cosine >= 0.98,
-# minimum cosine of every tensor).  Two frames give the training-mode BatchNorm statistics of only
-# 2 x H x W samples per channel, which amplifies the bf16 rounding of the activations; 32 frames
-# (the reference's clip shape) is the bench-like batch.  On both batches the lowest cosine is the
-# temporal-attention bias (64 values, the gradient of the attention logits' bias): 0.89-0.95
-# depending only on the fp32 summation order inside the trunk's reductions (measured across kernel
-# paths, depthwise tilings and BN channel groupings -- the fp32 runs of the same orders pass the
-# 1e-3 bounds above), hence 0.85; every other tensor stays above 0.94.  The 2-frame fraction sits at
-# the noise floor: 56-62 of 202 tensors outside across launch-fusion variants that only reorder fp64
-# sums (round 5), hence 0.65.  For scale: torch's own bf16 autocast of the same oracle step on the CPU
-# (tools/r05/bf16_floor.py) leaves 191 / 202 (2 frames) and 47 / 202 (32 frames) outside.
-BF16_BOUND = {"b1t2": (0.65, 0.85), "b4t8": (0.90, 0.85)}
-# fp16 storage (10 mantissa bits against bf16's 7) under a static loss scale of 1024: measured 0 of 202
-# tensors outside on both batches (round 5, call E), every cosine >= 0.98
-FP16_BOUND = {"b1t2": (0.95, 0.97), "b4t8": (0.97, 0.98)}
+# The 16-bit bound, per tensor: rel_err(HIP 16-bit grad, fp64 oracle grad) <= K * max(rel_err(torch bf16
+# autocast grad, fp64 oracle grad), 1e-3).  torch's autocast (CPU, same oracle module, same inputs and
+# weights) rounds conv inputs / outputs to bf16 like the HIP bf16 step stores its activations, so its
+# error on a tensor measures that tensor's conditioning under bf16 rounding; the HIP step must be no
+# worse than K times it.  K is stated per dtype; the measured worst ratios are printed by every run and
+# recorded in DESIGN.md (round 6).
+K_VS_AUTOCAST = {"bf16": 3.0, "fp16": 1.0}
+AUTOCAST_FLOOR = 1e-3
 FP16_LOSS_SCALE = 1024.0
+_F64, _AC = {}, {}
 
 
-def _bf16_vs_oracle(case, loss, grads, tag="", bound=None):
-    """the bf16 step's loss and gradients against the fp32 oracle within BF16_BOUND[case]"""
+def oracle64_step(case):
+    """the oracle step in float64 on the CPU (inputs, weights and every op in double; cached)"""
+    if case not in _F64:
+        torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+        x, labels = _inputs(case)
+        m = DetectorCPU(dropout_rate=0.0)
+        deterministic_init_(m, seed=SEED)
+        m = m.double().train()
+        logits, _ = m(x.double())
+        loss = torch.nn.functional.cross_entropy(logits, labels, weight=CLASS_W.double())
+        loss.backward()
+        _F64[case] = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    return _F64[case]
+
+
+def autocast_err(case):
+    """{tensor: rel. L2 error vs fp64} of torch's CPU bf16 autocast of the oracle step (cached)"""
+    if case not in _AC:
+        g64 = oracle64_step(case)
+        x, labels = _inputs(case)
+        m = DetectorCPU(dropout_rate=0.0)
+        deterministic_init_(m, seed=SEED)
+        m.train()
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            logits, _ = m(x)
+        torch.nn.functional.cross_entropy(logits.float(), labels, weight=CLASS_W).backward()
+        _AC[case] = {n: float((p.grad.double() - g64[n]).norm()) / (float(g64[n].norm()) + 1e-300)
+                     for n, p in m.named_parameters()}
+    return _AC[case]
+
+
+def _vs_fp64(case, dtype, loss, grads, tag=""):
+    """the 16-bit step's loss against the fp32 oracle (2 %) and every gradient against the fp64 oracle
+    within K_VS_AUTOCAST[dtype] x torch-bf16-autocast's error on that tensor"""
     ref = oracle_step(case)
     assert abs(loss - ref["loss"]) <= 2e-2 * abs(ref["loss"]), (loss, ref["loss"])
-    frac_ok, min_cos = (bound or BF16_BOUND)[case]
-    scale = max(float(g.double().norm()) for g in ref["grads"].values())
-    outside, low, counted = [], [], 0
-    for n, rg in ref["grads"].items():
-        r = rg.double().flatten()
+    g64, ac = oracle64_step(case), autocast_err(case)
+    k = K_VS_AUTOCAST[dtype]
+    scale = max(float(g.norm()) for g in g64.values())
+    rows, bad = [], []
+    for n, r in g64.items():
         rn = float(r.norm())
         # structurally ~zero (a BN shift feeding only a training-mode BN): rounding residue only
         if rn <= 1e-4 * scale:
             continue
-        counted += 1
-        g = grads[n].double().flatten()
-        cos = float(g @ r) / (float(g.norm()) * rn + 1e-30)
-        if abs(float(g.norm()) - rn) > 0.1 * rn or cos < 0.98:
-            outside.append((n, round(float(g.norm()) / rn, 4), round(cos, 5)))
-        if cos < min_cos:
-            low.append((n, round(cos, 5)))
-    print(f"{case}{tag}: {counted} gradients checked, {len(outside)} outside (10 %, cos 0.98): {outside}")
-    assert counted >= 0.85 * len(ref["grads"])
-    assert len(outside) <= (1 - frac_ok) * counted, (len(outside), counted)
-    assert not low, low
+        e = float((grads[n].double() - r).norm()) / rn
+        anchor = max(ac[n], AUTOCAST_FLOOR)
+        rows.append((e / anchor, n, e, ac[n]))
+        if e > k * anchor:
+            bad.append((n, round(e, 5), round(ac[n], 5)))
+    rows.sort(reverse=True)
+    print(f"{case}{tag} {dtype}: {len(rows)} gradients; worst err/autocast-err ratios (K = {k}): "
+          + "; ".join(f"{n} {q:.3f} ({e:.2e} vs {a:.2e})" for q, n, e, a in rows[:6]))
+    assert len(rows) >= 0.85 * len(g64)
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("case", list(CASES))
@@ -166,7 +193,7 @@ def test_train_step_224_bf16(cuda, case, kernel_paths):
     ref = oracle_step(case)
     logits, _, loss, grads, bufs = hip_step(case, "bf16", cuda)
     torch.testing.assert_close(logits, ref["logits"], rtol=5e-2, atol=5e-2)
-    _bf16_vs_oracle(case, loss, grads, f"/{kernel_paths}")
+    _vs_fp64(case, "bf16", loss, grads, f"/{kernel_paths}")
     for n, rb in ref["bufs"].items():
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
 
@@ -180,7 +207,7 @@ def test_train_step_224_fp16(cuda, case):
     logits, _, loss, grads, bufs = hip_step(case, "fp16", cuda, loss_scale=FP16_LOSS_SCALE)
     torch.testing.assert_close(logits, ref["logits"], rtol=5e-2, atol=5e-2)
     assert all(torch.isfinite(g).all() for g in grads.values())
-    _bf16_vs_oracle(case, loss, grads, "/fp16", bound=FP16_BOUND)
+    _vs_fp64(case, "fp16", loss, grads)
     for n, rb in ref["bufs"].items():
         torch.testing.assert_close(bufs[n], rb, rtol=2e-2, atol=2e-2, msg=lambda m: f"{n}: {m}")
 
@@ -251,8 +278,8 @@ def test_depthwise_schedule_knobs_close(cuda, knobs):
         backbone.DEFAULT_TUNING.update(prev)
     assert abs(loss_a - loss_b) <= 1e-2 * abs(loss_b)
     if knobs.get("dw_rb", 0) & 1:  # a forward knob: each run against the fp32 oracle
-        _bf16_vs_oracle("b4t8", loss_a, grads_a, f" {knobs}")
-        _bf16_vs_oracle("b4t8", loss_b, grads_b, " (knobs off)")
+        _vs_fp64("b4t8", "bf16", loss_a, grads_a, f" {knobs}")
+        _vs_fp64("b4t8", "bf16", loss_b, grads_b, " (knobs off)")
         return
     scale = max(float(g.double().norm()) for g in grads_b.values())
     bad = []

@@ -16,10 +16,11 @@ persistent grid.  Three checks:
    ``model(images)`` -> ``CrossEntropyLoss(weight)`` -> ``backward`` (``src/ensemble_trainer.py:188-198``).
    North-star tolerance: logits / frame scores / loss rtol 1e-3 atol 1e-5; every gradient norm
    within 1e-3 and its 64 leading elements within rtol 1e-3; BN running stats rtol 1e-4.
-2. **bf16 step** (the bench's dtype) and the **fp16 step** (loss-scaled) against the same fp32
-   oracle: loss within 2 %, and the
-   gradient bound of ``test_b0_224_gpu.py`` for the 32-frame batch (90 % of the tensors within 10 %
-   in norm and cosine >= 0.98, every tensor cosine >= 0.85).
+2. **bf16 step** and the **fp16 step** (loss-scaled; the bench's default dtype) against the same
+   fp32 oracle: loss within 2 %; at least 90 % (bf16) / 98 % (fp16) of the gradient tensors within
+   10 % in norm and cosine >= 0.98, every tensor cosine >= 0.85 (fp16: >= 0.99).  The per-tensor
+   fp64-anchored bound is checked at 2 and 32 frames (``test_b0_224_gpu.py``), where the fp64 oracle
+   runs on the CPU.
 3. **bf16, layer by layer** (what a fault confined to a few channels of one layer cannot escape):
    every conv of the forward is recomputed in fp32 torch from the HIP run's OWN bf16 inputs
    (saved in the workspace, ``dfd_b0_saved_tensor``) and compared PER CHANNEL; the backward runs
