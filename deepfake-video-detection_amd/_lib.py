@@ -52,6 +52,7 @@ _SIGS = {
     "dfd_b0_plan_status": (c_i, [c_p, ctypes.POINTER(c_i)]),
     "dfd_b0_plan_clear_status": (c_i, [c_p]),
     "dfd_test_occupy": (c_i, [c_p, c_i, c_i64]),
+    "dfd_test_group_sync": (c_i, [c_p, c_i, c_i, c_d, c_p, c_p]),
     "dfd_b0_probe_arm": (c_i, [c_p, c_i, c_i, c_i, c_i]),
     "dfd_b0_probe_read": (c_i, [c_p, ctypes.POINTER(c_f), c_i, ctypes.POINTER(c_i)]),
     "dfd_b0_probe_disarm": (c_i, [c_p]),

@@ -13,6 +13,7 @@
 #include "head.h"
 #include "plan.h"
 #include "rnn.h"
+#include "test_seams.h"
 #include "vit.h"
 
 namespace dfd {
@@ -246,6 +247,12 @@ int dfd_b0_plan_clear_status(dfd_b0_plan* plan) {
 int dfd_test_occupy(void* stream, int workgroups, int64_t microseconds) {
   DFD_GUARD_BEGIN
   return dfd::launch_occupy((hipStream_t)stream, workgroups, microseconds);
+  DFD_GUARD_END
+}
+
+int dfd_test_group_sync(void* stream, int workgroups, int expected, double seconds, int* scratch, int* host_word) {
+  DFD_GUARD_BEGIN
+  return dfd::launch_group_sync_test((hipStream_t)stream, workgroups, expected, seconds, scratch, host_word);
   DFD_GUARD_END
 }
 

@@ -13,6 +13,7 @@
 //   * per-channel statistics accumulate in registers across all tiles of a workgroup and are
 //     reduced once (wave shuffles + LDS) into one deterministic partial row.
 #pragma once
+#include <cstdio>
 #include "kernels.h"
 
 #include <cstdlib>
@@ -155,6 +156,15 @@ int resident_wgs() {
     int dev = 0, cus = 256, per_cu = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, KERN, NT, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+#ifdef DFD_OCC_PRINT  // experiment builds (tools/r06): what the occupancy API and the kernel attributes say
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KERN));
+    fprintf(stderr, "occupancy: %d per CU (regs %d, lds %zu, maxthreads %d)\n", per_cu, fa.numRegs,
+            fa.sharedSizeBytes, fa.maxThreadsPerBlock);
+#endif
+#ifdef DFD_OCC_MULT
+    per_cu *= DFD_OCC_MULT;
+#endif
     return std::max(1, cus * per_cu);
   }();
   return r;

@@ -33,3 +33,31 @@ int launch_occupy(hipStream_t s, int workgroups, int64_t microseconds) {
 }
 
 }  // namespace dfd
+
+#include "test_seams.h"
+
+namespace dfd {
+
+__global__ __launch_bounds__(256) void group_sync_test_kernel(int expected, unsigned long long budget, int* scratch,
+                                                              int* host_word) {
+  unsigned* ctr = reinterpret_cast<unsigned*>(scratch);
+  const bool ok = group_sync(ctr, ctr + 1, (unsigned)expected, SyncAbort{scratch + 2, host_word, budget});
+  if (threadIdx.x == 0) scratch[3 + blockIdx.x] = ok ? 1 : 2;
+}
+
+int launch_group_sync_test(hipStream_t s, int workgroups, int expected, double seconds, int* scratch, int* host_word) {
+  int dev = 0, cus = 0;
+  DFD_HIP_CHECK(hipGetDevice(&dev));
+  DFD_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  // a co-resident grid (the barrier's precondition) and a bounded wait
+  if (workgroups < 1 || workgroups > cus || expected < 1 || seconds <= 0.0 || seconds > 10.0 || !scratch) {
+    set_error("group_sync test: 1..CUs workgroups, 0 < seconds <= 10", __FILE__, __LINE__);
+    return -1;
+  }
+  hipLaunchKernelGGL(group_sync_test_kernel, dim3((unsigned)workgroups), dim3(256), 0, s, expected,
+                     sync_budget_ticks(seconds), scratch, host_word);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace dfd

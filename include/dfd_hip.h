@@ -124,6 +124,13 @@ DFD_API int dfd_b0_plan_clear_status(dfd_b0_plan* plan);
  * `microseconds` (wall clock, bounded) on `stream` -- occupies CUs so tests can run the plan next to
  * a kernel that denies it the device (tests/test_se_sync_gpu.py). */
 DFD_API int dfd_test_occupy(void* stream, int workgroups, int64_t microseconds);
+/* Test seam: `workgroups` (<= CUs) workgroups meet at the software group barrier the split SE excitation
+ * uses (csrc/tail.h group_sync), expecting `expected` arrivals within `seconds`: expected > workgroups
+ * can never complete, so every waiter must give up -- scratch (>= 3 + workgroups zeroed int32) receives
+ * per-workgroup results (1 passed, 2 gave up) at [3 + i], and the barrier raises *host_word (pinned,
+ * device-visible host memory), as it raises the plan status (tests/test_se_sync_gpu.py). */
+DFD_API int dfd_test_group_sync(void* stream, int workgroups, int expected, double seconds, int* scratch,
+                                int* host_word);
 /* Tensor index range [*lo, *hi) whose gradients are final after segment `seg`. */
 DFD_API int dfd_b0_segment_tensors(int seg, int* lo, int* hi);
 

@@ -112,3 +112,32 @@ def test_se_split_under_contention(cuda):
     got = _result(det, _step(det, x, y))
     det.backbone.runtime().check_status()
     assert _same(got, ref)
+
+
+@pytest.mark.parametrize("expected_extra", [0, 1])
+def test_group_sync_gives_up_loudly(cuda, expected_extra):
+    """The barrier itself (``dfd_test_group_sync``): a group that can complete (expected = the grid)
+    passes in every workgroup and raises nothing; one that never can (expected = grid + 1) makes every
+    workgroup give up within the budget -- the first to time out raises the device word the others
+    poll, and the host word the plans check -- instead of hanging or returning as if synchronised."""
+    lib = _lib.load()
+    wgs, seconds = 64, 0.5
+    scratch = torch.zeros(3 + wgs, dtype=torch.int32, device=cuda)
+    host = torch.zeros(1, dtype=torch.int32).pin_memory()
+    stream = torch.cuda.current_stream(cuda)
+    t0 = time.perf_counter()
+    _lib.check(lib.dfd_test_group_sync(ctypes.c_void_p(stream.cuda_stream), wgs, wgs + expected_extra,
+                                       ctypes.c_double(seconds), ctypes.c_void_p(scratch.data_ptr()),
+                                       ctypes.c_void_p(host.data_ptr())))
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    res = scratch[3:].cpu()
+    if expected_extra == 0:
+        assert torch.equal(res, torch.ones(wgs, dtype=torch.int32)), res
+        assert int(host[0]) == 0 and int(scratch[2]) == 0
+        assert int(scratch[0]) == 0 and int(scratch[1]) == 0  # counters back to zero at rest
+    else:
+        assert torch.equal(res, torch.full((wgs,), 2, dtype=torch.int32)), res
+        assert int(host[0]) == 1 and int(scratch[2]) == 1
+        assert seconds * 0.9 <= dt <= seconds * 3 + 1.0, dt
+    print(f"group_sync expected {wgs + expected_extra} of {wgs}: {dt:.3f} s, results {res.unique().tolist()}")

@@ -19,6 +19,10 @@
 
 using namespace dfd;
 
+#ifndef KB_T  // element type of the 16-bit kernels timed (bf16 default; -DKB_T=f16 for the fp16 builds)
+#define KB_T bf16
+#endif
+
 #define CK(x)                                                                  \
   do {                                                                         \
     hipError_t e_ = (x);                                                       \
@@ -99,7 +103,7 @@ int main(int argc, char** argv) {
   auto blocks = b0_blocks(H);
   // buffers sized for the largest tensor (stage-1 expanded map) and operands
   const int64_t big = (int64_t)F * 112 * 112 * 96;
-  bf16 *A, *B, *C, *D;
+  KB_T *A, *B, *C, *D;
   float *W, *stats, *slab, *dW, *sc, *sh, *gate, *coef, *mean, *invstd;
   CK(hipMalloc(&A, big * 2));
   CK(hipMalloc(&B, big * 2));
@@ -137,27 +141,27 @@ int main(int argc, char** argv) {
     if (!k.ds) {
       snprintf(nm, sizeof nm, "b%zu exp %ldx%dx%d", i, (long)Mi, k.mid, k.cin);
       b.run("pw_fwd", nm, 2.0 * (Mi * k.cin + Mi * k.mid), [&] {
-        return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mi, k.mid, k.cin, PRO_NONE, pn, stats, &rows);
+        return launch_pw_gemm<KB_T>(b.s, A, B, C, nullptr, Mi, k.mid, k.cin, PRO_NONE, pn, stats, &rows);
       });
       b.run("pw_dgrad", nm, 2.0 * (Mi * k.cin + Mi * k.mid), [&] {
-        return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mi, k.cin, k.mid, PRO_NONE, pn, nullptr, nullptr);
+        return launch_pw_gemm<KB_T>(b.s, A, B, C, nullptr, Mi, k.cin, k.mid, PRO_NONE, pn, nullptr, nullptr);
       });
       b.run("pw_wgrad", nm, 2.0 * (Mi * k.cin + Mi * k.mid), [&] {
-        return launch_pw_wgrad<bf16>(b.s, A, B, Mi, k.mid, k.cin, PRO_NONE, pn, slab, slab_cap, dW, false);
+        return launch_pw_wgrad<KB_T>(b.s, A, B, Mi, k.mid, k.cin, PRO_NONE, pn, slab, slab_cap, dW, false);
       });
     }
     DwGeom g{F, k.hin, k.hin, C1, k.k, k.s, k.k / 2, k.hout, k.hout};
     g.pad = ((k.s - 1) + (k.k - 1)) / 2;
     snprintf(nm, sizeof nm, "b%zu dw%d s%d %dx%d c%d", i, k.k, k.s, k.hin, k.hin, C1);
     const double dwb = 2.0 * (Mi * C1 + Mo * C1);
-    b.run("dw_fwd", nm, dwb, [&] { return launch_dw_fwd<bf16>(b.s, g, A, W, C, pb, PRO_BN_SILU, stats, &rows); });
+    b.run("dw_fwd", nm, dwb, [&] { return launch_dw_fwd<KB_T>(b.s, g, A, W, C, pb, PRO_BN_SILU, stats, &rows); });
     BnBwdIn bi{};
     bi.mean = mean; bi.invstd = invstd; bi.scale = sc; bi.shift = sh; bi.silu = true;
     b.run("dw_dgrad", nm, dwb + 2.0 * Mi * C1, [&] {
-      return launch_dw_dgrad<bf16>(b.s, g, A, W, C, B, &bi, stats, &rows);
+      return launch_dw_dgrad<KB_T>(b.s, g, A, W, C, B, &bi, stats, &rows);
     });
     b.run("dw_bwd", nm, dwb + 2.0 * Mi * C1, [&] {
-      return launch_dw_bwd<bf16>(b.s, g, A, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
+      return launch_dw_bwd<KB_T>(b.s, g, A, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
     });
     if (k.s == 1) {
       // the stride-1 backward with the BN2(+SiLU, gate) backward: fused kernel vs apply pass + dw_bwd
@@ -167,40 +171,40 @@ int main(int argc, char** argv) {
       const double b1 = 2.0 * 4 * Mi * C1;
       if (dw_bwd1_covers(g))
         b.run("dw_bwd1", nm, b1, [&] {
-          return launch_dw_bwd1<bf16>(b.s, g, D, A, gate, gate, sc, sh, coef, W, C, bi, B, stats, &rows, slab,
+          return launch_dw_bwd1<KB_T>(b.s, g, D, A, gate, gate, sc, sh, coef, W, C, bi, B, stats, &rows, slab,
                                       slab_cap, dW, false);
         });
       b.run("dw_bwdold", nm, b1, [&] {
-        int e = launch_bn_bwd_apply<bf16>(b.s, i2, A, coef, D, Mo, C1);
-        return e ? e : launch_dw_bwd<bf16>(b.s, g, D, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
+        int e = launch_bn_bwd_apply<KB_T>(b.s, i2, A, coef, D, Mo, C1);
+        return e ? e : launch_dw_bwd<KB_T>(b.s, g, D, W, C, B, &bi, stats, &rows, slab, slab_cap, dW, false);
       });
     }
     if (k.s == 2 && dw_bwd2_covers(g)) {
       BnBwdIn bi2{};
       bi2.mean = mean; bi2.invstd = invstd; bi2.scale = sc; bi2.shift = sh; bi2.silu = true;
       b.run("dw_bwd2", nm, 2.0 * (2 * Mi * C1 + 2 * Mo * C1), [&] {
-        return launch_dw_bwd2<bf16>(b.s, g, D, A, gate, gate, sc, sh, coef, W, C, bi2, B, stats, &rows, slab,
+        return launch_dw_bwd2<KB_T>(b.s, g, D, A, gate, gate, sc, sh, coef, W, C, bi2, B, stats, &rows, slab,
                                     slab_cap, dW, false);
       });
     }
     b.run("dw_wgrad", nm, dwb, [&] {
-      return launch_dw_wgrad<bf16>(b.s, g, A, B, pb, PRO_BN_SILU, slab, slab_cap, dW, false);
+      return launch_dw_wgrad<KB_T>(b.s, g, A, B, pb, PRO_BN_SILU, slab, slab_cap, dW, false);
     });
     snprintf(nm, sizeof nm, "b%zu proj %ldx%dx%d", i, (long)Mo, k.cout, C1);
     b.run("pwl_fwd", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
-      return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_BN_SILU_G, pg, stats, &rows);
+      return launch_pw_gemm<KB_T>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_BN_SILU_G, pg, stats, &rows);
     });
     b.run("pwlG_fwd", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {  // pre-activated input: gate-only prologue
-      return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_GATE, pg, stats, &rows);
+      return launch_pw_gemm<KB_T>(b.s, A, B, C, nullptr, Mo, k.cout, C1, PRO_GATE, pg, stats, &rows);
     });
     b.run("pwlG_wgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
-      return launch_pw_wgrad<bf16>(b.s, A, B, Mo, k.cout, C1, PRO_GATE, pg, slab, slab_cap, dW, false);
+      return launch_pw_wgrad<KB_T>(b.s, A, B, Mo, k.cout, C1, PRO_GATE, pg, slab, slab_cap, dW, false);
     });
     b.run("pwl_dgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
-      return launch_pw_gemm<bf16>(b.s, A, B, C, nullptr, Mo, C1, k.cout, PRO_NONE, pn, nullptr, nullptr);
+      return launch_pw_gemm<KB_T>(b.s, A, B, C, nullptr, Mo, C1, k.cout, PRO_NONE, pn, nullptr, nullptr);
     });
     b.run("pwl_wgrad", nm, 2.0 * (Mo * C1 + Mo * k.cout), [&] {
-      return launch_pw_wgrad<bf16>(b.s, A, B, Mo, k.cout, C1, PRO_BN_SILU_G, pg, slab, slab_cap, dW, false);
+      return launch_pw_wgrad<KB_T>(b.s, A, B, Mo, k.cout, C1, PRO_BN_SILU_G, pg, slab, slab_cap, dW, false);
     });
     if (!k.ds && k.hin == 7 && k.s == 1 && mbconv7_supported(F, 7, 7, k.cin, k.mid, k.cout, k.cin / 4, k.k, 1)) {
       // the fused 7x7 MBConv forward (k_mbconv7.hip), training and eval, then its per-phase timing
@@ -216,14 +220,14 @@ int main(int argc, char** argv) {
       Mb7Args a{};
       a.frames = F; a.cin = k.cin; a.mid = k.mid; a.cout = k.cout; a.rd = k.cin / 4; a.k = k.k;
       a.skip = k.cin == k.cout; a.momentum = 0.1f; a.eps = 1e-5f;
-      a.x = A; a.w1 = D; a.wdw = W; a.wr = W; a.br = W; a.we = W; a.be = W; a.w3 = D + (1 << 20);
+      a.x = (const bf16*)A; a.w1 = (const bf16*)D; a.wdw = W; a.wr = W; a.br = W; a.we = W; a.be = W; a.w3 = (const bf16*)(D + (1 << 20));  // (bf16-only kernel)
       for (int q = 0; q < 3; ++q) {
         float* o = bnv + q * 8 * 2048;
         a.bn[q] = Mb7Bn{o, o + 2048, o + 2 * 2048, o + 3 * 2048, o + 4 * 2048, o + 5 * 2048, o + 6 * 2048,
                         o + 7 * 2048};
       }
-      a.y1 = B; a.y2 = C; a.s2 = C + (int64_t)F * 49 * 1152; a.y3 = B + (int64_t)F * 49 * 1152;
-      a.xo = C + 2 * (int64_t)F * 49 * 1152;
+      a.y1 = (bf16*)B; a.y2 = (bf16*)C; a.s2 = (bf16*)(C + (int64_t)F * 49 * 1152); a.y3 = (bf16*)(B + (int64_t)F * 49 * 1152);
+      a.xo = (bf16*)(C + 2 * (int64_t)F * 49 * 1152);
       a.sq = gate; a.rpre = coef; a.gate = gate; a.part = stats;
       a.bar = bar; a.abort = reinterpret_cast<int*>(bar) + 63;
       const double mb = 2.0 * (Mo * k.cin + Mo * k.cout + 4.0 * Mo * k.mid);
@@ -274,23 +278,23 @@ int main(int argc, char** argv) {
       snprintf(nm, sizeof nm, "b%zu %dx%d c%d", i, k.hout, k.hout, C1);
       const bool mat = Mo < 20000;
       b.run("se_sq", nm, 2.0 * Mo * C1 * (mat ? 2 : 1), [&] {
-        return launch_se_squeeze<bf16>(b.s, A, pg, F, hwo, C1, stats, pcap, &hs, mat ? C : nullptr);
+        return launch_se_squeeze<KB_T>(b.s, A, pg, F, hwo, C1, stats, pcap, &hs, mat ? C : nullptr);
       });
       b.run("se_bn_bwd", nm, 2.0 * 2 * Mo * C1, [&] {
-        return launch_se_bn_bwd_reduce<bf16>(b.s, D, A, sc, sh, mean, invstd, F, hwo, C1, stats, pcap, &hs);
+        return launch_se_bn_bwd_reduce<KB_T>(b.s, D, A, sc, sh, mean, invstd, F, hwo, C1, stats, pcap, &hs);
       });
     }
     snprintf(nm, sizeof nm, "b%zu bn3 %ldx%d", i, (long)Mo, k.cout);
     b.run("bn_apply", nm, 2.0 * (k.s == 1 && k.cin == k.cout ? 3 : 2) * Mo * k.cout, [&] {
-      return launch_bn_apply<bf16>(b.s, B, sc, sh, k.s == 1 && k.cin == k.cout ? D : nullptr, C, Mo, k.cout);
+      return launch_bn_apply<KB_T>(b.s, B, sc, sh, k.s == 1 && k.cin == k.cout ? D : nullptr, C, Mo, k.cout);
     });
     BnBwdIn bo{};
     bo.dZ = A; bo.mean = mean; bo.invstd = invstd; bo.scale = sc; bo.shift = sh;
     b.run("bn_bwd_apply", nm, 2.0 * 3 * Mo * k.cout, [&] {
-      return launch_bn_bwd_apply<bf16>(b.s, bo, B, coef, C, Mo, k.cout);
+      return launch_bn_bwd_apply<KB_T>(b.s, bo, B, coef, C, Mo, k.cout);
     });
     b.run("bn_bwd_reduce", nm, 2.0 * 2 * Mo * k.cout, [&] {
-      return launch_bn_bwd_reduce<bf16>(b.s, bo, B, Mo, k.cout, stats, &rows);
+      return launch_bn_bwd_reduce<KB_T>(b.s, bo, B, Mo, k.cout, stats, &rows);
     });
   }
   if (b.filter == "fused") {
@@ -309,13 +313,13 @@ int main(int argc, char** argv) {
         int hs = 1;
         snprintf(nm, sizeof nm, "r%d %dx%d %d>%d", rows, q.hw, q.hw, q.K, q.N);
         b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + M * q.N), [&] {
-          const int rc = launch_pwl_bwd<bf16>(b.s, A, nullptr, nullptr, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw,
+          const int rc = launch_pwl_bwd<KB_T>(b.s, A, nullptr, nullptr, B, C, sc, sh, mean, invstd, gate, F, q.hw * q.hw,
                                         q.N, q.K, D, slab, slab_cap, dW, false, part, pcap, &hs);
           return rc == 1 ? -1 : rc;
         });
         snprintf(nm, sizeof nm, "bn3 %dx%d %d>%d", q.hw, q.hw, q.K, q.N);
         b.run("fused_pwl", nm, 2.0 * (2 * M * q.K + 2 * M * q.N), [&] {  // + the BN3 backward apply in staging
-          const int rc = launch_pwl_bwd<bf16>(b.s, A, A + (int64_t)M * 32, coef, B, C, sc, sh, mean, invstd, gate, F,
+          const int rc = launch_pwl_bwd<KB_T>(b.s, A, A + (int64_t)M * 32, coef, B, C, sc, sh, mean, invstd, gate, F,
                                         q.hw * q.hw, q.N, q.K, D, slab, slab_cap, dW, false, part, pcap, &hs);
           return rc == 1 ? -1 : rc;
         });
@@ -324,7 +328,7 @@ int main(int argc, char** argv) {
         const int64_t M = (int64_t)F * q.hw * q.hw;
         snprintf(nm, sizeof nm, "r%d %dx%d %d>%d%s", rows, q.hw, q.hw, q.cin, q.mid, q.skip ? " skip" : "");
         b.run("fused_fold", nm, 2.0 * (M * q.mid + (2 + q.skip) * M * q.cin), [&] {
-          const int rc = launch_pw_fold_bwd<bf16>(b.s, A, B, q.skip ? C : nullptr, D, D, sc, C + (int64_t)M * 64, M, q.mid,
+          const int rc = launch_pw_fold_bwd<KB_T>(b.s, A, B, q.skip ? C : nullptr, D, D, sc, C + (int64_t)M * 64, M, q.mid,
                                             q.cin, slab, slab_cap, dW, dW + (1 << 17), dW + (1 << 18));
           return rc == 1 ? -1 : rc;
         });
