@@ -1122,6 +1122,9 @@ int launch_gap(hipStream_t s, const T* Y, const Pro& pro, int frames, int HW, in
 //          B2(j,c) = Wr[j][c], out = bc = inv_hw * .   (the squeeze path's input gradient)
 // The channel slices (gridDim.y) recompute the small first product instead of a second launch.
 constexpr int SE_RDMAX = 48, SE_TS = SE_RDMAX + 4, SE_CSL = 256, SE_W = 16;  // SE_W waves per workgroup
+#ifndef DFD_SE_B2PF
+#define DFD_SE_B2PF 1
+#endif
 typedef float se_f32x4 __attribute__((ext_vector_type(4)));
 
 // A is read from the squeeze / SE-backward partials A[h][f][c] (h < hsplit, added in order):
@@ -1203,6 +1206,19 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
 #pragma unroll
         for (int q = 0; q < 4; ++q) fp[r][q] += ok ? fin.part[((int64_t)(q + 1) * fin.hsplit + h) * nfc + i] : 0.f;
       }
+  }
+  // the second product's B2 column of this wave's first (usually only) 16-channel block, loaded up front:
+  // independent of T, so its round trip overlaps the first product and the slice barrier instead of
+  // following them (DFD_SE_B2PF, A/B build switch)
+  float bw0[SE_RDMAX / 4];
+  if constexpr (DFD_SE_B2PF) {
+    const int n = cbeg + 16 * wave + li;
+#pragma unroll
+    for (int i = 0; i < SE_RDMAX / 4; ++i) {
+      const int k = 4 * i + lk;
+      const bool ok = n < cend && k < rd;
+      bw0[i] = ok ? (FWD ? W2[(int64_t)n * rd + k] : W2[(int64_t)k * C + n]) : 0.f;
+    }
   }
   // ---- T = A[16 frames][C] . B1[C][rd] ----
   se_f32x4 acc1[3];
@@ -1311,11 +1327,12 @@ __global__ __launch_bounds__(64 * SE_W) void se_chain_kernel(const float* __rest
     // all of B2's column for this lane first (<= 12 independent loads in flight), then the MFMA
     // chain in the same k order (one serialized load per MFMA step was the kernel's latency chain)
     float bw[SE_RDMAX / 4];
+    const bool pre = DFD_SE_B2PF && n0 == cbeg + 16 * wave;
 #pragma unroll
     for (int i = 0; i < SE_RDMAX / 4; ++i) {
       const int k = 4 * i + lk;
       const bool ok = nok && k < rd;
-      bw[i] = ok ? (FWD ? W2[(int64_t)n * rd + k] : W2[(int64_t)k * C + n]) : 0.f;
+      bw[i] = pre ? bw0[i] : ok ? (FWD ? W2[(int64_t)n * rd + k] : W2[(int64_t)k * C + n]) : 0.f;
     }
     se_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
