@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace dfd {
@@ -338,6 +340,24 @@ void plan_free(Plan& p) {
 namespace {
 
 
+// launch-site log for the PMC traffic attribution (tools/pmc_traffic_r06.py): with DFD_SITE_LOG=<path> every
+// launch of the attributed classes appends "<kernel class> <site>" in dispatch order, so per-launch counters
+// are matched to layers by the plan's own decisions (which BN takes the fused finalize + apply, ...)
+static FILE* site_log_file() {
+  static FILE* f = [] {
+    const char* path = getenv("DFD_SITE_LOG");
+    return path && *path ? fopen(path, "a") : nullptr;
+  }();
+  return f;
+}
+static void log_site(const char* cls, const char* what, const Block* b) {
+  FILE* f = site_log_file();
+  if (!f) return;
+  if (b) fprintf(f, "%s %s %d.%d\n", cls, what, b->stage, b->idx);
+  else fprintf(f, "%s %s\n", cls, what);
+  fflush(f);
+}
+
 inline bool probe_hit(const Plan& p, int kind, const Block* b) {
   return p.probe.kind == kind && p.probe.count < p.probe.n && b && b->stage == p.probe.stage &&
          b->idx == p.probe.idx;
@@ -546,30 +566,33 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
   // BN backward finalize + apply: one launch (bn_bwd_apply_fin, knob tail_fin bit 2) when the stat rows are
   // few enough for every apply workgroup to reduce its channels' rows itself, else the two launches
   const bool apply_fin = (tune(TK_TAIL_FIN) & 4) != 0;
-  auto fin_apply = [&](const BnBwdIn& in, const BNL& b, const T* Y, int64_t M, T* out, int nrows) {
+  auto fin_apply = [&](const BnBwdIn& in, const BNL& b, const T* Y, int64_t M, T* out, int nrows, const char* what,
+                       const Block* blk) {
     int rc = 0;
     if (apply_fin)
       rc = launch_bn_bwd_apply_fin<T>(s, in, Y, M, b.C, r.f(p.o_stats), nrows, M, r.prm(b.t_w), r.f(b.o_mean),
                                       r.f(b.o_invstd), tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef), out);
     if (rc < 0) return -1;
+    log_site(rc == 1 ? "bn_bwd_apply_fin" : "bn_bwd_apply", what, blk);
     if (rc == 1) return 0;
     DFD_TRY(launch_bn_bwd_finalize(s, r.f(p.o_stats), nrows, M, b.C, r.prm(b.t_w), r.f(b.o_mean), r.f(b.o_invstd),
                                    tr != 0, grad(b.t_w), grad(b.t_b), acc != 0, r.f(p.o_coef)));
     DFD_TRY(launch_bn_bwd_apply<T>(s, in, Y, r.f(p.o_coef), out, M, b.C));
     return 0;
   };
-  auto bwd_bn = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out) {
+  auto bwd_bn = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out, const char* what, const Block* blk) {
     in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
     // the fused finalize + apply reads <= 256 stat rows: the reduction takes that cap on the smaller
     // (late-stage) tensors, where its workgroups still cover the rows in a few passes
     const int cap = apply_fin && M <= 16384 ? 256 : 0;
     DFD_TRY(launch_bn_bwd_reduce<T>(s, in, Y, M, b.C, r.f(p.o_stats), &rows, cap));
-    return fin_apply(in, b, Y, M, out, rows);
+    return fin_apply(in, b, Y, M, out, rows, what, blk);
   };
   // BN backward when the partials of g, g*xhat are already in o_stats (written by a fused producer)
-  auto bwd_bn_from_stats = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out, int nrows) {
+  auto bwd_bn_from_stats = [&](BnBwdIn in, const BNL& b, const T* Y, int64_t M, T* out, int nrows, const char* what,
+                               const Block* blk) {
     in.mean = r.f(b.o_mean); in.invstd = r.f(b.o_invstd); in.scale = r.f(b.o_scale); in.shift = r.f(b.o_shift);
-    return fin_apply(in, b, Y, M, out, nrows);
+    return fin_apply(in, b, Y, M, out, nrows, what, blk);
   };
   const int nb = (int)p.blocks.size();
   // the gradient buffer's extent: slab reductions into it are deferred (one launch per segment)
@@ -645,7 +668,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
       const Block& last = p.blocks[nb - 1];
       BnBwdIn in{};
       in.bc = dfeat; in.bc_scale = 1.0f / (float)(p.Hf * p.Wf); in.rows_per_frame = p.Hf * p.Wf; in.silu = true;
-      DFD_TRY(bwd_bn(in, p.bn_head, r.a(p.o_yh), Mf, r.a(p.o_gs)));
+      DFD_TRY(bwd_bn(in, p.bn_head, r.a(p.o_yh), Mf, r.a(p.o_gs), "bn_head", nullptr));
       DFD_TRY(launch_pw_gemm<T>(s, r.a(p.o_gs), r.a(p.head.o_wt), r.a(p.o_gx[(nb - 1) & 1]), nullptr, Mf, p.head.cin,
                                 kHead, PRO_NONE, Pro{}, nullptr, nullptr));
       DFD_TRY(launch_pw_wgrad<T>(s, r.a(p.o_gs), r.a(last.o_x), Mf, kHead, p.head.cin, PRO_NONE, Pro{},
@@ -693,9 +716,10 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
             // or launched without the weight gradient (2): materialise gs with the apply pass for the
             // unfused launches below
             DFD_TRY(launch_bn_bwd_apply<T>(s, i3, r.a(b.o_y3), r.f(p.o_coef), r.a(p.o_gs), Mout, b.cout));
+            log_site("bn_bwd_apply", "bn3", &b);
           }
         } else {
-          DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs)));
+          DFD_TRY(bwd_bn(i3, b.bn3, r.a(b.o_y3), Mout, r.a(p.o_gs), "bn3", &b));
           if (fpwl) {
             if constexpr (is16<T>) {
               PROBED(PK_PWL_DGRAD, &b, ((pf = launch_pwl_bwd<T>(s, r.a(p.o_gs), nullptr, nullptr, r.a(b.pwl.o_wt),
@@ -767,12 +791,14 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
                                                      r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(p.o_coef),
                                                      r.prm(b.t_dw), y_in, fz, r.a(p.o_ge1), r.f(p.o_stats), &rows,
                                                      slab(), p.slab_cap, grad(b.t_dw), acc != 0)));
+          log_site("dw_bwd2", "dw", &b);
           fused = 0;
         } else if (dw_bwd1_covers(g)) {
           PROBED(PK_DW_DGRAD, &b, (launch_dw_bwd1<T>(s, g, r.a(p.o_ge2), r.a(b.o_y2), r.f(b.o_gate), r.f(p.o_bc),
                                                      r.f(bn_dw.o_scale), r.f(bn_dw.o_shift), r.f(p.o_coef),
                                                      r.prm(b.t_dw), y_in, fz, r.a(p.o_ge1), r.f(p.o_stats), &rows,
                                                      slab(), p.slab_cap, grad(b.t_dw), acc != 0)));
+          log_site("dw_bwd1", "dw", &b);
           fused = 0;
         } else {
           BnBwdIn i2{};
@@ -781,6 +807,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
           i2.mean = r.f(bn_dw.o_mean); i2.invstd = r.f(bn_dw.o_invstd);
           i2.scale = r.f(bn_dw.o_scale); i2.shift = r.f(bn_dw.o_shift);
           DFD_TRY(launch_bn_bwd_apply<T>(s, i2, r.a(b.o_y2), r.f(p.o_coef), r.a(p.o_ge2), Mout, b.mid));
+          log_site("bn_bwd_apply", "bn2", &b);
           PROBED(PK_DW_DGRAD, &b, ((fused = launch_dw_bwd<T>(s, g, r.a(p.o_ge2), r.prm(b.t_dw), r.a(p.o_ge1), y_in,
                                                              &fz, r.f(p.o_stats), &rows, slab(), p.slab_cap,
                                                              grad(b.t_dw), acc != 0)) < 0 ? -1 : 0));
@@ -797,7 +824,7 @@ int backward_impl(Plan& p, hipStream_t s, const void* x, const int64_t* xs, cons
         if (!b.ds && Min < tune(TK_FOLD_MIN_ROWS)) {
           BnBwdIn i1{};
           i1.dZ = r.a(p.o_ge1); i1.rows_per_frame = b.hin * b.win; i1.silu = false;
-          DFD_TRY(bwd_bn_from_stats(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1), p.pending_rows));
+          DFD_TRY(bwd_bn_from_stats(i1, b.bn1, r.a(b.o_y1), Min, r.a(p.o_ge1), p.pending_rows, "bn1", &b));
           const T* xin = r.a(p.blocks[i - 1].o_x);
           PROBED(PK_PW_DGRAD, &b, (launch_pw_gemm<T>(s, r.a(p.o_ge1), r.a(b.pw.o_wt), r.a(p.o_gx[(i - 1) & 1]),
                                                      b.skip ? gout : nullptr, Min, b.cin, b.mid, PRO_NONE, Pro{},
