@@ -23,11 +23,12 @@ def main():
     ap.add_argument("values", nargs="+", type=int)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     model = PretrainedBackboneDetector("efficientnet_b0", pretrained=False, num_classes=2, dropout_rate=0.5,
-                                       compute_dtype="bf16")
+                                       compute_dtype=a.dtype)
     deterministic_init_(model, seed=0)
     model = model.to(dev).train()
     step = DataParallelTrainer(model, lr=1e-4, weight_decay=1e-5, max_grad_norm=1.0,
