@@ -246,8 +246,9 @@ def bench_ensemble(args, dev):
                                 "ms_per_step": round(res["b0_mbconv7"] * 1e3, 3)}}
 
 
-def bench_ensemble_train(args, dev):
-    """SURVEY §8(f)4 training: the default ensemble's train step (both members, fp32)."""
+def bench_ensemble_train(args, dev, dtype="fp32"):
+    """SURVEY §8(f)4 training: the default ensemble's train step (both members, fp32 -- the reference's
+    precision -- or bf16: the B0 plan and the ResNet-50 bottlenecks on bf16 MFMA, k_rn16.hip)."""
     from deepfake_amd.pretrained_detector import EnsembleDetector
     from deepfake_amd.trainer import TrainStep
 
@@ -256,7 +257,7 @@ def bench_ensemble_train(args, dev):
     g.manual_seed(0)
     x = torch.rand(B, T, 3, S, S, generator=g, device=dev)
     y = torch.randint(0, 2, (B,), generator=g, device=dev)
-    ens = EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False, compute_dtype="fp32").to(dev).train()
+    ens = EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False, compute_dtype=dtype).to(dev).train()
     ts = TrainStep(ens, lr=1e-4, weight_decay=1e-5, class_weights=torch.tensor([0.7, 1.3]), max_grad_norm=1.0)
 
     def step():
@@ -265,7 +266,7 @@ def bench_ensemble_train(args, dev):
     dt = _time(step, args.steps, args.warmup)
     return {"metric": "frames/sec training EnsembleDetector(efficientnet_b0 + resnet50)", "value": round(B * T / dt, 2),
             "unit": "frames/s", "n_gpus": 1, "ms_per_step": round(dt * 1e3, 3), "higher_is_better": True,
-            "dtype": "f32", "data": "synthetic U(0,1) frames (seeded, on device), random-init weights",
+            "dtype": "f32" if dtype == "fp32" else dtype, "data": "synthetic U(0,1) frames (seeded, on device), random-init weights",
             "config": {"workload": "EnsembleDetector train step (both members; weighted CE, clip 1.0 + AdamW)",
                        "clips": B, "frames_per_clip": T, "image": [S, S, 3]}}
 
@@ -296,6 +297,7 @@ def main():
     if args.model in ("ensemble_train", "all"):
         args.clips = min(args.clips, 8)
         print(json.dumps(bench_ensemble_train(args, dev)), flush=True)
+        print(json.dumps(bench_ensemble_train(args, dev, "bf16")), flush=True)
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@
 #include "cnnlstm.h"
 #include "head.h"
 #include "plan.h"
+#include "rn16.h"
 #include "rnn.h"
 #include "test_seams.h"
 #include "vit.h"
@@ -623,6 +624,101 @@ int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, int N, i
   if ((int64_t)Cout * Cin * kh * kw > slab_floats) { dfd::set_error("rn wgrad: slab too small", __FILE__, __LINE__); return -1; }
   const int64_t xs[4] = {xs4[0], xs4[1], xs4[2], xs4[3]};
   return dfd::conv_wgrad((hipStream_t)stream, g, x, xs, dy, slab, slab_floats, dw);
+  DFD_GUARD_END
+}
+
+// ---- ResNet-50 training (bf16, k_rn16.hip)
+int dfd_rn16_pack_weights(void* stream, const float* w, int Cout, int Cin, int k, void* wf, void* wd) {
+  DFD_GUARD_BEGIN
+  if (!w || !wf) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_pack_weights((hipStream_t)stream, w, Cout, Cin, k * k, (dfd::bf16*)wf, (dfd::bf16*)wd);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_conv_fwd(void* stream, const void* x, int N, int H, int W, int Cin, const void* wf, int Cout, int k,
+                      int stride, int pad, void* y, float* stats, int* stat_rows) {
+  DFD_GUARD_BEGIN
+  if (!x || !wf || !y || !stats || !stat_rows) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_conv_fwd((hipStream_t)stream, (const dfd::bf16*)x, N, H, W, Cin, (const dfd::bf16*)wf, Cout, k, stride,
+                            pad, (dfd::bf16*)y, stats, stat_rows);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_conv_dgrad(void* stream, const void* dy, int N, int H, int W, int Cin, const void* wd, int Cout, int k,
+                        int stride, int pad, const void* res, void* dx) {
+  DFD_GUARD_BEGIN
+  if (!dy || !wd || !dx) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_conv_dgrad((hipStream_t)stream, (const dfd::bf16*)dy, N, H, W, Cin, (const dfd::bf16*)wd, Cout, k,
+                              stride, pad, (const dfd::bf16*)res, (dfd::bf16*)dx);
+  DFD_GUARD_END
+}
+
+int64_t dfd_rn16_conv_wgrad_slab_floats(int N, int H, int W, int Cin, int Cout, int k, int stride, int pad) {
+  return dfd::rn16_conv_wgrad_slab_floats(N, H, W, Cin, Cout, k, stride, pad);
+}
+
+int dfd_rn16_conv_wgrad(void* stream, const void* x, int N, int H, int W, int Cin, const void* dy, int Cout, int k,
+                        int stride, int pad, float* slab, int64_t slab_floats, float* dw) {
+  DFD_GUARD_BEGIN
+  if (!x || !dy || !slab || !dw) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_conv_wgrad((hipStream_t)stream, (const dfd::bf16*)x, N, H, W, Cin, (const dfd::bf16*)dy, Cout, k,
+                              stride, pad, slab, slab_floats, dw);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_bn_act(void* stream, const void* y, const float* mean, const float* scale, const float* beta,
+                    const void* res, int relu, int64_t M, int C, void* out) {
+  DFD_GUARD_BEGIN
+  if (!y || !mean || !scale || !beta || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_bn_act((hipStream_t)stream, (const dfd::bf16*)y, mean, scale, beta, (const dfd::bf16*)res, relu, M,
+                          C, (dfd::bf16*)out);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_relu_bwd(void* stream, const void* dout, const void* out, int64_t n, void* g) {
+  DFD_GUARD_BEGIN
+  if (!dout || !out || !g) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_relu_bwd((hipStream_t)stream, (const dfd::bf16*)dout, (const dfd::bf16*)out, n, (dfd::bf16*)g);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_gap_bwd(void* stream, const float* dfeat, const void* out, int N, int HW, int C, void* g) {
+  DFD_GUARD_BEGIN
+  if (!dfeat || !out || !g) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_gap_bwd((hipStream_t)stream, dfeat, (const dfd::bf16*)out, N, HW, C, (dfd::bf16*)g);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_cast(void* stream, const void* src, int to_bf16, int64_t n, void* dst) {
+  DFD_GUARD_BEGIN
+  if (!src || !dst) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_cast((hipStream_t)stream, src, to_bf16, n, dst);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_bn_finalize(void* stream, const float* stats, int rows, int64_t count, int C, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                         float* mean, float* invstd, float* scale, float* shift) {
+  DFD_GUARD_BEGIN
+  if (!stats || !gamma || !beta || !running_mean || !running_var || !mean || !invstd || !scale || !shift) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::launch_bn_finalize((hipStream_t)stream, stats, rows, count, C, gamma, beta, running_mean, running_var,
+                                 momentum, eps, true, mean, invstd, scale, shift);
+  DFD_GUARD_END
+}
+
+int dfd_rn16_bn_train_bwd(void* stream, const void* g, const void* y, int64_t M, int C, const float* mean,
+                          const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
+                          float* dbeta, float* stats, float* coef, void* dy) {
+  DFD_GUARD_BEGIN
+  if (!g || !y || !mean || !invstd || !scale || !shift || !gamma || !dgamma || !dbeta || !stats || !coef || !dy) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::rn16_bn_train_bwd((hipStream_t)stream, (const dfd::bf16*)g, (const dfd::bf16*)y, M, C, mean, invstd,
+                                scale, shift, gamma, dgamma, dbeta, stats, coef, (dfd::bf16*)dy);
   DFD_GUARD_END
 }
 

@@ -24,8 +24,12 @@ unbiased variance, ``num_batches_tracked`` counts -- as one autograd node over t
 (``_RnTrainFn``): every convolution's forward, data gradient (stride 1 and 2) and weight gradient
 are exact-fp32 implicit-GEMM MFMA kernels (``csrc/k_conv.hip``), the BatchNorm backward is the B0
 path's reduce / finalize / apply (``csrc/k_bn.hip``), the ReLU / residual / pooling pieces are
-``csrc/k_rntrain.hip`` and ``k_conv.hip`` kernels.  bf16 training of this member is refused
-(``compute_dtype='fp32'`` for training; bf16 remains the serving dtype).
+``csrc/k_rntrain.hip`` and ``k_conv.hip`` kernels.  With ``compute_dtype='bf16'`` the member trains in
+bf16 (round 6): conv1 + bn1 + relu + maxpool stay on those fp32 kernels, every bottleneck convolution
+(forward with the BN-stat partials, data gradient at stride 1 and 2, weight gradient) runs on bf16 MFMA
+over bf16 NHWC activations (``csrc/k_rn16.hip``: the EfficientNet-B0 1x1 GEMM tile loops reading an
+implicit-GEMM gather), fp32 master weights packed to bf16 once per step, BatchNorm statistics and
+coefficients in fp32 / fp64, the same train-mode semantics.
 """
 from __future__ import annotations
 
@@ -154,9 +158,6 @@ class ResNet50Trunk(nn.Sequential):
             raise ValueError(f"expected (N, 3, H, W) frames, got {tuple(x.shape)}")
         grads = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         if self.training:
-            if self.compute_dtype != "fp32":
-                raise NotImplementedError("training the ResNet-50 member runs in fp32: build it with "
-                                          "compute_dtype='fp32' (bf16 is its serving dtype)")
             if x.dtype == torch.uint8:  # the serving feed's uint8 crops: normalise like the conv1 gather
                 from .backbone import NORMALIZATIONS
 
@@ -200,7 +201,7 @@ class ResNet50Trunk(nn.Sequential):
 class _Unit:
     """One conv + train-mode BN of the trunk: the forward's saved tensors for the backward."""
 
-    __slots__ = ("conv", "bn", "x", "hw", "y", "ohw", "mean", "invstd", "scale", "shift")
+    __slots__ = ("conv", "bn", "x", "hw", "y", "ohw", "mean", "invstd", "scale", "shift", "wd")
 
 
 def _nhwc_strides(t, hw, c):
@@ -244,6 +245,47 @@ def _bn_act(lib, st, y, vecs, bn, res, relu):
     return out
 
 
+def _bn_momentum(bn):
+    with torch.no_grad():
+        bn.num_batches_tracked.add_(1)
+    # torch's momentum=None: the cumulative moving average, factor 1 / num_batches_tracked
+    return float(bn.momentum) if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
+
+
+def _conv_bn_fwd16(lib, st, u, x, n, hw, save):
+    """bf16: y = conv(x) on the packed bf16 weights, the BN batch statistics (running buffers updated)."""
+    conv, bn = u.conv, u.bn
+    k, s, p, cin, cout = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.in_channels, conv.out_channels
+    ho, wo = (hw[0] + 2 * p - k) // s + 1, (hw[1] + 2 * p - k) // s + 1
+    dev = x.device
+    w = conv.weight.detach().float().contiguous()
+    wf = torch.empty(w.numel(), dtype=torch.bfloat16, device=dev)
+    wd = torch.empty(w.numel(), dtype=torch.bfloat16, device=dev) if save else None
+    _lib.check(lib.dfd_rn16_pack_weights(st, w.data_ptr(), cout, cin, k, wf.data_ptr(), _lib.ptr(wd)))
+    y = torch.empty(n * ho * wo, cout, dtype=torch.bfloat16, device=dev)
+    stats = torch.empty(2048 * cout, dtype=torch.float32, device=dev)
+    rows = ctypes.c_int(0)
+    _lib.check(lib.dfd_rn16_conv_fwd(st, x.data_ptr(), n, hw[0], hw[1], cin, wf.data_ptr(), cout, k, s, p, y.data_ptr(),
+                                     stats.data_ptr(), ctypes.byref(rows)))
+    vecs = torch.empty(4, cout, dtype=torch.float32, device=dev)
+    mom = _bn_momentum(bn)
+    _lib.check(lib.dfd_rn16_bn_finalize(st, stats.data_ptr(), rows.value, n * ho * wo, cout, bn.weight.data_ptr(),
+                                        bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(), mom,
+                                        float(bn.eps), vecs[0].data_ptr(), vecs[1].data_ptr(), vecs[2].data_ptr(),
+                                        vecs[3].data_ptr()))
+    if save:
+        u.x, u.hw, u.y, u.ohw, u.wd = x, hw, y, (ho, wo), wd
+        u.mean, u.invstd, u.scale, u.shift = vecs[0], vecs[1], vecs[2], vecs[3]
+    return y, (ho, wo), vecs
+
+
+def _bn_act16(lib, st, y, vecs, bn, res, relu):
+    out = torch.empty_like(y)
+    _lib.check(lib.dfd_rn16_bn_act(st, y.data_ptr(), vecs[0].data_ptr(), vecs[2].data_ptr(), bn.bias.data_ptr(),
+                                   _lib.ptr(res), 1 if relu else 0, y.shape[0], y.shape[1], out.data_ptr()))
+    return out
+
+
 def _train_forward(trunk, x, save):
     """Train-mode forward of the trunk -> (features (N, 2048), saved state for the backward)."""
     lib = _lib.load()
@@ -251,6 +293,7 @@ def _train_forward(trunk, x, save):
     st = _lib.stream_of(dev)
     n, _, H, W = x.shape
     units, blocks = [], []
+    b16 = trunk.compute_dtype == "bf16"
 
     def unit(conv, bn):
         u = _Unit()
@@ -269,7 +312,31 @@ def _train_forward(trunk, x, save):
                                          trunk[1].bias.data_ptr(), n, hw0[0], hw0[1], 64,
                                          h.data_ptr(), arg.data_ptr()))
     hw = (hp, wp)
-    for li in range(4):
+    if b16:  # the bottlenecks in bf16 (k_rn16.hip); the stem above stays fp32
+        h16 = torch.empty(h.shape, dtype=torch.bfloat16, device=dev)
+        _lib.check(lib.dfd_rn16_cast(st, h.data_ptr(), 1, h.numel(), h16.data_ptr()))
+        h = h16
+        for li in range(4):
+            for blk in trunk[4 + li]:
+                b = {"in": h, "hw": hw}
+                u1, u2, u3 = unit(blk.conv1, blk.bn1), unit(blk.conv2, blk.bn2), unit(blk.conv3, blk.bn3)
+                y1, hw1, v1 = _conv_bn_fwd16(lib, st, u1, h, n, hw, save)
+                a1 = _bn_act16(lib, st, y1, v1, blk.bn1, None, True)
+                y2, hw2, v2 = _conv_bn_fwd16(lib, st, u2, a1, n, hw1, save)
+                a2 = _bn_act16(lib, st, y2, v2, blk.bn2, None, True)
+                y3, _, v3 = _conv_bn_fwd16(lib, st, u3, a2, n, hw2, save)
+                if blk.downsample is not None:
+                    ud = unit(blk.downsample[0], blk.downsample[1])
+                    yd, _, vd = _conv_bn_fwd16(lib, st, ud, h, n, hw, save)
+                    idn = _bn_act16(lib, st, yd, vd, blk.downsample[1], None, False)
+                    b["ds"] = ud
+                else:
+                    idn = h
+                h = _bn_act16(lib, st, y3, v3, blk.bn3, idn, True)
+                hw = hw2
+                b.update(u=(u1, u2, u3), a1=a1, a2=a2, out=h)
+                blocks.append(b)
+    for li in range(0 if not b16 else 4, 4):
         for blk in trunk[4 + li]:
             b = {"in": h, "hw": hw}
             u1, u2, u3 = unit(blk.conv1, blk.bn1), unit(blk.conv2, blk.bn2), unit(blk.conv3, blk.bn3)
@@ -290,7 +357,7 @@ def _train_forward(trunk, x, save):
             b.update(u=(u1, u2, u3), a1=a1, a2=a2, out=h)
             blocks.append(b)
     feats = torch.empty(n, FEATURE_DIM, dtype=torch.float32, device=dev)
-    _lib.check(lib.dfd_rn_avgpool(st, 0, h.data_ptr(), n, hw[0] * hw[1], FEATURE_DIM, feats.data_ptr()))
+    _lib.check(lib.dfd_rn_avgpool(st, 1 if b16 else 0, h.data_ptr(), n, hw[0] * hw[1], FEATURE_DIM, feats.data_ptr()))
     saved = dict(units=units, blocks=blocks, stem_arg=arg, stem_pool_hw=(hp, wp), final_hw=hw, n=n) if save else None
     return feats, saved
 
@@ -339,6 +406,45 @@ def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
     return dx
 
 
+def _bn_bwd16(lib, st, u, g, grads):
+    C = u.y.shape[1]
+    dev = g.device
+    stats = torch.empty(2048 * 2 * C, dtype=torch.float32, device=dev)
+    coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
+    dg, db = torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev)
+    dy = torch.empty_like(u.y)
+    _lib.check(lib.dfd_rn16_bn_train_bwd(st, g.data_ptr(), u.y.data_ptr(), u.y.shape[0], C, u.mean.data_ptr(),
+                                         u.invstd.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
+                                         u.bn.weight.data_ptr(), dg.data_ptr(), db.data_ptr(), stats.data_ptr(),
+                                         coef.data_ptr(), dy.data_ptr()))
+    grads[id(u.bn.weight)] = dg
+    grads[id(u.bn.bias)] = db
+    return dy
+
+
+def _conv_bwd16(lib, st, u, dy, n, grads, res=None):
+    """bf16 data gradient (+ res: the other path's input gradient) and fp32 weight gradient of unit u."""
+    conv = u.conv
+    k, s, p, cin, cout = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.in_channels, conv.out_channels
+    dev = dy.device
+    dx = torch.empty(n * u.hw[0] * u.hw[1], cin, dtype=torch.bfloat16, device=dev)
+    _lib.check(lib.dfd_rn16_conv_dgrad(st, dy.data_ptr(), n, u.hw[0], u.hw[1], cin, u.wd.data_ptr(), cout, k, s, p,
+                                       _lib.ptr(res), dx.data_ptr()))
+    slab = torch.empty(lib.dfd_rn16_conv_wgrad_slab_floats(n, u.hw[0], u.hw[1], cin, cout, k, s, p),
+                       dtype=torch.float32, device=dev)
+    dw = torch.empty_like(conv.weight, dtype=torch.float32)
+    _lib.check(lib.dfd_rn16_conv_wgrad(st, u.x.data_ptr(), n, u.hw[0], u.hw[1], cin, dy.data_ptr(), cout, k, s, p,
+                                       slab.data_ptr(), slab.numel(), dw.data_ptr()))
+    grads[id(conv.weight)] = dw
+    return dx
+
+
+def _relu_bwd16(lib, st, d, out):
+    g = torch.empty_like(d)
+    _lib.check(lib.dfd_rn16_relu_bwd(st, d.data_ptr(), out.data_ptr(), d.numel(), g.data_ptr()))
+    return g
+
+
 def _train_backward(trunk, saved, dfeat):
     lib = _lib.load()
     dev = dfeat.device
@@ -347,6 +453,29 @@ def _train_backward(trunk, saved, dfeat):
     grads = {}
     blocks = saved["blocks"]
     hw = saved["final_hw"]
+    if trunk.compute_dtype == "bf16":
+        last = blocks[-1]["out"]
+        g = torch.empty_like(last)
+        _lib.check(lib.dfd_rn16_gap_bwd(st, dfeat.contiguous().data_ptr(), last.data_ptr(), n, hw[0] * hw[1],
+                                        FEATURE_DIM, g.data_ptr()))
+        for bi, b in enumerate(reversed(blocks)):
+            u1, u2, u3 = b["u"]
+            if bi > 0:  # the block's output ReLU (the last block's went with the pool)
+                g = _relu_bwd16(lib, st, g, b["out"])
+            dy3 = _bn_bwd16(lib, st, u3, g, grads)
+            if "ds" in b:
+                dyd = _bn_bwd16(lib, st, b["ds"], g, grads)
+                other = _conv_bwd16(lib, st, b["ds"], dyd, n, grads)
+            else:
+                other = g
+            g2 = _relu_bwd16(lib, st, _conv_bwd16(lib, st, u3, dy3, n, grads), b["a2"])
+            dy2 = _bn_bwd16(lib, st, u2, g2, grads)
+            g1 = _relu_bwd16(lib, st, _conv_bwd16(lib, st, u2, dy2, n, grads), b["a1"])
+            dy1 = _bn_bwd16(lib, st, u1, g1, grads)
+            g = _conv_bwd16(lib, st, u1, dy1, n, grads, res=other)
+        g32 = torch.empty(g.shape, dtype=torch.float32, device=dev)
+        _lib.check(lib.dfd_rn16_cast(st, g.data_ptr(), 0, g.numel(), g32.data_ptr()))
+        return _stem_backward(lib, st, saved, g32, n, grads)
     # AdaptiveAvgPool2d + the last block's ReLU
     last = blocks[-1]["out"]
     g = torch.empty_like(last)
@@ -376,7 +505,11 @@ def _train_backward(trunk, saved, dfeat):
         dy1 = _bn_bwd(lib, st, u1, g1, grads)
         dx.add_(_conv_bwd(lib, st, u1, dy1, n, grads))
         g = dx
-    # maxpool + stem relu/bn + conv1 weight gradient (no gradient to the frames)
+    return _stem_backward(lib, st, saved, g, n, grads)
+
+
+def _stem_backward(lib, st, saved, g, n, grads):
+    """maxpool + stem relu/bn + conv1 weight gradient (fp32; no gradient to the frames)"""
     us = saved["units"][0]
     gs = torch.empty_like(us.y)
     _lib.check(lib.dfd_rn_pool_train_bwd(st, g.data_ptr(), saved["stem_arg"].data_ptr(), us.y.data_ptr(),

@@ -263,6 +263,42 @@ DFD_API int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, 
                               const float* dy, int Cout, int kh, int kw, int stride, int pad, float* slab,
                               int64_t slab_floats, float* dw);
 
+/* ---- ResNet-50 ensemble member: bf16 TRAINING (k_rn16.hip) -----------------------------------
+ * Replaces the same train-mode trunk as dfd_rn_train_* (torchvision resnet50 children()[:-1] under
+ * EnsembleTrainer.train_epoch, src/ensemble_trainer.py:158-229, src/pretrained_detector.py:37-40) for
+ * every bottleneck convolution (1x1 / 3x3, stride 1 / 2, pad (k-1)/2, Cin % 64, Cout % 64): bf16 NHWC
+ * activations, v_mfma_f32_16x16x32_bf16 with fp32 accumulation, fp32 master weights packed per step,
+ * BN statistics in fp32 partials merged in fp64.  conv1 + bn1 + relu + maxpool stay on dfd_rn_train_*.
+ * w OIHW fp32 -> wf [Cout][k][k][Cin] bf16 (forward), wd [Cin][k][k][Cout] bf16 (data gradient, or null) */
+DFD_API int dfd_rn16_pack_weights(void* stream, const float* w, int Cout, int Cin, int k, void* wf, void* wd);
+/* y = conv(x) NHWC bf16 (no bias); BN partial rows (sum, sum of squares) into stats (>= 2048*Cout floats),
+ * *stat_rows rows, for dfd_rn16_bn_finalize */
+DFD_API int dfd_rn16_conv_fwd(void* stream, const void* x, int N, int H, int W, int Cin, const void* wf, int Cout,
+                              int k, int stride, int pad, void* y, float* stats, int* stat_rows);
+/* train-mode BN of dfd_rn16_conv_fwd's output: batch mean / invstd, scale = gamma*invstd, shift, the running
+ * buffers updated like torch (unbiased variance, momentum) */
+DFD_API int dfd_rn16_bn_finalize(void* stream, const float* stats, int rows, int64_t count, int C, const float* gamma,
+                                 const float* beta, float* running_mean, float* running_var, float momentum,
+                                 float eps, float* mean, float* invstd, float* scale, float* shift);
+/* out = relu?((y - mean) * scale + beta (+ res)), bf16 in / out */
+DFD_API int dfd_rn16_bn_act(void* stream, const void* y, const float* mean, const float* scale, const float* beta,
+                            const void* res, int relu, int64_t M, int C, void* out);
+DFD_API int dfd_rn16_relu_bwd(void* stream, const void* dout, const void* out, int64_t n, void* g);
+DFD_API int dfd_rn16_gap_bwd(void* stream, const float* dfeat, const void* out, int N, int HW, int C, void* g);
+/* train-mode BN backward (centred), bf16 g / y / dy; dgamma, dbeta written; stats >= 2048*2*C, coef >= 3*C */
+DFD_API int dfd_rn16_bn_train_bwd(void* stream, const void* g, const void* y, int64_t M, int C, const float* mean,
+                                  const float* invstd, const float* scale, const float* shift, const float* gamma,
+                                  float* dgamma, float* dbeta, float* stats, float* coef, void* dy);
+/* dx [N][H][W][Cin] bf16 = transposed conv of dy [N][Ho][Wo][Cout] (+ res, same shape as dx) */
+DFD_API int dfd_rn16_conv_dgrad(void* stream, const void* dy, int N, int H, int W, int Cin, const void* wd, int Cout,
+                                int k, int stride, int pad, const void* res, void* dx);
+DFD_API int64_t dfd_rn16_conv_wgrad_slab_floats(int N, int H, int W, int Cin, int Cout, int k, int stride, int pad);
+/* dw OIHW fp32 (written) from x and dy (bf16 NHWC); slab: scratch of slab_floats */
+DFD_API int dfd_rn16_conv_wgrad(void* stream, const void* x, int N, int H, int W, int Cin, const void* dy, int Cout,
+                                int k, int stride, int pad, float* slab, int64_t slab_floats, float* dw);
+/* n elements (n % 8 == 0): fp32 -> bf16 (to_bf16 = 1) or bf16 -> fp32 */
+DFD_API int dfd_rn16_cast(void* stream, const void* src, int to_bf16, int64_t n, void* dst);
+
 /* ---- optimizer ----------------------------------------------------------------------------
  * Replaces torch.nn.utils.clip_grad_norm_(params, max_norm) (src/ensemble_trainer.py:199) and
  * optim.AdamW / optim.Adam .step() (src/ensemble_trainer.py:146,200; src/train.py:323,126)

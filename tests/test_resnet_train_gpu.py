@@ -21,6 +21,9 @@ infrastructure only).
 3. The ensemble step: ``EnsembleDetector`` in train mode, weighted CE, backward -- both members
    receive every gradient, the resnet member's logits and gradients match the oracle trunk + the
    reference head math.
+4. bf16 training (round 6, ``compute_dtype='bf16'``): the bottleneck convolutions' bf16 kernels against
+   autograd on the same bf16 operands, and the trunk / ensemble step against fp64 within 3x torch's
+   own bf16-autocast error.
 Parity against torchvision itself is unpinned (not importable here); the oracle is the
 restatement pinned by key names / shapes / parameter count (tests/test_resnet.py)."""
 import ctypes
@@ -161,13 +164,144 @@ def test_no_grad_train_forward_updates_running_stats(cuda):
             torch.testing.assert_close(b, rb[name], rtol=1e-4, atol=1e-5)
 
 
-def test_bf16_training_refused_and_eval_grad_refused(cuda):
-    t = ResNet50Trunk("bf16").to(cuda).train()
-    with pytest.raises(NotImplementedError):
-        t(torch.randn(1, 3, 64, 64).cuda())
+def test_eval_grad_refused(cuda):
     t = ResNet50Trunk("fp32").to(cuda).eval()
     with pytest.raises(NotImplementedError):
         t(torch.randn(1, 3, 64, 64).cuda())  # parameters require grad, eval mode
+
+
+# ------------------------------------------------------------------ bf16 training (k_rn16.hip)
+@pytest.mark.parametrize("cin,h,cout,k,s", [sh for sh in SHAPES if sh[0] % 64 == 0])
+def test_bf16_training_conv_kernels_vs_autograd(cuda, cin, h, cout, k, s):
+    """The bf16 training convolutions (bf16 operands, fp32 accumulation) against torch autograd of
+    conv2d in fp32 on the SAME bf16-rounded operands: forward (and its BN-stat partials), data gradient
+    (stride 1 and 2: the transposed gather) and weight gradient.  Bound: relative L2 <= 1e-2 for the
+    bf16-rounded outputs (measured ~2-3e-3: one bf16 rounding of each output), 1e-4 for the fp32 weight
+    gradient (fp32 accumulation of exact bf16 products, only the summation order differs)."""
+    lib = _lib.load()
+    st = _lib.stream_of(cuda)
+    g = torch.Generator().manual_seed(cin * 7 + k + 1)
+    n, p = 3, (k - 1) // 2
+    x = torch.randn(n, h, h, cin, generator=g).cuda().bfloat16()
+    w = (torch.randn(cout, cin, k, k, generator=g) / (k * k * cin) ** 0.5).cuda()
+    ho = (h + 2 * p - k) // s + 1
+    dy = torch.randn(n, ho, ho, cout, generator=g).cuda().bfloat16()
+    res = torch.randn(n, h, h, cin, generator=g).cuda().bfloat16()
+    wf = torch.empty(w.numel(), dtype=torch.bfloat16, device=cuda)
+    wd = torch.empty_like(wf)
+    _lib.check(lib.dfd_rn16_pack_weights(st, w.data_ptr(), cout, cin, k, wf.data_ptr(), wd.data_ptr()))
+    y = torch.empty(n * ho * ho, cout, dtype=torch.bfloat16, device=cuda)
+    stats = torch.empty(2048 * cout, device=cuda)
+    rows = ctypes.c_int(0)
+    _lib.check(lib.dfd_rn16_conv_fwd(st, x.data_ptr(), n, h, h, cin, wf.data_ptr(), cout, k, s, p, y.data_ptr(),
+                                     stats.data_ptr(), ctypes.byref(rows)))
+    dx = torch.empty(n * h * h, cin, dtype=torch.bfloat16, device=cuda)
+    _lib.check(lib.dfd_rn16_conv_dgrad(st, dy.data_ptr(), n, h, h, cin, wd.data_ptr(), cout, k, s, p, res.data_ptr(),
+                                       dx.data_ptr()))
+    slab = torch.empty(lib.dfd_rn16_conv_wgrad_slab_floats(n, h, h, cin, cout, k, s, p), device=cuda)
+    dw = torch.empty_like(w)
+    _lib.check(lib.dfd_rn16_conv_wgrad(st, x.data_ptr(), n, h, h, cin, dy.data_ptr(), cout, k, s, p, slab.data_ptr(),
+                                       slab.numel(), dw.data_ptr()))
+    torch.cuda.synchronize()
+    with torch.backends.cudnn.flags(enabled=False):
+        xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        wr = w.bfloat16().float().clone().requires_grad_(True)
+        yr = F.conv2d(xr, wr, stride=s, padding=p)
+        yr.backward(dy.float().permute(0, 3, 1, 2))
+    yref = yr.detach().permute(0, 2, 3, 1).reshape(-1, cout)
+    assert _rel(y.float(), yref) < 1e-2
+    # per-workgroup (sum, sum of squares) rows of the rounded outputs, summed: the batch sums
+    st2 = stats[: rows.value * 2 * cout].view(rows.value, 2, cout).double().sum(0)
+    yb = y.double()
+    torch.testing.assert_close(st2[0], yb.sum(0), rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(st2[1], (yb * yb).sum(0), rtol=1e-4, atol=1e-3)
+    dxref = xr.grad.permute(0, 2, 3, 1).reshape(-1, cin) + res.float().reshape(-1, cin)
+    assert _rel(dx.float(), dxref) < 1e-2
+    assert _rel(dw, wr.grad) < 1e-4
+
+
+def _bf16_pair(seed, cuda):
+    torch.manual_seed(seed)
+    t = ResNet50Trunk("bf16").to(cuda).train()
+    refs = {}
+    for dt in (torch.float32, torch.float64):
+        refs[dt] = ResNet50TrunkCPU().to(cuda).to(dt).train()
+        refs[dt].load_state_dict(t.state_dict())
+    return t, refs
+
+
+BF16_K = 3.0  # each HIP bf16 gradient within 3x torch-bf16-autocast's distance to fp64 on the same step
+
+
+def test_bf16_train_mode_trunk_vs_fp64(cuda):
+    """The bf16 train-mode trunk at 4 x 128^2 against the fp64 restatement, each gradient tensor held to
+    BF16_K x the error of torch's own bf16 autocast step (the oracle trunk under torch.autocast bf16,
+    MIOpen off) against the same fp64 -- a per-tensor bound anchored to fp64, like the B0 224^2 test.
+    Features and the running buffers after the step: the same bound.  At this size (layer4's BatchNorms
+    normalise 64 values) bf16 rounding amplified through 53 train-mode BatchNorms leaves BOTH bf16 steps
+    far from fp64 (measured: features ~0.16 relative, gradients 1.2-1.7), so the test pins "as close as
+    torch's own bf16 step" (worst ratio measured 1.14), not an absolute accuracy."""
+    t, refs = _bf16_pair(11, cuda)
+    ref_ac = ResNet50TrunkCPU().to(cuda).train()
+    ref_ac.load_state_dict(t.state_dict())
+    g = torch.Generator().manual_seed(128)
+    x = torch.randn(4, 3, 128, 128, generator=g).cuda()
+    dfeat = torch.randn(4, 2048, generator=g).cuda() * 1e-2
+    feats = t(x)
+    feats.backward(dfeat)
+    with torch.backends.cudnn.flags(enabled=False):
+        f64 = resnet_features(refs[torch.float64], x.double())
+        f64.backward(dfeat.double())
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            fac = resnet_features(ref_ac, x)
+        fac.float().backward(dfeat)
+    fe, fa = _rel(feats.detach(), f64.detach()), _rel(fac.detach().float(), f64.detach())
+    print(f"bf16 trunk: features rel L2 vs fp64 {fe:.3g} (autocast {fa:.3g})")
+    assert fe <= max(BF16_K * fa, 1e-3), (fe, fa)
+    r64, rac = dict(refs[torch.float64].named_parameters()), dict(ref_ac.named_parameters())
+    bad, rows = [], []
+    for name, p in t.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), name
+        e, ea = _rel(p.grad, r64[name].grad), _rel(rac[name].grad, r64[name].grad)
+        rows.append((e / max(ea, 1e-12), name, e, ea))
+        if e > max(BF16_K * ea, 1e-3):
+            bad.append((name, e, ea))
+    rows.sort(reverse=True)
+    print("bf16 trunk: worst gradient err / autocast err: " +
+          "; ".join(f"{n} {q:.2f} ({e:.2e} vs {a:.2e})" for q, n, e, a in rows[:6]))
+    assert not bad, bad
+    rb, rba = dict(refs[torch.float64].named_buffers()), dict(ref_ac.named_buffers())
+    badb = []
+    for name, b in t.named_buffers():
+        if name.endswith("num_batches_tracked"):
+            assert int(b) == 1, name
+        else:
+            e, ea = _rel(b, rb[name]), _rel(rba[name], rb[name])
+            if e > max(BF16_K * ea, 1e-3):
+                badb.append((name, e, ea))
+    assert not badb, badb
+
+
+def test_bf16_ensemble_training_step(cuda):
+    """EnsembleDetector(compute_dtype='bf16') trains both members in bf16 (the B0 plan and the ResNet-50
+    bottlenecks): every parameter of both members receives a finite gradient and the step is
+    bit-reproducible."""
+    def run():
+        torch.manual_seed(0)
+        ens = EnsembleDetector(["efficientnet_b0", "resnet50"], pretrained=False, dropout_rate=0.0,
+                               compute_dtype="bf16").to(cuda).train()
+        x = torch.randn(2, 2, 3, 128, 128, generator=torch.Generator().manual_seed(1)).cuda()
+        logits, _ = ens(x)
+        loss = F.cross_entropy(logits, torch.tensor([0, 1]).cuda(), weight=torch.tensor([0.7, 1.3]).cuda())
+        loss.backward()
+        return float(loss), {f"{mi}.{n}": p.grad.clone() for mi, m in enumerate(ens.models)
+                             for n, p in m.named_parameters()}
+    la, ga = run()
+    lb, gb = run()
+    assert all(torch.isfinite(v).all() for v in ga.values())
+    assert la == lb
+    diff = [n for n in ga if not torch.equal(ga[n], gb[n])]
+    assert not diff, diff[:8]
 
 
 def test_ensemble_training_step(cuda):
