@@ -281,6 +281,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ens-dtypes", default="fp32,bf16", help="ensemble_train: compute dtypes, one line each")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -296,8 +297,8 @@ def main():
         print(json.dumps(bench_ensemble(args, dev)), flush=True)
     if args.model in ("ensemble_train", "all"):
         args.clips = min(args.clips, 8)
-        print(json.dumps(bench_ensemble_train(args, dev)), flush=True)
-        print(json.dumps(bench_ensemble_train(args, dev, "bf16")), flush=True)
+        for dt in args.ens_dtypes.split(","):
+            print(json.dumps(bench_ensemble_train(args, dev, dt)), flush=True)
 
 
 if __name__ == "__main__":

@@ -72,17 +72,22 @@ static bool rn16_shape_ok(int N, int H, int W, int Cin, int Cout, int kh, int kw
   return (int64_t)N * H * W <= (int64_t)INT32_MAX / 2 && (int64_t)N * Ho * Wo * Cout < (1ll << 40);
 }
 
-// the tile of a (rows, N) product: 128x128 where the rows fill the device, 32x64 (64-deep k-steps) on
-// the small late maps, 128x64 for 64-wide N
+// the tile of a (rows, N) product: these convolutions have long K (576..4608) and are MFMA-bound, so the
+// largest tile that still gives the 256 CUs enough workgroups -- 128x128 (16 MFMAs per wave per 32-deep
+// k-slice) from 384 tiles, 128x64 from 256, else 32x64 (64-deep k-steps) on the 7x7 map
 static int rn16_cfg(int64_t M, int N) {
-  if (N <= 64) return 1;
-  if (M >= 65536) return 0;
+  const int64_t t128 = cdiv64(M, 128);
+  if (N > 64 && t128 * cdiv(N, 128) >= 384) return 0;
+  if (t128 * cdiv(N, 64) >= 256) return 1;
   return 3;
 }
 
-#define DFD_RN16_CFGS(GO)                          \
-  if (cfg == 0) GO(128, 128, 1, 2, 32, 2);          \
-  else if (cfg == 1) GO(128, 64, 1, 3, 32, 2);      \
+#ifndef DFD_RN16_BK  // k-step depth of the 128-row tiles (A/B build switch: 32 or 64)
+#define DFD_RN16_BK 64
+#endif
+#define DFD_RN16_CFGS(GO)                                                  \
+  if (cfg == 0) GO(128, 128, 1, DFD_RN16_BK == 64 ? 1 : 2, DFD_RN16_BK, 2); \
+  else if (cfg == 1) GO(128, 64, 1, DFD_RN16_BK == 64 ? 2 : 3, DFD_RN16_BK, 2); \
   else GO(32, 64, 2, 2, 64, 3);
 
 static int rn16_grid(int64_t M, int N, int cfg, int64_t* tiles_m, int* ntn) {
