@@ -137,7 +137,7 @@ class PretrainedBackboneDetector(FlatModule):
         x_flat = x.reshape(batch_size * num_frames, c, h, w)
         sink = GradSink(self)
         if isinstance(self.backbone, ResNet50Trunk):
-            feats = self.backbone(x_flat)  # (B*T, 2048); train mode: fp32 autograd node (resnet._RnTrainFn)
+            feats = self.backbone(x_flat, grad_sink=sink)  # (B*T, 2048); train mode: resnet._RnTrainFn
         else:
             feats = self.backbone(x_flat, grad_sink=sink)  # (B*T, 1280)
         p = float(self.dropout.p) if self.training else 0.0

@@ -151,8 +151,10 @@ class ResNet50Trunk(nn.Sequential):
         self._folded, self._folded_key = f, key
         return f
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        """(N, 3, H, W) frames (fp32, or uint8 normalised in the conv1 gather) -> (N, 2048) fp32."""
+    def forward(self, x: torch.Tensor, grad_sink=None) -> torch.Tensor:
+        """(N, 3, H, W) frames (fp32, or uint8 normalised in the conv1 gather) -> (N, 2048) fp32.
+        grad_sink (training inside a FlatModule owner, e.g. the detector): the parameter gradients are
+        written into its flat buffer."""
         _lib.require_hip(x, "frames")
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected (N, 3, H, W) frames, got {tuple(x.shape)}")
@@ -168,7 +170,7 @@ class ResNet50Trunk(nn.Sequential):
             x = x.float()
             params = self.train_parameters()
             if grads:
-                return _RnTrainFn.apply(x, self, *params)
+                return _RnTrainFn.apply(x, self, grad_sink, *params)
             with torch.no_grad():
                 return _train_forward(self, x, save=False)[0]
         if grads:
@@ -362,20 +364,29 @@ def _train_forward(trunk, x, save):
     return feats, saved
 
 
+def _gdst(grads, p):
+    """the gradient destination of parameter p: its view of the owner's flat gradient buffer when the
+    trunk runs inside a FlatModule (GradSink; autograd adopts the views, no gather / scatter in the
+    optimizer), else a new fp32 tensor"""
+    t = grads.get(id(p))
+    if t is None:
+        t = torch.empty(p.shape, dtype=torch.float32, device=p.device)
+        grads[id(p)] = t
+    return t
+
+
 def _bn_bwd(lib, st, u, g, grads):
     """train-mode BN backward of unit u from its output gradient g -> dy; dgamma / dbeta into grads."""
     C = u.y.shape[1]
     dev = g.device
     stats = torch.empty(2048 * 2 * C, dtype=torch.float32, device=dev)
     coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
-    dg, db = torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev)
+    dg, db = _gdst(grads, u.bn.weight), _gdst(grads, u.bn.bias)
     dy = torch.empty_like(u.y)
     _lib.check(lib.dfd_rn_bn_train_bwd(st, g.data_ptr(), u.y.data_ptr(), u.y.shape[0], C, u.mean.data_ptr(),
                                        u.invstd.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
                                        u.bn.weight.data_ptr(), dg.data_ptr(), db.data_ptr(), stats.data_ptr(),
                                        coef.data_ptr(), dy.data_ptr()))
-    grads[id(u.bn.weight)] = dg
-    grads[id(u.bn.bias)] = db
     return dy
 
 
@@ -394,7 +405,7 @@ def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
                                          wp.data_ptr(), wp[nw:].data_ptr(), dx.data_ptr()))
     slab = torch.empty(lib.dfd_rn_conv_wgrad_slab_floats(n, u.hw[0], u.hw[1], cin, cout, k, k, s, p),
                        dtype=torch.float32, device=dev)
-    dw = torch.empty_like(w)
+    dw = _gdst(grads, conv.weight)
     x = u.x
     if x.dim() == 4:  # the stem reads the frames through their strides
         xs = (ctypes.c_int64 * 4)(x.stride(0), x.stride(2), x.stride(3), x.stride(1))
@@ -402,7 +413,6 @@ def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
         xs = _nhwc_strides(x, u.hw, cin)
     _lib.check(lib.dfd_rn_conv_wgrad(st, x.data_ptr(), xs, n, u.hw[0], u.hw[1], cin, dy.data_ptr(), cout, k, k, s, p,
                                      slab.data_ptr(), slab.numel(), dw.data_ptr()))
-    grads[id(conv.weight)] = dw
     return dx
 
 
@@ -411,14 +421,12 @@ def _bn_bwd16(lib, st, u, g, grads):
     dev = g.device
     stats = torch.empty(2048 * 2 * C, dtype=torch.float32, device=dev)
     coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
-    dg, db = torch.empty(C, dtype=torch.float32, device=dev), torch.empty(C, dtype=torch.float32, device=dev)
+    dg, db = _gdst(grads, u.bn.weight), _gdst(grads, u.bn.bias)
     dy = torch.empty_like(u.y)
     _lib.check(lib.dfd_rn16_bn_train_bwd(st, g.data_ptr(), u.y.data_ptr(), u.y.shape[0], C, u.mean.data_ptr(),
                                          u.invstd.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
                                          u.bn.weight.data_ptr(), dg.data_ptr(), db.data_ptr(), stats.data_ptr(),
                                          coef.data_ptr(), dy.data_ptr()))
-    grads[id(u.bn.weight)] = dg
-    grads[id(u.bn.bias)] = db
     return dy
 
 
@@ -432,10 +440,9 @@ def _conv_bwd16(lib, st, u, dy, n, grads, res=None):
                                        _lib.ptr(res), dx.data_ptr()))
     slab = torch.empty(lib.dfd_rn16_conv_wgrad_slab_floats(n, u.hw[0], u.hw[1], cin, cout, k, s, p),
                        dtype=torch.float32, device=dev)
-    dw = torch.empty_like(conv.weight, dtype=torch.float32)
+    dw = _gdst(grads, conv.weight)
     _lib.check(lib.dfd_rn16_conv_wgrad(st, u.x.data_ptr(), n, u.hw[0], u.hw[1], cin, dy.data_ptr(), cout, k, s, p,
                                        slab.data_ptr(), slab.numel(), dw.data_ptr()))
-    grads[id(conv.weight)] = dw
     return dx
 
 
@@ -445,12 +452,12 @@ def _relu_bwd16(lib, st, d, out):
     return g
 
 
-def _train_backward(trunk, saved, dfeat):
+def _train_backward(trunk, saved, dfeat, grads=None):
     lib = _lib.load()
     dev = dfeat.device
     st = _lib.stream_of(dev)
     n = saved["n"]
-    grads = {}
+    grads = {} if grads is None else grads
     blocks = saved["blocks"]
     hw = saved["final_hw"]
     if trunk.compute_dtype == "bf16":
@@ -527,9 +534,9 @@ class _RnTrainFn(torch.autograd.Function):
     none: they are data)."""
 
     @staticmethod
-    def forward(ctx, x, trunk, *params):
+    def forward(ctx, x, trunk, sink, *params):
         feats, saved = _train_forward(trunk, x, save=True)
-        ctx.trunk, ctx.saved, ctx.nparams = trunk, saved, len(params)
+        ctx.trunk, ctx.saved, ctx.nparams, ctx.sink = trunk, saved, len(params), sink
         return feats
 
     @staticmethod
@@ -537,10 +544,22 @@ class _RnTrainFn(torch.autograd.Function):
         if ctx.saved is None:
             raise RuntimeError("the ResNet-50 training node frees its saved activations after the first backward: "
                                "a second backward through it (retain_graph=True) is not supported")
-        grads = _train_backward(ctx.trunk, ctx.saved, dfeat.float())
-        ctx.saved = None
         params = ctx.trunk.train_parameters()
-        return (None, None) + tuple(grads.get(id(p)) for p in params)
+        grads, span = {}, None
+        if ctx.sink is not None:  # write straight into the owner's flat gradient buffer
+            owner = ctx.sink.owner
+            prefix = next(n for n, m in owner.named_modules() if m is ctx.trunk) + "."
+            name_of = {id(p): prefix + n for n, p in ctx.trunk.named_parameters()}
+            names = [name_of[id(p)] for p in params]
+            for p, v in zip(params, ctx.sink.views(names)):
+                grads[id(p)] = v
+            offs = [owner._p_off[n] for n in names]
+            span = (min(offs), max(o + p.numel() for o, p in zip(offs, params)))
+        grads = _train_backward(ctx.trunk, ctx.saved, dfeat.float(), grads)
+        ctx.saved = None
+        if span is not None:
+            ctx.sink.ready(*span)
+        return (None, None, None) + tuple(grads.get(id(p)) for p in params)
 
 
 def _norm6(spec) -> ctypes.Array:
