@@ -92,12 +92,13 @@ _SIGS = {
     "dfd_rn_conv_wgrad": (c_i, [c_p, c_p, ctypes.POINTER(c_i64), c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_p,
                                 c_i64, c_p]),
     "dfd_rn16_pack_weights": (c_i, [c_p, c_p, c_i, c_i, c_i, c_p, c_p]),
+    "dfd_rn16_pack_all": (c_i, [c_p, c_p, c_i, c_i64, c_p]),
     "dfd_rn16_conv_fwd": (c_i, [c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_p, ctypes.POINTER(c_i)]),
     "dfd_rn16_bn_finalize": (c_i, [c_p, c_p, c_i, c_i64, c_i, c_p, c_p, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p]),
     "dfd_rn16_bn_act": (c_i, [c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i64, c_i, c_p]),
     "dfd_rn16_relu_bwd": (c_i, [c_p, c_p, c_p, c_i64, c_p]),
     "dfd_rn16_gap_bwd": (c_i, [c_p, c_p, c_p, c_i, c_i, c_i, c_p]),
-    "dfd_rn16_bn_train_bwd": (c_i, [c_p, c_p, c_p, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "dfd_rn16_bn_train_bwd": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "dfd_rn16_conv_dgrad": (c_i, [c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_p]),
     "dfd_rn16_conv_wgrad_slab_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i]),
     "dfd_rn16_conv_wgrad": (c_i, [c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_p, c_i64, c_p]),

@@ -635,6 +635,13 @@ int dfd_rn16_pack_weights(void* stream, const float* w, int Cout, int Cin, int k
   DFD_GUARD_END
 }
 
+int dfd_rn16_pack_all(void* stream, const int64_t* table, int n, int64_t max_elems, void* out) {
+  DFD_GUARD_BEGIN
+  if (!table || !out) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  return dfd::rn16_pack_all((hipStream_t)stream, table, n, max_elems, (dfd::bf16*)out);
+  DFD_GUARD_END
+}
+
 int dfd_rn16_conv_fwd(void* stream, const void* x, int N, int H, int W, int Cin, const void* wf, int Cout, int k,
                       int stride, int pad, void* y, float* stats, int* stat_rows) {
   DFD_GUARD_BEGIN
@@ -709,16 +716,17 @@ int dfd_rn16_bn_finalize(void* stream, const float* stats, int rows, int64_t cou
   DFD_GUARD_END
 }
 
-int dfd_rn16_bn_train_bwd(void* stream, const void* g, const void* y, int64_t M, int C, const float* mean,
-                          const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
-                          float* dbeta, float* stats, float* coef, void* dy) {
+int dfd_rn16_bn_train_bwd(void* stream, const void* g, const void* relu_out, const void* y, int64_t M, int C,
+                          const float* mean, const float* invstd, const float* scale, const float* shift,
+                          const float* gamma, float* dgamma, float* dbeta, float* stats, float* coef, void* dy) {
   DFD_GUARD_BEGIN
   if (!g || !y || !mean || !invstd || !scale || !shift || !gamma || !dgamma || !dbeta || !stats || !coef || !dy) {
     dfd::set_error("null argument", __FILE__, __LINE__);
     return -1;
   }
-  return dfd::rn16_bn_train_bwd((hipStream_t)stream, (const dfd::bf16*)g, (const dfd::bf16*)y, M, C, mean, invstd,
-                                scale, shift, gamma, dgamma, dbeta, stats, coef, (dfd::bf16*)dy);
+  return dfd::rn16_bn_train_bwd((hipStream_t)stream, (const dfd::bf16*)g, (const dfd::bf16*)relu_out,
+                                (const dfd::bf16*)y, M, C, mean, invstd, scale, shift, gamma, dgamma, dbeta, stats,
+                                coef, (dfd::bf16*)dy);
   DFD_GUARD_END
 }
 

@@ -227,6 +227,33 @@ __global__ void rn16_pack_kernel(const float* __restrict__ w, int Co, int Ci, in
   }
 }
 
+// every convolution of the step in ONE launch: table row i = {fp32 weight pointer, Co, Ci, KK, wf offset,
+// wd offset (elements of out, -1: none)}; blockIdx.y = row
+__global__ void rn16_pack_all_kernel(const int64_t* __restrict__ table, bf16* __restrict__ out) {
+  const int64_t* t = table + 6 * blockIdx.y;
+  const float* w = reinterpret_cast<const float*>(t[0]);
+  const int Co = (int)t[1], Ci = (int)t[2], KK = (int)t[3];
+  bf16* wf = out + t[4];
+  bf16* wd = t[5] >= 0 ? out + t[5] : nullptr;
+  const int64_t n = (int64_t)Co * Ci * KK;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int tp = (int)(i % KK);
+    const int64_t r = i / KK;
+    const int ci = (int)(r % Ci), co = (int)(r / Ci);
+    const bf16 v = Tr<bf16>::from_f(w[i]);
+    wf[((int64_t)co * KK + tp) * Ci + ci] = v;
+    if (wd) wd[((int64_t)ci * KK + tp) * Co + co] = v;
+  }
+}
+
+int rn16_pack_all(hipStream_t s, const int64_t* table, int n, int64_t max_elems, bf16* out) {
+  if (n <= 0) return 0;
+  const int gx = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(max_elems, 256), 256));
+  hipLaunchKernelGGL(rn16_pack_all_kernel, dim3((unsigned)gx, (unsigned)n), dim3(256), 0, s, table, out);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
 int rn16_pack_weights(hipStream_t s, const float* w, int Co, int Ci, int KK, bf16* wf, bf16* wd) {
   hipLaunchKernelGGL(rn16_pack_kernel, dim3(ew_blocks((int64_t)Co * Ci * KK)), dim3(256), 0, s, w, Co, Ci, KK, wf, wd);
   DFD_HIP_CHECK(hipGetLastError());
@@ -355,11 +382,105 @@ int rn16_cast(hipStream_t s, const void* src, int to_bf16, int64_t n, void* dst)
   return 0;
 }
 
-// the BN backward of a train-mode BatchNorm2d from its output gradient g (identity activation), centred
-int rn16_bn_train_bwd(hipStream_t s, const bf16* g, const bf16* y, int64_t M, int C, const float* mean,
-                      const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
-                      float* dbeta, float* stats, float* coef, bf16* dy) {
+// The ReLU between a BN and the next convolution folded into the BN backward: g = (a > 0) * da is never
+// materialised.  Partial rows (sum g, sum g * (y - mean) * invstd) per row chunk x 64-channel group
+// (8 channel vectors x 32 row lanes, two rows' loads in flight, lanes added in order through LDS:
+// deterministic), in launch_bn_bwd_finalize's [rows][2][C] layout.
+__global__ __launch_bounds__(256) void rn16_bn_bwd_reduce_relu_kernel(const bf16* __restrict__ da,
+                                                                      const bf16* __restrict__ a,
+                                                                      const bf16* __restrict__ y,
+                                                                      const float* __restrict__ mean,
+                                                                      const float* __restrict__ invstd, int64_t M, int C,
+                                                                      int64_t rows_per_wg, float* __restrict__ stats) {
+  __shared__ float sh[2][32][65];
+  const int tid = threadIdx.x, v = tid & 7, rl = tid >> 3;
+  const int c = blockIdx.y * 64 + v * 8;
+  float mu[8], is[8], s8[8], q8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { s8[j] = 0.f; q8[j] = 0.f; }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg, r1 = min(M, r0 + rows_per_wg);
+  if (c < C) {
+    ld8f(mean + c, mu);
+    ld8f(invstd + c, is);
+    auto one = [&](const float (&d)[8], const float (&av)[8], const float (&yv)[8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = av[j] > 0.f ? d[j] : 0.f;
+        s8[j] += g;
+        q8[j] += g * ((yv[j] - mu[j]) * is[j]);
+      }
+    };
+    int64_t r = r0 + rl;
+    for (; r + 32 < r1; r += 64) {
+      float d0[8], a0[8], y0[8], d1[8], a1[8], y1[8];
+      ld8(da + r * C + c, d0); ld8(a + r * C + c, a0); ld8(y + r * C + c, y0);
+      ld8(da + (r + 32) * C + c, d1); ld8(a + (r + 32) * C + c, a1); ld8(y + (r + 32) * C + c, y1);
+      one(d0, a0, y0);
+      one(d1, a1, y1);
+    }
+    if (r < r1) {
+      float d0[8], a0[8], y0[8];
+      ld8(da + r * C + c, d0); ld8(a + r * C + c, a0); ld8(y + r * C + c, y0);
+      one(d0, a0, y0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sh[0][rl][v * 8 + j] = s8[j]; sh[1][rl][v * 8 + j] = q8[j]; }
+  __syncthreads();
+  if (tid < 128) {
+    const int which = tid >> 6, cl = tid & 63;
+    float acc = 0.f;
+    for (int l = 0; l < 32; ++l) acc += sh[which][l][cl];
+    if (blockIdx.y * 64 + cl < C) stats[((int64_t)blockIdx.x * 2 + which) * C + blockIdx.y * 64 + cl] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void rn16_bn_bwd_apply_relu_kernel(const bf16* __restrict__ da,
+                                                                     const bf16* __restrict__ a,
+                                                                     const bf16* __restrict__ y,
+                                                                     const float* __restrict__ mu,
+                                                                     const float* __restrict__ coef, int64_t nvec, int C,
+                                                                     bf16* __restrict__ dy) {
+  const int cv = C / 8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % cv) * 8;
+    float ga[8], av[8], ya[8], m8[8], k1[8], k2[8], k3[8];
+    ld8(da + i * 8, ga);
+    ld8(a + i * 8, av);
+    ld8(y + i * 8, ya);
+    ld8f(mu + c, m8);
+    ld8f(coef + c, k1);
+    ld8f(coef + C + c, k2);
+    ld8f(coef + 2 * C + c, k3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ga[j] = k1[j] * (av[j] > 0.f ? ga[j] : 0.f) + k2[j] * (ya[j] - m8[j]) + k3[j];
+    st8(dy + i * 8, ga);
+  }
+}
+
+// the BN backward of a train-mode BatchNorm2d from its output gradient g (identity activation), centred;
+// relu_out != null: g = (relu_out > 0) * g, the ReLU that followed this BN's output (its saved output)
+int rn16_bn_train_bwd(hipStream_t s, const bf16* g, const bf16* relu_out, const bf16* y, int64_t M, int C,
+                      const float* mean, const float* invstd, const float* scale, const float* shift,
+                      const float* gamma, float* dgamma, float* dbeta, float* stats, float* coef, bf16* dy) {
   if (C % 8) { set_error("rn16_bn_train_bwd: C % 8", __FILE__, __LINE__); return -1; }
+  if (relu_out) {
+    if (C % 64) { set_error("rn16_bn_train_bwd: C % 64 with the ReLU mask", __FILE__, __LINE__); return -1; }
+    const int groups = C / 64;
+    const int64_t nx = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(512, cdiv64(M, 64)),
+                                                              std::max(1, 1024 / groups)));
+    const int64_t rpw = cdiv64(M, nx);
+    const int rows = (int)cdiv64(M, rpw);
+    hipLaunchKernelGGL(rn16_bn_bwd_reduce_relu_kernel, dim3((unsigned)rows, (unsigned)groups), dim3(256), 0, s, g,
+                       relu_out, y, mean, invstd, M, C, rpw, stats);
+    DFD_HIP_CHECK(hipGetLastError());
+    DFD_TRY(launch_bn_bwd_finalize(s, stats, rows, M, C, gamma, mean, invstd, true, dgamma, dbeta, false, coef, true));
+    const int64_t nvec = M * C / 8;
+    hipLaunchKernelGGL(rn16_bn_bwd_apply_relu_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, s, g, relu_out, y, mean,
+                       coef, nvec, C, dy);
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   BnBwdIn in{};
   in.dZ = g;
   in.silu = false;

@@ -8,6 +8,9 @@ namespace dfd {
 
 // fp32 w [Co][Ci][k*k] -> bf16 wf [Co][k*k][Ci] (forward) and, if wd, wd [Ci][k*k][Co] (data gradient)
 int rn16_pack_weights(hipStream_t s, const float* w, int Co, int Ci, int KK, bf16* wf, bf16* wd);
+// the same for n convolutions in one launch: table (device) rows {w, Co, Ci, KK, wf offset, wd offset or -1}
+// into out (bf16 elements); max_elems the largest Co*Ci*KK
+int rn16_pack_all(hipStream_t s, const int64_t* table, int n, int64_t max_elems, bf16* out);
 // y = conv(x) (no bias), per-workgroup BN partial rows (sum, sum of squares) of y into stats (<= 2048 x Cout
 // floats; *stat_rows rows written), for launch_bn_finalize
 int rn16_conv_fwd(hipStream_t s, const bf16* x, int N, int H, int W, int Cin, const bf16* wf, int Cout, int k, int stride,
@@ -24,8 +27,9 @@ int rn16_bn_act(hipStream_t s, const bf16* y, const float* mean, const float* sc
 int rn16_relu_bwd(hipStream_t s, const bf16* dout, const bf16* out, int64_t n, bf16* g);
 int rn16_gap_bwd(hipStream_t s, const float* dfeat, const bf16* out, int N, int HW, int C, bf16* g);
 int rn16_cast(hipStream_t s, const void* src, int to_bf16, int64_t n, void* dst);
-int rn16_bn_train_bwd(hipStream_t s, const bf16* g, const bf16* y, int64_t M, int C, const float* mean,
-                      const float* invstd, const float* scale, const float* shift, const float* gamma, float* dgamma,
-                      float* dbeta, float* stats, float* coef, bf16* dy);
+// relu_out (or null): the saved output of the ReLU that followed this BN -- g is masked by it inline
+int rn16_bn_train_bwd(hipStream_t s, const bf16* g, const bf16* relu_out, const bf16* y, int64_t M, int C,
+                      const float* mean, const float* invstd, const float* scale, const float* shift,
+                      const float* gamma, float* dgamma, float* dbeta, float* stats, float* coef, bf16* dy);
 
 }  // namespace dfd

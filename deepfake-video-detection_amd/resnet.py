@@ -254,16 +254,43 @@ def _bn_momentum(bn):
     return float(bn.momentum) if bn.momentum is not None else 1.0 / float(bn.num_batches_tracked)
 
 
-def _conv_bn_fwd16(lib, st, u, x, n, hw, save):
+def _pack16(trunk, lib, st, dev, save):
+    """Every bottleneck convolution's fp32 master weights -> bf16 wf (forward) and, for a backward, wd
+    (data gradient) in ONE launch (dfd_rn16_pack_all) -> {id(conv): (wf, wd or None)} views of one buffer.
+    The device table of weight pointers / shapes / offsets is built once per trunk and layout."""
+    convs = []
+    for li in range(4):
+        for blk in trunk[4 + li]:
+            convs += [blk.conv1, blk.conv2, blk.conv3] + ([blk.downsample[0]] if blk.downsample is not None else [])
+    key = (bool(save), str(dev), tuple(c.weight.data_ptr() for c in convs))
+    cache = getattr(trunk, "_rn16_pack", None)
+    if cache is None or cache[0] != key:
+        rows, off, spans = [], 0, []
+        for c in convs:
+            if c.weight.dtype != torch.float32 or not c.weight.is_contiguous():
+                raise RuntimeError("bf16 ResNet training: conv weights must be contiguous fp32 masters")
+            ne = c.weight.numel()
+            kk = c.kernel_size[0] * c.kernel_size[1]
+            od = off + ne if save else -1
+            rows.append([c.weight.data_ptr(), c.out_channels, c.in_channels, kk, off, od])
+            spans.append((off, od, ne))
+            off += 2 * ne if save else ne
+        table = torch.tensor(rows, dtype=torch.int64, device=dev)
+        cache = (key, table, spans, off, max(sp[2] for sp in spans))
+        trunk._rn16_pack = cache
+    _, table, spans, total, mx = cache
+    out = torch.empty(total, dtype=torch.bfloat16, device=dev)
+    _lib.check(lib.dfd_rn16_pack_all(st, table.data_ptr(), len(convs), mx, out.data_ptr()))
+    return {id(c): (out[o:o + ne], out[od:od + ne] if od >= 0 else None) for c, (o, od, ne) in zip(convs, spans)}
+
+
+def _conv_bn_fwd16(lib, st, u, x, n, hw, save, packs):
     """bf16: y = conv(x) on the packed bf16 weights, the BN batch statistics (running buffers updated)."""
     conv, bn = u.conv, u.bn
     k, s, p, cin, cout = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.in_channels, conv.out_channels
     ho, wo = (hw[0] + 2 * p - k) // s + 1, (hw[1] + 2 * p - k) // s + 1
     dev = x.device
-    w = conv.weight.detach().float().contiguous()
-    wf = torch.empty(w.numel(), dtype=torch.bfloat16, device=dev)
-    wd = torch.empty(w.numel(), dtype=torch.bfloat16, device=dev) if save else None
-    _lib.check(lib.dfd_rn16_pack_weights(st, w.data_ptr(), cout, cin, k, wf.data_ptr(), _lib.ptr(wd)))
+    wf, wd = packs[id(conv)]
     y = torch.empty(n * ho * wo, cout, dtype=torch.bfloat16, device=dev)
     stats = torch.empty(2048 * cout, dtype=torch.float32, device=dev)
     rows = ctypes.c_int(0)
@@ -318,18 +345,19 @@ def _train_forward(trunk, x, save):
         h16 = torch.empty(h.shape, dtype=torch.bfloat16, device=dev)
         _lib.check(lib.dfd_rn16_cast(st, h.data_ptr(), 1, h.numel(), h16.data_ptr()))
         h = h16
+        packs = _pack16(trunk, lib, st, dev, save)
         for li in range(4):
             for blk in trunk[4 + li]:
                 b = {"in": h, "hw": hw}
                 u1, u2, u3 = unit(blk.conv1, blk.bn1), unit(blk.conv2, blk.bn2), unit(blk.conv3, blk.bn3)
-                y1, hw1, v1 = _conv_bn_fwd16(lib, st, u1, h, n, hw, save)
+                y1, hw1, v1 = _conv_bn_fwd16(lib, st, u1, h, n, hw, save, packs)
                 a1 = _bn_act16(lib, st, y1, v1, blk.bn1, None, True)
-                y2, hw2, v2 = _conv_bn_fwd16(lib, st, u2, a1, n, hw1, save)
+                y2, hw2, v2 = _conv_bn_fwd16(lib, st, u2, a1, n, hw1, save, packs)
                 a2 = _bn_act16(lib, st, y2, v2, blk.bn2, None, True)
-                y3, _, v3 = _conv_bn_fwd16(lib, st, u3, a2, n, hw2, save)
+                y3, _, v3 = _conv_bn_fwd16(lib, st, u3, a2, n, hw2, save, packs)
                 if blk.downsample is not None:
                     ud = unit(blk.downsample[0], blk.downsample[1])
-                    yd, _, vd = _conv_bn_fwd16(lib, st, ud, h, n, hw, save)
+                    yd, _, vd = _conv_bn_fwd16(lib, st, ud, h, n, hw, save, packs)
                     idn = _bn_act16(lib, st, yd, vd, blk.downsample[1], None, False)
                     b["ds"] = ud
                 else:
@@ -416,14 +444,16 @@ def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
     return dx
 
 
-def _bn_bwd16(lib, st, u, g, grads):
+def _bn_bwd16(lib, st, u, g, grads, relu_out=None):
+    """relu_out: the saved output of the ReLU after this BN; g is then its INPUT gradient, masked inline"""
     C = u.y.shape[1]
     dev = g.device
     stats = torch.empty(2048 * 2 * C, dtype=torch.float32, device=dev)
     coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
     dg, db = _gdst(grads, u.bn.weight), _gdst(grads, u.bn.bias)
     dy = torch.empty_like(u.y)
-    _lib.check(lib.dfd_rn16_bn_train_bwd(st, g.data_ptr(), u.y.data_ptr(), u.y.shape[0], C, u.mean.data_ptr(),
+    _lib.check(lib.dfd_rn16_bn_train_bwd(st, g.data_ptr(), _lib.ptr(relu_out), u.y.data_ptr(), u.y.shape[0], C,
+                                         u.mean.data_ptr(),
                                          u.invstd.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
                                          u.bn.weight.data_ptr(), dg.data_ptr(), db.data_ptr(), stats.data_ptr(),
                                          coef.data_ptr(), dy.data_ptr()))
@@ -475,10 +505,9 @@ def _train_backward(trunk, saved, dfeat, grads=None):
                 other = _conv_bwd16(lib, st, b["ds"], dyd, n, grads)
             else:
                 other = g
-            g2 = _relu_bwd16(lib, st, _conv_bwd16(lib, st, u3, dy3, n, grads), b["a2"])
-            dy2 = _bn_bwd16(lib, st, u2, g2, grads)
-            g1 = _relu_bwd16(lib, st, _conv_bwd16(lib, st, u2, dy2, n, grads), b["a1"])
-            dy1 = _bn_bwd16(lib, st, u1, g1, grads)
+            # the ReLUs after bn2 / bn1 are folded into their BN backward (masked by the saved a2 / a1)
+            dy2 = _bn_bwd16(lib, st, u2, _conv_bwd16(lib, st, u3, dy3, n, grads), grads, relu_out=b["a2"])
+            dy1 = _bn_bwd16(lib, st, u1, _conv_bwd16(lib, st, u2, dy2, n, grads), grads, relu_out=b["a1"])
             g = _conv_bwd16(lib, st, u1, dy1, n, grads, res=other)
         g32 = torch.empty(g.shape, dtype=torch.float32, device=dev)
         _lib.check(lib.dfd_rn16_cast(st, g.data_ptr(), 0, g.numel(), g32.data_ptr()))

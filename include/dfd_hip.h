@@ -271,6 +271,9 @@ DFD_API int dfd_rn_conv_wgrad(void* stream, const float* x, const int64_t* xs4, 
  * BN statistics in fp32 partials merged in fp64.  conv1 + bn1 + relu + maxpool stay on dfd_rn_train_*.
  * w OIHW fp32 -> wf [Cout][k][k][Cin] bf16 (forward), wd [Cin][k][k][Cout] bf16 (data gradient, or null) */
 DFD_API int dfd_rn16_pack_weights(void* stream, const float* w, int Cout, int Cin, int k, void* wf, void* wd);
+/* every convolution of a step in one launch: table = n device rows of int64 {w (fp32 OIHW pointer), Cout, Cin, k*k,
+ * wf offset, wd offset or -1} (offsets in bf16 elements of out); max_elems = the largest Cout*Cin*k*k */
+DFD_API int dfd_rn16_pack_all(void* stream, const int64_t* table, int n, int64_t max_elems, void* out);
 /* y = conv(x) NHWC bf16 (no bias); BN partial rows (sum, sum of squares) into stats (>= 2048*Cout floats),
  * *stat_rows rows, for dfd_rn16_bn_finalize */
 DFD_API int dfd_rn16_conv_fwd(void* stream, const void* x, int N, int H, int W, int Cin, const void* wf, int Cout,
@@ -285,10 +288,12 @@ DFD_API int dfd_rn16_bn_act(void* stream, const void* y, const float* mean, cons
                             const void* res, int relu, int64_t M, int C, void* out);
 DFD_API int dfd_rn16_relu_bwd(void* stream, const void* dout, const void* out, int64_t n, void* g);
 DFD_API int dfd_rn16_gap_bwd(void* stream, const float* dfeat, const void* out, int N, int HW, int C, void* g);
-/* train-mode BN backward (centred), bf16 g / y / dy; dgamma, dbeta written; stats >= 2048*2*C, coef >= 3*C */
-DFD_API int dfd_rn16_bn_train_bwd(void* stream, const void* g, const void* y, int64_t M, int C, const float* mean,
-                                  const float* invstd, const float* scale, const float* shift, const float* gamma,
-                                  float* dgamma, float* dbeta, float* stats, float* coef, void* dy);
+/* train-mode BN backward (centred), bf16 g / y / dy; dgamma, dbeta written; stats >= 2048*2*C, coef >= 3*C;
+ * relu_out (or null; C % 64): the saved output of the ReLU after this BN, g is masked by it inline */
+DFD_API int dfd_rn16_bn_train_bwd(void* stream, const void* g, const void* relu_out, const void* y, int64_t M, int C,
+                                  const float* mean, const float* invstd, const float* scale, const float* shift,
+                                  const float* gamma, float* dgamma, float* dbeta, float* stats, float* coef,
+                                  void* dy);
 /* dx [N][H][W][Cin] bf16 = transposed conv of dy [N][Ho][Wo][Cout] (+ res, same shape as dx) */
 DFD_API int dfd_rn16_conv_dgrad(void* stream, const void* dy, int N, int H, int W, int Cin, const void* wd, int Cout,
                                 int k, int stride, int pad, const void* res, void* dx);
