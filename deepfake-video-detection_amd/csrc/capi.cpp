@@ -822,7 +822,7 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
   const dfd::TuningScope ts(&tn);
   hipStream_t s = (hipStream_t)stream;
   if (!A || !B || !C) { dfd::set_error("vgemm: null argument", __FILE__, __LINE__); return -1; }
-  if (op == 0 || op == 2 || op == 4 || op == 5) {  // NT: own kernel (0; 4 / 5: 256- / 128-wide tiles) or hipBLASLt (2)
+  if (op == 0 || op == 2 || op == 4 || op == 5 || op == 7) {  // NT: own kernel (0; 4 / 5 / 7: 256- / 128- / 64-wide tiles) or hipBLASLt (2)
     if (((epi & dfd::VG_BIAS) && !bias) || ((epi & dfd::VG_RESID) && !R) || ((epi & dfd::VG_DGELU) && !Z) ||
         ((epi & dfd::VG_GELU2) && !G)) {
       dfd::set_error("vgemm: epilogue operand missing", __FILE__, __LINE__);
@@ -837,7 +837,7 @@ int dfd_vgemm(void* stream, int op, const void* A, const void* B, void* C, const
     a.A = (const dfd::bf16*)A; a.B = (const dfd::bf16*)B; a.C = (dfd::bf16*)C; a.R = (const dfd::bf16*)R;
     a.bias = bias; a.Z = (const dfd::bf16*)Z; a.G = (dfd::bf16*)G;
     a.lda = K; a.ldb = K; a.ldc = N; a.M = (int)M; a.N = N; a.K = K;
-    a.bn = op == 4 ? 256 : op == 5 ? 128 : 0;
+    a.bn = op == 4 ? 256 : op == 5 ? 128 : op == 7 ? 64 : 0;
     return dfd::launch_vgemm_nt(s, a, epi);
   }
   if (op == 1 || op == 3 || op == 6) {  // TN: C (fp32 [N][K]) = A^T . B with A [M][N], B [M][K]

@@ -273,6 +273,33 @@ __device__ __forceinline__ void gelu_pair_rat_(float x, float& g, float& d) {
   g = 0.5f * x * e;
   d = 0.5f * e + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
+// the same pair for two values at once: the polynomial chains as packed-f32 FMAs (v_pk_fma_f32, two
+// lanes per instruction), the quotient by v_rcp_f32 (1 ulp) instead of the IEEE division sequence,
+// exp(-x^2 / 2) from the scaled argument's square.  For fc1's epilogue, whose per-element VALU work
+// ran longer than the tile's stores (k_vgemm.hip).
+__device__ __forceinline__ void gelu_pair2_rat_(f32x2_t x, f32x2_t& g, f32x2_t& d) {
+  const f32x2_t u = x * 0.70710678118654752f;
+  const f32x2_t uc = {fminf(fmaxf(u.x, -4.f), 4.f), fminf(fmaxf(u.y, -4.f), 4.f)};
+  const f32x2_t x2 = uc * uc;
+  auto fma2 = [](f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); };
+  auto splat = [](float v) { return f32x2_t{v, v}; };
+  f32x2_t p = fma2(x2, splat(-2.72614225801306e-10f), splat(2.77068142495902e-08f));
+  p = fma2(x2, p, splat(-2.10102402082508e-06f));
+  p = fma2(x2, p, splat(-5.69250639462346e-05f));
+  p = fma2(x2, p, splat(-7.34990630326855e-04f));
+  p = fma2(x2, p, splat(-2.95459980854025e-03f));
+  p = fma2(x2, p, splat(-1.60960333262415e-02f));
+  p *= uc;
+  f32x2_t q = fma2(x2, splat(-1.45660718464996e-05f), splat(-2.13374055278905e-04f));
+  q = fma2(x2, q, splat(-1.68282697438203e-03f));
+  q = fma2(x2, q, splat(-7.37332916720468e-03f));
+  q = fma2(x2, q, splat(-1.42647390514189e-02f));
+  const f32x2_t e = fma2(p, f32x2_t{__builtin_amdgcn_rcpf(q.x), __builtin_amdgcn_rcpf(q.y)}, splat(1.0f));
+  g = (x * 0.5f) * e;
+  const f32x2_t uu = u * u;
+  const f32x2_t ex = {__expf(-uu.x), __expf(-uu.y)};
+  d = fma2(x * 0.39894228040143268f, ex, e * 0.5f);
+}
 __device__ __forceinline__ void gelu_pair_(float x, float& g, float& d) {
   const float e = 1.0f + erff(x * 0.70710678118654752f);
   g = 0.5f * x * e;

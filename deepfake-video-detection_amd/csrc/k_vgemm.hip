@@ -359,19 +359,31 @@ __global__ __launch_bounds__(512, 1) void vgemm_nt_kernel(VgemmArgs a) {
           // C = gelu'(z), G = gelu(z) of the stored (rounded) pre-activation z
           float g[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (DFD_GELU_RAT) gelu_pair_rat_(Tr<bf16>::round(o[j]), g[j], o[j]);
-            else gelu_pair_(Tr<bf16>::round(o[j]), g[j], o[j]);
+          for (int j = 0; j < 8; j += 2) {
+            if (DFD_GELU_RAT) {
+              f32x2_t gg, dd;
+              gelu_pair2_rat_(f32x2_t{Tr<bf16>::round(o[j]), Tr<bf16>::round(o[j + 1])}, gg, dd);
+              g[j] = gg.x; g[j + 1] = gg.y; o[j] = dd.x; o[j + 1] = dd.y;
+            } else {
+              gelu_pair_(Tr<bf16>::round(o[j]), g[j], o[j]);
+              gelu_pair_(Tr<bf16>::round(o[j + 1]), g[j + 1], o[j + 1]);
+            }
           }
           st8bf(a.G + (int64_t)row * a.ldc + c, g);
         }
         if constexpr ((EP & VG_GELU) != 0) {
           // inference fc1: C = gelu(z) alone, the same value VG_GELU2 leaves in G (no derivative store)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float gd;
-            if (DFD_GELU_RAT) gelu_pair_rat_(Tr<bf16>::round(o[j]), o[j], gd);
-            else gelu_pair_(Tr<bf16>::round(o[j]), o[j], gd);
+          for (int j = 0; j < 8; j += 2) {
+            if (DFD_GELU_RAT) {
+              f32x2_t gg, dd;
+              gelu_pair2_rat_(f32x2_t{Tr<bf16>::round(o[j]), Tr<bf16>::round(o[j + 1])}, gg, dd);
+              o[j] = gg.x; o[j + 1] = gg.y;
+            } else {
+              float gd;
+              gelu_pair_(Tr<bf16>::round(o[j]), o[j], gd);
+              gelu_pair_(Tr<bf16>::round(o[j + 1]), o[j + 1], gd);
+            }
           }
         }
         st8bf(a.C + (int64_t)row * a.ldc + c, o);
@@ -581,6 +593,7 @@ int launch_vgemm_nt(hipStream_t s, const VgemmArgs& a0, int ep) {
   // (the weight-gradient kernel's form of it needs 2 x 24 fragment registers and spills: not built)
   if (bn == 64) {  // 64-wide outputs (ResNet-50 layer1): bias / identity / ReLU epilogues, plain K loop
     switch (ep) {
+      case 0: hipLaunchKernelGGL((vgemm_nt_kernel<0, 64>), dim3(tiles), dim3(512), 0, s, a); break;
       case VG_BIAS: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS, 64>), dim3(tiles), dim3(512), 0, s, a); break;
       case VG_BIAS | VG_RESID: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RESID, 64>), dim3(tiles), dim3(512), 0, s, a); break;
       case VG_BIAS | VG_RELU: hipLaunchKernelGGL((vgemm_nt_kernel<VG_BIAS | VG_RELU, 64>), dim3(tiles), dim3(512), 0, s, a); break;

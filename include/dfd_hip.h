@@ -374,9 +374,9 @@ DFD_API int dfd_attention(void* stream, int backward, int images, int heads, int
  * pre-activation, G = gelu(z) and C = gelu'(z) -- C does NOT keep the pre-activation; 8: C *= Z[M][N]
  * elementwise, Z being the derivative an epi-4 launch stored in its C (the MLP backward's x gelu').
  * Instantiated masks: 0, 1, 1|2, 1|4, 8, 1|16, 1|2|16.  K % 64 == 0 and N % 128 == 0, except that
- * N % 64 == 0 (the 64-wide tile) is accepted with the bias / identity / ReLU masks 1, 1|2, 1|16,
- * 1|2|16 only.  The tile width (256, 128 or 64 columns) is chosen by shape; ops 4 / 5 force 256
- * (N % 256 == 0) / 128.
+ * N % 64 == 0 (the 64-wide tile) is accepted with the masks 0, 1, 1|2, 1|16, 1|2|16 only.  The
+ * tile width (256, 128 or 64 columns) is chosen by shape; ops 4 / 5 / 7 force 256 (N % 256 == 0) /
+ * 128 / 64.
  * op 1 (TN): C (fp32 [N][K]) = A^T . B for A [M][N], B [M][K] (bf16), split over M into slab
  * (>= dfd_vgemm_tn_slab_floats) and summed in a fixed order; N, K % 256 == 0; with G non-null also
  * G (fp32 [N]) = the column sums of A (a linear's bias gradient) from the same launch.  op 6: op 1 with

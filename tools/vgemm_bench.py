@@ -1,6 +1,6 @@
 """Time the ViT trunk's GEMM shapes (C5: 128 images x 197 tokens = 25,216 rows) on the own LDS-DMA
 kernels (k_vgemm.hip; NT products also with the 256- / 128-wide tile forced, "own256" / "own128", and
-with the fragment-pipelined K loop, "xp")
+with the fragment-pipelined K loop, "xp"; the 768-wide ones also on the 64-wide tile, "own64")
 against hipBLASLt,
 HIP events on the current stream, interleaved rounds.
 
@@ -48,6 +48,8 @@ def main():
             slab = torch.empty(max(lib.dfd_vgemm_tn_slab_floats(M, N, K), 4 * N * K), device=dev)
             args = lambda o: (st, o, P(A), P(B), P(C), None, None, None, None, M, N, K, 0, P(slab), slab.numel())  # noqa: E731
         arms = (("own", op), ("blaslt", op + 2)) + ((("own256", 4), ("own128", 5), ("xp", 0)) if op == 0 else ())
+        if op == 0 and N == 768:
+            arms += (("own64", 7),)
         times = {arm: [] for arm, _ in arms}
         for r in range(rounds + 1):
             for arm, o in arms:
