@@ -18,6 +18,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <vector>
 
@@ -57,10 +58,16 @@ struct VitLayout {
   int64_t wpe, ape, pe, xfin, mu_f, rs_f, S, total;
   // scratch
   int64_t dx, dxm, dh, dZ, dqkv, dO, dS, part, slab, dpe, bar, stotal;
+  int64_t dx2, dxm2, dZ2, dqkv2;  // bf16: the second set of the side stream's double-buffered inputs
   int64_t part_cap, slab_cap;
 };
 
 constexpr int kVitBars = 256;  // >= vgemm_tn_bar_count of every ViT-B weight gradient (3072 x 768: 72)
+// 1: the bf16 weight gradients (GEMM + split reduction) run on a second stream, overlapping the
+// data-gradient chain (vit_backward_t); 0: everything on the caller's stream (A/B builds)
+#ifndef DFD_VIT_WG_SIDE
+#define DFD_VIT_WG_SIDE 1
+#endif
 #ifndef DFD_VIT_TN_COOP
 #define DFD_VIT_TN_COOP 0  // 1: the weight gradients' split partials reduced inside the GEMM launch (measured slower, DESIGN r5)
 #endif
@@ -120,6 +127,17 @@ VitLayout vit_layout(const VitDims& d) {
   L.dO = take(es * M * D);
   L.dS = take(es * SR * SLD);
   L.dpe = take(es * M0 * D);
+  if (d.dtype == 1) {
+    L.dx2 = take(es * M * D);
+    L.dxm2 = take(es * M * D);
+    L.dZ2 = take(es * M * FF);
+    L.dqkv2 = take(es * M * D3);
+  } else {
+    L.dx2 = L.dx;
+    L.dxm2 = L.dxm;
+    L.dZ2 = L.dZ;
+    L.dqkv2 = L.dqkv;
+  }
   L.part_cap = 2LL * 1024 * FF;
   L.part = take(4 * L.part_cap);
   L.slab_cap = 16LL * FF * D;
@@ -269,6 +287,42 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
                                  w.template at<float>(L.rs_f), I, D, LN_EPS);
 }
 
+// The side stream of the bf16 weight gradients: one non-blocking stream per device, created on first
+// use and kept for the process (never destroyed: its last work is joined by every backward), with
+// the events of the fork / join points; `mu` serialises backward enqueues that share it.
+struct VitSide {
+  std::mutex mu;
+  int dev = -1;
+  hipStream_t s = nullptr;
+  hipEvent_t fork[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};  // per layer parity: the side's work of that layer
+  hipEvent_t tail = nullptr;
+};
+VitSide* vit_side() {
+  static VitSide g[64];
+  static std::mutex init_mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("vit: no device for the weight-gradient stream", __FILE__, __LINE__);
+    return nullptr;
+  }
+  VitSide& v = g[dev];
+  const std::lock_guard<std::mutex> lk(init_mu);
+  if (v.dev == dev) return &v;
+  hipEvent_t* evs[] = {&v.fork[0], &v.fork[1], &v.done[0], &v.done[1], &v.tail};
+  // the lowest priority: the data-gradient chain's workgroups dispatch first when both streams wait
+  int least = 0, greatest = 0;
+  bool ok = hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+            hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, least) == hipSuccess;
+  for (hipEvent_t* e : evs) ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    set_error("vit: weight-gradient stream / event creation failed", __FILE__, __LINE__);
+    return nullptr;
+  }
+  v.dev = dev;
+  return &v;
+}
+
 template <typename T>
 int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, char* work,
                    char* scratch, const float* dfeats, float* const* G) {
@@ -279,43 +333,84 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
   float* part = sc.template at<float>(L.part);
   float* slab = sc.template at<float>(L.slab);
   unsigned* bar = sc.template at<unsigned>(L.bar);
+  // bf16: the weight gradients (vgemm TN + its split reduction, all through the one slab) run on the
+  // side stream in enqueue order while this stream runs the data-gradient chain.  The side waits at
+  // two forks per layer (after dZ; after dqkv); the gradient inputs it reads are double-buffered by
+  // layer parity, so this stream overwrites them only two layers later, after waiting for that
+  // layer's side work (done[parity], long finished by then); one join at the end.
+  const bool side = DFD_VIT_WG_SIDE && sizeof(T) == 2;
+  VitSide* vs = nullptr;
+  std::unique_lock<std::mutex> lk;
+  if (side) {
+    vs = vit_side();
+    if (!vs) return -1;
+    lk = std::unique_lock<std::mutex>(vs->mu);
+  }
+  hipStream_t ss = side ? vs->s : s;
+  int nfork = 0;
+  auto fork = [&]() -> int {  // the side stream waits for everything enqueued on s so far
+    if (!side) return 0;
+    hipEvent_t e = vs->fork[nfork++ & 1];
+    DFD_HIP_CHECK(hipEventRecord(e, s));
+    DFD_HIP_CHECK(hipStreamWaitEvent(ss, e, 0));
+    return 0;
+  };
+  auto join = [&](hipEvent_t e) -> int {  // s waits for everything enqueued on the side so far
+    if (!side) return 0;
+    DFD_HIP_CHECK(hipEventRecord(e, ss));
+    DFD_HIP_CHECK(hipStreamWaitEvent(s, e, 0));
+    return 0;
+  };
+  auto wgd = [&](const T* dY, const T* X, int64_t Mr, int N, int K, float* dW, float* dB) -> int {
+    if (side && vgemm_tn_covers(Mr, N, K))
+      return wgrad<T>(ss, dY, X, Mr, N, K, slab, L.slab_cap, dW, dB, part, L.part_cap, bar);
+    DFD_TRY(join(vs ? vs->tail : nullptr));  // the other forms share slab / part with this stream
+    return wgrad<T>(s, dY, X, Mr, N, K, slab, L.slab_cap, dW, dB, part, L.part_cap, bar);
+  };
   DFD_HIP_CHECK(hipMemsetAsync(bar, 0, 4 * kVitBars, s));  // zero at rest from here on (group_sync)
-  T* dx = sc.at(L.dx);
-  T* dxm = sc.at(L.dxm);
+  T* const dxb[2] = {sc.at(L.dx), sc.at(L.dx2)};
+  T* const dxmb[2] = {sc.at(L.dxm), sc.at(L.dxm2)};
+  T* const dZb[2] = {sc.at(L.dZ), sc.at(L.dZ2)};
+  T* const dqkvb[2] = {sc.at(L.dqkv), sc.at(L.dqkv2)};
   T* dh = sc.at(L.dh);
-  // final norm: only the CLS rows receive gradient
-  DFD_HIP_CHECK(hipMemsetAsync(dx, 0, sizeof(T) * M * D, s));
+  // final norm: only the CLS rows receive gradient (into the last layer's input-gradient buffer)
+  T* dx0 = dxb[(d.depth - 1) & 1];
+  DFD_HIP_CHECK(hipMemsetAsync(dx0, 0, sizeof(T) * M * D, s));
   const float* const* fn = P + 4 + 12 * d.depth;
   float* const* gn = G + 4 + 12 * d.depth;
   DFD_TRY((launch_ln_bwd<T, float>(s, w.at(L.xfin), (int64_t)nt * D, dfeats, D, fn[0], w.template at<float>(L.mu_f),
-                                  w.template at<float>(L.rs_f), nullptr, dx, I, D, part, L.part_cap, gn[0], gn[1],
+                                  w.template at<float>(L.rs_f), nullptr, dx0, I, D, part, L.part_cap, gn[0], gn[1],
                                   false)));
   Pro none{};
   for (int l = d.depth - 1; l >= 0; --l) {
     const float* const* q = P + 4 + 12 * l;
     float* const* g = G + 4 + 12 * l;
     const auto& b = L.blk[l];
+    const int par = l & 1;
     T* qkv = w.at(b.qkv);
-    T* dZ = sc.at(L.dZ);
-    T* dqkv = sc.at(L.dqkv);
+    T* dx = dxb[par];        // this layer's output gradient (side: fc2's weight gradient reads it)
+    T* dxo = dxb[par ^ 1];   // its input gradient, the next layer down's dx
+    T* dZ = dZb[par];
+    T* dxm = dxmb[par];
+    T* dqkv = dqkvb[par];
     T* dO = sc.at(L.dO);
     T* dS = sc.at(L.dS);
     // ---- MLP: dZ = (dx W2) * gelu'(Z); dW2 = dx^T gelu(Z); dh2 = dZ W1 ----
     DFD_TRY(lin<T>(s, dx, w.at(b.w2T), dZ, nullptr, nullptr, M, FF, D, VG_DGELU, w.at(b.Z)));
+    DFD_TRY(fork());
     if constexpr (sizeof(T) == 2) {  // G = gelu(Z) kept by the forward
-      DFD_TRY(wgrad<T>(s, dx, w.at(b.G), M, D, FF, slab, L.slab_cap, g[10], g[11], part, L.part_cap, bar));
+      DFD_TRY(wgd(dx, w.at(b.G), M, D, FF, g[10], g[11]));
     } else {
       DFD_TRY(launch_pw_wgrad<T>(s, dx, w.at(b.Z), M, D, FF, PRO_GELU, none, slab, L.slab_cap, g[10], false));
       DFD_TRY(launch_colsum<T>(s, dx, M, D, part, L.part_cap, g[11], false));
     }
+    DFD_TRY(wgd(dZ, w.at(b.h2), M, FF, D, g[8], g[9]));
     DFD_TRY(lin<T>(s, dZ, w.at(b.w1T), dh, nullptr, nullptr, M, D, FF));
-    DFD_TRY(wgrad<T>(s, dZ, w.at(b.h2), M, FF, D, slab, L.slab_cap, g[8], g[9], part, L.part_cap, bar));
     // LN2: dxm = dx + LN2'(dh2)
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.xm), D, dh, D, q[6], w.template at<float>(b.mu2),
                                 w.template at<float>(b.rs2), dx, dxm, M, D, part, L.part_cap, g[6], g[7], false)));
     // ---- attention projection ----
     DFD_TRY(lin<T>(s, dxm, w.at(b.wpT), dO, nullptr, nullptr, M, D, D));
-    DFD_TRY(wgrad<T>(s, dxm, w.at(b.O), M, D, D, slab, L.slab_cap, g[4], g[5], part, L.part_cap, bar));
     // ---- attention core: dP = dO v^T ; dS = scale P (dP - rowdot) ; dq = dS k ; dk = dS^T q ; dv = P^T dO
     if constexpr (sizeof(T) == 2) {  // fused (k_attn.hip): recomputes P from the saved log-sum-exp
       AttnArgs at = attn_args(I, nt, qkv, w.at(b.O), w.template at<float>(b.P));
@@ -335,16 +430,23 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
       DFD_TRY(launch_bgemm<T>(s, true, false, BH, nt, DH, nt, 1.f, w.at(b.P), op_score(), dO, op_tok(D),
                               dqkv + 2 * D, op_tok(D3)));
     }
+    DFD_TRY(fork());
+    DFD_TRY(wgd(dxm, w.at(b.O), M, D, D, g[4], g[5]));
+    DFD_TRY(wgd(dqkv, w.at(b.h1), M, D3, D, g[2], g[3]));
+    if (side) DFD_HIP_CHECK(hipEventRecord(vs->done[par], ss));
     // ---- qkv projection and LN1: dx_l = dxm + LN1'(dqkv Wqkv) ----
     DFD_TRY(lin<T>(s, dqkv, w.at(b.wqkvT), dh, nullptr, nullptr, M, D, D3));
-    DFD_TRY(wgrad<T>(s, dqkv, w.at(b.h1), M, D3, D, slab, L.slab_cap, g[2], g[3], part, L.part_cap, bar));
+    // dxo was the layer above's dx, read by that layer's side work: wait for it (long done)
+    if (side && l + 1 < d.depth) DFD_HIP_CHECK(hipStreamWaitEvent(s, vs->done[par ^ 1], 0));
     DFD_TRY((launch_ln_bwd<T, T>(s, w.at(b.x), D, dh, D, q[0], w.template at<float>(b.mu1), w.template at<float>(b.rs1),
-                                dxm, dx, M, D, part, L.part_cap, g[0], g[1], false)));
+                                dxm, dxo, M, D, part, L.part_cap, g[0], g[1], false)));
   }
   // tokens: dcls, dpos, patch rows -> patch-embedding weight / bias
   T* dpe = sc.at(L.dpe);
-  DFD_TRY(launch_tokens_bwd<T>(s, dx, I, nt, D, dpe, G[1], G[0]));
-  return wgrad<T>(s, dpe, w.at(L.ape), M0, D, D, slab, L.slab_cap, G[2], G[3], part, L.part_cap, bar);
+  DFD_TRY(launch_tokens_bwd<T>(s, dxb[1], I, nt, D, dpe, G[1], G[0]));
+  DFD_TRY(fork());
+  DFD_TRY(wgd(dpe, w.at(L.ape), M0, D, D, G[2], G[3]));
+  return join(vs ? vs->tail : nullptr);
 }
 
 // ------------------------------------------------------------------------------------------
