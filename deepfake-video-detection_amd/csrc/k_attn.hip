@@ -296,6 +296,125 @@ __global__ __launch_bounds__(1024) void attn_bwd_q_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- backward, one launch
+// The two kernels above as two phases of one workgroup: Q, dO, O (row dots) and L are read once for
+// the head.  Phase A (dK, dV, wave = 16 keys) runs on the Q / dO images; each wave then takes its 16
+// queries' Q and dO operand rows from those images, and the same LDS is refilled with K and V for
+// phase B (dQ, wave = 16 queries) -- K and V come back from L2 (the workgroup read them moments
+// before).  Same products in the same order as the two-kernel form: bit-identical.
+template <int NB>
+__global__ __launch_bounds__(1024) void attn_bwd_kernel(AttnArgs a) {
+  constexpr int NP = 16 * NB;
+  __shared__ __attribute__((aligned(16))) bf16 Xs[NP * RS];  // Q (phase A), K (phase B)
+  __shared__ __attribute__((aligned(16))) bf16 Ys[NP * RS];  // dO (phase A), V (phase B)
+  __shared__ float Ls[NP], Dq[NP];
+  const int bh = blockIdx.x, img = bh / a.heads, h = bh - img * a.heads;
+  const int nt = a.nt, lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
+  const int64_t row0 = (int64_t)img * nt;
+  const bf16* base = a.qkv + row0 * a.ldq + h * AD;
+  const bf16* dob = a.dO + row0 * a.lddo + h * AD;
+  load_head<NP>(base, a.ldq, nt, Xs, nullptr);
+  load_head<NP>(dob, a.lddo, nt, Ys, nullptr);
+  load_rowdot<NP>(dob, a.lddo, a.O + row0 * a.ldo + h * AD, a.ldo, nt, Dq);
+  for (int t = threadIdx.x; t < NP; t += blockDim.x) Ls[t] = t < nt ? a.lse[(int64_t)bh * nt + t] : 0.f;
+  __syncthreads();
+  const bool active = wave * 16 < nt;  // the waves past the last token only join the barriers
+  bf16* rowp0 = a.dqkv + row0 * a.lddq + h * AD;
+  if (active) {  // ---- phase A: dK, dV of keys wave * 16 + (lane & 15)
+    const int key = wave * 16 + (lane & 15);
+    bf16x8_t kb[2], vb[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bool ok = key < nt;
+      kb[kk] = ok ? ld16(base + (int64_t)key * a.ldq + a.koff + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      vb[kk] = ok ? ld16(base + (int64_t)key * a.ldq + a.voff + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    f32x4_t dv[4], dk[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db) dv[db] = dk[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < NB / 2; ++c) {
+      float pv[2][4], sv[2][4];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int qb = 2 * c + hf;
+        f32x4_t s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          s = mma(ld16(Xs + (qb * 16 + (lane & 15)) * RS + 32 * kk + 8 * g), kb[kk], s);
+          dp = mma(ld16(Ys + (qb * 16 + (lane & 15)) * RS + 32 * kk + 8 * g), vb[kk], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // rows q = 16 qb + 4g + r
+          const int qq = qb * 16 + 4 * g + r;
+          const float p = qq < nt ? __expf(s[r] * a.scale - Ls[qq]) : 0.f;
+          pv[hf][r] = p;
+          sv[hf][r] = p * (dp[r] - Dq[qq]);
+        }
+      }
+      const bf16x8_t pb = pack8(pv), sb = pack8(sv);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        dv[db] = mma(tr8(Ys, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), pb, dv[db]);
+        dk[db] = mma(tr8(Xs, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), sb, dk[db]);
+      }
+    }
+    if (key < nt) {
+      bf16* rowp = rowp0 + (int64_t)key * a.lddq;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        st4(rowp + a.koff + db * 16 + 4 * g, dk[db], a.scale);
+        st4(rowp + a.voff + db * 16 + 4 * g, dv[db], 1.f);
+      }
+    }
+  }
+  // this wave's queries for phase B, from the images before they are refilled (rows >= nt are zero)
+  const int q = wave * 16 + (lane & 15);
+  bf16x8_t qb[2], ob[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    qb[kk] = ld16(Xs + q * RS + 32 * kk + 8 * g);
+    ob[kk] = ld16(Ys + q * RS + 32 * kk + 8 * g);
+  }
+  __syncthreads();
+  load_head<NP>(base + a.koff, a.ldq, nt, Xs, nullptr);
+  load_head<NP>(base + a.voff, a.ldq, nt, Ys, nullptr);
+  __syncthreads();
+  if (!active) return;
+  // ---- phase B: dQ of queries q
+  const bool qok = q < nt;
+  const float L = Ls[q], Dv = Dq[q];
+  f32x4_t dq[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) dq[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < NB / 2; ++c) {
+    float sv[2][4];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int nb = 2 * c + hf;
+      f32x4_t s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        s = mma(ld16(Xs + (nb * 16 + (lane & 15)) * RS + 32 * kk + 8 * g), qb[kk], s);
+        dp = mma(ld16(Ys + (nb * 16 + (lane & 15)) * RS + 32 * kk + 8 * g), ob[kk], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // rows key = 16 nb + 4g + r
+        const int kk2 = nb * 16 + 4 * g + r;
+        const float p = (kk2 < nt && qok) ? __expf(s[r] * a.scale - L) : 0.f;
+        sv[hf][r] = p * (dp[r] - Dv);
+      }
+    }
+    const bf16x8_t sb = pack8(sv);
+#pragma unroll
+    for (int db = 0; db < 4; ++db) dq[db] = mma(tr8(Xs, 32 * c + 4 * g, 32 * c + 16 + 4 * g, db * 16), sb, dq[db]);
+  }
+  if (qok) {
+    bf16* rowp = rowp0 + (int64_t)q * a.lddq;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) st4(rowp + db * 16 + 4 * g, dq[db], a.scale);
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 static int attn_nb(int nt) { return ((nt + 31) / 32) * 2; }  // 16-token blocks, an even count
 
@@ -319,9 +438,15 @@ static int attn_go(hipStream_t s, const AttnArgs& a) {
 template <int N> struct FwdK { static constexpr auto fn = attn_fwd_kernel<N>; };
 template <int N> struct KvK { static constexpr auto fn = attn_bwd_kv_kernel<N>; };
 template <int N> struct QK { static constexpr auto fn = attn_bwd_q_kernel<N>; };
+template <int N> struct BwdK { static constexpr auto fn = attn_bwd_kernel<N>; };
 
 int launch_attn_fwd(hipStream_t s, const AttnArgs& a) { return attn_go<FwdK>(s, a); }
+// 1: the one-launch backward (attn_bwd_kernel); 0: the key/value and query kernels (A/B builds)
+#ifndef DFD_ATTN_BWD_FUSED
+#define DFD_ATTN_BWD_FUSED 1
+#endif
 int launch_attn_bwd(hipStream_t s, const AttnArgs& a) {
+  if (DFD_ATTN_BWD_FUSED) return attn_go<BwdK>(s, a);
   DFD_TRY(attn_go<KvK>(s, a));
   return attn_go<QK>(s, a);
 }
