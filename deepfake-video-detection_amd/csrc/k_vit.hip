@@ -472,9 +472,61 @@ __global__ __launch_bounds__(256) void wcast_kernel(VitCast cs) {
   }
 }
 
+// the same on 64 x 64 tiles with 16-B source loads and 8-B stores in both layouts (16-bit T; rows,
+// cols % 64: every ViT-B weight): a thread moves 4 consecutive elements per access
+template <typename T>
+__global__ __launch_bounds__(256) void wcast64_kernel(VitCast cs) {
+  const VitCastSeg sg = cs.seg[blockIdx.z];
+  const int tr = sg.cols / 64;
+  if ((int)blockIdx.x >= tr * (sg.rows / 64)) return;
+  const int ty = blockIdx.x / tr, tx = blockIdx.x - (blockIdx.x / tr) * tr;
+  __shared__ float tile[64][65];
+  const int l4 = threadIdx.x & 15, ly = threadIdx.x >> 4;
+  T* out = reinterpret_cast<T*>(sg.dst);
+  T* out_t = reinterpret_cast<T*>(sg.dst_t);
+  float4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // all four loads in flight first
+    const int r = ty * 64 + ly + 16 * i, c = tx * 64 + 4 * l4;
+    v[i] = *reinterpret_cast<const float4*>(sg.src + (int64_t)r * sg.cols + c);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rl = ly + 16 * i, r = ty * 64 + rl, c = tx * 64 + 4 * l4;
+    if (out)
+      *reinterpret_cast<uint2*>(out + (int64_t)r * sg.cols + c) =
+          make_uint2(Tr<T>::pack2(v[i].x, v[i].y), Tr<T>::pack2(v[i].z, v[i].w));
+    tile[rl][4 * l4] = v[i].x;
+    tile[rl][4 * l4 + 1] = v[i].y;
+    tile[rl][4 * l4 + 2] = v[i].z;
+    tile[rl][4 * l4 + 3] = v[i].w;
+  }
+  if (!out_t) return;  // uniform per segment
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // out_t[c][r .. r + 3]
+    const int cl = ly + 16 * i, c = tx * 64 + cl, r = ty * 64 + 4 * l4;
+    *reinterpret_cast<uint2*>(out_t + (int64_t)c * sg.rows + r) =
+        make_uint2(Tr<T>::pack2(tile[4 * l4][cl], tile[4 * l4 + 1][cl]), Tr<T>::pack2(tile[4 * l4 + 2][cl], tile[4 * l4 + 3][cl]));
+  }
+}
+
 template <typename T>
 int launch_wcast(hipStream_t s, const VitCast& cs, int nseg) {
   if (nseg <= 0) return 0;
+  bool t64 = true;
+  int tiles64 = 0;
+  for (int i = 0; i < nseg; ++i) {
+    t64 = t64 && cs.seg[i].rows % 64 == 0 && cs.seg[i].cols % 64 == 0;
+    tiles64 = std::max(tiles64, (cs.seg[i].rows / 64) * (cs.seg[i].cols / 64));
+  }
+  if constexpr (sizeof(T) == 2) {  // 16-bit storage (the fp32 parity mode keeps the 32 x 32 form)
+    if (t64) {
+      hipLaunchKernelGGL((wcast64_kernel<T>), dim3((unsigned)tiles64, 1, (unsigned)nseg), dim3(256), 0, s, cs);
+      DFD_HIP_CHECK(hipGetLastError());
+      return 0;
+    }
+  }
   int tiles = 0;
   for (int i = 0; i < nseg; ++i) tiles = std::max(tiles, cdiv(cs.seg[i].rows, 32) * cdiv(cs.seg[i].cols, 32));
   const dim3 grid((unsigned)tiles, 1, (unsigned)nseg);
