@@ -63,10 +63,11 @@ struct VitLayout {
 };
 
 constexpr int kVitBars = 256;  // >= vgemm_tn_bar_count of every ViT-B weight gradient (3072 x 768: 72)
-// 1: the bf16 weight gradients (GEMM + split reduction) run on a second stream, overlapping the
-// data-gradient chain (vit_backward_t); 0: everything on the caller's stream (A/B builds)
-#ifndef DFD_VIT_WG_SIDE
-#define DFD_VIT_WG_SIDE 1
+// 1: bf16 work off the critical chain runs on a second stream -- the forward's weight casts
+// (vit_forward_t) and the backward's weight gradients, GEMM + split reduction (vit_backward_t);
+// 0: everything on the caller's stream (A/B builds)
+#ifndef DFD_VIT_SIDE
+#define DFD_VIT_SIDE 1
 #endif
 #ifndef DFD_VIT_TN_COOP
 #define DFD_VIT_TN_COOP 0  // 1: the weight gradients' split partials reduced inside the GEMM launch (measured slower, DESIGN r5)
@@ -158,11 +159,60 @@ struct Ws {
   U* at(int64_t off) const { return reinterpret_cast<U*>(base + off); }
 };
 
+// The bf16 side stream (the forward's weight casts, the backward's weight gradients): one non-blocking
+// stream per device, created on first use and kept for the process (never destroyed: every forward /
+// backward joins its last work), with the events of the fork / join points; `mu` serialises the
+// enqueues that share it.
+struct VitSide {
+  std::mutex mu;
+  int dev = -1;
+  hipStream_t s = nullptr;
+  hipEvent_t fork[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};  // per layer parity: the side's work of that layer
+  hipEvent_t tail = nullptr;
+  hipEvent_t cast[13] = {};  // forward: the patch embedding's (0) and layer l's (l + 1) weight casts
+};
+VitSide* vit_side() {
+  static VitSide g[64];
+  static std::mutex init_mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("vit: no device for the side stream", __FILE__, __LINE__);
+    return nullptr;
+  }
+  VitSide& v = g[dev];
+  const std::lock_guard<std::mutex> lk(init_mu);
+  if (v.dev == dev) return &v;
+  std::vector<hipEvent_t*> evs = {&v.fork[0], &v.fork[1], &v.done[0], &v.done[1], &v.tail};
+  for (hipEvent_t& e : v.cast) evs.push_back(&e);
+  // the lowest priority: the data-gradient chain's workgroups dispatch first when both streams wait
+  int least = 0, greatest = 0;
+  bool ok = hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+            hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, least) == hipSuccess;
+  for (hipEvent_t* e : evs) ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    set_error("vit: side stream / event creation failed", __FILE__, __LINE__);
+    return nullptr;
+  }
+  v.dev = dev;
+  return &v;
+}
+
+// with a side stream the casts run there, after everything enqueued on s so far, and cast[i] marks the
+// patch embedding's (i = 0) and layer i - 1's weights ready
 template <typename T>
-int cast_weights(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, const Ws<T>& w) {
+int cast_weights(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, const Ws<T>& w,
+                 VitSide* vs = nullptr) {
+  hipStream_t cs = s;
+  if (vs) {
+    cs = vs->s;
+    DFD_HIP_CHECK(hipEventRecord(vs->fork[0], s));
+    DFD_HIP_CHECK(hipStreamWaitEvent(cs, vs->fork[0], 0));
+  }
   VitCast pe{};
   pe.seg[0] = {P[2], w.at(L.wpe), nullptr, D, D};
-  DFD_TRY(launch_wcast<T>(s, pe, 1));
+  DFD_TRY(launch_wcast<T>(cs, pe, 1));
+  if (vs) DFD_HIP_CHECK(hipEventRecord(vs->cast[0], cs));
   for (int l = 0; l < d.depth; ++l) {
     const float* const* q = P + 4 + 12 * l;
     const auto& b = L.blk[l];
@@ -171,7 +221,8 @@ int cast_weights(hipStream_t s, const VitDims& d, const VitLayout& L, const floa
     c.seg[1] = {q[4], w.at(b.wp), w.at(b.wpT), D, D};
     c.seg[2] = {q[8], w.at(b.w1), w.at(b.w1T), FF, D};
     c.seg[3] = {q[10], w.at(b.w2), w.at(b.w2T), D, FF};
-    DFD_TRY(launch_wcast<T>(s, c, 4));
+    DFD_TRY(launch_wcast<T>(cs, c, 4));
+    if (vs) DFD_HIP_CHECK(hipEventRecord(vs->cast[l + 1], cs));
   }
   return 0;
 }
@@ -242,9 +293,24 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
   const Ws<T> w{work};
   const int nt = d.ntok(), I = d.images, BH = I * HEADS;
   const int64_t M = d.rows(), M0 = (int64_t)I * (nt - 1), SR = (int64_t)BH * nt;
-  DFD_TRY(cast_weights<T>(s, d, L, P, w));
+  // bf16: the weight casts run ahead on the side stream; each layer waits for its own (the last wait
+  // joins the side stream's work)
+  const bool side = DFD_VIT_SIDE && sizeof(T) == 2;
+  VitSide* vs = nullptr;
+  std::unique_lock<std::mutex> lk;
+  if (side) {
+    vs = vit_side();
+    if (!vs) return -1;
+    lk = std::unique_lock<std::mutex>(vs->mu);
+  }
+  auto ready = [&](int i) -> int {
+    if (vs) DFD_HIP_CHECK(hipStreamWaitEvent(s, vs->cast[i], 0));
+    return 0;
+  };
+  DFD_TRY(cast_weights<T>(s, d, L, P, w, vs));
   // patch embedding (Conv2d 16x16/16 as a GEMM over gathered patches) + cls + pos
   DFD_TRY(launch_patch_gather<T>(s, x, im, I, w.at(L.ape)));
+  DFD_TRY(ready(0));
   DFD_TRY(lin<T>(s, w.at(L.ape), w.at(L.wpe), w.at(L.pe), nullptr, P[3], M0, D, D));
   DFD_TRY(launch_tokens_fwd<T>(s, w.at(L.pe), P[0], P[1], I, nt, D, w.at(L.blk[0].x)));
   for (int l = 0; l < d.depth; ++l) {
@@ -253,6 +319,7 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
     T* xnext = l + 1 < d.depth ? w.at(L.blk[l + 1].x) : w.at(L.xfin);
     DFD_TRY((launch_ln_fwd<T, T>(s, w.at(b.x), D, q[0], q[1], w.at(b.h1), D, w.template at<float>(b.mu1),
                                 w.template at<float>(b.rs1), M, D, LN_EPS)));
+    DFD_TRY(ready(l + 1));
     DFD_TRY(lin<T>(s, w.at(b.h1), w.at(b.wqkv), w.at(b.qkv), nullptr, q[3], M, D3, D));
     T* qkv = w.at(b.qkv);
     // S = (q * 64^-0.5) k^T ; P = softmax(S) ; O = P v
@@ -287,42 +354,6 @@ int vit_forward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const flo
                                  w.template at<float>(L.rs_f), I, D, LN_EPS);
 }
 
-// The side stream of the bf16 weight gradients: one non-blocking stream per device, created on first
-// use and kept for the process (never destroyed: its last work is joined by every backward), with
-// the events of the fork / join points; `mu` serialises backward enqueues that share it.
-struct VitSide {
-  std::mutex mu;
-  int dev = -1;
-  hipStream_t s = nullptr;
-  hipEvent_t fork[2] = {nullptr, nullptr};
-  hipEvent_t done[2] = {nullptr, nullptr};  // per layer parity: the side's work of that layer
-  hipEvent_t tail = nullptr;
-};
-VitSide* vit_side() {
-  static VitSide g[64];
-  static std::mutex init_mu;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-    set_error("vit: no device for the weight-gradient stream", __FILE__, __LINE__);
-    return nullptr;
-  }
-  VitSide& v = g[dev];
-  const std::lock_guard<std::mutex> lk(init_mu);
-  if (v.dev == dev) return &v;
-  hipEvent_t* evs[] = {&v.fork[0], &v.fork[1], &v.done[0], &v.done[1], &v.tail};
-  // the lowest priority: the data-gradient chain's workgroups dispatch first when both streams wait
-  int least = 0, greatest = 0;
-  bool ok = hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
-            hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, least) == hipSuccess;
-  for (hipEvent_t* e : evs) ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
-  if (!ok) {
-    set_error("vit: weight-gradient stream / event creation failed", __FILE__, __LINE__);
-    return nullptr;
-  }
-  v.dev = dev;
-  return &v;
-}
-
 template <typename T>
 int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const float* const* P, char* work,
                    char* scratch, const float* dfeats, float* const* G) {
@@ -338,7 +369,7 @@ int vit_backward_t(hipStream_t s, const VitDims& d, const VitLayout& L, const fl
   // two forks per layer (after dZ; after dqkv); the gradient inputs it reads are double-buffered by
   // layer parity, so this stream overwrites them only two layers later, after waiting for that
   // layer's side work (done[parity], long finished by then); one join at the end.
-  const bool side = DFD_VIT_WG_SIDE && sizeof(T) == 2;
+  const bool side = DFD_VIT_SIDE && sizeof(T) == 2;
   VitSide* vs = nullptr;
   std::unique_lock<std::mutex> lk;
   if (side) {
