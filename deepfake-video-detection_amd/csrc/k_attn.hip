@@ -75,6 +75,54 @@ __device__ __forceinline__ void load_head(const bf16* __restrict__ src, int64_t 
   }
 }
 
+// Two token-major head images at once (rows >= nt zero), for a workgroup of 64 NB threads: each thread
+// moves 16-B chunks t and t + 64 NB of both images (NP * 8 = 128 NB chunks per image), every global
+// load issued before the first LDS store
+template <int NB>
+__device__ __forceinline__ void load_heads2(const bf16* __restrict__ sa, int64_t lda, const bf16* __restrict__ sb,
+                                            int64_t ldb, int nt, bf16* ra, bf16* rb) {
+  uint4 va[2], vb[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + k * 64 * NB, t = i >> 3, c8 = (i & 7) * 8;
+    va[k] = vb[k] = make_uint4(0, 0, 0, 0);
+    if (t < nt) {
+      va[k] = *reinterpret_cast<const uint4*>(sa + (int64_t)t * lda + c8);
+      vb[k] = *reinterpret_cast<const uint4*>(sb + (int64_t)t * ldb + c8);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + k * 64 * NB, t = i >> 3, c8 = (i & 7) * 8;
+    *reinterpret_cast<uint4*>(ra + t * RS + c8) = va[k];
+    *reinterpret_cast<uint4*>(rb + t * RS + c8) = vb[k];
+  }
+}
+
+// D[t] = sum_d dO[t][d] * O[t][d] with four threads per token (16 columns each, the four partial sums
+// added by lane shuffles in a fixed order), 64 NB threads = 4 NP tokens' worth (0 beyond nt)
+template <int NB>
+__device__ __forceinline__ void load_rowdot4(const bf16* __restrict__ dO, int64_t lddo, const bf16* __restrict__ O,
+                                             int64_t ldo, int nt, float* out) {
+  const int t = threadIdx.x >> 2, c0 = (threadIdx.x & 3) * 16;
+  float acc = 0.f;
+  if (t < nt) {
+    float x[2][8], y[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ld8(dO + (int64_t)t * lddo + c0 + 8 * h, x[h]);
+      ld8(O + (int64_t)t * ldo + c0 + 8 * h, y[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += x[h][j] * y[h][j];
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  if ((threadIdx.x & 3) == 0) out[t] = acc;
+}
+
 // D[t] = sum_d dO[t][d] * O[t][d] for every token of the head (0 beyond nt)
 template <int NP>
 __device__ __forceinline__ void load_rowdot(const bf16* __restrict__ dO, int64_t lddo, const bf16* __restrict__ O,
@@ -107,15 +155,14 @@ __global__ __launch_bounds__(1024) void attn_fwd_kernel(AttnArgs a) {
   const int nt = a.nt, lane = threadIdx.x & 63, g = lane >> 4, wave = threadIdx.x >> 6;
   const int64_t row0 = (int64_t)img * nt;
   const bf16* base = a.qkv + row0 * a.ldq + h * AD;
-  load_head<NP>(base + a.koff, a.ldq, nt, Ks, nullptr);
-  load_head<NP>(base + a.voff, a.ldq, nt, Vs, nullptr);
-  __syncthreads();
   const int q = wave * 16 + (lane & 15);  // this lane's query (MFMA column)
-  if (wave * 16 >= nt) return;
-  bf16x8_t qb[2];
+  bf16x8_t qb[2];  // issued first: in flight with the K / V image loads
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk)
     qb[kk] = q < nt ? ld16(base + (int64_t)q * a.ldq + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  load_heads2<NB>(base + a.koff, a.ldq, base + a.voff, a.ldq, nt, Ks, Vs);
+  __syncthreads();
+  if (wave * 16 >= nt) return;
   // S^T blocks: rows key = 16 nb + 4g + r, column q
   f32x4_t st[NB];
 #pragma unroll
@@ -313,22 +360,21 @@ __global__ __launch_bounds__(1024) void attn_bwd_kernel(AttnArgs a) {
   const int64_t row0 = (int64_t)img * nt;
   const bf16* base = a.qkv + row0 * a.ldq + h * AD;
   const bf16* dob = a.dO + row0 * a.lddo + h * AD;
-  load_head<NP>(base, a.ldq, nt, Xs, nullptr);
-  load_head<NP>(dob, a.lddo, nt, Ys, nullptr);
-  load_rowdot<NP>(dob, a.lddo, a.O + row0 * a.ldo + h * AD, a.ldo, nt, Dq);
+  const int key = wave * 16 + (lane & 15);  // phase A's MFMA column
+  bf16x8_t kb[2], vb[2];  // issued first: in flight with the image loads
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    const bool ok = key < nt;
+    kb[kk] = ok ? ld16(base + (int64_t)key * a.ldq + a.koff + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    vb[kk] = ok ? ld16(base + (int64_t)key * a.ldq + a.voff + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
   for (int t = threadIdx.x; t < NP; t += blockDim.x) Ls[t] = t < nt ? a.lse[(int64_t)bh * nt + t] : 0.f;
+  load_heads2<NB>(base, a.ldq, dob, a.lddo, nt, Xs, Ys);
+  load_rowdot4<NB>(dob, a.lddo, a.O + row0 * a.ldo + h * AD, a.ldo, nt, Dq);
   __syncthreads();
   const bool active = wave * 16 < nt;  // the waves past the last token only join the barriers
   bf16* rowp0 = a.dqkv + row0 * a.lddq + h * AD;
   if (active) {  // ---- phase A: dK, dV of keys wave * 16 + (lane & 15)
-    const int key = wave * 16 + (lane & 15);
-    bf16x8_t kb[2], vb[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bool ok = key < nt;
-      kb[kk] = ok ? ld16(base + (int64_t)key * a.ldq + a.koff + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-      vb[kk] = ok ? ld16(base + (int64_t)key * a.ldq + a.voff + 32 * kk + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    }
     f32x4_t dv[4], dk[4];
 #pragma unroll
     for (int db = 0; db < 4; ++db) dv[db] = dk[db] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -376,8 +422,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_kernel(AttnArgs a) {
     ob[kk] = ld16(Ys + q * RS + 32 * kk + 8 * g);
   }
   __syncthreads();
-  load_head<NP>(base + a.koff, a.ldq, nt, Xs, nullptr);
-  load_head<NP>(base + a.voff, a.ldq, nt, Ys, nullptr);
+  load_heads2<NB>(base + a.koff, a.ldq, base + a.voff, a.ldq, nt, Xs, Ys);
   __syncthreads();
   if (!active) return;
   // ---- phase B: dQ of queries q
