@@ -113,7 +113,12 @@ __device__ __forceinline__ void lds_ld8(const T* p, float (&v)[8]) { ld8(p, v); 
 // k_rn16.hip): bid / nblk are the workgroup's index and count in its grid, the LDS arrays the
 // caller's (st_*: STATS only, pro_lds: BN prologues only).  GA = 1: A is not a dense row-major
 // matrix but the implicit-GEMM gather of a convolution (ConvGather, gemm_body.h), one tap per k-step.
-template <typename T, int MODE, bool STATS, int EPI, int BM, int BN, int WN, int D, int BK, int GA = 0>
+// STATS = 1: per-column (sum, sum of squares) of the outputs, one partial row per workgroup;
+// STATS = 2: per wave-row group (the BM / WM consecutive rows of one wave row of a tile) the column
+// sum and the sum of squared deviations from that group's own column mean: centred partials of
+// consecutive BM / WM-row groups, stats row mt * WM + wm (launch_bn_finalize chan_rows = BM / WM;
+// empty groups past M write nothing).
+template <typename T, int MODE, int STATS, int EPI, int BM, int BN, int WN, int D, int BK, int GA = 0>
 __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* __restrict__ B, T* __restrict__ C,
                                              const T* __restrict__ R, const float* __restrict__ bias,
                                              const T* __restrict__ Z, int64_t M, int N, int K, const Pro& pro,
@@ -140,7 +145,7 @@ __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* _
   const int n0 = nt * BN;
   const int nvalid = min(BN, N - n0);
   const int nk = (K + GBK - 1) / GBK;
-  if constexpr (STATS) {
+  if constexpr (STATS == 1) {
     for (int i = tid; i < BN; i += 256) { st_sum[i] = 0.f; st_sq[i] = 0.f; }
   }
 
@@ -314,12 +319,12 @@ __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* _
             const int row = rbase + r_ * 16 + 4 * (lane >> 4) + r;
             const float v = Tr<T>::round(acc[r_][cb][r] + bcol);
             Cs[row * G::CS + col] = Tr<T>::from_f(v);
-            if constexpr (STATS) {
+            if constexpr (STATS != 0) {
               if (m0 + row < M) { s += v; q += v * v; }
             }
           }
         }
-        if constexpr (STATS) {
+        if constexpr (STATS == 1) {
           s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
           q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
           if (lane < 16) {
@@ -327,10 +332,32 @@ __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* _
             st_part[(wm * 2 + 1) * BN + col] = q;
           }
         }
+        if constexpr (STATS == 2) {  // this wave's rows: sum, then squared deviations from their mean
+          s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+          const int64_t left = M - (m0 + rbase);
+          const int nrow = left < BM / WM ? (int)left : BM / WM;
+          const float mean = nrow > 0 ? s / (float)nrow : 0.f;
+          float m2 = 0.f;
+#pragma unroll
+          for (int r_ = 0; r_ < RB; ++r_)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = rbase + r_ * 16 + 4 * (lane >> 4) + r;
+              const float dv = Tr<T>::round(acc[r_][cb][r] + bcol) - mean;
+              if (m0 + row < M) m2 += dv * dv;
+            }
+          m2 += __shfl_xor(m2, 16, 64);
+          m2 += __shfl_xor(m2, 32, 64);
+          if (lane < 16 && nrow > 0 && col < nvalid) {
+            const int64_t srow = (m0 / BM) * WM + wm;
+            stats[(srow * 2 + 0) * N + n0 + col] = s;
+            stats[(srow * 2 + 1) * N + n0 + col] = m2;
+          }
+        }
       }
     }
     lds_barrier();
-    if constexpr (STATS) {
+    if constexpr (STATS == 1) {
       // wave rows in order: bit-reproducible BN statistics
       for (int i = tid; i < nvalid; i += 256) {
         float a = st_part[0 * BN + i], b = st_part[1 * BN + i];
@@ -363,7 +390,7 @@ __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* _
     }
     lds_barrier();
   }
-  if constexpr (STATS) {
+  if constexpr (STATS == 1) {
     for (int i = tid; i < nvalid; i += 256) {
       stats[(mg * 2 + 0) * N + n0 + i] = st_sum[i];
       stats[(mg * 2 + 1) * N + n0 + i] = st_sq[i];

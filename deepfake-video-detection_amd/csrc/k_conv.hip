@@ -11,8 +11,9 @@
 // SURVEY F10); the forward epilogue writes per-tile BatchNorm partial rows (sum, sum of squares).
 // BatchNorm+ReLU+MaxPool(3, 2, 1) is one fused kernel (argmax kept for backward, first maximum
 // in scan order like PyTorch's max_pool2d), BatchNorm+ReLU+global-average-pool another.
-#include "kernels.h"
 #include "cnnlstm.h"
+#include "gemm_body.h"
+#include "kernels.h"
 
 namespace dfd {
 
@@ -487,6 +488,109 @@ __global__ void bn_relu_gap_bwd_kernel(const float* __restrict__ dfeat, const fl
 
 static int ew(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, 256), 4096)); }
 
+// ------------------------------------------------------------------ wide-vector tile loops
+// The stride-1 KxK layers with Cin, Cout % 64 (CNNLSTMHybrid's conv 2..4: 5x5 64->128, 3x3 128->256,
+// 3x3 256->512 over dense NHWC maps) run the EfficientNet-B0 tile loops of gemm_body.h in their fp32
+// form (v_mfma_f32_16x16x4f32, exact fp32 products) with the implicit-GEMM gather ConvGather: one tap
+// per 32-deep k-step, whole 32-B channel vectors per load instead of the per-element gathers above,
+// 128 x 128 / 128 x 64 tiles of two wave rows.  The forward's BN partials are centred per wave row
+// (STATS = 2: 64 consecutive rows each, the same (sum, M2) rows conv_gemm's epilogue writes).
+constexpr int CG32_BK = 32;
+template <int EPI, int BM, int BN, int WN, int OCC>
+__global__ __launch_bounds__(256, OCC) void cg32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wf,
+                                                          const float* __restrict__ bias, float* __restrict__ y,
+                                                          int64_t M, int N, int K, float* __restrict__ stats,
+                                                          int64_t tiles_m, int ntn, ConvGather cg) {
+  using G = GemmCfg<float, BM, BN, WN, 2, CG32_BK>;
+  static_assert(BM / G::WM == kConvStatRows, "BN partial rows of conv_forward");
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  __shared__ float st_part[G::WM][2][BN];
+  pw_gemm_body<float, PRO_NONE, 2, EPI, BM, BN, WN, 2, CG32_BK, 1>(
+      x, wf, y, nullptr, bias, nullptr, M, N, K, Pro{}, stats, tiles_m, ntn, (int)blockIdx.x, (int)gridDim.x, smem,
+      nullptr, nullptr, &st_part[0][0][0], nullptr, cg);
+}
+template <int BM, int BN, int WN, int OCC>
+__global__ __launch_bounds__(256, OCC) void cg32_dgrad_kernel(const float* __restrict__ dy, const float* __restrict__ wd,
+                                                            float* __restrict__ dx, int64_t M, int N, int K,
+                                                            int64_t tiles_m, int ntn, ConvGather cg) {
+  using G = GemmCfg<float, BM, BN, WN, 2, CG32_BK>;
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  pw_gemm_body<float, PRO_NONE, 0, 0, BM, BN, WN, 2, CG32_BK, 1>(dy, wd, dx, nullptr, nullptr, nullptr, M, N, K, Pro{},
+                                                                 nullptr, tiles_m, ntn, (int)blockIdx.x,
+                                                                 (int)gridDim.x, smem, nullptr, nullptr, nullptr,
+                                                                 nullptr, cg);
+}
+__global__ __launch_bounds__(256, 2) void cg32_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                           int64_t M, int N, int K, float* __restrict__ slab, int tnk,
+                                                           int64_t m_per_split, ConvGather cg) {
+  __shared__ __attribute__((aligned(16))) char smem[WgCfg<float>::SMEM];
+  pw_wgrad_body<float, PRO_NONE, 1, 1>(dy, x, M, N, K, Pro{}, slab, tnk, m_per_split,
+                                       (int)(blockIdx.y * gridDim.x + blockIdx.x), (int)(gridDim.x * gridDim.y),
+                                       (int)gridDim.x, smem, cg);
+}
+
+static bool dense_nhwc(const int64_t (&xs)[4], int H, int W, int C) {
+  return xs[3] == 1 && xs[2] == C && xs[1] == (int64_t)W * C && xs[0] == (int64_t)H * W * C;
+}
+// the wide-vector path's shapes (above); DFD_CG32 = 0 keeps every layer on conv_gemm (A/B builds)
+#ifndef DFD_CG32
+#define DFD_CG32 1
+#endif
+// (not the ResNet-50 training convolutions: their two-level K sum (fold) keeps the BN-amplified rounding
+// within bounds, measured 3-5x torch fp32's error on the layer4.2 gradients with the plain K-order sum)
+static bool cg32_ok(const ConvGeom& g) {
+  return DFD_CG32 && !g.fold && g.S == 1 && g.KH == g.KW && (g.KH & 1) && g.P == g.KH / 2 && g.Ci % 64 == 0 && g.Co % 64 == 0 &&
+         (int64_t)g.N * g.H * g.W < (1ll << 31);
+}
+static ConvGather cg32_gather(int C, int H, int W, int Ho, int Wo, int kw, int s, int p, int dgrad) {
+  ConvGather c{};
+  c.C = C; c.H = H; c.W = W; c.Ho = Ho; c.Wo = Wo; c.KW = kw; c.S = s; c.P = p; c.dgrad = dgrad;
+  conv_gather_fdiv((uint32_t)(Ho * Wo), c.mhw, c.lhw);
+  conv_gather_fdiv((uint32_t)Wo, c.mw, c.lw);
+  return c;
+}
+// 128 x 128 tiles where N > 64, else 128 x 64; a persistent grid of <= 1024 workgroups
+template <bool FWD>
+static int cg32_launch(hipStream_t s, const float* a, const float* b, const float* bias, float* c, int64_t M, int N,
+                       int K, float* stats, const ConvGather& cg, int* stat_rows) {
+  const int bn = N > 64 ? 128 : 64;
+  const int ntn = cdiv(N, bn);
+  const int64_t tiles_m = cdiv64(M, 128);
+  const int gx = (int)std::min<int64_t>(tiles_m, std::max<int64_t>(1, 1024 / ntn));
+  if (stat_rows) *stat_rows = (int)cdiv64(M, kConvStatRows);
+  if (FWD) {  // the conv bias (CNNLSTMHybrid) is optional (ResNet-50: none)
+#define DFD_CG32F(E)                                                                                                 \
+  if (bn == 128)                                                                                                     \
+    hipLaunchKernelGGL((cg32_fwd_kernel<E, 128, 128, 2, 2>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, bias, \
+                       c, M, N, K, stats, tiles_m, ntn, cg);                                                         \
+  else                                                                                                               \
+    hipLaunchKernelGGL((cg32_fwd_kernel<E, 128, 64, 2, 3>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, bias,  \
+                       c, M, N, K, stats, tiles_m, ntn, cg);
+    if (bias) { DFD_CG32F(EPI_BIAS) } else { DFD_CG32F(0) }
+#undef DFD_CG32F
+  } else {
+    if (bn == 128)
+      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 128, 2, 2>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M, N,
+                         K, tiles_m, ntn, cg);
+    else
+      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 3>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M, N,
+                         K, tiles_m, ntn, cg);
+  }
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+// the weight gradient's M-split: ~512 workgroups of 64 x 64 tiles, 128-row multiples
+static void cg32_wgrad_split(int64_t M, int N, int K, int64_t slab_floats, int* tnk, int* tiles, int64_t* splits,
+                             int64_t* mps) {
+  *tnk = cdiv(K, 64);
+  *tiles = cdiv(N, 64) * *tnk;
+  int64_t sp = std::max<int64_t>(1, 512 / *tiles);
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, cdiv64(M, 128)));
+  sp = std::min<int64_t>(sp, std::max<int64_t>(1, slab_floats / ((int64_t)N * K)));
+  *mps = cdiv64(cdiv64(std::max<int64_t>(M, 1), sp), 128) * 128;
+  *splits = cdiv64(std::max<int64_t>(M, 1), *mps);
+}
+
 // ------------------------------------------------------------------ layer launchers
 // a 1x1 stride-1 unpadded convolution over a dense NHWC input is a plain GEMM on the activation rows
 static bool plain_1x1(const ConvGeom& g, const int64_t (&xs)[4]) {
@@ -500,6 +604,11 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
                      (float*)nullptr);
   const int M = g.N * g.Ho * g.Wo, K = KK * g.Ci;
+  if (cg32_ok(g) && dense_nhwc(xs, g.H, g.W, g.Ci) && stats) {
+    const ConvGather cg = cg32_gather(g.Ci, g.H, g.W, g.Ho, g.Wo, g.KW, 1, g.P, 0);
+    DFD_TRY(cg32_launch<true>(s, x, wf, bias, Y, M, g.Co, K, stats, cg, stat_rows));
+    return 0;
+  }
   OpRows pb{wf, K, g.Co, K};
   if (stat_rows) *stat_rows = cdiv(M, CG_T);
   if (plain_1x1(g, xs))  // the activation rows themselves are the A operand (no gather index math)
@@ -516,6 +625,10 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
                      wd);
   const int M = g.N * g.H * g.W, K = KK * g.Co;
+  if (cg32_ok(g)) {  // rows: input pixels; source: dY [N][Ho][Wo][Co]
+    const ConvGather cg = cg32_gather(g.Co, g.Ho, g.Wo, g.H, g.W, g.KW, 1, g.P, 1);
+    return cg32_launch<false>(s, dY, wd, nullptr, dX, M, g.Ci, K, nullptr, cg, nullptr);
+  }
   OpRows pb{wd, K, g.Ci, K};
   if (g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0)  // dY rows are the A operand
     return conv_gemm<OpRows, OpRows, CEPI_STORE>(s, OpRows{dY, g.Co, M, K}, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr,
@@ -544,6 +657,18 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
   const int KK = g.KH * g.KW;
   const int M = g.N * g.Ho * g.Wo, Kp = KK * g.Ci;  // GEMM: C[Co][Kp] = sum_m dY[m][co] X(m, kp)
   const int64_t per = (int64_t)g.Co * Kp;
+  if (cg32_ok(g) && dense_nhwc(xs, g.H, g.W, g.Ci)) {
+    int tnk, tiles;
+    int64_t sp, mps;
+    cg32_wgrad_split(M, g.Co, Kp, slab_cap, &tnk, &tiles, &sp, &mps);
+    const ConvGather cg = cg32_gather(g.Ci, g.H, g.W, g.Ho, g.Wo, g.KW, 1, g.P, 0);
+    hipLaunchKernelGGL(cg32_wgrad_kernel, dim3((unsigned)tiles, (unsigned)sp), dim3(256), 0, s, dY, x, (int64_t)M,
+                       g.Co, Kp, slab, tnk, mps, cg);
+    DFD_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(conv_unpack_grad_kernel, dim3(ew(per)), dim3(256), 0, s, slab, (int)sp, g.Co, g.Ci, KK, gw);
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   int splits = conv_wgrad_splits(g);
   splits = (int)std::max<int64_t>(1, std::min<int64_t>(splits, slab_cap / per));
   OpCols pa{dY, g.Co, g.Co, M};
