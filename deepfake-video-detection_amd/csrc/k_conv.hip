@@ -520,11 +520,17 @@ __global__ __launch_bounds__(256, OCC) void cg32_dgrad_kernel(const float* __res
                                                                  (int)gridDim.x, smem, nullptr, nullptr, nullptr,
                                                                  nullptr, cg);
 }
+#ifndef DFD_CG32_WPF  // m-steps of loads in flight in the weight gradient (2: +0.2 ms, ab_cg32_r06ah.txt)
+#define DFD_CG32_WPF 1
+#endif
+#ifndef DFD_CG32_N64  // 64-wide data gradients: 1 = 256 x 64 tiles of 4 x 1 waves (CNN-LSTM step -0.25..-0.9 ms, ab_cg32_r06ah.txt), 0 = 128 x 64 of 2 x 2
+#define DFD_CG32_N64 1
+#endif
 __global__ __launch_bounds__(256, 2) void cg32_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                            int64_t M, int N, int K, float* __restrict__ slab, int tnk,
                                                            int64_t m_per_split, ConvGather cg) {
   __shared__ __attribute__((aligned(16))) char smem[WgCfg<float>::SMEM];
-  pw_wgrad_body<float, PRO_NONE, 1, 1>(dy, x, M, N, K, Pro{}, slab, tnk, m_per_split,
+  pw_wgrad_body<float, PRO_NONE, DFD_CG32_WPF, 1>(dy, x, M, N, K, Pro{}, slab, tnk, m_per_split,
                                        (int)(blockIdx.y * gridDim.x + blockIdx.x), (int)(gridDim.x * gridDim.y),
                                        (int)gridDim.x, smem, cg);
 }
@@ -569,12 +575,18 @@ static int cg32_launch(hipStream_t s, const float* a, const float* b, const floa
     if (bias) { DFD_CG32F(EPI_BIAS) } else { DFD_CG32F(0) }
 #undef DFD_CG32F
   } else {
-    if (bn == 128)
+    if (bn == 128) {
       hipLaunchKernelGGL((cg32_dgrad_kernel<128, 128, 2, 2>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M, N,
                          K, tiles_m, ntn, cg);
-    else
+    } else if (DFD_CG32_N64) {
+      const int64_t t256 = cdiv64(M, 256);
+      const int g2 = (int)std::min<int64_t>(t256, std::max<int64_t>(1, 1024 / ntn));
+      hipLaunchKernelGGL((cg32_dgrad_kernel<256, 64, 1, 2>), dim3((unsigned)(g2 * ntn)), dim3(256), 0, s, a, b, c, M, N,
+                         K, t256, ntn, cg);
+    } else {
       hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 3>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M, N,
                          K, tiles_m, ntn, cg);
+    }
   }
   DFD_HIP_CHECK(hipGetLastError());
   return 0;
