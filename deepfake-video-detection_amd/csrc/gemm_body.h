@@ -118,7 +118,9 @@ __device__ __forceinline__ void lds_ld8(const T* p, float (&v)[8]) { ld8(p, v); 
 // sum and the sum of squared deviations from that group's own column mean: centred partials of
 // consecutive BM / WM-row groups, stats row mt * WM + wm (launch_bn_finalize chan_rows = BM / WM;
 // empty groups past M write nothing).
-template <typename T, int MODE, int STATS, int EPI, int BM, int BN, int WN, int D, int BK, int GA = 0>
+// FOLD (fp32): two-level K sum -- each k-step's products go to a fresh tile that is then added to the
+// running sum (the ResNet-50 fp32 training convolutions, whose train-mode BatchNorm amplifies rounding).
+template <typename T, int MODE, int STATS, int EPI, int BM, int BN, int WN, int D, int BK, int GA = 0, bool FOLD = false>
 __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* __restrict__ B, T* __restrict__ C,
                                              const T* __restrict__ R, const float* __restrict__ bias,
                                              const T* __restrict__ Z, int64_t M, int N, int K, const Pro& pro,
@@ -283,6 +285,13 @@ __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* _
             }
           }
         } else {
+          f32x4_t fold[FOLD ? RB : 1][FOLD ? CB : 1];
+          if constexpr (FOLD) {
+#pragma unroll
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+              for (int b = 0; b < CB; ++b) fold[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          }
 #pragma unroll
           for (int s4 = 0; s4 < GBK / 4; ++s4) {
             const int kk = 4 * s4 + (lane >> 4);
@@ -294,9 +303,17 @@ __device__ __forceinline__ void pw_gemm_body(const T* __restrict__ A, const T* _
             for (int cb = 0; cb < CB; ++cb) {
               const float bv = reinterpret_cast<const float*>(Bs)[(cbase + cb * 16 + (lane & 15)) * G::AS + kk];
 #pragma unroll
-              for (int r_ = 0; r_ < RB; ++r_)
-                acc[r_][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r_], bv, acc[r_][cb], 0, 0, 0);
+              for (int r_ = 0; r_ < RB; ++r_) {
+                if constexpr (FOLD) fold[r_][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r_], bv, fold[r_][cb], 0, 0, 0);
+                else acc[r_][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r_], bv, acc[r_][cb], 0, 0, 0);
+              }
             }
+          }
+          if constexpr (FOLD) {
+#pragma unroll
+            for (int a = 0; a < RB; ++a)
+#pragma unroll
+              for (int b = 0; b < CB; ++b) acc[a][b] += fold[a][b];
           }
         }
         lds_barrier();
@@ -420,7 +437,7 @@ template <typename T> struct WgCfg {
 // One workgroup of the weight gradient: lin / nb its linear index and the workgroup count of its grid
 // (tiles x splits), tiles the tile count, smem the caller's LDS (WgCfg<T>::SMEM bytes).  GX = 1: X is
 // the implicit-GEMM gather of a convolution input (ConvGather; one tap per 64-wide K tile).
-template <typename T, int MODE, int PF, int GX = 0>
+template <typename T, int MODE, int PF, int GX = 0, bool FOLD = false>
 __device__ __forceinline__ void pw_wgrad_body(const T* __restrict__ dY, const T* __restrict__ X, int64_t M, int N,
                                               int K, const Pro& pro, float* __restrict__ slab, int tnk,
                                               int64_t m_per_split, int lin, int nb, int tiles, char* smem,
@@ -536,6 +553,14 @@ __device__ __forceinline__ void pw_wgrad_body(const T* __restrict__ dY, const T*
     } else {
       const float* Yf = reinterpret_cast<const float*>(Ys);
       const float* Xf = reinterpret_cast<const float*>(Xs);
+      // FOLD: each m-step's products into a fresh tile added to the running sum (two-level M sum)
+      f32x4_t fold[FOLD ? 4 : 1][FOLD ? 4 : 1];
+      if constexpr (FOLD) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) fold[a][b] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
       for (int s = 0; s < WMS / 4; ++s) {
         const int mm = 4 * s + (lane >> 4);
@@ -546,8 +571,17 @@ __device__ __forceinline__ void pw_wgrad_body(const T* __restrict__ dY, const T*
         for (int nb_ = 0; nb_ < 4; ++nb_) {
           const float av = Yf[mm * G::LS + nb_ * 16 + (lane & 15)];
 #pragma unroll
-          for (int kb = 0; kb < 4; ++kb) acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kb], acc[nb_][kb], 0, 0, 0);
+          for (int kb = 0; kb < 4; ++kb) {
+            if constexpr (FOLD) fold[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kb], fold[nb_][kb], 0, 0, 0);
+            else acc[nb_][kb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kb], acc[nb_][kb], 0, 0, 0);
+          }
         }
+      }
+      if constexpr (FOLD) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] += fold[a][b];
       }
     }
     __builtin_amdgcn_wave_barrier();

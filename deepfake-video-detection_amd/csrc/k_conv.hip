@@ -496,7 +496,7 @@ static int ew(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(cd
 // 128 x 128 / 128 x 64 tiles of two wave rows.  The forward's BN partials are centred per wave row
 // (STATS = 2: 64 consecutive rows each, the same (sum, M2) rows conv_gemm's epilogue writes).
 constexpr int CG32_BK = 32;
-template <int EPI, int BM, int BN, int WN, int OCC>
+template <int EPI, int BM, int BN, int WN, int OCC, bool FOLD = false>
 __global__ __launch_bounds__(256, OCC) void cg32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wf,
                                                           const float* __restrict__ bias, float* __restrict__ y,
                                                           int64_t M, int N, int K, float* __restrict__ stats,
@@ -505,17 +505,17 @@ __global__ __launch_bounds__(256, OCC) void cg32_fwd_kernel(const float* __restr
   static_assert(BM / G::WM == kConvStatRows, "BN partial rows of conv_forward");
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
   __shared__ float st_part[G::WM][2][BN];
-  pw_gemm_body<float, PRO_NONE, 2, EPI, BM, BN, WN, 2, CG32_BK, 1>(
+  pw_gemm_body<float, PRO_NONE, 2, EPI, BM, BN, WN, 2, CG32_BK, 1, FOLD>(
       x, wf, y, nullptr, bias, nullptr, M, N, K, Pro{}, stats, tiles_m, ntn, (int)blockIdx.x, (int)gridDim.x, smem,
       nullptr, nullptr, &st_part[0][0][0], nullptr, cg);
 }
-template <int BM, int BN, int WN, int OCC>
+template <int BM, int BN, int WN, int OCC, bool FOLD = false>
 __global__ __launch_bounds__(256, OCC) void cg32_dgrad_kernel(const float* __restrict__ dy, const float* __restrict__ wd,
                                                             float* __restrict__ dx, int64_t M, int N, int K,
                                                             int64_t tiles_m, int ntn, ConvGather cg) {
   using G = GemmCfg<float, BM, BN, WN, 2, CG32_BK>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  pw_gemm_body<float, PRO_NONE, 0, 0, BM, BN, WN, 2, CG32_BK, 1>(dy, wd, dx, nullptr, nullptr, nullptr, M, N, K, Pro{},
+  pw_gemm_body<float, PRO_NONE, 0, 0, BM, BN, WN, 2, CG32_BK, 1, FOLD>(dy, wd, dx, nullptr, nullptr, nullptr, M, N, K, Pro{},
                                                                  nullptr, tiles_m, ntn, (int)blockIdx.x,
                                                                  (int)gridDim.x, smem, nullptr, nullptr, nullptr,
                                                                  nullptr, cg);
@@ -526,11 +526,12 @@ __global__ __launch_bounds__(256, OCC) void cg32_dgrad_kernel(const float* __res
 #ifndef DFD_CG32_N64  // 64-wide data gradients: 1 = 256 x 64 tiles of 4 x 1 waves (CNN-LSTM step -0.25..-0.9 ms, ab_cg32_r06ah.txt), 0 = 128 x 64 of 2 x 2
 #define DFD_CG32_N64 1
 #endif
+template <bool FOLD>
 __global__ __launch_bounds__(256, 2) void cg32_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                            int64_t M, int N, int K, float* __restrict__ slab, int tnk,
                                                            int64_t m_per_split, ConvGather cg) {
   __shared__ __attribute__((aligned(16))) char smem[WgCfg<float>::SMEM];
-  pw_wgrad_body<float, PRO_NONE, DFD_CG32_WPF, 1>(dy, x, M, N, K, Pro{}, slab, tnk, m_per_split,
+  pw_wgrad_body<float, PRO_NONE, DFD_CG32_WPF, 1, FOLD>(dy, x, M, N, K, Pro{}, slab, tnk, m_per_split,
                                        (int)(blockIdx.y * gridDim.x + blockIdx.x), (int)(gridDim.x * gridDim.y),
                                        (int)gridDim.x, smem, cg);
 }
@@ -542,11 +543,15 @@ static bool dense_nhwc(const int64_t (&xs)[4], int H, int W, int C) {
 #ifndef DFD_CG32
 #define DFD_CG32 1
 #endif
-// (not the ResNet-50 training convolutions: their two-level K sum (fold) keeps the BN-amplified rounding
-// within bounds, measured 3-5x torch fp32's error on the layer4.2 gradients with the plain K-order sum)
+// The ResNet-50 training convolutions (g.fold) take the two-level K / M sum (FOLD): their train-mode BN
+// amplifies conv rounding, and the plain K-order sum measured 3-5x torch fp32's error on the layer4.2
+// gradients.  Stride 2 through the gather's parity test.
+#ifndef DFD_CG32_FOLD  // 1: the fold convolutions (ResNet-50 fp32 training) on these loops too (A/B build switch)
+#define DFD_CG32_FOLD 1
+#endif
 static bool cg32_ok(const ConvGeom& g) {
-  return DFD_CG32 && !g.fold && g.S == 1 && g.KH == g.KW && (g.KH & 1) && g.P == g.KH / 2 && g.Ci % 64 == 0 && g.Co % 64 == 0 &&
-         (int64_t)g.N * g.H * g.W < (1ll << 31);
+  return DFD_CG32 && (!g.fold || DFD_CG32_FOLD) && (g.S == 1 || g.S == 2) && g.KH == g.KW && (g.KH & 1) &&
+         g.P == g.KH / 2 && g.Ci % 64 == 0 && g.Co % 64 == 0 && (int64_t)g.N * g.H * g.W < (1ll << 31);
 }
 static ConvGather cg32_gather(int C, int H, int W, int Ho, int Wo, int kw, int s, int p, int dgrad) {
   ConvGather c{};
@@ -558,7 +563,26 @@ static ConvGather cg32_gather(int C, int H, int W, int Ho, int Wo, int kw, int s
 // 128 x 128 tiles where N > 64, else 128 x 64; a persistent grid of <= 1024 workgroups
 template <bool FWD>
 static int cg32_launch(hipStream_t s, const float* a, const float* b, const float* bias, float* c, int64_t M, int N,
-                       int K, float* stats, const ConvGather& cg, int* stat_rows) {
+                       int K, float* stats, const ConvGather& cg, int* stat_rows, bool fold) {
+  if (fold) {  // 128 x 64 tiles (the fresh per-step tile doubles the accumulators)
+    const int ntn = cdiv(N, 64);
+    const int64_t tiles_m = cdiv64(M, 128);
+    const int gx = (int)std::min<int64_t>(tiles_m, std::max<int64_t>(1, 1024 / ntn));
+    if (FWD) {
+      if (stat_rows) *stat_rows = (int)cdiv64(M, kConvStatRows);
+      if (bias)
+        hipLaunchKernelGGL((cg32_fwd_kernel<EPI_BIAS, 128, 64, 2, 2, true>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a,
+                           b, bias, c, M, N, K, stats, tiles_m, ntn, cg);
+      else
+        hipLaunchKernelGGL((cg32_fwd_kernel<0, 128, 64, 2, 2, true>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b,
+                           bias, c, M, N, K, stats, tiles_m, ntn, cg);
+    } else {
+      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 2, true>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M,
+                         N, K, tiles_m, ntn, cg);
+    }
+    DFD_HIP_CHECK(hipGetLastError());
+    return 0;
+  }
   const int bn = N > 64 ? 128 : 64;
   const int ntn = cdiv(N, bn);
   const int64_t tiles_m = cdiv64(M, 128);
@@ -617,8 +641,8 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
                      (float*)nullptr);
   const int M = g.N * g.Ho * g.Wo, K = KK * g.Ci;
   if (cg32_ok(g) && dense_nhwc(xs, g.H, g.W, g.Ci) && stats) {
-    const ConvGather cg = cg32_gather(g.Ci, g.H, g.W, g.Ho, g.Wo, g.KW, 1, g.P, 0);
-    DFD_TRY(cg32_launch<true>(s, x, wf, bias, Y, M, g.Co, K, stats, cg, stat_rows));
+    const ConvGather cg = cg32_gather(g.Ci, g.H, g.W, g.Ho, g.Wo, g.KW, g.S, g.P, 0);
+    DFD_TRY(cg32_launch<true>(s, x, wf, bias, Y, M, g.Co, K, stats, cg, stat_rows, g.fold));
     return 0;
   }
   OpRows pb{wf, K, g.Co, K};
@@ -638,8 +662,8 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
                      wd);
   const int M = g.N * g.H * g.W, K = KK * g.Co;
   if (cg32_ok(g)) {  // rows: input pixels; source: dY [N][Ho][Wo][Co]
-    const ConvGather cg = cg32_gather(g.Co, g.Ho, g.Wo, g.H, g.W, g.KW, 1, g.P, 1);
-    return cg32_launch<false>(s, dY, wd, nullptr, dX, M, g.Ci, K, nullptr, cg, nullptr);
+    const ConvGather cg = cg32_gather(g.Co, g.Ho, g.Wo, g.H, g.W, g.KW, g.S, g.P, 1);
+    return cg32_launch<false>(s, dY, wd, nullptr, dX, M, g.Ci, K, nullptr, cg, nullptr, g.fold);
   }
   OpRows pb{wd, K, g.Ci, K};
   if (g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0)  // dY rows are the A operand
@@ -673,9 +697,13 @@ int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (
     int tnk, tiles;
     int64_t sp, mps;
     cg32_wgrad_split(M, g.Co, Kp, slab_cap, &tnk, &tiles, &sp, &mps);
-    const ConvGather cg = cg32_gather(g.Ci, g.H, g.W, g.Ho, g.Wo, g.KW, 1, g.P, 0);
-    hipLaunchKernelGGL(cg32_wgrad_kernel, dim3((unsigned)tiles, (unsigned)sp), dim3(256), 0, s, dY, x, (int64_t)M,
-                       g.Co, Kp, slab, tnk, mps, cg);
+    const ConvGather cg = cg32_gather(g.Ci, g.H, g.W, g.Ho, g.Wo, g.KW, g.S, g.P, 0);
+    if (g.fold)
+      hipLaunchKernelGGL(cg32_wgrad_kernel<true>, dim3((unsigned)tiles, (unsigned)sp), dim3(256), 0, s, dY, x,
+                         (int64_t)M, g.Co, Kp, slab, tnk, mps, cg);
+    else
+      hipLaunchKernelGGL(cg32_wgrad_kernel<false>, dim3((unsigned)tiles, (unsigned)sp), dim3(256), 0, s, dY, x,
+                         (int64_t)M, g.Co, Kp, slab, tnk, mps, cg);
     DFD_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(conv_unpack_grad_kernel, dim3(ew(per)), dim3(256), 0, s, slab, (int)sp, g.Co, g.Ci, KK, gw);
     DFD_HIP_CHECK(hipGetLastError());
