@@ -612,6 +612,15 @@ int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Ci
   DFD_GUARD_END
 }
 
+int dfd_rn_conv_dgrad_res(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout, int kh,
+                          int kw, int stride, int pad, float* wpack, float* wpack_t, const float* res, float* dx) {
+  DFD_GUARD_BEGIN
+  if (!dy || !w || !wpack || !wpack_t || !res || !dx) { dfd::set_error("null argument", __FILE__, __LINE__); return -1; }
+  const dfd::ConvGeom g = rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad);
+  return dfd::conv_dgrad((hipStream_t)stream, g, dy, w, wpack, wpack_t, dx, res);
+  DFD_GUARD_END
+}
+
 int64_t dfd_rn_conv_wgrad_slab_floats(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride, int pad) {
   return dfd::conv_wgrad_slab_floats(rn_geom(N, H, W, Cin, Cout, kh, kw, stride, pad));
 }

@@ -13,7 +13,9 @@ struct ConvGeom {
 
 int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* w,
                  const float* bias, float* wf, float* Y, float* stats, int* stat_rows);
-int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX);
+// res (optional): dX = data gradient + res (the bottleneck's other path, same layout as dX)
+int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX,
+               const float* res = nullptr);
 int64_t conv_wgrad_slab_floats(const ConvGeom& g);  // the slab conv_wgrad uses in full
 int conv_wgrad(hipStream_t s, const ConvGeom& g, const float* x, const int64_t (&xs)[4], const float* dY, float* slab,
                int64_t slab_cap, float* gw);

@@ -509,13 +509,14 @@ __global__ __launch_bounds__(256, OCC) void cg32_fwd_kernel(const float* __restr
       x, wf, y, nullptr, bias, nullptr, M, N, K, Pro{}, stats, tiles_m, ntn, (int)blockIdx.x, (int)gridDim.x, smem,
       nullptr, nullptr, &st_part[0][0][0], nullptr, cg);
 }
-template <int BM, int BN, int WN, int OCC, bool FOLD = false>
+template <int BM, int BN, int WN, int OCC, bool FOLD = false, int EPI = 0>
 __global__ __launch_bounds__(256, OCC) void cg32_dgrad_kernel(const float* __restrict__ dy, const float* __restrict__ wd,
-                                                            float* __restrict__ dx, int64_t M, int N, int K,
-                                                            int64_t tiles_m, int ntn, ConvGather cg) {
+                                                            float* __restrict__ dx, const float* __restrict__ res,
+                                                            int64_t M, int N, int K, int64_t tiles_m, int ntn,
+                                                            ConvGather cg) {
   using G = GemmCfg<float, BM, BN, WN, 2, CG32_BK>;
   __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  pw_gemm_body<float, PRO_NONE, 0, 0, BM, BN, WN, 2, CG32_BK, 1, FOLD>(dy, wd, dx, nullptr, nullptr, nullptr, M, N, K, Pro{},
+  pw_gemm_body<float, PRO_NONE, 0, EPI, BM, BN, WN, 2, CG32_BK, 1, FOLD>(dy, wd, dx, res, nullptr, nullptr, M, N, K, Pro{},
                                                                  nullptr, tiles_m, ntn, (int)blockIdx.x,
                                                                  (int)gridDim.x, smem, nullptr, nullptr, nullptr,
                                                                  nullptr, cg);
@@ -563,7 +564,8 @@ static ConvGather cg32_gather(int C, int H, int W, int Ho, int Wo, int kw, int s
 // 128 x 128 tiles where N > 64, else 128 x 64; a persistent grid of <= 1024 workgroups
 template <bool FWD>
 static int cg32_launch(hipStream_t s, const float* a, const float* b, const float* bias, float* c, int64_t M, int N,
-                       int K, float* stats, const ConvGather& cg, int* stat_rows, bool fold) {
+                       int K, float* stats, const ConvGather& cg, int* stat_rows, bool fold,
+                       const float* res = nullptr) {
   if (fold) {  // 128 x 64 tiles (the fresh per-step tile doubles the accumulators)
     const int ntn = cdiv(N, 64);
     const int64_t tiles_m = cdiv64(M, 128);
@@ -577,8 +579,12 @@ static int cg32_launch(hipStream_t s, const float* a, const float* b, const floa
         hipLaunchKernelGGL((cg32_fwd_kernel<0, 128, 64, 2, 2, true>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b,
                            bias, c, M, N, K, stats, tiles_m, ntn, cg);
     } else {
-      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 2, true>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M,
-                         N, K, tiles_m, ntn, cg);
+      if (res)  // the bottleneck's residual path added in the epilogue
+        hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 2, true, EPI_RESID>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s,
+                           a, b, c, res, M, N, K, tiles_m, ntn, cg);
+      else
+        hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 2, true>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c,
+                           res, M, N, K, tiles_m, ntn, cg);
     }
     DFD_HIP_CHECK(hipGetLastError());
     return 0;
@@ -600,16 +606,16 @@ static int cg32_launch(hipStream_t s, const float* a, const float* b, const floa
 #undef DFD_CG32F
   } else {
     if (bn == 128) {
-      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 128, 2, 2>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M, N,
-                         K, tiles_m, ntn, cg);
+      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 128, 2, 2>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, res, M,
+                         N, K, tiles_m, ntn, cg);
     } else if (DFD_CG32_N64) {
       const int64_t t256 = cdiv64(M, 256);
       const int g2 = (int)std::min<int64_t>(t256, std::max<int64_t>(1, 1024 / ntn));
-      hipLaunchKernelGGL((cg32_dgrad_kernel<256, 64, 1, 2>), dim3((unsigned)(g2 * ntn)), dim3(256), 0, s, a, b, c, M, N,
-                         K, t256, ntn, cg);
+      hipLaunchKernelGGL((cg32_dgrad_kernel<256, 64, 1, 2>), dim3((unsigned)(g2 * ntn)), dim3(256), 0, s, a, b, c, res, M,
+                         N, K, t256, ntn, cg);
     } else {
-      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 3>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, M, N,
-                         K, tiles_m, ntn, cg);
+      hipLaunchKernelGGL((cg32_dgrad_kernel<128, 64, 2, 3>), dim3((unsigned)(gx * ntn)), dim3(256), 0, s, a, b, c, res, M,
+                         N, K, tiles_m, ntn, cg);
     }
   }
   DFD_HIP_CHECK(hipGetLastError());
@@ -655,7 +661,8 @@ int conv_forward(hipStream_t s, const ConvGeom& g, const float* x, const int64_t
   return conv_gemm<OpConvA, OpRows, CEPI_STATS>(s, pa, pb, Y, g.Co, M, g.Co, K, 1, bias, stats, g.fold);
 }
 
-int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX) {
+int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w, float* wf, float* wd, float* dX,
+               const float* res) {
   if (g.S != 1 && g.S != 2) { set_error("conv dgrad: stride 1 or 2", __FILE__, __LINE__); return -1; }
   const int KK = g.KH * g.KW;
   hipLaunchKernelGGL(conv_pack_kernel, dim3(ew((int64_t)g.Co * g.Ci * KK)), dim3(256), 0, s, w, g.Co, g.Ci, KK, wf,
@@ -663,8 +670,10 @@ int conv_dgrad(hipStream_t s, const ConvGeom& g, const float* dY, const float* w
   const int M = g.N * g.H * g.W, K = KK * g.Co;
   if (cg32_ok(g)) {  // rows: input pixels; source: dY [N][Ho][Wo][Co]
     const ConvGather cg = cg32_gather(g.Co, g.Ho, g.Wo, g.H, g.W, g.KW, g.S, g.P, 1);
-    return cg32_launch<false>(s, dY, wd, nullptr, dX, M, g.Ci, K, nullptr, cg, nullptr, g.fold);
+    if (res && !g.fold) { set_error("conv dgrad: residual form is the fold (ResNet-50) path's", __FILE__, __LINE__); return -1; }
+    return cg32_launch<false>(s, dY, wd, nullptr, dX, M, g.Ci, K, nullptr, cg, nullptr, g.fold, res);
   }
+  if (res) { set_error("conv dgrad: residual form needs Cin, Cout % 64", __FILE__, __LINE__); return -1; }
   OpRows pb{wd, K, g.Ci, K};
   if (g.KH == 1 && g.KW == 1 && g.S == 1 && g.P == 0)  // dY rows are the A operand
     return conv_gemm<OpRows, OpRows, CEPI_STORE>(s, OpRows{dY, g.Co, M, K}, pb, dX, g.Ci, M, g.Ci, K, 1, nullptr,

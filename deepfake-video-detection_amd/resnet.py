@@ -418,8 +418,9 @@ def _bn_bwd(lib, st, u, g, grads):
     return dy
 
 
-def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
-    """data gradient (if needed) and weight gradient of unit u's convolution from dy = dL/dy."""
+def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True, res=None):
+    """data gradient (if needed; + res, the block's other path, added in the kernel's epilogue) and
+    weight gradient of unit u's convolution from dy = dL/dy."""
     conv = u.conv
     k, s, p, cin, cout = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.in_channels, conv.out_channels
     dev = dy.device
@@ -429,8 +430,13 @@ def _conv_bwd(lib, st, u, dy, n, grads, need_dx=True):
     if need_dx:
         wp = torch.empty(2 * nw, dtype=torch.float32, device=dev)
         dx = torch.empty(n * u.hw[0] * u.hw[1], cin, dtype=torch.float32, device=dev)
-        _lib.check(lib.dfd_rn_conv_dgrad(st, dy.data_ptr(), n, u.hw[0], u.hw[1], cin, w.data_ptr(), cout, k, k, s, p,
-                                         wp.data_ptr(), wp[nw:].data_ptr(), dx.data_ptr()))
+        if res is not None:
+            _lib.check(lib.dfd_rn_conv_dgrad_res(st, dy.data_ptr(), n, u.hw[0], u.hw[1], cin, w.data_ptr(), cout, k, k,
+                                                 s, p, wp.data_ptr(), wp[nw:].data_ptr(), res.data_ptr(),
+                                                 dx.data_ptr()))
+        else:
+            _lib.check(lib.dfd_rn_conv_dgrad(st, dy.data_ptr(), n, u.hw[0], u.hw[1], cin, w.data_ptr(), cout, k, k, s,
+                                             p, wp.data_ptr(), wp[nw:].data_ptr(), dx.data_ptr()))
     slab = torch.empty(lib.dfd_rn_conv_wgrad_slab_floats(n, u.hw[0], u.hw[1], cin, cout, k, k, s, p),
                        dtype=torch.float32, device=dev)
     dw = _gdst(grads, conv.weight)
@@ -528,9 +534,9 @@ def _train_backward(trunk, saved, dfeat, grads=None):
         dy3 = _bn_bwd(lib, st, u3, g, grads)
         if "ds" in b:
             dyd = _bn_bwd(lib, st, b["ds"], g, grads)
-            dx = _conv_bwd(lib, st, b["ds"], dyd, n, grads)
+            other = _conv_bwd(lib, st, b["ds"], dyd, n, grads)
         else:
-            dx = g.clone()
+            other = g  # the identity path
         da2 = _conv_bwd(lib, st, u3, dy3, n, grads)
         g2 = torch.empty_like(da2)
         _lib.check(lib.dfd_rn_relu_bwd(st, da2.data_ptr(), b["a2"].data_ptr(), da2.numel(), g2.data_ptr()))
@@ -539,8 +545,7 @@ def _train_backward(trunk, saved, dfeat, grads=None):
         g1 = torch.empty_like(da1)
         _lib.check(lib.dfd_rn_relu_bwd(st, da1.data_ptr(), b["a1"].data_ptr(), da1.numel(), g1.data_ptr()))
         dy1 = _bn_bwd(lib, st, u1, g1, grads)
-        dx.add_(_conv_bwd(lib, st, u1, dy1, n, grads))
-        g = dx
+        g = _conv_bwd(lib, st, u1, dy1, n, grads, res=other)  # conv1's data gradient + the other path
     return _stem_backward(lib, st, saved, g, n, grads)
 
 

@@ -254,6 +254,11 @@ DFD_API int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, in
  * Cout*Cin*kh*kw floats each */
 DFD_API int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout,
                               int kh, int kw, int stride, int pad, float* wpack, float* wpack_t, float* dx);
+/* the same with dx = data gradient + res (the bottleneck's identity / downsample path, (N,H,W,Cin)) added
+ * in the epilogue; Cin, Cout % 64 (the shapes of the fp32 tile loops) */
+DFD_API int dfd_rn_conv_dgrad_res(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w,
+                                  int Cout, int kh, int kw, int stride, int pad, float* wpack, float* wpack_t,
+                                  const float* res, float* dx);
 /* the slab size (floats) dfd_rn_conv_wgrad uses in full for this shape (its pixel splits x |dw|; a
  * smaller slab runs fewer splits) */
 DFD_API int64_t dfd_rn_conv_wgrad_slab_floats(int N, int H, int W, int Cin, int Cout, int kh, int kw, int stride,
