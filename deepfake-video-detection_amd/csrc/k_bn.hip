@@ -147,9 +147,86 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
   }
 }
 
+// Many centred partial rows (the CNN-LSTM's early convolutions: up to 200k rows of 64-row tiles): the
+// single-pass form over row chunks.  With S = sum_t s_t, Q = sum_t M2_t and P = sum_t s_t^2 / n_t,
+// sum_t n_t (mean_t - mean)^2 = P - S^2 / count, so one pass gives every term: chunk partials (S, Q, P)
+// in fp64 over CHUNK rows per workgroup (4 row lanes x 64 channels, lanes added in order), then one
+// thread per channel adds the chunks in order (deterministic) and finalizes as bn_finalize_kernel.
+constexpr int BNF_CHUNK = 512;
+__global__ __launch_bounds__(256) void bn_chan_chunks_kernel(const float* __restrict__ stats, int rows, int64_t count,
+                                                             int C, int chan_rows, double* __restrict__ part) {
+  __shared__ double sh[3][4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl;
+  const int r0 = blockIdx.x * BNF_CHUNK, r1 = min(rows, r0 + BNF_CHUNK);
+  double S = 0.0, Q = 0.0, P = 0.0;
+  if (c < C)
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const int64_t left = count - (int64_t)r * chan_rows, nt = left < chan_rows ? left : chan_rows;
+      const double st = stats[((int64_t)r * 2 + 0) * C + c];
+      S += st;
+      Q += (double)stats[((int64_t)r * 2 + 1) * C + c];
+      P += st * st / (double)nt;
+    }
+  sh[0][rl][cl] = S;
+  sh[1][rl][cl] = Q;
+  sh[2][rl][cl] = P;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double v = ((sh[k][0][cl] + sh[k][1][cl]) + sh[k][2][cl]) + sh[k][3][cl];
+      part[((int64_t)blockIdx.x * 3 + k) * C + c] = v;
+    }
+  }
+}
+__global__ void bn_chan_final_kernel(const double* __restrict__ part, int nchunks, int64_t count, int C,
+                                     const float* __restrict__ gamma, const float* __restrict__ beta, float* run_mean,
+                                     float* run_var, float momentum, float eps, float* mean, float* invstd,
+                                     float* scale, float* shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double S = 0.0, Q = 0.0, P = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    S += part[((int64_t)k * 3 + 0) * C + c];
+    Q += part[((int64_t)k * 3 + 1) * C + c];
+    P += part[((int64_t)k * 3 + 2) * C + c];
+  }
+  const double m = S / (double)count;
+  double between = P - S * m;
+  if (between < 0.0) between = 0.0;
+  double var = (Q + between) / (double)count;
+  if (var < 0.0) var = 0.0;
+  const float mu = (float)m, is = (float)(1.0 / sqrt(var + (double)eps));
+  if (run_mean) {
+    const double unb = count > 1 ? var * (double)count / (double)(count - 1) : var;
+    run_mean[c] = (float)((1.0 - momentum) * run_mean[c] + momentum * m);
+    run_var[c] = (float)((1.0 - momentum) * run_var[c] + momentum * unb);
+  }
+  const float sc = gamma[c] * is;
+  mean[c] = mu;
+  invstd[c] = is;
+  scale[c] = sc;
+  shift[c] = beta[c] - mu * sc;
+}
+
 int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t count, int C, const float* gamma,
                        const float* beta, float* run_mean, float* run_var, float momentum, float eps, bool training,
                        float* mean, float* invstd, float* scale, float* shift, int chan_rows) {
+  if (training && chan_rows > 0 && rows > 4 * BNF_CHUNK) {
+    const int nch = cdiv(rows, BNF_CHUNK);
+    // stream-ordered scratch for the chunk partials (nch x 3 x C doubles; < 1 MB at 200k rows)
+    double* part = nullptr;
+    DFD_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&part), sizeof(double) * (size_t)nch * 3 * C, s));
+    hipLaunchKernelGGL(bn_chan_chunks_kernel, dim3((unsigned)nch, (unsigned)cdiv(C, 64)), dim3(256), 0, s, stats, rows,
+                       count, C, chan_rows, part);
+    DFD_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(bn_chan_final_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, s, part, nch, count, C, gamma,
+                       beta, run_mean, run_var, momentum, eps, mean, invstd, scale, shift);
+    DFD_HIP_CHECK(hipGetLastError());
+    DFD_HIP_CHECK(hipFreeAsync(part, s));
+    return 0;
+  }
   const int ch = training ? fin_ch(rows) : 16;
 #define DFD_FIN(CH)                                                                                                 \
   hipLaunchKernelGGL((bn_finalize_kernel<CH>), dim3(cdiv(C, CH)), dim3(1024), 0, s, stats, rows, count, C, gamma, beta, \
