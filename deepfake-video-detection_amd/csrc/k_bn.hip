@@ -7,6 +7,10 @@
 // deterministic two-level reduction: producers write per-workgroup partial rows
 // [rows][2][C] and bn_finalize sums them in a fixed order (fp64) -- no float atomics in HBM.
 #include "kernels.h"
+
+#include <mutex>
+#include <utility>
+#include <vector>
 #include "tail.h"
 
 namespace dfd {
@@ -153,6 +157,36 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const float* __restri
 // in fp64 over CHUNK rows per workgroup (4 row lanes x 64 channels, lanes added in order), then one
 // thread per channel adds the chunks in order (deterministic) and finalizes as bn_finalize_kernel.
 constexpr int BNF_CHUNK = 512;
+// the chunk partials' scratch (< 1 MB at 200k rows): one buffer per stream, kept and grown on demand
+// (a stream's finalize calls are ordered on it; hipMallocAsync / hipFreeAsync per call measured ~2 ms
+// per step of allocator traffic in the bf16 ensemble step)
+static double* bn_chunk_scratch(hipStream_t s, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<hipStream_t, std::pair<void*, size_t>>> bufs;
+  const std::lock_guard<std::mutex> lk(mu);
+  for (auto& b : bufs)
+    if (b.first == s) {
+      if (b.second.second >= bytes) return static_cast<double*>(b.second.first);
+      if (hipStreamSynchronize(s) != hipSuccess || hipFree(b.second.first) != hipSuccess) {
+        set_error("bn finalize: scratch release failed", __FILE__, __LINE__);
+        return nullptr;
+      }
+      b.second = {nullptr, 0};
+      if (hipMalloc(&b.second.first, bytes) != hipSuccess) {
+        set_error("bn finalize: scratch allocation failed", __FILE__, __LINE__);
+        return nullptr;
+      }
+      b.second.second = bytes;
+      return static_cast<double*>(b.second.first);
+    }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    set_error("bn finalize: scratch allocation failed", __FILE__, __LINE__);
+    return nullptr;
+  }
+  bufs.push_back({s, {p, bytes}});
+  return static_cast<double*>(p);
+}
 __global__ __launch_bounds__(256) void bn_chan_chunks_kernel(const float* __restrict__ stats, int rows, int64_t count,
                                                              int C, int chan_rows, double* __restrict__ part) {
   __shared__ double sh[3][4][64];
@@ -215,16 +249,14 @@ int launch_bn_finalize(hipStream_t s, const float* stats, int rows, int64_t coun
                        float* mean, float* invstd, float* scale, float* shift, int chan_rows) {
   if (training && chan_rows > 0 && rows > 4 * BNF_CHUNK) {
     const int nch = cdiv(rows, BNF_CHUNK);
-    // stream-ordered scratch for the chunk partials (nch x 3 x C doubles; < 1 MB at 200k rows)
-    double* part = nullptr;
-    DFD_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&part), sizeof(double) * (size_t)nch * 3 * C, s));
+    double* part = bn_chunk_scratch(s, sizeof(double) * (size_t)nch * 3 * C);
+    if (!part) return -1;
     hipLaunchKernelGGL(bn_chan_chunks_kernel, dim3((unsigned)nch, (unsigned)cdiv(C, 64)), dim3(256), 0, s, stats, rows,
                        count, C, chan_rows, part);
     DFD_HIP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(bn_chan_final_kernel, dim3((unsigned)cdiv(C, 256)), dim3(256), 0, s, part, nch, count, C, gamma,
                        beta, run_mean, run_var, momentum, eps, mean, invstd, scale, shift);
     DFD_HIP_CHECK(hipGetLastError());
-    DFD_HIP_CHECK(hipFreeAsync(part, s));
     return 0;
   }
   const int ch = training ? fin_ch(rows) : 16;
