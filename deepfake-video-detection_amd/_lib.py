@@ -87,6 +87,7 @@ _SIGS = {
     "dfd_rn_relu_bwd": (c_i, [c_p, c_p, c_p, c_i64, c_p]),
     "dfd_rn_gap_bwd": (c_i, [c_p, c_p, c_p, c_i, c_i, c_i, c_p]),
     "dfd_rn_bn_train_bwd": (c_i, [c_p, c_p, c_p, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "dfd_rn_bn_train_bwd_relu": (c_i, [c_p, c_p, c_p, c_p, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "dfd_rn_conv_dgrad": (c_i, [c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p]),
     "dfd_rn_conv_dgrad_res": (c_i, [c_p, c_p, c_i, c_i, c_i, c_i, c_p, c_i, c_i, c_i, c_i, c_i, c_p, c_p, c_p, c_p]),
     "dfd_rn_conv_wgrad_slab_floats": (c_i64, [c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i]),

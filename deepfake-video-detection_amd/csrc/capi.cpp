@@ -603,6 +603,19 @@ int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, int64_t M,
   DFD_GUARD_END
 }
 
+int dfd_rn_bn_train_bwd_relu(void* stream, const float* da, const float* relu_out, const float* y, int64_t M, int C,
+                             const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                             float* stats, float* coef, float* dy) {
+  DFD_GUARD_BEGIN
+  if (!da || !relu_out || !y || !mean || !invstd || !gamma || !dgamma || !dbeta || !stats || !coef || !dy) {
+    dfd::set_error("null argument", __FILE__, __LINE__);
+    return -1;
+  }
+  return dfd::rn_bn_train_bwd_relu((hipStream_t)stream, da, relu_out, y, M, C, mean, invstd, gamma, dgamma, dbeta,
+                                   stats, coef, dy);
+  DFD_GUARD_END
+}
+
 int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout, int kh,
                       int kw, int stride, int pad, float* wpack, float* wpack_t, float* dx) {
   DFD_GUARD_BEGIN

@@ -386,9 +386,10 @@ int rn16_cast(hipStream_t s, const void* src, int to_bf16, int64_t n, void* dst)
 // materialised.  Partial rows (sum g, sum g * (y - mean) * invstd) per row chunk x 64-channel group
 // (8 channel vectors x 32 row lanes, two rows' loads in flight, lanes added in order through LDS:
 // deterministic), in launch_bn_bwd_finalize's [rows][2][C] layout.
-__global__ __launch_bounds__(256) void rn16_bn_bwd_reduce_relu_kernel(const bf16* __restrict__ da,
-                                                                      const bf16* __restrict__ a,
-                                                                      const bf16* __restrict__ y,
+template <typename T>  // bf16 (this file's training path) or float (the fp32 training path, k_rntrain.hip)
+__global__ __launch_bounds__(256) void rn16_bn_bwd_reduce_relu_kernel(const T* __restrict__ da,
+                                                                      const T* __restrict__ a,
+                                                                      const T* __restrict__ y,
                                                                       const float* __restrict__ mean,
                                                                       const float* __restrict__ invstd, int64_t M, int C,
                                                                       int64_t rows_per_wg, float* __restrict__ stats) {
@@ -435,12 +436,13 @@ __global__ __launch_bounds__(256) void rn16_bn_bwd_reduce_relu_kernel(const bf16
   }
 }
 
-__global__ __launch_bounds__(256) void rn16_bn_bwd_apply_relu_kernel(const bf16* __restrict__ da,
-                                                                     const bf16* __restrict__ a,
-                                                                     const bf16* __restrict__ y,
+template <typename T>
+__global__ __launch_bounds__(256) void rn16_bn_bwd_apply_relu_kernel(const T* __restrict__ da,
+                                                                     const T* __restrict__ a,
+                                                                     const T* __restrict__ y,
                                                                      const float* __restrict__ mu,
                                                                      const float* __restrict__ coef, int64_t nvec, int C,
-                                                                     bf16* __restrict__ dy) {
+                                                                     T* __restrict__ dy) {
   const int cv = C / 8;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
     const int c = (int)(i % cv) * 8;
@@ -458,29 +460,44 @@ __global__ __launch_bounds__(256) void rn16_bn_bwd_apply_relu_kernel(const bf16*
   }
 }
 
+// the masked form for either storage type: reduce, finalize (centred), apply
+template <typename T>
+static int bn_train_bwd_relu(hipStream_t s, const T* g, const T* relu_out, const T* y, int64_t M, int C,
+                             const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                             float* stats, float* coef, T* dy) {
+  if (C % 64) { set_error("bn_train_bwd: C % 64 with the ReLU mask", __FILE__, __LINE__); return -1; }
+  const int groups = C / 64;
+  const int64_t nx = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(512, cdiv64(M, 64)),
+                                                            std::max(1, 1024 / groups)));
+  const int64_t rpw = cdiv64(M, nx);
+  const int rows = (int)cdiv64(M, rpw);
+  hipLaunchKernelGGL(rn16_bn_bwd_reduce_relu_kernel<T>, dim3((unsigned)rows, (unsigned)groups), dim3(256), 0, s, g,
+                     relu_out, y, mean, invstd, M, C, rpw, stats);
+  DFD_HIP_CHECK(hipGetLastError());
+  DFD_TRY(launch_bn_bwd_finalize(s, stats, rows, M, C, gamma, mean, invstd, true, dgamma, dbeta, false, coef, true));
+  const int64_t nvec = M * C / 8;
+  hipLaunchKernelGGL(rn16_bn_bwd_apply_relu_kernel<T>, dim3(ew_blocks(nvec)), dim3(256), 0, s, g, relu_out, y, mean,
+                     coef, nvec, C, dy);
+  DFD_HIP_CHECK(hipGetLastError());
+  return 0;
+}
+
+// fp32 training path: g = (relu_out > 0) * da folded into the BN backward (k_rntrain.hip's unmasked form
+// otherwise)
+int rn_bn_train_bwd_relu(hipStream_t s, const float* da, const float* relu_out, const float* y, int64_t M, int C,
+                         const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                         float* stats, float* coef, float* dy) {
+  return bn_train_bwd_relu<float>(s, da, relu_out, y, M, C, mean, invstd, gamma, dgamma, dbeta, stats, coef, dy);
+}
+
 // the BN backward of a train-mode BatchNorm2d from its output gradient g (identity activation), centred;
 // relu_out != null: g = (relu_out > 0) * g, the ReLU that followed this BN's output (its saved output)
 int rn16_bn_train_bwd(hipStream_t s, const bf16* g, const bf16* relu_out, const bf16* y, int64_t M, int C,
                       const float* mean, const float* invstd, const float* scale, const float* shift,
                       const float* gamma, float* dgamma, float* dbeta, float* stats, float* coef, bf16* dy) {
   if (C % 8) { set_error("rn16_bn_train_bwd: C % 8", __FILE__, __LINE__); return -1; }
-  if (relu_out) {
-    if (C % 64) { set_error("rn16_bn_train_bwd: C % 64 with the ReLU mask", __FILE__, __LINE__); return -1; }
-    const int groups = C / 64;
-    const int64_t nx = std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(512, cdiv64(M, 64)),
-                                                              std::max(1, 1024 / groups)));
-    const int64_t rpw = cdiv64(M, nx);
-    const int rows = (int)cdiv64(M, rpw);
-    hipLaunchKernelGGL(rn16_bn_bwd_reduce_relu_kernel, dim3((unsigned)rows, (unsigned)groups), dim3(256), 0, s, g,
-                       relu_out, y, mean, invstd, M, C, rpw, stats);
-    DFD_HIP_CHECK(hipGetLastError());
-    DFD_TRY(launch_bn_bwd_finalize(s, stats, rows, M, C, gamma, mean, invstd, true, dgamma, dbeta, false, coef, true));
-    const int64_t nvec = M * C / 8;
-    hipLaunchKernelGGL(rn16_bn_bwd_apply_relu_kernel, dim3(ew_blocks(nvec)), dim3(256), 0, s, g, relu_out, y, mean,
-                       coef, nvec, C, dy);
-    DFD_HIP_CHECK(hipGetLastError());
-    return 0;
-  }
+  if (relu_out)
+    return bn_train_bwd_relu<bf16>(s, g, relu_out, y, M, C, mean, invstd, gamma, dgamma, dbeta, stats, coef, dy);
   BnBwdIn in{};
   in.dZ = g;
   in.silu = false;

@@ -28,6 +28,9 @@ int rn16_relu_bwd(hipStream_t s, const bf16* dout, const bf16* out, int64_t n, b
 int rn16_gap_bwd(hipStream_t s, const float* dfeat, const bf16* out, int N, int HW, int C, bf16* g);
 int rn16_cast(hipStream_t s, const void* src, int to_bf16, int64_t n, void* dst);
 // relu_out (or null): the saved output of the ReLU that followed this BN -- g is masked by it inline
+int rn_bn_train_bwd_relu(hipStream_t s, const float* da, const float* relu_out, const float* y, int64_t M, int C,
+                         const float* mean, const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                         float* stats, float* coef, float* dy);
 int rn16_bn_train_bwd(hipStream_t s, const bf16* g, const bf16* relu_out, const bf16* y, int64_t M, int C,
                       const float* mean, const float* invstd, const float* scale, const float* shift,
                       const float* gamma, float* dgamma, float* dbeta, float* stats, float* coef, bf16* dy);

@@ -403,14 +403,22 @@ def _gdst(grads, p):
     return t
 
 
-def _bn_bwd(lib, st, u, g, grads):
-    """train-mode BN backward of unit u from its output gradient g -> dy; dgamma / dbeta into grads."""
+def _bn_bwd(lib, st, u, g, grads, relu_out=None):
+    """train-mode BN backward of unit u from its output gradient g -> dy; dgamma / dbeta into grads.
+    relu_out: the saved output of the ReLU after this BN; g is then that ReLU's INPUT gradient, masked
+    inside the kernels (never materialised)"""
     C = u.y.shape[1]
     dev = g.device
     stats = torch.empty(2048 * 2 * C, dtype=torch.float32, device=dev)
     coef = torch.empty(3 * C, dtype=torch.float32, device=dev)
     dg, db = _gdst(grads, u.bn.weight), _gdst(grads, u.bn.bias)
     dy = torch.empty_like(u.y)
+    if relu_out is not None:
+        _lib.check(lib.dfd_rn_bn_train_bwd_relu(st, g.data_ptr(), relu_out.data_ptr(), u.y.data_ptr(), u.y.shape[0], C,
+                                                u.mean.data_ptr(), u.invstd.data_ptr(), u.bn.weight.data_ptr(),
+                                                dg.data_ptr(), db.data_ptr(), stats.data_ptr(), coef.data_ptr(),
+                                                dy.data_ptr()))
+        return dy
     _lib.check(lib.dfd_rn_bn_train_bwd(st, g.data_ptr(), u.y.data_ptr(), u.y.shape[0], C, u.mean.data_ptr(),
                                        u.invstd.data_ptr(), u.scale.data_ptr(), u.shift.data_ptr(),
                                        u.bn.weight.data_ptr(), dg.data_ptr(), db.data_ptr(), stats.data_ptr(),
@@ -538,13 +546,9 @@ def _train_backward(trunk, saved, dfeat, grads=None):
         else:
             other = g  # the identity path
         da2 = _conv_bwd(lib, st, u3, dy3, n, grads)
-        g2 = torch.empty_like(da2)
-        _lib.check(lib.dfd_rn_relu_bwd(st, da2.data_ptr(), b["a2"].data_ptr(), da2.numel(), g2.data_ptr()))
-        dy2 = _bn_bwd(lib, st, u2, g2, grads)
+        dy2 = _bn_bwd(lib, st, u2, da2, grads, relu_out=b["a2"])  # the ReLU after bn2 masked inside
         da1 = _conv_bwd(lib, st, u2, dy2, n, grads)
-        g1 = torch.empty_like(da1)
-        _lib.check(lib.dfd_rn_relu_bwd(st, da1.data_ptr(), b["a1"].data_ptr(), da1.numel(), g1.data_ptr()))
-        dy1 = _bn_bwd(lib, st, u1, g1, grads)
+        dy1 = _bn_bwd(lib, st, u1, da1, grads, relu_out=b["a1"])
         g = _conv_bwd(lib, st, u1, dy1, n, grads, res=other)  # conv1's data gradient + the other path
     return _stem_backward(lib, st, saved, g, n, grads)
 

@@ -250,6 +250,12 @@ DFD_API int dfd_rn_gap_bwd(void* stream, const float* dfeat, const float* out, i
 DFD_API int dfd_rn_bn_train_bwd(void* stream, const float* g, const float* y, int64_t M, int C, const float* mean,
                                 const float* invstd, const float* scale, const float* shift, const float* gamma,
                                 float* dgamma, float* dbeta, float* stats, float* coef, float* dy);
+/* the same from the gradient da of the ReLU that follows the BN (its saved output relu_out): g =
+ * (relu_out > 0) * da is folded into the reduction and the apply pass, never stored; C % 64; stats >= 512
+ * rows x 2 x C floats */
+DFD_API int dfd_rn_bn_train_bwd_relu(void* stream, const float* da, const float* relu_out, const float* y, int64_t M,
+                                     int C, const float* mean, const float* invstd, const float* gamma,
+                                     float* dgamma, float* dbeta, float* stats, float* coef, float* dy);
 /* dx (N,H,W,Cin) = conv data gradient of dy (N,Ho,Wo,Cout), stride 1 or 2; wpack, wpack_t scratch of
  * Cout*Cin*kh*kw floats each */
 DFD_API int dfd_rn_conv_dgrad(void* stream, const float* dy, int N, int H, int W, int Cin, const float* w, int Cout,
